@@ -1,0 +1,230 @@
+"""Configuration layer (SURVEY §2.6 schema, §5.6 config system).
+
+Keeps quorum's YAML schema and every ``.get(..., default)`` default bit-for-bit
+(reference ``src/quorum/oai_proxy.py:40-63`` for the loader and default config,
+``:1049-1075`` / ``:1166-1189`` for the per-strategy flag defaults, ``:772-825`` for the
+aggregate block).  Additions, none of which change reference semantics:
+
+* ``--config PATH`` / ``QMX_CONFIG`` override the file location;
+* ``validate_config`` gives clear errors (opt-in; the loader keeps the silent
+  default-config fallback of the reference, but logs it loudly);
+* a separate ``runtime`` section holds MI355X knobs (device, tick, batch caps,
+  placement) — see :class:`RuntimeConfig`.
+"""
+from __future__ import annotations
+
+import copy
+import logging
+import os
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Any, Dict, List, Optional
+
+import yaml
+
+logger = logging.getLogger("quorum_amd.config")
+
+DEFAULT_THINKING_TAGS: List[str] = ["think", "reason", "reasoning", "thought"]
+DEFAULT_PROMPT_TEMPLATE = (
+    "You have received the following responses regarding the user's query:\n\n"
+    "{responses}\n\nProvide a concise synthesis of these responses."
+)
+DEFAULT_QUERY_FORMAT = "Original query: {query}\n\n"
+DEFAULT_SOURCE_LABEL_FORMAT = "Response from {backend_name}:\n"
+DEFAULT_INTERMEDIATE_SEPARATOR = "\n\n---\n\n"
+
+# reference oai_proxy.py:54-63
+DEFAULT_CONFIG: Dict[str, Any] = {
+    "primary_backends": [
+        {"name": "default", "url": "https://api.openai.com/v1", "model": ""}
+    ],
+    "settings": {"timeout": 60},
+}
+
+REPO_ROOT = Path(__file__).resolve().parent.parent.parent
+
+
+def default_config_path() -> Path:
+    env = os.environ.get("QMX_CONFIG")
+    if env:
+        return Path(env)
+    return REPO_ROOT / "config.yaml"
+
+
+def load_config(path: Optional[os.PathLike] = None) -> Dict[str, Any]:
+    """Load the YAML config; on ANY error return the reference default config.
+
+    Mirrors reference ``load_config`` (oai_proxy.py:40-63): ``yaml.safe_load`` of the
+    file, silent fallback to a single OpenAI backend with ``timeout: 60``.
+    """
+    cfg_path = Path(path) if path is not None else default_config_path()
+    try:
+        text = cfg_path.read_text()
+        cfg = yaml.safe_load(text)
+        logger.info("loaded configuration from %s", cfg_path)
+        return cfg
+    except Exception as exc:  # noqa: BLE001 - reference behaviour: any error -> default
+        logger.error("error loading %s (%s); using the default configuration", cfg_path, exc)
+        return copy.deepcopy(DEFAULT_CONFIG)
+
+
+class ConfigError(ValueError):
+    pass
+
+
+def validate_config(cfg: Dict[str, Any]) -> List[str]:
+    """Strict validation (opt-in). Returns a list of warnings; raises ConfigError on errors."""
+    warnings: List[str] = []
+    if not isinstance(cfg, dict):
+        raise ConfigError("config root must be a mapping")
+    backends = cfg.get("primary_backends")
+    if not isinstance(backends, list) or not backends:
+        raise ConfigError("primary_backends must be a non-empty list")
+    names = set()
+    for i, b in enumerate(backends):
+        if not isinstance(b, dict):
+            raise ConfigError(f"primary_backends[{i}] must be a mapping")
+        for key in ("name", "url", "model"):
+            if key not in b:
+                raise ConfigError(f"primary_backends[{i}] is missing '{key}'")
+        if b["name"] in names:
+            warnings.append(f"duplicate backend name {b['name']!r}")
+        names.add(b["name"])
+        if not b.get("url"):
+            warnings.append(f"backend {b['name']!r} has no url and will be ignored")
+    if not isinstance(cfg.get("settings"), dict):
+        raise ConfigError("settings must be a mapping (reference crashes at import without it)")
+    sel = strategy_name(cfg)
+    if "strategy" in cfg and sel not in (cfg.get("strategy") or {}):
+        warnings.append(f"selected strategy {sel!r} has no block under 'strategy'; defaults apply")
+    agg = (cfg.get("strategy") or {}).get("aggregate") or {}
+    for unused in ("strip_intermediate_thinking", "hide_aggregator_thinking"):
+        if unused in agg:
+            warnings.append(f"strategy.aggregate.{unused} is accepted but, as in quorum, has no effect")
+    if agg.get("aggregator_backend") and agg["aggregator_backend"] not in names:
+        warnings.append(f"aggregator_backend {agg['aggregator_backend']!r} is not a primary backend")
+    return warnings
+
+
+def strategy_name(cfg: Dict[str, Any]) -> str:
+    return (cfg.get("iterations") or {}).get("aggregation", {}).get("strategy", "concatenate")
+
+
+@dataclass
+class StrategyFlags:
+    """Per-request resolved strategy flags (reference oai_proxy.py:1049-1075)."""
+
+    name: str = "concatenate"
+    separator: str = "\n"
+    hide_intermediate_think: bool = True
+    hide_final_think: bool = False
+    thinking_tags: List[str] = field(default_factory=lambda: list(DEFAULT_THINKING_TAGS))
+    skip_final_aggregation: bool = False
+    suppress_individual_responses: bool = False
+
+
+@dataclass
+class AggregateSettings:
+    """``strategy.aggregate`` block (reference oai_proxy.py:772-825, 1205-1268).
+
+    NOTE: like quorum, this block is consulted regardless of the selected
+    strategy (oai_proxy.py:772/1205) — with an ``aggregator_backend`` set, even
+    ``concatenate`` routes the final through the aggregator.
+    """
+
+    aggregator_backend: Optional[str] = None
+    source_backends: Any = "all"  # computed-but-unused in quorum (oai_proxy.py:774-780)
+    prompt_template: str = DEFAULT_PROMPT_TEMPLATE
+    intermediate_separator: str = DEFAULT_INTERMEDIATE_SEPARATOR
+    include_original_query: bool = True
+    query_format: str = DEFAULT_QUERY_FORMAT
+    include_source_names: bool = False
+    source_label_format: str = DEFAULT_SOURCE_LABEL_FORMAT
+
+
+def resolve_flags(cfg: Dict[str, Any], body: Optional[Dict[str, Any]] = None) -> StrategyFlags:
+    name = strategy_name(cfg)
+    block = (cfg.get("strategy") or {}).get(name, {}) or {}
+    flags = StrategyFlags(
+        name=name,
+        separator=block.get("separator", "\n"),
+        hide_intermediate_think=block.get("hide_intermediate_think", True),
+        hide_final_think=block.get("hide_final_think", False),
+        thinking_tags=list(block.get("thinking_tags", DEFAULT_THINKING_TAGS)),
+        skip_final_aggregation=block.get("skip_final_aggregation", False),
+        suppress_individual_responses=block.get("suppress_individual_responses", False),
+    )
+    if body is not None and isinstance(body, dict) and "suppress_individual_responses" in body:
+        flags.suppress_individual_responses = body.get("suppress_individual_responses")
+    return flags
+
+
+def resolve_aggregate(cfg: Dict[str, Any]) -> AggregateSettings:
+    block = (cfg.get("strategy") or {}).get("aggregate", {}) or {}
+    template = block.get("prompt_template", DEFAULT_PROMPT_TEMPLATE)
+    if "{intermediate_results}" in template:  # reference oai_proxy.py:806-809
+        template = template.replace("{intermediate_results}", "{responses}")
+    return AggregateSettings(
+        aggregator_backend=block.get("aggregator_backend"),
+        source_backends=block.get("source_backends", "all"),
+        prompt_template=template,
+        intermediate_separator=block.get("intermediate_separator", DEFAULT_INTERMEDIATE_SEPARATOR),
+        include_original_query=block.get("include_original_query", True),
+        query_format=block.get("query_format", DEFAULT_QUERY_FORMAT),
+        include_source_names=block.get("include_source_names", False),
+        source_label_format=block.get("source_label_format", DEFAULT_SOURCE_LABEL_FORMAT),
+    )
+
+
+def find_backend(cfg: Dict[str, Any], name: Optional[str]) -> Optional[Dict[str, Any]]:
+    if not name:
+        return None
+    for b in cfg.get("primary_backends", []) or []:
+        if b.get("name") == name:
+            return b
+    return None
+
+
+def valid_backends(cfg: Dict[str, Any]) -> List[Dict[str, Any]]:
+    return [b for b in cfg.get("primary_backends", []) if b.get("url")]
+
+
+def is_parallel(cfg: Dict[str, Any], n_valid: int) -> bool:
+    """reference oai_proxy.py:1043-1044."""
+    return ("iterations" in cfg and "strategy" in cfg) and n_valid > 1
+
+
+def request_timeout(cfg: Dict[str, Any]) -> float:
+    return float((cfg.get("settings") or {}).get("timeout", 60))
+
+
+@dataclass
+class RuntimeConfig:
+    """MI355X runtime knobs (``runtime:`` YAML section / env). Never changes semantics.
+
+    engine:    "auto" (hip when a GPU is visible, else cpu) | "hip" | "cpu" | "python"
+    device:    HIP device ordinal (default LOCAL_RANK)
+    tile_bytes: per-stream input bytes per tick (LDS tile in the fused tick kernel)
+    max_slots: concurrent upstream streams resident per rank
+    content_cap: device-resident filtered-content bytes per stream slot
+    placement: "local" (a session's backends run on the owner rank) | "spread" (EP analog)
+    total_timeout: optional per-backend total deadline in seconds (None = quorum semantics)
+    """
+
+    engine: str = "auto"
+    device: Optional[int] = None
+    tile_bytes: int = 16384
+    max_slots: int = 8192
+    content_cap: int = 1 << 20
+    placement: str = "local"
+    total_timeout: Optional[float] = None
+    log_content: bool = False
+
+    @classmethod
+    def from_config(cls, cfg: Dict[str, Any]) -> "RuntimeConfig":
+        rt = dict((cfg or {}).get("runtime") or {})
+        env_engine = os.environ.get("QMX_ENGINE")
+        if env_engine:
+            rt["engine"] = env_engine
+        known = {k: v for k, v in rt.items() if k in cls.__dataclass_fields__}
+        return cls(**known)
