@@ -1,0 +1,110 @@
+// bindings.cpp — pybind11 module `quorum_amd._qmx` (CPU engine, HIP engine, text ops).
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "qmx_engine.h"
+#include "qmx_hip.h"
+
+namespace py = pybind11;
+using namespace qmx;
+
+namespace {
+
+struct PyStreamFilter {
+  TagSet ts;
+  FilterState fs;
+  explicit PyStreamFilter(const std::vector<std::string>& tags) : ts(make_tagset(tags)) {}
+  py::bytes feed(const std::string& s) {
+    std::string out;
+    filter_feed(ts, fs, (const uint8_t*)s.data(), s.size(), out);
+    return py::bytes(out);
+  }
+  py::bytes flush() {
+    fs = FilterState();
+    return py::bytes("");
+  }
+};
+
+struct PyStripper {
+  TagSet ts;
+  explicit PyStripper(const std::vector<std::string>& tags) : ts(make_tagset(tags)) {}
+  py::bytes strip(const std::string& s) { return py::bytes(strip_final(ts, (const uint8_t*)s.data(), s.size())); }
+};
+
+py::tuple tick_to_py(HostEngine& e, int64_t created) {
+  std::vector<SlotResult> results;
+  std::vector<FinalizeRes> fres;
+  {
+    py::gil_scoped_release nogil;
+    e.tick(created, results, fres);
+  }
+  py::list r;
+  for (auto& x : results) r.append(py::make_tuple(x.slot, py::bytes(x.sse), x.flags));
+  py::list f;
+  for (auto& x : fres) {
+    if (x.kind == 0) {
+      f.append(py::make_tuple(x.id, 0, py::none()));
+    } else if (x.kind == 1) {
+      f.append(py::make_tuple(x.id, 1, py::bytes(x.event)));
+    } else {
+      py::list t;
+      for (auto& s : x.texts) t.append(py::bytes(s));
+      f.append(py::make_tuple(x.id, 2, t));
+    }
+  }
+  return py::make_tuple(r, f);
+}
+
+template <class E>
+void bind_engine(py::class_<E>& c) {
+  c.def("open", &E::open, py::arg("index"), py::arg("filter"), py::arg("emit"))
+      .def("feed", [](E& e, int slot, const py::bytes& b) { e.feed(slot, std::string(b)); })
+      .def("finish", &E::finish)
+      .def("release", &E::release)
+      .def("submit_finalize", &E::submit_finalize)
+      .def("has_work", &E::has_work)
+      .def("tick", [](E& e, int64_t created) { return tick_to_py(e, created); })
+      .def("text", [](E& e, int slot) { return py::bytes(e.text(slot)); })
+      .def("stats", &E::stats);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_qmx, m) {
+  m.doc() = "qmx native core: CPU stream engine, CDNA4 HIP stream engine, text ops";
+  m.def("device_count", []() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+  });
+  m.def("classify", [](const py::bytes& b) -> py::tuple {
+    std::string s(b);
+    EvResult r = classify_event((const uint8_t*)s.data(), (int)s.size());
+    if (r.kind != EV_CONTENT) return py::make_tuple(r.kind, py::none());
+    int n = json_unescape((const uint8_t*)s.data(), r.str_a, r.str_b, nullptr);
+    std::string out(n, '\0');
+    json_unescape((const uint8_t*)s.data(), r.str_a, r.str_b, (uint8_t*)&out[0]);
+    return py::make_tuple(r.kind, py::bytes(out));
+  });
+  m.def("escape", [](const py::bytes& b) {
+    std::string s(b), out;
+    escape_append((const uint8_t*)s.data(), s.size(), out);
+    return py::bytes(out);
+  });
+  py::class_<PyStreamFilter>(m, "StreamFilter")
+      .def(py::init<const std::vector<std::string>&>())
+      .def("feed", &PyStreamFilter::feed)
+      .def("flush", &PyStreamFilter::flush);
+  py::class_<PyStripper>(m, "Stripper")
+      .def(py::init<const std::vector<std::string>&>())
+      .def("strip", &PyStripper::strip);
+  py::class_<CpuEngine> ce(m, "CpuEngine");
+  ce.def(py::init<const std::vector<std::string>&>());
+  bind_engine(ce);
+  py::class_<HipEngine> he(m, "HipEngine");
+  he.def(py::init<const std::vector<std::string>&, int, int, int, int>(), py::arg("tags"), py::arg("device"),
+         py::arg("tile_bytes") = 16384, py::arg("max_slots") = 8192, py::arg("content_cap") = 1 << 20);
+  bind_engine(he);
+  he.def("kernel_stats", &HipEngine::kernel_stats);
+}

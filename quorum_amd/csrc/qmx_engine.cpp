@@ -1,0 +1,381 @@
+// qmx_engine.cpp — host engine core + the sequential (oracle-equivalent) CPU algorithms.
+#include "qmx_engine.h"
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+
+namespace qmx {
+
+const char* kDeltaSuffix = "\"}, \"finish_reason\": null}]}\n\n";
+const char* kFinalSuffix = "\"}, \"finish_reason\": \"stop\"}]}\n\n";
+
+TagSet make_tagset(const std::vector<std::string>& tags) {
+  TagSet ts;
+  std::memset(&ts, 0, sizeof(ts));
+  std::vector<std::string> seen;
+  for (const auto& t0 : tags) {
+    std::string t;
+    for (char c : t0) t.push_back((char)lower_ascii((uint8_t)c));
+    if (std::find(seen.begin(), seen.end(), t) != seen.end()) continue;
+    if (t.empty() || (int)t.size() > kMaxTagLen) throw std::invalid_argument("unsupported tag length: " + t0);
+    for (char c : t) {
+      bool ok = (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9') || c == '_' || c == '-' || c == ':';
+      if (!ok) throw std::invalid_argument("tag needs regex semantics: " + t0);
+    }
+    if (ts.n >= kMaxTags) throw std::invalid_argument("too many thinking tags");
+    seen.push_back(t);
+    ts.len[ts.n] = (int)t.size();
+    std::memcpy(ts.name[ts.n], t.data(), t.size());
+    ++ts.n;
+  }
+  if (ts.n == 0) throw std::invalid_argument("empty tag set");
+  return ts;
+}
+
+// --------------------------------------------------------------------------------
+// streaming filter: state (depth, tail); X = tail ++ text, token walk left to right
+// --------------------------------------------------------------------------------
+void filter_feed(const TagSet& ts, FilterState& fs, const uint8_t* text, size_t n, std::string& out) {
+  std::string xs;
+  xs.reserve(fs.tail_len + n);
+  xs.append((const char*)fs.tail, fs.tail_len);
+  xs.append((const char*)text, n);
+  const uint8_t* x = (const uint8_t*)xs.data();
+  int N = (int)xs.size();
+  int i = 0;
+  fs.tail_len = 0;
+  while (true) {
+    // next token at or after i (depth 0: opens only are tokens)
+    int p = i, tok = 0, L = 0;
+    for (; p < N; ++p) {
+      if (x[p] != '<') continue;
+      tok = match_at(x, N, p, ts, &L);
+      if (tok > 0 || (tok < 0 && fs.depth > 0)) break;
+      tok = 0;
+    }
+    if (p < N) {
+      if (fs.depth == 0) {
+        out.append((const char*)x + i, p - i);
+        fs.depth = 1;
+      } else {
+        fs.depth = tok > 0 ? fs.depth + 1 : std::max(fs.depth - 1, 0);
+      }
+      i = p + L;
+      continue;
+    }
+    // no more tokens: hold back a trailing partial tag from the LAST '<'
+    int q = N - 1;
+    while (q >= i && x[q] != '<') --q;
+    bool hold = q >= i && pattern_prefix(x, q, N, ts, fs.depth == 0);
+    int cut = hold ? q : N;
+    if (fs.depth == 0) out.append((const char*)x + i, cut - i);
+    if (hold) {
+      fs.tail_len = N - q;
+      std::memcpy(fs.tail, x + q, fs.tail_len);
+    }
+    return;
+  }
+}
+
+// --------------------------------------------------------------------------------
+// final strip: tokens, per-tag next-close links, leftmost-first walk, Unicode strip
+// --------------------------------------------------------------------------------
+std::string strip_final(const TagSet& ts, const uint8_t* x, size_t n) {
+  struct Tok { int pos, len, id; };
+  std::vector<Tok> toks;
+  for (int p = 0; p < (int)n; ++p) {
+    if (x[p] != '<') continue;
+    int L = 0;
+    int id = match_at(x, (int)n, p, ts, &L);
+    if (id != 0) toks.push_back({p, L, id});
+  }
+  std::vector<int> next_close(toks.size(), -1);
+  int last[kMaxTags];
+  for (int t = 0; t < kMaxTags; ++t) last[t] = -1;
+  for (int k = (int)toks.size() - 1; k >= 0; --k) {
+    int id = toks[k].id;
+    if (id > 0) next_close[k] = last[id - 1];
+    else last[-id - 1] = k;
+  }
+  std::string out;
+  out.reserve(n);
+  int i = 0;
+  for (int k = 0; k < (int)toks.size(); ++k) {
+    if (toks[k].id <= 0 || toks[k].pos < i) continue;
+    int j = next_close[k];
+    if (j < 0) continue;
+    out.append((const char*)x + i, toks[k].pos - i);
+    i = toks[j].pos + toks[j].len;
+    k = j;
+  }
+  out.append((const char*)x + i, n - i);
+  int a = 0, b = (int)out.size();
+  ustrip((const uint8_t*)out.data(), &a, &b);
+  return out.substr(a, b - a);
+}
+
+// --------------------------------------------------------------------------------
+// SSE encoding
+// --------------------------------------------------------------------------------
+size_t escaped_size(const uint8_t* y, size_t n) {
+  size_t s = 0;
+  for (size_t p = 0; p < n;) {
+    uint32_t cp;
+    p += wtf8_decode(y, (int)p, (int)n, &cp);
+    s += escaped_len_cp(cp);
+  }
+  return s;
+}
+void escape_append(const uint8_t* y, size_t n, std::string& out) {
+  uint8_t buf[12];
+  for (size_t p = 0; p < n;) {
+    uint32_t cp;
+    p += wtf8_decode(y, (int)p, (int)n, &cp);
+    int k = escape_cp(cp, buf);
+    out.append((const char*)buf, k);
+  }
+}
+std::string delta_prefix(int index, int64_t created) {
+  return "data: {\"id\": \"chatcmpl-parallel-" + std::to_string(index) +
+         "\", \"object\": \"chat.completion.chunk\", \"created\": " + std::to_string(created) +
+         ", \"model\": \"parallel-proxy\", \"choices\": [{\"index\": 0, \"delta\": {\"content\": \"";
+}
+std::string final_prefix(int64_t created) {
+  return "data: {\"id\": \"chatcmpl-parallel-final\", \"object\": \"chat.completion.chunk\", \"created\": " +
+         std::to_string(created) +
+         ", \"model\": \"parallel-proxy\", \"choices\": [{\"index\": 0, \"delta\": {\"content\": \"";
+}
+
+// --------------------------------------------------------------------------------
+// per-stream processing (sequential)
+// --------------------------------------------------------------------------------
+static void handle_event(const TagSet& ts, SlotCore& s, const uint8_t* e, int m, int64_t created,
+                         std::string& out, std::string& scratch) {
+  EvResult r = classify_event(e, m);
+  if (r.kind == EV_SKIP) return;
+  if (r.kind == EV_ABORT) {
+    s.aborted = true;
+    return;
+  }
+  int dl = json_unescape(e, r.str_a, r.str_b, nullptr);
+  std::string c(dl, '\0');
+  json_unescape(e, r.str_a, r.str_b, (uint8_t*)&c[0]);
+  scratch.clear();
+  if (s.filter) filter_feed(ts, s.fs, (const uint8_t*)c.data(), c.size(), scratch);
+  else scratch.swap(c);
+  s.content += scratch;
+  if (!scratch.empty() && s.emit) {
+    out += delta_prefix(s.index, created);
+    escape_append((const uint8_t*)scratch.data(), scratch.size(), out);
+    out += kDeltaSuffix;
+  }
+}
+
+void process_slot(const TagSet& ts, SlotCore& s, const uint8_t* data, size_t n, bool eof, int64_t created,
+                  std::string& out) {
+  if (s.aborted || s.done) return;
+  s.carry.append((const char*)data, n);
+  const uint8_t* x = (const uint8_t*)s.carry.data();
+  int N = (int)s.carry.size();
+  int pos = 0;
+  if (!s.started) {
+    while (pos < N) {
+      int w = ws_at(x, pos, N);
+      if (w <= 0) break;
+      pos += w;
+    }
+    bool undecided = pos < N && ws_at(x, pos, N) < 0;
+    if (pos >= N || (undecided && !eof)) {
+      s.carry.erase(0, pos);
+      if (eof) s.done = true;
+      return;
+    }
+    s.started = true;
+  }
+  std::string scratch;
+  while (!s.aborted) {
+    int j = pos;
+    while (j + 1 < N && !(x[j] == '\n' && x[j + 1] == '\n')) ++j;
+    if (j + 1 >= N) break;
+    handle_event(ts, s, x + pos, j - pos, created, out, scratch);
+    pos = j + 2;
+  }
+  if (s.aborted) {
+    s.carry.clear();
+    return;
+  }
+  if (eof) {
+    if (pos < N) handle_event(ts, s, x + pos, N - pos, created, out, scratch);
+    s.carry.clear();
+    if (!s.aborted) s.done = true;
+    return;
+  }
+  s.carry.erase(0, pos);
+}
+
+void finalize_texts(const TagSet& ts, const std::vector<std::string>& texts, const FinalizeReq& r,
+                    FinalizeRes& out) {
+  out.id = r.id;
+  std::vector<std::string> kept;
+  for (const auto& t : texts) {
+    if (t.empty()) continue;
+    kept.push_back(r.strip ? strip_final(ts, (const uint8_t*)t.data(), t.size()) : t);
+  }
+  if (r.texts) {
+    out.kind = 2;
+    out.texts = std::move(kept);
+    return;
+  }
+  if (kept.empty()) {
+    out.kind = 0;
+    return;
+  }
+  std::string joined;
+  for (size_t i = 0; i < kept.size(); ++i) {
+    if (i) joined += r.joiner;
+    joined += kept[i];
+  }
+  out.kind = 1;
+  out.event = final_prefix(r.created);
+  escape_append((const uint8_t*)joined.data(), joined.size(), out.event);
+  out.event += kFinalSuffix;
+}
+
+// --------------------------------------------------------------------------------
+// HostEngine
+// --------------------------------------------------------------------------------
+HostEngine::HostEngine(const std::vector<std::string>& tags) : ts_(make_tagset(tags)) {}
+
+int HostEngine::open(int index, bool filter, bool emit) {
+  std::lock_guard<std::mutex> g(mu_);
+  int slot;
+  if (!free_.empty()) {
+    slot = free_.back();
+    free_.pop_back();
+  } else {
+    slot = (int)meta_.size();
+    meta_.emplace_back();
+    core_.emplace_back();
+  }
+  Meta& m = meta_[slot];
+  m = Meta();
+  m.live = true;
+  SlotCore& c = core_[slot];
+  c = SlotCore();
+  c.index = index;
+  c.filter = filter;
+  c.emit = emit;
+  return slot;
+}
+
+void HostEngine::feed(int slot, const std::string& data) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (slot < 0 || slot >= (int)meta_.size() || !meta_[slot].live) return;
+  Meta& m = meta_[slot];
+  m.incoming += data;
+  bytes_in_ += data.size();
+  if (!m.dirty) {
+    m.dirty = true;
+    dirty_.push_back(slot);
+  }
+}
+
+void HostEngine::finish(int slot) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (slot < 0 || slot >= (int)meta_.size() || !meta_[slot].live) return;
+  Meta& m = meta_[slot];
+  m.eof = true;
+  if (!m.dirty) {
+    m.dirty = true;
+    dirty_.push_back(slot);
+  }
+}
+
+void HostEngine::release(int slot) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (slot < 0 || slot >= (int)meta_.size() || !meta_[slot].live) return;
+  meta_[slot].live = false;
+  meta_[slot].incoming.clear();
+  pending_free_.push_back(slot);
+}
+
+int HostEngine::submit_finalize(const std::vector<int>& slots, bool strip, bool texts, const std::string& joiner,
+                                int64_t created) {
+  std::lock_guard<std::mutex> g(mu_);
+  FinalizeReq r{++next_fid_, slots, strip, texts, joiner, created};
+  fin_.push_back(std::move(r));
+  return next_fid_;
+}
+
+bool HostEngine::has_work() {
+  std::lock_guard<std::mutex> g(mu_);
+  return !dirty_.empty() || !fin_.empty();
+}
+
+void HostEngine::tick(int64_t created, std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres) {
+  std::vector<Work> work;
+  std::vector<FinalizeReq> fin;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (int s : pending_free_) {
+      on_free(s);
+      free_.push_back(s);
+    }
+    pending_free_.clear();
+    work.reserve(dirty_.size());
+    for (int s : dirty_) {
+      Meta& m = meta_[s];
+      m.dirty = false;
+      if (!m.live) continue;
+      Work w{s, std::string(), m.eof, m.fresh};
+      w.data.swap(m.incoming);
+      m.fresh = false;
+      work.push_back(std::move(w));
+    }
+    dirty_.clear();
+    fin.swap(fin_);
+    ++ticks_;
+  }
+  if (!work.empty()) process(work, created, results);
+  for (auto& r : results) bytes_out_ += r.sse.size();
+  if (!fin.empty()) finalize(fin, fres);
+}
+
+std::string HostEngine::text(int slot) {
+  if (slot < 0 || slot >= (int)core_.size()) return std::string();
+  const SlotCore& c = core_[slot];
+  return c.aborted ? std::string() : c.content;
+}
+
+std::unordered_map<std::string, double> HostEngine::stats() {
+  std::lock_guard<std::mutex> g(mu_);
+  return {{"ticks", (double)ticks_}, {"bytes_in", (double)bytes_in_}, {"bytes_out", (double)bytes_out_},
+          {"slots", (double)meta_.size()}, {"free", (double)free_.size()}};
+}
+
+// --------------------------------------------------------------------------------
+// CpuEngine
+// --------------------------------------------------------------------------------
+void CpuEngine::process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results) {
+  for (auto& w : work) {
+    SlotCore& c = core_[w.slot];
+    bool was_closed = c.done || c.aborted;
+    std::string out;
+    process_slot(ts_, c, (const uint8_t*)w.data.data(), w.data.size(), w.eof, created, out);
+    int flags = (c.done ? RF_DONE : 0) | (c.aborted ? RF_ABORTED : 0);
+    if (!out.empty() || (flags && !was_closed)) results.push_back({w.slot, std::move(out), flags});
+  }
+}
+
+void CpuEngine::finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out) {
+  for (auto& r : reqs) {
+    std::vector<std::string> texts;
+    for (int s : r.slots) texts.push_back(text(s));
+    FinalizeRes fr;
+    finalize_texts(ts_, texts, r, fr);
+    out.push_back(std::move(fr));
+  }
+}
+
+}  // namespace qmx

@@ -1,0 +1,145 @@
+// qmx_engine.h — host-side stream engine core (slot table, batching, CPU algorithms).
+//
+// HostEngine owns the per-rank slot table and the tick protocol used by both engines:
+//   open/feed/finish/release/submit_finalize  (event-loop thread, under mu_)
+//   tick()                                    (ticker: inline or worker thread)
+// CpuEngine runs the sequential oracle algorithm per slot; HipEngine (qmx_hip.hip)
+// runs the fused CDNA4 tick kernel over all slots of the batch at once.
+//
+// Reference counterpart: the per-backend processing loop of progress_streaming_aggregator
+// (src/quorum/oai_proxy.py:554-747) and the final combine (:759-881).
+#pragma once
+#include <stdint.h>
+
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "qmx_text.h"
+
+namespace qmx {
+
+enum ResultFlags : int { RF_DONE = 1, RF_ABORTED = 2, RF_ESCALATED = 4 };
+
+TagSet make_tagset(const std::vector<std::string>& tags);
+
+struct FilterState {
+  int depth = 0;
+  int tail_len = 0;
+  uint8_t tail[kMaxTail] = {0};
+};
+
+// Sequential streaming think filter: appends released bytes to `out`.
+void filter_feed(const TagSet& ts, FilterState& fs, const uint8_t* text, size_t n, std::string& out);
+
+// Final strip: same-tag leftmost non-greedy removal + Unicode strip.
+std::string strip_final(const TagSet& ts, const uint8_t* x, size_t n);
+
+// SSE envelopes (json.dumps(ensure_ascii=True) of quorum's event dicts, oai_proxy.py:629-646, 847-860)
+void escape_append(const uint8_t* y, size_t n, std::string& out);
+size_t escaped_size(const uint8_t* y, size_t n);
+std::string delta_prefix(int index, int64_t created);
+std::string final_prefix(int64_t created);
+extern const char* kDeltaSuffix;
+extern const char* kFinalSuffix;
+
+// Host-side per-stream state.
+struct SlotCore {
+  bool filter = true, emit = true, started = false, aborted = false, done = false;
+  int index = 0;
+  std::string carry;  // unframed upstream bytes
+  FilterState fs;
+  std::string content;  // accumulated filtered content (host engine / fallback)
+};
+
+// Process newly arrived bytes of one stream (sequential algorithm); appends SSE to out.
+void process_slot(const TagSet& ts, SlotCore& s, const uint8_t* data, size_t n, bool eof,
+                  int64_t created, std::string& out);
+
+struct SlotResult {
+  int slot;
+  std::string sse;
+  int flags;
+};
+struct FinalizeReq {
+  int id;
+  std::vector<int> slots;
+  bool strip;
+  bool texts;  // return stripped texts instead of the final event
+  std::string joiner;
+  int64_t created;
+};
+struct FinalizeRes {
+  int id;
+  int kind;  // 0 none (all empty), 1 event bytes, 2 texts
+  std::string event;
+  std::vector<std::string> texts;
+};
+
+class HostEngine {
+ public:
+  explicit HostEngine(const std::vector<std::string>& tags);
+  virtual ~HostEngine() = default;
+
+  int open(int index, bool filter, bool emit);
+  void feed(int slot, const std::string& data);
+  void finish(int slot);
+  void release(int slot);
+  int submit_finalize(const std::vector<int>& slots, bool strip, bool texts, const std::string& joiner,
+                      int64_t created);
+  bool has_work();
+  void tick(int64_t created, std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres);
+  virtual std::string text(int slot);
+  virtual std::unordered_map<std::string, double> stats();
+
+  const TagSet& tagset() const { return ts_; }
+
+ protected:
+  struct Work {
+    int slot;
+    std::string data;
+    bool eof;
+    bool fresh;
+  };
+  // engine-specific batch processing
+  virtual void process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results) = 0;
+  virtual void finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out) = 0;
+  virtual void on_free(int /*slot*/) {}
+
+  struct Meta {
+    bool live = false;
+    bool dirty = false;
+    bool eof = false;
+    bool fresh = true;
+    bool closed = false;  // DONE/ABORTED reported
+    std::string incoming;
+  };
+
+  TagSet ts_;
+  std::mutex mu_;
+  std::vector<Meta> meta_;
+  std::vector<SlotCore> core_;  // host state (CPU engine; HIP engine: flags + fallback)
+  std::vector<int> free_, pending_free_;
+  std::vector<int> dirty_;
+  std::vector<FinalizeReq> fin_;
+  int next_fid_ = 0;
+  uint64_t ticks_ = 0, bytes_in_ = 0, bytes_out_ = 0;
+};
+
+class CpuEngine : public HostEngine {
+ public:
+  explicit CpuEngine(const std::vector<std::string>& tags) : HostEngine(tags) {}
+
+ protected:
+  void process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results) override;
+  void finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out) override;
+};
+
+// Shared by both engines' host-side finalisation.
+void finalize_texts(const TagSet& ts, const std::vector<std::string>& texts, const FinalizeReq& r,
+                    FinalizeRes& out);
+
+}  // namespace qmx

@@ -1,0 +1,108 @@
+// qmx_hip.h — HipEngine: the CDNA4 (gfx950) batched stream engine.
+//
+// One fused kernel launch per tick processes every slot with pending upstream bytes:
+//   LDS-staged input tile → parallel SSE framing scan → per-event validating JSON delta
+//   extraction → MFMA int8 think-tag matcher (mfma_i32_16x16x64_i8) → (a,b)-monoid depth
+//   scan → holdback cuts per delta → compaction → device-resident content append →
+//   ensure_ascii SSE encoding staged in LDS → coalesced 16-B stores to host-mapped output.
+// Per-slot filter state and filtered content stay resident in HBM; input/output arenas
+// are pinned host memory mapped into the GPU (zero-copy: no hipMemcpy per tick).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "qmx_engine.h"
+
+namespace qmx {
+
+struct WorkItem {
+  uint32_t slot, in_off, in_len, out_off, out_cap, flags, index, content_len;
+};
+struct WorkResult {
+  uint32_t consumed, out_len, status, content_len;
+};
+struct DevSlot {
+  int32_t depth;
+  int32_t tail_len;
+  uint8_t tail[kMaxTail];
+};
+
+enum WorkFlags : uint32_t { WF_EOF = 1, WF_FILTER = 2, WF_EMIT = 4, WF_STARTED = 8, WF_FRESH = 16 };
+enum WorkStatus : uint32_t { WS_DONE = 1, WS_ABORTED = 2, WS_STARTED = 4, WS_ESCALATE = 8, WS_MORE = 16 };
+
+struct KParams {
+  TagSet ts;
+  int npat;
+  int32_t pat_E[2 * kMaxTags];  // Σ_j m(q0²+q1²) per pattern (match iff dot == -E)
+  uint32_t content_cap;
+  int pre1_len, pre2_len, suf_len;
+  char pre1[48];
+  char pre2[176];
+  char suf[48];
+};
+
+struct FinItem {
+  uint32_t first_text, n_texts;  // into the FinText array
+  uint32_t out_off, out_cap;
+  uint32_t flags;                // 1 strip, 2 texts-kind
+  uint32_t tok_off, tok_cap;     // global scratch for tokens/intervals
+  uint32_t joiner_off, joiner_len;  // into the input arena
+};
+struct FinText {
+  uint32_t slot, len;
+};
+struct FinResult {
+  uint32_t out_len, status, n_kept;  // status: 1 escalate
+  uint32_t text_len[8];              // kind=texts: per-text stripped lengths (first 8)
+};
+
+class HipEngine : public HostEngine {
+ public:
+  HipEngine(const std::vector<std::string>& tags, int device, int tile_bytes, int max_slots, int content_cap);
+  ~HipEngine() override;
+  std::string text(int slot) override;
+  std::unordered_map<std::string, double> kernel_stats();
+
+ protected:
+  void process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results) override;
+  void finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out) override;
+  void on_free(int slot) override;
+
+ private:
+  void escalate(int slot, bool fresh);
+  void ensure_in(size_t bytes);
+  void ensure_out(size_t bytes);
+  void build_params(int64_t created);
+  std::string device_content(int slot, uint32_t len);
+
+  int device_;
+  int tile_;
+  int max_slots_;
+  uint32_t content_cap_;
+  hipStream_t stream_ = nullptr;
+  KParams params_;
+  // host-mapped arenas
+  uint8_t* h_in_ = nullptr;
+  size_t in_cap_ = 0;
+  uint8_t* h_out_ = nullptr;
+  size_t out_cap_ = 0;
+  WorkItem* h_items_ = nullptr;
+  WorkResult* h_res_ = nullptr;
+  FinItem* h_fin_ = nullptr;
+  FinText* h_fint_ = nullptr;
+  FinResult* h_finres_ = nullptr;
+  size_t items_cap_ = 0;
+  // device-resident
+  DevSlot* d_state_ = nullptr;
+  uint8_t* d_content_ = nullptr;
+  uint32_t* d_scratch_ = nullptr;
+  size_t scratch_words_ = 0;
+  // host mirrors
+  std::vector<uint8_t> host_mode_;       // slot escalated to the host path
+  std::vector<uint32_t> content_len_;    // device content bytes per slot
+  // stats
+  uint64_t launches_ = 0, items_ = 0, escalations_ = 0, fin_launches_ = 0;
+  double kernel_ms_ = 0.0;
+  hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
+};
+
+}  // namespace qmx

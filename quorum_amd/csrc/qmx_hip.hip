@@ -1,0 +1,1059 @@
+// qmx_hip.hip — CDNA4 (gfx950) fused tick kernel + HipEngine host runtime.
+//
+// One workgroup (256 threads = 4 wave64) per stream slot with pending bytes; everything
+// between the input tile load and the output store happens in LDS:
+//
+//   S0 load      host-mapped input tile → LDS (16-B vector loads, zero-copy)
+//   S1 start     leading Unicode-whitespace strip at stream start (quorum's body.strip())
+//   S2 framing   "\n\n" separators with Python split() pairing: newline-run lengths via a
+//                block scan over the map monoid x ↦ (all-newline ? x+len : trailing)
+//   S3 extract   one thread per event: strict UTF-8 + validating JSON scan with quorum's
+//                exception semantics (qmx_text.h classify_event); ordered compaction of
+//                content deltas; JSON unescape into Z = tail ++ deltas
+//   S4 filter    '<' candidates → MFMA int8 matcher (v_mfma_i32_16x16x64_i8: 16 candidate
+//                windows × 16 patterns per instruction, exact via digit-split squared
+//                distance) → token list → depth scan over the (a,b) monoid
+//                f(x)=max(x+a,b) → per-delta holdback cuts → kept-byte compaction
+//   S5 content   filtered bytes appended to the slot's HBM-resident content arena
+//   S6 encode    json.dumps(ensure_ascii) SSE events staged in an LDS window, stored with
+//                coalesced 16-B stores to host-mapped output
+//
+// Semantics: SURVEY §2.7 (reference src/quorum/oai_proxy.py:262-371, 578-673).
+#include "qmx_hip.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+namespace qmx {
+
+#define HIP_CHECK(x)                                                                       \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess)                                                                  \
+      throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__));                 \
+  } while (0)
+
+constexpr int BS = 256;
+constexpr int TILE_MAX = 16384;
+constexpr int MAX_EV = 1024;
+constexpr int MAX_CAND = 1024;
+constexpr int PAD = 16;
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+struct Smem {
+  alignas(16) uint8_t A[TILE_MAX + 64];  // X (input) → W (kept bytes) / output window
+  alignas(16) uint8_t B[TILE_MAX + 64];  // Z = tail ++ decoded deltas (at B+PAD) → output window
+  uint16_t ev_a[MAX_EV], ev_b[MAX_EV], ev_sa[MAX_EV], ev_sb[MAX_EV], ev_dl[MAX_EV];
+  uint8_t ev_kind[MAX_EV];
+  uint16_t dl_end[MAX_EV];
+  uint16_t cut[MAX_EV];
+  uint16_t wpos[MAX_EV];
+  uint32_t epos[MAX_EV];
+  uint16_t eidx[MAX_EV];
+  uint16_t cand[MAX_CAND];
+  int8_t cand_tok[MAX_CAND];
+  uint16_t tok_pos[MAX_CAND];
+  uint8_t tok_len[MAX_CAND];
+  int8_t tok_id[MAX_CAND];
+  int16_t tok_dep[MAX_CAND + 1];
+  int32_t chunk_base[BS + 1];
+  int32_t scr[16];
+  int32_t v[32];
+};
+
+enum : int {
+  V_START = 0, V_NSEP, V_LASTSEP, V_ABORT, V_NEV, V_CONSUMED, V_STATUS, V_NDELTA, V_YLEN, V_NCAND,
+  V_NTOK, V_BAIL, V_DEPTH0, V_TAILLEN, V_NEWTAIL, V_NEWDEPTH, V_WLEN, V_NEMIT, V_ETOT, V_OUTLEN
+};
+
+// ------------------------------------------------------------------------------------
+// block-level scans (wave64 shuffles + 4-wave combine)
+// ------------------------------------------------------------------------------------
+__device__ inline int block_excl_sum(int v, int32_t* scr, int* total) {
+  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) scr[w] = x;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < BS / 64; ++i) {
+    int s = scr[i];
+    if (i < w) base += s;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + x - v;
+}
+
+// generic pair monoid scan: T = int2 {a, b}
+template <class Op>
+__device__ inline int2 block_excl_pair(int2 v, int2 ident, Op op, int32_t* scr, int2* total) {
+  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int2 x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int2 y;
+    y.x = __shfl_up(x.x, o, 64);
+    y.y = __shfl_up(x.y, o, 64);
+    if (lane >= o) x = op(y, x);
+  }
+  if (lane == 63) {
+    scr[2 * w] = x.x;
+    scr[2 * w + 1] = x.y;
+  }
+  __syncthreads();
+  int2 base = ident, tot = ident;
+#pragma unroll
+  for (int i = 0; i < BS / 64; ++i) {
+    int2 s = make_int2(scr[2 * i], scr[2 * i + 1]);
+    if (i < w) base = op(base, s);
+    tot = op(tot, s);
+  }
+  __syncthreads();
+  int2 ex;
+  ex.x = __shfl_up(x.x, 1, 64);
+  ex.y = __shfl_up(x.y, 1, 64);
+  if (lane == 0) ex = ident;
+  *total = tot;
+  return op(base, ex);
+}
+
+// newline-run map x ↦ (x.x ? x + x.y : x.y); compose (first f then g)
+struct RunOp {
+  __device__ int2 operator()(int2 f, int2 g) const { return g.x ? make_int2(f.x, f.y + g.y) : g; }
+};
+// depth map x ↦ max(x + a, b); compose (first f then g)
+struct DepthOp {
+  __device__ int2 operator()(int2 f, int2 g) const { return make_int2(f.x + g.x, max(f.y + g.x, g.y)); }
+};
+
+// ------------------------------------------------------------------------------------
+// MFMA tag matcher
+// ------------------------------------------------------------------------------------
+__device__ inline int code_of(uint8_t b) {
+  if (b >= 'a' && b <= 'z') return b - 'a' + 1;
+  if (b >= 'A' && b <= 'Z') return b - 'A' + 1;
+  if (b >= '0' && b <= '9') return 27 + b - '0';
+  switch (b) {
+    case '<': return 37;
+    case '/': return 38;
+    case '>': return 39;
+    case '_': return 40;
+    case '-': return 41;
+    case ':': return 42;
+    default: return 63;
+  }
+}
+
+// B operand (patterns × window features), built once per wave: lane l = pattern (l&15),
+// feature group (l>>4): 0: -2·q0, 1: -2·q1, 2/3: mask (pairs with d0², d1² in A).
+__device__ inline v4i build_pattern_frag(const KParams& P) {
+  int l = threadIdx.x & 63, t = l & 15, kg = l >> 4;
+  int8_t bytes[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    int v = 0;
+    if (t < P.npat && j < pattern_len(P.ts, t)) {
+      int q = code_of(pattern_byte(P.ts, t, j));
+      v = kg == 0 ? -2 * (q & 7) : kg == 1 ? -2 * (q >> 3) : 1;
+    }
+    bytes[j] = (int8_t)v;
+  }
+  v4i b;
+  __builtin_memcpy(&b, bytes, 16);
+  return b;
+}
+
+// 16 candidate windows per MFMA; result[row][pat] == -E[pat]  <=>  window == pattern.
+__device__ inline void mfma_match_group(const uint8_t* Z, int Zn, const uint16_t* cand, int ncand, int g,
+                                        const KParams& P, v4i bfrag, int8_t* cand_tok) {
+  int l = threadIdx.x & 63, r = l & 15, kg = l >> 4;
+  int c = g * 16 + r;
+  int p = c < ncand ? (int)cand[c] : -1;
+  int8_t bytes[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    int code = (p >= 0 && p + j < Zn) ? code_of(Z[p + j]) : 0;
+    int d0 = code & 7, d1 = code >> 3;
+    bytes[j] = (int8_t)(kg == 0 ? d0 : kg == 1 ? d1 : kg == 2 ? d0 * d0 : d1 * d1);
+  }
+  v4i a;
+  __builtin_memcpy(&a, bytes, 16);
+  v4i acc = {0, 0, 0, 0};
+  acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bfrag, acc, 0, 0, 0);
+  int t = l & 15;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int row = 4 * (l >> 4) + i;
+    int cc = g * 16 + row;
+    if (t < P.npat && cc < ncand && acc[i] == -P.pat_E[t])
+      cand_tok[cc] = (int8_t)(t < P.ts.n ? t + 1 : -(t - P.ts.n + 1));
+  }
+}
+
+__device__ inline int tok_plen(const KParams& P, int id) {
+  return id > 0 ? P.ts.len[id - 1] + 2 : P.ts.len[-id - 1] + 3;
+}
+
+// number of tokens with pos < x  /  <= x
+__device__ inline int tok_lower(const Smem& s, int ntok, int x) {
+  int lo = 0, hi = ntok;
+  while (lo < hi) {
+    int m = (lo + hi) >> 1;
+    if (s.tok_pos[m] < x) lo = m + 1;
+    else hi = m;
+  }
+  return lo;
+}
+__device__ inline int tok_upper(const Smem& s, int ntok, int x) {
+  int lo = 0, hi = ntok;
+  while (lo < hi) {
+    int m = (lo + hi) >> 1;
+    if (s.tok_pos[m] <= x) lo = m + 1;
+    else hi = m;
+  }
+  return lo;
+}
+// kept(x) given k = #tokens with pos <= x
+__device__ inline bool kept_at(const Smem& s, int k, int x) {
+  if (k > 0 && x < (int)s.tok_pos[k - 1] + (int)s.tok_len[k - 1])
+    return s.tok_id[k - 1] < 0 && s.tok_dep[k - 1] == 0;
+  return s.tok_dep[k] == 0;
+}
+
+// holdback test at stream position e (Z coords): returns cut (q when held, else e).
+// opens_only=false also reports any-pattern prefixes at depth > 0 (tail carry).
+__device__ inline int hold_cut(const Smem& s, const uint8_t* Z, int ncand, int ntok, int e, const KParams& P,
+                               bool for_tail, int* q_out) {
+  int lo = 0, hi = ncand;  // last candidate index with cand < e
+  while (lo < hi) {
+    int m = (lo + hi) >> 1;
+    if ((int)s.cand[m] < e) lo = m + 1;
+    else hi = m;
+  }
+  int idx = lo - 1;
+  *q_out = -1;
+  if (idx < 0) return e;
+  int q = s.cand[idx];
+  int tk = s.cand_tok[idx];
+  if (tk != 0 && q + tok_plen(P, tk) <= e) return e;  // completed token
+  int dq = s.tok_dep[tok_lower(s, ntok, q)];
+  bool pre = pattern_prefix(Z, q, e, P.ts, dq == 0);
+  if (!pre) return e;
+  if (dq == 0 || for_tail) {
+    *q_out = q;
+    return dq == 0 ? q : e;
+  }
+  return e;
+}
+
+// ------------------------------------------------------------------------------------
+// the fused tick kernel
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict__ items,
+                                                      const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                      WorkResult* __restrict__ res, DevSlot* __restrict__ state,
+                                                      uint8_t* __restrict__ content, KParams P) {
+  __shared__ Smem s;
+  const int tid = threadIdx.x;
+  const WorkItem it = items[blockIdx.x];
+  const int in_len = (int)it.in_len;
+  const bool eof = it.flags & WF_EOF;
+  const bool filt = it.flags & WF_FILTER;
+  const bool emit = it.flags & WF_EMIT;
+  const bool fresh = it.flags & WF_FRESH;
+
+  // ---- S0: load tile (16-B vector loads from host-mapped memory) -----------------
+  for (int i = tid * 16; i < in_len; i += BS * 16)
+    *(uint4*)&s.A[i] = *(const uint4*)&in[it.in_off + i];
+  if (tid == 0) {
+    s.v[V_ABORT] = MAX_EV;
+    s.v[V_LASTSEP] = -1;
+    s.v[V_BAIL] = 0;
+    s.v[V_STATUS] = 0;
+    if (fresh) {
+      s.v[V_DEPTH0] = 0;
+      s.v[V_TAILLEN] = 0;
+    } else {
+      s.v[V_DEPTH0] = state[it.slot].depth;
+      s.v[V_TAILLEN] = state[it.slot].tail_len;
+    }
+  }
+  __syncthreads();
+  const int tail_len = filt ? s.v[V_TAILLEN] : 0;
+  uint8_t* Z = s.B + PAD;
+  if (tid < tail_len) Z[tid] = state[it.slot].tail[tid];
+
+  // ---- S1: leading whitespace at stream start ---------------------------------------
+  if (tid == 0) {
+    int pos = 0;
+    bool started = it.flags & WF_STARTED;
+    bool wait = false;
+    if (!started) {
+      while (pos < in_len) {
+        int w = ws_at(s.A, pos, in_len);
+        if (w <= 0) break;
+        pos += w;
+      }
+      bool undecided = pos < in_len && ws_at(s.A, pos, in_len) < 0;
+      if (pos >= in_len || (undecided && !eof)) wait = true;
+      else s.v[V_STATUS] |= WS_STARTED;
+    }
+    s.v[V_START] = pos;
+    s.v[V_BAIL] = wait ? 1 : 0;
+    if (wait) {
+      s.v[V_CONSUMED] = pos;
+      if (eof) s.v[V_STATUS] |= WS_DONE;
+    }
+  }
+  __syncthreads();
+  if (s.v[V_BAIL]) {
+    if (tid == 0 && fresh) {
+      state[it.slot].depth = 0;
+      state[it.slot].tail_len = 0;
+    }
+    if (tid == 0) {
+      WorkResult r{(uint32_t)s.v[V_CONSUMED], 0u, (uint32_t)s.v[V_STATUS], it.content_len};
+      res[blockIdx.x] = r;
+    }
+    return;
+  }
+  const int start = s.v[V_START];
+
+  // ---- S2: framing -----------------------------------------------------------------
+  {
+    int flen = in_len - start;
+    int C = (flen + BS - 1) / BS;
+    int lo = min(start + tid * C, in_len), hi = min(lo + C, in_len);
+    bool all_nl = true;
+    int trail = 0;
+    for (int p = lo; p < hi; ++p) {
+      if (s.A[p] == '\n') ++trail;
+      else { trail = 0; all_nl = false; }
+    }
+    int2 run = all_nl ? make_int2(1, hi - lo) : make_int2(0, trail);
+    int2 tot2;
+    int2 ex = block_excl_pair(run, make_int2(1, 0), RunOp(), s.scr, &tot2);
+    int r = ex.y;
+    int cnt = 0;
+    for (int p = lo; p < hi; ++p) {
+      if (s.A[p] == '\n') {
+        if (!(r & 1) && p + 1 < in_len && s.A[p + 1] == '\n') ++cnt;
+        ++r;
+      } else {
+        r = 0;
+      }
+    }
+    int nsep;
+    int k = block_excl_sum(cnt, s.scr, &nsep);
+    r = ex.y;
+    for (int p = lo; p < hi; ++p) {
+      if (s.A[p] == '\n') {
+        if (!(r & 1) && p + 1 < in_len && s.A[p + 1] == '\n') {
+          if (k < MAX_EV) s.ev_b[k] = (uint16_t)p;
+          if (k + 1 < MAX_EV) s.ev_a[k + 1] = (uint16_t)(p + 2);
+          atomicMax(&s.v[V_LASTSEP], p);
+          ++k;
+        }
+        ++r;
+      } else {
+        r = 0;
+      }
+    }
+    if (tid == 0) {
+      s.ev_a[0] = (uint16_t)start;
+      s.v[V_NSEP] = nsep;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int nsep = s.v[V_NSEP];
+    int nev, consumed;
+    bool done = false, more = false;
+    if (nsep > MAX_EV) {
+      nev = MAX_EV;
+      consumed = s.ev_b[MAX_EV - 1] + 2;
+      more = true;
+    } else {
+      nev = nsep;
+      int rem = nsep > 0 ? s.v[V_LASTSEP] + 2 : start;
+      consumed = rem;
+      if (eof) {
+        if (rem < in_len) {
+          if (nev < MAX_EV) {
+            s.ev_a[nev] = (uint16_t)rem;
+            s.ev_b[nev] = (uint16_t)in_len;
+            ++nev;
+            consumed = in_len;
+            done = true;
+          } else {
+            more = true;
+          }
+        } else {
+          consumed = in_len;
+          done = true;
+        }
+      }
+    }
+    s.v[V_NEV] = nev;
+    s.v[V_CONSUMED] = consumed;
+    if (done) s.v[V_STATUS] |= WS_DONE;
+    if (more) s.v[V_STATUS] |= WS_MORE;
+  }
+  __syncthreads();
+  const int nev = s.v[V_NEV];
+
+  // ---- S3: per-event extraction (4 consecutive events per thread) --------------------
+  int packed_local[4];
+  {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int k = tid * 4 + i;
+      packed_local[i] = 0;
+      if (k < nev) {
+        int a = s.ev_a[k], b = s.ev_b[k];
+        EvResult r = classify_event(s.A + a, b - a);
+        s.ev_kind[k] = (uint8_t)r.kind;
+        if (r.kind == EV_CONTENT) {
+          int sa = a + r.str_a, sb = a + r.str_b;
+          s.ev_sa[k] = (uint16_t)sa;
+          s.ev_sb[k] = (uint16_t)sb;
+          s.ev_dl[k] = (uint16_t)json_unescape(s.A, sa, sb, nullptr);
+        } else if (r.kind == EV_ABORT) {
+          atomicMin(&s.v[V_ABORT], k);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int kab = s.v[V_ABORT];
+  {
+    int loc = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int k = tid * 4 + i;
+      int pk = 0;
+      if (k < nev && k < kab && s.ev_kind[k] == EV_CONTENT) pk = (1 << 16) | s.ev_dl[k];
+      packed_local[i] = loc;
+      loc += pk;
+    }
+    int tot;
+    int base = block_excl_sum(loc, s.scr, &tot);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int k = tid * 4 + i;
+      if (k < nev && k < kab && s.ev_kind[k] == EV_CONTENT) {
+        int pre = base + packed_local[i];
+        int j = pre >> 16, doff = pre & 0xFFFF;
+        int dl = s.ev_dl[k];
+        s.dl_end[j] = (uint16_t)(tail_len + doff + dl);
+        json_unescape(s.A, s.ev_sa[k], s.ev_sb[k], Z + tail_len + doff);
+      }
+    }
+    if (tid == 0) {
+      s.v[V_NDELTA] = tot >> 16;
+      s.v[V_YLEN] = tot & 0xFFFF;
+      if (kab < MAX_EV && kab < nev) {
+        s.v[V_STATUS] = (s.v[V_STATUS] | WS_ABORTED) & ~(WS_DONE | WS_MORE);
+        s.v[V_CONSUMED] = in_len;
+      }
+    }
+  }
+  __syncthreads();
+  const int ndelta = s.v[V_NDELTA];
+  const int Zn = tail_len + s.v[V_YLEN];
+  const int depth0 = s.v[V_DEPTH0];
+
+  // ---- S4: think filter ----------------------------------------------------------------
+  const uint8_t* W = Z;  // identity when not filtering
+  int ncand = 0, ntok = 0;
+  if (filt && ndelta > 0) {
+    // candidates
+    {
+      int C = (Zn + BS - 1) / BS;
+      int lo = min(tid * C, Zn), hi = min(lo + C, Zn);
+      int cnt = 0;
+      for (int p = lo; p < hi; ++p) cnt += Z[p] == '<';
+      int tot;
+      int k = block_excl_sum(cnt, s.scr, &tot);
+      if (tot <= MAX_CAND)
+        for (int p = lo; p < hi; ++p)
+          if (Z[p] == '<') s.cand[k++] = (uint16_t)p;
+      ncand = tot;
+    }
+    if (ncand > MAX_CAND) {
+      if (tid == 0) {
+        WorkResult r{0u, 0u, (uint32_t)WS_ESCALATE, it.content_len};
+        res[blockIdx.x] = r;
+      }
+      return;  // uniform: every thread saw the same total
+    }
+    for (int c = tid; c < ncand; c += BS) s.cand_tok[c] = 0;
+    __syncthreads();
+    {
+      v4i bfrag = build_pattern_frag(P);
+      int w = tid >> 6;
+      for (int g = w; g * 16 < ncand; g += BS / 64) mfma_match_group(Z, Zn, s.cand, ncand, g, P, bfrag, s.cand_tok);
+    }
+    __syncthreads();
+    // token compaction (4 candidates per thread)
+    {
+      int loc = 0, flags[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int c = tid * 4 + i;
+        flags[i] = loc;
+        loc += (c < ncand && s.cand_tok[c] != 0) ? 1 : 0;
+      }
+      int tot;
+      int base = block_excl_sum(loc, s.scr, &tot);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int c = tid * 4 + i;
+        if (c < ncand && s.cand_tok[c] != 0) {
+          int k = base + flags[i];
+          int id = s.cand_tok[c];
+          s.tok_pos[k] = s.cand[c];
+          s.tok_id[k] = (int8_t)id;
+          s.tok_len[k] = (uint8_t)tok_plen(P, id);
+        }
+      }
+      ntok = tot;
+    }
+    __syncthreads();
+    // depth scan over tokens: open (1,1), close (-1,0)
+    {
+      int2 loc = make_int2(0, 0);
+      int2 pre[4];
+      DepthOp op;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int k = tid * 4 + i;
+        pre[i] = loc;
+        if (k < ntok) loc = op(loc, s.tok_id[k] > 0 ? make_int2(1, 1) : make_int2(-1, 0));
+      }
+      int2 tot;
+      int2 base = block_excl_pair(loc, make_int2(0, 0), op, s.scr, &tot);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int k = tid * 4 + i;
+        if (k < ntok) {
+          int2 f = op(base, pre[i]);
+          s.tok_dep[k] = (int16_t)max(depth0 + f.x, f.y);
+        }
+      }
+      if (tid == 0) s.tok_dep[ntok] = (int16_t)max(depth0 + tot.x, tot.y);
+    }
+    __syncthreads();
+    // cuts per delta + new tail
+    for (int j = tid; j < ndelta; j += BS) {
+      int q;
+      s.cut[j] = (uint16_t)hold_cut(s, Z, ncand, ntok, s.dl_end[j], P, false, &q);
+    }
+    if (tid == 0) {
+      int q;
+      hold_cut(s, Z, ncand, ntok, Zn, P, true, &q);
+      s.v[V_NEWTAIL] = q;
+      s.v[V_NEWDEPTH] = s.tok_dep[ntok];
+    }
+    __syncthreads();
+    // compaction of kept bytes in [0, cutN) into W (= A; input tile no longer needed)
+    {
+      const int cutN = s.cut[ndelta - 1];
+      int C = (cutN + BS - 1) / BS;
+      int lo = min(tid * C, cutN), hi = min(lo + C, cutN);
+      int k = tok_upper(s, ntok, lo);
+      int cnt = 0;
+      for (int x = lo; x < hi; ++x) {
+        while (k < ntok && (int)s.tok_pos[k] <= x) ++k;
+        cnt += kept_at(s, k, x);
+      }
+      int tot;
+      int base = block_excl_sum(cnt, s.scr, &tot);
+      s.chunk_base[tid] = base;
+      if (tid == 0) {
+        s.chunk_base[BS] = tot;
+        s.v[V_WLEN] = tot;
+      }
+      k = tok_upper(s, ntok, lo);
+      int o = base;
+      for (int x = lo; x < hi; ++x) {
+        while (k < ntok && (int)s.tok_pos[k] <= x) ++k;
+        if (kept_at(s, k, x)) s.A[o++] = Z[x];
+      }
+      __syncthreads();
+      for (int j = tid; j < ndelta; j += BS) {
+        int c = s.cut[j];
+        if (c >= cutN) {
+          s.wpos[j] = (uint16_t)s.chunk_base[BS];
+          continue;
+        }
+        int t = C > 0 ? c / C : 0;
+        int tlo = min(t * C, cutN);
+        int kk = tok_upper(s, ntok, tlo);
+        int cc = s.chunk_base[t];
+        for (int x = tlo; x < c; ++x) {
+          while (kk < ntok && (int)s.tok_pos[kk] <= x) ++kk;
+          cc += kept_at(s, kk, x);
+        }
+        s.wpos[j] = (uint16_t)cc;
+      }
+    }
+    W = s.A;
+  } else {
+    for (int j = tid; j < ndelta; j += BS) {
+      s.cut[j] = s.dl_end[j];
+      s.wpos[j] = s.dl_end[j];  // tail_len == 0 when not filtering
+    }
+    if (tid == 0) {
+      s.v[V_WLEN] = ndelta > 0 ? Zn : 0;
+      s.v[V_NEWTAIL] = -1;
+      s.v[V_NEWDEPTH] = depth0;
+    }
+  }
+  __syncthreads();
+  const int Wlen = s.v[V_WLEN];
+
+  // ---- S6 (sizing): emitted deltas, escaped lengths -------------------------------------
+  int n_emit = 0, etot = 0;
+  const int ndig = it.index >= 100 ? 3 : it.index >= 10 ? 2 : 1;
+  const int PRE = P.pre1_len + ndig + P.pre2_len, SUF = P.suf_len, EVL = PRE + SUF;
+  if (emit && ndelta > 0) {
+    {
+      int loc = 0, pre[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int j = tid * 4 + i;
+        pre[i] = loc;
+        if (j < ndelta) loc += (s.wpos[j] > (j ? s.wpos[j - 1] : 0)) ? 1 : 0;
+      }
+      int tot;
+      int base = block_excl_sum(loc, s.scr, &tot);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int j = tid * 4 + i;
+        if (j < ndelta) s.eidx[j] = (uint16_t)(base + pre[i]);
+      }
+      n_emit = tot;
+    }
+    {
+      int C = (Wlen + BS - 1) / BS;
+      int lo = min(tid * C, Wlen), hi = min(lo + C, Wlen);
+      int x = lo;
+      while (x < hi && is_cont(W[x])) ++x;
+      int e = 0;
+      while (x < hi) {
+        uint32_t cp;
+        x += wtf8_decode(W, x, Wlen, &cp);
+        e += escaped_len_cp(cp);
+      }
+      int base = block_excl_sum(e, s.scr, &etot);
+      s.chunk_base[tid] = base;
+      __syncthreads();
+      for (int j = tid; j < ndelta; j += BS) {
+        int wp = s.wpos[j];
+        if (wp >= Wlen) {
+          s.epos[j] = (uint32_t)etot;
+          continue;
+        }
+        int t = C > 0 ? wp / C : 0;
+        int tlo = min(t * C, Wlen);
+        int xx = tlo;
+        while (xx < wp && is_cont(W[xx])) ++xx;
+        int ee = s.chunk_base[t];
+        while (xx < wp) {
+          uint32_t cp;
+          xx += wtf8_decode(W, xx, Wlen, &cp);
+          ee += escaped_len_cp(cp);
+        }
+        s.epos[j] = (uint32_t)ee;
+      }
+    }
+    __syncthreads();
+  }
+  const int out_len = emit ? n_emit * EVL + etot : 0;
+  const uint32_t new_clen = it.content_len + (uint32_t)Wlen;
+  if ((uint32_t)out_len > it.out_cap || new_clen > P.content_cap) {
+    if (tid == 0) {
+      WorkResult r{0u, 0u, (uint32_t)WS_ESCALATE, it.content_len};
+      res[blockIdx.x] = r;
+    }
+    return;
+  }
+
+  // ---- S5: commit content + state ---------------------------------------------------
+  {
+    uint8_t* dst = content + (size_t)it.slot * P.content_cap + it.content_len;
+    for (int x = tid; x < Wlen; x += BS) dst[x] = W[x];
+  }
+  if (filt) {
+    int q = s.v[V_NEWTAIL];
+    int tl = (ndelta > 0) ? (q >= 0 ? Zn - q : 0) : tail_len;
+    if (tid < tl) state[it.slot].tail[tid] = ndelta > 0 ? Z[q + tid] : Z[tid];
+    if (tid == 0) {
+      state[it.slot].tail_len = tl;
+      state[it.slot].depth = ndelta > 0 ? s.v[V_NEWDEPTH] : depth0;
+    }
+  } else if (fresh && tid == 0) {
+    state[it.slot].tail_len = 0;
+    state[it.slot].depth = 0;
+  }
+  __syncthreads();
+
+  // ---- S6 (write): SSE events through an LDS window, 16-B stores to host memory ------
+  if (out_len > 0) {
+    // output window: whichever tile buffer does not hold W (Z's tail is already committed)
+    uint8_t* O = (W == s.A) ? s.B : s.A;
+    const int WIN = TILE_MAX;
+    const int C = (Wlen + BS - 1) / BS;
+    for (int w0 = 0; w0 < out_len; w0 += WIN) {
+      const int w1 = min(w0 + WIN, out_len);
+      // envelopes
+      for (int j = tid; j < ndelta; j += BS) {
+        int wb = j ? s.wpos[j - 1] : 0;
+        if (s.wpos[j] <= wb) continue;
+        int k = s.eidx[j];
+        int es = j ? (int)s.epos[j - 1] : 0;
+        int ee = (int)s.epos[j];
+        int o = k * EVL + es;
+        for (int i = 0; i < P.pre1_len; ++i, ++o)
+          if (o >= w0 && o < w1) O[o - w0] = P.pre1[i];
+        char dg[3];
+        int v = it.index;
+        for (int i = ndig - 1; i >= 0; --i) { dg[i] = (char)('0' + v % 10); v /= 10; }
+        for (int i = 0; i < ndig; ++i, ++o)
+          if (o >= w0 && o < w1) O[o - w0] = dg[i];
+        for (int i = 0; i < P.pre2_len; ++i, ++o)
+          if (o >= w0 && o < w1) O[o - w0] = P.pre2[i];
+        o = k * EVL + PRE + ee;
+        for (int i = 0; i < SUF; ++i, ++o)
+          if (o >= w0 && o < w1) O[o - w0] = P.suf[i];
+      }
+      // escaped content
+      {
+        int lo = min(tid * C, Wlen), hi = min(lo + C, Wlen);
+        int x = lo;
+        while (x < hi && is_cont(W[x])) ++x;
+        // delta containing x: first j with wpos[j] > x
+        int j = 0;
+        {
+          int a = 0, b = ndelta;
+          while (a < b) {
+            int m = (a + b) >> 1;
+            if ((int)s.wpos[m] <= x) a = m + 1;
+            else b = m;
+          }
+          j = a;
+        }
+        int e = s.chunk_base[tid];
+        uint8_t buf[12];
+        while (x < hi) {
+          while (j < ndelta && (int)s.wpos[j] <= x) ++j;
+          uint32_t cp;
+          x += wtf8_decode(W, x, Wlen, &cp);
+          int n = escape_cp(cp, buf);
+          int o = (int)s.eidx[j] * EVL + PRE + e;
+          for (int i = 0; i < n; ++i)
+            if (o + i >= w0 && o + i < w1) O[o + i - w0] = buf[i];
+          e += n;
+        }
+      }
+      __syncthreads();
+      const int wl = w1 - w0;
+      for (int i = tid * 16; i < wl; i += BS * 16) *(uint4*)&out[it.out_off + w0 + i] = *(const uint4*)&O[i];
+      __syncthreads();
+    }
+  }
+  if (tid == 0) {
+    WorkResult r{(uint32_t)s.v[V_CONSUMED], (uint32_t)out_len, (uint32_t)s.v[V_STATUS], new_clen};
+    res[blockIdx.x] = r;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// HipEngine host runtime
+// ------------------------------------------------------------------------------------
+static void put(char* dst, int cap, int* len, const std::string& s) {
+  if ((int)s.size() > cap) throw std::runtime_error("envelope too long");
+  std::memcpy(dst, s.data(), s.size());
+  *len = (int)s.size();
+}
+
+HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_bytes, int max_slots,
+                     int content_cap)
+    : HostEngine(tags),
+      device_(device),
+      tile_(std::min(std::max(tile_bytes, 1024), TILE_MAX) & ~15),
+      max_slots_(max_slots),
+      content_cap_((uint32_t)content_cap) {
+  HIP_CHECK(hipSetDevice(device_));
+  HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  HIP_CHECK(hipEventCreate(&ev0_));
+  HIP_CHECK(hipEventCreate(&ev1_));
+  HIP_CHECK(hipMalloc(&d_state_, sizeof(DevSlot) * (size_t)max_slots_));
+  HIP_CHECK(hipMemset(d_state_, 0, sizeof(DevSlot) * (size_t)max_slots_));
+  HIP_CHECK(hipMalloc(&d_content_, (size_t)content_cap_ * (size_t)max_slots_));
+  ensure_in(8u << 20);
+  ensure_out(32u << 20);
+  items_cap_ = 4096;
+  HIP_CHECK(hipHostMalloc((void**)&h_items_, sizeof(WorkItem) * items_cap_, hipHostMallocMapped));
+  HIP_CHECK(hipHostMalloc((void**)&h_res_, sizeof(WorkResult) * items_cap_, hipHostMallocMapped));
+  std::memset(&params_, 0, sizeof(params_));
+  params_.ts = ts_;
+  params_.npat = 2 * ts_.n;
+  for (int p = 0; p < params_.npat; ++p) {
+    int E = 0;
+    for (int j = 0; j < pattern_len(ts_, p); ++j) {
+      uint8_t b = pattern_byte(ts_, p, j);
+      int q = (b >= 'a' && b <= 'z') ? b - 'a' + 1 : (b >= '0' && b <= '9') ? 27 + b - '0'
+              : b == '<' ? 37 : b == '/' ? 38 : b == '>' ? 39 : b == '_' ? 40 : b == '-' ? 41 : b == ':' ? 42 : 63;
+      E += (q & 7) * (q & 7) + (q >> 3) * (q >> 3);
+    }
+    params_.pat_E[p] = E;
+  }
+  params_.content_cap = content_cap_;
+  host_mode_.assign(max_slots_, 0);
+  content_len_.assign(max_slots_, 0);
+}
+
+HipEngine::~HipEngine() {
+  if (stream_) hipStreamSynchronize(stream_);
+  if (h_in_) hipHostFree(h_in_);
+  if (h_out_) hipHostFree(h_out_);
+  if (h_items_) hipHostFree(h_items_);
+  if (h_res_) hipHostFree(h_res_);
+  if (d_state_) hipFree(d_state_);
+  if (d_content_) hipFree(d_content_);
+  if (d_scratch_) hipFree(d_scratch_);
+  if (ev0_) hipEventDestroy(ev0_);
+  if (ev1_) hipEventDestroy(ev1_);
+  if (stream_) hipStreamDestroy(stream_);
+}
+
+void HipEngine::ensure_in(size_t bytes) {
+  if (bytes <= in_cap_) return;
+  if (h_in_) HIP_CHECK(hipHostFree(h_in_));
+  in_cap_ = std::max(bytes, in_cap_ * 2);
+  HIP_CHECK(hipHostMalloc((void**)&h_in_, in_cap_ + 64, hipHostMallocMapped));
+}
+void HipEngine::ensure_out(size_t bytes) {
+  if (bytes <= out_cap_) return;
+  if (h_out_) HIP_CHECK(hipHostFree(h_out_));
+  out_cap_ = std::max(bytes, out_cap_ * 2);
+  HIP_CHECK(hipHostMalloc((void**)&h_out_, out_cap_ + 64, hipHostMallocMapped));
+}
+
+void HipEngine::build_params(int64_t created) {
+  put(params_.pre1, sizeof(params_.pre1), &params_.pre1_len, "data: {\"id\": \"chatcmpl-parallel-");
+  put(params_.pre2, sizeof(params_.pre2), &params_.pre2_len,
+      "\", \"object\": \"chat.completion.chunk\", \"created\": " + std::to_string(created) +
+          ", \"model\": \"parallel-proxy\", \"choices\": [{\"index\": 0, \"delta\": {\"content\": \"");
+  put(params_.suf, sizeof(params_.suf), &params_.suf_len, kDeltaSuffix);
+}
+
+void HipEngine::on_free(int slot) {
+  if (slot >= 0 && slot < max_slots_) {
+    host_mode_[slot] = 0;
+    content_len_[slot] = 0;
+  }
+}
+
+std::string HipEngine::device_content(int slot, uint32_t len) {
+  std::string out(len, '\0');
+  if (len)
+    HIP_CHECK(hipMemcpy(&out[0], d_content_ + (size_t)slot * content_cap_, len, hipMemcpyDeviceToHost));
+  return out;
+}
+
+void HipEngine::escalate(int slot, bool fresh) {
+  // migrate the slot to the host path: import filter state + content from HBM
+  SlotCore& c = core_[slot];
+  if (!fresh) {
+    DevSlot ds;
+    HIP_CHECK(hipMemcpy(&ds, d_state_ + slot, sizeof(DevSlot), hipMemcpyDeviceToHost));
+    c.fs.depth = ds.depth;
+    c.fs.tail_len = ds.tail_len;
+    std::memcpy(c.fs.tail, ds.tail, kMaxTail);
+  } else {
+    c.fs = FilterState();
+  }
+  c.content = device_content(slot, content_len_[slot]);
+  host_mode_[slot] = 1;
+  ++escalations_;
+}
+
+std::string HipEngine::text(int slot) {
+  if (slot < 0 || slot >= (int)core_.size()) return std::string();
+  const SlotCore& c = core_[slot];
+  if (c.aborted) return std::string();
+  if (slot >= max_slots_ || host_mode_[slot]) return c.content;
+  return device_content(slot, content_len_[slot]);
+}
+
+void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results) {
+  struct Pending {
+    int slot;
+    size_t carry_len;  // carry bytes that preceded w.data in the tile
+    size_t submitted;  // tile bytes
+    bool eof_sent;
+    Work* w;
+  };
+  std::vector<Pending> pend;
+  pend.reserve(work.size());
+  std::vector<int> requeue;
+  size_t in_need = 0, out_need = 0;
+  for (auto& w : work) {
+    size_t tot = core_[w.slot].carry.size() + w.data.size();
+    size_t sub = std::min(tot, (size_t)tile_);
+    in_need += (sub + 15) & ~(size_t)15;
+    out_need += ((12 * sub + 1024) + 15) & ~(size_t)15;
+  }
+  ensure_in(in_need + 64);
+  ensure_out(out_need + 64);
+  if (work.size() > items_cap_) {
+    hipHostFree(h_items_);
+    hipHostFree(h_res_);
+    items_cap_ = work.size() * 2;
+    HIP_CHECK(hipHostMalloc((void**)&h_items_, sizeof(WorkItem) * items_cap_, hipHostMallocMapped));
+    HIP_CHECK(hipHostMalloc((void**)&h_res_, sizeof(WorkResult) * items_cap_, hipHostMallocMapped));
+  }
+  size_t in_off = 0, out_off = 0;
+  int n = 0;
+  for (auto& w : work) {
+    int slot = w.slot;
+    SlotCore& c = core_[slot];
+    if (slot >= max_slots_ || host_mode_[slot]) {
+      bool was_closed = c.done || c.aborted;
+      std::string o;
+      process_slot(ts_, c, (const uint8_t*)w.data.data(), w.data.size(), w.eof, created, o);
+      int flags = (c.done ? RF_DONE : 0) | (c.aborted ? RF_ABORTED : 0) | RF_ESCALATED;
+      if (!o.empty() || ((flags & (RF_DONE | RF_ABORTED)) && !was_closed)) results.push_back({slot, std::move(o), flags});
+      continue;
+    }
+    if (c.done || c.aborted) continue;
+    size_t cl = c.carry.size(), tot = cl + w.data.size();
+    size_t sub = std::min(tot, (size_t)tile_);
+    bool eof_sent = w.eof && sub == tot;
+    // copy carry + data prefix into the arena
+    size_t a = std::min(cl, sub);
+    std::memcpy(h_in_ + in_off, c.carry.data(), a);
+    if (sub > a) std::memcpy(h_in_ + in_off + a, w.data.data(), sub - a);
+    WorkItem& it = h_items_[n];
+    it.slot = (uint32_t)slot;
+    it.in_off = (uint32_t)in_off;
+    it.in_len = (uint32_t)sub;
+    it.out_off = (uint32_t)out_off;
+    it.out_cap = (uint32_t)(12 * sub + 1024);
+    it.flags = (eof_sent ? WF_EOF : 0) | (c.filter ? WF_FILTER : 0) | (c.emit ? WF_EMIT : 0) |
+               (c.started ? WF_STARTED : 0) | (w.fresh ? WF_FRESH : 0);
+    it.index = (uint32_t)c.index;
+    it.content_len = content_len_[slot];
+    in_off += (sub + 15) & ~(size_t)15;
+    out_off += ((size_t)it.out_cap + 15) & ~(size_t)15;
+    pend.push_back({slot, cl, sub, eof_sent, &w});
+    ++n;
+  }
+  if (n > 0) {
+    build_params(created);
+    HIP_CHECK(hipEventRecord(ev0_, stream_));
+    hipLaunchKernelGGL(qmx_tick_kernel, dim3(n), dim3(BS), 0, stream_, h_items_, h_in_, h_out_, h_res_, d_state_,
+                       d_content_, params_);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipEventRecord(ev1_, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, ev0_, ev1_);
+    kernel_ms_ += ms;
+    ++launches_;
+    items_ += n;
+  }
+  for (int i = 0; i < n; ++i) {
+    Pending& p = pend[i];
+    SlotCore& c = core_[p.slot];
+    const WorkResult r = h_res_[i];
+    Work& w = *p.w;
+    // rebuild the unconsumed remainder: (carry + data)[consumed:]
+    auto remainder = [&](size_t consumed) {
+      std::string rem;
+      size_t cl = p.carry_len;
+      if (consumed < cl) {
+        rem.assign(c.carry, consumed, std::string::npos);
+        rem += w.data;
+      } else {
+        rem.assign(w.data, consumed - cl, std::string::npos);
+      }
+      return rem;
+    };
+    bool no_progress = (r.status & WS_ESCALATE) ||
+                       (p.submitted == (size_t)tile_ && r.consumed == 0 && !(r.status & (WS_DONE | WS_ABORTED)));
+    if (no_progress) {
+      escalate(p.slot, w.fresh);
+      std::string all = remainder(0);
+      c.carry.clear();
+      bool was_closed = c.done || c.aborted;
+      std::string o;
+      process_slot(ts_, c, (const uint8_t*)all.data(), all.size(), w.eof, created, o);
+      int flags = (c.done ? RF_DONE : 0) | (c.aborted ? RF_ABORTED : 0) | RF_ESCALATED;
+      if (!o.empty() || ((flags & (RF_DONE | RF_ABORTED)) && !was_closed)) results.push_back({p.slot, std::move(o), flags});
+      continue;
+    }
+    if (r.status & WS_STARTED) c.started = true;
+    content_len_[p.slot] = r.content_len;
+    int flags = 0;
+    if (r.status & WS_ABORTED) {
+      c.aborted = true;
+      c.carry.clear();
+      flags |= RF_ABORTED;
+    } else {
+      c.carry = remainder(r.consumed);
+      if (r.status & WS_DONE) {
+        c.done = true;
+        c.carry.clear();
+        flags |= RF_DONE;
+      } else if ((r.status & WS_MORE) || p.submitted < p.carry_len + w.data.size()) {
+        requeue.push_back(p.slot);  // unprocessed bytes (or a pending EOF) remain
+      }
+    }
+    std::string sse;
+    if (r.out_len) sse.assign((const char*)h_out_ + h_items_[i].out_off, r.out_len);
+    if (!sse.empty() || flags) results.push_back({p.slot, std::move(sse), flags});
+  }
+  if (!requeue.empty()) {
+    std::lock_guard<std::mutex> g(mu_);
+    for (int s : requeue) {
+      Meta& m = meta_[s];
+      if (!m.live || m.dirty) continue;
+      m.dirty = true;
+      dirty_.push_back(s);
+    }
+  }
+}
+
+void HipEngine::finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out) {
+  // v1: texts gathered from HBM, strip/join/encode on the host library
+  for (auto& r : reqs) {
+    std::vector<std::string> texts;
+    for (int s : r.slots) texts.push_back(text(s));
+    FinalizeRes fr;
+    finalize_texts(ts_, texts, r, fr);
+    out.push_back(std::move(fr));
+  }
+}
+
+std::unordered_map<std::string, double> HipEngine::kernel_stats() {
+  return {{"launches", (double)launches_}, {"items", (double)items_}, {"kernel_ms", kernel_ms_},
+          {"escalations", (double)escalations_}, {"fin_launches", (double)fin_launches_}};
+}
+
+}  // namespace qmx

@@ -1,0 +1,94 @@
+"""Build the native extension in-tree: ``quorum_amd/_qmx<EXT_SUFFIX>``.
+
+Every translation unit is compiled by ``hipcc -x hip --offload-arch=gfx950`` (host code for
+the CPU engine, device code for the CDNA4 kernels) and linked into one pybind11 module,
+so the built ``.so`` travels with the repo snapshot to the GPU box.
+
+    python -m quorum_amd.ops.build [--debug] [--jobs N]
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent.parent
+CSRC = PKG / "csrc"
+BUILD = PKG.parent / "build" / "qmx"
+SOURCES = ["qmx_engine.cpp", "qmx_hip.hip", "bindings.cpp"]
+ARCH = os.environ.get("QMX_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm is required to build quorum_amd)")
+
+
+def ext_path() -> Path:
+    return PKG / ("_qmx" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def _flags(debug: bool):
+    import pybind11
+
+    inc = [f"-I{CSRC}", f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
+    opt = ["-O0", "-g"] if debug else ["-O3"]
+    return inc + opt + ["-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
+                        "-fvisibility=hidden"]
+
+
+def build(debug: bool = False, jobs: int = 3, verbose: bool = False) -> Path:
+    cc = hipcc()
+    BUILD.mkdir(parents=True, exist_ok=True)
+    flags = _flags(debug)
+    out = ext_path()
+    headers = list(CSRC.glob("*.h"))
+    newest_hdr = max((h.stat().st_mtime for h in headers), default=0)
+
+    def obj(src: str) -> Path:
+        s = CSRC / src
+        o = BUILD / (src + ".o")
+        if o.exists() and o.stat().st_mtime > max(s.stat().st_mtime, newest_hdr):
+            return o
+        cmd = [cc, "-x", "hip", "-c", str(s), "-o", str(o)] + flags
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {src}\n{r.stdout}\n{r.stderr}")
+        return o
+
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(obj, SOURCES))
+    if out.exists() and out.stat().st_mtime > max(o.stat().st_mtime for o in objs):
+        return out
+    cmd = [cc, "-shared", "-o", str(out)] + [str(o) for o in objs] + [
+        f"--offload-arch={ARCH}", "-fPIC", "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed\n{r.stdout}\n{r.stderr}")
+    return out
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--debug", action="store_true")
+    ap.add_argument("--jobs", type=int, default=3)
+    ap.add_argument("-v", "--verbose", action="store_true")
+    args = ap.parse_args(argv)
+    path = build(args.debug, args.jobs, args.verbose)
+    print(path)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
