@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""Headline benchmark: proxied req/s (whole node) + p50 TTFT, 2-backend concatenate stream.
+
+BASELINE.json metric/config: 2 mock backends, streaming ``concatenate`` with
+``hide_intermediate_think: true`` and ``skip_final_aggregation: true``; every upstream
+response is the survey's shape (role + 4 split <think> fragments + 20 tokens + stop +
+[DONE]).  One rank per GPU (``torch.distributed.run``); each rank runs:
+
+* its proxy (``--impl native``: C++ epoll data plane; ``python``: FastAPI/uvicorn workers)
+  on ONE node-wide SO_REUSEPORT port — the kernel shards client sessions across the
+  node's GPUs — with the CDNA4 tick kernel on its own GPU (``--engine hip``);
+* two C++ mock backends and a C++ closed-loop load generator (synthetic traffic).
+
+A *step* = ``--batch`` completed client requests per rank.  W warmup steps, then EXACTLY
+K timed steps bracketed by barrier + ``torch.cuda.synchronize()``; the slowest rank's
+time is used; rank 0 prints one JSON line.  ``value`` = total completed requests / time
+(whole node).  Weak scaling: per-rank load is fixed as N grows.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import signal
+import socket
+import statistics
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_RPS = 9.1  # reference, 2 backends, same config, 16 clients
+
+
+def _free_port_block(base: int) -> int:
+    return base
+
+
+def _kill(procs):
+    for p in procs:
+        try:
+            os.killpg(p.pid, signal.SIGTERM)
+        except OSError:
+            pass
+    for p in procs:
+        try:
+            p.wait(timeout=10)
+        except Exception:  # noqa: BLE001
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except OSError:
+                pass
+
+
+def write_config(path: str, mock_ports, skip_final: bool, tile: int) -> None:
+    import yaml
+
+    cfg = {
+        "settings": {"timeout": 30},
+        "primary_backends": [{"name": f"LLM{i + 1}", "url": f"http://127.0.0.1:{p}/v1", "model": f"mock-{i + 1}"}
+                             for i, p in enumerate(mock_ports)],
+        "iterations": {"aggregation": {"strategy": "concatenate"}},
+        "strategy": {"concatenate": {
+            "separator": "\n-------------\n", "hide_intermediate_think": True, "hide_final_think": False,
+            "thinking_tags": ["think", "reason", "reasoning", "thought"],
+            "skip_final_aggregation": skip_final}},
+        "runtime": {"tile_bytes": tile, "max_slots": 4096, "content_cap": 1 << 18},
+    }
+    with open(path, "w") as f:
+        yaml.safe_dump(cfg, f)
+
+
+def loadgen(bin_dir, port, conns, requests, threads, timeout):
+    out = subprocess.run([os.path.join(bin_dir, "qmx_loadgen"), "--port", str(port), "--conns", str(conns),
+                          "--requests", str(requests), "--threads", str(threads), "--timeout", str(timeout),
+                          "--path", "/v1/chat/completions"], capture_output=True, text=True, timeout=timeout + 60)
+    if out.returncode != 0:
+        raise RuntimeError(f"loadgen failed: {out.stderr}")
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=512, help="requests per step per rank")
+    ap.add_argument("--conns", type=int, default=64, help="concurrent client connections per rank")
+    ap.add_argument("--impl", default=os.environ.get("QMX_BENCH_IMPL", "native"), choices=["native", "python"])
+    ap.add_argument("--engine", default=os.environ.get("QMX_BENCH_ENGINE", "auto"))
+    ap.add_argument("--workers", type=int, default=4, help="python impl: proxy processes per rank")
+    ap.add_argument("--threads", type=int, default=4, help="native impl: io threads per rank")
+    ap.add_argument("--lg-threads", type=int, default=2)
+    ap.add_argument("--mock-threads", type=int, default=2)
+    ap.add_argument("--skip-final", type=int, default=1)
+    ap.add_argument("--tile", type=int, default=16384)
+    ap.add_argument("--port", type=int, default=int(os.environ.get("QMX_BENCH_PORT", "18000")))
+    ap.add_argument("--timeout", type=float, default=300)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+
+    use_cuda = torch.cuda.is_available()
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+
+        dist.init_process_group("nccl" if use_cuda else "gloo")
+    if use_cuda:
+        torch.cuda.set_device(local_rank)
+    engine = args.engine
+    if engine == "auto":
+        engine = "hip" if use_cuda else "cpu"
+
+    from quorum_amd.ops import build as qbuild
+
+    qbuild.build()
+    bin_dir = os.path.dirname(str(qbuild.build_tools()[0]))
+    from quorum_amd.serve import spawn_workers, wait_healthy
+
+    procs = []
+    tmp = tempfile.mkdtemp(prefix=f"qmx_bench_r{rank}_")
+    try:
+        mock_ports = [args.port + 100 + rank * 10 + i for i in range(2)]
+        for p in mock_ports:
+            procs.append(subprocess.Popen([os.path.join(bin_dir, "qmx_mock"), "--port", str(p), "--threads",
+                                           str(args.mock_threads), "--tokens", "20", "--think", "1"],
+                                          stderr=subprocess.DEVNULL, start_new_session=True))
+        cfg_path = os.path.join(tmp, "config.yaml")
+        write_config(cfg_path, mock_ports, bool(args.skip_final), args.tile)
+        procs += spawn_workers(cfg_path, "127.0.0.1", args.port, args.workers, engine,
+                               local_rank if use_cuda else None, impl=args.impl, threads=args.threads)
+        if not wait_healthy("127.0.0.1", args.port, 180):
+            raise RuntimeError("proxy did not become healthy")
+        if dist is not None:
+            dist.barrier()
+        # warmup
+        if args.warmup > 0:
+            loadgen(bin_dir, args.port, args.conns, args.warmup * args.batch, args.lg_threads, args.timeout)
+        if dist is not None:
+            dist.barrier()
+        if use_cuda:
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        stats = loadgen(bin_dir, args.port, args.conns, args.steps * args.batch, args.lg_threads, args.timeout)
+        if use_cuda:
+            torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        local = [elapsed, float(stats["completed"]), float(stats["ttft_p50_ms"]), float(stats["ttft_p99_ms"]),
+                 float(stats["errors"] + stats["non200"]), float(stats["ttfb_p50_ms"]), float(stats["lat_p50_ms"])]
+        if dist is not None:
+            t = torch.tensor(local, dtype=torch.float64, device="cuda" if use_cuda else "cpu")
+            gathered = [torch.zeros_like(t) for _ in range(world)]
+            dist.all_gather(gathered, t)
+            rows = [g.cpu().tolist() for g in gathered]
+        else:
+            rows = [local]
+        if rank == 0:
+            max_el = max(r[0] for r in rows)
+            total = sum(r[1] for r in rows)
+            value = total / max_el
+            p50 = statistics.median(r[2] for r in rows)
+            res = {
+                "metric": "proxied req/sec (whole node) + p50 TTFT, 2-backend concatenate stream",
+                "value": round(value, 3),
+                "unit": "req/s",
+                "n_gpus": world,
+                "steps": args.steps,
+                "warmup": args.warmup,
+                "ms_per_step": round(1000.0 * max_el / args.steps, 3),
+                "higher_is_better": True,
+                "scaling": "weak",
+                "vs_baseline": round(value / BASELINE_RPS, 3),
+                "dtype": "bytes (utf-8 SSE text; no float compute)",
+                "data": "synthetic: C++ mock backends (role + 4 split <think> fragments + 20 tokens + stop + "
+                        "[DONE]) and C++ closed-loop load generator",
+                "config": {"model": "2 mock backends, streaming concatenate, hide_intermediate_think, "
+                                    f"skip_final_aggregation={bool(args.skip_final)}",
+                           "global_batch": args.batch * world, "seq_len": 26,
+                           "parallelism": f"dp{world} (sessions sharded over GPUs via SO_REUSEPORT)",
+                           "impl": args.impl, "engine": engine, "conns_per_rank": args.conns},
+                "p50_ttft_ms": round(p50, 3),
+                "p99_ttft_ms": round(max(r[3] for r in rows), 3),
+                "p50_ttfb_ms": round(statistics.median(r[5] for r in rows), 3),
+                "p50_latency_ms": round(statistics.median(r[6] for r in rows), 3),
+                "errors": int(sum(r[4] for r in rows)),
+                "baseline_p50_ttft_ms_16_clients": 1605,
+            }
+            print(json.dumps(res), flush=True)
+    finally:
+        _kill(procs)
+        if dist is not None:
+            dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

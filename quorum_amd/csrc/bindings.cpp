@@ -5,6 +5,8 @@
 
 #include "qmx_engine.h"
 #include "qmx_hip.h"
+#include "qmx_json.h"
+#include "qmx_server.h"
 
 namespace py = pybind11;
 using namespace qmx;
@@ -71,6 +73,44 @@ void bind_engine(py::class_<E>& c) {
 
 }  // namespace
 
+ServerCfg server_cfg_from(const py::dict& d) {
+  ServerCfg c;
+  auto gs = [&](const char* k, std::string& v) { if (d.contains(k)) v = py::cast<std::string>(d[k]); };
+  auto gi = [&](const char* k, int& v) { if (d.contains(k)) v = py::cast<int>(d[k]); };
+  auto gd = [&](const char* k, double& v) { if (d.contains(k)) v = py::cast<double>(d[k]); };
+  auto gb = [&](const char* k, bool& v) { if (d.contains(k)) v = py::cast<bool>(d[k]); };
+  gs("host", c.host); gi("port", c.port); gi("threads", c.threads);
+  gs("engine", c.engine); gi("device", c.device); gi("tile", c.tile); gi("max_slots", c.max_slots);
+  gi("content_cap", c.content_cap);
+  gb("has_iterations_and_strategy", c.has_iterations_and_strategy);
+  gd("timeout", c.timeout); gd("total_timeout", c.total_timeout);
+  gs("separator", c.separator); gb("hide_intermediate", c.hide_intermediate); gb("hide_final", c.hide_final);
+  gb("skip_final", c.skip_final); gb("suppress", c.suppress);
+  if (d.contains("tags")) c.tags = py::cast<std::vector<std::string>>(d["tags"]);
+  gs("aggregator_name", c.aggregator_name); gs("prompt_template", c.prompt_template);
+  gs("intermediate_separator", c.intermediate_separator); gs("query_format", c.query_format);
+  gs("source_label_format", c.source_label_format); gb("include_original_query", c.include_original_query);
+  gb("include_source_names", c.include_source_names); gs("env_api_key", c.env_api_key);
+  gb("install_signals", c.install_signals);
+  if (d.contains("backends")) {
+    for (auto item : py::cast<py::list>(d["backends"])) {
+      py::dict b = py::cast<py::dict>(item);
+      BackendCfg bc;
+      bc.name = py::cast<std::string>(b["name"]);
+      bc.url = py::cast<std::string>(b["url"]);
+      bc.model = py::cast<std::string>(b["model"]);
+      bc.has_model_key = py::cast<bool>(b["has_model_key"]);
+      bc.valid = py::cast<bool>(b["valid"]);
+      bc.host = py::cast<std::string>(b["host"]);
+      bc.port = py::cast<int>(b["port"]);
+      bc.path = py::cast<std::string>(b["path"]);
+      bc.https = py::cast<bool>(b["https"]);
+      c.backends.push_back(bc);
+    }
+  }
+  return c;
+}
+
 PYBIND11_MODULE(_qmx, m) {
   m.doc() = "qmx native core: CPU stream engine, CDNA4 HIP stream engine, text ops";
   m.def("device_count", []() {
@@ -87,6 +127,20 @@ PYBIND11_MODULE(_qmx, m) {
     json_unescape((const uint8_t*)s.data(), r.str_a, r.str_b, (uint8_t*)&out[0]);
     return py::make_tuple(r.kind, py::bytes(out));
   });
+  m.def("run_server", [](const py::dict& d) {
+    ServerCfg c = server_cfg_from(d);
+    py::gil_scoped_release nogil;
+    return run_server(c);
+  });
+  m.def("server_counters", &server_counters);
+  m.def("stop_server", &stop_server);
+  m.def("json_roundtrip", [](const py::bytes& b) -> py::object {
+    std::string s(b), err;
+    JVal v;
+    if (!json_parse(s.data(), s.size(), v, &err)) return py::make_tuple(false, err);
+    return py::make_tuple(true, py::bytes(json_dumps(v)));
+  });
+  m.def("py_float_repr", &py_float_repr);
   m.def("escape", [](const py::bytes& b) {
     std::string s(b), out;
     escape_append((const uint8_t*)s.data(), s.size(), out);

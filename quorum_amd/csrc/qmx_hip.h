@@ -38,6 +38,7 @@ struct KParams {
   char pre1[48];
   char pre2[176];
   char suf[48];
+  unsigned long long* dbg;  // optional per-stage stamps [item][16] (QMX_STAGE_TIMING=1)
 };
 
 struct FinItem {
@@ -102,6 +103,10 @@ class HipEngine : public HostEngine {
   // stats
   uint64_t launches_ = 0, items_ = 0, escalations_ = 0, fin_launches_ = 0;
   double kernel_ms_ = 0.0;
+  unsigned long long* h_dbg_ = nullptr;
+  size_t dbg_cap_ = 0;
+  double stage_us_[16] = {0};
+  uint64_t stage_n_ = 0;
   hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
 };
 

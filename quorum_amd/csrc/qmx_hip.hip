@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -44,6 +45,13 @@ constexpr int MAX_CAND = 1024;
 constexpr int PAD = 16;
 
 typedef int v4i __attribute__((ext_vector_type(4)));
+
+// optional per-stage wall-clock stamps (s_memrealtime, 100 MHz) written by thread 0
+#define QMX_STAMP(k)                                               \
+  do {                                                             \
+    if (Pk.dbg != nullptr && threadIdx.x == 0)                     \
+      Pk.dbg[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 
 struct Smem {
   alignas(16) uint8_t A[TILE_MAX + 64];  // X (input) → W (kept bytes) / output window
@@ -69,6 +77,23 @@ struct Smem {
 enum : int {
   V_START = 0, V_NSEP, V_LASTSEP, V_ABORT, V_NEV, V_CONSUMED, V_STATUS, V_NDELTA, V_YLEN, V_NCAND,
   V_NTOK, V_BAIL, V_DEPTH0, V_TAILLEN, V_NEWTAIL, V_NEWDEPTH, V_WLEN, V_NEMIT, V_ETOT, V_OUTLEN
+};
+
+// LDS byte reader that fetches one aligned 64-bit word per 8 sequential bytes: a byte-serial
+// scanner otherwise pays a dependent ds_read_u8 latency per character.
+struct LdsWords {
+  const uint64_t* base;  // 8-byte aligned LDS array
+  mutable int wb;
+  mutable uint64_t w;
+  __device__ explicit LdsWords(const uint8_t* b) : base((const uint64_t*)b), wb(-1), w(0) {}
+  QMX_HD uint8_t operator[](int i) const {
+    int b = i >> 3;
+    if (b != wb) {
+      wb = b;
+      w = base[b];
+    }
+    return (uint8_t)(w >> ((i & 7) << 3));
+  }
 };
 
 // ------------------------------------------------------------------------------------
@@ -264,9 +289,12 @@ __device__ inline int hold_cut(const Smem& s, const uint8_t* Z, int ncand, int n
 __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict__ items,
                                                       const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                       WorkResult* __restrict__ res, DevSlot* __restrict__ state,
-                                                      uint8_t* __restrict__ content, KParams P) {
+                                                      uint8_t* __restrict__ content, KParams Pk) {
   __shared__ Smem s;
+  __shared__ KParams P;  // kernel args staged in LDS: lane-divergent pattern/envelope reads
   const int tid = threadIdx.x;
+  for (int i = tid; i < (int)(sizeof(KParams) / 4); i += BS) ((uint32_t*)&P)[i] = ((const uint32_t*)&Pk)[i];
+  QMX_STAMP(0);
   const WorkItem it = items[blockIdx.x];
   const int in_len = (int)it.in_len;
   const bool eof = it.flags & WF_EOF;
@@ -291,6 +319,7 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
     }
   }
   __syncthreads();
+  QMX_STAMP(1);
   const int tail_len = filt ? s.v[V_TAILLEN] : 0;
   uint8_t* Z = s.B + PAD;
   if (tid < tail_len) Z[tid] = state[it.slot].tail[tid];
@@ -330,6 +359,7 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
     return;
   }
   const int start = s.v[V_START];
+  QMX_STAMP(2);
 
   // ---- S2: framing -----------------------------------------------------------------
   {
@@ -412,31 +442,30 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
     if (more) s.v[V_STATUS] |= WS_MORE;
   }
   __syncthreads();
+  QMX_STAMP(3);
   const int nev = s.v[V_NEV];
 
   // ---- S3: per-event extraction (4 consecutive events per thread) --------------------
   int packed_local[4];
   {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int k = tid * 4 + i;
-      packed_local[i] = 0;
-      if (k < nev) {
-        int a = s.ev_a[k], b = s.ev_b[k];
-        EvResult r = classify_event(s.A + a, b - a);
-        s.ev_kind[k] = (uint8_t)r.kind;
-        if (r.kind == EV_CONTENT) {
-          int sa = a + r.str_a, sb = a + r.str_b;
-          s.ev_sa[k] = (uint16_t)sa;
-          s.ev_sb[k] = (uint16_t)sb;
-          s.ev_dl[k] = (uint16_t)json_unescape(s.A, sa, sb, nullptr);
-        } else if (r.kind == EV_ABORT) {
-          atomicMin(&s.v[V_ABORT], k);
-        }
+    // event k -> wave (k & 3), lane (k >> 2): consecutive events run on different SIMDs
+    const LdsWords rd(s.A);
+    for (int k = ((tid & 63) << 2) | (tid >> 6); k < nev; k += BS) {
+      int a = s.ev_a[k], b = s.ev_b[k];
+      EvResult r = classify_event_at(rd, a, b - a);
+      s.ev_kind[k] = (uint8_t)r.kind;
+      if (r.kind == EV_CONTENT) {
+        int sa = a + r.str_a, sb = a + r.str_b;
+        s.ev_sa[k] = (uint16_t)sa;
+        s.ev_sb[k] = (uint16_t)sb;
+        s.ev_dl[k] = (uint16_t)json_unescape(rd, sa, sb, nullptr);
+      } else if (r.kind == EV_ABORT) {
+        atomicMin(&s.v[V_ABORT], k);
       }
     }
   }
   __syncthreads();
+  QMX_STAMP(4);
   const int kab = s.v[V_ABORT];
   {
     int loc = 0;
@@ -458,7 +487,7 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
         int j = pre >> 16, doff = pre & 0xFFFF;
         int dl = s.ev_dl[k];
         s.dl_end[j] = (uint16_t)(tail_len + doff + dl);
-        json_unescape(s.A, s.ev_sa[k], s.ev_sb[k], Z + tail_len + doff);
+        json_unescape(LdsWords(s.A), s.ev_sa[k], s.ev_sb[k], Z + tail_len + doff);
       }
     }
     if (tid == 0) {
@@ -474,6 +503,7 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
   const int ndelta = s.v[V_NDELTA];
   const int Zn = tail_len + s.v[V_YLEN];
   const int depth0 = s.v[V_DEPTH0];
+  QMX_STAMP(5);
 
   // ---- S4: think filter ----------------------------------------------------------------
   const uint8_t* W = Z;  // identity when not filtering
@@ -507,6 +537,7 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
       for (int g = w; g * 16 < ncand; g += BS / 64) mfma_match_group(Z, Zn, s.cand, ncand, g, P, bfrag, s.cand_tok);
     }
     __syncthreads();
+    QMX_STAMP(6);
     // token compaction (4 candidates per thread)
     {
       int loc = 0, flags[4];
@@ -623,6 +654,7 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
     }
   }
   __syncthreads();
+  QMX_STAMP(7);
   const int Wlen = s.v[V_WLEN];
 
   // ---- S6 (sizing): emitted deltas, escaped lengths -------------------------------------
@@ -682,6 +714,7 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
     }
     __syncthreads();
   }
+  QMX_STAMP(8);
   const int out_len = emit ? n_emit * EVL + etot : 0;
   const uint32_t new_clen = it.content_len + (uint32_t)Wlen;
   if ((uint32_t)out_len > it.out_cap || new_clen > P.content_cap) {
@@ -710,6 +743,7 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
     state[it.slot].depth = 0;
   }
   __syncthreads();
+  QMX_STAMP(9);
 
   // ---- S6 (write): SSE events through an LDS window, 16-B stores to host memory ------
   if (out_len > 0) {
@@ -775,6 +809,7 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
       __syncthreads();
     }
   }
+  QMX_STAMP(10);
   if (tid == 0) {
     WorkResult r{(uint32_t)s.v[V_CONSUMED], (uint32_t)out_len, (uint32_t)s.v[V_STATUS], new_clen};
     res[blockIdx.x] = r;
@@ -833,6 +868,7 @@ HipEngine::~HipEngine() {
   if (h_out_) hipHostFree(h_out_);
   if (h_items_) hipHostFree(h_items_);
   if (h_res_) hipHostFree(h_res_);
+  if (h_dbg_) hipHostFree(h_dbg_);
   if (d_state_) hipFree(d_state_);
   if (d_content_) hipFree(d_content_);
   if (d_scratch_) hipFree(d_scratch_);
@@ -966,6 +1002,16 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
   }
   if (n > 0) {
     build_params(created);
+    params_.dbg = nullptr;
+    if (getenv("QMX_STAGE_TIMING")) {
+      if (dbg_cap_ < (size_t)n) {
+        if (h_dbg_) hipHostFree(h_dbg_);
+        dbg_cap_ = std::max((size_t)n, items_cap_);
+        HIP_CHECK(hipHostMalloc((void**)&h_dbg_, sizeof(unsigned long long) * 16 * dbg_cap_, hipHostMallocMapped));
+      }
+      std::memset(h_dbg_, 0, sizeof(unsigned long long) * 16 * n);
+      params_.dbg = h_dbg_;
+    }
     HIP_CHECK(hipEventRecord(ev0_, stream_));
     hipLaunchKernelGGL(qmx_tick_kernel, dim3(n), dim3(BS), 0, stream_, h_items_, h_in_, h_out_, h_res_, d_state_,
                        d_content_, params_);
@@ -977,6 +1023,18 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
     kernel_ms_ += ms;
     ++launches_;
     items_ += n;
+    if (params_.dbg) {
+      for (int i = 0; i < n; ++i) {
+        const unsigned long long* d = h_dbg_ + 16 * i;
+        int prev = 0;
+        for (int k = 1; k < 11; ++k) {
+          if (!d[k]) continue;
+          stage_us_[k] += (double)(d[k] - d[prev]) * 0.01;  // 100 MHz ticks -> us
+          prev = k;
+        }
+      }
+      stage_n_ += n;
+    }
   }
   for (int i = 0; i < n; ++i) {
     Pending& p = pend[i];
@@ -1052,8 +1110,11 @@ void HipEngine::finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes
 }
 
 std::unordered_map<std::string, double> HipEngine::kernel_stats() {
-  return {{"launches", (double)launches_}, {"items", (double)items_}, {"kernel_ms", kernel_ms_},
-          {"escalations", (double)escalations_}, {"fin_launches", (double)fin_launches_}};
+  std::unordered_map<std::string, double> m{{"launches", (double)launches_}, {"items", (double)items_},
+                                             {"kernel_ms", kernel_ms_}, {"escalations", (double)escalations_},
+                                             {"fin_launches", (double)fin_launches_}, {"stage_items", (double)stage_n_}};
+  for (int k = 1; k < 11; ++k) m["stage" + std::to_string(k) + "_us"] = stage_us_[k];
+  return m;
 }
 
 }  // namespace qmx

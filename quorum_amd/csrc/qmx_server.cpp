@@ -1,0 +1,1531 @@
+// qmx_server.cpp — native epoll data plane (see qmx_server.h).
+#include "qmx_server.h"
+
+#include <arpa/inet.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <netdb.h>
+#include <netinet/tcp.h>
+#include <signal.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <thread>
+
+#include "qmx_engine.h"
+#include "qmx_hip.h"
+#include "qmx_json.h"
+
+namespace qmx {
+namespace {
+
+std::atomic<bool> g_stop{false};
+std::atomic<uint64_t> c_requests{0}, c_stream{0}, c_nonstream{0}, c_errors{0}, c_up_fail{0}, c_ticks{0},
+    c_tick_slots{0}, c_up_conns{0}, c_clients{0};
+
+using Clock = std::chrono::steady_clock;
+inline double now_s() { return std::chrono::duration<double>(Clock::now().time_since_epoch()).count(); }
+
+std::string lower(std::string s) {
+  for (auto& c : s) c = (char)tolower((unsigned char)c);
+  return s;
+}
+std::string trim(const std::string& s) {
+  size_t a = 0, b = s.size();
+  while (a < b && (s[a] == ' ' || s[a] == '\t')) ++a;
+  while (b > a && (s[b - 1] == ' ' || s[b - 1] == '\t' || s[b - 1] == '\r')) --b;
+  return s.substr(a, b - a);
+}
+const char* reason(int st) {
+  switch (st) {
+    case 200: return "OK";
+    case 400: return "Bad Request";
+    case 401: return "Unauthorized";
+    case 404: return "Not Found";
+    case 500: return "Internal Server Error";
+    case 502: return "Bad Gateway";
+    case 503: return "Service Unavailable";
+    default: return "Status";
+  }
+}
+std::string chunk(const std::string& s) {
+  char h[24];
+  snprintf(h, sizeof(h), "%zx\r\n", s.size());
+  return std::string(h) + s + "\r\n";
+}
+std::string err_json(const std::string& msg, const char* type) {
+  JVal e;
+  e.t = JVal::OBJ;
+  e.set("message", JVal::str(msg));
+  e.set("type", JVal::str(type));
+  JVal o;
+  o.t = JVal::OBJ;
+  o.set("error", e);
+  return json_dumps(o);
+}
+std::string http_response(int status, const std::string& ctype, const std::string& body,
+                          const std::vector<std::pair<std::string, std::string>>* extra = nullptr) {
+  std::string r = "HTTP/1.1 " + std::to_string(status) + " " + reason(status) + "\r\n";
+  r += "content-length: " + std::to_string(body.size()) + "\r\ncontent-type: " + ctype + "\r\n";
+  if (extra)
+    for (auto& h : *extra) r += h.first + ": " + h.second + "\r\n";
+  r += "\r\n";
+  r += body;
+  return r;
+}
+const char* kSseHdr =
+    "HTTP/1.1 200 OK\r\ncontent-type: text/event-stream; charset=utf-8\r\ntransfer-encoding: chunked\r\n\r\n";
+const char* kDone = "data: [DONE]\n\n";
+
+std::string chunk_event_json(const char* id, int64_t created, const std::string& model_json,
+                             const std::string& delta_json, const char* finish) {
+  return std::string("data: {\"id\": \"") + id + "\", \"object\": \"chat.completion.chunk\", \"created\": " +
+         std::to_string(created) + ", \"model\": " + model_json + ", \"choices\": [{\"index\": 0, \"delta\": " +
+         delta_json + ", \"finish_reason\": " + finish + "}]}\n\n";
+}
+
+// --------------------------------------------------------------------------------------
+// incremental HTTP/1.1 response parser (upstream side)
+// --------------------------------------------------------------------------------------
+struct RespParser {
+  int phase = 0;  // 0 headers, 1 length body, 2 chunk size, 3 chunk data, 4 chunk crlf, 5 trailers, 6 until close, 7 done
+  int status = 0;
+  std::vector<std::pair<std::string, std::string>> headers;
+  long remaining = 0;
+  bool close = false;
+  std::string buf;
+  // returns -1 on protocol error; appends body bytes to out
+  int feed(const char* p, size_t n, std::string& out) {
+    buf.append(p, n);
+    size_t i = 0;
+    while (phase != 7) {
+      if (phase == 0) {
+        size_t he = buf.find("\r\n\r\n", i);
+        if (he == std::string::npos) break;
+        std::string head = buf.substr(i, he - i);
+        i = he + 4;
+        size_t le = head.find("\r\n");
+        std::string sl = head.substr(0, le);
+        if (sl.size() < 12 || sl.compare(0, 5, "HTTP/") != 0) return -1;
+        status = atoi(sl.c_str() + 9);
+        bool chunked = false, has_len = false;
+        size_t pos = le == std::string::npos ? head.size() : le + 2;
+        while (pos < head.size()) {
+          size_t e = head.find("\r\n", pos);
+          if (e == std::string::npos) e = head.size();
+          std::string line = head.substr(pos, e - pos);
+          size_t c = line.find(':');
+          if (c != std::string::npos) {
+            std::string k = lower(trim(line.substr(0, c))), v = trim(line.substr(c + 1));
+            if (k == "transfer-encoding" && lower(v).find("chunked") != std::string::npos) chunked = true;
+            if (k == "content-length") {
+              has_len = true;
+              remaining = atol(v.c_str());
+            }
+            if (k == "connection" && lower(v) == "close") close = true;
+            headers.emplace_back(k, v);
+          }
+          pos = e + 2;
+        }
+        if (status == 204 || status == 304) phase = 7;
+        else if (chunked) phase = 2;
+        else if (has_len) phase = remaining > 0 ? 1 : 7;
+        else {
+          phase = 6;
+          close = true;
+        }
+        continue;
+      }
+      if (phase == 1) {
+        size_t take = std::min((size_t)remaining, buf.size() - i);
+        out.append(buf, i, take);
+        i += take;
+        remaining -= take;
+        if (remaining == 0) phase = 7;
+        break;
+      }
+      if (phase == 6) {
+        out.append(buf, i, std::string::npos);
+        i = buf.size();
+        break;
+      }
+      if (phase == 2) {
+        size_t le = buf.find("\r\n", i);
+        if (le == std::string::npos) break;
+        remaining = strtol(buf.c_str() + i, nullptr, 16);
+        i = le + 2;
+        phase = remaining == 0 ? 5 : 3;
+        continue;
+      }
+      if (phase == 3) {
+        size_t take = std::min((size_t)remaining, buf.size() - i);
+        out.append(buf, i, take);
+        i += take;
+        remaining -= take;
+        if (remaining > 0) break;
+        phase = 4;
+        continue;
+      }
+      if (phase == 4) {
+        if (buf.size() - i < 2) break;
+        i += 2;
+        phase = 2;
+        continue;
+      }
+      if (phase == 5) {
+        size_t le = buf.find("\r\n", i);
+        if (le == std::string::npos) break;
+        bool empty = le == i;
+        i = le + 2;
+        if (empty) phase = 7;
+        continue;
+      }
+    }
+    buf.erase(0, i);
+    return 0;
+  }
+  bool done() const { return phase == 7; }
+  const std::string* header(const std::string& k) const {
+    for (auto& h : headers)
+      if (h.first == k) return &h.second;
+    return nullptr;
+  }
+};
+
+// --------------------------------------------------------------------------------------
+// connection / session state
+// --------------------------------------------------------------------------------------
+struct Session;
+struct Client {
+  int fd = -1;
+  std::string in, out;
+  size_t out_off = 0;
+  Session* sess = nullptr;
+  bool keepalive = true;
+  bool dead = false;         // error: close now
+  bool close_after = false;  // graceful: close once output is flushed
+};
+
+enum UpMode { UP_ENGINE, UP_BUFFER, UP_PASS };
+struct Up {
+  int fd = -1;
+  int backend = -1;  // index into cfg.backends
+  Session* sess = nullptr;
+  int bi = -1;  // index into sess->bs, -1 = aggregator call
+  UpMode mode = UP_BUFFER;
+  std::string req;
+  size_t req_off = 0;
+  bool connecting = false, reused = false, got_bytes = false, headers_seen = false;
+  RespParser rp;
+  std::string body;  // buffered body (UP_BUFFER / non-200)
+  double last_io = 0, deadline = 0, timeout = 60;
+};
+
+struct BState {
+  int backend = -1;
+  int slot = -1;
+  Up* up = nullptr;
+  int state = 0;  // 0 running, 1 done, 2 failed
+  int status = 0;
+  bool aborted = false;
+  // buffered (non-stream) result, call_backend contract
+  bool is_json = false;
+  JVal js;
+  std::string text;
+  std::vector<std::pair<std::string, std::string>> rheaders;
+};
+
+enum SKind { K_PAR, K_SINGLE, K_NONSTREAM };
+struct Session {
+  Client* cl = nullptr;
+  SKind kind = K_PAR;
+  JVal body;
+  std::string raw;
+  std::vector<std::pair<std::string, std::string>> fwd;  // forwarded headers
+  std::string auth;                                      // normalized Authorization value
+  std::vector<BState> bs;
+  int finished = 0;
+  bool filter = true, emit = true;
+  int stage = 0;  // 0 streaming, 1 finalize pending, 2 aggregator pending, 3 done
+  int fin_id = -1;
+  bool fin_texts = false;
+  std::vector<std::string> texts;
+  Up* agg = nullptr;
+  // single-stream passthrough
+  std::string first_buf;
+  bool first_decided = false, saw_done = false, pass_started = false;
+  std::string done_tail;
+  std::string role_model_json;
+  double t0 = 0;
+};
+
+struct ResultBatch {
+  std::vector<SlotResult> r;
+  std::vector<FinalizeRes> f;
+};
+
+// --------------------------------------------------------------------------------------
+// io loop (one per thread)
+// --------------------------------------------------------------------------------------
+class Loop {
+ public:
+  Loop(const ServerCfg& cfg, int idx) : cfg_(cfg), idx_(idx) {}
+  ~Loop() {
+    stop_gpu_ = true;
+    cv_.notify_all();
+    if (gpu_thread_.joinable()) gpu_thread_.join();
+  }
+
+  void run() {
+    setup();
+    std::vector<epoll_event> evs(512);
+    double last_sweep = now_s();
+    while (!g_stop.load()) {
+      int n = epoll_wait(ep_, evs.data(), (int)evs.size(), 50);
+      for (int i = 0; i < n; ++i) dispatch(evs[i]);
+      if (!offload_ && eng_->has_work()) tick_inline();
+      if (offload_ && kick_) {
+        kick_ = false;
+        std::lock_guard<std::mutex> g(mu_);
+        work_ = true;
+        cv_.notify_one();
+      }
+      if (!pending_requests_.empty()) {
+        std::vector<int> fds;
+        fds.swap(pending_requests_);
+        for (int fd : fds) {
+          auto it = clients_.find(fd);
+          if (it != clients_.end() && !it->second->sess && !it->second->dead) process_requests(it->second.get());
+        }
+      }
+      if (!pending_close_.empty()) reap_clients();
+      double t = now_s();
+      if (t - last_sweep > 0.1) {
+        sweep_timeouts(t);
+        last_sweep = t;
+      }
+    }
+  }
+
+ private:
+  // ---------------------------------------------------------------- setup
+  void setup() {
+    ep_ = epoll_create1(0);
+    lfd_ = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK, 0);
+    int one = 1;
+    setsockopt(lfd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    setsockopt(lfd_, SOL_SOCKET, SO_REUSEPORT, &one, sizeof(one));
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons(cfg_.port);
+    inet_pton(AF_INET, cfg_.host.c_str(), &a.sin_addr);
+    if (bind(lfd_, (sockaddr*)&a, sizeof(a)) != 0) throw std::runtime_error("bind failed: " + std::string(strerror(errno)));
+    listen(lfd_, 4096);
+    add(lfd_, EPOLLIN, tag_listen());
+    evfd_ = eventfd(0, EFD_NONBLOCK);
+    add(evfd_, EPOLLIN, tag_event());
+    idle_.resize(cfg_.backends.size());
+    if (cfg_.engine == "hip") {
+      eng_.reset(new HipEngine(cfg_.tags, cfg_.device, cfg_.tile, cfg_.max_slots, cfg_.content_cap));
+      offload_ = true;
+      gpu_thread_ = std::thread([this] { gpu_loop(); });
+    } else {
+      eng_.reset(new CpuEngine(cfg_.tags));
+      offload_ = false;
+    }
+  }
+
+  // epoll tags: fd in low 32 bits, kind in high bits
+  static uint64_t tag(int kind, int fd) { return ((uint64_t)kind << 32) | (uint32_t)fd; }
+  static uint64_t tag_listen() { return tag(1, 0); }
+  static uint64_t tag_event() { return tag(2, 0); }
+  void add(int fd, uint32_t ev, uint64_t t) {
+    epoll_event e{};
+    e.events = ev;
+    e.data.u64 = t;
+    epoll_ctl(ep_, EPOLL_CTL_ADD, fd, &e);
+  }
+  void mod(int fd, uint32_t ev, uint64_t t) {
+    epoll_event e{};
+    e.events = ev;
+    e.data.u64 = t;
+    epoll_ctl(ep_, EPOLL_CTL_MOD, fd, &e);
+  }
+
+  void dispatch(const epoll_event& e) {
+    int kind = (int)(e.data.u64 >> 32);
+    int fd = (int)(uint32_t)e.data.u64;
+    if (kind == 1) return on_accept();
+    if (kind == 2) return on_results();
+    if (kind == 3) {
+      auto it = clients_.find(fd);
+      if (it != clients_.end()) on_client(it->second.get(), e.events);
+      return;
+    }
+    if (kind == 4) {
+      auto it = ups_.find(fd);
+      if (it != ups_.end()) on_up(it->second.get(), e.events);
+      return;
+    }
+  }
+
+  // ---------------------------------------------------------------- engine plumbing
+  void gpu_loop() {
+    while (!stop_gpu_) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait_for(lk, std::chrono::milliseconds(2), [this] { return work_ || stop_gpu_; });
+        work_ = false;
+      }
+      if (stop_gpu_) break;
+      while (eng_->has_work()) {
+        ResultBatch rb;
+        eng_->tick((int64_t)time(nullptr), rb.r, rb.f);
+        c_ticks++;
+        c_tick_slots += rb.r.size();
+        if (rb.r.empty() && rb.f.empty()) continue;
+        {
+          std::lock_guard<std::mutex> g(rmu_);
+          rq_.push_back(std::move(rb));
+        }
+        uint64_t one = 1;
+        ssize_t w = write(evfd_, &one, 8);
+        (void)w;
+      }
+    }
+  }
+  void tick_inline() {
+    ResultBatch rb;
+    eng_->tick((int64_t)time(nullptr), rb.r, rb.f);
+    c_ticks++;
+    c_tick_slots += rb.r.size();
+    apply(rb);
+  }
+  void on_results() {
+    uint64_t v;
+    ssize_t r = read(evfd_, &v, 8);
+    (void)r;
+    std::vector<ResultBatch> q;
+    {
+      std::lock_guard<std::mutex> g(rmu_);
+      q.swap(rq_);
+    }
+    for (auto& rb : q) apply(rb);
+  }
+  void apply(ResultBatch& rb) {
+    for (auto& r : rb.r) {
+      auto it = slot_owner_.find(r.slot);
+      if (it == slot_owner_.end()) continue;
+      Session* s = it->second.first;
+      int bi = it->second.second;
+      if (!r.sse.empty() && s->cl) send_chunk(s, r.sse);
+      if ((r.flags & (RF_DONE | RF_ABORTED)) && s->bs[bi].state == 0) {
+        s->bs[bi].state = 1;
+        s->bs[bi].aborted = (r.flags & RF_ABORTED) != 0;
+        s->finished++;
+      }
+      if (s->stage == 0 && s->finished == (int)s->bs.size()) begin_final(s);
+    }
+    for (auto& f : rb.f) {
+      auto it = fin_owner_.find(f.id);
+      if (it == fin_owner_.end()) continue;
+      Session* s = it->second;
+      fin_owner_.erase(it);
+      on_finalized(s, f);
+    }
+  }
+  void kick() { kick_ = true; }
+
+  // ---------------------------------------------------------------- clients
+  void on_accept() {
+    while (true) {
+      int fd = accept4(lfd_, nullptr, nullptr, SOCK_NONBLOCK);
+      if (fd < 0) break;
+      int one = 1;
+      setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+      auto c = std::make_unique<Client>();
+      c->fd = fd;
+      add(fd, EPOLLIN, tag(3, fd));
+      clients_[fd] = std::move(c);
+      c_clients++;
+    }
+  }
+  void reap_clients() {
+    std::vector<int> fds;
+    fds.swap(pending_close_);
+    for (int fd : fds) {
+      auto it = clients_.find(fd);
+      if (it == clients_.end()) continue;
+      Client* c = it->second.get();
+      if (c->dead || (c->close_after && c->out_off >= c->out.size())) close_client(c);
+    }
+  }
+  void mark_close(Client* c) {
+    c->close_after = true;
+    pending_close_.push_back(c->fd);
+  }
+  void on_client(Client* c, uint32_t ev) {
+    if (ev & EPOLLOUT) flush_client(c);
+    if (c->dead) return close_client(c);
+    if (ev & (EPOLLIN | EPOLLHUP | EPOLLERR)) {
+      char buf[65536];
+      while (true) {
+        ssize_t r = recv(c->fd, buf, sizeof(buf), 0);
+        if (r > 0) {
+          c->in.append(buf, r);
+          continue;
+        }
+        if (r == 0 || (errno != EAGAIN && errno != EWOULDBLOCK)) c->dead = true;
+        break;
+      }
+      if (!c->dead && !c->sess) process_requests(c);
+      if (c->dead) return close_client(c);
+    }
+  }
+  void close_client(Client* c) {
+    if (c->sess) {
+      c->sess->cl = nullptr;
+      abort_session(c->sess);
+    }
+    epoll_ctl(ep_, EPOLL_CTL_DEL, c->fd, nullptr);
+    close(c->fd);
+    clients_.erase(c->fd);
+  }
+  void write_client(Client* c, const std::string& data) {
+    if (c->dead) return;
+    if (c->out.size() == c->out_off) {
+      c->out.clear();
+      c->out_off = 0;
+      ssize_t w = send(c->fd, data.data(), data.size(), MSG_NOSIGNAL);
+      if (w == (ssize_t)data.size()) return;
+      if (w < 0) {
+        if (errno != EAGAIN && errno != EWOULDBLOCK) {
+          c->dead = true;
+          return;
+        }
+        w = 0;
+      }
+      c->out.assign(data, w, std::string::npos);
+      mod(c->fd, EPOLLIN | EPOLLOUT, tag(3, c->fd));
+      return;
+    }
+    c->out += data;
+  }
+  void flush_client(Client* c) {
+    while (c->out_off < c->out.size()) {
+      ssize_t w = send(c->fd, c->out.data() + c->out_off, c->out.size() - c->out_off, MSG_NOSIGNAL);
+      if (w > 0) {
+        c->out_off += w;
+        continue;
+      }
+      if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) return;
+      c->dead = true;
+      return;
+    }
+    c->out.clear();
+    c->out_off = 0;
+    mod(c->fd, EPOLLIN, tag(3, c->fd));
+    if (c->close_after) pending_close_.push_back(c->fd);
+  }
+
+  // parse as many complete requests as possible (one in flight at a time)
+  void process_requests(Client* c) {
+    while (!c->sess && !c->dead) {
+      size_t he = c->in.find("\r\n\r\n");
+      if (he == std::string::npos) {
+        if (c->in.size() > (1 << 20)) c->dead = true;
+        return;
+      }
+      std::string head = c->in.substr(0, he);
+      size_t le = head.find("\r\n");
+      std::string rl = head.substr(0, le);
+      size_t sp1 = rl.find(' '), sp2 = rl.rfind(' ');
+      if (sp1 == std::string::npos || sp2 == sp1) {
+        c->dead = true;
+        return;
+      }
+      std::string method = rl.substr(0, sp1), target = rl.substr(sp1 + 1, sp2 - sp1 - 1),
+                  version = rl.substr(sp2 + 1);
+      std::vector<std::pair<std::string, std::string>> hdrs;
+      size_t pos = le == std::string::npos ? head.size() : le + 2;
+      long clen = 0;
+      bool chunked = false;
+      bool keepalive = version != "HTTP/1.0";
+      while (pos < head.size()) {
+        size_t e = head.find("\r\n", pos);
+        if (e == std::string::npos) e = head.size();
+        std::string line = head.substr(pos, e - pos);
+        size_t colon = line.find(':');
+        if (colon != std::string::npos) {
+          std::string k = lower(trim(line.substr(0, colon))), v = trim(line.substr(colon + 1));
+          if (k == "content-length") clen = atol(v.c_str());
+          if (k == "transfer-encoding" && lower(v).find("chunked") != std::string::npos) chunked = true;
+          if (k == "connection") {
+            std::string lv = lower(v);
+            if (lv == "close") keepalive = false;
+            if (lv == "keep-alive") keepalive = true;
+          }
+          hdrs.emplace_back(k, v);
+        }
+        pos = e + 2;
+      }
+      std::string body;
+      size_t used;
+      if (chunked) {
+        // decode a chunked request body
+        size_t i = he + 4;
+        bool complete = false;
+        while (true) {
+          size_t l2 = c->in.find("\r\n", i);
+          if (l2 == std::string::npos) break;
+          long sz = strtol(c->in.c_str() + i, nullptr, 16);
+          if (sz == 0) {
+            size_t t = c->in.find("\r\n\r\n", l2);
+            if (t == std::string::npos) {
+              if (c->in.size() >= l2 + 4 && c->in.compare(l2, 4, "\r\n\r\n") == 0) t = l2;
+              else break;
+            }
+            i = t + 4;
+            complete = true;
+            break;
+          }
+          if (c->in.size() < l2 + 2 + sz + 2) break;
+          body.append(c->in, l2 + 2, sz);
+          i = l2 + 2 + sz + 2;
+        }
+        if (!complete) return;
+        used = i;
+      } else {
+        if (c->in.size() < he + 4 + (size_t)clen) return;
+        body = c->in.substr(he + 4, clen);
+        used = he + 4 + clen;
+      }
+      c->in.erase(0, used);
+      c->keepalive = keepalive;
+      handle_request(c, method, target, hdrs, body);
+      if (!c->sess && !c->keepalive) {
+        mark_close(c);
+        return;
+      }
+    }
+  }
+
+  void respond(Client* c, int status, const std::string& ctype, const std::string& body,
+               const std::vector<std::pair<std::string, std::string>>* extra = nullptr) {
+    write_client(c, http_response(status, ctype, body, extra));
+  }
+
+  void handle_request(Client* c, const std::string& method, std::string target,
+                      std::vector<std::pair<std::string, std::string>>& hdrs, std::string& body) {
+    size_t q = target.find('?');
+    if (q != std::string::npos) target.resize(q);
+    if (method == "GET" && target == "/health") return respond(c, 200, "application/json", "{\"status\":\"healthy\"}");
+    if (method == "GET" && target == "/metrics") return respond(c, 200, "text/plain; version=0.0.4", metrics_text());
+    if (target != "/chat/completions" && target != "/v1/chat/completions")
+      return respond(c, 404, "application/json", "{\"detail\":\"Not Found\"}");
+    if (method != "POST") return respond(c, 405, "application/json", "{\"detail\":\"Method Not Allowed\"}");
+    c_requests++;
+    auto s = std::make_unique<Session>();
+    s->t0 = now_s();
+    std::string perr;
+    if (!json_parse(body.data(), body.size(), s->body, &perr)) {
+      c_errors++;
+      return respond(c, 500, "application/json", err_json("Error processing request: " + perr, "proxy_error"));
+    }
+    if (s->body.t != JVal::OBJ) {
+      c_errors++;
+      const char* tn = s->body.t == JVal::ARR ? "list" : s->body.t == JVal::STR ? "str" : "int";
+      return respond(c, 500, "application/json",
+                     err_json(std::string("Error processing request: '") + tn + "' object has no attribute 'get'",
+                              "proxy_error"));
+    }
+    const JVal* sv = s->body.get("stream");
+    bool streaming = sv && sv->truthy();
+    // forward all headers but host; auth fallback/normalisation; content-type default (quorum :972-1008)
+    bool has_auth = false, has_ctype = false;
+    for (auto& h : hdrs) {
+      if (h.first == "host") continue;
+      if (h.first == "authorization") {
+        has_auth = true;
+        s->auth = h.second;
+        continue;
+      }
+      if (h.first == "content-type") has_ctype = true;
+      // hop-by-hop / entity headers are re-framed; accept-encoding dropped so upstream sends identity
+      if (h.first == "content-length" || h.first == "transfer-encoding" || h.first == "connection" ||
+          h.first == "keep-alive" || h.first == "te" || h.first == "upgrade" || h.first == "accept-encoding")
+        continue;
+      s->fwd.push_back(h);
+    }
+    if (!has_auth) {
+      if (cfg_.env_api_key.empty()) {
+        c_errors++;
+        return respond(c, 401, "application/json",
+                       err_json("Authorization header is required and OPENAI_API_KEY environment variable is not set",
+                                "auth_error"));
+      }
+      s->auth = "Bearer " + cfg_.env_api_key;
+    }
+    s->fwd.emplace_back("Authorization", s->auth);
+    if (!has_ctype) s->fwd.emplace_back("Content-Type", "application/json");
+    std::vector<int> valid;
+    for (int i = 0; i < (int)cfg_.backends.size(); ++i)
+      if (cfg_.backends[i].valid) valid.push_back(i);
+    if (valid.empty())
+      return respond(c, 500, "application/json", err_json("No valid backends configured", "configuration_error"));
+    if (!s->body.get("model")) {
+      bool any = false;
+      for (int i : valid) any = any || !cfg_.backends[i].model.empty();
+      if (!any)
+        return respond(c, 400, "application/json",
+                       err_json("Model must be specified when config.yaml model is blank", "invalid_request_error"));
+    }
+    bool parallel = cfg_.has_iterations_and_strategy && valid.size() > 1;
+    s->raw = std::move(body);
+    s->cl = c;
+    Session* sp = s.get();
+    sessions_[sp] = std::move(s);
+    c->sess = sp;
+    if (streaming && parallel) start_parallel(sp, valid);
+    else if (streaming) start_single(sp, valid[0]);
+    else start_nonstream(sp, valid, parallel);
+  }
+
+  // ---------------------------------------------------------------- upstream requests
+  // call_backend body logic (quorum :157-180). Returns false with a synthetic result.
+  bool upstream_body(Session* s, int b, std::string& out, int* st, std::string* msg, const char** etype) {
+    const BackendCfg& be = cfg_.backends[b];
+    if (!be.has_model_key) {
+      *st = 500;
+      *msg = "'model'";
+      *etype = "proxy_error";
+      return false;
+    }
+    if (!be.model.empty()) {
+      JVal j = s->body;
+      j.set("model", JVal::str(be.model));
+      out = json_dumps(j);
+      return true;
+    }
+    if (!s->body.get("model")) {
+      *st = 400;
+      *msg = "No model specified in config.yaml or request";
+      *etype = "invalid_request_error";
+      return false;
+    }
+    out = s->raw;
+    return true;
+  }
+  std::string build_req(const BackendCfg& be, const std::vector<std::pair<std::string, std::string>>& hdrs,
+                        const std::string& body) {
+    std::string r = "POST " + be.path + "/chat/completions HTTP/1.1\r\nhost: " + be.host +
+                    (be.port != 80 ? ":" + std::to_string(be.port) : std::string()) + "\r\n";
+    for (auto& h : hdrs) r += h.first + ": " + h.second + "\r\n";
+    r += "content-length: " + std::to_string(body.size()) + "\r\n\r\n";
+    r += body;
+    return r;
+  }
+  Up* open_up(Session* s, int bi, int backend, UpMode mode, std::string req, double timeout) {
+    const BackendCfg& be = cfg_.backends[backend];
+    auto u = std::make_unique<Up>();
+    u->backend = backend;
+    u->sess = s;
+    u->bi = bi;
+    u->mode = mode;
+    u->req = std::move(req);
+    u->timeout = timeout;
+    u->last_io = now_s();
+    u->deadline = cfg_.total_timeout > 0 ? u->last_io + cfg_.total_timeout : 0;
+    if (!be.resolved || be.https) return nullptr;
+    int fd = -1;
+    auto& pool = idle_[backend];
+    while (!pool.empty() && fd < 0) {
+      fd = pool.back();
+      pool.pop_back();
+      u->reused = true;
+    }
+    if (fd < 0) {
+      fd = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK, 0);
+      int one = 1;
+      setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+      int r = connect(fd, (const sockaddr*)&be.addr, sizeof(be.addr));
+      if (r != 0 && errno != EINPROGRESS) {
+        close(fd);
+        return nullptr;
+      }
+      u->connecting = r != 0;
+      c_up_conns++;
+      u->fd = fd;
+      add(fd, EPOLLIN | EPOLLOUT, tag(4, fd));
+    } else {
+      u->fd = fd;
+      add(fd, EPOLLIN | EPOLLOUT, tag(4, fd));
+    }
+    Up* p = u.get();
+    ups_[fd] = std::move(u);
+    if (!p->connecting) write_up(p);
+    return p;
+  }
+  void write_up(Up* u) {
+    while (u->req_off < u->req.size()) {
+      ssize_t w = send(u->fd, u->req.data() + u->req_off, u->req.size() - u->req_off, MSG_NOSIGNAL);
+      if (w > 0) {
+        u->req_off += w;
+        u->last_io = now_s();
+        continue;
+      }
+      if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) return;
+      return up_error(u, "All connection attempts failed");
+    }
+    mod(u->fd, EPOLLIN, tag(4, u->fd));
+  }
+  void on_up(Up* u, uint32_t ev) {
+    if (u->connecting && (ev & (EPOLLOUT | EPOLLERR | EPOLLHUP))) {
+      int err = 0;
+      socklen_t len = sizeof(err);
+      getsockopt(u->fd, SOL_SOCKET, SO_ERROR, &err, &len);
+      if (err != 0) return up_error(u, "All connection attempts failed");
+      u->connecting = false;
+    }
+    const int fd = u->fd;
+    if ((ev & EPOLLOUT) && u->req_off < u->req.size()) {
+      write_up(u);
+      if (ups_.find(fd) == ups_.end()) return;
+    }
+    if (ev & (EPOLLIN | EPOLLHUP | EPOLLERR)) {
+      char buf[65536];
+      bool eof = false;
+      std::string body;
+      while (true) {
+        ssize_t r = recv(u->fd, buf, sizeof(buf), 0);
+        if (r > 0) {
+          u->got_bytes = true;
+          u->last_io = now_s();
+          if (u->rp.feed(buf, r, body) < 0) return up_error(u, "invalid HTTP response");
+          continue;
+        }
+        if (r == 0) eof = true;
+        else if (errno != EAGAIN && errno != EWOULDBLOCK) eof = true;
+        break;
+      }
+      if (!u->headers_seen && u->rp.phase > 0) {
+        u->headers_seen = true;
+        on_up_headers(u);
+        if (ups_.find(fd) == ups_.end()) return;
+      }
+      if (!body.empty()) on_up_body(u, body);
+      if (u->rp.done()) return up_complete(u, true);
+      if (eof) {
+        if (u->rp.phase == 6) return up_complete(u, false);
+        if (!u->got_bytes && u->reused) return retry_fresh(u);
+        return up_error(u, "Server disconnected without sending a response.");
+      }
+    }
+  }
+  void retry_fresh(Up* u) {
+    Session* s = u->sess;
+    int bi = u->bi, backend = u->backend;
+    UpMode mode = u->mode;
+    std::string req = u->req;
+    double to = u->timeout;
+    drop_up(u, false);
+    Up* nu = open_up(s, bi, backend, mode, req, to);
+    if (!nu) return fail_backend(s, bi, 500, "All connection attempts failed", "proxy_error");
+    if (bi >= 0) s->bs[bi].up = nu;
+    else s->agg = nu;
+  }
+  void drop_up(Up* u, bool reuse) {
+    int fd = u->fd;
+    if (reuse && !u->rp.close) {
+      epoll_ctl(ep_, EPOLL_CTL_DEL, fd, nullptr);  // parked: re-armed when reused
+      idle_[u->backend].push_back(fd);
+    } else {
+      epoll_ctl(ep_, EPOLL_CTL_DEL, fd, nullptr);
+      close(fd);
+    }
+    ups_.erase(fd);
+  }
+  void up_error(Up* u, const std::string& msg) {
+    Session* s = u->sess;
+    int bi = u->bi;
+    c_up_fail++;
+    drop_up(u, false);
+    if (bi >= 0) s->bs[bi].up = nullptr;
+    else s->agg = nullptr;
+    fail_backend(s, bi, 500, msg, "proxy_error");
+  }
+  void sweep_timeouts(double t) {
+    std::vector<int> expired;
+    for (auto& kv : ups_) {
+      Up* u = kv.second.get();
+      if (t - u->last_io > u->timeout || (u->deadline > 0 && t > u->deadline)) expired.push_back(kv.first);
+    }
+    for (int fd : expired) {
+      auto it = ups_.find(fd);
+      if (it != ups_.end()) up_error(it->second.get(), "");  // httpx timeouts stringify to ""
+    }
+  }
+
+  void on_up_headers(Up* u) {
+    Session* s = u->sess;
+    if (u->mode == UP_PASS && u->rp.status == 200) {
+      // single-backend passthrough: upstream headers (minus entity/hop-by-hop) + own role event
+      std::string h = "HTTP/1.1 200 OK\r\n";
+      bool has_ct = false;
+      for (auto& kv : u->rp.headers) {
+        if (kv.first == "content-length" || kv.first == "transfer-encoding" || kv.first == "content-encoding" ||
+            kv.first == "connection" || kv.first == "keep-alive")
+          continue;
+        if (kv.first == "content-type") has_ct = true;
+        h += kv.first + ": " + kv.second + "\r\n";
+      }
+      if (!has_ct) h += "content-type: text/event-stream; charset=utf-8\r\n";
+      h += "transfer-encoding: chunked\r\n\r\n";
+      s->pass_started = true;
+      if (s->cl) {
+        write_client(s->cl, h);
+        send_chunk(s, chunk_event_json("chatcmpl-role", (int64_t)time(nullptr), s->role_model_json,
+                                       "{\"role\": \"assistant\"}", "null"));
+      }
+    }
+  }
+  void on_up_body(Up* u, const std::string& body) {
+    Session* s = u->sess;
+    if (u->rp.status == 200 && u->mode == UP_ENGINE) {
+      eng_->feed(s->bs[u->bi].slot, body);
+      kick();
+      return;
+    }
+    if (u->rp.status == 200 && u->mode == UP_PASS) return pass_body(s, body);
+    u->body += body;
+  }
+  void up_complete(Up* u, bool reusable) {
+    Session* s = u->sess;
+    int bi = u->bi;
+    int status = u->rp.status;
+    UpMode mode = u->mode;
+    std::string body = std::move(u->body);
+    auto rh = u->rp.headers;
+    drop_up(u, reusable);
+    if (bi >= 0) s->bs[bi].up = nullptr;
+    else s->agg = nullptr;
+    if (mode == UP_ENGINE && status == 200) {
+      eng_->finish(s->bs[bi].slot);
+      kick();
+      return;
+    }
+    if (mode == UP_PASS && status == 200) return pass_end(s);
+    // buffered result (call_backend classification)
+    if (bi < 0) return on_aggregator_done(s, status, body);
+    BState& b = s->bs[bi];
+    b.status = status;
+    b.rheaders = rh;
+    JVal j;
+    bool ok = utf8_valid((const uint8_t*)body.data(), 0, (int)body.size()) &&
+              json_parse(body.data(), body.size(), j, nullptr);
+    if (status == 200) {
+      if (ok) {
+        if (j.t == JVal::OBJ) j.set("backend", JVal::str(cfg_.backends[b.backend].name));
+        else if (j.t == JVal::ARR) {
+          return fail_backend(s, bi, 500, "list indices must be integers or slices, not str", "proxy_error");
+        }
+        b.is_json = true;
+        b.js = std::move(j);
+      } else {
+        b.is_json = false;
+        b.text = body;
+      }
+    } else {
+      if (ok) {
+        b.is_json = true;
+        b.js = std::move(j);
+      } else {
+        JVal e;
+        e.t = JVal::OBJ;
+        JVal in;
+        in.t = JVal::OBJ;
+        in.set("message", JVal::str(body));
+        in.set("type", JVal::str("backend_error"));
+        e.set("error", in);
+        b.is_json = true;
+        b.js = std::move(e);
+      }
+      c_up_fail++;
+    }
+    if (mode == UP_ENGINE || mode == UP_PASS) {
+      // non-200 on a streaming call
+      return fail_backend(s, bi, status, error_message(b), nullptr, true);
+    }
+    b.state = 1;
+    s->finished++;
+    if (s->finished == (int)s->bs.size()) finish_nonstream(s);
+  }
+  static std::string error_message(const BState& b) {
+    if (!b.is_json) return b.text;
+    const JVal* e = b.js.get("error");
+    if (e) {
+      if (e->t == JVal::OBJ) {
+        const JVal* m = e->get("message");
+        return m ? py_str(*m) : "Unknown error";
+      }
+      return py_str(*e);
+    }
+    return py_str(b.js);
+  }
+
+  // record a failed backend (synthetic or transport) and advance the session
+  void fail_backend(Session* s, int bi, int status, const std::string& msg, const char* etype, bool have_result = false) {
+    if (bi < 0) return on_aggregator_done(s, 500, std::string());
+    BState& b = s->bs[bi];
+    if (b.state != 0) return;
+    if (!have_result) {
+      b.status = status;
+      JVal e;
+      e.t = JVal::OBJ;
+      JVal in;
+      in.t = JVal::OBJ;
+      in.set("message", JVal::str(msg));
+      in.set("type", JVal::str(etype ? etype : "proxy_error"));
+      e.set("error", in);
+      b.is_json = true;
+      b.js = std::move(e);
+    }
+    b.state = 2;
+    s->finished++;
+    if (s->kind == K_PAR) {
+      if (s->stage == 0 && s->finished == (int)s->bs.size()) begin_final(s);
+    } else if (s->kind == K_SINGLE) {
+      if (s->cl) {
+        if (s->pass_started) {
+          write_client(s->cl, "0\r\n\r\n");
+          s->cl->keepalive = false;
+        } else {
+          respond(s->cl, b.status, "application/json", err_json("Backend failed: " + error_message(b), "proxy_error"));
+        }
+      }
+      end_session(s);
+    } else if (s->finished == (int)s->bs.size()) {
+      finish_nonstream(s);
+    }
+  }
+
+  // ---------------------------------------------------------------- parallel streaming
+  void send_chunk(Session* s, const std::string& data) {
+    if (s->cl) write_client(s->cl, chunk(data));
+  }
+  void start_parallel(Session* s, const std::vector<int>& valid) {
+    c_stream++;
+    s->kind = K_PAR;
+    s->filter = cfg_.hide_intermediate;
+    s->emit = !cfg_.suppress;
+    if (const JVal* sup = s->body.get("suppress_individual_responses")) s->emit = !sup->truthy();
+    write_client(s->cl, kSseHdr);
+    send_chunk(s, chunk_event_json("chatcmpl-parallel", (int64_t)time(nullptr), "\"parallel-proxy\"",
+                                   "{\"role\": \"assistant\"}", "null"));
+    s->bs.resize(valid.size());
+    for (size_t i = 0; i < valid.size(); ++i) {
+      s->bs[i].backend = valid[i];
+      s->bs[i].slot = eng_->open((int)i, s->filter, s->emit);
+      slot_owner_[s->bs[i].slot] = {s, (int)i};
+    }
+    for (size_t i = 0; i < valid.size(); ++i) {
+      std::string body, msg;
+      int st = 0;
+      const char* et = nullptr;
+      if (!upstream_body(s, valid[i], body, &st, &msg, &et)) {
+        fail_backend(s, (int)i, st, msg, et);
+        continue;
+      }
+      Up* u = open_up(s, (int)i, valid[i], UP_ENGINE, build_req(cfg_.backends[valid[i]], s->fwd, body), cfg_.timeout);
+      if (!u) fail_backend(s, (int)i, 500, "All connection attempts failed", "proxy_error");
+      else s->bs[i].up = u;
+    }
+  }
+  std::vector<int> good_slots(Session* s) {
+    std::vector<int> g;
+    for (auto& b : s->bs)
+      if (b.state == 1 && !b.aborted) g.push_back(b.slot);
+    return g;
+  }
+  void begin_final(Session* s) {
+    s->stage = 1;
+    if (cfg_.skip_final) return finish_stream(s);
+    std::vector<int> g = good_slots(s);
+    bool texts = !cfg_.aggregator_name.empty();
+    s->fin_texts = texts;
+    s->fin_id = eng_->submit_finalize(g, cfg_.hide_final, texts, "\n" + cfg_.separator, (int64_t)time(nullptr));
+    fin_owner_[s->fin_id] = s;
+    kick();
+  }
+  void on_finalized(Session* s, FinalizeRes& f) {
+    if (s->kind == K_NONSTREAM) return;  // not used
+    if (!s->fin_texts) {
+      if (f.kind == 1) send_chunk(s, f.event);
+      else send_chunk(s, error_event());
+      return finish_stream(s);
+    }
+    if (f.texts.empty()) {
+      send_chunk(s, error_event());
+      return finish_stream(s);
+    }
+    s->texts = std::move(f.texts);
+    start_aggregator(s, "\n" + cfg_.separator);
+  }
+  std::string error_event() {
+    return chunk_event_json("error", (int64_t)time(nullptr), "\"parallel-proxy\"",
+                            "{\"content\": \"Error: All backends failed to provide content\"}", "\"error\"");
+  }
+  std::string joined(const std::vector<std::string>& t, const std::string& sep) {
+    std::string o;
+    for (size_t i = 0; i < t.size(); ++i) {
+      if (i) o += sep;
+      o += t[i];
+    }
+    return o;
+  }
+  void emit_final_value(Session* s, const JVal& content) {
+    std::string delta = "{\"content\": " + json_dumps(content) + "}";
+    send_chunk(s, chunk_event_json("chatcmpl-parallel-final", (int64_t)time(nullptr), "\"parallel-proxy\"", delta,
+                                   "\"stop\""));
+    finish_stream(s);
+  }
+  void finish_stream(Session* s) {
+    send_chunk(s, kDone);
+    if (s->cl) write_client(s->cl, "0\r\n\r\n");
+    end_session(s);
+  }
+
+  // ---------------------------------------------------------------- aggregator
+  // exc_joiner: join used when prompt building raises (quorum's outer except)
+  void start_aggregator(Session* s, const std::string& exc_joiner) {
+    s->stage = 2;
+    int ab = -1;
+    for (int i = 0; i < (int)cfg_.backends.size(); ++i)
+      if (cfg_.backends[i].name == cfg_.aggregator_name) {
+        ab = i;
+        break;
+      }
+    if (ab < 0) return aggregate_result(s, JVal::str(joined(s->texts, exc_joiner)));
+    // prompt (quorum :406-423)
+    std::vector<std::string> parts;
+    for (size_t i = 0; i < s->texts.size(); ++i) {
+      if (cfg_.include_source_names) {
+        std::string lab;
+        if (!py_format(cfg_.source_label_format, "backend_name", "LLM" + std::to_string(i + 1), lab))
+          return aggregate_result(s, JVal::str(joined(s->texts, exc_joiner)));
+        parts.push_back(lab + s->texts[i]);
+      } else {
+        parts.push_back(s->texts[i]);
+      }
+    }
+    std::string prompt;
+    if (cfg_.include_original_query) {
+      std::string uq;
+      const JVal* msgs = s->body.get("messages");
+      if (msgs && msgs->truthy() && msgs->t == JVal::ARR) {
+        for (auto& m : msgs->a) {
+          const JVal* r = m.get("role");
+          if (r && r->t == JVal::STR && r->s == "user") {
+            const JVal* ct = m.get("content");
+            uq = ct ? py_str(*ct) : "";
+            break;
+          }
+        }
+      }
+      if (!py_format(cfg_.query_format, "query", uq, prompt))
+        return aggregate_result(s, JVal::str(joined(s->texts, exc_joiner)));
+    }
+    std::string inter = joined(parts, cfg_.intermediate_separator);
+    std::string tmpl = cfg_.prompt_template;
+    std::string out;
+    for (size_t i = 0; i < tmpl.size();) {
+      if (tmpl.compare(i, 11, "{responses}") == 0) {
+        out += inter;
+        i += 11;
+      } else {
+        out.push_back(tmpl[i++]);
+      }
+    }
+    prompt += out;
+    const BackendCfg& be = cfg_.backends[ab];
+    JVal req;
+    req.t = JVal::OBJ;
+    req.set("model", JVal::str(be.model));
+    JVal msgs;
+    msgs.t = JVal::ARR;
+    JVal m;
+    m.t = JVal::OBJ;
+    m.set("role", JVal::str("user"));
+    m.set("content", JVal::str(prompt));
+    msgs.a.push_back(m);
+    req.set("messages", msgs);
+    req.set("stream", JVal::boolean(false));
+    std::vector<std::pair<std::string, std::string>> h = {{"Authorization", s->auth},
+                                                          {"Content-Type", "application/json"}};
+    if (!be.valid || !be.has_model_key) return on_aggregator_done(s, 500, std::string());
+    Up* u = open_up(s, -1, ab, UP_BUFFER, build_req(be, h, json_dumps(req)), 60.0);
+    if (!u) return on_aggregator_done(s, 500, std::string());
+    s->agg = u;
+  }
+  void on_aggregator_done(Session* s, int status, const std::string& body) {
+    JVal j;
+    if (status == 200 && json_parse(body.data(), body.size(), j, nullptr)) {
+      const JVal* ch = j.get("choices");
+      if (ch && ch->t == JVal::ARR && !ch->a.empty()) {
+        const JVal* msg = ch->a[0].get("message");
+        const JVal* ct = msg ? msg->get("content") : nullptr;
+        if (ct) return aggregate_result(s, *ct);
+      }
+    }
+    aggregate_result(s, JVal::str(joined(s->texts, cfg_.intermediate_separator)));
+  }
+  void aggregate_result(Session* s, const JVal& v) {
+    if (s->kind == K_PAR) return emit_final_value(s, v);
+    finish_nonstream_combined(s, v);
+  }
+
+  // ---------------------------------------------------------------- single-backend streaming
+  void start_single(Session* s, int backend) {
+    c_stream++;
+    s->kind = K_SINGLE;
+    s->bs.resize(1);
+    s->bs[0].backend = backend;
+    const JVal* m = s->body.get("model");
+    if (m && m->truthy()) s->role_model_json = json_dumps(*m);
+    else s->role_model_json = cfg_.backends[backend].has_model_key ? json_dumps(JVal::str(cfg_.backends[backend].model))
+                                                                   : "\"unknown\"";
+    std::string body, msg;
+    int st = 0;
+    const char* et = nullptr;
+    if (!upstream_body(s, backend, body, &st, &msg, &et)) return fail_backend(s, 0, st, msg, et);
+    Up* u = open_up(s, 0, backend, UP_PASS, build_req(cfg_.backends[backend], s->fwd, body), cfg_.timeout);
+    if (!u) return fail_backend(s, 0, 500, "All connection attempts failed", "proxy_error");
+    s->bs[0].up = u;
+  }
+  static bool bare_role(const std::string& ev) {
+    std::string t = ev;
+    if (t.compare(0, 6, "data: ") == 0) t = t.substr(6);
+    JVal j;
+    if (!json_parse(t.data(), t.size(), j, nullptr) || j.t != JVal::OBJ) return false;
+    const JVal* ch = j.get("choices");
+    if (!ch || ch->t != JVal::ARR || ch->a.empty() || ch->a[0].t != JVal::OBJ) return false;
+    const JVal* d = ch->a[0].get("delta");
+    if (!d || d->t != JVal::OBJ) return false;
+    const JVal* r = d->get("role");
+    const JVal* c = d->get("content");
+    bool content_empty = !c || (c->t == JVal::STR && c->s.empty());
+    return r && r->truthy() && content_empty;
+  }
+  void pass_forward(Session* s, const std::string& data) {
+    bool all_ws = true;
+    for (char ch : data)
+      if (!(ch == ' ' || ch == '\n' || ch == '\r' || ch == '\t')) all_ws = false;
+    if (all_ws) return;
+    std::string w = s->done_tail + data;
+    if (w.find("data: [DONE]") != std::string::npos) s->saw_done = true;
+    s->done_tail = w.size() > 16 ? w.substr(w.size() - 16) : w;
+    send_chunk(s, data);
+  }
+  void pass_body(Session* s, const std::string& body) {
+    if (!s->first_decided) {
+      s->first_buf += body;
+      size_t j = s->first_buf.find("\n\n");
+      if (j == std::string::npos) return;
+      s->first_decided = true;
+      std::string first = s->first_buf.substr(0, j + 2), rest = s->first_buf.substr(j + 2);
+      s->first_buf.clear();
+      if (!bare_role(first)) rest = first + rest;
+      if (!rest.empty()) pass_forward(s, rest);
+      return;
+    }
+    pass_forward(s, body);
+  }
+  void pass_end(Session* s) {
+    if (!s->first_decided && !s->first_buf.empty() && !bare_role(s->first_buf)) pass_forward(s, s->first_buf);
+    if (!s->saw_done) send_chunk(s, kDone);
+    if (s->cl) write_client(s->cl, "0\r\n\r\n");
+    s->bs[0].state = 1;
+    end_session(s);
+  }
+
+  // ---------------------------------------------------------------- non-streaming
+  void start_nonstream(Session* s, const std::vector<int>& valid, bool parallel) {
+    c_nonstream++;
+    s->kind = K_NONSTREAM;
+    s->stage = parallel ? 10 : 11;
+    s->bs.resize(valid.size());
+    for (size_t i = 0; i < valid.size(); ++i) s->bs[i].backend = valid[i];
+    for (size_t i = 0; i < valid.size(); ++i) {
+      std::string body, msg;
+      int st = 0;
+      const char* et = nullptr;
+      if (!upstream_body(s, valid[i], body, &st, &msg, &et)) {
+        fail_backend(s, (int)i, st, msg, et);
+        if (sessions_.find(s) == sessions_.end()) return;
+        continue;
+      }
+      Up* u = open_up(s, (int)i, valid[i], UP_BUFFER, build_req(cfg_.backends[valid[i]], s->fwd, body), cfg_.timeout);
+      if (!u) {
+        fail_backend(s, (int)i, 500, "All connection attempts failed", "proxy_error");
+        if (sessions_.find(s) == sessions_.end()) return;
+      } else {
+        s->bs[i].up = u;
+      }
+    }
+  }
+  void finish_nonstream(Session* s) {
+    std::vector<BState*> ok;
+    for (auto& b : s->bs)
+      if (b.status == 200) ok.push_back(&b);
+    if (ok.empty()) {
+      if (s->cl)
+        respond(s->cl, 500, "application/json",
+                err_json("All backends failed. First error: " + error_message(s->bs[0]), "proxy_error"));
+      return end_session(s);
+    }
+    if (s->stage == 11) {
+      BState* f = ok[0];
+      const std::string* ct = nullptr;
+      for (auto& h : f->rheaders)
+        if (h.first == "content-type") ct = &h.second;
+      std::vector<std::pair<std::string, std::string>> extra;
+      for (auto& h : f->rheaders)
+        if (h.first != "content-length" && h.first != "content-type" && h.first != "transfer-encoding" &&
+            h.first != "content-encoding" && h.first != "connection" && h.first != "keep-alive")
+          extra.push_back(h);
+      std::string body = f->is_json ? json_dumps(f->js) : f->text;
+      if (s->cl) respond(s->cl, 200, ct ? *ct : "application/json", body, &extra);
+      return end_session(s);
+    }
+    // parallel combine (quorum :1191-1341)
+    std::vector<std::string> processed;
+    std::string err;
+    for (BState* b : ok) {
+      const JVal* content = nullptr;
+      if (b->is_json) {
+        const JVal* ch = b->js.get("choices");
+        if (ch && ch->t == JVal::ARR && !ch->a.empty()) {
+          const JVal* m = ch->a[0].get("message");
+          if (m) content = m->get("content");
+          else err = "'message'";
+        } else {
+          err = ch ? "list index out of range" : "'choices'";
+        }
+      } else {
+        err = "string indices must be integers";
+      }
+      if (!content) {
+        if (err.empty()) err = "'content'";
+        break;
+      }
+      if (content->t != JVal::STR) {
+        err = cfg_.hide_final ? "expected string or bytes-like object" : "sequence item 0: expected str instance";
+        break;
+      }
+      processed.push_back(cfg_.hide_final ? strip_final(eng_->tagset(), (const uint8_t*)content->s.data(),
+                                                        content->s.size())
+                                          : content->s);
+    }
+    if (!err.empty()) {
+      if (s->cl) respond(s->cl, 500, "application/json", err_json("Error combining responses: " + err, "proxy_error"));
+      return end_session(s);
+    }
+    s->texts = processed;
+    s->fin_texts = true;
+    if (!cfg_.aggregator_name.empty()) return start_aggregator(s, cfg_.separator);
+    finish_nonstream_combined(s, JVal::str(joined(processed, cfg_.separator)));
+  }
+  void finish_nonstream_combined(Session* s, const JVal& combined) {
+    std::vector<BState*> ok;
+    for (auto& b : s->bs)
+      if (b.status == 200) ok.push_back(&b);
+    std::string err;
+    JVal usage;
+    usage.t = JVal::OBJ;
+    for (const char* k : {"prompt_tokens", "completion_tokens", "total_tokens"}) {
+      long long isum = 0;
+      double fsum = 0;
+      bool isf = false;
+      for (BState* b : ok) {
+        const JVal* u = b->is_json ? b->js.get("usage") : nullptr;
+        const JVal* v = u ? u->get(k) : nullptr;
+        if (!u) { err = "'usage'"; break; }
+        if (!v) { err = std::string("'") + k + "'"; break; }
+        if (v->t == JVal::INT) { isum += atoll(v->s.c_str()); fsum += atof(v->s.c_str()); }
+        else if (v->t == JVal::FLOAT) { isf = true; fsum += v->d; }
+        else { err = "unsupported operand type(s) for +"; break; }
+      }
+      if (!err.empty()) break;
+      if (isf) {
+        JVal f;
+        f.t = JVal::FLOAT;
+        f.d = fsum;
+        usage.set(k, f);
+      } else {
+        usage.set(k, JVal::integer(isum));
+      }
+    }
+    const JVal& first = ok[0]->js;
+    for (const char* k : {"id", "created", "model"})
+      if (err.empty() && !first.get(k)) err = std::string("'") + k + "'";
+    if (!err.empty()) {
+      if (s->cl) respond(s->cl, 500, "application/json", err_json("Error combining responses: " + err, "proxy_error"));
+      return end_session(s);
+    }
+    JVal out;
+    out.t = JVal::OBJ;
+    out.set("id", *first.get("id"));
+    out.set("object", JVal::str("chat.completion"));
+    out.set("created", *first.get("created"));
+    out.set("model", *first.get("model"));
+    const JVal* fp = first.get("system_fingerprint");
+    out.set("system_fingerprint", fp ? *fp : JVal::str(""));
+    JVal choice;
+    choice.t = JVal::OBJ;
+    choice.set("index", JVal::integer(0));
+    JVal msg;
+    msg.t = JVal::OBJ;
+    msg.set("role", JVal::str("assistant"));
+    msg.set("content", combined);
+    choice.set("message", msg);
+    choice.set("logprobs", JVal());
+    choice.set("finish_reason", JVal::str("stop"));
+    JVal choices;
+    choices.t = JVal::ARR;
+    choices.a.push_back(choice);
+    out.set("choices", choices);
+    out.set("usage", usage);
+    if (s->cl) respond(s->cl, 200, "application/json", json_dumps(out));
+    end_session(s);
+  }
+
+  // ---------------------------------------------------------------- session lifecycle
+  void end_session(Session* s) {
+    if (s->stage == 3) return;
+    s->stage = 3;
+    for (auto& b : s->bs) {
+      if (b.up) {
+        drop_up(b.up, false);
+        b.up = nullptr;
+      }
+      if (b.slot >= 0) {
+        slot_owner_.erase(b.slot);
+        eng_->release(b.slot);
+        b.slot = -1;
+      }
+    }
+    if (s->agg) {
+      drop_up(s->agg, false);
+      s->agg = nullptr;
+    }
+    if (s->fin_id >= 0) fin_owner_.erase(s->fin_id);
+    Client* c = s->cl;
+    sessions_.erase(s);
+    if (c) {
+      c->sess = nullptr;
+      if (!c->keepalive || c->dead) mark_close(c);
+      else if (!c->in.empty()) pending_requests_.push_back(c->fd);
+    }
+  }
+  void abort_session(Session* s) { end_session(s); }
+
+  std::string metrics_text() {
+    std::string m;
+    auto put = [&](const char* k, double v) { m += std::string(k) + " " + std::to_string(v) + "\n"; };
+    put("qmx_requests_total", (double)c_requests.load());
+    put("qmx_stream_requests_total", (double)c_stream.load());
+    put("qmx_nonstream_requests_total", (double)c_nonstream.load());
+    put("qmx_errors_total", (double)c_errors.load());
+    put("qmx_upstream_failures_total", (double)c_up_fail.load());
+    put("qmx_upstream_connections_total", (double)c_up_conns.load());
+    put("qmx_client_connections_total", (double)c_clients.load());
+    put("qmx_ticks_total", (double)c_ticks.load());
+    put("qmx_tick_slots_total", (double)c_tick_slots.load());
+    for (auto& kv : eng_->stats()) put(("qmx_engine_" + kv.first).c_str(), kv.second);
+    if (offload_)
+      for (auto& kv : static_cast<HipEngine*>(eng_.get())->kernel_stats())
+        put(("qmx_kernel_" + kv.first).c_str(), kv.second);
+    return m;
+  }
+
+  const ServerCfg& cfg_;
+  int idx_;
+  int ep_ = -1, lfd_ = -1, evfd_ = -1;
+  std::unique_ptr<HostEngine> eng_;
+  bool offload_ = false, kick_ = false;
+  std::thread gpu_thread_;
+  std::mutex mu_, rmu_;
+  std::condition_variable cv_;
+  bool work_ = false;
+  std::atomic<bool> stop_gpu_{false};
+  std::vector<ResultBatch> rq_;
+  std::unordered_map<int, std::unique_ptr<Client>> clients_;
+  std::unordered_map<int, std::unique_ptr<Up>> ups_;
+  std::unordered_map<Session*, std::unique_ptr<Session>> sessions_;
+  std::unordered_map<int, std::pair<Session*, int>> slot_owner_;
+  std::unordered_map<int, Session*> fin_owner_;
+  std::vector<std::vector<int>> idle_;
+  std::vector<int> pending_close_, pending_requests_;
+};
+
+void on_signal(int) { g_stop.store(true); }
+
+}  // namespace
+
+int run_server(const ServerCfg& cfg0) {
+  ServerCfg cfg = cfg0;
+  for (auto& b : cfg.backends) {
+    if (!b.valid || b.https || b.host.empty()) continue;
+    addrinfo hints{}, *res = nullptr;
+    hints.ai_family = AF_INET;
+    hints.ai_socktype = SOCK_STREAM;
+    if (getaddrinfo(b.host.c_str(), std::to_string(b.port).c_str(), &hints, &res) == 0 && res) {
+      std::memcpy(&b.addr, res->ai_addr, sizeof(sockaddr_in));
+      b.resolved = true;
+      freeaddrinfo(res);
+    }
+  }
+  signal(SIGPIPE, SIG_IGN);
+  if (cfg.install_signals) {
+    struct sigaction sa {};
+    sa.sa_handler = on_signal;
+    sigaction(SIGTERM, &sa, nullptr);
+    sigaction(SIGINT, &sa, nullptr);
+  }
+  g_stop.store(false);
+  std::vector<std::unique_ptr<Loop>> loops;
+  std::vector<std::thread> ts;
+  for (int i = 0; i < std::max(1, cfg.threads); ++i) loops.emplace_back(new Loop(cfg, i));
+  for (auto& l : loops) {
+    Loop* lp = l.get();
+    ts.emplace_back([lp] {
+      try {
+        lp->run();
+      } catch (const std::exception& e) {
+        fprintf(stderr, "qmx_server loop error: %s\n", e.what());
+        g_stop.store(true);
+      }
+    });
+  }
+  for (auto& t : ts) t.join();
+  loops.clear();
+  return 0;
+}
+
+void stop_server() { g_stop.store(true); }
+
+std::unordered_map<std::string, double> server_counters() {
+  return {{"requests", (double)c_requests.load()}, {"errors", (double)c_errors.load()},
+          {"ticks", (double)c_ticks.load()}, {"upstream_failures", (double)c_up_fail.load()}};
+}
+
+}  // namespace qmx

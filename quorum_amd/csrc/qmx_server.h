@@ -1,0 +1,58 @@
+// qmx_server.h — native data plane: epoll HTTP/1.1 proxy front-end + upstream client.
+//
+// One process per GPU; T io threads per process, each owning an SO_REUSEPORT listener, its
+// client/upstream connections, keep-alive upstream pools, and its own stream engine (for
+// `hip`: its own HIP stream + device-resident slot arena, driven by a companion tick
+// thread so socket I/O overlaps the fused tick kernel).  Semantics mirror the FastAPI
+// conformance app (quorum_amd/server/app.py) and quorum's handler
+// (src/quorum/oai_proxy.py:959-1408).
+#pragma once
+#include <netinet/in.h>
+
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace qmx {
+
+struct BackendCfg {
+  std::string name, url, model;
+  bool has_model_key = true;  // quorum indexes backend["model"] (KeyError → proxy_error)
+  bool valid = false;         // url truthy
+  std::string host, path;     // parsed http URL
+  int port = 80;
+  bool https = false;
+  sockaddr_in addr{};
+  bool resolved = false;
+};
+
+struct ServerCfg {
+  std::string host = "127.0.0.1";
+  int port = 8000;
+  int threads = 2;
+  // engine
+  std::string engine = "cpu";
+  int device = 0;
+  int tile = 16384, max_slots = 4096, content_cap = 1 << 20;
+  // config
+  std::vector<BackendCfg> backends;  // all primary_backends (config order)
+  bool has_iterations_and_strategy = false;
+  double timeout = 60.0;
+  double total_timeout = 0.0;  // 0 = none (quorum semantics)
+  std::string separator = "\n";
+  bool hide_intermediate = true, hide_final = false, skip_final = false, suppress = false;
+  std::vector<std::string> tags;
+  // strategy.aggregate (consulted whatever strategy is selected, as in quorum)
+  std::string aggregator_name;  // empty = none
+  std::string prompt_template, intermediate_separator, query_format, source_label_format;
+  bool include_original_query = true, include_source_names = false;
+  std::string env_api_key;
+  bool install_signals = true;
+};
+
+// Runs until SIGTERM/SIGINT. Returns 0 on clean shutdown.
+int run_server(const ServerCfg& cfg);
+std::unordered_map<std::string, double> server_counters();
+void stop_server();  // thread-safe; run_server returns within ~50 ms
+
+}  // namespace qmx

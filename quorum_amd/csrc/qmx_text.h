@@ -49,7 +49,8 @@ QMX_HD uint8_t pattern_byte(const TagSet& ts, int pat, int i) {
 }
 
 // Token at position p of x[0:n): +(t+1) open tag t, -(t+1) close tag t, 0 none.
-QMX_HD int match_at(const uint8_t* x, int n, int p, const TagSet& ts, int* tok_len) {
+template <class R>
+QMX_HD int match_at(const R& x, int n, int p, const TagSet& ts, int* tok_len) {
   if (x[p] != '<') return 0;
   bool close = (p + 1 < n && x[p + 1] == '/');
   int s = p + 1 + (close ? 1 : 0);
@@ -67,7 +68,8 @@ QMX_HD int match_at(const uint8_t* x, int n, int p, const TagSet& ts, int* tok_l
 }
 
 // Is x[q:n) (lowercased) a prefix of some pattern?  opens_only: open patterns only.
-QMX_HD bool pattern_prefix(const uint8_t* x, int q, int n, const TagSet& ts, bool opens_only) {
+template <class R>
+QMX_HD bool pattern_prefix(const R& x, int q, int n, const TagSet& ts, bool opens_only) {
   int m = n - q;
   int npat = opens_only ? ts.n : 2 * ts.n;
   for (int pat = 0; pat < npat; ++pat) {
@@ -84,7 +86,8 @@ QMX_HD bool pattern_prefix(const uint8_t* x, int q, int n, const TagSet& ts, boo
 // Unicode (Python str.isspace) whitespace on UTF-8 bytes
 // ---------------------------------------------------------------------------
 // Byte length of the whitespace char starting at x[p] (0: not whitespace, -1: incomplete).
-QMX_HD int ws_at(const uint8_t* x, int p, int n) {
+template <class R>
+QMX_HD int ws_at(const R& x, int p, int n) {
   uint8_t c = x[p];
   if (c < 0x80) return (c == ' ' || (c >= 0x09 && c <= 0x0d) || (c >= 0x1c && c <= 0x1f)) ? 1 : 0;
   if (c == 0xC2) {
@@ -103,14 +106,16 @@ QMX_HD int ws_at(const uint8_t* x, int p, int n) {
   return 0;
 }
 // Byte length of a whitespace char ENDING at x[e-1] (lo = lower bound), 0 if none.
-QMX_HD int ws_before(const uint8_t* x, int lo, int e) {
+template <class R>
+QMX_HD int ws_before(const R& x, int lo, int e) {
   if (e - 1 >= lo && x[e - 1] < 0x80) return ws_at(x, e - 1, e) == 1 ? 1 : 0;
   if (e - 2 >= lo && ws_at(x, e - 2, e) == 2) return 2;
   if (e - 3 >= lo && ws_at(x, e - 3, e) == 3) return 3;
   return 0;
 }
 // Python str.strip() on a UTF-8 range.
-QMX_HD void ustrip(const uint8_t* x, int* a, int* b) {
+template <class R>
+QMX_HD void ustrip(const R& x, int* a, int* b) {
   while (*a < *b) {
     int w = ws_at(x, *a, *b);
     if (w <= 0) break;
@@ -124,7 +129,8 @@ QMX_HD void ustrip(const uint8_t* x, int* a, int* b) {
 }
 
 // Strict UTF-8 validation (Python bytes.decode('utf-8')): no overlongs, no surrogates.
-QMX_HD bool utf8_valid(const uint8_t* x, int a, int b) {
+template <class R>
+QMX_HD bool utf8_valid(const R& x, int a, int b) {
   int i = a;
   while (i < b) {
     uint8_t c = x[i];
@@ -149,7 +155,8 @@ QMX_HD bool utf8_valid(const uint8_t* x, int a, int b) {
 }
 
 // Decode one (W)UTF-8 code point at y[p] (input known well-formed WTF-8); returns length.
-QMX_HD int wtf8_decode(const uint8_t* y, int p, int n, uint32_t* cp) {
+template <class R>
+QMX_HD int wtf8_decode(const R& y, int p, int n, uint32_t* cp) {
   uint8_t c = y[p];
   if (c < 0x80) { *cp = c; return 1; }
   if (c < 0xE0 && p + 1 < n) { *cp = ((c & 0x1F) << 6) | (y[p + 1] & 0x3F); return 2; }
@@ -210,8 +217,9 @@ QMX_HD int hexv(uint8_t c) {
   if (c >= 'a' && c <= 'f') return c - 'a' + 10;
   return -1;
 }
-QMX_HD uint32_t hex4(const uint8_t* x) {
-  return (uint32_t)((hexv(x[0]) << 12) | (hexv(x[1]) << 8) | (hexv(x[2]) << 4) | hexv(x[3]));
+template <class R>
+QMX_HD uint32_t hex4(const R& x, int i) {
+  return (uint32_t)((hexv(x[i]) << 12) | (hexv(x[i + 1]) << 8) | (hexv(x[i + 2]) << 4) | hexv(x[i + 3]));
 }
 QMX_HD int put_wtf8(uint32_t cp, uint8_t* o) {
   if (cp < 0x80) { if (o) o[0] = (uint8_t)cp; return 1; }
@@ -228,7 +236,8 @@ QMX_HD int put_wtf8(uint32_t cp, uint8_t* o) {
 }
 // Decode JSON string body x[a:b) → out (may be null: length only). Python json semantics:
 // \uD8xx\uDCxx pairs combine, lone surrogates are kept (as 3-byte WTF-8).
-QMX_HD int json_unescape(const uint8_t* x, int a, int b, uint8_t* out) {
+template <class R>
+QMX_HD int json_unescape(const R& x, int a, int b, uint8_t* out) {
   int o = 0, i = a;
   while (i < b) {
     uint8_t c = x[i];
@@ -240,10 +249,10 @@ QMX_HD int json_unescape(const uint8_t* x, int a, int b, uint8_t* out) {
     uint8_t e = x[i + 1];
     uint32_t cp;
     if (e == 'u') {
-      cp = hex4(x + i + 2);
+      cp = hex4(x, i + 2);
       i += 6;
       if (cp >= 0xD800 && cp <= 0xDBFF && i + 6 <= b && x[i] == '\\' && x[i + 1] == 'u') {
-        uint32_t lo = hex4(x + i + 2);
+        uint32_t lo = hex4(x, i + 2);
         if (lo >= 0xDC00 && lo <= 0xDFFF) {
           cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
           i += 6;
@@ -268,6 +277,27 @@ QMX_HD int json_unescape(const uint8_t* x, int a, int b, uint8_t* out) {
 // ---------------------------------------------------------------------------
 // Validating JSON delta extractor (Python json.loads + quorum's exception semantics)
 // ---------------------------------------------------------------------------
+// Literals are packed into 64-bit immediates (byte k = char k): device code must never
+// index string literals in per-byte loops (that is a global-memory load per byte).
+constexpr uint64_t pack_lit(const char* s) {
+  uint64_t v = 0;
+  for (int k = 0; s[k] && k < 8; ++k) v |= (uint64_t)(uint8_t)s[k] << (8 * k);
+  return v;
+}
+constexpr int lit_len(const char* s) {
+  int k = 0;
+  while (s[k]) ++k;
+  return k;
+}
+// packed with the LAST char in the lowest byte (for a left-shifting rolling window)
+constexpr uint64_t pack_rev(const char* s) {
+  uint64_t v = 0;
+  int n = lit_len(s);
+  for (int k = 0; k < n; ++k) v = (v << 8) | (uint8_t)s[k];
+  return v;
+}
+QMX_HD uint8_t lit_ch(uint64_t v, int k) { return (uint8_t)(v >> (8 * k)); }
+
 enum EvKind : int { EV_SKIP = 0, EV_CONTENT = 1, EV_ABORT = 2 };
 struct EvResult {
   int kind;
@@ -289,17 +319,18 @@ struct StrScan {
 
 // Scan a JSON string starting at x[p] == '"'.  Validates (control chars, escapes) and
 // computes equality / containment against the fixed ASCII targets on DECODED chars.
-QMX_HD StrScan scan_string(const uint8_t* x, int p, int b, bool want_contains) {
+template <class R>
+QMX_HD StrScan scan_string(const R& x, int p, int b, bool want_contains) {
   StrScan r;
   r.ok = false; r.eq_choices = r.eq_delta = r.eq_content = false;
   r.has_choices = r.has_content = false; r.nonempty = false; r.end = p;
-  const char* T0 = "choices";
-  const char* T1 = "delta";
-  const char* T2 = "content";
+  constexpr uint64_t T0 = pack_lit("choices"), T1 = pack_lit("delta"), T2 = pack_lit("content");
+  constexpr uint64_t R0 = pack_rev("choices"), R2 = pack_rev("content");
+  constexpr uint64_t M56 = (1ull << 56) - 1;
   int k = 0;               // decoded unit index
   bool e0 = true, e1 = true, e2 = true;
-  // rolling window of the last 7 decoded units (ASCII or 0 for non-ASCII)
-  uint8_t win[7] = {0, 0, 0, 0, 0, 0, 0};
+  // rolling window of the last 7 decoded units (ASCII, 0 for non-ASCII), newest in byte 0
+  uint64_t win = 0;
   int i = p + 1;
   while (true) {
     if (i >= b) return r;
@@ -313,7 +344,7 @@ QMX_HD StrScan scan_string(const uint8_t* x, int p, int b, bool want_contains) {
       if (e == 'u') {
         if (i + 5 >= b) return r;
         for (int q = 2; q < 6; ++q) if (hexv(x[i + q]) < 0) return r;
-        uint32_t cp = hex4(x + i + 2);
+        uint32_t cp = hex4(x, i + 2);
         u = cp < 0x80 ? cp : 0x100;
         i += 6;
       } else {
@@ -339,22 +370,14 @@ QMX_HD StrScan scan_string(const uint8_t* x, int p, int b, bool want_contains) {
       u = c;
       ++i;
     }
-    e0 = e0 && k < 7 && u == (uint32_t)T0[k];
-    e1 = e1 && k < 5 && u == (uint32_t)T1[k];
-    e2 = e2 && k < 7 && u == (uint32_t)T2[k];
+    e0 = e0 && k < 7 && u == lit_ch(T0, k);
+    e1 = e1 && k < 5 && u == lit_ch(T1, k);
+    e2 = e2 && k < 7 && u == lit_ch(T2, k);
     ++k;
     if (want_contains) {
-      for (int q = 0; q < 6; ++q) win[q] = win[q + 1];
-      win[6] = u < 0x80 ? (uint8_t)u : 0;
-      if (k >= 7) {
-        bool m0 = true, m2 = true;
-        for (int q = 0; q < 7; ++q) {
-          m0 = m0 && win[q] == (uint8_t)T0[q];
-          m2 = m2 && win[q] == (uint8_t)T2[q];
-        }
-        r.has_choices = r.has_choices || m0;
-        r.has_content = r.has_content || m2;
-      }
+      win = ((win << 8) | (u < 0x80 ? u : 0u)) & M56;
+      r.has_choices = r.has_choices || (k >= 7 && win == R0);
+      r.has_content = r.has_content || (k >= 7 && win == R2);
     }
   }
   r.ok = true;
@@ -372,7 +395,8 @@ struct NumScan {
   int end;
 };
 // Python NUMBER_RE: -?(0|[1-9]\d*)(\.\d+)?([eE][-+]?\d+)?  (+ float underflow to 0.0)
-QMX_HD NumScan scan_number(const uint8_t* x, int p, int b) {
+template <class R>
+QMX_HD NumScan scan_number(const R& x, int p, int b) {
   NumScan r{false, true, p};
   int i = p;
   if (i < b && x[i] == '-') ++i;
@@ -424,26 +448,26 @@ QMX_HD NumScan scan_number(const uint8_t* x, int p, int b) {
   return r;
 }
 
-QMX_HD bool lit_at(const uint8_t* x, int p, int b, const char* lit) {
-  int i = 0;
-  for (; lit[i]; ++i)
-    if (p + i >= b || x[p + i] != (uint8_t)lit[i]) return false;
+template <class R>
+QMX_HD bool lit_at(const R& x, int p, int b, uint64_t lit, int len) {
+  if (p + len > b) return false;
+  for (int i = 0; i < len; ++i)
+    if (x[p + i] != lit_ch(lit, i)) return false;
   return true;
 }
+#define QMX_LIT(s) pack_lit(s), lit_len(s)
 
 QMX_HD bool json_ws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
 
 // Classify one framed SSE event e[0:m) (see reference.classify_event for the contract).
-QMX_HD EvResult classify_event(const uint8_t* e, int m) {
+template <class R>
+QMX_HD EvResult classify_event(const R& e, int m) {
   EvResult res{EV_SKIP, 0, 0};
-  const char* pre = "data: ";
-  if (m < 6) return res;
-  for (int i = 0; i < 6; ++i)
-    if (e[i] != (uint8_t)pre[i]) return res;
+  if (!lit_at(e, 0, m, QMX_LIT("data: "))) return res;
   if (!utf8_valid(e, 0, m)) return res;
   int a = 6, b = m;
   ustrip(e, &a, &b);
-  if (b - a == 6 && lit_at(e, a, b, "[DONE]")) return res;
+  if (b - a == 6 && lit_at(e, a, b, QMX_LIT("[DONE]"))) return res;
 
   // --- parse ---------------------------------------------------------------------
   uint64_t stk[kJsonMaxDepth / 64] = {0, 0, 0, 0};  // bit = container is array
@@ -553,18 +577,18 @@ QMX_HD EvResult classify_event(const uint8_t* e, int m) {
         else if (role == R_CONTENT) { ca = pos + 1; cb = s.end - 1; }
         pos = s.end;
       } else if (c == '-' || (c >= '0' && c <= '9')) {
-        if (c == '-' && lit_at(e, pos, b, "-Infinity")) {
+        if (c == '-' && lit_at(e, pos, b, pack_lit("-Infinit"), 8) && lit_at(e, pos + 8, b, QMX_LIT("y"))) {
           pos += 9; vkind = K_NUM; vtruthy = true;
         } else {
           NumScan ns = scan_number(e, pos, b);
           if (!ns.ok) return res;
           pos = ns.end; vkind = K_NUM; vtruthy = !ns.zero;
         }
-      } else if (lit_at(e, pos, b, "true")) { pos += 4; vkind = K_TRUE; vtruthy = true; }
-      else if (lit_at(e, pos, b, "false")) { pos += 5; vkind = K_FALSE; vtruthy = false; }
-      else if (lit_at(e, pos, b, "null")) { pos += 4; vkind = K_NULL; vtruthy = false; }
-      else if (lit_at(e, pos, b, "NaN")) { pos += 3; vkind = K_NUM; vtruthy = true; }
-      else if (lit_at(e, pos, b, "Infinity")) { pos += 8; vkind = K_NUM; vtruthy = true; }
+      } else if (lit_at(e, pos, b, QMX_LIT("true"))) { pos += 4; vkind = K_TRUE; vtruthy = true; }
+      else if (lit_at(e, pos, b, QMX_LIT("false"))) { pos += 5; vkind = K_FALSE; vtruthy = false; }
+      else if (lit_at(e, pos, b, QMX_LIT("null"))) { pos += 4; vkind = K_NULL; vtruthy = false; }
+      else if (lit_at(e, pos, b, QMX_LIT("NaN"))) { pos += 3; vkind = K_NUM; vtruthy = true; }
+      else if (lit_at(e, pos, b, QMX_LIT("Infinity"))) { pos += 8; vkind = K_NUM; vtruthy = true; }
       else return res;
       if (role == R_ROOT) root_kind = vkind;
       else if (role == R_CHOICES) { ch_kind = vkind; ch_truthy = vtruthy; }
@@ -636,6 +660,20 @@ QMX_HD EvResult classify_event(const uint8_t* e, int m) {
   res.str_a = ca;
   res.str_b = cb;
   return res;
+}
+
+// Reader adaptors: R is a raw pointer on the host; on the device an LDS word reader.
+template <class R>
+struct OffsetReader {
+  const R& r;
+  int off;
+  QMX_HD uint8_t operator[](int i) const { return r[off + i]; }
+};
+// Event at x[e0 : e0+m); string offsets in the result are relative to e0.
+template <class R>
+QMX_HD EvResult classify_event_at(const R& x, int e0, int m) {
+  OffsetReader<R> o{x, e0};
+  return classify_event(o, m);
 }
 
 }  // namespace qmx

@@ -20,7 +20,7 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent.parent
 CSRC = PKG / "csrc"
 BUILD = PKG.parent / "build" / "qmx"
-SOURCES = ["qmx_engine.cpp", "qmx_hip.hip", "bindings.cpp"]
+SOURCES = ["qmx_engine.cpp", "qmx_json.cpp", "qmx_server.cpp", "qmx_hip.hip", "bindings.cpp"]
 ARCH = os.environ.get("QMX_ARCH", "gfx950")
 
 
@@ -79,6 +79,30 @@ def build(debug: bool = False, jobs: int = 3, verbose: bool = False) -> Path:
     return out
 
 
+TOOLS = {"qmx_mock": "mock_backend.cpp", "qmx_loadgen": "loadgen.cpp"}
+BIN = PKG / "bin"
+
+
+def build_tools(verbose: bool = False) -> list:
+    """Host-only C++ tools (mock backend, load generator) -> quorum_amd/bin/."""
+    BIN.mkdir(exist_ok=True)
+    out = []
+    cxx = shutil.which("g++") or shutil.which("c++")
+    for name, src in TOOLS.items():
+        s = PKG / "tools" / "csrc" / src
+        b = BIN / name
+        out.append(b)
+        if b.exists() and b.stat().st_mtime > s.stat().st_mtime:
+            continue
+        cmd = [cxx, "-O2", "-std=c++17", "-pthread", str(s), "-o", str(b)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"tool build failed: {src}\n{r.stderr}")
+    return out
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--debug", action="store_true")
@@ -87,6 +111,8 @@ def main(argv=None) -> int:
     args = ap.parse_args(argv)
     path = build(args.debug, args.jobs, args.verbose)
     print(path)
+    for t in build_tools(args.verbose):
+        print(t)
     return 0
 
 

@@ -1,0 +1,77 @@
+"""Launch the native C++ data plane (quorum_amd/csrc/qmx_server.cpp) from a YAML config.
+
+The YAML is resolved with the same helpers the FastAPI app uses (``quorum_amd.utils.config``)
+so both front-ends share one definition of every default; the C++ server receives a flat,
+fully-resolved dict.  Reference semantics: ``src/quorum/oai_proxy.py:959-1408``.
+"""
+from __future__ import annotations
+
+import os
+from typing import Any, Dict, Optional
+from urllib.parse import urlsplit
+
+from ..utils.config import (RuntimeConfig, is_parallel, load_config, request_timeout, resolve_aggregate,
+                            resolve_flags)
+
+
+class NativeUnsupported(RuntimeError):
+    pass
+
+
+def native_config(cfg: Dict[str, Any], host: str, port: int, engine: str, device: Optional[int],
+                  threads: int) -> Dict[str, Any]:
+    if not isinstance(cfg, dict) or "primary_backends" not in cfg or not isinstance(cfg.get("settings"), dict):
+        raise NativeUnsupported("config lacks primary_backends/settings (quorum would crash at import)")
+    flags = resolve_flags(cfg)
+    agg = resolve_aggregate(cfg)
+    rt = RuntimeConfig.from_config(cfg)
+    backends = []
+    for b in cfg.get("primary_backends") or []:
+        url = b.get("url") or ""
+        parts = urlsplit(url) if url else None
+        https = bool(parts and parts.scheme == "https")
+        if parts and parts.scheme not in ("http", "https"):
+            raise NativeUnsupported(f"backend {b.get('name')!r}: unsupported URL {url!r}")
+        if https:
+            raise NativeUnsupported(f"backend {b.get('name')!r} uses https: run with --impl python")
+        model = b.get("model", "")
+        backends.append({
+            "name": str(b.get("name", "")), "url": url, "model": "" if model is None else str(model),
+            "has_model_key": "model" in b, "valid": bool(url), "https": https,
+            "host": parts.hostname if parts else "", "port": (parts.port or 80) if parts else 80,
+            "path": (parts.path.rstrip("/") if parts else ""),
+        })
+    tags = [str(t) for t in flags.thinking_tags]
+    from ..ops.engine import native_tag_ok
+
+    if not native_tag_ok(tags):
+        raise NativeUnsupported(f"thinking_tags {tags!r} need regex semantics: run with --impl python")
+    if engine == "auto":
+        from ..ops import native
+        engine = "hip" if native.gpu_available() else "cpu"
+    return {
+        "host": host, "port": port, "threads": threads, "engine": engine,
+        "device": int(device if device is not None else os.environ.get("LOCAL_RANK", "0")),
+        "tile": rt.tile_bytes, "max_slots": rt.max_slots, "content_cap": rt.content_cap,
+        "has_iterations_and_strategy": "iterations" in cfg and "strategy" in cfg,
+        "timeout": request_timeout(cfg), "total_timeout": float(rt.total_timeout or 0.0),
+        "separator": str(flags.separator), "hide_intermediate": bool(flags.hide_intermediate_think),
+        "hide_final": bool(flags.hide_final_think), "skip_final": bool(flags.skip_final_aggregation),
+        "suppress": bool(flags.suppress_individual_responses), "tags": tags,
+        "aggregator_name": str(agg.aggregator_backend or ""), "prompt_template": str(agg.prompt_template),
+        "intermediate_separator": str(agg.intermediate_separator), "query_format": str(agg.query_format),
+        "source_label_format": str(agg.source_label_format),
+        "include_original_query": bool(agg.include_original_query),
+        "include_source_names": bool(agg.include_source_names),
+        "env_api_key": os.environ.get("OPENAI_API_KEY", ""),
+        "backends": backends,
+    }
+
+
+def run_native(config: str, host: str, port: int, engine: str, device: Optional[int], threads: int) -> int:
+    from ..ops import native
+
+    ext = native.require()
+    cfg = load_config(config)
+    d = native_config(cfg, host, port, engine, device, threads)
+    return int(ext.run_server(d))

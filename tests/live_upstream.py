@@ -1,0 +1,131 @@
+"""Real-socket fake upstream backends + an in-process native server runner (for tests).
+
+A behaviour is one of
+    ("json", status, payload)          JSON response (content-length)
+    ("text", status, text)             raw body
+    ("stream", status, [chunks...])    chunked transfer, one HTTP chunk per item
+    ("refuse",)                        nothing listening on the port
+"""
+from __future__ import annotations
+
+import contextlib
+import json
+import socket
+import threading
+import time
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from typing import Any, Dict, List
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class _Handler(BaseHTTPRequestHandler):
+    protocol_version = "HTTP/1.1"
+
+    def log_message(self, *a):  # quiet
+        pass
+
+    def do_POST(self):
+        n = int(self.headers.get("content-length", "0"))
+        raw = self.rfile.read(n)
+        try:
+            body = json.loads(raw)
+        except Exception:  # noqa: BLE001
+            body = None
+        srv = self.server
+        srv.owner.calls.append({"host": srv.name, "path": self.path, "headers": {k.lower(): v for k, v in self.headers.items()},
+                                "raw": raw, "body": body})
+        beh = srv.owner.behaviours.get(srv.name)
+        if callable(beh):
+            beh = beh(body)
+        kind = beh[0]
+        if kind == "json":
+            data = json.dumps(beh[2]).encode()
+            self.send_response(beh[1])
+            self.send_header("content-type", "application/json")
+            self.send_header("content-length", str(len(data)))
+            self.end_headers()
+            self.wfile.write(data)
+        elif kind == "text":
+            data = beh[2].encode() if isinstance(beh[2], str) else beh[2]
+            self.send_response(beh[1])
+            self.send_header("content-type", "text/plain")
+            self.send_header("content-length", str(len(data)))
+            self.end_headers()
+            self.wfile.write(data)
+        elif kind == "stream":
+            self.send_response(beh[1])
+            self.send_header("content-type", "text/event-stream")
+            self.send_header("transfer-encoding", "chunked")
+            self.end_headers()
+            for c in beh[2]:
+                self.wfile.write(b"%x\r\n%s\r\n" % (len(c), c))
+                self.wfile.flush()
+            self.wfile.write(b"0\r\n\r\n")
+        self.wfile.flush()
+
+
+class LiveUpstream:
+    def __init__(self):
+        self.behaviours: Dict[str, Any] = {}
+        self.calls: List[Dict[str, Any]] = []
+        self.ports: Dict[str, int] = {}
+        self._servers = []
+
+    def serve(self, name: str, behaviour) -> int:
+        self.behaviours[name] = behaviour
+        if behaviour is not None and not callable(behaviour) and behaviour[0] == "refuse":
+            self.ports[name] = free_port()
+            return self.ports[name]
+        srv = ThreadingHTTPServer(("127.0.0.1", 0), _Handler)
+        srv.daemon_threads = True
+        srv.owner = self
+        srv.name = name
+        t = threading.Thread(target=srv.serve_forever, daemon=True)
+        t.start()
+        self._servers.append(srv)
+        self.ports[name] = srv.server_address[1]
+        return self.ports[name]
+
+    def close(self):
+        for s in self._servers:
+            s.shutdown()
+            s.server_close()
+
+
+@contextlib.contextmanager
+def native_server(cfg: Dict[str, Any], engine: str = "cpu", threads: int = 1, env_key: str = ""):
+    """Run the C++ data plane in-process (background thread) for one config."""
+    import http.client
+    import os
+
+    from quorum_amd.ops import native
+    from quorum_amd.runtime.native_server import native_config
+
+    ext = native.require()
+    port = free_port()
+    d = native_config(cfg, "127.0.0.1", port, engine, 0, threads)
+    d["install_signals"] = False
+    d["env_api_key"] = env_key
+    th = threading.Thread(target=ext.run_server, args=(d,), daemon=True)
+    th.start()
+    t0 = time.time()
+    while time.time() - t0 < 20:
+        try:
+            c = http.client.HTTPConnection("127.0.0.1", port, timeout=1)
+            c.request("GET", "/health")
+            if c.getresponse().status == 200:
+                break
+        except OSError:
+            time.sleep(0.02)
+    try:
+        yield port
+    finally:
+        ext.stop_server()
+        th.join(timeout=10)

@@ -1,0 +1,23 @@
+"""GPU: the native data plane with the CDNA4 HIP engine vs the FastAPI conformance app."""
+import pytest
+
+import test_native_server as T
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", sorted(T.SCENARIOS))
+def test_native_hip_matches_python(name, monkeypatch):
+    monkeypatch.setattr(T, "ENGINE", "hip")
+    T.test_native_matches_python(name)
+
+
+def test_native_hip_keepalive(monkeypatch):
+    import live_upstream as L
+    orig = L.native_server
+
+    def hip_server(cfg, engine="cpu", threads=1, env_key=""):
+        return orig(cfg, engine="hip", threads=threads, env_key=env_key)
+
+    monkeypatch.setattr(T, "native_server", hip_server)
+    T.test_native_keepalive_many_requests()

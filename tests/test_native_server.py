@@ -1,0 +1,264 @@
+"""Differential conformance: native C++ data plane vs the FastAPI conformance app.
+
+Every scenario runs twice — through the FastAPI app (quorum semantics, transport-level fake
+upstream) and through the C++ epoll server (real sockets, live fake upstream) — and the
+client-visible results (status, content type, SSE events / JSON body with timestamps
+normalised) and what the upstreams received must match.
+"""
+import copy
+import json
+import os
+
+import httpx
+import pytest
+
+from quorum_amd.ops import native
+
+from conftest import FakeUpstream, cfg_parallel, completion, make_client, sse_chunk, sse_stream
+from live_upstream import LiveUpstream, native_server
+
+pytestmark = pytest.mark.skipif(not native.available(), reason="native extension not built")
+ENGINE = os.environ.get("QMX_NATIVE_TEST_ENGINE", "cpu")
+
+AUTH = {"Authorization": "Bearer test-key"}
+MSG = [{"role": "user", "content": "What is 2+2?"}]
+CONCAT = {"separator": "\n-------------\n", "hide_intermediate_think": True, "hide_final_think": False,
+          "thinking_tags": ["think", "reason", "reasoning", "thought"], "skip_final_aggregation": False}
+AGG = {"aggregator_backend": "LLM3", "intermediate_separator": "\n\n---\n\n", "include_source_names": True,
+       "source_label_format": "Response from {backend_name}:\n", "prompt_template": "R:\n{responses}\nEnd.",
+       "include_original_query": True}
+THINK = [sse_chunk({"role": "assistant"}), sse_chunk({"content": "<think>"}), sse_chunk({"content": "hmm"}),
+         sse_chunk({"content": "</think>"}), sse_chunk({"content": "The answer "}), sse_chunk({"content": "is 4."}),
+         sse_chunk({}, finish="stop"), b"data: [DONE]\n\n"]
+
+
+def split7(chunks):
+    raw = b"".join(chunks)
+    return [raw[i:i + 7] for i in range(0, len(raw), 7)]
+
+
+SCENARIOS = {
+    "par_stream_concat": (cfg_parallel(2, block=CONCAT),
+                          {"b1.test": ("stream", 200, sse_stream(["Hel", "lo"])),
+                           "b2.test": ("stream", 200, sse_stream(["Wor", "ld"]))},
+                          {"messages": MSG, "stream": True}, AUTH),
+    "par_stream_skip_final": (cfg_parallel(2, block=dict(CONCAT, skip_final_aggregation=True)),
+                              {"b1.test": ("stream", 200, sse_stream(["a é😀\"\\\n"])),
+                               "b2.test": ("stream", 200, sse_stream(["b"]))},
+                              {"messages": MSG, "stream": True}, AUTH),
+    "par_stream_think_split": (cfg_parallel(2, block=dict(CONCAT, hide_final_think=True)),
+                               {"b1.test": ("stream", 200, split7(THINK)), "b2.test": ("stream", 200, THINK)},
+                               {"messages": MSG, "stream": True}, AUTH),
+    "par_stream_suppress": (cfg_parallel(2, block=CONCAT),
+                            {"b1.test": ("stream", 200, sse_stream(["a"])),
+                             "b2.test": ("stream", 200, sse_stream(["b"]))},
+                            {"messages": MSG, "stream": True, "suppress_individual_responses": True}, AUTH),
+    "par_stream_all_fail": (cfg_parallel(2, block=CONCAT),
+                            {"b1.test": ("json", 500, {"error": {"message": "x"}}),
+                             "b2.test": ("json", 503, {"error": {"message": "y"}})},
+                            {"messages": MSG, "stream": True}, AUTH),
+    "par_stream_one_refused": (cfg_parallel(2, block=CONCAT),
+                               {"b1.test": ("refuse",), "b2.test": ("stream", 200, sse_stream(["B"]))},
+                               {"messages": MSG, "stream": True}, AUTH),
+    "par_stream_null_abort": (cfg_parallel(2, block=CONCAT),
+                              {"b1.test": ("stream", 200, [sse_chunk({"content": "alpha "}), sse_chunk({"content": None}),
+                                                            sse_chunk({"content": "beta"}), b"data: [DONE]\n\n"]),
+                               "b2.test": ("stream", 200, sse_stream(["B"]))},
+                              {"messages": MSG, "stream": True}, AUTH),
+    "par_stream_malformed": (cfg_parallel(2, block=CONCAT),
+                             {"b1.test": ("stream", 200, [b"data: {bad}\n\n", b"event: x\n\n", sse_chunk({"content": "ok"}),
+                                                          b"data: [DONE]\n\n"]),
+                              "b2.test": ("stream", 200, sse_stream(["B"]))},
+                             {"messages": MSG, "stream": True}, AUTH),
+    "par_stream_empty_after_strip": (cfg_parallel(2, block=dict(CONCAT, hide_intermediate_think=False,
+                                                                hide_final_think=True)),
+                                     {"b1.test": ("stream", 200, sse_stream(["<think>only</think>"])),
+                                      "b2.test": ("stream", 200, sse_stream(["B"]))},
+                                     {"messages": MSG, "stream": True}, AUTH),
+    "par_stream_aggregate_fallback": (cfg_parallel(3, strategy="aggregate", block=AGG),
+                                      {"b1.test": ("stream", 200, sse_stream(["one"])),
+                                       "b2.test": ("stream", 200, sse_stream(["two"])),
+                                       "b3.test": lambda body: (("stream", 200, sse_stream(["three"]))
+                                                                if body.get("stream") else ("text", 200, "not json"))},
+                                      {"messages": MSG, "stream": True}, AUTH),
+    "par_stream_aggregate_ok": (cfg_parallel(3, strategy="aggregate", block=AGG),
+                                {"b1.test": ("stream", 200, sse_stream(["one"])),
+                                 "b2.test": ("stream", 200, sse_stream(["two"])),
+                                 "b3.test": lambda body: (("stream", 200, sse_stream(["three"]))
+                                                          if body.get("stream") else ("json", 200, completion("SYN")))},
+                                {"messages": MSG, "stream": True}, AUTH),
+    "nonstream_concat_usage": (cfg_parallel(2, block=CONCAT),
+                               {"b1.test": ("json", 200, completion("first", cid="c1", usage=(9, 12, 21))),
+                                "b2.test": ("json", 200, completion("second", cid="c2", usage=(10, 15, 25)))},
+                               {"messages": MSG}, AUTH),
+    "nonstream_strip": (cfg_parallel(2, block=dict(CONCAT, hide_final_think=True)),
+                        {"b1.test": ("json", 200, completion("<think>t</think>The answer is 4.")),
+                         "b2.test": ("json", 200, completion("  <reason>r</reason>4  "))},
+                        {"messages": MSG}, AUTH),
+    "nonstream_partial": (cfg_parallel(2, block=CONCAT),
+                          {"b1.test": ("json", 200, completion("only")), "b2.test": ("text", 502, "bad gateway")},
+                          {"messages": MSG}, AUTH),
+    "nonstream_all_fail": (cfg_parallel(2, block=CONCAT),
+                           {"b1.test": ("text", 503, "overloaded"), "b2.test": ("json", 500, {"error": {"message": "e"}})},
+                           {"messages": MSG}, AUTH),
+    "nonstream_missing_usage": (cfg_parallel(2, block=CONCAT),
+                                {"b1.test": ("json", 200, completion("a", usage=None)),
+                                 "b2.test": ("json", 200, completion("b"))},
+                                {"messages": MSG}, AUTH),
+    "nonstream_aggregate": (cfg_parallel(3, strategy="aggregate", block=AGG),
+                            {"b1.test": ("json", 200, completion("<think>t1</think>R1")),
+                             "b2.test": ("json", 200, completion("R2")),
+                             "b3.test": ("json", 200, completion("SYNTH", cid="agg"))},
+                            {"messages": MSG}, AUTH),
+    "single_nonstream_passthrough": ({"primary_backends": [{"name": "LLM1", "url": "http://b1.test/v1", "model": ""}],
+                                      "settings": {"timeout": 30}},
+                                     {"b1.test": ("json", 200, completion("hi"))},
+                                     {"model": "gpt-4", "messages": MSG}, AUTH),
+    "single_stream": ({"primary_backends": [{"name": "LLM1", "url": "http://b1.test/v1", "model": ""}],
+                       "settings": {"timeout": 30}},
+                      {"b1.test": ("stream", 200, sse_stream(["Hello"]))},
+                      {"model": "gpt-4", "messages": MSG, "stream": True}, AUTH),
+    "single_stream_no_done": ({"primary_backends": [{"name": "LLM1", "url": "http://b1.test/v1", "model": "cfgm"}],
+                               "settings": {"timeout": 30}},
+                              {"b1.test": ("stream", 200, sse_stream(["x", "y"], role=False, done=False))},
+                              {"messages": MSG, "stream": True}, AUTH),
+    "single_stream_fail": ({"primary_backends": [{"name": "LLM1", "url": "http://b1.test/v1", "model": ""}],
+                            "settings": {"timeout": 30}},
+                           {"b1.test": ("json", 502, {"error": {"message": "boom"}})},
+                           {"model": "gpt-4", "messages": MSG, "stream": True}, AUTH),
+    "no_auth": ({"primary_backends": [{"name": "LLM1", "url": "http://b1.test/v1", "model": ""}],
+                 "settings": {"timeout": 30}}, {}, {"model": "gpt-4", "messages": MSG}, {}),
+    "no_model": ({"primary_backends": [{"name": "LLM1", "url": "http://b1.test/v1", "model": ""}],
+                  "settings": {"timeout": 30}}, {}, {"messages": MSG}, AUTH),
+    "model_override": ({"primary_backends": [{"name": "LLM1", "url": "http://b1.test/v1", "model": "cfg-model"}],
+                        "settings": {"timeout": 30}},
+                       {"b1.test": ("json", 200, completion("x"))},
+                       {"model": "gpt-4", "messages": MSG, "temperature": 0.7, "n": 1}, AUTH),
+    "no_valid_backend": ({"primary_backends": [{"name": "a", "url": "", "model": "m"}], "settings": {"timeout": 3}},
+                         {}, {"messages": MSG}, AUTH),
+}
+
+
+def _norm_sse(text):
+    out = []
+    for seg in text.split("\n\n"):
+        if not seg.strip():
+            continue
+        assert seg.startswith("data: "), seg
+        p = seg[6:]
+        if p == "[DONE]":
+            out.append(p)
+            continue
+        ev = json.loads(p)
+        ev["created"] = 0
+        out.append(ev)
+    return out
+
+
+def _normalize(status, ctype, body: bytes):
+    ctype = (ctype or "").split(";")[0]
+    if ctype == "text/event-stream":
+        return status, ctype, _norm_sse(body.decode())
+    try:
+        return status, ctype, json.loads(body)
+    except Exception:  # noqa: BLE001
+        return status, ctype, body
+
+
+def _python_side(cfg, ups, req, hdrs):
+    fu = FakeUpstream()
+    for host, beh in ups.items():
+        def mk(beh=beh):
+            def fn(request, body):
+                b = beh(body) if callable(beh) else beh
+                if b[0] == "json":
+                    return httpx.Response(b[1], json=b[2])
+                if b[0] == "text":
+                    return httpx.Response(b[1], text=b[2])
+                if b[0] == "refuse":
+                    return httpx.ConnectError("All connection attempts failed")
+
+                async def gen():
+                    for c in b[2]:
+                        yield c
+                return httpx.Response(b[1], headers={"content-type": "text/event-stream"}, content=gen())
+            return fn
+        fu.route(host, mk())
+    c = make_client(cfg, fu, engine="python")
+    r = c.post("/chat/completions", json=req, headers=hdrs)
+    return _normalize(r.status_code, r.headers.get("content-type"), r.content), fu.calls
+
+
+def _native_side(cfg, ups, req, hdrs):
+    live = LiveUpstream()
+    cfg = copy.deepcopy(cfg)
+    try:
+        for b in cfg["primary_backends"]:
+            host = b["url"].split("//")[1].split("/")[0] if b["url"] else None
+            if host and host in ups:
+                port = live.serve(host, ups[host])
+                b["url"] = f"http://127.0.0.1:{port}/v1"
+        with native_server(cfg, engine=ENGINE) as port:
+            r = httpx.post(f"http://127.0.0.1:{port}/chat/completions", json=req, headers=hdrs, timeout=30)
+            return _normalize(r.status_code, r.headers.get("content-type"), r.content), live.calls
+    finally:
+        live.close()
+
+
+@pytest.mark.parametrize("name", sorted(SCENARIOS))
+def test_native_matches_python(name):
+    cfg, ups, req, hdrs = SCENARIOS[name]
+    py, py_calls = _python_side(cfg, ups, req, hdrs)
+    nat, nat_calls = _native_side(cfg, ups, req, hdrs)
+    if py[1] == "text/event-stream" and py[0] == 200:
+        # backends interleave differently; compare per-backend streams + the tail
+        def per(evs):
+            d = {}
+            for e in evs:
+                if e != "[DONE]" and e["id"].startswith("chatcmpl-parallel-") and e["id"][-1].isdigit():
+                    d.setdefault(e["id"], []).append(e)
+            return d, [e for e in evs if e == "[DONE]" or not (e["id"].startswith("chatcmpl-parallel-")
+                                                                and e["id"][-1].isdigit())]
+        assert (py[0], py[1]) == (nat[0], nat[1])
+        assert per(py[2]) == per(nat[2]), name
+    else:
+        assert py == nat, name
+    # what the upstreams received (bodies; auth header)
+    refused = {h for h, b in ups.items() if not callable(b) and b[0] == "refuse"}
+
+    def norm_calls(calls, live):
+        out = []
+        for c in calls:
+            if not live and c["host"] in refused:
+                continue  # the transport fake "receives" a request a refused socket never does
+            out.append((c["body"] and json.dumps(c["body"], sort_keys=True), c["headers"].get("authorization")))
+        return sorted(out, key=lambda x: (x[0] or "", x[1] or ""))
+    assert norm_calls(py_calls, False) == norm_calls(nat_calls, True), name
+
+
+def test_native_health_and_metrics():
+    cfg = {"primary_backends": [{"name": "a", "url": "http://127.0.0.1:9/v1", "model": "m"}], "settings": {"timeout": 3}}
+    with native_server(cfg) as port:
+        r = httpx.get(f"http://127.0.0.1:{port}/health")
+        assert r.status_code == 200 and r.json() == {"status": "healthy"}
+        m = httpx.get(f"http://127.0.0.1:{port}/metrics").text
+        assert "qmx_requests_total" in m
+        assert httpx.post(f"http://127.0.0.1:{port}/nope", json={}).status_code == 404
+
+
+def test_native_keepalive_many_requests():
+    live = LiveUpstream()
+    p1 = live.serve("b1", ("stream", 200, sse_stream(["x", "y"])))
+    p2 = live.serve("b2", ("stream", 200, sse_stream(["z"])))
+    cfg = cfg_parallel(2, block=dict(CONCAT, skip_final_aggregation=True))
+    cfg["primary_backends"][0]["url"] = f"http://127.0.0.1:{p1}/v1"
+    cfg["primary_backends"][1]["url"] = f"http://127.0.0.1:{p2}/v1"
+    try:
+        with native_server(cfg) as port:
+            with httpx.Client(base_url=f"http://127.0.0.1:{port}") as cl:
+                for _ in range(30):
+                    r = cl.post("/v1/chat/completions", json={"messages": MSG, "stream": True}, headers=AUTH)
+                    evs = _norm_sse(r.text)
+                    assert evs[-1] == "[DONE]" and len(evs) == 5
+    finally:
+        live.close()

@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Tick-kernel microbenchmark: one tick over N slots of the benchmark's upstream stream shape.
+
+    QMX_STAGE_TIMING=1 python tools/kbench.py [--slots 1,16,256] [--iters 50]
+
+Prints per-configuration host wall time per tick, GPU kernel time and (with
+QMX_STAGE_TIMING=1) the per-stage wall-time split measured in-kernel with s_memrealtime.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def mock_stream(tokens=20, think=True):
+    def ev(delta, finish="null"):
+        return ('data: {"id": "chatcmpl-mock", "object": "chat.completion.chunk", "created": 1700000000, '
+                '"model": "mock", "choices": [{"index": 0, "delta": %s, "finish_reason": %s}]}\n\n'
+                % (delta, finish)).encode()
+    out = [ev('{"role": "assistant", "content": ""}')]
+    if think:
+        out += [ev('{"content": "<thi"}'), ev('{"content": "nk>let me reason about the request"}'),
+                ev('{"content": " carefully before answering</th"}'), ev('{"content": "ink>"}')]
+    words = ["The", " quick", " brown", " fox", " jumps", " over", " the", " lazy", " dog", "."]
+    out += [ev('{"content": "%s"}' % words[i % 10]) for i in range(tokens)]
+    out += [ev("{}", '"stop"'), b"data: [DONE]\n\n"]
+    return b"".join(out)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--slots", default="1,16,64,256,1024")
+    ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--engine", default="hip")
+    args = ap.parse_args()
+    from quorum_amd.ops.native import NativeEngine
+
+    body = mock_stream()
+    tags = ["think", "reason", "reasoning", "thought"]
+    results = []
+    for filt, emit in ((True, True), (False, True), (True, False)):
+        for n in [int(x) for x in args.slots.split(",")]:
+            eng = NativeEngine(args.engine, tags, device=0, max_slots=4096, content_cap=1 << 16)
+            walls = []
+            for it in range(args.iters):
+                slots = [eng.open(i % 8, filt, emit) for i in range(n)]
+                for s in slots:
+                    eng.feed(s, body)
+                    eng.finish(s)
+                t0 = time.perf_counter()
+                res, _ = eng.tick(1700000000)
+                walls.append(time.perf_counter() - t0)
+                assert len(res) == n, (len(res), n)
+                for s in slots:
+                    eng.release(s)
+            st = eng._e.kernel_stats() if args.engine == "hip" else {}
+            walls.sort()
+            rec = {"filter": filt, "emit": emit, "slots": n, "bytes_per_slot": len(body),
+                   "wall_us_p50": round(1e6 * walls[len(walls) // 2], 1),
+                   "wall_us_min": round(1e6 * walls[0], 1)}
+            if st:
+                rec["kernel_us_avg"] = round(1000 * st["kernel_ms"] / max(st["launches"], 1), 1)
+                if st.get("stage_items"):
+                    ni = st["stage_items"]
+                    rec["stage_us_per_item"] = {k: round(v / ni, 2) for k, v in st.items()
+                                                if k.startswith("stage") and k.endswith("_us")}
+                rec["MB_per_s"] = round(n * len(body) / (st["kernel_ms"] / max(st["launches"], 1)) / 1e3, 1)
+            results.append(rec)
+            print(json.dumps(rec), flush=True)
+    return results
+
+
+if __name__ == "__main__":
+    main()
