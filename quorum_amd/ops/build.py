@@ -44,7 +44,30 @@ def _flags(debug: bool):
                         "-fvisibility=hidden"]
 
 
+class _BuildLock:
+    """Inter-process lock so concurrent ranks never race on the in-tree .so/.o files."""
+
+    def __enter__(self):
+        import fcntl
+
+        BUILD.mkdir(parents=True, exist_ok=True)
+        self.f = open(BUILD / ".lock", "w")
+        fcntl.flock(self.f, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *a):
+        import fcntl
+
+        fcntl.flock(self.f, fcntl.LOCK_UN)
+        self.f.close()
+
+
 def build(debug: bool = False, jobs: int = 3, verbose: bool = False) -> Path:
+    with _BuildLock():
+        return _build(debug, jobs, verbose)
+
+
+def _build(debug: bool = False, jobs: int = 3, verbose: bool = False) -> Path:
     cc = hipcc()
     BUILD.mkdir(parents=True, exist_ok=True)
     flags = _flags(debug)
@@ -85,6 +108,11 @@ BIN = PKG / "bin"
 
 def build_tools(verbose: bool = False) -> list:
     """Host-only C++ tools (mock backend, load generator) -> quorum_amd/bin/."""
+    with _BuildLock():
+        return _build_tools(verbose)
+
+
+def _build_tools(verbose: bool = False) -> list:
     BIN.mkdir(exist_ok=True)
     out = []
     cxx = shutil.which("g++") or shutil.which("c++")
