@@ -20,9 +20,12 @@ struct WorkItem {
 struct WorkResult {
   uint32_t consumed, out_len, status, content_len;
 };
+constexpr int kTplBytes = 320;  // per-stream event shape template (qmx_lex.h TPL_*)
 struct DevSlot {
+  alignas(16) uint8_t tpl[kTplBytes];  // prefix at [0, 256), suffix at [256, 320)
   int32_t depth;
   int32_t tail_len;
+  uint16_t tpl_pre, tpl_suf;           // 0: no template yet
   uint8_t tail[kMaxTail];
 };
 
@@ -107,6 +110,7 @@ class HipEngine : public HostEngine {
   size_t dbg_cap_ = 0;
   double stage_us_[16] = {0};
   uint64_t stage_n_ = 0;
+  double clk_cycles_ = 0, clk_us_ = 0;
   hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
 };
 

@@ -21,6 +21,8 @@
 // Semantics: SURVEY §2.7 (reference src/quorum/oai_proxy.py:262-371, 578-673).
 #include "qmx_hip.h"
 
+#include "qmx_lex.h"
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -40,9 +42,10 @@ namespace qmx {
 
 constexpr int BS = 256;
 constexpr int TILE_MAX = 16384;
-constexpr int MAX_EV = 1024;
+constexpr int MAX_EV = 512;  // events per tile (more → WS_MORE requeue); keeps LDS < 80 KiB (2 WG/CU)
 constexpr int MAX_CAND = 1024;
 constexpr int PAD = 16;
+constexpr int TOK_CAP = 1024;  // tokens per wave per round of 64 events
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 
@@ -63,6 +66,7 @@ struct Smem {
   uint16_t wpos[MAX_EV];
   uint32_t epos[MAX_EV];
   uint16_t eidx[MAX_EV];
+  uint16_t ejx[MAX_EV];  // emitted event k -> delta j
   uint16_t cand[MAX_CAND];
   int8_t cand_tok[MAX_CAND];
   uint16_t tok_pos[MAX_CAND];
@@ -72,11 +76,14 @@ struct Smem {
   int32_t chunk_base[BS + 1];
   int32_t scr[16];
   int32_t v[32];
+  alignas(16) uint8_t tpl[TPL_BYTES];  // this stream's event shape template
 };
+static_assert(TPL_BYTES == kTplBytes, "template size");
 
 enum : int {
   V_START = 0, V_NSEP, V_LASTSEP, V_ABORT, V_NEV, V_CONSUMED, V_STATUS, V_NDELTA, V_YLEN, V_NCAND,
-  V_NTOK, V_BAIL, V_DEPTH0, V_TAILLEN, V_NEWTAIL, V_NEWDEPTH, V_WLEN, V_NEMIT, V_ETOT, V_OUTLEN
+  V_NTOK, V_BAIL, V_DEPTH0, V_TAILLEN, V_NEWTAIL, V_NEWDEPTH, V_WLEN, V_NEMIT, V_ETOT, V_OUTLEN,
+  V_TPLPRE, V_TPLSUF, V_TPLK
 };
 
 // LDS byte reader that fetches one aligned 64-bit word per 8 sequential bytes: a byte-serial
@@ -292,9 +299,12 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
                                                       uint8_t* __restrict__ content, KParams Pk) {
   __shared__ Smem s;
   __shared__ KParams P;  // kernel args staged in LDS: lane-divergent pattern/envelope reads
+  __shared__ uint16_t TKP[BS / 64][TOK_CAP];  // per-wave token buffers (positions)
+  __shared__ alignas(8) uint8_t TKT[BS / 64][TOK_CAP];  // token bytes (type | key id | flags)
   const int tid = threadIdx.x;
   for (int i = tid; i < (int)(sizeof(KParams) / 4); i += BS) ((uint32_t*)&P)[i] = ((const uint32_t*)&Pk)[i];
   QMX_STAMP(0);
+  if (Pk.dbg != nullptr && threadIdx.x == 0) Pk.dbg[blockIdx.x * 16 + 11] = __builtin_amdgcn_s_memtime();
   const WorkItem it = items[blockIdx.x];
   const int in_len = (int)it.in_len;
   const bool eof = it.flags & WF_EOF;
@@ -310,14 +320,19 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
     s.v[V_LASTSEP] = -1;
     s.v[V_BAIL] = 0;
     s.v[V_STATUS] = 0;
+    s.v[V_TPLK] = -1;
     if (fresh) {
       s.v[V_DEPTH0] = 0;
       s.v[V_TAILLEN] = 0;
+      s.v[V_TPLPRE] = s.v[V_TPLSUF] = 0;
     } else {
       s.v[V_DEPTH0] = state[it.slot].depth;
       s.v[V_TAILLEN] = state[it.slot].tail_len;
+      s.v[V_TPLPRE] = state[it.slot].tpl_pre;
+      s.v[V_TPLSUF] = state[it.slot].tpl_suf;
     }
   }
+  if (!fresh && tid < TPL_BYTES / 16) ((uint4*)s.tpl)[tid] = ((const uint4*)state[it.slot].tpl)[tid];
   __syncthreads();
   QMX_STAMP(1);
   const int tail_len = filt ? s.v[V_TAILLEN] : 0;
@@ -351,6 +366,7 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
     if (tid == 0 && fresh) {
       state[it.slot].depth = 0;
       state[it.slot].tail_len = 0;
+      state[it.slot].tpl_pre = state[it.slot].tpl_suf = 0;
     }
     if (tid == 0) {
       WorkResult r{(uint32_t)s.v[V_CONSUMED], 0u, (uint32_t)s.v[V_STATUS], it.content_len};
@@ -448,14 +464,71 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
   // ---- S3: per-event extraction (4 consecutive events per thread) --------------------
   int packed_local[4];
   {
-    // event k -> wave (k & 3), lane (k >> 2): consecutive events run on different SIMDs
+    // Rounds of BS events: event k = round*BS + 4*l + w is lexed wave-cooperatively by wave w
+    // (one event after another, 64 bytes per step), then lane l of wave w runs the token
+    // grammar for it.  Token buffers are private to a wave: no barrier between phases.
+    const int w = tid >> 6, lane = tid & 63;
     const LdsWords rd(s.A);
-    for (int k = ((tid & 63) << 2) | (tid >> 6); k < nev; k += BS) {
-      int a = s.ev_a[k], b = s.ev_b[k];
-      EvResult r = classify_event_at(rd, a, b - a);
+    enum { O_SKIP, O_LEXED, O_COMPLEX, O_TPL };
+    const int tp = s.v[V_TPLPRE], ts = s.v[V_TPLSUF];
+    for (int base = 0; base < nev; base += BS) {
+      int my_out = O_SKIP, my_t0 = 0, my_t1 = 0;
+      int ntok = 0;
+      for (int l = 0; l < 64; ++l) {
+        const int k = base + 4 * l + w;
+        if (k >= nev) break;  // wave-uniform
+        const int e0 = s.ev_a[k], e1 = s.ev_b[k];
+        int out = O_SKIP, t0 = ntok, t1 = ntok;
+        if (tp > 0 && e1 - e0 >= tp + ts && wave_tpl_match(s.A, e0, e1, s.tpl, tp, ts) &&
+            wave_str_body(s.A, e0 + tp, e1 - ts)) {
+          out = O_TPL;  // same shape as this stream's last parsed content event
+        } else if (lit_at(s.A, e0, e1, QMX_LIT("data: "))) {
+          int a = e0 + 6, b = e1;
+          ustrip(s.A, &a, &b);
+          if (!(b - a == 6 && lit_at(s.A, a, b, QMX_LIT("[DONE]")))) {
+            const int nt = wave_lex(s.A, a, b, TKP[w], TKT[w], ntok, TOK_CAP);
+            if (nt == -LEX_COMPLEX) {
+              out = O_COMPLEX;
+            } else if (nt >= 0) {
+              out = O_LEXED;
+              t1 = ntok + nt;
+              ntok = t1;
+            }
+          }
+        }
+        if (lane == l) {
+          my_out = out;
+          my_t0 = t0;
+          my_t1 = t1;
+        }
+      }
+      const int k = base + 4 * lane + w;
+      if (k >= nev) continue;
+      const int a = s.ev_a[k], b = s.ev_b[k];
+      EvResult r;
+      r.kind = EV_SKIP;
+      r.str_a = r.str_b = 0;
+      if (my_out == O_TPL) {
+        r.kind = EV_CONTENT;
+        r.str_a = a + tp;
+        r.str_b = b - ts;
+      } else {
+        if (my_out == O_LEXED) {
+          const int g = token_grammar(TKP[w], TKT[w], my_t0, my_t1, r);
+          if (g == LEX_INVALID) r.kind = EV_SKIP;
+          else if (g == LEX_COMPLEX) my_out = O_COMPLEX;
+        }
+        if (my_out == O_COMPLEX) {  // rare shapes: the validating scalar scanner
+          r = classify_event_at(rd, a, b - a);
+          r.str_a += a;
+          r.str_b += a;
+        }
+        if (r.kind == EV_CONTENT && r.str_a - a <= TPL_PRE_MAX && b - r.str_b <= TPL_SUF_MAX)
+          atomicMax(&s.v[V_TPLK], k);  // newest parsed content event becomes the template
+      }
       s.ev_kind[k] = (uint8_t)r.kind;
       if (r.kind == EV_CONTENT) {
-        int sa = a + r.str_a, sb = a + r.str_b;
+        int sa = r.str_a, sb = r.str_b;
         s.ev_sa[k] = (uint16_t)sa;
         s.ev_sb[k] = (uint16_t)sb;
         s.ev_dl[k] = (uint16_t)json_unescape(rd, sa, sb, nullptr);
@@ -465,6 +538,21 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
     }
   }
   __syncthreads();
+  {  // persist the newest template now: S4 reuses the input tile
+    const int tk = s.v[V_TPLK];
+    if (tk >= 0) {
+      const int e0 = s.ev_a[tk], pre = s.ev_sa[tk] - e0, e1 = s.ev_b[tk], suf = e1 - s.ev_sb[tk];
+      DevSlot& ds = state[it.slot];
+      if (tid < pre) ds.tpl[tid] = s.A[e0 + tid];
+      if (tid < suf) ds.tpl[TPL_PRE_MAX + tid] = s.A[e1 - suf + tid];
+      if (tid == 0) {
+        ds.tpl_pre = (uint16_t)pre;
+        ds.tpl_suf = (uint16_t)suf;
+      }
+    } else if (fresh && tid == 0) {
+      state[it.slot].tpl_pre = state[it.slot].tpl_suf = 0;
+    }
+  }
   QMX_STAMP(4);
   const int kab = s.v[V_ABORT];
   {
@@ -675,7 +763,10 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         int j = tid * 4 + i;
-        if (j < ndelta) s.eidx[j] = (uint16_t)(base + pre[i]);
+        if (j < ndelta) {
+          s.eidx[j] = (uint16_t)(base + pre[i]);
+          if (s.wpos[j] > (j ? s.wpos[j - 1] : 0)) s.ejx[base + pre[i]] = (uint16_t)j;
+        }
       }
       n_emit = tot;
     }
@@ -753,26 +844,30 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
     const int C = (Wlen + BS - 1) / BS;
     for (int w0 = 0; w0 < out_len; w0 += WIN) {
       const int w1 = min(w0 + WIN, out_len);
-      // envelopes
-      for (int j = tid; j < ndelta; j += BS) {
-        int wb = j ? s.wpos[j - 1] : 0;
-        if (s.wpos[j] <= wb) continue;
-        int k = s.eidx[j];
-        int es = j ? (int)s.epos[j - 1] : 0;
-        int ee = (int)s.epos[j];
-        int o = k * EVL + es;
-        for (int i = 0; i < P.pre1_len; ++i, ++o)
-          if (o >= w0 && o < w1) O[o - w0] = P.pre1[i];
+      // envelopes: fully parallel over (emitted event, envelope byte)
+      {
         char dg[3];
         int v = it.index;
-        for (int i = ndig - 1; i >= 0; --i) { dg[i] = (char)('0' + v % 10); v /= 10; }
-        for (int i = 0; i < ndig; ++i, ++o)
-          if (o >= w0 && o < w1) O[o - w0] = dg[i];
-        for (int i = 0; i < P.pre2_len; ++i, ++o)
-          if (o >= w0 && o < w1) O[o - w0] = P.pre2[i];
-        o = k * EVL + PRE + ee;
-        for (int i = 0; i < SUF; ++i, ++o)
-          if (o >= w0 && o < w1) O[o - w0] = P.suf[i];
+        for (int i = ndig - 1; i >= 0; --i) {
+          dg[i] = (char)('0' + v % 10);
+          v /= 10;
+        }
+        for (int idx = tid; idx < n_emit * EVL; idx += BS) {
+          int k = idx / EVL, bpos = idx - k * EVL;
+          int j = s.ejx[k];
+          int o;
+          uint8_t ch;
+          if (bpos < PRE) {
+            o = k * EVL + (j ? (int)s.epos[j - 1] : 0) + bpos;
+            ch = bpos < P.pre1_len ? (uint8_t)P.pre1[bpos]
+                 : bpos < P.pre1_len + ndig ? (uint8_t)dg[bpos - P.pre1_len]
+                                            : (uint8_t)P.pre2[bpos - P.pre1_len - ndig];
+          } else {
+            o = k * EVL + PRE + (int)s.epos[j] + (bpos - PRE);
+            ch = (uint8_t)P.suf[bpos - PRE];
+          }
+          if (o >= w0 && o < w1) O[o - w0] = ch;
+        }
       }
       // escaped content
       {
@@ -810,6 +905,7 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
     }
   }
   QMX_STAMP(10);
+  if (Pk.dbg != nullptr && threadIdx.x == 0) Pk.dbg[blockIdx.x * 16 + 12] = __builtin_amdgcn_s_memtime();
   if (tid == 0) {
     WorkResult r{(uint32_t)s.v[V_CONSUMED], (uint32_t)out_len, (uint32_t)s.v[V_STATUS], new_clen};
     res[blockIdx.x] = r;
@@ -839,6 +935,7 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
   HIP_CHECK(hipMalloc(&d_state_, sizeof(DevSlot) * (size_t)max_slots_));
   HIP_CHECK(hipMemset(d_state_, 0, sizeof(DevSlot) * (size_t)max_slots_));
   HIP_CHECK(hipMalloc(&d_content_, (size_t)content_cap_ * (size_t)max_slots_));
+
   ensure_in(8u << 20);
   ensure_out(32u << 20);
   items_cap_ = 4096;
@@ -858,6 +955,7 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
     params_.pat_E[p] = E;
   }
   params_.content_cap = content_cap_;
+
   host_mode_.assign(max_slots_, 0);
   content_len_.assign(max_slots_, 0);
 }
@@ -871,6 +969,7 @@ HipEngine::~HipEngine() {
   if (h_dbg_) hipHostFree(h_dbg_);
   if (d_state_) hipFree(d_state_);
   if (d_content_) hipFree(d_content_);
+
   if (d_scratch_) hipFree(d_scratch_);
   if (ev0_) hipEventDestroy(ev0_);
   if (ev1_) hipEventDestroy(ev1_);
@@ -1026,6 +1125,10 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
     if (params_.dbg) {
       for (int i = 0; i < n; ++i) {
         const unsigned long long* d = h_dbg_ + 16 * i;
+        if (d[12] > d[11] && d[10] > d[0]) {
+          clk_cycles_ += (double)(d[12] - d[11]);
+          clk_us_ += (double)(d[10] - d[0]) * 0.01;
+        }
         int prev = 0;
         for (int k = 1; k < 11; ++k) {
           if (!d[k]) continue;
@@ -1114,6 +1217,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
                                              {"kernel_ms", kernel_ms_}, {"escalations", (double)escalations_},
                                              {"fin_launches", (double)fin_launches_}, {"stage_items", (double)stage_n_}};
   for (int k = 1; k < 11; ++k) m["stage" + std::to_string(k) + "_us"] = stage_us_[k];
+  m["shader_mhz"] = clk_us_ > 0 ? clk_cycles_ / clk_us_ : 0.0;
   return m;
 }
 

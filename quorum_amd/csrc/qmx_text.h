@@ -178,6 +178,7 @@ QMX_HD bool is_cont(uint8_t c) { return (c & 0xC0) == 0x80; }
 // JSON string escaping, json.dumps(ensure_ascii=True) byte-exact
 // ---------------------------------------------------------------------------
 QMX_HD int escaped_len_cp(uint32_t cp) {
+  if (cp >= 0x20 && cp < 0x7F && cp != '"' && cp != '\\') return 1;  // common case first
   if (cp == '"' || cp == '\\' || cp == '\n' || cp == '\r' || cp == '\t' || cp == 0x08 || cp == 0x0C) return 2;
   if (cp >= 0x20 && cp <= 0x7E) return 1;
   if (cp < 0x10000) return 6;
@@ -190,6 +191,10 @@ QMX_HD int write_u4(uint8_t* o, uint32_t u) {
   return 6;
 }
 QMX_HD int escape_cp(uint32_t cp, uint8_t* o) {
+  if (cp >= 0x20 && cp < 0x7F && cp != '"' && cp != '\\') {  // common case first (no switch tree)
+    o[0] = (uint8_t)cp;
+    return 1;
+  }
   switch (cp) {
     case '"': o[0] = '\\'; o[1] = '"'; return 2;
     case '\\': o[0] = '\\'; o[1] = '\\'; return 2;

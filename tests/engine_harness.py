@@ -137,3 +137,25 @@ def run_engine(engine, streams: Sequence[List[bytes]], filt: Sequence[bool], emi
 
 def python_engine(tags):
     return PyEngine(tags)
+
+
+# random JSON documents around quorum's choices[0].delta.content path (classifier fuzzing)
+JSON_ATOMS = ['"choices"', '"delta"', '"content"', '"x"', '""', "0", "0.0", "-0", "1e-400", "1", "true",
+              "false", "null", "NaN", "-Infinity", '"cho\\u0069ces"', '"content here"', '"\\ud800"']
+
+
+def rand_json(rng, depth=0):
+    r = rng.random()
+    if depth == 0 and r < 0.35:
+        inner = rng.choice(JSON_ATOMS + ['"hi <think>x"', '"a\\u00e9\\n"'])
+        delta = rng.choice(['{"content": %s}', '{"role": "assistant", "content": %s}', '{"content": %s, "x": [1]}',
+                            '%s', '{"content": {"a": %s}}']) % inner
+        c0 = rng.choice(['{"delta": %s}', '{"index": 0, "delta": %s, "finish_reason": null}', '[%s]']) % delta
+        return rng.choice(['{"choices": [%s]}', '{"id": "x", "choices": [%s, 1]}', '{"choices": %s}']) % c0
+    if depth > 4 or r < 0.3:
+        return rng.choice(JSON_ATOMS)
+    if r < 0.65:
+        keys = rng.sample(['"choices"', '"delta"', '"content"', '"index"', '"c\\u006fntent"', '"role"'],
+                          rng.randint(0, 3))
+        return "{" + ", ".join(f"{k}: {rand_json(rng, depth + 1)}" for k in keys) + "}"
+    return "[" + ", ".join(rand_json(rng, depth + 1) for _ in range(rng.randint(0, 3))) + "]"

@@ -97,6 +97,64 @@ def test_hip_think_stream_exact(ext):
     eng.release(slot)
 
 
+def test_hip_classify_corpus(ext):
+    """Classifier fuzz through the tick kernel (wave lexer + token grammar + fallback):
+    thousands of random/truncated JSON shapes, 4 events per slot, HIP == C++ CPU engine."""
+    rng = random.Random(4321)
+    events = []
+    for _ in range(6000):
+        js = H.rand_json(rng)
+        if rng.random() < 0.15:
+            js = js[: rng.randint(0, len(js))]
+        events.append(b"data: " + js.encode() + b"\n\n")
+    events += H.ODD_EVENTS + [e for e in H.ABORT_EVENTS]
+    events += [b"data: {\"choices\": [{\"delta\": {\"content\": \"\xff\"}}]}\n\n",
+               b"data: \xc2\xa0{} \xe2\x80\x83\n\n",
+               b"data: {\"choices\": [{\"delta\": {\"content\": \"\xed\xa0\x80\"}}]}\n\n",
+               b"data: {\"choices\": [{\"delta\": {\"content\": \"" + b"\\\\" * 70 + b"\\\"x\"}}]}\n\n",
+               b"data: {\"choices\": [{\"delta\": {\"content\": \"" + "é".encode() * 60 + b"\"}}]}\n\n",
+               b"data: {\"choices\": [{\"delta\": {\"content\": \"" + b"x" * 63 + "é".encode() + b"\"}}]}\n\n",
+               b"data: " + b"[" * 300 + b"]" * 300 + b"\n\n", b"data: " + b"[1," * 1500 + b"1" + b"]" * 1500 + b"\n\n",
+               b"data: {\"choices\": [{\"delta\": {\"content\": \"big\"}}], \"n\": " + b"1" * 200 + b"}\n\n"]
+    streams = [[b"".join(events[i:i + 4])] for i in range(0, len(events), 4)]
+    n = len(streams)
+    c = H.run_engine(NativeEngine("cpu", ["think"]), streams, [True] * n, [True] * n, random.Random(9))
+    g = H.run_engine(_hip(["think"], max_slots=4096), streams, [True] * n, [True] * n, random.Random(9))
+    for i in range(n):
+        assert c[0][i] == g[0][i], streams[i]
+    assert c[1:] == g[1:]
+
+
+TPL_MIDDLES = [b"hello", b"", b"a\\nb", b"q\\\"q", b"\\\\", b"\\\\\\\\", b"x\\", b"\\u00e9", b"\\u00", b"\\ud83d\\ude00",
+               "\u00e9\u4e2d".encode(), b"\xff", b"\xe4\xb8", b'", "content": "override', b'"}, "x": {"y": "',
+               b"tab\there", b"<think>", b"</think>", b"\\/", b"\\q", b"a" * 300, b"\\\\" * 40 + b"\\\"",
+               b"\\" * 63 + b"n", b"e\xcc\x81" * 30]
+
+
+def test_hip_template_path(ext):
+    """Per-stream shape template: events identical outside the content string take the
+    one-compare path; every anomaly in the middle must fall back to the full parse."""
+    shapes = [(b'data: {"id": "c1", "choices": [{"index": 0, "delta": {"content": "', b'"}, "finish_reason": null}]}'),
+              (b'data: {"choices":[{"delta":{"content":"', b'"}}]}  '),
+              (b'data:  {"choices": [{"delta": {"role": "assistant", "content": "', b'", "x": 1}}]}')]
+    rng = random.Random(77)
+    streams = []
+    for sh in range(30):
+        pre, suf = shapes[sh % len(shapes)]
+        evs = [pre + b"warm" + suf + b"\n\n"]
+        for _ in range(40):
+            evs.append(pre + rng.choice(TPL_MIDDLES) + suf + b"\n\n")
+        body = b"".join(evs)
+        streams.append(H.split_random(rng, body, rng.choice([50, 400, 5000])))
+    n = len(streams)
+    tags = ["think"]
+    c = H.run_engine(NativeEngine("cpu", tags), streams, [True] * n, [True] * n, random.Random(3))
+    g = H.run_engine(_hip(tags), streams, [True] * n, [True] * n, random.Random(3))
+    for i in range(n):
+        assert c[0][i] == g[0][i], i
+    assert c[1:] == g[1:]
+
+
 def test_hip_engine_stats(ext):
     eng = _hip(["think"])
     slot = eng.open(0, True, True)

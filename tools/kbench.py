@@ -67,6 +67,7 @@ def main():
                     ni = st["stage_items"]
                     rec["stage_us_per_item"] = {k: round(v / ni, 2) for k, v in st.items()
                                                 if k.startswith("stage") and k.endswith("_us")}
+                rec["shader_mhz"] = round(st.get("shader_mhz", 0), 1)
                 rec["MB_per_s"] = round(n * len(body) / (st["kernel_ms"] / max(st["launches"], 1)) / 1e3, 1)
             results.append(rec)
             print(json.dumps(rec), flush=True)
