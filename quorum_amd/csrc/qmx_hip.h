@@ -44,19 +44,21 @@ struct KParams {
   unsigned long long* dbg;  // optional per-stage stamps [item][16] (QMX_STAGE_TIMING=1)
 };
 
+// Finalize (K3 strip + K4 join + K5 encode) work: one workgroup per session request.
 struct FinItem {
-  uint32_t first_text, n_texts;  // into the FinText array
-  uint32_t out_off, out_cap;
-  uint32_t flags;                // 1 strip, 2 texts-kind
-  uint32_t tok_off, tok_cap;     // global scratch for tokens/intervals
-  uint32_t joiner_off, joiner_len;  // into the input arena
+  uint32_t first_text, n_texts;     // into the FinText array
+  uint32_t flags;                   // 1 strip, 2 texts-kind (no join / encode)
+  uint32_t join_off;                // device join buffer offset (16-B aligned)
+  uint32_t out_off, out_cap;        // device + host output offset (16-B aligned), capacity
+  uint32_t joiner_off, joiner_len;  // in the finalize input arena
+  uint32_t pre_off, pre_len, suf_off, suf_len;
 };
 struct FinText {
   uint32_t slot, len;
 };
 struct FinResult {
-  uint32_t out_len, status, n_kept;  // status: 1 escalate
-  uint32_t text_len[8];              // kind=texts: per-text stripped lengths (first 8)
+  uint32_t out_len, status, n_kept;  // status 1: escalate to the host path
+  uint32_t text_len[8];              // texts-kind: per-text stripped lengths
 };
 
 class HipEngine : public HostEngine {
@@ -73,6 +75,7 @@ class HipEngine : public HostEngine {
 
  private:
   void escalate(int slot, bool fresh);
+  void finalize_host(const FinalizeReq& r, std::vector<FinalizeRes>& out);
   void ensure_in(size_t bytes);
   void ensure_out(size_t bytes);
   void build_params(int64_t created);
@@ -91,21 +94,31 @@ class HipEngine : public HostEngine {
   size_t out_cap_ = 0;
   WorkItem* h_items_ = nullptr;
   WorkResult* h_res_ = nullptr;
-  FinItem* h_fin_ = nullptr;
-  FinText* h_fint_ = nullptr;
-  FinResult* h_finres_ = nullptr;
   size_t items_cap_ = 0;
+  // finalize arenas
+  FinItem* h_fin_ = nullptr;
+  size_t fin_cap_ = 0;
+  FinResult* h_finres_ = nullptr;
+  size_t finres_cap_ = 0;
+  FinText* h_fint_ = nullptr;
+  size_t fint_cap_ = 0;
+  uint8_t* h_fin_in_ = nullptr;
+  size_t fin_in_cap_ = 0;
+  uint8_t* h_fout_ = nullptr;
+  size_t fout_cap_ = 0;
+  uint8_t* d_join_ = nullptr;
+  size_t join_cap_ = 0;
+  uint8_t* d_fout_ = nullptr;
+  size_t dfout_cap_ = 0;
   // device-resident
   DevSlot* d_state_ = nullptr;
   uint8_t* d_content_ = nullptr;
-  uint32_t* d_scratch_ = nullptr;
-  size_t scratch_words_ = 0;
   // host mirrors
   std::vector<uint8_t> host_mode_;       // slot escalated to the host path
   std::vector<uint32_t> content_len_;    // device content bytes per slot
   // stats
-  uint64_t launches_ = 0, items_ = 0, escalations_ = 0, fin_launches_ = 0;
-  double kernel_ms_ = 0.0;
+  uint64_t launches_ = 0, items_ = 0, escalations_ = 0, fin_launches_ = 0, fin_items_ = 0, fin_host_ = 0;
+  double kernel_ms_ = 0.0, fin_ms_ = 0.0;
   unsigned long long* h_dbg_ = nullptr;
   size_t dbg_cap_ = 0;
   double stage_us_[16] = {0};

@@ -913,6 +913,207 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
 }
 
 // ------------------------------------------------------------------------------------
+// the finalize kernel: K3 think_strip_final + K4 join_pack + K5 sse_encode, one workgroup
+// per session request, texts read straight from the HBM-resident content arena
+// (reference oai_proxy.py:120-139 strip, :834-860 join + final event)
+// ------------------------------------------------------------------------------------
+constexpr int FIN_TOK_MAX = 4096;  // tag tokens per text staged in LDS (more → host path)
+constexpr int FIN_SEG_MAX = FIN_TOK_MAX / 2 + 2;
+
+struct FinSmem {
+  int32_t tpos[FIN_TOK_MAX];
+  int8_t tkid[FIN_TOK_MAX];  // +(t+1) open, -(t+1) close
+  uint8_t tlen[FIN_TOK_MAX];
+  int32_t seg_a[FIN_SEG_MAX], seg_b[FIN_SEG_MAX], seg_o[FIN_SEG_MAX + 1];
+  int32_t scr[16];
+  int32_t v[4];
+};
+
+__global__ __launch_bounds__(BS) void qmx_finalize_kernel(const FinItem* __restrict__ items,
+                                                          const FinText* __restrict__ texts,
+                                                          const uint8_t* __restrict__ fin_in,
+                                                          const uint8_t* __restrict__ content, uint32_t content_cap,
+                                                          uint8_t* __restrict__ join_buf, uint8_t* __restrict__ out_dev,
+                                                          uint8_t* __restrict__ out_host, FinResult* __restrict__ res,
+                                                          TagSet ts) {
+  __shared__ FinSmem f;
+  const int tid = threadIdx.x;
+  const FinItem it = items[blockIdx.x];
+  const bool strip = it.flags & 1, as_texts = it.flags & 2;
+  uint8_t* J = join_buf + it.join_off;
+  int jl = 0, nk = 0;
+  uint32_t tlens[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  auto bail = [&]() {
+    if (tid == 0) {
+      FinResult r;
+      r.out_len = 0;
+      r.status = 1;
+      r.n_kept = 0;
+      res[blockIdx.x] = r;
+    }
+  };
+  for (uint32_t i = 0; i < it.n_texts; ++i) {
+    const FinText ft = texts[it.first_text + i];
+    const int n = (int)ft.len;
+    if (n == 0) continue;  // empty texts are not kept (nor joined)
+    if (as_texts && nk >= 8) {
+      bail();
+      return;
+    }
+    const uint8_t* src = content + (size_t)ft.slot * content_cap;
+    if (nk > 0 && !as_texts) {
+      for (uint32_t k = tid; k < it.joiner_len; k += BS) J[jl + k] = fin_in[it.joiner_off + k];
+      jl += (int)it.joiner_len;
+    }
+    if (strip) {
+      // K3a: tag tokens (contiguous byte range per thread, compacted in order)
+      const int C = (n + BS - 1) / BS;
+      const int lo = min(tid * C, n), hi = min(lo + C, n);
+      int cnt = 0;
+      for (int p = lo; p < hi; ++p) {
+        if (src[p] != '<') continue;
+        int L = 0;
+        cnt += match_at(src, n, p, ts, &L) != 0;
+      }
+      int tot;
+      int k = block_excl_sum(cnt, f.scr, &tot);
+      if (tot > FIN_TOK_MAX) {
+        bail();
+        return;
+      }
+      for (int p = lo; p < hi && cnt > 0; ++p) {
+        if (src[p] != '<') continue;
+        int L = 0;
+        const int id = match_at(src, n, p, ts, &L);
+        if (id == 0) continue;
+        f.tpos[k] = p;
+        f.tkid[k] = (int8_t)id;
+        f.tlen[k] = (uint8_t)L;
+        ++k;
+      }
+      __syncthreads();
+      // K3b: leftmost-first, non-greedy, same-tag intervals (regex <(t)>.*?</\1>), then
+      // str.strip() across the kept segments.  Per-tag close pointers only move forward.
+      if (tid == 0) {
+        int cp[kMaxTags];
+        for (int t = 0; t < kMaxTags; ++t) cp[t] = 0;
+        int pos = 0, ns = 0;
+        for (int q = 0; q < tot; ++q) {
+          const int id = f.tkid[q];
+          if (id <= 0 || f.tpos[q] < pos) continue;
+          int j = max(cp[id - 1], q + 1);
+          while (j < tot && f.tkid[j] != -id) ++j;
+          cp[id - 1] = j;
+          if (j >= tot) continue;
+          f.seg_a[ns] = pos;
+          f.seg_b[ns] = f.tpos[q];
+          ++ns;
+          pos = f.tpos[j] + f.tlen[j];
+          q = j;
+        }
+        f.seg_a[ns] = pos;
+        f.seg_b[ns] = n;
+        ++ns;
+        int s0 = 0;
+        for (; s0 < ns; ++s0) {
+          while (f.seg_a[s0] < f.seg_b[s0]) {
+            const int w = ws_at(src, f.seg_a[s0], f.seg_b[s0]);
+            if (w <= 0) break;
+            f.seg_a[s0] += w;
+          }
+          if (f.seg_a[s0] < f.seg_b[s0]) break;
+        }
+        int s1 = ns - 1;
+        for (; s1 >= s0; --s1) {
+          while (f.seg_b[s1] > f.seg_a[s1]) {
+            const int w = ws_before(src, f.seg_a[s1], f.seg_b[s1]);
+            if (w <= 0) break;
+            f.seg_b[s1] -= w;
+          }
+          if (f.seg_b[s1] > f.seg_a[s1]) break;
+        }
+        int m = 0, off = 0;
+        for (int q = s0; q <= s1; ++q) {
+          f.seg_a[m] = f.seg_a[q];
+          f.seg_b[m] = f.seg_b[q];
+          f.seg_o[m] = off;
+          off += f.seg_b[q] - f.seg_a[q];
+          ++m;
+        }
+        f.seg_o[m] = off;
+        f.v[0] = m;
+      }
+    } else if (tid == 0) {
+      f.seg_a[0] = 0;
+      f.seg_b[0] = n;
+      f.seg_o[0] = 0;
+      f.seg_o[1] = n;
+      f.v[0] = 1;
+    }
+    __syncthreads();
+    // K4: copy the kept segments into the join buffer
+    const int nseg = f.v[0];
+    for (int q = 0; q < nseg; ++q) {
+      const int a = f.seg_a[q], len = f.seg_b[q] - a, o = jl + f.seg_o[q];
+      for (int x = tid; x < len; x += BS) J[o + x] = src[a + x];
+    }
+    const int tl = f.seg_o[nseg];
+    if (as_texts) tlens[nk] = (uint32_t)tl;
+    jl += tl;
+    ++nk;
+    __syncthreads();  // LDS token/segment arrays are reused by the next text
+  }
+  __syncthreads();
+  uint8_t* O = out_dev + it.out_off;
+  int out_len = 0;
+  const uint8_t* src_out = J;
+  if (as_texts) {
+    out_len = jl;
+  } else if (nk > 0) {
+    // K5: ensure_ascii JSON escape of the joined text inside the final-event envelope
+    for (uint32_t k = tid; k < it.pre_len; k += BS) O[k] = fin_in[it.pre_off + k];
+    const int C = (jl + BS - 1) / BS;
+    int lo = min(tid * C, jl), hi = min(lo + C, jl);
+    while (lo < jl && is_cont(J[lo])) ++lo;  // code points starting in [lo, hi): both bounds
+    while (hi < jl && is_cont(J[hi])) ++hi;  // move to the next code-point start
+    hi = max(hi, lo);
+    int el = 0;
+    for (int p = lo; p < hi;) {
+      uint32_t cpv;
+      p += wtf8_decode(J, p, jl, &cpv);
+      el += escaped_len_cp(cpv);
+    }
+    int tot;
+    int o = (int)it.pre_len + block_excl_sum(el, f.scr, &tot);
+    out_len = (int)it.pre_len + tot + (int)it.suf_len;
+    if ((uint32_t)out_len > it.out_cap) {
+      bail();
+      return;
+    }
+    for (int p = lo; p < hi;) {
+      uint32_t cpv;
+      p += wtf8_decode(J, p, jl, &cpv);
+      o += escape_cp(cpv, O + o);
+    }
+    for (uint32_t k = tid; k < it.suf_len; k += BS) O[it.pre_len + tot + k] = fin_in[it.suf_off + k];
+    src_out = O;
+  }
+  __syncthreads();
+  // coalesced 16-B stores into the host-mapped output arena
+  uint4* dst = (uint4*)(out_host + it.out_off);
+  const uint4* sv = (const uint4*)src_out;
+  for (int k = tid; k * 16 < out_len; k += BS) dst[k] = sv[k];
+  if (tid == 0) {
+    FinResult r;
+    r.out_len = (uint32_t)out_len;
+    r.status = 0;
+    r.n_kept = (uint32_t)nk;
+    for (int q = 0; q < 8; ++q) r.text_len[q] = tlens[q];
+    res[blockIdx.x] = r;
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // HipEngine host runtime
 // ------------------------------------------------------------------------------------
 static void put(char* dst, int cap, int* len, const std::string& s) {
@@ -970,7 +1171,13 @@ HipEngine::~HipEngine() {
   if (d_state_) hipFree(d_state_);
   if (d_content_) hipFree(d_content_);
 
-  if (d_scratch_) hipFree(d_scratch_);
+  if (h_fin_) hipHostFree(h_fin_);
+  if (h_finres_) hipHostFree(h_finres_);
+  if (h_fint_) hipHostFree(h_fint_);
+  if (h_fin_in_) hipHostFree(h_fin_in_);
+  if (h_fout_) hipHostFree(h_fout_);
+  if (d_join_) hipFree(d_join_);
+  if (d_fout_) hipFree(d_fout_);
   if (ev0_) hipEventDestroy(ev0_);
   if (ev1_) hipEventDestroy(ev1_);
   if (stream_) hipStreamDestroy(stream_);
@@ -1201,21 +1408,135 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
   }
 }
 
+void HipEngine::finalize_host(const FinalizeReq& r, std::vector<FinalizeRes>& out) {
+  std::vector<std::string> texts;
+  for (int s : r.slots) texts.push_back(text(s));
+  FinalizeRes fr;
+  finalize_texts(ts_, texts, r, fr);
+  out.push_back(std::move(fr));
+  ++fin_host_;
+}
+
+template <class T>
+static void grow_mapped(T** p, size_t* cap, size_t need) {
+  if (need <= *cap) return;
+  if (*p) HIP_CHECK(hipHostFree(*p));
+  *cap = std::max(need, *cap * 2);
+  HIP_CHECK(hipHostMalloc((void**)p, sizeof(T) * *cap + 64, hipHostMallocMapped));
+}
+static void grow_device(uint8_t** p, size_t* cap, size_t need) {
+  if (need <= *cap) return;
+  if (*p) HIP_CHECK(hipFree(*p));
+  *cap = std::max(need, *cap * 2);
+  HIP_CHECK(hipMalloc((void**)p, *cap + 64));
+}
+
 void HipEngine::finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out) {
-  // v1: texts gathered from HBM, strip/join/encode on the host library
+  // Sessions whose texts are all HBM-resident run on the GPU (K3+K4+K5); a session with an
+  // escalated (host-path) stream, or > 8 texts in texts-kind, is finalized on the host.
+  std::vector<const FinalizeReq*> gpu;
+  size_t ntext = 0, in_bytes = 0;
   for (auto& r : reqs) {
-    std::vector<std::string> texts;
-    for (int s : r.slots) texts.push_back(text(s));
-    FinalizeRes fr;
-    finalize_texts(ts_, texts, r, fr);
-    out.push_back(std::move(fr));
+    bool dev = !(r.texts && r.slots.size() > 8);
+    for (int s : r.slots) dev = dev && s >= 0 && s < max_slots_ && s < (int)core_.size() && !host_mode_[s];
+    if (!dev) {
+      finalize_host(r, out);
+      continue;
+    }
+    gpu.push_back(&r);
+    ntext += r.slots.size();
+    in_bytes += ((r.joiner.size() + 15) & ~(size_t)15) + 256 + 64;
+  }
+  if (gpu.empty()) return;
+  const int n = (int)gpu.size();
+  grow_mapped(&h_fin_, &fin_cap_, (size_t)n);
+  grow_mapped(&h_finres_, &finres_cap_, (size_t)n);
+  grow_mapped(&h_fint_, &fint_cap_, ntext);
+  grow_mapped(&h_fin_in_, &fin_in_cap_, in_bytes);
+  size_t join_off = 0, out_off = 0, in_off = 0, t_off = 0;
+  const std::string suf = kFinalSuffix;
+  std::vector<size_t> caps(n);
+  for (int i = 0; i < n; ++i) {
+    const FinalizeReq& r = *gpu[i];
+    FinItem& it = h_fin_[i];
+    size_t total = 0;
+    it.first_text = (uint32_t)t_off;
+    it.n_texts = (uint32_t)r.slots.size();
+    for (int s : r.slots) {
+      const uint32_t len = core_[s].aborted ? 0u : content_len_[s];
+      h_fint_[t_off++] = FinText{(uint32_t)s, len};
+      total += len;
+    }
+    if (r.slots.size() > 1) total += (r.slots.size() - 1) * r.joiner.size();
+    const std::string pre = r.texts ? std::string() : final_prefix(r.created);
+    it.flags = (r.strip ? 1u : 0u) | (r.texts ? 2u : 0u);
+    it.joiner_off = (uint32_t)in_off;
+    it.joiner_len = (uint32_t)r.joiner.size();
+    std::memcpy(h_fin_in_ + in_off, r.joiner.data(), r.joiner.size());
+    in_off += (r.joiner.size() + 15) & ~(size_t)15;
+    it.pre_off = (uint32_t)in_off;
+    it.pre_len = (uint32_t)pre.size();
+    std::memcpy(h_fin_in_ + in_off, pre.data(), pre.size());
+    in_off += (pre.size() + 15) & ~(size_t)15;
+    it.suf_off = (uint32_t)in_off;
+    it.suf_len = (uint32_t)suf.size();
+    std::memcpy(h_fin_in_ + in_off, suf.data(), suf.size());
+    in_off += (suf.size() + 15) & ~(size_t)15;
+    it.join_off = (uint32_t)join_off;
+    join_off += (total + 15) & ~(size_t)15;
+    const size_t cap = r.texts ? total : 6 * total + pre.size() + suf.size();
+    it.out_off = (uint32_t)out_off;
+    it.out_cap = (uint32_t)cap;
+    caps[i] = cap;
+    out_off += (cap + 15) & ~(size_t)15;
+  }
+  grow_device(&d_join_, &join_cap_, join_off + 16);
+  grow_device(&d_fout_, &dfout_cap_, out_off + 16);
+  grow_mapped(&h_fout_, &fout_cap_, out_off + 16);
+  HIP_CHECK(hipEventRecord(ev0_, stream_));
+  hipLaunchKernelGGL(qmx_finalize_kernel, dim3(n), dim3(BS), 0, stream_, h_fin_, h_fint_, h_fin_in_, d_content_,
+                     content_cap_, d_join_, d_fout_, h_fout_, h_finres_, ts_);
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipEventRecord(ev1_, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, ev0_, ev1_);
+  fin_ms_ += ms;
+  ++fin_launches_;
+  fin_items_ += n;
+  for (int i = 0; i < n; ++i) {
+    const FinalizeReq& r = *gpu[i];
+    const FinResult fr = h_finres_[i];
+    if (fr.status) {
+      finalize_host(r, out);
+      continue;
+    }
+    FinalizeRes res;
+    res.id = r.id;
+    const char* base = (const char*)h_fout_ + h_fin_[i].out_off;
+    if (r.texts) {
+      res.kind = 2;
+      size_t o = 0;
+      for (uint32_t k = 0; k < fr.n_kept; ++k) {
+        res.texts.emplace_back(base + o, fr.text_len[k]);
+        o += fr.text_len[k];
+      }
+    } else if (fr.n_kept == 0) {
+      res.kind = 0;
+    } else {
+      res.kind = 1;
+      res.event.assign(base, fr.out_len);
+    }
+    out.push_back(std::move(res));
   }
 }
 
 std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   std::unordered_map<std::string, double> m{{"launches", (double)launches_}, {"items", (double)items_},
                                              {"kernel_ms", kernel_ms_}, {"escalations", (double)escalations_},
-                                             {"fin_launches", (double)fin_launches_}, {"stage_items", (double)stage_n_}};
+                                             {"fin_launches", (double)fin_launches_}, {"stage_items", (double)stage_n_},
+                                             {"fin_items", (double)fin_items_}, {"fin_host", (double)fin_host_},
+                                             {"fin_ms", fin_ms_}};
   for (int k = 1; k < 11; ++k) m["stage" + std::to_string(k) + "_us"] = stage_us_[k];
   m["shader_mhz"] = clk_us_ > 0 ? clk_cycles_ / clk_us_ : 0.0;
   return m;

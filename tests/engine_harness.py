@@ -35,7 +35,11 @@ def event_bytes(rng: random.Random, content) -> bytes:
     s = json.dumps(ev, ensure_ascii=rng.random() < 0.5)
     if rng.random() < 0.1:
         s = s.replace(", ", ",").replace(": ", ":")
-    return b"data: " + s.encode() + b"\n\n"
+    try:
+        b = s.encode()
+    except UnicodeEncodeError:  # lone surrogate: only the escaped form is valid UTF-8
+        b = json.dumps(ev).encode()
+    return b"data: " + b + b"\n\n"
 
 
 ODD_EVENTS = [

@@ -155,6 +155,41 @@ def test_hip_template_path(ext):
     assert c[1:] == g[1:]
 
 
+FIN_PIECES = ["<think>", "</think>", "<THINK>", "</Think>", "<reason>", "</reason>", "<reasoning>", "</reasoning>",
+              "<thought>", "</thought>", "<thi", "nk>", "x", " ", "\n", "\u3000", "\u00a0", "\u2003", "\u0085",
+              "\u00e9", "\u4e2d", "\U0001f600", "\ud83d", "\"", "\\", "\t", "\x01", "<", ">", "/", "</"]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_hip_finalize_kernel_matches_cpu(ext, seed):
+    """K3 strip + K4 join + K5 encode on the GPU vs the C++ host algorithms (both
+    finalize kinds), over unfiltered texts full of tags, Unicode whitespace and escapes."""
+    rng = random.Random(500 + seed)
+    tags = ["think", "reason", "reasoning", "thought"]
+    n = rng.choice([1, 2, 3, 8, 9])
+    streams = []
+    for _ in range(n):
+        body = b""
+        for _ in range(rng.randint(0, 12)):
+            txt = "".join(rng.choice(FIN_PIECES) for _ in range(rng.randint(1, 30)))
+            body += H.event_bytes(rng, txt)
+        streams.append([body] if body else [])
+    big = "".join(rng.choice(FIN_PIECES) for _ in range(1200))  # ~5 KB text, hundreds of tokens
+    streams.append([H.event_bytes(rng, big)])
+    m = len(streams)
+    filt = [False] * m  # keep tags in the content so the final strip has work
+    for strip in (True, False):
+        for joiner in ("\n---\n", "", "\u00e9|"):
+            c = H.run_engine(NativeEngine("cpu", tags), streams, filt, [True] * m, random.Random(1),
+                             strip_final=strip, joiner=joiner)
+            eng = _hip(tags)
+            g = H.run_engine(eng, streams, filt, [True] * m, random.Random(1), strip_final=strip, joiner=joiner)
+            assert c[1] == g[1], (strip, joiner)
+            assert c[2] == g[2], (strip, joiner)
+    st = eng._e.kernel_stats()
+    assert st["fin_items"] >= 1, st  # the GPU path ran (texts-kind with 9+ texts falls back)
+
+
 def test_hip_engine_stats(ext):
     eng = _hip(["think"])
     slot = eng.open(0, True, True)
