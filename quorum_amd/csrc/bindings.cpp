@@ -6,6 +6,7 @@
 #include "qmx_engine.h"
 #include "qmx_hip.h"
 #include "qmx_json.h"
+#include "qmx_exchange.h"
 #include "qmx_server.h"
 
 namespace py = pybind11;
@@ -92,6 +93,9 @@ ServerCfg server_cfg_from(const py::dict& d) {
   gs("source_label_format", c.source_label_format); gb("include_original_query", c.include_original_query);
   gb("include_source_names", c.include_source_names); gs("env_api_key", c.env_api_key);
   gb("install_signals", c.install_signals);
+  gi("rank", c.rank); gi("world", c.world); gs("placement", c.placement); gs("xchg", c.xchg);
+  gs("xchg_addr", c.xchg_addr); gi("xchg_port", c.xchg_port); gs("xchg_id_file", c.xchg_id_file);
+  gi("xchg_round_us", c.xchg_round_us); gd("xchg_timeout", c.xchg_timeout);
   if (d.contains("backends")) {
     for (auto item : py::cast<py::list>(d["backends"])) {
       py::dict b = py::cast<py::dict>(item);
@@ -133,6 +137,7 @@ PYBIND11_MODULE(_qmx, m) {
     return run_server(c);
   });
   m.def("server_counters", &server_counters);
+  m.def("rccl_unique_id", &rccl_unique_id_hex);
   m.def("stop_server", &stop_server);
   m.def("json_roundtrip", [](const py::bytes& b) -> py::object {
     std::string s(b), err;

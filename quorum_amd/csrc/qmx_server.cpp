@@ -21,7 +21,10 @@
 #include <mutex>
 #include <thread>
 
+#include <map>
+
 #include "qmx_engine.h"
+#include "qmx_exchange.h"
 #include "qmx_hip.h"
 #include "qmx_json.h"
 
@@ -30,7 +33,7 @@ namespace {
 
 std::atomic<bool> g_stop{false};
 std::atomic<uint64_t> c_requests{0}, c_stream{0}, c_nonstream{0}, c_errors{0}, c_up_fail{0}, c_ticks{0},
-    c_tick_slots{0}, c_up_conns{0}, c_clients{0};
+    c_tick_slots{0}, c_up_conns{0}, c_clients{0}, c_remote_streams{0};
 
 using Clock = std::chrono::steady_clock;
 inline double now_s() { return std::chrono::duration<double>(Clock::now().time_since_epoch()).count(); }
@@ -233,6 +236,9 @@ struct Up {
 struct BState {
   int backend = -1;
   int slot = -1;
+  int remote = -1;        // spread placement: rank running this stream (-1 = local)
+  bool has_text = false;  // per-stream final text (spread sessions)
+  std::string ftext;
   Up* up = nullptr;
   int state = 0;  // 0 running, 1 done, 2 failed
   int status = 0;
@@ -244,7 +250,7 @@ struct BState {
   std::vector<std::pair<std::string, std::string>> rheaders;
 };
 
-enum SKind { K_PAR, K_SINGLE, K_NONSTREAM };
+enum SKind { K_PAR, K_SINGLE, K_NONSTREAM, K_REMOTE };  // K_REMOTE: worker side of a spread stream
 struct Session {
   Client* cl = nullptr;
   SKind kind = K_PAR;
@@ -266,6 +272,11 @@ struct Session {
   std::string done_tail;
   std::string role_model_json;
   double t0 = 0;
+  // spread placement
+  uint64_t skey = 0;  // owner: key under which workers address this session
+  int remote_n = 0, fin_pending = 0;
+  int owner_rank = -1, owner_loop = 0, shadow_bi = 0;  // worker (K_REMOTE)
+  uint64_t owner_skey = 0;
 };
 
 struct ResultBatch {
@@ -278,7 +289,18 @@ struct ResultBatch {
 // --------------------------------------------------------------------------------------
 class Loop {
  public:
-  Loop(const ServerCfg& cfg, int idx) : cfg_(cfg), idx_(idx) {}
+  Loop(const ServerCfg& cfg, int idx) : cfg_(cfg), idx_(idx) { xfd_ = eventfd(0, EFD_NONBLOCK); }
+  void attach_exchange(Exchange* x) { xch_ = x; }
+  // exchange thread → this loop (thread-safe)
+  void x_deliver(std::vector<XMsg>&& v) {
+    {
+      std::lock_guard<std::mutex> g(xmu_);
+      for (auto& m : v) xin_.push_back(std::move(m));
+    }
+    uint64_t one = 1;
+    ssize_t w = write(xfd_, &one, 8);
+    (void)w;
+  }
   ~Loop() {
     stop_gpu_ = true;
     cv_.notify_all();
@@ -333,6 +355,7 @@ class Loop {
     add(lfd_, EPOLLIN, tag_listen());
     evfd_ = eventfd(0, EFD_NONBLOCK);
     add(evfd_, EPOLLIN, tag_event());
+    add(xfd_, EPOLLIN, tag(5, 0));
     idle_.resize(cfg_.backends.size());
     if (cfg_.engine == "hip") {
       eng_.reset(new HipEngine(cfg_.tags, cfg_.device, cfg_.tile, cfg_.max_slots, cfg_.content_cap));
@@ -366,6 +389,7 @@ class Loop {
     int fd = (int)(uint32_t)e.data.u64;
     if (kind == 1) return on_accept();
     if (kind == 2) return on_results();
+    if (kind == 5) return on_xmsgs();
     if (kind == 3) {
       auto it = clients_.find(fd);
       if (it != clients_.end()) on_client(it->second.get(), e.events);
@@ -427,7 +451,10 @@ class Loop {
       if (it == slot_owner_.end()) continue;
       Session* s = it->second.first;
       int bi = it->second.second;
-      if (!r.sse.empty() && s->cl) send_chunk(s, r.sse);
+      if (!r.sse.empty()) {
+        if (s->kind == K_REMOTE) post_owner(s, X_DATA, 0, 0, r.sse);
+        else if (s->cl) send_chunk(s, r.sse);
+      }
       if ((r.flags & (RF_DONE | RF_ABORTED)) && s->bs[bi].state == 0) {
         s->bs[bi].state = 1;
         s->bs[bi].aborted = (r.flags & RF_ABORTED) != 0;
@@ -438,9 +465,11 @@ class Loop {
     for (auto& f : rb.f) {
       auto it = fin_owner_.find(f.id);
       if (it == fin_owner_.end()) continue;
-      Session* s = it->second;
+      Session* s = it->second.first;
+      const int bi = it->second.second;
       fin_owner_.erase(it);
-      on_finalized(s, f);
+      if (s->fin_id == f.id) s->fin_id = -1;
+      on_finalized(s, f, bi);
     }
   }
   void kick() { kick_ = true; }
@@ -987,6 +1016,11 @@ class Loop {
     if (bi < 0) return on_aggregator_done(s, 500, std::string());
     BState& b = s->bs[bi];
     if (b.state != 0) return;
+    if (s->kind == K_REMOTE) {
+      b.state = 2;
+      post_owner(s, X_FINAL, XF_FAILED, status, have_result ? error_message(b) : msg);
+      return end_session(s);
+    }
     if (!have_result) {
       b.status = status;
       JVal e;
@@ -1032,8 +1066,21 @@ class Loop {
     send_chunk(s, chunk_event_json("chatcmpl-parallel", (int64_t)time(nullptr), "\"parallel-proxy\"",
                                    "{\"role\": \"assistant\"}", "null"));
     s->bs.resize(valid.size());
+    // spread placement (EP analog): backend i of a session owned by rank r runs on rank
+    // (r + i) % world; its deltas and final text come back through the exchange (R1)
+    const bool spread = xch_ && xch_->healthy() && xch_->world() > 1;
+    if (spread) {
+      s->skey = ((uint64_t)xch_->rank() << 56) | ((uint64_t)idx_ << 48) | next_skey_++;
+      rsess_[s->skey] = s;
+    }
     for (size_t i = 0; i < valid.size(); ++i) {
       s->bs[i].backend = valid[i];
+      const int target = spread ? (xch_->rank() + (int)i) % xch_->world() : -1;
+      if (spread && target != xch_->rank()) {
+        s->bs[i].remote = target;
+        s->remote_n++;
+        continue;
+      }
       s->bs[i].slot = eng_->open((int)i, s->filter, s->emit);
       slot_owner_[s->bs[i].slot] = {s, (int)i};
     }
@@ -1043,6 +1090,21 @@ class Loop {
       const char* et = nullptr;
       if (!upstream_body(s, valid[i], body, &st, &msg, &et)) {
         fail_backend(s, (int)i, st, msg, et);
+        continue;
+      }
+      if (s->bs[i].remote >= 0) {
+        XMsg m;
+        m.type = X_OPEN;
+        m.flags = (uint8_t)((s->filter ? 1 : 0) | (s->emit ? 2 : 0));
+        m.dst_rank = s->bs[i].remote;
+        m.src_rank = xch_->rank();
+        m.dst_loop = m.src_loop = (uint16_t)idx_;
+        m.bi = (int)i;
+        m.skey = s->skey;
+        m.a = valid[i];
+        m.b = (int)(cfg_.timeout * 1000.0);
+        m.payload = build_req(cfg_.backends[valid[i]], s->fwd, body);
+        xch_->post(std::move(m));
         continue;
       }
       Up* u = open_up(s, (int)i, valid[i], UP_ENGINE, build_req(cfg_.backends[valid[i]], s->fwd, body), cfg_.timeout);
@@ -1058,16 +1120,163 @@ class Loop {
   }
   void begin_final(Session* s) {
     s->stage = 1;
+    if (s->kind == K_REMOTE) {  // worker: hand the stream's (stripped) final text to the owner
+      const BState& b = s->bs[0];
+      if (b.aborted || cfg_.skip_final) {
+        post_owner(s, X_FINAL, b.aborted ? XF_ABORTED : 0, 0, std::string());
+        return end_session(s);
+      }
+      s->fin_id = eng_->submit_finalize({b.slot}, cfg_.hide_final, true, std::string(), (int64_t)time(nullptr));
+      fin_owner_[s->fin_id] = {s, -1};
+      kick();
+      return;
+    }
     if (cfg_.skip_final) return finish_stream(s);
+    if (s->remote_n > 0) {  // owner of a spread session: per-stream texts, merged in backend order
+      for (int i = 0; i < (int)s->bs.size(); ++i) {
+        const BState& b = s->bs[i];
+        if (b.remote >= 0 || b.state != 1 || b.aborted) continue;
+        int id = eng_->submit_finalize({b.slot}, cfg_.hide_final, true, std::string(), (int64_t)time(nullptr));
+        fin_owner_[id] = {s, i};
+        s->fin_pending++;
+      }
+      if (s->fin_pending == 0) return merge_final(s);
+      kick();
+      return;
+    }
     std::vector<int> g = good_slots(s);
     bool texts = !cfg_.aggregator_name.empty();
     s->fin_texts = texts;
     s->fin_id = eng_->submit_finalize(g, cfg_.hide_final, texts, "\n" + cfg_.separator, (int64_t)time(nullptr));
-    fin_owner_[s->fin_id] = s;
+    fin_owner_[s->fin_id] = {s, -1};
     kick();
   }
-  void on_finalized(Session* s, FinalizeRes& f) {
+  // spread session: every stream's final text is in (local finalize or X_FINAL from a worker)
+  void merge_final(Session* s) {
+    std::vector<std::string> texts;
+    for (auto& b : s->bs)
+      if (b.state == 1 && !b.aborted && b.has_text) texts.push_back(b.ftext);
+    if (texts.empty()) {
+      send_chunk(s, error_event());
+      return finish_stream(s);
+    }
+    if (!cfg_.aggregator_name.empty()) {
+      s->texts = std::move(texts);
+      s->fin_texts = true;
+      return start_aggregator(s, "\n" + cfg_.separator);
+    }
+    std::string j = joined(texts, "\n" + cfg_.separator);
+    std::string ev = final_prefix((int64_t)time(nullptr));
+    escape_append((const uint8_t*)j.data(), j.size(), ev);
+    ev += kFinalSuffix;
+    send_chunk(s, ev);
+    finish_stream(s);
+  }
+  void post_owner(Session* s, uint8_t type, uint8_t flags, int a, const std::string& payload) {
+    if (!xch_) return;
+    XMsg m;
+    m.type = type;
+    m.flags = flags;
+    m.dst_rank = s->owner_rank;
+    m.src_rank = xch_->rank();
+    m.dst_loop = (uint16_t)s->owner_loop;
+    m.src_loop = (uint16_t)idx_;
+    m.bi = s->shadow_bi;
+    m.skey = s->owner_skey;
+    m.a = a;
+    m.payload = payload;
+    xch_->post(std::move(m));
+  }
+  void on_xmsgs() {
+    uint64_t v;
+    ssize_t r = read(xfd_, &v, 8);
+    (void)r;
+    std::vector<XMsg> in;
+    {
+      std::lock_guard<std::mutex> g(xmu_);
+      in.swap(xin_);
+    }
+    for (auto& m : in) {
+      if (m.type == X_DOWN) {
+        // exchange failed (peer death / timeout): fail remote streams, drop worker streams
+        std::vector<Session*> owners, shadows;
+        for (auto& kv : rsess_) owners.push_back(kv.second);
+        for (auto& kv : shadow_) shadows.push_back(kv.second);
+        for (Session* s : shadows)
+          if (sessions_.count(s)) end_session(s);
+        for (Session* s : owners) {
+          for (int i = 0; i < (int)s->bs.size() && sessions_.count(s); ++i)
+            if (s->bs[i].remote >= 0 && s->bs[i].state == 0)
+              fail_backend(s, i, 500, "rank exchange failed", "proxy_error");
+        }
+        continue;
+      }
+      if (m.type == X_OPEN) {
+        auto sp = std::make_unique<Session>();
+        Session* s = sp.get();
+        sessions_[s] = std::move(sp);
+        s->kind = K_REMOTE;
+        s->owner_rank = m.src_rank;
+        s->owner_loop = m.src_loop;
+        s->owner_skey = m.skey;
+        s->shadow_bi = m.bi;
+        s->filter = m.flags & 1;
+        s->emit = (m.flags & 2) != 0;
+        s->bs.resize(1);
+        s->bs[0].backend = m.a;
+        s->bs[0].slot = eng_->open(m.bi, s->filter, s->emit);
+        slot_owner_[s->bs[0].slot] = {s, 0};
+        shadow_[{m.skey, m.bi}] = s;
+        c_remote_streams++;
+        Up* u = (m.a >= 0 && m.a < (int)cfg_.backends.size())
+                    ? open_up(s, 0, m.a, UP_ENGINE, std::move(m.payload), m.b / 1000.0) : nullptr;
+        if (!u) fail_backend(s, 0, 500, "All connection attempts failed", "proxy_error");
+        else s->bs[0].up = u;
+        continue;
+      }
+      if (m.type == X_CANCEL) {
+        auto it = shadow_.find({m.skey, m.bi});
+        if (it != shadow_.end()) end_session(it->second);
+        continue;
+      }
+      auto it = rsess_.find(m.skey);
+      if (it == rsess_.end()) continue;
+      Session* s = it->second;
+      if (m.bi < 0 || m.bi >= (int)s->bs.size()) continue;
+      if (m.type == X_DATA) {
+        if (s->cl) send_chunk(s, m.payload);
+        continue;
+      }
+      if (m.type == X_FINAL) {
+        BState& b = s->bs[m.bi];
+        if (b.state != 0) continue;
+        if (m.flags & XF_FAILED) {
+          fail_backend(s, m.bi, m.a, m.payload, "proxy_error");
+          continue;
+        }
+        b.state = 1;
+        b.aborted = (m.flags & XF_ABORTED) != 0;
+        b.has_text = (m.flags & XF_TEXT) != 0;
+        b.ftext = std::move(m.payload);
+        s->finished++;
+        if (s->stage == 0 && s->finished == (int)s->bs.size()) begin_final(s);
+      }
+    }
+  }
+  void on_finalized(Session* s, FinalizeRes& f, int bi) {
     if (s->kind == K_NONSTREAM) return;  // not used
+    if (s->kind == K_REMOTE) {
+      const bool has = !f.texts.empty();
+      post_owner(s, X_FINAL, has ? XF_TEXT : 0, 0, has ? f.texts[0] : std::string());
+      return end_session(s);
+    }
+    if (bi >= 0) {
+      BState& b = s->bs[bi];
+      b.has_text = !f.texts.empty();
+      if (b.has_text) b.ftext = std::move(f.texts[0]);
+      if (--s->fin_pending == 0) merge_final(s);
+      return;
+    }
     if (!s->fin_texts) {
       if (f.kind == 1) send_chunk(s, f.event);
       else send_chunk(s, error_event());
@@ -1412,6 +1621,21 @@ class Loop {
   void end_session(Session* s) {
     if (s->stage == 3) return;
     s->stage = 3;
+    if (s->kind == K_REMOTE) shadow_.erase({s->owner_skey, s->shadow_bi});
+    if (s->skey) {
+      rsess_.erase(s->skey);
+      for (int i = 0; i < (int)s->bs.size(); ++i) {
+        if (s->bs[i].remote < 0 || s->bs[i].state != 0 || !xch_) continue;
+        XMsg m;  // client gone / session over before the worker finished: cancel it
+        m.type = X_CANCEL;
+        m.dst_rank = s->bs[i].remote;
+        m.src_rank = xch_->rank();
+        m.dst_loop = m.src_loop = (uint16_t)idx_;
+        m.bi = i;
+        m.skey = s->skey;
+        xch_->post(std::move(m));
+      }
+    }
     for (auto& b : s->bs) {
       if (b.up) {
         drop_up(b.up, false);
@@ -1428,6 +1652,10 @@ class Loop {
       s->agg = nullptr;
     }
     if (s->fin_id >= 0) fin_owner_.erase(s->fin_id);
+    for (auto it = fin_owner_.begin(); s->fin_pending > 0 && it != fin_owner_.end();) {
+      if (it->second.first == s) it = fin_owner_.erase(it);
+      else ++it;
+    }
     Client* c = s->cl;
     sessions_.erase(s);
     if (c) {
@@ -1450,6 +1678,13 @@ class Loop {
     put("qmx_client_connections_total", (double)c_clients.load());
     put("qmx_ticks_total", (double)c_ticks.load());
     put("qmx_tick_slots_total", (double)c_tick_slots.load());
+    put("qmx_remote_streams_total", (double)c_remote_streams.load());
+    if (xch_) {
+      put("qmx_exchange_rounds_total", (double)xch_->rounds());
+      put("qmx_exchange_bytes_total", (double)xch_->bytes());
+      put("qmx_exchange_busy_us_total", xch_->busy_us());
+      put("qmx_exchange_healthy", xch_->healthy() ? 1.0 : 0.0);
+    }
     for (auto& kv : eng_->stats()) put(("qmx_engine_" + kv.first).c_str(), kv.second);
     if (offload_)
       for (auto& kv : static_cast<HipEngine*>(eng_.get())->kernel_stats())
@@ -1472,7 +1707,15 @@ class Loop {
   std::unordered_map<int, std::unique_ptr<Up>> ups_;
   std::unordered_map<Session*, std::unique_ptr<Session>> sessions_;
   std::unordered_map<int, std::pair<Session*, int>> slot_owner_;
-  std::unordered_map<int, Session*> fin_owner_;
+  std::unordered_map<int, std::pair<Session*, int>> fin_owner_;  // fin id → (session, bs index | -1)
+  // spread placement
+  Exchange* xch_ = nullptr;
+  int xfd_ = -1;
+  std::mutex xmu_;
+  std::vector<XMsg> xin_;
+  uint64_t next_skey_ = 1;
+  std::unordered_map<uint64_t, Session*> rsess_;            // owner sessions with remote streams
+  std::map<std::pair<uint64_t, int>, Session*> shadow_;     // worker streams by (owner key, bi)
   std::vector<std::vector<int>> idle_;
   std::vector<int> pending_close_, pending_requests_;
 };
@@ -1505,6 +1748,23 @@ int run_server(const ServerCfg& cfg0) {
   std::vector<std::unique_ptr<Loop>> loops;
   std::vector<std::thread> ts;
   for (int i = 0; i < std::max(1, cfg.threads); ++i) loops.emplace_back(new Loop(cfg, i));
+  std::unique_ptr<Exchange> xch;
+  if (cfg.world > 1 && cfg.placement == "spread") {
+    XOptions o;
+    o.rank = cfg.rank;
+    o.world = cfg.world;
+    o.transport = cfg.xchg;
+    o.addr = cfg.xchg_addr;
+    o.port = cfg.xchg_port;
+    o.id_file = cfg.xchg_id_file;
+    o.device = cfg.device;
+    o.round_us = cfg.xchg_round_us;
+    o.timeout_s = cfg.xchg_timeout;
+    std::vector<Loop*> lp;
+    for (auto& l : loops) lp.push_back(l.get());
+    xch.reset(new Exchange(o, (int)lp.size(), [lp](int l, std::vector<XMsg>&& v) { lp[l]->x_deliver(std::move(v)); }));
+    for (auto& l : loops) l->attach_exchange(xch.get());
+  }
   for (auto& l : loops) {
     Loop* lp = l.get();
     ts.emplace_back([lp] {
@@ -1517,6 +1777,11 @@ int run_server(const ServerCfg& cfg0) {
     });
   }
   for (auto& t : ts) t.join();
+  if (xch) {
+    xch->request_stop();  // keeps taking part in rounds until every rank has stopped
+    xch->join();
+    xch.reset();
+  }
   loops.clear();
   return 0;
 }

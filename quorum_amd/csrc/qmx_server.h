@@ -48,6 +48,16 @@ struct ServerCfg {
   bool include_original_query = true, include_source_names = false;
   std::string env_api_key;
   bool install_signals = true;
+  // multi-rank: one process per GPU.  placement "local" = DP session sharding only;
+  // "spread" = a session's backend streams run on ranks owner..owner+N-1 (qmx_exchange.h)
+  int rank = 0, world = 1;
+  std::string placement = "local";
+  std::string xchg = "tcp";  // tcp | rccl
+  std::string xchg_addr = "127.0.0.1";
+  int xchg_port = 0;
+  std::string xchg_id_file;
+  int xchg_round_us = 200;
+  double xchg_timeout = 30.0;
 };
 
 // Runs until SIGTERM/SIGINT. Returns 0 on clean shutdown.

@@ -65,6 +65,28 @@ def native_config(cfg: Dict[str, Any], host: str, port: int, engine: str, device
         "include_source_names": bool(agg.include_source_names),
         "env_api_key": os.environ.get("OPENAI_API_KEY", ""),
         "backends": backends,
+        **cluster_config(rt, port, engine),
+    }
+
+
+def cluster_config(rt: RuntimeConfig, port: int, engine: str) -> Dict[str, Any]:
+    """Rank / placement / exchange settings (env wins: QMX_RANK, QMX_WORLD, QMX_XCHG_*)."""
+    env = os.environ
+    rank = int(env.get("QMX_RANK", env.get("RANK", "0")))
+    world = int(env.get("QMX_WORLD", env.get("WORLD_SIZE", "1")))
+    xchg = env.get("QMX_XCHG", rt.exchange)
+    if xchg == "auto":
+        xchg = "rccl" if engine == "hip" else "tcp"
+    if rt.placement not in ("local", "spread"):
+        raise NativeUnsupported(f"runtime.placement {rt.placement!r}: expected 'local' or 'spread'")
+    nonce = env.get("QMX_XCHG_NONCE", "0")
+    return {
+        "rank": rank, "world": world, "placement": rt.placement, "xchg": xchg,
+        "xchg_addr": env.get("QMX_XCHG_ADDR", "127.0.0.1"),
+        "xchg_port": int(env.get("QMX_XCHG_PORT", str(port + 7))),
+        "xchg_id_file": env.get("QMX_XCHG_ID_FILE", f"/tmp/qmx_xchg_{port}_{nonce}.id"),
+        "xchg_round_us": int(env.get("QMX_XCHG_ROUND_US", str(rt.exchange_round_us))),
+        "xchg_timeout": float(env.get("QMX_XCHG_TIMEOUT", str(rt.exchange_timeout))),
     }
 
 

@@ -208,6 +208,9 @@ class RuntimeConfig:
     max_slots: concurrent upstream streams resident per rank
     content_cap: device-resident filtered-content bytes per stream slot
     placement: "local" (a session's backends run on the owner rank) | "spread" (EP analog)
+    exchange:  spread transport: "auto" (rccl with a GPU engine, else tcp) | "rccl" | "tcp"
+    exchange_round_us: pacing of the lock-step all-gather rounds while traffic flows
+    exchange_timeout: a round slower than this = peer failure (fall back to local placement)
     total_timeout: optional per-backend total deadline in seconds (None = quorum semantics)
     """
 
@@ -217,6 +220,9 @@ class RuntimeConfig:
     max_slots: int = 8192
     content_cap: int = 1 << 20
     placement: str = "local"
+    exchange: str = "auto"
+    exchange_round_us: int = 200
+    exchange_timeout: float = 30.0
     total_timeout: Optional[float] = None
     log_content: bool = False
 
@@ -226,5 +232,7 @@ class RuntimeConfig:
         env_engine = os.environ.get("QMX_ENGINE")
         if env_engine:
             rt["engine"] = env_engine
+        if os.environ.get("QMX_PLACEMENT"):
+            rt["placement"] = os.environ["QMX_PLACEMENT"]
         known = {k: v for k, v in rt.items() if k in cls.__dataclass_fields__}
         return cls(**known)

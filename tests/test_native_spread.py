@@ -1,0 +1,195 @@
+"""Spread (EP-style) backend placement across ranks, CPU rehearsal with the TCP exchange.
+
+Two (or three) native server "ranks" run in this process, each with its own port, engine
+and keep-alive pools; with ``placement: spread`` backend i of a session owned by rank r
+runs on rank (r + i) % world and its SSE deltas + final text come back through the
+lock-step all-gather exchange (qmx_exchange.cpp).  Results must match the single-rank
+(local placement) server exactly — per-backend event streams, final event, aggregator
+prompt — whichever rank owns the session.  On MI355X the same code path uses RCCL
+(``exchange: rccl``) instead of the TCP hub.
+"""
+import contextlib
+import copy
+import json
+import os
+import threading
+import time
+
+import httpx
+import pytest
+
+from quorum_amd.ops import native
+
+from conftest import cfg_parallel, completion, sse_chunk, sse_stream
+from live_upstream import LiveUpstream, free_port, native_server
+
+pytestmark = pytest.mark.skipif(not native.available(), reason="native extension not built")
+
+AUTH = {"Authorization": "Bearer test-key"}
+MSG = [{"role": "user", "content": "What is 2+2?"}]
+CONCAT = {"separator": "\n-------------\n", "hide_intermediate_think": True, "hide_final_think": True,
+          "thinking_tags": ["think", "reason", "reasoning", "thought"], "skip_final_aggregation": False}
+AGG = {"aggregator_backend": "LLM4", "intermediate_separator": "\n\n---\n\n", "include_source_names": True,
+       "source_label_format": "Response from {backend_name}:\n", "prompt_template": "R:\n{responses}\nEnd.",
+       "include_original_query": True}
+THINK = [sse_chunk({"role": "assistant"}), sse_chunk({"content": "<think>"}), sse_chunk({"content": "hmm"}),
+         sse_chunk({"content": "</think>"}), sse_chunk({"content": "The answer "}), sse_chunk({"content": "is 4."}),
+         sse_chunk({}, finish="stop"), b"data: [DONE]\n\n"]
+
+
+@contextlib.contextmanager
+def native_cluster(cfg, world: int, placement: str = "spread"):
+    """`world` native ranks in-process (threads), TCP exchange hub on a free port."""
+    from quorum_amd.runtime.native_server import native_config
+
+    ext = native.require()
+    cfg = copy.deepcopy(cfg)
+    cfg.setdefault("runtime", {})["placement"] = placement
+    ports = [free_port() for _ in range(world)]
+    xport = free_port()
+    threads = []
+    for r in range(world):
+        env = {"QMX_RANK": str(r), "QMX_WORLD": str(world), "QMX_XCHG": "tcp", "QMX_XCHG_PORT": str(xport),
+               "QMX_XCHG_ROUND_US": "100"}
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            d = native_config(cfg, "127.0.0.1", ports[r], "cpu", 0, 1)
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        d["install_signals"] = False
+        th = threading.Thread(target=ext.run_server, args=(d,), daemon=True)
+        th.start()
+        threads.append(th)
+    for p in ports:
+        t0 = time.time()
+        while time.time() - t0 < 20:
+            try:
+                if httpx.get(f"http://127.0.0.1:{p}/health", timeout=1).status_code == 200:
+                    break
+            except httpx.HTTPError:
+                time.sleep(0.02)
+    try:
+        yield ports
+    finally:
+        ext.stop_server()
+        for th in threads:
+            th.join(timeout=15)
+
+
+def _events(text):
+    out = []
+    for seg in text.split("\n\n"):
+        if not seg.strip():
+            continue
+        p = seg[6:]
+        if p == "[DONE]":
+            out.append(p)
+            continue
+        ev = json.loads(p)
+        ev["created"] = 0
+        out.append(ev)
+    return out
+
+
+def _split(evs):
+    per, rest = {}, []
+    for e in evs:
+        if e != "[DONE]" and e["id"].startswith("chatcmpl-parallel-") and e["id"][-1].isdigit():
+            per.setdefault(e["id"], []).append(e)
+        else:
+            rest.append(e)
+    return per, rest
+
+
+def _live(ups):
+    live = LiveUpstream()
+    return live, {h: live.serve(h, b) for h, b in ups.items()}
+
+
+def _cfg(n, block, strategy="concatenate", urls=None):
+    cfg = cfg_parallel(n, strategy=strategy, block=block)
+    for i, b in enumerate(cfg["primary_backends"]):
+        b["url"] = urls[i]
+    return cfg
+
+
+SPREAD_CASES = {
+    "concat_think": (2, CONCAT, "concatenate",
+                     [("stream", 200, THINK), ("stream", 200, sse_stream(["Wor", "ld <think>x</think>"]))]),
+    "concat_4_one_fails": (4, CONCAT, "concatenate",
+                           [("stream", 200, sse_stream(["a"])), ("json", 503, {"error": {"message": "down"}}),
+                            ("stream", 200, THINK), ("refuse",)]),
+    "concat_all_fail": (2, CONCAT, "concatenate", [("json", 500, {"error": {"message": "x"}}), ("refuse",)]),
+    "concat_null_abort": (3, CONCAT, "concatenate",
+                          [("stream", 200, [sse_chunk({"content": "alpha "}), sse_chunk({"content": None}),
+                                            sse_chunk({"content": "beta"}), b"data: [DONE]\n\n"]),
+                           ("stream", 200, sse_stream(["B"])), ("stream", 200, sse_stream(["C é😀"]))]),
+    "skip_final": (3, dict(CONCAT, skip_final_aggregation=True), "concatenate",
+                   [("stream", 200, sse_stream(["x"])), ("stream", 200, sse_stream(["y"])),
+                    ("stream", 200, sse_stream(["z"]))]),
+    "aggregate_4": (4, AGG, "aggregate",
+                    [("stream", 200, sse_stream(["one"])), ("stream", 200, THINK),
+                     ("stream", 200, sse_stream(["three"])),
+                     lambda body: (("stream", 200, sse_stream(["four"])) if body.get("stream")
+                                   else ("json", 200, completion("SYNTH")))]),
+}
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("name", sorted(SPREAD_CASES))
+def test_spread_matches_local(name, world):
+    n, block, strategy, behs = SPREAD_CASES[name]
+    live, ports = _live({f"b{i + 1}": b for i, b in enumerate(behs)})
+    try:
+        cfg = _cfg(n, block, strategy, [f"http://127.0.0.1:{ports[f'b{i + 1}']}/v1" for i in range(n)])
+        req = {"messages": MSG, "stream": True}
+        with native_server(cfg) as p:
+            ref = httpx.post(f"http://127.0.0.1:{p}/chat/completions", json=req, headers=AUTH, timeout=30)
+        ref_calls = sorted(json.dumps(c["body"], sort_keys=True) for c in live.calls)
+        live.calls.clear()
+        with native_cluster(cfg, world) as cports:
+            for owner in range(world):  # every rank as session owner
+                r = httpx.post(f"http://127.0.0.1:{cports[owner]}/chat/completions", json=req, headers=AUTH,
+                               timeout=30)
+                assert r.status_code == ref.status_code
+                assert _split(_events(r.text)) == _split(_events(ref.text)), (name, owner)
+            m = httpx.get(f"http://127.0.0.1:{cports[0]}/metrics").text
+        # each owner's run sent exactly the single-rank upstream requests
+        calls = sorted(json.dumps(c["body"], sort_keys=True) for c in live.calls)
+        assert calls == sorted(ref_calls * world)
+        assert "qmx_exchange_rounds_total" in m
+        remote = float([ln for ln in m.splitlines() if ln.startswith("qmx_remote_streams_total")][0].split()[1])
+        assert remote >= 1, m
+    finally:
+        live.close()
+
+
+def test_spread_many_concurrent_sessions():
+    """Concurrent sessions on both ranks; every response complete and correct."""
+    behs = [("stream", 200, THINK), ("stream", 200, sse_stream(["x", "y", "z"]))]
+    live, ports = _live({"b1": behs[0], "b2": behs[1]})
+    try:
+        cfg = _cfg(2, dict(CONCAT, skip_final_aggregation=False), "concatenate",
+                   [f"http://127.0.0.1:{ports['b1']}/v1", f"http://127.0.0.1:{ports['b2']}/v1"])
+        req = {"messages": MSG, "stream": True}
+        with native_server(cfg) as p:
+            ref = _split(_events(httpx.post(f"http://127.0.0.1:{p}/chat/completions", json=req, headers=AUTH,
+                                            timeout=30).text))
+        with native_cluster(cfg, 2) as cports:
+            import concurrent.futures as cf
+
+            def one(i):
+                with httpx.Client(base_url=f"http://127.0.0.1:{cports[i % 2]}") as c:
+                    return [_split(_events(c.post("/chat/completions", json=req, headers=AUTH, timeout=30).text))
+                            for _ in range(5)]
+            with cf.ThreadPoolExecutor(8) as ex:
+                for res in ex.map(one, range(8)):
+                    for r in res:
+                        assert r == ref
+    finally:
+        live.close()
