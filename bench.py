@@ -34,6 +34,21 @@ sys.path.insert(0, ROOT)
 
 BASELINE_RPS = 9.1  # reference, 2 backends, same config, 16 clients
 
+# BASELINE.json configs.  "headline" is the driver's metric; the others are measured with
+# --scenario (reference numbers from BASELINE.md where one exists for that shape).
+SCENARIOS = {
+    "headline": dict(n=2, strategy="concatenate", hide_final=False, skip=True, faults={}, timeout=30,
+                     baseline=9.1, desc="2 mock backends, streaming concatenate, hide_intermediate_think"),
+    "aggregate4": dict(n=4, strategy="aggregate", hide_final=False, skip=False, faults={}, timeout=30,
+                       baseline=3.8, desc="4 mock backends, streaming aggregate strategy (LLM4 also aggregates)"),
+    "highqps8": dict(n=8, strategy="concatenate", hide_final=True, skip=True, faults={}, timeout=30,
+                     baseline=2.4, desc="8 mock backends, streaming, hide_final_think + skip_final_aggregation"),
+    "failure": dict(n=2, strategy="concatenate", hide_final=False, skip=False, timeout=2,
+                    faults={1: ["--fail-rate", "0.3", "--drop-rate", "0.2", "--null-rate", "0.1"]},
+                    baseline=6.9, desc="2 mock backends, backend 2 injects 30% HTTP 500 / 20% mid-stream "
+                                       "disconnect / 10% content:null; 2 s timeout"),
+}
+
 
 def _free_port_block(base: int) -> int:
     return base
@@ -55,20 +70,27 @@ def _kill(procs):
                 pass
 
 
-def write_config(path: str, mock_ports, skip_final: bool, tile: int) -> None:
+def write_config(path: str, mock_ports, skip_final: bool, tile: int, sc=None, placement="local") -> None:
     import yaml
 
+    sc = sc or SCENARIOS["headline"]
+    block = {"separator": "\n-------------\n", "hide_intermediate_think": True,
+             "hide_final_think": bool(sc["hide_final"]), "thinking_tags": ["think", "reason", "reasoning", "thought"],
+             "skip_final_aggregation": skip_final}
     cfg = {
-        "settings": {"timeout": 30},
+        "settings": {"timeout": sc["timeout"]},
         "primary_backends": [{"name": f"LLM{i + 1}", "url": f"http://127.0.0.1:{p}/v1", "model": f"mock-{i + 1}"}
                              for i, p in enumerate(mock_ports)],
-        "iterations": {"aggregation": {"strategy": "concatenate"}},
-        "strategy": {"concatenate": {
-            "separator": "\n-------------\n", "hide_intermediate_think": True, "hide_final_think": False,
-            "thinking_tags": ["think", "reason", "reasoning", "thought"],
-            "skip_final_aggregation": skip_final}},
-        "runtime": {"tile_bytes": tile, "max_slots": 4096, "content_cap": 1 << 18},
+        "iterations": {"aggregation": {"strategy": sc["strategy"]}},
+        "strategy": {"concatenate": block},
+        "runtime": {"tile_bytes": tile, "max_slots": 4096, "content_cap": 1 << 18, "placement": placement},
     }
+    if sc["strategy"] == "aggregate":
+        cfg["strategy"]["aggregate"] = dict(block, aggregator_backend=f"LLM{len(mock_ports)}",
+                                            intermediate_separator="\n\n---\n\n", include_source_names=True,
+                                            source_label_format="Response from {backend_name}:\n",
+                                            prompt_template="Synthesize:\n\n{responses}",
+                                            include_original_query=True)
     with open(path, "w") as f:
         yaml.safe_dump(cfg, f)
 
@@ -99,7 +121,12 @@ def main() -> int:
     ap.add_argument("--tile", type=int, default=16384)
     ap.add_argument("--port", type=int, default=int(os.environ.get("QMX_BENCH_PORT", "18000")))
     ap.add_argument("--timeout", type=float, default=300)
+    ap.add_argument("--scenario", default="headline", choices=sorted(SCENARIOS))
+    ap.add_argument("--placement", default="local", choices=["local", "spread"],
+                    help="spread: a session's backend streams run on consecutive ranks (RCCL exchange)")
     args = ap.parse_args()
+    sc = SCENARIOS[args.scenario]
+    skip_final = bool(args.skip_final) if args.scenario == "headline" else sc["skip"]
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -128,15 +155,22 @@ def main() -> int:
     procs = []
     tmp = tempfile.mkdtemp(prefix=f"qmx_bench_r{rank}_")
     try:
-        mock_ports = [args.port + 100 + rank * 10 + i for i in range(2)]
-        for p in mock_ports:
+        mock_ports = [args.port + 100 + rank * 10 + i for i in range(sc["n"])]
+        for i, p in enumerate(mock_ports):
             procs.append(subprocess.Popen([os.path.join(bin_dir, "qmx_mock"), "--port", str(p), "--threads",
-                                           str(args.mock_threads), "--tokens", "20", "--think", "1"],
+                                           str(args.mock_threads), "--tokens", "20", "--think", "1"]
+                                          + sc["faults"].get(i, []),
                                           stderr=subprocess.DEVNULL, start_new_session=True))
         cfg_path = os.path.join(tmp, "config.yaml")
-        write_config(cfg_path, mock_ports, bool(args.skip_final), args.tile)
+        write_config(cfg_path, mock_ports, skip_final, args.tile, sc, args.placement)
+        env = dict(os.environ)
+        if args.placement == "spread" and world > 1:
+            nonce = [str(time.time_ns()) if rank == 0 else None]
+            dist.broadcast_object_list(nonce, src=0)
+            env.update({"QMX_XCHG_NONCE": nonce[0], "QMX_XCHG_PORT": str(args.port + 7),
+                        "QMX_RANK": str(rank), "QMX_WORLD": str(world)})
         procs += spawn_workers(cfg_path, "127.0.0.1", args.port, args.workers, engine,
-                               local_rank if use_cuda else None, impl=args.impl, threads=args.threads)
+                               local_rank if use_cuda else None, impl=args.impl, threads=args.threads, env=env)
         if not wait_healthy("127.0.0.1", args.port, 180):
             raise RuntimeError("proxy did not become healthy")
         if dist is not None:
@@ -170,7 +204,8 @@ def main() -> int:
             value = total / max_el
             p50 = statistics.median(r[2] for r in rows)
             res = {
-                "metric": "proxied req/sec (whole node) + p50 TTFT, 2-backend concatenate stream",
+                "metric": "proxied req/sec (whole node) + p50 TTFT, 2-backend concatenate stream"
+                          if args.scenario == "headline" else f"proxied req/sec (whole node) + p50 TTFT, {args.scenario}",
                 "value": round(value, 3),
                 "unit": "req/s",
                 "n_gpus": world,
@@ -179,14 +214,16 @@ def main() -> int:
                 "ms_per_step": round(1000.0 * max_el / args.steps, 3),
                 "higher_is_better": True,
                 "scaling": "weak",
-                "vs_baseline": round(value / BASELINE_RPS, 3),
+                "vs_baseline": round(value / sc["baseline"], 3),
                 "dtype": "bytes (utf-8 SSE text; no float compute)",
                 "data": "synthetic: C++ mock backends (role + 4 split <think> fragments + 20 tokens + stop + "
                         "[DONE]) and C++ closed-loop load generator",
-                "config": {"model": "2 mock backends, streaming concatenate, hide_intermediate_think, "
-                                    f"skip_final_aggregation={bool(args.skip_final)}",
+                "config": {"model": f"{sc['desc']}, skip_final_aggregation={skip_final}",
                            "global_batch": args.batch * world, "seq_len": 26,
-                           "parallelism": f"dp{world} (sessions sharded over GPUs via SO_REUSEPORT)",
+                           "parallelism": f"dp{world} (sessions sharded over GPUs via SO_REUSEPORT)"
+                                          + (f" + ep{world} (backend streams spread over ranks, "
+                                                f"{'RCCL' if engine == 'hip' else 'TCP'} all-gather exchange)"
+                                             if args.placement == "spread" and world > 1 else ""),
                            "impl": args.impl, "engine": engine, "conns_per_rank": args.conns},
                 "p50_ttft_ms": round(p50, 3),
                 "p99_ttft_ms": round(max(r[3] for r in rows), 3),

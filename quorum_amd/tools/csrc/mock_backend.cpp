@@ -96,9 +96,9 @@ void build_responses() {
                 std::to_string(body.size()) + "\r\n\r\n" + body;
 }
 
-const std::string kFail =
-    "HTTP/1.1 500 Internal Server Error\r\ncontent-type: application/json\r\ncontent-length: 62\r\n\r\n"
-    "{\"error\": {\"message\": \"injected failure\", \"type\": \"mock\"}}  ";
+const std::string kFailBody = "{\"error\": {\"message\": \"injected failure\", \"type\": \"mock\"}}";
+const std::string kFail = "HTTP/1.1 500 Internal Server Error\r\ncontent-type: application/json\r\ncontent-length: " +
+                          std::to_string(kFailBody.size()) + "\r\n\r\n" + kFailBody;
 
 struct Conn {
   int fd;
