@@ -109,7 +109,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=512, help="requests per step per rank")
+    ap.add_argument("--batch", type=int, default=4096, help="requests per step per rank")
     ap.add_argument("--conns", type=int, default=64, help="concurrent client connections per rank")
     ap.add_argument("--impl", default=os.environ.get("QMX_BENCH_IMPL", "native"), choices=["native", "python"])
     ap.add_argument("--engine", default=os.environ.get("QMX_BENCH_ENGINE", "auto"))

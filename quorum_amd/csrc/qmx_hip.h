@@ -76,6 +76,7 @@ class HipEngine : public HostEngine {
  private:
   void escalate(int slot, bool fresh);
   void finalize_host(const FinalizeReq& r, std::vector<FinalizeRes>& out);
+  void wait_stream();
   void ensure_in(size_t bytes);
   void ensure_out(size_t bytes);
   void build_params(int64_t created);

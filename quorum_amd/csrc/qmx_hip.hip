@@ -21,6 +21,9 @@
 // Semantics: SURVEY §2.7 (reference src/quorum/oai_proxy.py:262-371, 578-673).
 #include "qmx_hip.h"
 
+#include <chrono>
+#include <thread>
+
 #include "qmx_lex.h"
 
 #include <algorithm>
@@ -1122,6 +1125,20 @@ static void put(char* dst, int cap, int* len, const std::string& s) {
   *len = (int)s.size();
 }
 
+// Wait for this engine's stream without pinning a core: the io loops share the CPU with
+// the tick threads, and a spinning hipStreamSynchronize costs a whole core per engine.
+// Spin briefly (the common tick finishes in ~100-200 us), then poll with short sleeps.
+void HipEngine::wait_stream() {
+  const auto t0 = std::chrono::steady_clock::now();
+  while (true) {
+    hipError_t e = hipStreamQuery(stream_);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) HIP_CHECK(e);
+    if (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(20)) continue;
+    std::this_thread::sleep_for(std::chrono::microseconds(15));
+  }
+}
+
 HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_bytes, int max_slots,
                      int content_cap)
     : HostEngine(tags),
@@ -1323,7 +1340,7 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
                        d_content_, params_);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipEventRecord(ev1_, stream_));
-    HIP_CHECK(hipStreamSynchronize(stream_));
+    wait_stream();
     float ms = 0.f;
     hipEventElapsedTime(&ms, ev0_, ev1_);
     kernel_ms_ += ms;
@@ -1498,7 +1515,7 @@ void HipEngine::finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes
                      content_cap_, d_join_, d_fout_, h_fout_, h_finres_, ts_);
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipEventRecord(ev1_, stream_));
-  HIP_CHECK(hipStreamSynchronize(stream_));
+  wait_stream();
   float ms = 0.f;
   hipEventElapsedTime(&ms, ev0_, ev1_);
   fin_ms_ += ms;
