@@ -21,6 +21,8 @@
 // Semantics: SURVEY §2.7 (reference src/quorum/oai_proxy.py:262-371, 578-673).
 #include "qmx_hip.h"
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include <chrono>
 #include <thread>
 
@@ -1335,12 +1337,15 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
       std::memset(h_dbg_, 0, sizeof(unsigned long long) * 16 * n);
       params_.dbg = h_dbg_;
     }
+    roctxRangePushA("qmx_tick");  // rocprofv3 --marker-trace: one range per tick launch + wait
+    h2d_bytes_ += in_off;
     HIP_CHECK(hipEventRecord(ev0_, stream_));
     hipLaunchKernelGGL(qmx_tick_kernel, dim3(n), dim3(BS), 0, stream_, h_items_, h_in_, h_out_, h_res_, d_state_,
                        d_content_, params_);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipEventRecord(ev1_, stream_));
     wait_stream();
+    roctxRangePop();
     float ms = 0.f;
     hipEventElapsedTime(&ms, ev0_, ev1_);
     kernel_ms_ += ms;
@@ -1411,6 +1416,7 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
       }
     }
     std::string sse;
+    d2h_bytes_ += r.out_len;
     if (r.out_len) sse.assign((const char*)h_out_ + h_items_[i].out_off, r.out_len);
     if (!sse.empty() || flags) results.push_back({p.slot, std::move(sse), flags});
   }
@@ -1510,12 +1516,14 @@ void HipEngine::finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes
   grow_device(&d_join_, &join_cap_, join_off + 16);
   grow_device(&d_fout_, &dfout_cap_, out_off + 16);
   grow_mapped(&h_fout_, &fout_cap_, out_off + 16);
+  roctxRangePushA("qmx_finalize");
   HIP_CHECK(hipEventRecord(ev0_, stream_));
   hipLaunchKernelGGL(qmx_finalize_kernel, dim3(n), dim3(BS), 0, stream_, h_fin_, h_fint_, h_fin_in_, d_content_,
                      content_cap_, d_join_, d_fout_, h_fout_, h_finres_, ts_);
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipEventRecord(ev1_, stream_));
   wait_stream();
+  roctxRangePop();
   float ms = 0.f;
   hipEventElapsedTime(&ms, ev0_, ev1_);
   fin_ms_ += ms;
@@ -1553,7 +1561,8 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
                                              {"kernel_ms", kernel_ms_}, {"escalations", (double)escalations_},
                                              {"fin_launches", (double)fin_launches_}, {"stage_items", (double)stage_n_},
                                              {"fin_items", (double)fin_items_}, {"fin_host", (double)fin_host_},
-                                             {"fin_ms", fin_ms_}};
+                                             {"fin_ms", fin_ms_}, {"h2d_bytes", (double)h2d_bytes_},
+                                             {"d2h_bytes", (double)d2h_bytes_}};
   for (int k = 1; k < 11; ++k) m["stage" + std::to_string(k) + "_us"] = stage_us_[k];
   m["shader_mhz"] = clk_us_ > 0 ? clk_cycles_ / clk_us_ : 0.0;
   return m;

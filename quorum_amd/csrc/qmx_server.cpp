@@ -34,6 +34,43 @@ namespace {
 std::atomic<bool> g_stop{false};
 std::atomic<uint64_t> c_requests{0}, c_stream{0}, c_nonstream{0}, c_errors{0}, c_up_fail{0}, c_ticks{0},
     c_tick_slots{0}, c_up_conns{0}, c_clients{0}, c_remote_streams{0};
+// failures by class
+std::atomic<uint64_t> c_fail_connect{0}, c_fail_timeout{0}, c_fail_status{0}, c_fail_disconnect{0},
+    c_fail_protocol{0}, c_stream_aborts{0};
+
+// Prometheus histogram with lock-free buckets (seconds)
+struct Hist {
+  static constexpr int N = 17;
+  static constexpr double le[N] = {1e-4, 2.5e-4, 5e-4, 1e-3, 2.5e-3, 5e-3, 1e-2, 2.5e-2, 5e-2,
+                                   0.1,  0.25,   0.5,  1.0,  2.5,    5.0,  10.0, 30.0};
+  std::atomic<uint64_t> b[N + 1];
+  std::atomic<uint64_t> count{0}, sum_ns{0};
+  Hist() {
+    for (auto& x : b) x.store(0);
+  }
+  void observe(double sec) {
+    int i = 0;
+    while (i < N && sec > le[i]) ++i;
+    b[i]++;
+    count++;
+    sum_ns += (uint64_t)(sec * 1e9);
+  }
+  void render(std::string& m, const std::string& name, const std::string& labels = std::string()) const {
+    uint64_t acc = 0;
+    const std::string sep = labels.empty() ? "" : ",";
+    for (int i = 0; i <= N; ++i) {
+      acc += b[i].load();
+      char le_s[32];
+      if (i < N) snprintf(le_s, sizeof(le_s), "%g", le[i]);
+      else snprintf(le_s, sizeof(le_s), "+Inf");
+      m += name + "_bucket{" + labels + sep + "le=\"" + le_s + "\"} " + std::to_string(acc) + "\n";
+    }
+    m += name + "_sum" + (labels.empty() ? "" : "{" + labels + "}") + " " + std::to_string(sum_ns.load() / 1e9) + "\n";
+    m += name + "_count" + (labels.empty() ? "" : "{" + labels + "}") + " " + std::to_string(acc) + "\n";
+  }
+};
+constexpr double Hist::le[Hist::N];
+Hist h_ttft, h_latency, h_tick, h_upstream_ttfb;
 
 using Clock = std::chrono::steady_clock;
 inline double now_s() { return std::chrono::duration<double>(Clock::now().time_since_epoch()).count(); }
@@ -230,7 +267,7 @@ struct Up {
   bool connecting = false, reused = false, got_bytes = false, headers_seen = false;
   RespParser rp;
   std::string body;  // buffered body (UP_BUFFER / non-200)
-  double last_io = 0, deadline = 0, timeout = 60;
+  double last_io = 0, deadline = 0, timeout = 60, t_open = 0;
 };
 
 struct BState {
@@ -277,6 +314,7 @@ struct Session {
   int remote_n = 0, fin_pending = 0;
   int owner_rank = -1, owner_loop = 0, shadow_bi = 0;  // worker (K_REMOTE)
   uint64_t owner_skey = 0;
+  bool first_content = false;  // TTFT recorded
 };
 
 struct ResultBatch {
@@ -291,6 +329,17 @@ class Loop {
  public:
   Loop(const ServerCfg& cfg, int idx) : cfg_(cfg), idx_(idx) { xfd_ = eventfd(0, EFD_NONBLOCK); }
   void attach_exchange(Exchange* x) { xch_ = x; }
+  void attach_loops(const std::vector<Loop*>* ls) { loops_ = ls; }
+  std::mutex smu_;
+  std::unordered_map<std::string, double> snap_;  // engine stats snapshot (read by /metrics on any loop)
+  void snapshot() {
+    std::unordered_map<std::string, double> m;
+    for (auto& kv : eng_->stats()) m["qmx_engine_" + kv.first] = kv.second;
+    if (offload_)
+      for (auto& kv : static_cast<HipEngine*>(eng_.get())->kernel_stats()) m["qmx_kernel_" + kv.first] = kv.second;
+    std::lock_guard<std::mutex> g(smu_);
+    snap_.swap(m);
+  }
   // exchange thread → this loop (thread-safe)
   void x_deliver(std::vector<XMsg>&& v) {
     {
@@ -334,6 +383,7 @@ class Loop {
       if (t - last_sweep > 0.1) {
         sweep_timeouts(t);
         last_sweep = t;
+        if (!offload_) snapshot();  // (the HIP tick thread snapshots its own engine)
       }
     }
   }
@@ -413,7 +463,13 @@ class Loop {
       if (stop_gpu_) break;
       while (eng_->has_work()) {
         ResultBatch rb;
+        const double tt = now_s();
         eng_->tick((int64_t)time(nullptr), rb.r, rb.f);
+        h_tick.observe(now_s() - tt);
+        if (tt - last_snap_ > 0.05) {
+          snapshot();
+          last_snap_ = tt;
+        }
         c_ticks++;
         c_tick_slots += rb.r.size();
         if (rb.r.empty() && rb.f.empty()) continue;
@@ -429,7 +485,9 @@ class Loop {
   }
   void tick_inline() {
     ResultBatch rb;
+    const double tt = now_s();
     eng_->tick((int64_t)time(nullptr), rb.r, rb.f);
+    h_tick.observe(now_s() - tt);
     c_ticks++;
     c_tick_slots += rb.r.size();
     apply(rb);
@@ -453,8 +511,9 @@ class Loop {
       int bi = it->second.second;
       if (!r.sse.empty()) {
         if (s->kind == K_REMOTE) post_owner(s, X_DATA, 0, 0, r.sse);
-        else if (s->cl) send_chunk(s, r.sse);
+        else if (s->cl) send_content(s, r.sse);
       }
+      if ((r.flags & RF_ABORTED)) c_stream_aborts++;
       if ((r.flags & (RF_DONE | RF_ABORTED)) && s->bs[bi].state == 0) {
         s->bs[bi].state = 1;
         s->bs[bi].aborted = (r.flags & RF_ABORTED) != 0;
@@ -773,6 +832,7 @@ class Loop {
     u->req = std::move(req);
     u->timeout = timeout;
     u->last_io = now_s();
+    u->t_open = u->last_io;
     u->deadline = cfg_.total_timeout > 0 ? u->last_io + cfg_.total_timeout : 0;
     if (!be.resolved || be.https) return nullptr;
     int fd = -1;
@@ -813,6 +873,7 @@ class Loop {
         continue;
       }
       if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) return;
+      c_fail_connect++;
       return up_error(u, "All connection attempts failed");
     }
     mod(u->fd, EPOLLIN, tag(4, u->fd));
@@ -822,7 +883,10 @@ class Loop {
       int err = 0;
       socklen_t len = sizeof(err);
       getsockopt(u->fd, SOL_SOCKET, SO_ERROR, &err, &len);
-      if (err != 0) return up_error(u, "All connection attempts failed");
+      if (err != 0) {
+        c_fail_connect++;
+        return up_error(u, "All connection attempts failed");
+      }
       u->connecting = false;
     }
     const int fd = u->fd;
@@ -837,9 +901,13 @@ class Loop {
       while (true) {
         ssize_t r = recv(u->fd, buf, sizeof(buf), 0);
         if (r > 0) {
+          if (!u->got_bytes) h_upstream_ttfb.observe(now_s() - u->t_open);
           u->got_bytes = true;
           u->last_io = now_s();
-          if (u->rp.feed(buf, r, body) < 0) return up_error(u, "invalid HTTP response");
+          if (u->rp.feed(buf, r, body) < 0) {
+            c_fail_protocol++;
+            return up_error(u, "invalid HTTP response");
+          }
           continue;
         }
         if (r == 0) eof = true;
@@ -856,6 +924,7 @@ class Loop {
       if (eof) {
         if (u->rp.phase == 6) return up_complete(u, false);
         if (!u->got_bytes && u->reused) return retry_fresh(u);
+        c_fail_disconnect++;
         return up_error(u, "Server disconnected without sending a response.");
       }
     }
@@ -900,7 +969,10 @@ class Loop {
     }
     for (int fd : expired) {
       auto it = ups_.find(fd);
-      if (it != ups_.end()) up_error(it->second.get(), "");  // httpx timeouts stringify to ""
+      if (it != ups_.end()) {
+        c_fail_timeout++;
+        up_error(it->second.get(), "");  // httpx timeouts stringify to ""
+      }
     }
   }
 
@@ -988,7 +1060,7 @@ class Loop {
         b.is_json = true;
         b.js = std::move(e);
       }
-      c_up_fail++;
+      c_up_fail++; c_fail_status++;
     }
     if (mode == UP_ENGINE || mode == UP_PASS) {
       // non-200 on a streaming call
@@ -1055,6 +1127,14 @@ class Loop {
   // ---------------------------------------------------------------- parallel streaming
   void send_chunk(Session* s, const std::string& data) {
     if (s->cl) write_client(s->cl, chunk(data));
+  }
+  // content-bearing events: the first one closes the session's TTFT span
+  void send_content(Session* s, const std::string& data) {
+    if (!s->first_content) {
+      s->first_content = true;
+      h_ttft.observe(now_s() - s->t0);
+    }
+    send_chunk(s, data);
   }
   void start_parallel(Session* s, const std::vector<int>& valid) {
     c_stream++;
@@ -1244,7 +1324,7 @@ class Loop {
       Session* s = it->second;
       if (m.bi < 0 || m.bi >= (int)s->bs.size()) continue;
       if (m.type == X_DATA) {
-        if (s->cl) send_chunk(s, m.payload);
+        if (s->cl) send_content(s, m.payload);
         continue;
       }
       if (m.type == X_FINAL) {
@@ -1442,7 +1522,7 @@ class Loop {
     std::string w = s->done_tail + data;
     if (w.find("data: [DONE]") != std::string::npos) s->saw_done = true;
     s->done_tail = w.size() > 16 ? w.substr(w.size() - 16) : w;
-    send_chunk(s, data);
+    send_content(s, data);
   }
   void pass_body(Session* s, const std::string& body) {
     if (!s->first_decided) {
@@ -1621,6 +1701,7 @@ class Loop {
   void end_session(Session* s) {
     if (s->stage == 3) return;
     s->stage = 3;
+    if (s->kind != K_REMOTE && s->t0 > 0) h_latency.observe(now_s() - s->t0);
     if (s->kind == K_REMOTE) shadow_.erase({s->owner_skey, s->shadow_bi});
     if (s->skey) {
       rsess_.erase(s->skey);
@@ -1679,16 +1760,29 @@ class Loop {
     put("qmx_ticks_total", (double)c_ticks.load());
     put("qmx_tick_slots_total", (double)c_tick_slots.load());
     put("qmx_remote_streams_total", (double)c_remote_streams.load());
+    m += "qmx_upstream_failures_by_class_total{class=\"connect\"} " + std::to_string(c_fail_connect.load()) + "\n";
+    m += "qmx_upstream_failures_by_class_total{class=\"timeout\"} " + std::to_string(c_fail_timeout.load()) + "\n";
+    m += "qmx_upstream_failures_by_class_total{class=\"http_status\"} " + std::to_string(c_fail_status.load()) + "\n";
+    m += "qmx_upstream_failures_by_class_total{class=\"disconnect\"} " + std::to_string(c_fail_disconnect.load()) + "\n";
+    m += "qmx_upstream_failures_by_class_total{class=\"protocol\"} " + std::to_string(c_fail_protocol.load()) + "\n";
+    put("qmx_stream_aborts_total", (double)c_stream_aborts.load());
+    h_ttft.render(m, "qmx_ttft_seconds");
+    h_latency.render(m, "qmx_request_latency_seconds");
+    h_tick.render(m, "qmx_tick_seconds");
+    h_upstream_ttfb.render(m, "qmx_upstream_ttfb_seconds");
     if (xch_) {
       put("qmx_exchange_rounds_total", (double)xch_->rounds());
       put("qmx_exchange_bytes_total", (double)xch_->bytes());
       put("qmx_exchange_busy_us_total", xch_->busy_us());
       put("qmx_exchange_healthy", xch_->healthy() ? 1.0 : 0.0);
     }
-    for (auto& kv : eng_->stats()) put(("qmx_engine_" + kv.first).c_str(), kv.second);
-    if (offload_)
-      for (auto& kv : static_cast<HipEngine*>(eng_.get())->kernel_stats())
-        put(("qmx_kernel_" + kv.first).c_str(), kv.second);
+    // engine/kernel stats summed over every io loop's engine (snapshots taken by their tick threads)
+    std::map<std::string, double> tot;
+    for (Loop* l : *loops_) {
+      std::lock_guard<std::mutex> g(l->smu_);
+      for (auto& kv : l->snap_) tot[kv.first] += kv.second;
+    }
+    for (auto& kv : tot) put(kv.first.c_str(), kv.second);
     return m;
   }
 
@@ -1710,6 +1804,8 @@ class Loop {
   std::unordered_map<int, std::pair<Session*, int>> fin_owner_;  // fin id → (session, bs index | -1)
   // spread placement
   Exchange* xch_ = nullptr;
+  const std::vector<Loop*>* loops_ = nullptr;
+  double last_snap_ = 0;
   int xfd_ = -1;
   std::mutex xmu_;
   std::vector<XMsg> xin_;
@@ -1748,6 +1844,9 @@ int run_server(const ServerCfg& cfg0) {
   std::vector<std::unique_ptr<Loop>> loops;
   std::vector<std::thread> ts;
   for (int i = 0; i < std::max(1, cfg.threads); ++i) loops.emplace_back(new Loop(cfg, i));
+  std::vector<Loop*> loop_ptrs;
+  for (auto& l : loops) loop_ptrs.push_back(l.get());
+  for (auto& l : loops) l->attach_loops(&loop_ptrs);
   std::unique_ptr<Exchange> xch;
   if (cfg.world > 1 && cfg.placement == "spread") {
     XOptions o;

@@ -93,7 +93,7 @@ def _build(debug: bool = False, jobs: int = 3, verbose: bool = False) -> Path:
     if out.exists() and out.stat().st_mtime > max(o.stat().st_mtime for o in objs):
         return out
     cmd = [cc, "-shared", "-o", str(out)] + [str(o) for o in objs] + [
-        f"--offload-arch={ARCH}", "-fPIC", "-L/opt/rocm/lib", "-lamdhip64", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
+        f"--offload-arch={ARCH}", "-fPIC", "-L/opt/rocm/lib", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)

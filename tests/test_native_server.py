@@ -262,3 +262,34 @@ def test_native_keepalive_many_requests():
                     assert evs[-1] == "[DONE]" and len(evs) == 5
     finally:
         live.close()
+
+
+def test_native_metrics_histograms_and_failure_classes():
+    """/metrics: TTFT / latency / tick / upstream-TTFB histograms and failures by class."""
+    live = LiveUpstream()
+    p1 = live.serve("b1", ("stream", 200, sse_stream(["x", "y"])))
+    p2 = live.serve("b2", ("refuse",))
+    cfg = cfg_parallel(2, block=CONCAT)
+    cfg["primary_backends"][0]["url"] = f"http://127.0.0.1:{p1}/v1"
+    cfg["primary_backends"][1]["url"] = f"http://127.0.0.1:{p2}/v1"
+    try:
+        with native_server(cfg) as port:
+            for _ in range(3):
+                r = httpx.post(f"http://127.0.0.1:{port}/chat/completions", json={"messages": MSG, "stream": True},
+                               headers=AUTH, timeout=30)
+                assert r.status_code == 200
+            import time as _t
+            _t.sleep(0.25)  # engine stats snapshots refresh every 50-100 ms
+            m = httpx.get(f"http://127.0.0.1:{port}/metrics").text
+    finally:
+        live.close()
+
+    def val(prefix):
+        return float([ln for ln in m.splitlines() if ln.startswith(prefix)][0].rsplit(" ", 1)[1])
+    assert val("qmx_ttft_seconds_count") >= 3
+    assert val('qmx_ttft_seconds_bucket{le="+Inf"}') == val("qmx_ttft_seconds_count")
+    assert val("qmx_request_latency_seconds_count") >= 3
+    assert val("qmx_tick_seconds_count") >= 1
+    assert val("qmx_upstream_ttfb_seconds_count") >= 3
+    assert val('qmx_upstream_failures_by_class_total{class="connect"}') >= 3
+    assert val("qmx_engine_") >= 0  # engine stats are exported
