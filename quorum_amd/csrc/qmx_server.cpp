@@ -32,6 +32,8 @@ namespace qmx {
 namespace {
 
 std::atomic<bool> g_stop{false};
+std::atomic<bool> g_drain{false};  // SIGTERM: stop accepting, finish in-flight sessions, then exit
+std::atomic<int> g_ready{0};       // io loops with a bound listener
 std::atomic<uint64_t> c_requests{0}, c_stream{0}, c_nonstream{0}, c_errors{0}, c_up_fail{0}, c_ticks{0},
     c_tick_slots{0}, c_up_conns{0}, c_clients{0}, c_remote_streams{0};
 // failures by class
@@ -358,11 +360,19 @@ class Loop {
 
   void run() {
     setup();
+    if (++g_ready == cfg_.threads && !cfg_.ready_file.empty()) {
+      FILE* f = fopen(cfg_.ready_file.c_str(), "w");  // supervisor: this generation is serving
+      if (f) {
+        fprintf(f, "%d\n", (int)getpid());
+        fclose(f);
+      }
+    }
     std::vector<epoll_event> evs(512);
     double last_sweep = now_s();
     while (!g_stop.load()) {
       int n = epoll_wait(ep_, evs.data(), (int)evs.size(), 50);
       for (int i = 0; i < n; ++i) dispatch(evs[i]);
+      if (g_drain.load() && drain_step()) break;
       if (!offload_ && eng_->has_work()) tick_inline();
       if (offload_ && kick_) {
         kick_ = false;
@@ -533,6 +543,28 @@ class Loop {
   }
   void kick() { kick_ = true; }
 
+  // Graceful drain: close the listener (SO_REUSEPORT peers / the next generation keep
+  // accepting), close idle keep-alive connections, let in-flight sessions finish.
+  // Returns true when this loop may exit.
+  bool drain_step() {
+    const double t = now_s();
+    if (!draining_) {
+      draining_ = true;
+      drain_deadline_ = t + cfg_.drain_s;
+      if (lfd_ >= 0) {
+        epoll_ctl(ep_, EPOLL_CTL_DEL, lfd_, nullptr);
+        close(lfd_);
+        lfd_ = -1;
+      }
+    }
+    for (auto& kv : clients_) {
+      Client* c = kv.second.get();
+      if (!c->sess && c->in.empty() && c->out_off >= c->out.size()) mark_close(c);
+    }
+    if (!pending_close_.empty()) reap_clients();
+    return (sessions_.empty() && clients_.empty()) || t > drain_deadline_;
+  }
+
   // ---------------------------------------------------------------- clients
   void on_accept() {
     while (true) {
@@ -698,7 +730,7 @@ class Loop {
         used = he + 4 + clen;
       }
       c->in.erase(0, used);
-      c->keepalive = keepalive;
+      c->keepalive = keepalive && !draining_;
       handle_request(c, method, target, hdrs, body);
       if (!c->sess && !c->keepalive) {
         mark_close(c);
@@ -1804,6 +1836,8 @@ class Loop {
   std::unordered_map<int, std::pair<Session*, int>> fin_owner_;  // fin id → (session, bs index | -1)
   // spread placement
   Exchange* xch_ = nullptr;
+  bool draining_ = false;
+  double drain_deadline_ = 0;
   const std::vector<Loop*>* loops_ = nullptr;
   double last_snap_ = 0;
   int xfd_ = -1;
@@ -1816,7 +1850,10 @@ class Loop {
   std::vector<int> pending_close_, pending_requests_;
 };
 
-void on_signal(int) { g_stop.store(true); }
+void on_signal(int sig) {
+  if (sig == SIGTERM) g_drain.store(true);
+  else g_stop.store(true);
+}
 
 }  // namespace
 
@@ -1841,6 +1878,8 @@ int run_server(const ServerCfg& cfg0) {
     sigaction(SIGINT, &sa, nullptr);
   }
   g_stop.store(false);
+  g_drain.store(false);
+  g_ready.store(0);
   std::vector<std::unique_ptr<Loop>> loops;
   std::vector<std::thread> ts;
   for (int i = 0; i < std::max(1, cfg.threads); ++i) loops.emplace_back(new Loop(cfg, i));

@@ -58,9 +58,14 @@ struct ServerCfg {
   std::string xchg_id_file;
   int xchg_round_us = 200;
   double xchg_timeout = 30.0;
+  // lifecycle: SIGTERM drains (no new connections; in-flight sessions finish, at most
+  // drain_s seconds), SIGINT / stop_server() stop at once; ready_file is written once
+  // every io loop is listening (supervisor rolling reloads)
+  double drain_s = 10.0;
+  std::string ready_file;
 };
 
-// Runs until SIGTERM/SIGINT. Returns 0 on clean shutdown.
+// Runs until SIGINT / stop_server(), or until drained after SIGTERM. Returns 0.
 int run_server(const ServerCfg& cfg);
 std::unordered_map<std::string, double> server_counters();
 void stop_server();  // thread-safe; run_server returns within ~50 ms

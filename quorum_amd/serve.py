@@ -49,7 +49,12 @@ def run_worker(config: str, host: str, port: int, engine: str, device: Optional[
     app = create_app(lambda: cfg, runtime=rt)
     sock = reuseport_socket(host, port)
     ucfg = uvicorn.Config(app, log_level="warning", access_log=False, lifespan="off", http="h11",
-                          loop="asyncio", timeout_keep_alive=60, backlog=4096)
+                          loop="asyncio", timeout_keep_alive=60, backlog=4096,
+                          timeout_graceful_shutdown=int(rt.drain_timeout))
+    ready = os.environ.get("QMX_READY_FILE")
+    if ready:
+        with open(ready + f".{os.getpid()}", "w") as f:
+            f.write(str(os.getpid()))
     uvicorn.Server(ucfg).run(sockets=[sock])
 
 
@@ -87,6 +92,137 @@ def wait_healthy(host: str, port: int, timeout: float = 120.0) -> bool:
     return False
 
 
+class Supervisor:
+    """Per-rank process supervisor: worker generations, rolling reload, restart on crash.
+
+    * SIGHUP  — re-read and validate the config; start a new generation of workers on the
+      same SO_REUSEPORT port; once every new worker reports ready (ready file), SIGTERM
+      the old generation, which drains (no new connections, in-flight sessions finish).
+      An invalid config is rejected and the running generation keeps serving.
+    * SIGTERM / SIGINT — drain and stop every worker, then exit.
+    * A worker of the current generation that dies unexpectedly is restarted (the
+      surviving workers / ranks keep serving meanwhile) with exponential backoff.
+    Reference counterpart: none (uvicorn --reload restarts the process, Makefile:4).
+    """
+
+    def __init__(self, args, config: str):
+        import tempfile
+
+        self.args = args
+        self.config = config
+        self.tmp = tempfile.mkdtemp(prefix="qmx_sup_")
+        self.gen = 0
+        self.current: List[subprocess.Popen] = []
+        self.retiring: List[subprocess.Popen] = []
+        self.stop_requested = False
+        self.reload_requested = False
+        self.restarts = 0
+        self.backoff = 0.5
+        self.active = config  # config the current generation runs (restarts reuse it)
+
+    def validate(self) -> Optional[str]:
+        import yaml
+
+        from .utils.config import validate_config
+
+        try:  # strict: a reload never falls back to the built-in default config
+            with open(self.config) as f:
+                cfg = yaml.safe_load(f)
+            validate_config(cfg)
+            if self.args.impl == "native":
+                from .runtime.native_server import native_config
+
+                native_config(cfg, self.args.host, self.args.port, self.args.engine, self.args.device,
+                              self.args.threads)
+        except Exception as e:  # noqa: BLE001
+            logging.getLogger("qmx.serve").error("config %s rejected: %s", self.config, e)
+            return None
+        snap = os.path.join(self.tmp, f"config.gen{self.gen + 1}.yaml")  # immutable snapshot
+        with open(snap, "w") as f:
+            yaml.safe_dump(cfg, f)
+        return snap
+
+    def spawn(self, n: Optional[int] = None, config: Optional[str] = None) -> List[subprocess.Popen]:
+        self.gen += 1
+        ready = os.path.join(self.tmp, f"gen{self.gen}")
+        env = dict(os.environ)
+        env["QMX_READY_FILE"] = ready
+        procs = spawn_workers(config or self.active, self.args.host, self.args.port, n or self.args.workers, self.args.engine,
+                              self.args.device, self.args.impl, self.args.threads, env=env)
+        for p in procs:
+            p.ready_file = f"{ready}.{p.pid}"  # type: ignore[attr-defined]  (written by the worker)
+        return procs
+
+    def wait_ready(self, procs, timeout: float = 120.0) -> bool:
+        t0 = time.time()
+        while time.time() - t0 < timeout:
+            if any(p.poll() is not None for p in procs):
+                return False
+            if all(os.path.exists(p.ready_file) for p in procs):  # type: ignore[attr-defined]
+                return True
+            time.sleep(0.05)
+        return False
+
+    @staticmethod
+    def term(procs) -> None:
+        for p in procs:
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except OSError:
+                pass
+
+    def reload(self) -> None:
+        snap = self.validate()
+        if snap is None:
+            return
+        new = self.spawn(config=snap)
+        if not self.wait_ready(new):
+            logging.getLogger("qmx.serve").error("new generation failed to start; keeping the old one")
+            self.term(new)
+            self.retiring += new
+            return
+        old, self.current = self.current, new
+        self.active = snap
+        self.term(old)  # drain
+        self.retiring += old
+
+    def run(self) -> int:
+        self.current = self.spawn()
+
+        def on_hup(*_):
+            self.reload_requested = True
+
+        def on_stop(*_):
+            self.stop_requested = True
+
+        signal.signal(signal.SIGHUP, on_hup)
+        signal.signal(signal.SIGTERM, on_stop)
+        signal.signal(signal.SIGINT, on_stop)
+        while True:
+            if self.stop_requested:
+                self.term(self.current + self.retiring)
+                t0 = time.time()
+                while any(p.poll() is None for p in self.current + self.retiring) and time.time() - t0 < 60:
+                    time.sleep(0.05)
+                return 0
+            if self.reload_requested:
+                self.reload_requested = False
+                self.reload()
+            self.retiring = [p for p in self.retiring if p.poll() is None]
+            dead = [p for p in self.current if p.poll() is not None]
+            if dead:
+                self.current = [p for p in self.current if p.poll() is None]
+                time.sleep(self.backoff)
+                self.backoff = min(self.backoff * 2, 30.0)
+                self.restarts += len(dead)
+                logging.getLogger("qmx.serve").warning("restarting %d worker(s) (exit %s)", len(dead),
+                                                       [p.returncode for p in dead])
+                self.current += self.spawn(len(dead) if self.args.impl == "python" else 1)
+            else:
+                self.backoff = max(0.5, self.backoff * 0.9)
+            time.sleep(0.05)
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="qmx serve")
     ap.add_argument("--config", default=None)
@@ -109,22 +245,7 @@ def main(argv=None) -> int:
         from .runtime.native_server import run_native
 
         return run_native(config, args.host, args.port, args.engine, args.device, args.threads)
-    procs = spawn_workers(config, args.host, args.port, args.workers, args.engine, args.device, args.impl,
-                          args.threads)
-
-    def stop(*_):
-        for p in procs:
-            try:
-                os.killpg(p.pid, signal.SIGTERM)
-            except OSError:
-                pass
-
-    signal.signal(signal.SIGTERM, stop)
-    signal.signal(signal.SIGINT, stop)
-    rc = 0
-    for p in procs:
-        rc = p.wait() or rc
-    return rc
+    return Supervisor(args, config).run()
 
 
 if __name__ == "__main__":

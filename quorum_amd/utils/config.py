@@ -212,6 +212,7 @@ class RuntimeConfig:
     exchange_round_us: pacing of the lock-step all-gather rounds while traffic flows
     exchange_timeout: a round slower than this = peer failure (fall back to local placement)
     total_timeout: optional per-backend total deadline in seconds (None = quorum semantics)
+    drain_timeout: SIGTERM grace period for in-flight sessions (rolling reload / shutdown)
     """
 
     engine: str = "auto"
@@ -224,6 +225,7 @@ class RuntimeConfig:
     exchange_round_us: int = 200
     exchange_timeout: float = 30.0
     total_timeout: Optional[float] = None
+    drain_timeout: float = 10.0
     log_content: bool = False
 
     @classmethod

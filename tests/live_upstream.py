@@ -65,6 +65,9 @@ class _Handler(BaseHTTPRequestHandler):
             self.send_header("transfer-encoding", "chunked")
             self.end_headers()
             for c in beh[2]:
+                if isinstance(c, (int, float)):  # pause between chunks (slow upstream)
+                    time.sleep(c)
+                    continue
                 self.wfile.write(b"%x\r\n%s\r\n" % (len(c), c))
                 self.wfile.flush()
             self.wfile.write(b"0\r\n\r\n")

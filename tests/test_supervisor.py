@@ -1,0 +1,170 @@
+"""Process lifecycle: graceful drain (SIGTERM), rolling config reload (SIGHUP), crash restart.
+
+The supervisor (``python -m quorum_amd.serve``) runs worker generations on one
+SO_REUSEPORT port.  A reload starts the new generation, waits until it is listening,
+then drains the old one, so a client hammering the port never sees a failed request;
+a killed worker is restarted; an invalid config is rejected without disturbing service.
+"""
+import os
+import signal
+import subprocess
+import sys
+import threading
+import time
+
+import httpx
+import pytest
+import yaml
+
+from quorum_amd.ops import native
+
+from conftest import cfg_parallel, sse_stream
+from live_upstream import LiveUpstream, free_port
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+AUTH = {"Authorization": "Bearer k"}
+MSG = [{"role": "user", "content": "hi"}]
+BLOCK = {"separator": "\n--\n", "hide_intermediate_think": True, "hide_final_think": False,
+         "thinking_tags": ["think"], "skip_final_aggregation": False}
+
+
+def _write(path, urls, drain=5.0):
+    cfg = cfg_parallel(len(urls), block=BLOCK)
+    for b, u in zip(cfg["primary_backends"], urls):
+        b["url"] = u
+    cfg["runtime"] = {"drain_timeout": drain}
+    with open(path, "w") as f:
+        yaml.safe_dump(cfg, f)
+
+
+def _final(text):
+    for seg in text.split("\n\n"):
+        if '"chatcmpl-parallel-final"' in seg:
+            import json
+            return json.loads(seg[6:])["choices"][0]["delta"]["content"]
+    return None
+
+
+def _post(port):
+    return httpx.post(f"http://127.0.0.1:{port}/chat/completions", json={"messages": MSG, "stream": True},
+                      headers=AUTH, timeout=20)
+
+
+def _wait(port, pred, timeout=60):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        try:
+            r = _post(port)
+            if pred(r):
+                return r
+        except httpx.HTTPError:
+            pass
+        time.sleep(0.05)
+    raise AssertionError("condition not reached")
+
+
+@pytest.mark.parametrize("impl", ["native", "python"])
+def test_reload_drain_restart(tmp_path, impl):
+    if impl == "native" and not native.available():
+        pytest.skip("native extension not built")
+    live = LiveUpstream()
+    pa = live.serve("a", ("stream", 200, sse_stream(["AAA"])))
+    pb = live.serve("b", ("stream", 200, sse_stream(["BBB"])))
+    cfg = str(tmp_path / "config.yaml")
+    _write(cfg, [f"http://127.0.0.1:{pa}/v1", f"http://127.0.0.1:{pa}/v1"])
+    port = free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT, QMX_ENGINE="cpu" if impl == "native" else "python")
+    sup = subprocess.Popen([sys.executable, "-m", "quorum_amd.serve", "--impl", impl, "--engine",
+                            "cpu" if impl == "native" else "python", "--config", cfg, "--port", str(port),
+                            "--workers", "2", "--threads", "2"], cwd=ROOT, env=env, start_new_session=True)
+    errors, stop = [], threading.Event()
+
+    def hammer():
+        while not stop.is_set():
+            try:
+                r = _post(port)
+                if r.status_code != 200 or _final(r.text) is None:
+                    errors.append(r.status_code)
+            except httpx.HTTPError as e:
+                errors.append(repr(e))
+
+    try:
+        assert _final(_wait(port, lambda r: r.status_code == 200).text) == "AAA\n\n--\nAAA"
+        th = threading.Thread(target=hammer)
+        th.start()
+        # 1. rolling reload to backend b: no failed request while generations swap
+        _write(cfg, [f"http://127.0.0.1:{pb}/v1", f"http://127.0.0.1:{pb}/v1"])
+        os.kill(sup.pid, signal.SIGHUP)
+        _wait(port, lambda r: _final(r.text) == "BBB\n\n--\nBBB")
+        time.sleep(0.5)
+        # 2. an invalid config is rejected; the current generation keeps serving
+        with open(cfg, "w") as f:
+            f.write("primary_backends: [unclosed\n")
+        os.kill(sup.pid, signal.SIGHUP)
+        time.sleep(1.0)
+        assert _final(_post(port).text) == "BBB\n\n--\nBBB"
+        stop.set()
+        th.join()
+        assert errors == [], errors[:5]
+        # 3. crash restart: kill every worker process of the supervisor
+        out = subprocess.run(["pgrep", "-P", str(sup.pid)], capture_output=True, text=True).stdout.split()
+        assert out
+        for pid in out:
+            os.kill(int(pid), signal.SIGKILL)
+        _wait(port, lambda r: _final(r.text) == "BBB\n\n--\nBBB")
+    finally:
+        stop.set()
+        # 4. graceful stop
+        os.kill(sup.pid, signal.SIGTERM)
+        try:
+            rc = sup.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            os.killpg(sup.pid, signal.SIGKILL)
+            rc = None
+        live.close()
+    assert rc == 0
+
+
+def test_native_drain_finishes_inflight(tmp_path):
+    """SIGTERM to a native worker: the listener closes at once, an in-flight slow stream
+    still completes, then the process exits 0."""
+    if not native.available():
+        pytest.skip("native extension not built")
+    import json as _j
+
+    slow = []
+    for i in range(6):  # numbers = pauses (seconds) between upstream chunks
+        slow += [b"data: " + _j.dumps({"choices": [{"delta": {"content": f"t{i} "}}]}).encode() + b"\n\n", 0.2]
+    slow += [b"data: [DONE]\n\n"]
+    live = LiveUpstream()
+    pa = live.serve("a", ("stream", 200, slow))
+    cfg = str(tmp_path / "config.yaml")
+    _write(cfg, [f"http://127.0.0.1:{pa}/v1"] * 2)
+    port = free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    w = subprocess.Popen([sys.executable, "-m", "quorum_amd.serve", "--native-worker", "--engine", "cpu", "--config",
+                          cfg, "--port", str(port), "--threads", "1"], cwd=ROOT, env=env, start_new_session=True)
+    try:
+        _wait(port, lambda r: r.status_code == 200)
+        res = {}
+
+        def client():
+            with httpx.Client() as c:
+                with c.stream("POST", f"http://127.0.0.1:{port}/chat/completions",
+                              json={"messages": MSG, "stream": True}, headers=AUTH, timeout=20) as r:
+                    res["status"] = r.status_code
+                    res["body"] = b"".join(r.iter_bytes())
+        th = threading.Thread(target=client)
+        th.start()
+        time.sleep(0.3)
+        os.kill(w.pid, signal.SIGTERM)
+        th.join(timeout=20)
+        assert res.get("status") == 200
+        assert res["body"].rstrip().endswith(b"data: [DONE]")
+        assert w.wait(timeout=20) == 0
+        with pytest.raises(httpx.HTTPError):
+            _post(port)
+    finally:
+        if w.poll() is None:
+            os.killpg(w.pid, signal.SIGKILL)
+        live.close()
