@@ -96,7 +96,7 @@ ServerCfg server_cfg_from(const py::dict& d) {
   gi("rank", c.rank); gi("world", c.world); gs("placement", c.placement); gs("xchg", c.xchg);
   gs("xchg_addr", c.xchg_addr); gi("xchg_port", c.xchg_port); gs("xchg_id_file", c.xchg_id_file);
   gi("xchg_round_us", c.xchg_round_us); gd("xchg_timeout", c.xchg_timeout);
-  gd("drain_s", c.drain_s); gs("ready_file", c.ready_file);
+  gd("drain_s", c.drain_s); gs("ready_file", c.ready_file); gb("verify", c.verify);
   if (d.contains("backends")) {
     for (auto item : py::cast<py::list>(d["backends"])) {
       py::dict b = py::cast<py::dict>(item);

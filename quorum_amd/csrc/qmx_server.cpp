@@ -325,6 +325,137 @@ struct ResultBatch {
 };
 
 // --------------------------------------------------------------------------------------
+// verify mode (QMX_VERIFY / runtime.verify): a shadow C++ CPU engine sees every open / feed /
+// finish / finalize of the primary (HIP) engine and is ticked right after it; per-stream
+// SSE output, terminal flags and finalize results must be byte-identical (the SURVEY §5.2
+// "run the CPU oracle on every tick and compare" debug mode).  Mismatches are counted in
+// /metrics and logged.
+// --------------------------------------------------------------------------------------
+std::atomic<uint64_t> c_verify_checked{0}, c_verify_mismatch{0};
+
+class Verifier {
+ public:
+  explicit Verifier(const std::vector<std::string>& tags) : cpu_(tags) {}
+  void open(int slot, int index, bool f, bool e) {
+    std::lock_guard<std::mutex> g(mu_);
+    Track t;
+    t.shadow = cpu_.open(index, f, e);
+    rmap_[t.shadow] = slot;
+    map_[slot] = std::move(t);
+  }
+  void feed(int slot, const std::string& d) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = map_.find(slot);
+    if (it != map_.end()) cpu_.feed(it->second.shadow, d);
+  }
+  void finish(int slot) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = map_.find(slot);
+    if (it != map_.end()) cpu_.finish(it->second.shadow);
+  }
+  void release(int slot) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = map_.find(slot);
+    if (it == map_.end()) return;
+    rmap_.erase(it->second.shadow);
+    cpu_.release(it->second.shadow);
+    map_.erase(it);
+  }
+  void submit(int fid, const std::vector<int>& slots, bool strip, bool texts, const std::string& joiner,
+              int64_t created) {
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<int> sh;
+    for (int s : slots) {
+      auto it = map_.find(s);
+      if (it == map_.end()) return;  // not tracked (opened before verify): skip
+      sh.push_back(it->second.shadow);
+    }
+    fin_[cpu_.submit_finalize(sh, strip, texts, joiner, created)] = fid;
+  }
+  // tick thread, right after the primary engine's tick(created)
+  void check(int64_t created, const std::vector<SlotResult>& r, const std::vector<FinalizeRes>& f) {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& x : r) {
+      auto it = map_.find(x.slot);
+      if (it == map_.end()) continue;
+      it->second.acc[0] += x.sse;
+      it->second.term[0] |= x.flags & (RF_DONE | RF_ABORTED);
+    }
+    for (auto& x : f) pfin_[x.id] = x;
+    std::vector<SlotResult> sr;
+    std::vector<FinalizeRes> sf;
+    for (int k = 0; k < 64 && cpu_.has_work(); ++k) cpu_.tick(created, sr, sf);
+    for (auto& x : sr) {
+      auto rit = rmap_.find(x.slot);
+      if (rit == rmap_.end()) continue;
+      Track& t = map_[rit->second];
+      t.acc[1] += x.sse;
+      t.term[1] |= x.flags & (RF_DONE | RF_ABORTED);
+    }
+    for (auto& kv : map_) {
+      Track& t = kv.second;
+      if (t.compared || !t.term[0] || !t.term[1]) continue;
+      t.compared = true;
+      c_verify_checked++;
+      if (t.term[0] != t.term[1] || norm(t.acc[0]) != norm(t.acc[1])) report("stream", kv.first, t.acc[0], t.acc[1]);
+    }
+    for (auto& x : sf) {
+      auto it = fin_.find(x.id);
+      if (it == fin_.end()) continue;
+      sfin_[it->second] = x;
+      fin_.erase(it);
+    }
+    for (auto it = sfin_.begin(); it != sfin_.end();) {
+      auto p = pfin_.find(it->first);
+      if (p == pfin_.end()) {
+        ++it;
+        continue;
+      }
+      c_verify_checked++;
+      const FinalizeRes &a = p->second, &b = it->second;
+      if (a.kind != b.kind || norm(a.event) != norm(b.event) || a.texts != b.texts)
+        report("finalize", a.id, a.event, b.event);
+      pfin_.erase(p);
+      it = sfin_.erase(it);
+    }
+  }
+
+ private:
+  struct Track {
+    int shadow = -1;
+    std::string acc[2];
+    int term[2] = {0, 0};
+    bool compared = false;
+  };
+  // a stream's bytes can straddle a one-second boundary differently in the two engines
+  static std::string norm(const std::string& x) {
+    std::string o;
+    o.reserve(x.size());
+    static const std::string key = "\"created\": ";
+    for (size_t i = 0; i < x.size();) {
+      if (x.compare(i, key.size(), key) == 0) {
+        o += key;
+        i += key.size();
+        while (i < x.size() && x[i] >= '0' && x[i] <= '9') ++i;
+        continue;
+      }
+      o.push_back(x[i++]);
+    }
+    return o;
+  }
+  void report(const char* what, int id, const std::string& a, const std::string& b) {
+    if (c_verify_mismatch++ < 20)
+      fprintf(stderr, "qmx verify: %s %d differs (primary %zu B, cpu oracle %zu B)\n  primary: %.300s\n  oracle:  %.300s\n",
+              what, id, a.size(), b.size(), a.c_str(), b.c_str());
+  }
+  std::mutex mu_;
+  CpuEngine cpu_;
+  std::unordered_map<int, Track> map_;
+  std::unordered_map<int, int> rmap_, fin_;
+  std::unordered_map<int, FinalizeRes> pfin_, sfin_;
+};
+
+// --------------------------------------------------------------------------------------
 // io loop (one per thread)
 // --------------------------------------------------------------------------------------
 class Loop {
@@ -425,6 +556,7 @@ class Loop {
       eng_.reset(new CpuEngine(cfg_.tags));
       offload_ = false;
     }
+    if (cfg_.verify) ver_.reset(new Verifier(cfg_.tags));
   }
 
   // epoll tags: fd in low 32 bits, kind in high bits
@@ -474,8 +606,10 @@ class Loop {
       while (eng_->has_work()) {
         ResultBatch rb;
         const double tt = now_s();
-        eng_->tick((int64_t)time(nullptr), rb.r, rb.f);
+        const int64_t created = (int64_t)time(nullptr);
+        eng_->tick(created, rb.r, rb.f);
         h_tick.observe(now_s() - tt);
+        if (ver_) ver_->check(created, rb.r, rb.f);
         if (tt - last_snap_ > 0.05) {
           snapshot();
           last_snap_ = tt;
@@ -496,8 +630,10 @@ class Loop {
   void tick_inline() {
     ResultBatch rb;
     const double tt = now_s();
-    eng_->tick((int64_t)time(nullptr), rb.r, rb.f);
+    const int64_t created = (int64_t)time(nullptr);
+    eng_->tick(created, rb.r, rb.f);
     h_tick.observe(now_s() - tt);
+    if (ver_) ver_->check(created, rb.r, rb.f);
     c_ticks++;
     c_tick_slots += rb.r.size();
     apply(rb);
@@ -542,6 +678,29 @@ class Loop {
     }
   }
   void kick() { kick_ = true; }
+  // engine calls, mirrored into the verify shadow when enabled
+  int e_open(int index, bool f, bool e) {
+    int slot = eng_->open(index, f, e);
+    if (ver_) ver_->open(slot, index, f, e);
+    return slot;
+  }
+  void e_feed(int slot, const std::string& d) {
+    eng_->feed(slot, d);
+    if (ver_) ver_->feed(slot, d);
+  }
+  void e_finish(int slot) {
+    eng_->finish(slot);
+    if (ver_) ver_->finish(slot);
+  }
+  void e_release(int slot) {
+    eng_->release(slot);
+    if (ver_) ver_->release(slot);
+  }
+  int e_submit(const std::vector<int>& slots, bool strip, bool texts, const std::string& joiner, int64_t created) {
+    int id = eng_->submit_finalize(slots, strip, texts, joiner, created);
+    if (ver_) ver_->submit(id, slots, strip, texts, joiner, created);
+    return id;
+  }
 
   // Graceful drain: close the listener (SO_REUSEPORT peers / the next generation keep
   // accepting), close idle keep-alive connections, let in-flight sessions finish.
@@ -1034,7 +1193,7 @@ class Loop {
   void on_up_body(Up* u, const std::string& body) {
     Session* s = u->sess;
     if (u->rp.status == 200 && u->mode == UP_ENGINE) {
-      eng_->feed(s->bs[u->bi].slot, body);
+      e_feed(s->bs[u->bi].slot, body);
       kick();
       return;
     }
@@ -1052,7 +1211,7 @@ class Loop {
     if (bi >= 0) s->bs[bi].up = nullptr;
     else s->agg = nullptr;
     if (mode == UP_ENGINE && status == 200) {
-      eng_->finish(s->bs[bi].slot);
+      e_finish(s->bs[bi].slot);
       kick();
       return;
     }
@@ -1193,7 +1352,7 @@ class Loop {
         s->remote_n++;
         continue;
       }
-      s->bs[i].slot = eng_->open((int)i, s->filter, s->emit);
+      s->bs[i].slot = e_open((int)i, s->filter, s->emit);
       slot_owner_[s->bs[i].slot] = {s, (int)i};
     }
     for (size_t i = 0; i < valid.size(); ++i) {
@@ -1238,7 +1397,7 @@ class Loop {
         post_owner(s, X_FINAL, b.aborted ? XF_ABORTED : 0, 0, std::string());
         return end_session(s);
       }
-      s->fin_id = eng_->submit_finalize({b.slot}, cfg_.hide_final, true, std::string(), (int64_t)time(nullptr));
+      s->fin_id = e_submit({b.slot}, cfg_.hide_final, true, std::string(), (int64_t)time(nullptr));
       fin_owner_[s->fin_id] = {s, -1};
       kick();
       return;
@@ -1248,7 +1407,7 @@ class Loop {
       for (int i = 0; i < (int)s->bs.size(); ++i) {
         const BState& b = s->bs[i];
         if (b.remote >= 0 || b.state != 1 || b.aborted) continue;
-        int id = eng_->submit_finalize({b.slot}, cfg_.hide_final, true, std::string(), (int64_t)time(nullptr));
+        int id = e_submit({b.slot}, cfg_.hide_final, true, std::string(), (int64_t)time(nullptr));
         fin_owner_[id] = {s, i};
         s->fin_pending++;
       }
@@ -1259,7 +1418,7 @@ class Loop {
     std::vector<int> g = good_slots(s);
     bool texts = !cfg_.aggregator_name.empty();
     s->fin_texts = texts;
-    s->fin_id = eng_->submit_finalize(g, cfg_.hide_final, texts, "\n" + cfg_.separator, (int64_t)time(nullptr));
+    s->fin_id = e_submit(g, cfg_.hide_final, texts, "\n" + cfg_.separator, (int64_t)time(nullptr));
     fin_owner_[s->fin_id] = {s, -1};
     kick();
   }
@@ -1336,7 +1495,7 @@ class Loop {
         s->emit = (m.flags & 2) != 0;
         s->bs.resize(1);
         s->bs[0].backend = m.a;
-        s->bs[0].slot = eng_->open(m.bi, s->filter, s->emit);
+        s->bs[0].slot = e_open(m.bi, s->filter, s->emit);
         slot_owner_[s->bs[0].slot] = {s, 0};
         shadow_[{m.skey, m.bi}] = s;
         c_remote_streams++;
@@ -1756,7 +1915,7 @@ class Loop {
       }
       if (b.slot >= 0) {
         slot_owner_.erase(b.slot);
-        eng_->release(b.slot);
+        e_release(b.slot);
         b.slot = -1;
       }
     }
@@ -1798,6 +1957,8 @@ class Loop {
     m += "qmx_upstream_failures_by_class_total{class=\"disconnect\"} " + std::to_string(c_fail_disconnect.load()) + "\n";
     m += "qmx_upstream_failures_by_class_total{class=\"protocol\"} " + std::to_string(c_fail_protocol.load()) + "\n";
     put("qmx_stream_aborts_total", (double)c_stream_aborts.load());
+    put("qmx_verify_checked_total", (double)c_verify_checked.load());
+    put("qmx_verify_mismatches_total", (double)c_verify_mismatch.load());
     h_ttft.render(m, "qmx_ttft_seconds");
     h_latency.render(m, "qmx_request_latency_seconds");
     h_tick.render(m, "qmx_tick_seconds");
@@ -1822,6 +1983,7 @@ class Loop {
   int idx_;
   int ep_ = -1, lfd_ = -1, evfd_ = -1;
   std::unique_ptr<HostEngine> eng_;
+  std::unique_ptr<Verifier> ver_;
   bool offload_ = false, kick_ = false;
   std::thread gpu_thread_;
   std::mutex mu_, rmu_;
@@ -1928,7 +2090,9 @@ void stop_server() { g_stop.store(true); }
 
 std::unordered_map<std::string, double> server_counters() {
   return {{"requests", (double)c_requests.load()}, {"errors", (double)c_errors.load()},
-          {"ticks", (double)c_ticks.load()}, {"upstream_failures", (double)c_up_fail.load()}};
+          {"ticks", (double)c_ticks.load()}, {"upstream_failures", (double)c_up_fail.load()},
+          {"verify_checked", (double)c_verify_checked.load()},
+          {"verify_mismatches", (double)c_verify_mismatch.load()}};
 }
 
 }  // namespace qmx

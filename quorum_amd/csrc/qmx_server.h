@@ -63,6 +63,7 @@ struct ServerCfg {
   // every io loop is listening (supervisor rolling reloads)
   double drain_s = 10.0;
   std::string ready_file;
+  bool verify = false;  // shadow CPU oracle engine compares every stream + finalize result
 };
 
 // Runs until SIGINT / stop_server(), or until drained after SIGTERM. Returns 0.

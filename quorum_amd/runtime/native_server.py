@@ -65,7 +65,7 @@ def native_config(cfg: Dict[str, Any], host: str, port: int, engine: str, device
         "include_source_names": bool(agg.include_source_names),
         "env_api_key": os.environ.get("OPENAI_API_KEY", ""),
         "backends": backends,
-        "drain_s": float(rt.drain_timeout), "ready_file": (os.environ["QMX_READY_FILE"] + f".{os.getpid()}") if os.environ.get("QMX_READY_FILE") else "",
+        "drain_s": float(rt.drain_timeout), "verify": bool(rt.verify), "ready_file": (os.environ["QMX_READY_FILE"] + f".{os.getpid()}") if os.environ.get("QMX_READY_FILE") else "",
         **cluster_config(rt, port, engine),
     }
 

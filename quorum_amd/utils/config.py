@@ -213,6 +213,7 @@ class RuntimeConfig:
     exchange_timeout: a round slower than this = peer failure (fall back to local placement)
     total_timeout: optional per-backend total deadline in seconds (None = quorum semantics)
     drain_timeout: SIGTERM grace period for in-flight sessions (rolling reload / shutdown)
+    verify:    debug mode: a shadow CPU oracle engine checks every stream and final (QMX_VERIFY=1)
     """
 
     engine: str = "auto"
@@ -226,6 +227,7 @@ class RuntimeConfig:
     exchange_timeout: float = 30.0
     total_timeout: Optional[float] = None
     drain_timeout: float = 10.0
+    verify: bool = False
     log_content: bool = False
 
     @classmethod
@@ -236,5 +238,7 @@ class RuntimeConfig:
             rt["engine"] = env_engine
         if os.environ.get("QMX_PLACEMENT"):
             rt["placement"] = os.environ["QMX_PLACEMENT"]
+        if os.environ.get("QMX_VERIFY"):
+            rt["verify"] = os.environ["QMX_VERIFY"] not in ("0", "", "false")
         known = {k: v for k, v in rt.items() if k in cls.__dataclass_fields__}
         return cls(**known)

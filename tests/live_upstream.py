@@ -103,8 +103,11 @@ class LiveUpstream:
 
 
 @contextlib.contextmanager
-def native_server(cfg: Dict[str, Any], engine: str = "cpu", threads: int = 1, env_key: str = ""):
-    """Run the C++ data plane in-process (background thread) for one config."""
+def native_server(cfg: Dict[str, Any], engine: str = "cpu", threads: int = 1, env_key: str = "",
+                  verify: bool = False):
+    """Run the C++ data plane in-process (background thread) for one config.
+
+    verify: run the shadow CPU-oracle engine (server_counters()['verify_mismatches'])."""
     import http.client
     import os
 
@@ -116,6 +119,7 @@ def native_server(cfg: Dict[str, Any], engine: str = "cpu", threads: int = 1, en
     d = native_config(cfg, "127.0.0.1", port, engine, 0, threads)
     d["install_signals"] = False
     d["env_api_key"] = env_key
+    d["verify"] = verify
     th = threading.Thread(target=ext.run_server, args=(d,), daemon=True)
     th.start()
     t0 = time.time()

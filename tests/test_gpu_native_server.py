@@ -8,8 +8,16 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("name", sorted(T.SCENARIOS))
 def test_native_hip_matches_python(name, monkeypatch):
+    """HIP engine + verify mode: every stream and final is also checked against the
+    shadow C++ CPU oracle inside the server (byte-identical or counted as mismatch)."""
+    from quorum_amd.ops import native
+
+    ext = native.require()
+    before = ext.server_counters()["verify_mismatches"]
     monkeypatch.setattr(T, "ENGINE", "hip")
+    monkeypatch.setattr(T, "VERIFY", True)
     T.test_native_matches_python(name)
+    assert ext.server_counters()["verify_mismatches"] == before
 
 
 def test_native_hip_keepalive(monkeypatch):

@@ -19,6 +19,7 @@ from live_upstream import LiveUpstream, native_server
 
 pytestmark = pytest.mark.skipif(not native.available(), reason="native extension not built")
 ENGINE = os.environ.get("QMX_NATIVE_TEST_ENGINE", "cpu")
+VERIFY = False  # GPU runs set this: the shadow CPU oracle checks every stream / final
 
 AUTH = {"Authorization": "Bearer test-key"}
 MSG = [{"role": "user", "content": "What is 2+2?"}]
@@ -198,7 +199,7 @@ def _native_side(cfg, ups, req, hdrs):
             if host and host in ups:
                 port = live.serve(host, ups[host])
                 b["url"] = f"http://127.0.0.1:{port}/v1"
-        with native_server(cfg, engine=ENGINE) as port:
+        with native_server(cfg, engine=ENGINE, verify=VERIFY) as port:
             r = httpx.post(f"http://127.0.0.1:{port}/chat/completions", json=req, headers=hdrs, timeout=30)
             return _normalize(r.status_code, r.headers.get("content-type"), r.content), live.calls
     finally:
@@ -293,3 +294,26 @@ def test_native_metrics_histograms_and_failure_classes():
     assert val("qmx_upstream_ttfb_seconds_count") >= 3
     assert val('qmx_upstream_failures_by_class_total{class="connect"}') >= 3
     assert val("qmx_engine_") >= 0  # engine stats are exported
+
+
+def test_native_verify_mode_plumbing():
+    """Verify mode with the CPU engine: the shadow oracle checks streams and finals."""
+    ext = native.require()
+    before = ext.server_counters()
+    live = LiveUpstream()
+    p1 = live.serve("b1", ("stream", 200, THINK))
+    p2 = live.serve("b2", ("stream", 200, sse_stream(["Wor", "ld"])))
+    cfg = cfg_parallel(2, block=dict(CONCAT, hide_final_think=True))
+    cfg["primary_backends"][0]["url"] = f"http://127.0.0.1:{p1}/v1"
+    cfg["primary_backends"][1]["url"] = f"http://127.0.0.1:{p2}/v1"
+    try:
+        with native_server(cfg, verify=True) as port:
+            for _ in range(4):
+                r = httpx.post(f"http://127.0.0.1:{port}/chat/completions", json={"messages": MSG, "stream": True},
+                               headers=AUTH, timeout=30)
+                assert r.status_code == 200
+    finally:
+        live.close()
+    after = ext.server_counters()
+    assert after["verify_checked"] - before["verify_checked"] >= 12  # 8 streams + 4 finals
+    assert after["verify_mismatches"] == before["verify_mismatches"]
