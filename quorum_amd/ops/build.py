@@ -131,16 +131,61 @@ def _build_tools(verbose: bool = False) -> list:
     return out
 
 
+# Sanitizer builds of the host runtime.  Device code is never sanitized:
+# every -fsanitize= goes after -Xarch_host so hipcc applies it to host compilation only.
+SAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+             "-Xarch_host", "-fno-omit-frame-pointer", "-Xarch_host", "-fno-sanitize-recover=undefined"]
+SAN_TARGETS = {
+    "qmx_fuzz_asan": (["tools/csrc/fuzz_host.cpp", "csrc/qmx_engine.cpp", "csrc/qmx_json.cpp"], []),
+    "qmx_server_asan": (["tools/csrc/server_main.cpp", "csrc/qmx_server.cpp", "csrc/qmx_engine.cpp",
+                         "csrc/qmx_json.cpp", "csrc/qmx_exchange.cpp", "csrc/qmx_hip.hip"],
+                        ["-L/opt/rocm/lib", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx",
+                         "-Wl,-rpath,/opt/rocm/lib", "-pthread"]),
+}
+
+
+def build_sanitized(verbose: bool = False) -> list:
+    """ASan+UBSan host builds -> quorum_amd/bin/qmx_fuzz_asan, qmx_server_asan."""
+    with _BuildLock():
+        BIN.mkdir(exist_ok=True)
+        cc = hipcc()
+        newest_hdr = max((h.stat().st_mtime for h in CSRC.glob("*.h")), default=0)
+        out = []
+
+        def one(item):
+            name, (srcs, libs) = item
+            b = BIN / name
+            paths = [PKG / x for x in srcs]
+            if b.exists() and b.stat().st_mtime > max([newest_hdr] + [x.stat().st_mtime for x in paths]):
+                return b
+            cmd = [cc, "-x", "hip", f"--offload-arch={ARCH}", "-O1", "-g", "-std=c++17", f"-I{CSRC}"] + SAN_FLAGS + \
+                [str(x) for x in paths] + ["-o", str(b), "-fsanitize=address", "-fsanitize=undefined"] + libs
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"sanitizer build failed: {name}\n{r.stderr[-4000:]}")
+            return b
+
+        with cf.ThreadPoolExecutor(max_workers=2) as ex:
+            out = list(ex.map(one, SAN_TARGETS.items()))
+        return out
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--jobs", type=int, default=3)
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--sanitize", action="store_true", help="also build the ASan/UBSan host binaries")
     args = ap.parse_args(argv)
     path = build(args.debug, args.jobs, args.verbose)
     print(path)
     for t in build_tools(args.verbose):
         print(t)
+    if args.sanitize:
+        for t in build_sanitized(args.verbose):
+            print(t)
     return 0
 
 

@@ -1,0 +1,151 @@
+"""ASan + UBSan builds of the host runtime (GPU sanitizers are not used).
+
+* qmx_fuzz_asan: streaming-invariance / JSON round-trip fuzzer over the C++ engine + DOM.
+* qmx_server_asan: the standalone C++ data plane under traffic that exercises every
+  connection-lifetime path — parallel streams, aborts (content:null), upstream 5xx,
+  refused connections, mid-stream disconnects, client disconnects mid-response,
+  keep-alive reuse, aggregator calls — then a clean SIGINT shutdown.  Any ASan/UBSan
+  report fails the test.
+"""
+import json
+import os
+import signal
+import socket
+import subprocess
+import time
+
+import httpx
+import pytest
+
+from quorum_amd.ops import native
+
+from conftest import cfg_parallel, completion, sse_chunk, sse_stream
+from live_upstream import LiveUpstream, free_port
+
+pytestmark = pytest.mark.skipif(not native.available(), reason="native toolchain/extension not built")
+ASAN_ENV = {"ASAN_OPTIONS": "detect_leaks=0:abort_on_error=0:halt_on_error=1",
+            "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1"}
+
+
+@pytest.fixture(scope="module")
+def san_bins():
+    from quorum_amd.ops import build
+
+    return {p.name: p for p in build.build_sanitized()}
+
+
+def test_fuzz_host_asan(san_bins):
+    for seed in ("1", "20260101"):
+        r = subprocess.run([str(san_bins["qmx_fuzz_asan"]), "1500", seed], capture_output=True, text=True,
+                           timeout=300, env=dict(os.environ, **ASAN_ENV))
+        assert r.returncode == 0, r.stderr[-3000:]
+        assert json.loads(r.stdout.strip().splitlines()[-1])["failures"] == 0
+        assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
+
+
+def test_server_asan_traffic(san_bins, tmp_path):
+    from quorum_amd.runtime.native_server import native_config
+
+    live = LiveUpstream()
+    stream = sse_stream(["Hel", "lo <think>x</think> wor", "ld"])
+    ports = {
+        "ok": live.serve("ok", ("stream", 200, stream)),
+        "null": live.serve("null", ("stream", 200, [sse_chunk({"content": "a"}), sse_chunk({"content": None}),
+                                                      sse_chunk({"content": "b"}), b"data: [DONE]\n\n"])),
+        "e500": live.serve("e500", ("json", 500, {"error": {"message": "boom"}})),
+        "refused": live.serve("refused", ("refuse",)),
+        "agg": live.serve("agg", lambda body: (("stream", 200, stream) if body.get("stream")
+                                               else ("json", 200, completion("SYNTH")))),
+    }
+    # a backend that drops the connection mid-stream
+    drop_srv = socket.socket()
+    drop_srv.bind(("127.0.0.1", 0))
+    drop_srv.listen(64)
+    drop_port = drop_srv.getsockname()[1]
+    import threading
+
+    def dropper():
+        while True:
+            try:
+                c, _ = drop_srv.accept()
+            except OSError:
+                return
+            c.recv(65536)
+            c.sendall(b"HTTP/1.1 200 OK\r\ncontent-type: text/event-stream\r\ntransfer-encoding: chunked\r\n\r\n"
+                      b"20\r\ndata: {\"choices\": [{\"delta\": {\"con")
+            c.close()
+    threading.Thread(target=dropper, daemon=True).start()
+
+    urls = [f"http://127.0.0.1:{ports[k]}/v1" for k in ("ok", "null", "e500", "refused", "agg")]
+    urls.append(f"http://127.0.0.1:{drop_port}/v1")
+    block = {"separator": "\n--\n", "hide_intermediate_think": True, "hide_final_think": True,
+             "thinking_tags": ["think"], "skip_final_aggregation": False}
+    cfgs = {
+        "concat": cfg_parallel(6, block=block),
+        "aggregate": cfg_parallel(6, strategy="aggregate",
+                                  block={"aggregator_backend": "LLM5", "prompt_template": "P {responses}"}),
+    }
+    for cfg in cfgs.values():
+        for b, u in zip(cfg["primary_backends"], urls):
+            b["url"] = u
+    errs = []
+    try:
+        for name, cfg in cfgs.items():
+            port = free_port()
+            d = native_config(cfg, "127.0.0.1", port, "cpu", 0, 2)
+            d["env_api_key"] = ""
+            path = tmp_path / f"{name}.json"
+            path.write_text(json.dumps(d))
+            srv = subprocess.Popen([str(san_bins["qmx_server_asan"]), str(path)], stderr=subprocess.PIPE,
+                                   env=dict(os.environ, **ASAN_ENV))
+            try:
+                t0 = time.time()
+                while time.time() - t0 < 30:
+                    try:
+                        if httpx.get(f"http://127.0.0.1:{port}/health", timeout=1).status_code == 200:
+                            break
+                    except httpx.HTTPError:
+                        time.sleep(0.05)
+                req = {"messages": [{"role": "user", "content": "q"}], "stream": True}
+                hdr = {"Authorization": "Bearer k"}
+                with httpx.Client(base_url=f"http://127.0.0.1:{port}") as c:
+                    for i in range(20):
+                        r = c.post("/chat/completions", json=req, headers=hdr, timeout=30)
+                        assert r.status_code == 200 and r.text.rstrip().endswith("data: [DONE]")
+                        r = c.post("/v1/chat/completions", json={"messages": req["messages"]}, headers=hdr,
+                                   timeout=30)
+                        assert r.status_code in (200, 500)
+                # clients that vanish mid-response
+                for i in range(10):
+                    s = socket.create_connection(("127.0.0.1", port))
+                    body = json.dumps(req).encode()
+                    s.sendall(b"POST /chat/completions HTTP/1.1\r\nhost: x\r\nauthorization: Bearer k\r\n"
+                              b"content-type: application/json\r\ncontent-length: %d\r\n\r\n%s" % (len(body), body))
+                    if i % 2:
+                        s.recv(64)
+                    s.close()
+                # garbage requests
+                for junk in (b"GARBAGE\r\n\r\n", b"POST /chat/completions HTTP/1.1\r\ncontent-length: 5\r\n\r\n{bad}"):
+                    s = socket.create_connection(("127.0.0.1", port))
+                    s.sendall(junk)
+                    s.settimeout(5)
+                    try:
+                        s.recv(4096)
+                    except OSError:
+                        pass
+                    s.close()
+                assert httpx.get(f"http://127.0.0.1:{port}/metrics").status_code == 200
+            finally:
+                srv.send_signal(signal.SIGINT)
+                try:
+                    _, err = srv.communicate(timeout=30)
+                except subprocess.TimeoutExpired:
+                    srv.kill()
+                    _, err = srv.communicate()
+                err = err.decode(errors="replace")
+                if srv.returncode != 0 or "AddressSanitizer" in err or "runtime error" in err:
+                    errs.append((name, srv.returncode, err[-4000:]))
+    finally:
+        drop_srv.close()
+        live.close()
+    assert not errs, errs
