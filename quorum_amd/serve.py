@@ -2,6 +2,7 @@
 
     python -m quorum_amd.serve --config config.yaml --port 8000 --workers 4 [--device 0]
                                [--engine hip|cpu|python|auto] [--impl python|native]
+                               [--gpus N]     # one rank (supervisor + workers) per GPU
 
 Each worker owns its own stream engine (for ``hip``: its own HIP stream, device-resident
 slot arena and pinned arenas on the rank's GPU).  The kernel's SO_REUSEPORT hashing
@@ -233,6 +234,7 @@ def main(argv=None) -> int:
     ap.add_argument("--engine", default="auto")
     ap.add_argument("--device", type=int, default=None)
     ap.add_argument("--impl", default="python", choices=["python", "native"])
+    ap.add_argument("--gpus", type=int, default=1, help="rank processes on this node (one per GPU)")
     ap.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--native-worker", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
@@ -245,7 +247,36 @@ def main(argv=None) -> int:
         from .runtime.native_server import run_native
 
         return run_native(config, args.host, args.port, args.engine, args.device, args.threads)
+    if args.gpus > 1 and "QMX_RANK" not in os.environ:
+        return launch_ranks(argv, args)
     return Supervisor(args, config).run()
+
+
+def launch_ranks(argv, args) -> int:
+    """Node launcher: one rank per GPU on the shared SO_REUSEPORT port (DP session sharding);
+    with ``runtime.placement: spread`` the ranks also exchange backend streams (RCCL).
+    SIGHUP / SIGTERM are forwarded to every rank's supervisor."""
+    nonce = str(time.time_ns())
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, QMX_RANK=str(r), QMX_WORLD=str(args.gpus), LOCAL_RANK=str(r), QMX_XCHG_NONCE=nonce)
+        cmd = [sys.executable, "-m", "quorum_amd.serve"] + [a for a in (argv or sys.argv[1:])]
+        if args.device is None:
+            cmd += ["--device", str(r)]
+        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
+
+    def fwd(sig, _frame):
+        for p in procs:
+            try:
+                os.kill(p.pid, sig)
+            except OSError:
+                pass
+    for sig in (signal.SIGHUP, signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, fwd)
+    rc = 0
+    for p in procs:
+        rc = p.wait() or rc
+    return rc
 
 
 if __name__ == "__main__":

@@ -168,3 +168,45 @@ def test_native_drain_finishes_inflight(tmp_path):
         if w.poll() is None:
             os.killpg(w.pid, signal.SIGKILL)
         live.close()
+
+
+def test_launcher_two_ranks_spread(tmp_path):
+    """`serve --gpus 2`: two rank supervisors on one port; with placement: spread each
+    session's second backend stream runs on the other rank (TCP exchange on CPU)."""
+    if not native.available():
+        pytest.skip("native extension not built")
+    live = LiveUpstream()
+    pa = live.serve("a", ("stream", 200, sse_stream(["AAA"])))
+    pb = live.serve("b", ("stream", 200, sse_stream(["BBB"])))
+    cfg = str(tmp_path / "config.yaml")
+    _write(cfg, [f"http://127.0.0.1:{pa}/v1", f"http://127.0.0.1:{pb}/v1"])
+    with open(cfg) as f:
+        c = yaml.safe_load(f)
+    c["runtime"]["placement"] = "spread"
+    with open(cfg, "w") as f:
+        yaml.safe_dump(c, f)
+    port = free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT, QMX_XCHG_PORT=str(free_port()))
+    env.pop("QMX_RANK", None)
+    sup = subprocess.Popen([sys.executable, "-m", "quorum_amd.serve", "--impl", "native", "--engine", "cpu",
+                            "--gpus", "2", "--config", cfg, "--port", str(port), "--threads", "1"], cwd=ROOT,
+                           env=env, start_new_session=True)
+    try:
+        _wait(port, lambda r: r.status_code == 200)
+        remote = 0.0
+        for _ in range(40):
+            r = _post(port)
+            assert _final(r.text) == "AAA\n\n--\nBBB"
+            m = httpx.get(f"http://127.0.0.1:{port}/metrics").text
+            remote = max(remote, float([ln for ln in m.splitlines()
+                                        if ln.startswith("qmx_remote_streams_total")][0].split()[1]))
+        assert remote >= 1
+    finally:
+        os.kill(sup.pid, signal.SIGTERM)
+        try:
+            rc = sup.wait(timeout=40)
+        except subprocess.TimeoutExpired:
+            os.killpg(sup.pid, signal.SIGKILL)
+            rc = None
+        live.close()
+    assert rc == 0
