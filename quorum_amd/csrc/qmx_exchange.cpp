@@ -8,6 +8,7 @@
 #include <netinet/tcp.h>
 #include <rccl/rccl.h>
 #include <sys/socket.h>
+#include <sched.h>
 #include <unistd.h>
 
 #include <chrono>
@@ -291,7 +292,9 @@ class RcclX : public XTransport {
         aborted_ = true;
         return false;
       }
-      usleep(10);
+      // yield while the round is young (collectives take tens of us), then back off
+      if (now_s() - (t_end - o_.timeout_s) < 5e-4) sched_yield();
+      else usleep(50);
     }
   }
   bool allgather(const std::string& mine, uint32_t flags, std::vector<std::string>& all,

@@ -126,7 +126,7 @@ class HipEngine : public HostEngine {
   double stage_us_[16] = {0};
   uint64_t stage_n_ = 0;
   double clk_cycles_ = 0, clk_us_ = 0;
-  hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
+  hipEvent_t ev0_ = nullptr, ev1_ = nullptr, evb_ = nullptr;
 };
 
 }  // namespace qmx

@@ -88,7 +88,7 @@ static_assert(TPL_BYTES == kTplBytes, "template size");
 enum : int {
   V_START = 0, V_NSEP, V_LASTSEP, V_ABORT, V_NEV, V_CONSUMED, V_STATUS, V_NDELTA, V_YLEN, V_NCAND,
   V_NTOK, V_BAIL, V_DEPTH0, V_TAILLEN, V_NEWTAIL, V_NEWDEPTH, V_WLEN, V_NEMIT, V_ETOT, V_OUTLEN,
-  V_TPLPRE, V_TPLSUF, V_TPLK
+  V_TPLPRE, V_TPLSUF, V_TPLK, V_NEXTEV
 };
 
 // LDS byte reader that fetches one aligned 64-bit word per 8 sequential bytes: a byte-serial
@@ -306,6 +306,7 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
   __shared__ KParams P;  // kernel args staged in LDS: lane-divergent pattern/envelope reads
   __shared__ uint16_t TKP[BS / 64][TOK_CAP];  // per-wave token buffers (positions)
   __shared__ alignas(8) uint8_t TKT[BS / 64][TOK_CAP];  // token bytes (type | key id | flags)
+  __shared__ int wtpl[BS / 64][4];  // S3: per-wave in-tile templates {p0, tp, s0, ts} (p0 < 0: none)
   const int tid = threadIdx.x;
   for (int i = tid; i < (int)(sizeof(KParams) / 4); i += BS) ((uint32_t*)&P)[i] = ((const uint32_t*)&Pk)[i];
   QMX_STAMP(0);
@@ -326,6 +327,8 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
     s.v[V_BAIL] = 0;
     s.v[V_STATUS] = 0;
     s.v[V_TPLK] = -1;
+    s.v[V_NEXTEV] = 0;
+    for (int q = 0; q < BS / 64; ++q) wtpl[q][0] = -1;
     if (fresh) {
       s.v[V_DEPTH0] = 0;
       s.v[V_TAILLEN] = 0;
@@ -466,79 +469,110 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
   QMX_STAMP(3);
   const int nev = s.v[V_NEV];
 
-  // ---- S3: per-event extraction (4 consecutive events per thread) --------------------
+  // ---- S3: per-event extraction --------------------------------------------------------
+  // Waves pull events from a shared counter (load balance: a few events need a full parse,
+  // most only a template compare).  Per event, wave-wide: compare against the stream's shape
+  // template (device state from earlier ticks) or any template published by a wave in this
+  // tile; else the wave-cooperative lexer + wave grammar (publishing a template on success).
+  // Lane 0 writes the result.  > 64 tokens → per-token walk; exotic → validating scalar
+  // scanner (both by lane 0, rare) — exact either way.
   int packed_local[4];
   {
-    // Rounds of BS events: event k = round*BS + 4*l + w is lexed wave-cooperatively by wave w
-    // (one event after another, 64 bytes per step), then lane l of wave w runs the token
-    // grammar for it.  Token buffers are private to a wave: no barrier between phases.
     const int w = tid >> 6, lane = tid & 63;
     const LdsWords rd(s.A);
-    enum { O_SKIP, O_LEXED, O_COMPLEX, O_TPL };
     const int tp = s.v[V_TPLPRE], ts = s.v[V_TPLSUF];
-    for (int base = 0; base < nev; base += BS) {
-      int my_out = O_SKIP, my_t0 = 0, my_t1 = 0;
-      int ntok = 0;
-      for (int l = 0; l < 64; ++l) {
-        const int k = base + 4 * l + w;
-        if (k >= nev) break;  // wave-uniform
-        const int e0 = s.ev_a[k], e1 = s.ev_b[k];
-        int out = O_SKIP, t0 = ntok, t1 = ntok;
-        if (tp > 0 && e1 - e0 >= tp + ts && wave_tpl_match(s.A, e0, e1, s.tpl, tp, ts) &&
-            wave_str_body(s.A, e0 + tp, e1 - ts)) {
-          out = O_TPL;  // same shape as this stream's last parsed content event
-        } else if (lit_at(s.A, e0, e1, QMX_LIT("data: "))) {
+    bool published = false;
+    int hint = w;  // template that matched last (tried first)
+    while (true) {
+      int k = 0;
+      if (lane == 0) k = atomicAdd(&s.v[V_NEXTEV], 1);
+      k = __builtin_amdgcn_readfirstlane(k);
+      if (k >= nev) break;
+      const int e0 = s.ev_a[k], e1 = s.ev_b[k];
+      int kind = EV_SKIP, sa = 0, sb = 0, body = -1;
+      bool slow = false, lexed = false;
+      int nt = 0;
+      if (tp > 0 && e1 - e0 >= tp + ts && wave_tpl_match(s.A, e0, e1, s.tpl, tp, ts) &&
+          (body = wave_str_body(s.A, e0 + tp, e1 - ts)) >= 0) {
+        kind = EV_CONTENT;  // same shape as this stream's last parsed content event
+        sa = e0 + tp;
+        sb = e1 - ts;
+      } else {
+        for (int q = 0; q < BS / 64 && kind != EV_CONTENT; ++q) {
+          const int qi = (hint + q) & (BS / 64 - 1);
+          const int p0 = __atomic_load_n(&wtpl[qi][0], __ATOMIC_ACQUIRE);  // published last
+          if (p0 < 0) continue;
+          const int ttp = wtpl[qi][1], s0 = wtpl[qi][2], tts = wtpl[qi][3];
+          if (e1 - e0 >= ttp + tts && wave_tpl_match_tile(s.A, e0, e1, p0, ttp, s0, tts) &&
+              (body = wave_str_body(s.A, e0 + ttp, e1 - tts)) >= 0) {
+            kind = EV_CONTENT;  // same shape as an event parsed earlier in this tile
+            sa = e0 + ttp;
+            sb = e1 - tts;
+            hint = qi;
+          }
+        }
+        if (kind != EV_CONTENT && lit_at(s.A, e0, e1, QMX_LIT("data: "))) {
           int a = e0 + 6, b = e1;
           ustrip(s.A, &a, &b);
           if (!(b - a == 6 && lit_at(s.A, a, b, QMX_LIT("[DONE]")))) {
-            const int nt = wave_lex(s.A, a, b, TKP[w], TKT[w], ntok, TOK_CAP);
+            nt = wave_lex(s.A, a, b, TKP[w], TKT[w], 0, TOK_CAP);
             if (nt == -LEX_COMPLEX) {
-              out = O_COMPLEX;
+              slow = true;
+            } else if (nt > 64) {
+              lexed = true;
             } else if (nt >= 0) {
-              out = O_LEXED;
-              t1 = ntok + nt;
-              ntok = t1;
+              EvResult r;
+              bool esc = true;
+              const int g = wave_grammar(TKP[w], TKT[w], 0, nt, r, &esc);
+              if (g == LEX_COMPLEX) {
+                slow = true;
+              } else if (g == LEX_OK) {
+                kind = r.kind;
+                sa = r.str_a;
+                sb = r.str_b;
+                body = esc ? 1 : 0;
+                if (kind == EV_CONTENT && sa - e0 <= TPL_PRE_MAX && e1 - sb <= TPL_SUF_MAX && lane == 0) {
+                  if (!published) {  // later events (any wave) compare against this one
+                    wtpl[w][1] = sa - e0;
+                    wtpl[w][2] = sb;
+                    wtpl[w][3] = e1 - sb;
+                    __atomic_store_n(&wtpl[w][0], e0, __ATOMIC_RELEASE);
+                  }
+                  atomicMax(&s.v[V_TPLK], k);  // newest parsed content → device template
+                }
+                if (kind == EV_CONTENT && sa - e0 <= TPL_PRE_MAX && e1 - sb <= TPL_SUF_MAX) published = true;
+              }
             }
           }
         }
-        if (lane == l) {
-          my_out = out;
-          my_t0 = t0;
-          my_t1 = t1;
-        }
       }
-      const int k = base + 4 * lane + w;
-      if (k >= nev) continue;
-      const int a = s.ev_a[k], b = s.ev_b[k];
-      EvResult r;
-      r.kind = EV_SKIP;
-      r.str_a = r.str_b = 0;
-      if (my_out == O_TPL) {
-        r.kind = EV_CONTENT;
-        r.str_a = a + tp;
-        r.str_b = b - ts;
-      } else {
-        if (my_out == O_LEXED) {
-          const int g = token_grammar(TKP[w], TKT[w], my_t0, my_t1, r);
+      if (lane == 0) {
+        EvResult r;
+        r.kind = kind;
+        r.str_a = sa;
+        r.str_b = sb;
+        if (lexed) {  // long token list: the per-token walk
+          const int g = token_grammar(TKP[w], TKT[w], 0, nt, r);
           if (g == LEX_INVALID) r.kind = EV_SKIP;
-          else if (g == LEX_COMPLEX) my_out = O_COMPLEX;
+          else if (g == LEX_COMPLEX) slow = true;
+          body = 1;
         }
-        if (my_out == O_COMPLEX) {  // rare shapes: the validating scalar scanner
-          r = classify_event_at(rd, a, b - a);
-          r.str_a += a;
-          r.str_b += a;
+        if (slow) {  // rare shapes: the validating scalar scanner
+          r = classify_event_at(rd, e0, e1 - e0);
+          r.str_a += e0;
+          r.str_b += e0;
+          body = 1;
         }
-        if (r.kind == EV_CONTENT && r.str_a - a <= TPL_PRE_MAX && b - r.str_b <= TPL_SUF_MAX)
-          atomicMax(&s.v[V_TPLK], k);  // newest parsed content event becomes the template
-      }
-      s.ev_kind[k] = (uint8_t)r.kind;
-      if (r.kind == EV_CONTENT) {
-        int sa = r.str_a, sb = r.str_b;
-        s.ev_sa[k] = (uint16_t)sa;
-        s.ev_sb[k] = (uint16_t)sb;
-        s.ev_dl[k] = (uint16_t)json_unescape(rd, sa, sb, nullptr);
-      } else if (r.kind == EV_ABORT) {
-        atomicMin(&s.v[V_ABORT], k);
+        if ((lexed || slow) && r.kind == EV_CONTENT && r.str_a - e0 <= TPL_PRE_MAX && e1 - r.str_b <= TPL_SUF_MAX)
+          atomicMax(&s.v[V_TPLK], k);
+        s.ev_kind[k] = (uint8_t)r.kind;
+        if (r.kind == EV_CONTENT) {
+          s.ev_sa[k] = (uint16_t)r.str_a;
+          s.ev_sb[k] = (uint16_t)r.str_b;
+          s.ev_dl[k] = (uint16_t)(body == 0 ? r.str_b - r.str_a : json_unescape(rd, r.str_a, r.str_b, nullptr));
+        } else if (r.kind == EV_ABORT) {
+          atomicMin(&s.v[V_ABORT], k);
+        }
       }
     }
   }
@@ -1128,17 +1162,12 @@ static void put(char* dst, int cap, int* len, const std::string& s) {
 }
 
 // Wait for this engine's stream without pinning a core: the io loops share the CPU with
-// the tick threads, and a spinning hipStreamSynchronize costs a whole core per engine.
-// Spin briefly (the common tick finishes in ~100-200 us), then poll with short sleeps.
+// the tick threads.  A blocking-sync event sleeps on the completion interrupt: measured on
+// MI355X (tools/probes/launch_bench.hip) launch+wait = 11 us, vs 18 us spinning
+// hipStreamSynchronize (one core burnt per engine) and 77 us polling with sleep_for.
 void HipEngine::wait_stream() {
-  const auto t0 = std::chrono::steady_clock::now();
-  while (true) {
-    hipError_t e = hipStreamQuery(stream_);
-    if (e == hipSuccess) return;
-    if (e != hipErrorNotReady) HIP_CHECK(e);
-    if (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(20)) continue;
-    std::this_thread::sleep_for(std::chrono::microseconds(15));
-  }
+  HIP_CHECK(hipEventRecord(evb_, stream_));
+  HIP_CHECK(hipEventSynchronize(evb_));
 }
 
 HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_bytes, int max_slots,
@@ -1152,6 +1181,7 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
   HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   HIP_CHECK(hipEventCreate(&ev0_));
   HIP_CHECK(hipEventCreate(&ev1_));
+  HIP_CHECK(hipEventCreateWithFlags(&evb_, hipEventBlockingSync | hipEventDisableTiming));
   HIP_CHECK(hipMalloc(&d_state_, sizeof(DevSlot) * (size_t)max_slots_));
   HIP_CHECK(hipMemset(d_state_, 0, sizeof(DevSlot) * (size_t)max_slots_));
   HIP_CHECK(hipMalloc(&d_content_, (size_t)content_cap_ * (size_t)max_slots_));
@@ -1199,6 +1229,7 @@ HipEngine::~HipEngine() {
   if (d_fout_) hipFree(d_fout_);
   if (ev0_) hipEventDestroy(ev0_);
   if (ev1_) hipEventDestroy(ev1_);
+  if (evb_) hipEventDestroy(evb_);
   if (stream_) hipStreamDestroy(stream_);
 }
 

@@ -223,15 +223,18 @@ __device__ inline bool wave_tpl_match(const uint8_t* x, int e0, int e1, const ui
 
 // Is x[a:b) a complete JSON string body (no unescaped quote, valid escapes, no control
 // characters, strict UTF-8, not ending inside an escape)?  Wave-uniform.
-__device__ inline bool wave_str_body(const uint8_t* x, int a, int b) {
+// Returns -1 (no), 0 (yes, no backslash: decoded length = b - a), 1 (yes, has escapes).
+__device__ inline int wave_str_body(const uint8_t* x, int a, int b) {
   const int lane = threadIdx.x & 63;
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
   int carry_run = 0;
+  bool any_bs = false;
   for (int blk = a; blk < b; blk += 64) {
     const int pos = blk + lane;
     const bool v = pos < b;
     const uint32_t c = v ? x[pos] : (uint32_t)'a';
     const uint64_t BSm = __ballot(v && c == '\\');
+    any_bs = any_bs || BSm != 0;
     const uint64_t nb = ~BSm & below;
     const int run = nb ? (lane - 1 - (63 - __clzll(nb))) : (lane + carry_run);
     const bool esc = run & 1;
@@ -246,14 +249,130 @@ __device__ inline bool wave_str_body(const uint8_t* x, int a, int b) {
     if (__ballot(v && c >= 0x80)) {
       if (v && c >= 0x80) e = e || utf8_lane_bad(x, pos, a, b, c);
     }
-    if (__ballot(e) != 0) return false;
+    if (__ballot(e) != 0) return -1;
     const int nv = min(64, b - blk);  // trailing backslash run of this block's valid bytes
     const uint64_t vm = nv == 64 ? ~0ull : ((1ull << nv) - 1);
     const uint64_t bsv = BSm & vm;
     const uint64_t nbs = ~bsv & vm;
     carry_run = nbs ? (nv - 1 - (63 - __clzll(nbs))) : carry_run + nv;
   }
-  return (carry_run & 1) == 0;  // an odd run would escape the closing quote
+  if (carry_run & 1) return -1;  // an odd run would escape the closing quote
+  return any_bs ? 1 : 0;
+}
+
+// Wave-parallel grammar + quorum target path for ONE event whose nt <= 64 tokens start at
+// t0 (lane j owns token j).  Replaces a per-lane walk (~250 instructions per token) by
+// ~O(depth) ballots per event:
+//   depth before each token = popc(openers below) - popc(closers below);
+//   container of a token    = the last opener below at depth-1 (one ballot per level);
+//   JSON validity           = local adjacency rules given the container kind (keys vs values
+//                             by the previous token), closers matching their container, a
+//                             single root object closing at the last token;
+//   path                    = last "choices" key of the root → its "[" → first element →
+//                             last "delta" key → its "{" → last "content" key → its value.
+// Returns LEX_OK / LEX_INVALID / LEX_COMPLEX exactly like token_grammar (wave-uniform; res
+// is valid in every lane).
+__device__ inline int wave_grammar(const uint16_t* tpos, const uint8_t* ttype, int t0, int nt, EvResult& res,
+                                   bool* content_esc) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  res.kind = EV_SKIP;
+  res.str_a = res.str_b = 0;
+  const bool v = lane < nt;
+  const int tb = v ? ttype[t0 + lane] : 0;
+  const int ty = tb & TK_TYPE;
+  if (__builtin_amdgcn_readlane(ty, 0) != TK_LBRACE) return LEX_COMPLEX;  // non-object root
+  const bool isO = ty == TK_LBRACE || ty == TK_LBRACK, isC = ty == TK_RBRACE || ty == TK_RBRACK;
+  const uint64_t Om = __ballot(isO), Cm = __ballot(isC);
+  const int db = __popcll(Om & below) - __popcll(Cm & below);
+  const int da = db + (isO ? 1 : 0) - (isC ? 1 : 0);
+  // depth: never negative, root closes exactly at the last token
+  if (__ballot(v && (da < 0 || (lane < nt - 1 && da < 1) || (lane == nt - 1 && da != 0))) != 0) return LEX_INVALID;
+  // container of each token: last opener below at depth db-1
+  int cont = -1;
+  int maxd = db;
+  for (int o = 32; o; o >>= 1) maxd = max(maxd, __shfl_xor(maxd, o, 64));
+  if (maxd > 64) return LEX_COMPLEX;
+  for (int L = 0; L < maxd; ++L) {
+    const uint64_t OL = __ballot(isO && db == L) & below;
+    if (db == L + 1 && OL) cont = 63 - __clzll(OL);
+  }
+  const int ctype = __shfl(ty, cont < 0 ? 0 : cont, 64);
+  const bool inObj = cont >= 0 && ctype == TK_LBRACE;
+  const int p = __shfl_up(ty, 1, 64);  // previous token type (lane 0: none)
+  const bool keyopen = v && lane > 0 && ty == TK_SOPEN && inObj && (p == TK_LBRACE || p == TK_COMMA);
+  const uint64_t KOm = __ballot(keyopen);
+  const bool keyclose = v && ty == TK_SCLOSE && lane > 0 && ((KOm >> (lane - 1)) & 1);
+  const bool valend = v && (ty == TK_SCALAR || isC || (ty == TK_SCLOSE && !keyclose));
+  const uint64_t VEm = __ballot(valend), KCm = __ballot(keyclose);
+  const bool prevVE = lane > 0 && ((VEm >> (lane - 1)) & 1), prevKC = lane > 0 && ((KCm >> (lane - 1)) & 1);
+  bool ok = true;
+  if (v && lane > 0) {
+    if (ty == TK_SOPEN) ok = inObj ? (p == TK_LBRACE || p == TK_COMMA || p == TK_COLON) : (p == TK_LBRACK || p == TK_COMMA);
+    else if (ty == TK_SCLOSE) ok = true;
+    else if (ty == TK_COLON) ok = inObj && prevKC;
+    else if (ty == TK_COMMA) ok = prevVE;
+    else if (ty == TK_RBRACE) ok = inObj && (p == TK_LBRACE || prevVE);
+    else if (ty == TK_RBRACK) ok = !inObj && (p == TK_LBRACK || prevVE);
+    else ok = inObj ? p == TK_COLON : (p == TK_LBRACK || p == TK_COMMA);  // { [ scalar
+  }
+  if (__ballot(!ok) != 0) return LEX_INVALID;
+  // quorum path: choices[0].delta.content (duplicate keys: the last one wins)
+  const int kid = (tb >> KID_SHIFT) & 3;
+  const bool bs_next = (__shfl_down(tb, 1, 64) & TKF_BS) != 0;  // key string holds a backslash
+  auto last_key = [&](int c, int want, int* k) -> bool {        // false: COMPLEX (escaped key)
+    const uint64_t mine = __ballot(keyopen && cont == c && kid == want);
+    if (__ballot(keyopen && cont == c && kid != want && bs_next) != 0) return false;
+    *k = mine ? 63 - __clzll(mine) : -1;
+    return true;
+  };
+  auto ty_at = [&](int j) { return __builtin_amdgcn_readlane(ty, j); };
+  int kc, kd, kk;
+  if (!last_key(0, KID_CHOICES, &kc)) return LEX_COMPLEX;
+  if (kc < 0) return LEX_OK;
+  const int vc = kc + 3;  // "choices" SCLOSE COLON value
+  if (ty_at(vc) != TK_LBRACK) return LEX_COMPLEX;
+  const int c0 = vc + 1;
+  if (ty_at(c0) == TK_RBRACK) return LEX_OK;  // empty choices
+  if (ty_at(c0) != TK_LBRACE) {
+    res.kind = EV_ABORT;
+    return LEX_OK;
+  }
+  if (!last_key(c0, KID_DELTA, &kd)) return LEX_COMPLEX;
+  if (kd < 0) return LEX_OK;
+  const int vd = kd + 3, tvd = ty_at(vd);
+  if (tvd == TK_LBRACK || tvd == TK_SOPEN) return LEX_COMPLEX;
+  if (tvd != TK_LBRACE) {
+    res.kind = EV_ABORT;
+    return LEX_OK;
+  }
+  if (!last_key(vd, KID_CONTENT, &kk)) return LEX_COMPLEX;
+  if (kk < 0) return LEX_OK;
+  const int vk = kk + 3;
+  if (ty_at(vk) != TK_SOPEN) {
+    res.kind = EV_ABORT;
+    return LEX_OK;
+  }
+  res.kind = EV_CONTENT;
+  res.str_a = tpos[t0 + vk] + 1;
+  res.str_b = tpos[t0 + vk + 1];
+  *content_esc = (__builtin_amdgcn_readlane(tb, vk + 1) & TKF_BS) != 0;
+  return LEX_OK;
+}
+
+// Template check against an earlier event of the same tile: x[e0:e0+tp) == x[p0:p0+tp) and
+// x[e1-ts:e1) == x[s0:s0+ts) (tp <= 256, ts <= 64).
+__device__ inline bool wave_tpl_match_tile(const uint8_t* x, int e0, int e1, int p0, int tp, int s0, int ts) {
+  const int lane = threadIdx.x & 63;
+  bool bad = false;
+  if (lane < 32) {
+    const int o = lane * 8;
+    if (o < tp) bad = lds_window8(x, e0 + o, e0 + tp) != lds_window8(x, p0 + o, p0 + tp);
+  } else if (lane < 40) {
+    const int o = (lane - 32) * 8;
+    if (o < ts) bad = lds_window8(x, e1 - ts + o, e1) != lds_window8(x, s0 + o, s0 + ts);
+  }
+  return __ballot(bad) == 0;
 }
 
 // Per-lane grammar + quorum target-path tracking over tokens [t0, t1).

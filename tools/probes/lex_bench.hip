@@ -168,6 +168,24 @@ __global__ __launch_bounds__(256) void k(const uint8_t* ev, int elen, int stride
     acc += r2.kind + r2.str_a;
   }
   unsigned long long c4 = __builtin_amdgcn_s_memtime();
+  // wave grammar: re-lex + wave_grammar per event (what the kernel's S3 does per fresh event)
+  int wg = 0;
+  for (int l = 0; l < 16; ++l) {
+    int e = 4 * l + w;
+    int nt = wave_lex(A, e * stride + 6, e * stride + elen, TKP[w], TKT[w], 0, 1024);
+    EvResult r3;
+    bool esc;
+    wg += wave_grammar(TKP[w], TKT[w], 0, nt, r3, &esc) * 3 + r3.kind + (nt > 64);
+  }
+  unsigned long long c5 = __builtin_amdgcn_s_memtime();
+  // template compare + string-body check per event
+  for (int l = 0; l < 16; ++l) {
+    int e = 4 * l + w;
+    wg += wave_tpl_match_tile(A, e * stride, e * stride + elen, 0, 150, 160, 26) +
+          wave_str_body(A, e * stride + 150, e * stride + 160);
+  }
+  unsigned long long c6 = __builtin_amdgcn_s_memtime();
+  acc += wg;
   if (tid == 0) {
     out[0] = c1 - c0;
     out[1] = c2 - c1;
@@ -177,6 +195,9 @@ __global__ __launch_bounds__(256) void k(const uint8_t* ev, int elen, int stride
     out[5] = (unsigned long long)g;
     out[6] = (unsigned long long)r.kind;
     for (int i = 0; i < 5; ++i) out[7 + i] = abl[i];
+    out[12] = c5 - c4;
+    out[13] = c6 - c5;
+    out[14] = (unsigned long long)wg;
   }
   sink[tid] = acc;
 }
@@ -196,7 +217,7 @@ int main() {
   hipMalloc(&sink, 1024);
   hipMemcpy(dev, buf.data(), stride, hipMemcpyHostToDevice);
   for (int rep = 0; rep < 3; ++rep) {
-    unsigned long long c[12];
+    unsigned long long c[15];
     hipLaunchKernelGGL(k, dim3(1), dim3(256), 0, 0, dev, elen, stride, dout, sink);
     hipMemcpy(c, dout, sizeof(c), hipMemcpyDeviceToHost);
     // s_memtime counts shader clocks (~2.4 GHz, see kbench shader_mhz)
@@ -205,6 +226,7 @@ int main() {
            elen, c[0], c[1], c[2], c[3], c[4], (long long)c[5], c[6]);
     printf("  ablation: full %llu  -keywin %llu  -scalar %llu  -utf8/esc %llu  minimal %llu\n", c[7], c[8], c[9], c[10],
            c[11]);
+    printf("  lex+wave_grammar x16: %llu ticks; template+body x16: %llu ticks (check %llu)\n", c[12], c[13], c[14]);
   }
   return 0;
 }
