@@ -6,6 +6,8 @@
 #include "qmx_engine.h"
 #include "qmx_hip.h"
 #include "qmx_json.h"
+#include <chrono>
+
 #include "qmx_exchange.h"
 #include "qmx_server.h"
 
@@ -139,6 +141,60 @@ PYBIND11_MODULE(_qmx, m) {
   });
   m.def("server_counters", &server_counters);
   m.def("rccl_unique_id", &rccl_unique_id_hex);
+  // Transport self-test: `rounds` all-gathers of random payloads (some larger than the fixed
+  // slot, exercising the padded second phase); every rank must receive every rank's bytes.
+  m.def("exchange_selftest", [](const py::dict& d, int rounds) {
+    XOptions o;
+    auto gs = [&](const char* k, std::string& v) { if (d.contains(k)) v = py::cast<std::string>(d[k]); };
+    auto gi = [&](const char* k, int& v) { if (d.contains(k)) v = py::cast<int>(d[k]); };
+    gi("rank", o.rank); gi("world", o.world); gs("transport", o.transport); gs("addr", o.addr);
+    gi("port", o.port); gs("id_file", o.id_file); gi("device", o.device);
+    bool ok = true;
+    int bad = 0, fail_round = -1;
+    double t_small = 0, t_big = 0;
+    int n_small = 0, n_big = 0;
+    {
+      py::gil_scoped_release nogil;
+      auto tr = o.transport == "rccl" ? make_rccl_transport(o) : make_tcp_transport(o);
+      std::vector<std::string> all;
+      std::vector<uint32_t> fl;
+      const uint64_t seed = 1234567;
+      for (int r = 0; r < rounds && ok; ++r) {
+        // every rank derives every rank's payload from (round, rank): receivers can verify
+        auto payload = [&](int rk) {
+          uint64_t x = seed ^ ((uint64_t)r * 1000003ull) ^ ((uint64_t)rk * 7919ull);
+          size_t n = (r % 5 == 4) ? 20000 + (x % 5000) : (x % 3000);
+          std::string s(n, '\0');
+          for (size_t i = 0; i < n; ++i) {
+            x = x * 6364136223846793005ull + 1442695040888963407ull;
+            s[i] = (char)(x >> 56);
+          }
+          return s;
+        };
+        std::string mine = payload(o.rank);
+        auto t0 = std::chrono::steady_clock::now();
+        if (!tr->allgather(mine, (uint32_t)r, all, fl)) {
+          ok = false;
+          fail_round = r;
+          break;
+        }
+        double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        if (r % 5 == 4) {
+          t_big += us;
+          ++n_big;
+        } else {
+          t_small += us;
+          ++n_small;
+        }
+        for (int rk = 0; rk < o.world; ++rk)
+          if (all[rk] != payload(rk) || fl[rk] != (uint32_t)r) ++bad;
+      }
+    }
+    return py::dict(py::arg("ok") = ok && bad == 0, py::arg("bad") = bad, py::arg("rounds") = rounds,
+                    py::arg("fail_round") = fail_round,
+                    py::arg("small_round_us") = n_small ? t_small / n_small : 0.0,
+                    py::arg("large_round_us") = n_big ? t_big / n_big : 0.0);
+  });
   m.def("stop_server", &stop_server);
   m.def("json_roundtrip", [](const py::bytes& b) -> py::object {
     std::string s(b), err;

@@ -193,3 +193,20 @@ def test_spread_many_concurrent_sessions():
                         assert r == ref
     finally:
         live.close()
+
+
+def test_exchange_transport_selftest_tcp():
+    """Raw transport: 3 ranks, 60 all-gather rounds with payloads below and above the fixed
+    first-phase slot; every rank must receive every rank's exact bytes and flags."""
+    ext = native.require()
+    port = free_port()
+    res = {}
+
+    def run(r):
+        res[r] = ext.exchange_selftest({"rank": r, "world": 3, "transport": "tcp", "port": port}, 60)
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(3)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=60)
+    assert len(res) == 3 and all(v["ok"] for v in res.values()), res
