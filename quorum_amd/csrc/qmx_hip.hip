@@ -614,7 +614,24 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
         int j = pre >> 16, doff = pre & 0xFFFF;
         int dl = s.ev_dl[k];
         s.dl_end[j] = (uint16_t)(tail_len + doff + dl);
-        json_unescape(LdsWords(s.A), s.ev_sa[k], s.ev_sb[k], Z + tail_len + doff);
+        if (dl == s.ev_sb[k] - s.ev_sa[k]) {  // escape-free (every escape shrinks): copied below
+          s.ev_a[k] = (uint16_t)doff;
+        } else {
+          json_unescape(LdsWords(s.A), s.ev_sa[k], s.ev_sb[k], Z + tail_len + doff);
+          s.ev_a[k] = 0xFFFF;
+        }
+      } else if (k < nev) {
+        s.ev_a[k] = 0xFFFF;
+      }
+    }
+    __syncthreads();
+    {  // escape-free contents: one wave per event, 64 bytes per step
+      const int w = tid >> 6, lane = tid & 63;
+      for (int k = w; k < nev; k += BS / 64) {
+        const int off = s.ev_a[k];
+        if (off == 0xFFFF) continue;
+        const int sa = s.ev_sa[k], n = s.ev_sb[k] - sa;
+        for (int x = lane; x < n; x += 64) Z[tail_len + off + x] = s.A[sa + x];
       }
     }
     if (tid == 0) {
