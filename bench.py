@@ -104,6 +104,46 @@ def loadgen(bin_dir, port, conns, requests, threads, timeout):
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
+def scrape(port):
+    """Sum the proxy's /metrics counters (engine / kernel / tick / exchange) — one process
+    per rank, io loops already aggregated inside it."""
+    import urllib.request
+
+    out = {}
+    try:
+        txt = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode()
+    except Exception:  # noqa: BLE001
+        return out
+    for ln in txt.splitlines():
+        if not ln or ln[0] == "#" or "{" in ln:
+            continue
+        k, _, v = ln.rpartition(" ")
+        try:
+            out[k] = float(v)
+        except ValueError:
+            pass
+    return out
+
+
+def breakdown(m0, m1, elapsed):
+    d = {k: m1.get(k, 0.0) - m0.get(k, 0.0) for k in m1}
+    launches = d.get("qmx_kernel_launches", 0.0)
+    ticks = d.get("qmx_tick_seconds_count", 0.0)
+    return {
+        "ticks": int(ticks),
+        "tick_wall_us_avg": round(1e6 * d.get("qmx_tick_seconds_sum", 0.0) / ticks, 1) if ticks else None,
+        "streams_per_tick": round(d.get("qmx_tick_slots_total", 0.0) / ticks, 2) if ticks else None,
+        "kernel_launches": int(launches),
+        "tick_kernel_us_avg": round(1000 * d.get("qmx_kernel_kernel_ms", 0.0) / launches, 1) if launches else None,
+        "gpu_busy_frac": round(d.get("qmx_kernel_kernel_ms", 0.0) / 1000 / elapsed, 4) if elapsed else None,
+        "finalize_launches": int(d.get("qmx_kernel_fin_launches", 0.0)),
+        "h2d_MB": round(d.get("qmx_kernel_h2d_bytes", 0.0) / 1e6, 2),
+        "d2h_MB": round(d.get("qmx_kernel_d2h_bytes", 0.0) / 1e6, 2),
+        "escalations": int(d.get("qmx_kernel_escalations", 0.0)),
+        "exchange_rounds": int(d.get("qmx_exchange_rounds_total", 0.0)),
+    }
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -182,6 +222,7 @@ def main() -> int:
             dist.barrier()
         if use_cuda:
             torch.cuda.synchronize()
+        m0 = scrape(args.port)
         t0 = time.perf_counter()
         stats = loadgen(bin_dir, args.port, args.conns, args.steps * args.batch, args.lg_threads, args.timeout)
         if use_cuda:
@@ -189,6 +230,7 @@ def main() -> int:
         if dist is not None:
             dist.barrier()
         elapsed = time.perf_counter() - t0
+        bd = breakdown(m0, scrape(args.port), elapsed) if args.impl == "native" else {}
         local = [elapsed, float(stats["completed"]), float(stats["ttft_p50_ms"]), float(stats["ttft_p99_ms"]),
                  float(stats["errors"] + stats["non200"]), float(stats["ttfb_p50_ms"]), float(stats["lat_p50_ms"])]
         if dist is not None:
@@ -204,7 +246,7 @@ def main() -> int:
             value = total / max_el
             p50 = statistics.median(r[2] for r in rows)
             res = {
-                "metric": "proxied req/sec (whole node) + p50 TTFT, 2-backend concatenate stream"
+                "metric": "proxied req/sec (whole node) + p50 TTFT, 2-backend concatenate stream at 1/2/4/8 GPU"
                           if args.scenario == "headline" else f"proxied req/sec (whole node) + p50 TTFT, {args.scenario}",
                 "value": round(value, 3),
                 "unit": "req/s",
@@ -231,6 +273,9 @@ def main() -> int:
                 "p50_latency_ms": round(statistics.median(r[6] for r in rows), 3),
                 "errors": int(sum(r[4] for r in rows)),
                 "baseline_p50_ttft_ms_16_clients": 1605,
+                # one rank proxy process counters over the timed region (SURVEY §5.1 time breakdown;
+                # with N>1 the shared port answers from any rank)
+                "breakdown_one_rank": bd,
             }
             print(json.dumps(res), flush=True)
     finally:
