@@ -23,6 +23,10 @@
 
 #include <map>
 
+#include <openssl/err.h>
+#include <openssl/ssl.h>
+#include <openssl/x509v3.h>
+
 #include "qmx_engine.h"
 #include "qmx_exchange.h"
 #include "qmx_hip.h"
@@ -270,6 +274,8 @@ struct Up {
   RespParser rp;
   std::string body;  // buffered body (UP_BUFFER / non-200)
   double last_io = 0, deadline = 0, timeout = 60, t_open = 0;
+  SSL* ssl = nullptr;     // https backend
+  bool tls_hs = false;    // handshake in progress
 };
 
 struct BState {
@@ -462,6 +468,7 @@ class Loop {
  public:
   Loop(const ServerCfg& cfg, int idx) : cfg_(cfg), idx_(idx) { xfd_ = eventfd(0, EFD_NONBLOCK); }
   void attach_exchange(Exchange* x) { xch_ = x; }
+  void attach_tls(SSL_CTX* t) { tls_ = t; }
   void attach_loops(const std::vector<Loop*>* ls) { loops_ = ls; }
   std::mutex smu_;
   std::unordered_map<std::string, double> snap_;  // engine stats snapshot (read by /metrics on any loop)
@@ -487,6 +494,9 @@ class Loop {
     stop_gpu_ = true;
     cv_.notify_all();
     if (gpu_thread_.joinable()) gpu_thread_.join();
+    for (auto& kv : idle_ssl_) SSL_free(kv.second);  // before the run's SSL_CTX goes away
+    for (auto& kv : ups_)
+      if (kv.second->ssl) SSL_free(kv.second->ssl);
   }
 
   void run() {
@@ -1007,7 +1017,7 @@ class Loop {
   std::string build_req(const BackendCfg& be, const std::vector<std::pair<std::string, std::string>>& hdrs,
                         const std::string& body) {
     std::string r = "POST " + be.path + "/chat/completions HTTP/1.1\r\nhost: " + be.host +
-                    (be.port != 80 ? ":" + std::to_string(be.port) : std::string()) + "\r\n";
+                    (be.port != (be.https ? 443 : 80) ? ":" + std::to_string(be.port) : std::string()) + "\r\n";
     for (auto& h : hdrs) r += h.first + ": " + h.second + "\r\n";
     r += "content-length: " + std::to_string(body.size()) + "\r\n\r\n";
     r += body;
@@ -1025,13 +1035,18 @@ class Loop {
     u->last_io = now_s();
     u->t_open = u->last_io;
     u->deadline = cfg_.total_timeout > 0 ? u->last_io + cfg_.total_timeout : 0;
-    if (!be.resolved || be.https) return nullptr;
+    if (!be.resolved || (be.https && !tls_)) return nullptr;
     int fd = -1;
     auto& pool = idle_[backend];
     while (!pool.empty() && fd < 0) {
       fd = pool.back();
       pool.pop_back();
       u->reused = true;
+      auto it = idle_ssl_.find(fd);
+      if (it != idle_ssl_.end()) {
+        u->ssl = it->second;
+        idle_ssl_.erase(it);
+      }
     }
     if (fd < 0) {
       fd = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK, 0);
@@ -1046,17 +1061,59 @@ class Loop {
       c_up_conns++;
       u->fd = fd;
       add(fd, EPOLLIN | EPOLLOUT, tag(4, fd));
+      if (be.https) {
+        u->ssl = SSL_new(tls_);
+        SSL_set_fd(u->ssl, fd);
+        SSL_set_tlsext_host_name(u->ssl, be.host.c_str());
+        X509_VERIFY_PARAM* vp = SSL_get0_param(u->ssl);
+        in_addr ip4;
+        if (inet_pton(AF_INET, be.host.c_str(), &ip4) == 1) X509_VERIFY_PARAM_set1_ip_asc(vp, be.host.c_str());
+        else SSL_set1_host(u->ssl, be.host.c_str());
+        u->tls_hs = true;
+      }
     } else {
       u->fd = fd;
       add(fd, EPOLLIN | EPOLLOUT, tag(4, fd));
     }
     Up* p = u.get();
     ups_[fd] = std::move(u);
-    if (!p->connecting) write_up(p);
+    if (!p->connecting) {
+      if (p->tls_hs) tls_step(p);
+      else write_up(p);
+    }
     return p;
+  }
+  // non-blocking TLS handshake step; on completion the request goes out
+  void tls_step(Up* u) {
+    ERR_clear_error();
+    int r = SSL_connect(u->ssl);
+    if (r == 1) {
+      u->tls_hs = false;
+      return write_up(u);
+    }
+    int e = SSL_get_error(u->ssl, r);
+    if (e == SSL_ERROR_WANT_READ) return mod(u->fd, EPOLLIN, tag(4, u->fd));
+    if (e == SSL_ERROR_WANT_WRITE) return mod(u->fd, EPOLLIN | EPOLLOUT, tag(4, u->fd));
+    c_fail_connect++;
+    up_error(u, "All connection attempts failed");
   }
   void write_up(Up* u) {
     while (u->req_off < u->req.size()) {
+      if (u->ssl) {
+        ERR_clear_error();
+        int w = SSL_write(u->ssl, u->req.data() + u->req_off, (int)(u->req.size() - u->req_off));
+        if (w > 0) {
+          u->req_off += w;
+          u->last_io = now_s();
+          continue;
+        }
+        int e = SSL_get_error(u->ssl, w);
+        if (e == SSL_ERROR_WANT_WRITE) return mod(u->fd, EPOLLIN | EPOLLOUT, tag(4, u->fd));
+        if (e == SSL_ERROR_WANT_READ) return mod(u->fd, EPOLLIN, tag(4, u->fd));
+        if (u->reused && !u->got_bytes) return retry_fresh(u);  // stale pooled TLS connection
+        c_fail_connect++;
+        return up_error(u, "All connection attempts failed");
+      }
       ssize_t w = send(u->fd, u->req.data() + u->req_off, u->req.size() - u->req_off, MSG_NOSIGNAL);
       if (w > 0) {
         u->req_off += w;
@@ -1068,6 +1125,21 @@ class Loop {
       return up_error(u, "All connection attempts failed");
     }
     mod(u->fd, EPOLLIN, tag(4, u->fd));
+  }
+  // read what the socket (or the TLS layer) has: >0 bytes, 0 would block, -1 eof/error
+  ssize_t up_read(Up* u, char* buf, size_t n) {
+    if (!u->ssl) {
+      ssize_t r = recv(u->fd, buf, n, 0);
+      if (r > 0) return r;
+      if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) return 0;
+      return -1;
+    }
+    ERR_clear_error();
+    int r = SSL_read(u->ssl, buf, (int)n);
+    if (r > 0) return r;
+    int e = SSL_get_error(u->ssl, r);
+    if (e == SSL_ERROR_WANT_READ || e == SSL_ERROR_WANT_WRITE) return 0;
+    return -1;
   }
   void on_up(Up* u, uint32_t ev) {
     if (u->connecting && (ev & (EPOLLOUT | EPOLLERR | EPOLLHUP))) {
@@ -1081,16 +1153,21 @@ class Loop {
       u->connecting = false;
     }
     const int fd = u->fd;
-    if ((ev & EPOLLOUT) && u->req_off < u->req.size()) {
+    if (u->tls_hs) {
+      if (!u->connecting) tls_step(u);
+      return;
+    }
+    if ((ev & (EPOLLOUT | (u->ssl ? EPOLLIN : 0))) && u->req_off < u->req.size()) {
       write_up(u);
       if (ups_.find(fd) == ups_.end()) return;
+      if (u->req_off < u->req.size()) return;
     }
     if (ev & (EPOLLIN | EPOLLHUP | EPOLLERR)) {
       char buf[65536];
       bool eof = false;
       std::string body;
       while (true) {
-        ssize_t r = recv(u->fd, buf, sizeof(buf), 0);
+        ssize_t r = up_read(u, buf, sizeof(buf));
         if (r > 0) {
           if (!u->got_bytes) h_upstream_ttfb.observe(now_s() - u->t_open);
           u->got_bytes = true;
@@ -1101,8 +1178,7 @@ class Loop {
           }
           continue;
         }
-        if (r == 0) eof = true;
-        else if (errno != EAGAIN && errno != EWOULDBLOCK) eof = true;
+        if (r < 0) eof = true;
         break;
       }
       if (!u->headers_seen && u->rp.phase > 0) {
@@ -1134,13 +1210,16 @@ class Loop {
   }
   void drop_up(Up* u, bool reuse) {
     int fd = u->fd;
-    if (reuse && !u->rp.close) {
+    if (reuse && !u->rp.close && !u->tls_hs) {
       epoll_ctl(ep_, EPOLL_CTL_DEL, fd, nullptr);  // parked: re-armed when reused
       idle_[u->backend].push_back(fd);
+      if (u->ssl) idle_ssl_[fd] = u->ssl;  // the TLS session stays with the pooled socket
     } else {
       epoll_ctl(ep_, EPOLL_CTL_DEL, fd, nullptr);
+      if (u->ssl) SSL_free(u->ssl);
       close(fd);
     }
+    u->ssl = nullptr;
     ups_.erase(fd);
   }
   void up_error(Up* u, const std::string& msg) {
@@ -2009,6 +2088,8 @@ class Loop {
   std::unordered_map<uint64_t, Session*> rsess_;            // owner sessions with remote streams
   std::map<std::pair<uint64_t, int>, Session*> shadow_;     // worker streams by (owner key, bi)
   std::vector<std::vector<int>> idle_;
+  std::unordered_map<int, SSL*> idle_ssl_;  // pooled https connections
+  SSL_CTX* tls_ = nullptr;                  // https upstreams (peer + host verification, as httpx)
   std::vector<int> pending_close_, pending_requests_;
 };
 
@@ -2021,8 +2102,10 @@ void on_signal(int sig) {
 
 int run_server(const ServerCfg& cfg0) {
   ServerCfg cfg = cfg0;
+  bool any_https = false;
   for (auto& b : cfg.backends) {
-    if (!b.valid || b.https || b.host.empty()) continue;
+    if (!b.valid || b.host.empty()) continue;
+    any_https = any_https || b.https;
     addrinfo hints{}, *res = nullptr;
     hints.ai_family = AF_INET;
     hints.ai_socktype = SOCK_STREAM;
@@ -2031,6 +2114,15 @@ int run_server(const ServerCfg& cfg0) {
       b.resolved = true;
       freeaddrinfo(res);
     }
+  }
+  SSL_CTX* tls = nullptr;
+  if (any_https) {
+    tls = SSL_CTX_new(TLS_client_method());
+    SSL_CTX_set_min_proto_version(tls, TLS1_2_VERSION);
+    SSL_CTX_set_verify(tls, cfg.tls_verify ? SSL_VERIFY_PEER : SSL_VERIFY_NONE, nullptr);
+    if (!cfg.ca_file.empty()) SSL_CTX_load_verify_locations(tls, cfg.ca_file.c_str(), nullptr);
+    else SSL_CTX_set_default_verify_paths(tls);
+    SSL_CTX_set_mode(tls, SSL_MODE_ENABLE_PARTIAL_WRITE | SSL_MODE_ACCEPT_MOVING_WRITE_BUFFER);
   }
   signal(SIGPIPE, SIG_IGN);
   if (cfg.install_signals) {
@@ -2047,7 +2139,10 @@ int run_server(const ServerCfg& cfg0) {
   for (int i = 0; i < std::max(1, cfg.threads); ++i) loops.emplace_back(new Loop(cfg, i));
   std::vector<Loop*> loop_ptrs;
   for (auto& l : loops) loop_ptrs.push_back(l.get());
-  for (auto& l : loops) l->attach_loops(&loop_ptrs);
+  for (auto& l : loops) {
+    l->attach_loops(&loop_ptrs);
+    l->attach_tls(tls);
+  }
   std::unique_ptr<Exchange> xch;
   if (cfg.world > 1 && cfg.placement == "spread") {
     XOptions o;
@@ -2083,6 +2178,7 @@ int run_server(const ServerCfg& cfg0) {
     xch.reset();
   }
   loops.clear();
+  if (tls) SSL_CTX_free(tls);
   return 0;
 }
 

@@ -64,6 +64,9 @@ struct ServerCfg {
   double drain_s = 10.0;
   std::string ready_file;
   bool verify = false;  // shadow CPU oracle engine compares every stream + finalize result
+  // https upstreams: CA bundle (httpx default: certifi) and peer verification
+  std::string ca_file;
+  bool tls_verify = true;
 };
 
 // Runs until SIGINT / stop_server(), or until drained after SIGTERM. Returns 0.

@@ -93,7 +93,7 @@ def _build(debug: bool = False, jobs: int = 3, verbose: bool = False) -> Path:
     if out.exists() and out.stat().st_mtime > max(o.stat().st_mtime for o in objs):
         return out
     cmd = [cc, "-shared", "-o", str(out)] + [str(o) for o in objs] + [
-        f"--offload-arch={ARCH}", "-fPIC", "-L/opt/rocm/lib", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]
+        f"--offload-arch={ARCH}", "-fPIC", "-L/opt/rocm/lib", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", "-lssl", "-lcrypto", "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -139,7 +139,7 @@ SAN_TARGETS = {
     "qmx_fuzz_asan": (["tools/csrc/fuzz_host.cpp", "csrc/qmx_engine.cpp", "csrc/qmx_json.cpp"], []),
     "qmx_server_asan": (["tools/csrc/server_main.cpp", "csrc/qmx_server.cpp", "csrc/qmx_engine.cpp",
                          "csrc/qmx_json.cpp", "csrc/qmx_exchange.cpp", "csrc/qmx_hip.hip"],
-                        ["-L/opt/rocm/lib", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx",
+                        ["-L/opt/rocm/lib", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", "-lssl", "-lcrypto",
                          "-Wl,-rpath,/opt/rocm/lib", "-pthread"]),
 }
 

@@ -32,13 +32,12 @@ def native_config(cfg: Dict[str, Any], host: str, port: int, engine: str, device
         https = bool(parts and parts.scheme == "https")
         if parts and parts.scheme not in ("http", "https"):
             raise NativeUnsupported(f"backend {b.get('name')!r}: unsupported URL {url!r}")
-        if https:
-            raise NativeUnsupported(f"backend {b.get('name')!r} uses https: run with --impl python")
         model = b.get("model", "")
         backends.append({
             "name": str(b.get("name", "")), "url": url, "model": "" if model is None else str(model),
             "has_model_key": "model" in b, "valid": bool(url), "https": https,
-            "host": parts.hostname if parts else "", "port": (parts.port or 80) if parts else 80,
+            "host": parts.hostname if parts else "",
+            "port": (parts.port or (443 if https else 80)) if parts else 80,
             "path": (parts.path.rstrip("/") if parts else ""),
         })
     tags = [str(t) for t in flags.thinking_tags]
@@ -65,9 +64,22 @@ def native_config(cfg: Dict[str, Any], host: str, port: int, engine: str, device
         "include_source_names": bool(agg.include_source_names),
         "env_api_key": os.environ.get("OPENAI_API_KEY", ""),
         "backends": backends,
-        "drain_s": float(rt.drain_timeout), "verify": bool(rt.verify), "ready_file": (os.environ["QMX_READY_FILE"] + f".{os.getpid()}") if os.environ.get("QMX_READY_FILE") else "",
+        "drain_s": float(rt.drain_timeout), "verify": bool(rt.verify),
+        "ca_file": _ca_bundle(), "tls_verify": os.environ.get("QMX_TLS_VERIFY", "1") not in ("0", "false"), "ready_file": (os.environ["QMX_READY_FILE"] + f".{os.getpid()}") if os.environ.get("QMX_READY_FILE") else "",
         **cluster_config(rt, port, engine),
     }
+
+
+def _ca_bundle() -> str:
+    """CA bundle for https upstreams: SSL_CERT_FILE, else certifi's (httpx's default), else system."""
+    if os.environ.get("SSL_CERT_FILE"):
+        return os.environ["SSL_CERT_FILE"]
+    try:
+        import certifi
+
+        return certifi.where()
+    except ImportError:
+        return ""
 
 
 def cluster_config(rt: RuntimeConfig, port: int, engine: str) -> Dict[str, Any]:

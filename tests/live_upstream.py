@@ -81,12 +81,19 @@ class LiveUpstream:
         self.ports: Dict[str, int] = {}
         self._servers = []
 
-    def serve(self, name: str, behaviour) -> int:
+    def serve(self, name: str, behaviour, tls=None) -> int:
+        """tls=(certfile, keyfile): serve HTTPS with that certificate."""
         self.behaviours[name] = behaviour
         if behaviour is not None and not callable(behaviour) and behaviour[0] == "refuse":
             self.ports[name] = free_port()
             return self.ports[name]
         srv = ThreadingHTTPServer(("127.0.0.1", 0), _Handler)
+        if tls:
+            import ssl
+
+            ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+            ctx.load_cert_chain(*tls)
+            srv.socket = ctx.wrap_socket(srv.socket, server_side=True)
         srv.daemon_threads = True
         srv.owner = self
         srv.name = name
