@@ -154,7 +154,7 @@ def main() -> int:
     ap.add_argument("--impl", default=os.environ.get("QMX_BENCH_IMPL", "native"), choices=["native", "python"])
     ap.add_argument("--engine", default=os.environ.get("QMX_BENCH_ENGINE", "auto"))
     ap.add_argument("--workers", type=int, default=4, help="python impl: proxy processes per rank")
-    ap.add_argument("--threads", type=int, default=4, help="native impl: io threads per rank")
+    ap.add_argument("--threads", type=int, default=8, help="native impl: io threads per rank")
     ap.add_argument("--lg-threads", type=int, default=2)
     ap.add_argument("--mock-threads", type=int, default=2)
     ap.add_argument("--skip-final", type=int, default=1)
