@@ -88,7 +88,7 @@ static_assert(TPL_BYTES == kTplBytes, "template size");
 enum : int {
   V_START = 0, V_NSEP, V_LASTSEP, V_ABORT, V_NEV, V_CONSUMED, V_STATUS, V_NDELTA, V_YLEN, V_NCAND,
   V_NTOK, V_BAIL, V_DEPTH0, V_TAILLEN, V_NEWTAIL, V_NEWDEPTH, V_WLEN, V_NEMIT, V_ETOT, V_OUTLEN,
-  V_TPLPRE, V_TPLSUF, V_TPLK, V_NEXTEV
+  V_TPLPRE, V_TPLSUF, V_TPLK, V_NEXTEV, V_NFULL, V_NTPL
 };
 
 // LDS byte reader that fetches one aligned 64-bit word per 8 sequential bytes: a byte-serial
@@ -328,6 +328,7 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
     s.v[V_STATUS] = 0;
     s.v[V_TPLK] = -1;
     s.v[V_NEXTEV] = 0;
+    s.v[V_NFULL] = s.v[V_NTPL] = 0;
     for (int q = 0; q < BS / 64; ++q) wtpl[q][0] = -1;
     if (fresh) {
       s.v[V_DEPTH0] = 0;
@@ -497,6 +498,7 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
         kind = EV_CONTENT;  // same shape as this stream's last parsed content event
         sa = e0 + tp;
         sb = e1 - ts;
+        if (lane == 0) atomicAdd(&s.v[V_NTPL], 1);
       } else {
         for (int q = 0; q < BS / 64 && kind != EV_CONTENT; ++q) {
           const int qi = (hint + q) & (BS / 64 - 1);
@@ -509,6 +511,7 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
             sa = e0 + ttp;
             sb = e1 - tts;
             hint = qi;
+            if (lane == 0) atomicAdd(&s.v[V_NTPL], 1);
           }
         }
         if (kind != EV_CONTENT && lit_at(s.A, e0, e1, QMX_LIT("data: "))) {
@@ -516,6 +519,7 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
           ustrip(s.A, &a, &b);
           if (!(b - a == 6 && lit_at(s.A, a, b, QMX_LIT("[DONE]")))) {
             nt = wave_lex(s.A, a, b, TKP[w], TKT[w], 0, TOK_CAP);
+            if (lane == 0) atomicAdd(&s.v[V_NFULL], 1);
             if (nt == -LEX_COMPLEX) {
               slow = true;
             } else if (nt > 64) {
@@ -961,7 +965,12 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
     }
   }
   QMX_STAMP(10);
-  if (Pk.dbg != nullptr && threadIdx.x == 0) Pk.dbg[blockIdx.x * 16 + 12] = __builtin_amdgcn_s_memtime();
+  if (Pk.dbg != nullptr && threadIdx.x == 0) {
+    Pk.dbg[blockIdx.x * 16 + 12] = __builtin_amdgcn_s_memtime();
+    Pk.dbg[blockIdx.x * 16 + 13] = (unsigned long long)s.v[V_NFULL];  // S3: events fully parsed
+    Pk.dbg[blockIdx.x * 16 + 14] = (unsigned long long)s.v[V_NTPL];   // S3: template hits
+    Pk.dbg[blockIdx.x * 16 + 15] = (unsigned long long)nev;
+  }
   if (tid == 0) {
     WorkResult r{(uint32_t)s.v[V_CONSUMED], (uint32_t)out_len, (uint32_t)s.v[V_STATUS], new_clen};
     res[blockIdx.x] = r;
@@ -1414,6 +1423,11 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
         }
       }
       stage_n_ += n;
+      for (int i = 0; i < n; ++i) {
+        s3_full_ += h_dbg_[16 * i + 13];
+        s3_tpl_ += h_dbg_[16 * i + 14];
+        s3_events_ += h_dbg_[16 * i + 15];
+      }
     }
   }
   for (int i = 0; i < n; ++i) {
@@ -1610,7 +1624,9 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
                                              {"fin_launches", (double)fin_launches_}, {"stage_items", (double)stage_n_},
                                              {"fin_items", (double)fin_items_}, {"fin_host", (double)fin_host_},
                                              {"fin_ms", fin_ms_}, {"h2d_bytes", (double)h2d_bytes_},
-                                             {"d2h_bytes", (double)d2h_bytes_}};
+                                             {"d2h_bytes", (double)d2h_bytes_},
+                                             {"s3_full_parses", (double)s3_full_}, {"s3_template_hits", (double)s3_tpl_},
+                                             {"s3_events", (double)s3_events_}};
   for (int k = 1; k < 11; ++k) m["stage" + std::to_string(k) + "_us"] = stage_us_[k];
   m["shader_mhz"] = clk_us_ > 0 ? clk_cycles_ / clk_us_ : 0.0;
   return m;

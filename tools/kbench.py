@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--slots", default="1,16,64,256,1024")
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--engine", default="hip")
+    ap.add_argument("--events-per-tick", type=int, default=0,
+                    help="stream the body N events per tick (steady-state serving shape); 0 = whole body in one tick")
     args = ap.parse_args()
     from quorum_amd.ops.native import NativeEngine
 
@@ -45,20 +47,24 @@ def main():
         for n in [int(x) for x in args.slots.split(",")]:
             eng = NativeEngine(args.engine, tags, device=0, max_slots=4096, content_cap=1 << 16)
             walls = []
+            evs = [e + b"\n\n" for e in body.split(b"\n\n") if e]
+            k = args.events_per_tick or len(evs)
+            pieces = [b"".join(evs[i:i + k]) for i in range(0, len(evs), k)]
             for it in range(args.iters):
                 slots = [eng.open(i % 8, filt, emit) for i in range(n)]
-                for s in slots:
-                    eng.feed(s, body)
-                    eng.finish(s)
-                t0 = time.perf_counter()
-                res, _ = eng.tick(1700000000)
-                walls.append(time.perf_counter() - t0)
-                assert len(res) == n, (len(res), n)
+                for pi, piece in enumerate(pieces):
+                    for s in slots:
+                        eng.feed(s, piece)
+                        if pi == len(pieces) - 1:
+                            eng.finish(s)
+                    t0 = time.perf_counter()
+                    res, _ = eng.tick(1700000000)
+                    walls.append(time.perf_counter() - t0)
                 for s in slots:
                     eng.release(s)
             st = eng._e.kernel_stats() if args.engine == "hip" else {}
             walls.sort()
-            rec = {"filter": filt, "emit": emit, "slots": n, "bytes_per_slot": len(body),
+            rec = {"filter": filt, "emit": emit, "slots": n, "bytes_per_slot": len(body), "events_per_tick": k,
                    "wall_us_p50": round(1e6 * walls[len(walls) // 2], 1),
                    "wall_us_min": round(1e6 * walls[0], 1)}
             if st:
@@ -68,7 +74,10 @@ def main():
                     rec["stage_us_per_item"] = {k: round(v / ni, 2) for k, v in st.items()
                                                 if k.startswith("stage") and k.endswith("_us")}
                 rec["shader_mhz"] = round(st.get("shader_mhz", 0), 1)
-                rec["MB_per_s"] = round(n * len(body) / (st["kernel_ms"] / max(st["launches"], 1)) / 1e3, 1)
+                if st.get("s3_events"):
+                    rec["s3_per_item"] = {k: round(st[k] / st["stage_items"], 2)
+                                          for k in ("s3_events", "s3_full_parses", "s3_template_hits")}
+                rec["MB_per_s"] = round(n * len(body) / len(pieces) / (st["kernel_ms"] / max(st["launches"], 1)) / 1e3, 1)
             results.append(rec)
             print(json.dumps(rec), flush=True)
     return results
