@@ -390,7 +390,7 @@ Exchange::~Exchange() {
   join();
 }
 void Exchange::post(XMsg&& m) {
-  if (!healthy_.load()) return;
+  if (stop_.load()) return;
   std::lock_guard<std::mutex> g(mu_);
   out_.push_back(std::move(m));
 }
@@ -418,6 +418,7 @@ void Exchange::run() {
     fprintf(stderr, "qmx exchange (rank %d): %s — spread placement disabled\n", o_.rank, e.what());
     return down();
   }
+  healthy_.store(true);  // sessions start placing streams on other ranks from now on
   int idle = 0;
   std::vector<std::string> all;
   std::vector<uint32_t> fl;

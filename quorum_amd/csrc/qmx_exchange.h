@@ -73,7 +73,7 @@ class Exchange {
   void post(XMsg&& m);       // thread-safe
   void request_stop();       // the thread exits once every rank has requested stop
   void join();
-  bool healthy() const { return healthy_.load(); }
+  bool healthy() const { return healthy_.load(); }  // false until connected and after a failure
   int rank() const { return o_.rank; }
   int world() const { return o_.world; }
   uint64_t rounds() const { return rounds_.load(); }
@@ -88,7 +88,7 @@ class Exchange {
   std::mutex mu_;
   std::condition_variable cv_;
   std::vector<XMsg> out_;
-  std::atomic<bool> stop_{false}, healthy_{true};
+  std::atomic<bool> stop_{false}, healthy_{false};  // healthy once the transport is up
   std::atomic<uint64_t> rounds_{0}, bytes_{0};
   std::atomic<double> busy_us_{0};
   std::thread th_;
