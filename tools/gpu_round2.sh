@@ -17,6 +17,5 @@ QMX_STAGE_TIMING=1 timeout -k 10 300 python tools/kbench.py --slots 1,64,256,102
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o native --output-format csv -- python3 bench.py --steps 5 --warmup 1 > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err || { echo "prof failed"; tail -5 gpurun_out/bench_prof.err; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VALU_MFMA_I8 SQ_INSTS_VALU_MFMA_MOPS_I8 --kernel-trace --stats -d gpurun_out/pmc -o pmc1 --output-format csv -- python3 tools/kbench.py --slots 256 --iters 10 > gpurun_out/pmc1.log 2>&1 || { echo "pmc1 failed"; tail -5 gpurun_out/pmc1.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --kernel-trace --stats -d gpurun_out/pmc -o pmc2 --output-format csv -- python3 tools/kbench.py --slots 256 --iters 10 > gpurun_out/pmc2.log 2>&1 || { echo "pmc2 failed"; tail -5 gpurun_out/pmc2.log; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE WRITE_SIZE --kernel-trace --stats -d gpurun_out/pmc -o pmc3 --output-format csv -- python3 tools/kbench.py --slots 256 --iters 10 > gpurun_out/pmc3.log 2>&1 || { echo "pmc3 failed"; tail -5 gpurun_out/pmc3.log; exit 1; }
 timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --stats -d gpurun_out/prof -o markers --output-format csv -- python3 bench.py --steps 2 --warmup 1 --batch 2048 > gpurun_out/bench_markers.json 2> gpurun_out/bench_markers.err || { echo "marker trace failed"; tail -5 gpurun_out/bench_markers.err; exit 1; }
 echo "all done"
