@@ -656,7 +656,26 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
   // ---- S4: think filter ----------------------------------------------------------------
   const uint8_t* W = Z;  // identity when not filtering
   int ncand = 0, ntok = 0;
+  bool any_lt = false;  // a '<' anywhere in Z (old holdback tail + new deltas)?
   if (filt && ndelta > 0) {
+    int found = 0;
+    for (int p = tid; p < Zn; p += BS) found |= Z[p] == '<';
+    any_lt = __syncthreads_or(found) != 0;
+  }
+  if (filt && ndelta > 0 && !any_lt) {
+    // no tag can start in these bytes (and no holdback is pending: a held tail starts with
+    // '<'): outside a think block every byte is kept, inside one every byte is dropped
+    const bool keep = depth0 == 0;
+    for (int j = tid; j < ndelta; j += BS) {
+      s.cut[j] = s.dl_end[j];
+      s.wpos[j] = keep ? s.dl_end[j] : 0;
+    }
+    if (tid == 0) {
+      s.v[V_WLEN] = keep ? Zn : 0;
+      s.v[V_NEWTAIL] = -1;
+      s.v[V_NEWDEPTH] = depth0;
+    }
+  } else if (filt && ndelta > 0) {
     // candidates
     {
       int C = (Zn + BS - 1) / BS;
@@ -1348,7 +1367,31 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
   }
   size_t in_off = 0, out_off = 0;
   int n = 0;
-  for (auto& w : work) {
+  // XCD-aware item order: the dispatcher hands workgroup i to XCD i % 8, so item i gets a
+  // stream with slot % 8 == i % 8 where possible — a stream's DevSlot state, template and
+  // content-arena tail stay in one XCD's L2 from tick to tick.  Host-path streams first.
+  std::vector<Work*> order;
+  order.reserve(work.size());
+  {
+    std::vector<Work*> b[8];
+    for (auto& w : work) {
+      if (w.slot >= max_slots_ || host_mode_[w.slot]) order.push_back(&w);
+      else b[w.slot & 7].push_back(&w);
+    }
+    size_t left = 0;
+    for (auto& q : b) left += q.size();
+    for (int i = 0; left; ++i) {
+      int bi = i & 7;
+      if (b[bi].empty())
+        for (int j = 0; j < 8; ++j)
+          if (b[j].size() > b[bi].size()) bi = j;  // affinity bucket empty: the fullest one
+      order.push_back(b[bi].back());
+      b[bi].pop_back();
+      --left;
+    }
+  }
+  for (Work* wp : order) {
+    Work& w = *wp;
     int slot = w.slot;
     SlotCore& c = core_[slot];
     if (slot >= max_slots_ || host_mode_[slot]) {
