@@ -29,3 +29,18 @@ def test_native_hip_keepalive(monkeypatch):
 
     monkeypatch.setattr(T, "native_server", hip_server)
     T.test_native_keepalive_many_requests()
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_native_hip_random_sessions(seed, monkeypatch):
+    """Random sessions (test_native_random_differential) through the HIP engine + verify."""
+    from quorum_amd.ops import native
+
+    import test_native_random_differential as R
+
+    ext = native.require()
+    before = ext.server_counters()["verify_mismatches"]
+    monkeypatch.setattr(T, "ENGINE", "hip")
+    monkeypatch.setattr(T, "VERIFY", True)
+    R.test_random_session_native_matches_python(seed)
+    assert ext.server_counters()["verify_mismatches"] == before
