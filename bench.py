@@ -135,6 +135,9 @@ def breakdown(m0, m1, elapsed):
         "streams_per_tick": round(d.get("qmx_tick_slots_total", 0.0) / ticks, 2) if ticks else None,
         "kernel_launches": int(launches),
         "tick_kernel_us_avg": round(1000 * d.get("qmx_kernel_kernel_ms", 0.0) / launches, 1) if launches else None,
+        "tick_host_prep_us_avg": round(d.get("qmx_kernel_host_prep_us", 0.0) / launches, 1) if launches else None,
+        "tick_launch_wait_us_avg": round(d.get("qmx_kernel_gpu_wait_us", 0.0) / launches, 1) if launches else None,
+        "tick_process_us_avg": round(d.get("qmx_kernel_process_us", 0.0) / launches, 1) if launches else None,
         "gpu_busy_frac": round(d.get("qmx_kernel_kernel_ms", 0.0) / 1000 / elapsed, 4) if elapsed else None,
         "finalize_launches": int(d.get("qmx_kernel_fin_launches", 0.0)),
         "h2d_MB": round(d.get("qmx_kernel_h2d_bytes", 0.0) / 1e6, 2),

@@ -1339,6 +1339,8 @@ std::string HipEngine::text(int slot) {
 }
 
 void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results) {
+  using HC = std::chrono::steady_clock;
+  const auto tp0 = HC::now();
   struct Pending {
     int slot;
     size_t carry_len;  // carry bytes that preceded w.data in the tile
@@ -1437,6 +1439,8 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
       std::memset(h_dbg_, 0, sizeof(unsigned long long) * 16 * n);
       params_.dbg = h_dbg_;
     }
+    const auto tp1 = HC::now();
+    host_prep_us_ += std::chrono::duration<double, std::micro>(tp1 - tp0).count();
     roctxRangePushA("qmx_tick");  // rocprofv3 --marker-trace: one range per tick launch + wait
     h2d_bytes_ += in_off;
     HIP_CHECK(hipEventRecord(ev0_, stream_));
@@ -1446,6 +1450,7 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
     HIP_CHECK(hipEventRecord(ev1_, stream_));
     wait_stream();
     roctxRangePop();
+    gpu_wait_us_ += std::chrono::duration<double, std::micro>(HC::now() - tp1).count();
     float ms = 0.f;
     hipEventElapsedTime(&ms, ev0_, ev1_);
     kernel_ms_ += ms;
@@ -1534,6 +1539,7 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
       dirty_.push_back(s);
     }
   }
+  process_us_ += std::chrono::duration<double, std::micro>(HC::now() - tp0).count();
 }
 
 void HipEngine::finalize_host(const FinalizeReq& r, std::vector<FinalizeRes>& out) {
@@ -1669,7 +1675,9 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
                                              {"fin_ms", fin_ms_}, {"h2d_bytes", (double)h2d_bytes_},
                                              {"d2h_bytes", (double)d2h_bytes_},
                                              {"s3_full_parses", (double)s3_full_}, {"s3_template_hits", (double)s3_tpl_},
-                                             {"s3_events", (double)s3_events_}};
+                                             {"s3_events", (double)s3_events_},
+                                             {"host_prep_us", host_prep_us_}, {"gpu_wait_us", gpu_wait_us_},
+                                             {"process_us", process_us_}};
   for (int k = 1; k < 11; ++k) m["stage" + std::to_string(k) + "_us"] = stage_us_[k];
   m["shader_mhz"] = clk_us_ > 0 ? clk_cycles_ / clk_us_ : 0.0;
   return m;
