@@ -45,12 +45,12 @@ namespace qmx {
                                __FILE__ + ":" + std::to_string(__LINE__));                 \
   } while (0)
 
-constexpr int BS = 256;
+constexpr int BS = 512;  // 8 waves: S3 spreads events over 8 waves; 2 waves per SIMD hide LDS latency
 constexpr int TILE_MAX = 16384;
 constexpr int MAX_EV = 512;  // events per tile (more → WS_MORE requeue); keeps LDS < 80 KiB (2 WG/CU)
 constexpr int MAX_CAND = 1024;
 constexpr int PAD = 16;
-constexpr int TOK_CAP = 1024;  // tokens per wave per round of 64 events
+constexpr int TOK_CAP = 512;  // tokens per wave (an event with more → scalar fallback)
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 
@@ -485,10 +485,14 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
     bool published = false;
     int hint = w;  // template that matched last (tried first)
     while (true) {
-      int k = 0;
-      if (lane == 0) k = atomicAdd(&s.v[V_NEXTEV], 1);
-      k = __builtin_amdgcn_readfirstlane(k);
-      if (k >= nev) break;
+      int g = 0;
+      if (lane == 0) g = atomicAdd(&s.v[V_NEXTEV], 1);
+      g = __builtin_amdgcn_readfirstlane(g);
+      if (g >= nev) break;
+      // pull order: the first 4 events, then the last 4 (a stream's closing events — finish
+      // reason, usage, [DONE] — usually have their own shape and need a full parse), then the
+      // middle, which by then matches a published template: the few full parses overlap
+      const int k = nev <= 8 ? g : g < 4 ? g : g < 8 ? nev - 1 - (g - 4) : g - 4;
       const int e0 = s.ev_a[k], e1 = s.ev_b[k];
       int kind = EV_SKIP, sa = 0, sb = 0, body = -1;
       bool slow = false, lexed = false;
