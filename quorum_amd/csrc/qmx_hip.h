@@ -122,7 +122,8 @@ class HipEngine : public HostEngine {
   double kernel_ms_ = 0.0, fin_ms_ = 0.0;
   uint64_t h2d_bytes_ = 0, d2h_bytes_ = 0;
   uint64_t s3_full_ = 0, s3_tpl_ = 0, s3_events_ = 0;  // QMX_STAGE_TIMING: S3 path counters
-  double host_prep_us_ = 0, gpu_wait_us_ = 0, process_us_ = 0;  // host-side tick breakdown  // zero-copy arena traffic (device reads / host reads)
+  double host_prep_us_ = 0, gpu_wait_us_ = 0, process_us_ = 0;  // host-side tick breakdown
+  int spin_us_ = 0;  // QMX_WAIT_SPIN_US: yield-poll before the blocking wait  // zero-copy arena traffic (device reads / host reads)
   unsigned long long* h_dbg_ = nullptr;
   size_t dbg_cap_ = 0;
   double stage_us_[16] = {0};

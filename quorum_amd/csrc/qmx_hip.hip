@@ -23,6 +23,8 @@
 
 #include <rocprofiler-sdk-roctx/roctx.h>
 
+#include <sched.h>
+
 #include <chrono>
 #include <thread>
 
@@ -1216,6 +1218,13 @@ static void put(char* dst, int cap, int* len, const std::string& s) {
 // hipStreamSynchronize (one core burnt per engine) and 77 us polling with sleep_for.
 void HipEngine::wait_stream() {
   HIP_CHECK(hipEventRecord(evb_, stream_));
+  if (spin_us_ > 0) {  // optional: yield-poll for the expected kernel time before sleeping
+    const auto t0 = std::chrono::steady_clock::now();
+    while (hipEventQuery(evb_) == hipErrorNotReady) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_)) break;
+      sched_yield();
+    }
+  }
   HIP_CHECK(hipEventSynchronize(evb_));
 }
 
@@ -1231,6 +1240,7 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
   HIP_CHECK(hipEventCreate(&ev0_));
   HIP_CHECK(hipEventCreate(&ev1_));
   HIP_CHECK(hipEventCreateWithFlags(&evb_, hipEventBlockingSync | hipEventDisableTiming));
+  if (const char* sp = getenv("QMX_WAIT_SPIN_US")) spin_us_ = atoi(sp);
   HIP_CHECK(hipMalloc(&d_state_, sizeof(DevSlot) * (size_t)max_slots_));
   HIP_CHECK(hipMemset(d_state_, 0, sizeof(DevSlot) * (size_t)max_slots_));
   HIP_CHECK(hipMalloc(&d_content_, (size_t)content_cap_ * (size_t)max_slots_));
