@@ -150,9 +150,45 @@ std::string final_prefix(int64_t created) {
 // --------------------------------------------------------------------------------
 // per-stream processing (sequential)
 // --------------------------------------------------------------------------------
+// Is x[a:b) a complete JSON string body (valid escapes, no control characters, no unescaped
+// quote, strict UTF-8)?  The template fast path of the CPU engine (the HIP kernel's
+// wave_str_body, sequentially).
+static bool str_body_ok(const uint8_t* x, int a, int b) {
+  for (int p = a; p < b; ++p) {
+    const uint8_t c = x[p];
+    if (c == '"' || c < 0x20) return false;
+    if (c == '\\') {
+      if (++p >= b) return false;
+      const uint8_t d = x[p];
+      if (d == 'u') {
+        if (p + 4 >= b) return false;
+        for (int k = 1; k <= 4; ++k)
+          if (hexv(x[p + k]) < 0) return false;
+        p += 4;
+      } else if (!(d == '"' || d == '\\' || d == '/' || d == 'b' || d == 'f' || d == 'n' || d == 'r' || d == 't')) {
+        return false;
+      }
+    }
+  }
+  return utf8_valid(x, a, b);
+}
+
 static void handle_event(const TagSet& ts, SlotCore& s, const uint8_t* e, int m, int64_t created,
                          std::string& out, std::string& scratch) {
-  EvResult r = classify_event(e, m);
+  EvResult r;
+  const int tp = (int)s.tpl_pre.size(), tsz = (int)s.tpl_suf.size();
+  if (tp > 0 && m >= tp + tsz && std::memcmp(e, s.tpl_pre.data(), tp) == 0 &&
+      std::memcmp(e + m - tsz, s.tpl_suf.data(), tsz) == 0 && str_body_ok(e, tp, m - tsz)) {
+    r.kind = EV_CONTENT;  // same shape as this stream's last parsed content event
+    r.str_a = tp;
+    r.str_b = m - tsz;
+  } else {
+    r = classify_event(e, m);
+    if (r.kind == EV_CONTENT && r.str_a <= 256 && m - r.str_b <= 64) {
+      s.tpl_pre.assign((const char*)e, r.str_a);
+      s.tpl_suf.assign((const char*)e + r.str_b, m - r.str_b);
+    }
+  }
   if (r.kind == EV_SKIP) return;
   if (r.kind == EV_ABORT) {
     s.aborted = true;
@@ -195,9 +231,9 @@ void process_slot(const TagSet& ts, SlotCore& s, const uint8_t* data, size_t n, 
   }
   std::string scratch;
   while (!s.aborted) {
-    int j = pos;
-    while (j + 1 < N && !(x[j] == '\n' && x[j + 1] == '\n')) ++j;
-    if (j + 1 >= N) break;
+    const void* hit = memmem(x + pos, (size_t)(N - pos), "\n\n", 2);  // leftmost separator
+    if (!hit) break;
+    const int j = (int)((const uint8_t*)hit - x);
     handle_event(ts, s, x + pos, j - pos, created, out, scratch);
     pos = j + 2;
   }

@@ -53,6 +53,9 @@ struct SlotCore {
   std::string carry;  // unframed upstream bytes
   FilterState fs;
   std::string content;  // accumulated filtered content (host engine / fallback)
+  // shape template: bytes around the content string of the last fully parsed content event
+  // (an event identical outside a valid string body has the same parse — see qmx_lex.h)
+  std::string tpl_pre, tpl_suf;
 };
 
 // Process newly arrived bytes of one stream (sequential algorithm); appends SSE to out.
