@@ -99,6 +99,7 @@ ServerCfg server_cfg_from(const py::dict& d) {
   gs("xchg_addr", c.xchg_addr); gi("xchg_port", c.xchg_port); gs("xchg_id_file", c.xchg_id_file);
   gi("xchg_round_us", c.xchg_round_us); gd("xchg_timeout", c.xchg_timeout);
   gd("drain_s", c.drain_s); gs("ready_file", c.ready_file); gb("verify", c.verify);
+  gi("shared_engine", c.shared_engine);
   gs("ca_file", c.ca_file); gb("tls_verify", c.tls_verify);
   if (d.contains("backends")) {
     for (auto item : py::cast<py::list>(d["backends"])) {

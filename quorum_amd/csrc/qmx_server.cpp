@@ -21,6 +21,7 @@
 #include <mutex>
 #include <thread>
 
+#include <functional>
 #include <map>
 
 #include <openssl/err.h>
@@ -462,21 +463,163 @@ class Verifier {
 };
 
 // --------------------------------------------------------------------------------------
+// GPU hub: ONE HIP engine per process shared by every io loop.  A single tick thread batches
+// the pending bytes of all loops' streams into one launch of the fused tick kernel (the
+// SURVEY's "pack pending upstream bytes of ALL active streams on this rank"), then routes
+// each stream's results back to the loop that owns it (per-loop queue + eventfd).
+// --------------------------------------------------------------------------------------
+class GpuHub {
+ public:
+  using Sink = std::function<void(ResultBatch&&)>;
+  GpuHub(const ServerCfg& cfg, int nloops) : cfg_(cfg), sinks_(nloops) {
+    if (cfg.engine == "hip")
+      eng_.reset(new HipEngine(cfg.tags, cfg.device, cfg.tile, cfg.max_slots, cfg.content_cap));
+    else
+      eng_.reset(new CpuEngine(cfg.tags));  // shared CPU engine: exercises the hub routing on CPU
+    if (cfg.verify) ver_.reset(new Verifier(cfg.tags));
+  }
+  ~GpuHub() {
+    stop_ = true;
+    cv_.notify_all();
+    if (th_.joinable()) th_.join();
+  }
+  void start() { th_ = std::thread([this] { run(); }); }
+  void attach(int loop, Sink s) { sinks_[loop] = std::move(s); }
+  int open(int loop, int index, bool f, bool e) {
+    int slot = eng_->open(index, f, e);
+    {
+      std::lock_guard<std::mutex> g(omu_);
+      if ((int)owner_.size() <= slot) owner_.resize(slot + 1024, -1);
+      owner_[slot] = loop;
+    }
+    if (ver_) ver_->open(slot, index, f, e);
+    return slot;
+  }
+  void feed(int slot, const std::string& d) {
+    eng_->feed(slot, d);
+    if (ver_) ver_->feed(slot, d);
+  }
+  void finish(int slot) {
+    eng_->finish(slot);
+    if (ver_) ver_->finish(slot);
+  }
+  void release(int slot) {
+    eng_->release(slot);
+    if (ver_) ver_->release(slot);
+  }
+  int submit(int loop, const std::vector<int>& slots, bool strip, bool texts, const std::string& joiner,
+             int64_t created) {
+    std::lock_guard<std::mutex> g(omu_);  // the id must be routable before the tick thread sees it
+    int id = eng_->submit_finalize(slots, strip, texts, joiner, created);
+    fin_owner_[id] = loop;
+    if (ver_) ver_->submit(id, slots, strip, texts, joiner, created);
+    return id;
+  }
+  void kick() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      work_ = true;
+    }
+    cv_.notify_one();
+  }
+  std::unordered_map<std::string, double> snapshot() {
+    std::lock_guard<std::mutex> g(smu_);
+    return snap_;
+  }
+
+ private:
+  void run() {
+    if (cfg_.engine == "hip") hipSetDevice(cfg_.device);
+    double last_snap = 0;
+    std::vector<ResultBatch> per(sinks_.size());
+    while (!stop_) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait_for(lk, std::chrono::milliseconds(2), [this] { return work_ || stop_; });
+        work_ = false;
+      }
+      if (stop_) break;
+      while (eng_->has_work()) {
+        ResultBatch rb;
+        const double tt = now_s();
+        const int64_t created = (int64_t)time(nullptr);
+        eng_->tick(created, rb.r, rb.f);
+        h_tick.observe(now_s() - tt);
+        if (ver_) ver_->check(created, rb.r, rb.f);
+        c_ticks++;
+        c_tick_slots += rb.r.size();
+        {
+          std::lock_guard<std::mutex> g(omu_);
+          for (auto& r : rb.r) {
+            const int l = r.slot < (int)owner_.size() ? owner_[r.slot] : -1;
+            if (l >= 0) per[l].r.push_back(std::move(r));
+          }
+          for (auto& f : rb.f) {
+            auto it = fin_owner_.find(f.id);
+            if (it == fin_owner_.end()) continue;
+            per[it->second].f.push_back(std::move(f));
+            fin_owner_.erase(it);
+          }
+        }
+        for (size_t l = 0; l < per.size(); ++l) {
+          if (per[l].r.empty() && per[l].f.empty()) continue;
+          if (sinks_[l]) sinks_[l](std::move(per[l]));
+          per[l] = ResultBatch();
+        }
+        if (tt - last_snap > 0.05) {
+          std::unordered_map<std::string, double> m;
+          for (auto& kv : eng_->stats()) m["qmx_engine_" + kv.first] = kv.second;
+          if (auto* h = dynamic_cast<HipEngine*>(eng_.get()))
+            for (auto& kv : h->kernel_stats()) m["qmx_kernel_" + kv.first] = kv.second;
+          std::lock_guard<std::mutex> g(smu_);
+          snap_.swap(m);
+          last_snap = tt;
+        }
+      }
+    }
+  }
+  const ServerCfg& cfg_;
+  std::unique_ptr<HostEngine> eng_;
+  std::unique_ptr<Verifier> ver_;
+  std::vector<Sink> sinks_;
+  std::mutex mu_, omu_, smu_;
+  std::condition_variable cv_;
+  bool work_ = false;
+  std::atomic<bool> stop_{false};
+  std::vector<int> owner_;                  // slot → io loop
+  std::unordered_map<int, int> fin_owner_;  // finalize id → io loop
+  std::unordered_map<std::string, double> snap_;
+  std::thread th_;
+};
+
+// --------------------------------------------------------------------------------------
 // io loop (one per thread)
 // --------------------------------------------------------------------------------------
 class Loop {
  public:
   Loop(const ServerCfg& cfg, int idx) : cfg_(cfg), idx_(idx) { xfd_ = eventfd(0, EFD_NONBLOCK); }
   void attach_exchange(Exchange* x) { xch_ = x; }
+  void attach_hub(GpuHub* h) {
+    hub_ = h;
+    if (h)
+      h->attach(idx_, [this](ResultBatch&& rb) {
+        {
+          std::lock_guard<std::mutex> g(rmu_);
+          rq_.push_back(std::move(rb));
+        }
+        uint64_t one = 1;
+        ssize_t w = write(evfd_, &one, 8);
+        (void)w;
+      });
+  }
   void attach_tls(SSL_CTX* t) { tls_ = t; }
   void attach_loops(const std::vector<Loop*>* ls) { loops_ = ls; }
   std::mutex smu_;
   std::unordered_map<std::string, double> snap_;  // engine stats snapshot (read by /metrics on any loop)
   void snapshot() {
+    if (!eng_) return;
     std::unordered_map<std::string, double> m;
     for (auto& kv : eng_->stats()) m["qmx_engine_" + kv.first] = kv.second;
-    if (offload_)
-      for (auto& kv : static_cast<HipEngine*>(eng_.get())->kernel_stats()) m["qmx_kernel_" + kv.first] = kv.second;
     std::lock_guard<std::mutex> g(smu_);
     snap_.swap(m);
   }
@@ -491,9 +634,6 @@ class Loop {
     (void)w;
   }
   ~Loop() {
-    stop_gpu_ = true;
-    cv_.notify_all();
-    if (gpu_thread_.joinable()) gpu_thread_.join();
     for (auto& kv : idle_ssl_) SSL_free(kv.second);  // before the run's SSL_CTX goes away
     for (auto& kv : ups_)
       if (kv.second->ssl) SSL_free(kv.second->ssl);
@@ -514,12 +654,10 @@ class Loop {
       int n = epoll_wait(ep_, evs.data(), (int)evs.size(), 50);
       for (int i = 0; i < n; ++i) dispatch(evs[i]);
       if (g_drain.load() && drain_step()) break;
-      if (!offload_ && eng_->has_work()) tick_inline();
-      if (offload_ && kick_) {
+      if (!hub_ && eng_->has_work()) tick_inline();
+      if (hub_ && kick_) {
         kick_ = false;
-        std::lock_guard<std::mutex> g(mu_);
-        work_ = true;
-        cv_.notify_one();
+        hub_->kick();
       }
       if (!pending_requests_.empty()) {
         std::vector<int> fds;
@@ -534,7 +672,7 @@ class Loop {
       if (t - last_sweep > 0.1) {
         sweep_timeouts(t);
         last_sweep = t;
-        if (!offload_) snapshot();  // (the HIP tick thread snapshots its own engine)
+        snapshot();  // own CPU engine (the GPU hub snapshots the shared HIP engine)
       }
     }
   }
@@ -558,15 +696,10 @@ class Loop {
     add(evfd_, EPOLLIN, tag_event());
     add(xfd_, EPOLLIN, tag(5, 0));
     idle_.resize(cfg_.backends.size());
-    if (cfg_.engine == "hip") {
-      eng_.reset(new HipEngine(cfg_.tags, cfg_.device, cfg_.tile, cfg_.max_slots, cfg_.content_cap));
-      offload_ = true;
-      gpu_thread_ = std::thread([this] { gpu_loop(); });
-    } else {
+    if (!hub_) {  // CPU engine: ticked inline by this io loop
       eng_.reset(new CpuEngine(cfg_.tags));
-      offload_ = false;
+      if (cfg_.verify) ver_.reset(new Verifier(cfg_.tags));
     }
-    if (cfg_.verify) ver_.reset(new Verifier(cfg_.tags));
   }
 
   // epoll tags: fd in low 32 bits, kind in high bits
@@ -605,38 +738,6 @@ class Loop {
   }
 
   // ---------------------------------------------------------------- engine plumbing
-  void gpu_loop() {
-    while (!stop_gpu_) {
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait_for(lk, std::chrono::milliseconds(2), [this] { return work_ || stop_gpu_; });
-        work_ = false;
-      }
-      if (stop_gpu_) break;
-      while (eng_->has_work()) {
-        ResultBatch rb;
-        const double tt = now_s();
-        const int64_t created = (int64_t)time(nullptr);
-        eng_->tick(created, rb.r, rb.f);
-        h_tick.observe(now_s() - tt);
-        if (ver_) ver_->check(created, rb.r, rb.f);
-        if (tt - last_snap_ > 0.05) {
-          snapshot();
-          last_snap_ = tt;
-        }
-        c_ticks++;
-        c_tick_slots += rb.r.size();
-        if (rb.r.empty() && rb.f.empty()) continue;
-        {
-          std::lock_guard<std::mutex> g(rmu_);
-          rq_.push_back(std::move(rb));
-        }
-        uint64_t one = 1;
-        ssize_t w = write(evfd_, &one, 8);
-        (void)w;
-      }
-    }
-  }
   void tick_inline() {
     ResultBatch rb;
     const double tt = now_s();
@@ -690,23 +791,28 @@ class Loop {
   void kick() { kick_ = true; }
   // engine calls, mirrored into the verify shadow when enabled
   int e_open(int index, bool f, bool e) {
+    if (hub_) return hub_->open(idx_, index, f, e);
     int slot = eng_->open(index, f, e);
     if (ver_) ver_->open(slot, index, f, e);
     return slot;
   }
   void e_feed(int slot, const std::string& d) {
+    if (hub_) return hub_->feed(slot, d);
     eng_->feed(slot, d);
     if (ver_) ver_->feed(slot, d);
   }
   void e_finish(int slot) {
+    if (hub_) return hub_->finish(slot);
     eng_->finish(slot);
     if (ver_) ver_->finish(slot);
   }
   void e_release(int slot) {
+    if (hub_) return hub_->release(slot);
     eng_->release(slot);
     if (ver_) ver_->release(slot);
   }
   int e_submit(const std::vector<int>& slots, bool strip, bool texts, const std::string& joiner, int64_t created) {
+    if (hub_) return hub_->submit(idx_, slots, strip, texts, joiner, created);
     int id = eng_->submit_finalize(slots, strip, texts, joiner, created);
     if (ver_) ver_->submit(id, slots, strip, texts, joiner, created);
     return id;
@@ -1890,7 +1996,7 @@ class Loop {
         err = cfg_.hide_final ? "expected string or bytes-like object" : "sequence item 0: expected str instance";
         break;
       }
-      processed.push_back(cfg_.hide_final ? strip_final(eng_->tagset(), (const uint8_t*)content->s.data(),
+      processed.push_back(cfg_.hide_final ? strip_final(ts_, (const uint8_t*)content->s.data(),
                                                         content->s.size())
                                           : content->s);
     }
@@ -2054,6 +2160,8 @@ class Loop {
       std::lock_guard<std::mutex> g(l->smu_);
       for (auto& kv : l->snap_) tot[kv.first] += kv.second;
     }
+    if (hub_)
+      for (auto& kv : hub_->snapshot()) tot[kv.first] += kv.second;
     for (auto& kv : tot) put(kv.first.c_str(), kv.second);
     return m;
   }
@@ -2061,14 +2169,12 @@ class Loop {
   const ServerCfg& cfg_;
   int idx_;
   int ep_ = -1, lfd_ = -1, evfd_ = -1;
-  std::unique_ptr<HostEngine> eng_;
+  std::unique_ptr<HostEngine> eng_;  // CPU engine (no GPU hub)
   std::unique_ptr<Verifier> ver_;
-  bool offload_ = false, kick_ = false;
-  std::thread gpu_thread_;
-  std::mutex mu_, rmu_;
-  std::condition_variable cv_;
-  bool work_ = false;
-  std::atomic<bool> stop_gpu_{false};
+  GpuHub* hub_ = nullptr;            // shared HIP engine
+  TagSet ts_ = make_tagset(cfg_.tags);
+  bool kick_ = false;
+  std::mutex rmu_;
   std::vector<ResultBatch> rq_;
   std::unordered_map<int, std::unique_ptr<Client>> clients_;
   std::unordered_map<int, std::unique_ptr<Up>> ups_;
@@ -2139,10 +2245,15 @@ int run_server(const ServerCfg& cfg0) {
   for (int i = 0; i < std::max(1, cfg.threads); ++i) loops.emplace_back(new Loop(cfg, i));
   std::vector<Loop*> loop_ptrs;
   for (auto& l : loops) loop_ptrs.push_back(l.get());
+  std::unique_ptr<GpuHub> hub;
+  const bool shared = cfg.shared_engine < 0 ? cfg.engine == "hip" : cfg.shared_engine > 0;
+  if (shared) hub.reset(new GpuHub(cfg, (int)loops.size()));
   for (auto& l : loops) {
     l->attach_loops(&loop_ptrs);
     l->attach_tls(tls);
+    l->attach_hub(hub.get());
   }
+  if (hub) hub->start();
   std::unique_ptr<Exchange> xch;
   if (cfg.world > 1 && cfg.placement == "spread") {
     XOptions o;
@@ -2177,6 +2288,7 @@ int run_server(const ServerCfg& cfg0) {
     xch->join();
     xch.reset();
   }
+  hub.reset();  // tick thread joined before the loops (its result sinks) go away
   loops.clear();
   if (tls) SSL_CTX_free(tls);
   return 0;

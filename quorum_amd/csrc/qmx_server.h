@@ -32,6 +32,7 @@ struct ServerCfg {
   int threads = 2;
   // engine
   std::string engine = "cpu";
+  int shared_engine = -1;  // one engine per process shared by all io loops (-1: auto = hip only)
   int device = 0;
   int tile = 16384, max_slots = 4096, content_cap = 1 << 20;
   // config

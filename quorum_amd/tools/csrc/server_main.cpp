@@ -88,6 +88,7 @@ int main(int argc, char** argv) {
   c.drain_s = gd(d, "drain_s", c.drain_s);
   c.ready_file = gs(d, "ready_file", "");
   c.verify = gb(d, "verify", false);
+  c.shared_engine = gi(d, "shared_engine", -1);
   c.ca_file = gs(d, "ca_file", "");
   c.tls_verify = gb(d, "tls_verify", true);
   if (const JVal* bs = d.get("backends")) {

@@ -214,6 +214,8 @@ class RuntimeConfig:
     total_timeout: optional per-backend total deadline in seconds (None = quorum semantics)
     drain_timeout: SIGTERM grace period for in-flight sessions (rolling reload / shutdown)
     verify:    debug mode: a shadow CPU oracle engine checks every stream and final (QMX_VERIFY=1)
+    shared_engine: "auto" (one engine per process shared by all io loops for hip, per-loop
+               engines for cpu) | true | false (QMX_SHARED_ENGINE=0/1)
     """
 
     engine: str = "auto"
@@ -228,6 +230,7 @@ class RuntimeConfig:
     total_timeout: Optional[float] = None
     drain_timeout: float = 10.0
     verify: bool = False
+    shared_engine: Any = "auto"
     log_content: bool = False
 
     @classmethod
@@ -240,5 +243,7 @@ class RuntimeConfig:
             rt["placement"] = os.environ["QMX_PLACEMENT"]
         if os.environ.get("QMX_VERIFY"):
             rt["verify"] = os.environ["QMX_VERIFY"] not in ("0", "", "false")
+        if os.environ.get("QMX_SHARED_ENGINE"):
+            rt["shared_engine"] = os.environ["QMX_SHARED_ENGINE"] not in ("0", "false")
         known = {k: v for k, v in rt.items() if k in cls.__dataclass_fields__}
         return cls(**known)

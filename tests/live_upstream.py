@@ -14,7 +14,7 @@ import socket
 import threading
 import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
-from typing import Any, Dict, List
+from typing import Any, Dict, List, Optional
 
 
 def free_port() -> int:
@@ -111,10 +111,11 @@ class LiveUpstream:
 
 @contextlib.contextmanager
 def native_server(cfg: Dict[str, Any], engine: str = "cpu", threads: int = 1, env_key: str = "",
-                  verify: bool = False):
+                  verify: bool = False, shared: Optional[bool] = None):
     """Run the C++ data plane in-process (background thread) for one config.
 
-    verify: run the shadow CPU-oracle engine (server_counters()['verify_mismatches'])."""
+    verify: run the shadow CPU-oracle engine (server_counters()['verify_mismatches']).
+    shared: one engine per process shared by all io loops (None = the config's default)."""
     import http.client
     import os
 
@@ -127,6 +128,8 @@ def native_server(cfg: Dict[str, Any], engine: str = "cpu", threads: int = 1, en
     d["install_signals"] = False
     d["env_api_key"] = env_key
     d["verify"] = verify
+    if shared is not None:
+        d["shared_engine"] = int(shared)
     th = threading.Thread(target=ext.run_server, args=(d,), daemon=True)
     th.start()
     t0 = time.time()

@@ -323,3 +323,46 @@ def test_native_verify_mode_plumbing():
     after = ext.server_counters()
     assert after["verify_checked"] - before["verify_checked"] >= 12  # 8 streams + 4 finals
     assert after["verify_mismatches"] == before["verify_mismatches"]
+
+
+def _per_stream(evs):
+    per = {}
+    for e in evs:
+        per.setdefault(e["id"] if isinstance(e, dict) else e, []).append(e)
+    return per
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_native_shared_engine_many_loops(threads):
+    """One engine per process shared by every io loop (the GPU-hub topology, here with the
+    CPU engine): concurrent sessions land on different loops, the hub's tick thread routes
+    each stream's results back to its owning loop, and the shadow oracle sees no mismatch."""
+    import concurrent.futures as cf
+
+    ext = native.require()
+    before = ext.server_counters()
+    live = LiveUpstream()
+    p1 = live.serve("b1", ("stream", 200, THINK))
+    p2 = live.serve("b2", ("stream", 200, sse_stream(["Wor", "ld <think>x</think>", " é😀"])))
+    cfg = cfg_parallel(2, block=dict(CONCAT, hide_final_think=True))
+    cfg["primary_backends"][0]["url"] = f"http://127.0.0.1:{p1}/v1"
+    cfg["primary_backends"][1]["url"] = f"http://127.0.0.1:{p2}/v1"
+    req = {"messages": MSG, "stream": True}
+    try:
+        with native_server(cfg) as port:
+            ref = _norm_sse(httpx.post(f"http://127.0.0.1:{port}/chat/completions", json=req, headers=AUTH,
+                                       timeout=30).text)
+        with native_server(cfg, threads=threads, verify=True, shared=True) as port:
+            def one(_):
+                with httpx.Client(base_url=f"http://127.0.0.1:{port}") as cl:
+                    return [_norm_sse(cl.post("/chat/completions", json=req, headers=AUTH, timeout=30).text)
+                            for _ in range(6)]
+            with cf.ThreadPoolExecutor(8) as ex:
+                for res in ex.map(one, range(8)):
+                    for r in res:  # backends interleave in arrival order: compare per stream
+                        assert _per_stream(r) == _per_stream(ref)
+    finally:
+        live.close()
+    after = ext.server_counters()
+    assert after["verify_checked"] - before["verify_checked"] >= 48 * 3
+    assert after["verify_mismatches"] == before["verify_mismatches"]
