@@ -37,12 +37,12 @@ struct PyStripper {
   py::bytes strip(const std::string& s) { return py::bytes(strip_final(ts, (const uint8_t*)s.data(), s.size())); }
 };
 
-py::tuple tick_to_py(HostEngine& e, int64_t created) {
+py::tuple tick_to_py(HostEngine& e, int64_t created, int lane = 0, std::vector<int>* taken = nullptr) {
   std::vector<SlotResult> results;
   std::vector<FinalizeRes> fres;
   {
     py::gil_scoped_release nogil;
-    e.tick(created, results, fres);
+    e.tick(created, results, fres, lane, taken);
   }
   py::list r;
   for (auto& x : results) r.append(py::make_tuple(x.slot, py::bytes(x.sse), x.flags));
@@ -69,7 +69,19 @@ void bind_engine(py::class_<E>& c) {
       .def("release", &E::release)
       .def("submit_finalize", &E::submit_finalize)
       .def("has_work", &E::has_work)
-      .def("tick", [](E& e, int64_t created) { return tick_to_py(e, created); })
+      .def("tick", [](E& e, int64_t created, int lane) { return tick_to_py(e, created, lane); }, py::arg("created"),
+           py::arg("lane") = 0)
+      // multi-lane protocol: the slots of an unsettled tick stay busy (skipped by other lanes)
+      // until settle(taken) — callers deliver the results first, keeping per-stream order
+      .def("tick_unsettled", [](E& e, int64_t created, int lane) {
+        std::vector<int> taken;
+        py::tuple t = tick_to_py(e, created, lane, &taken);
+        return py::make_tuple(t[0], t[1], taken);
+      })
+      .def("settle", [](E& e, const std::vector<int>& taken) {
+        py::gil_scoped_release nogil;
+        e.settle(taken);
+      })
       .def("text", [](E& e, int slot) { return py::bytes(e.text(slot)); })
       .def("stats", &E::stats);
 }
@@ -99,7 +111,7 @@ ServerCfg server_cfg_from(const py::dict& d) {
   gs("xchg_addr", c.xchg_addr); gi("xchg_port", c.xchg_port); gs("xchg_id_file", c.xchg_id_file);
   gi("xchg_round_us", c.xchg_round_us); gd("xchg_timeout", c.xchg_timeout);
   gd("drain_s", c.drain_s); gs("ready_file", c.ready_file); gb("verify", c.verify);
-  gi("shared_engine", c.shared_engine);
+  gi("shared_engine", c.shared_engine); gi("tick_lanes", c.tick_lanes);
   gs("ca_file", c.ca_file); gb("tls_verify", c.tls_verify);
   if (d.contains("backends")) {
     for (auto item : py::cast<py::list>(d["backends"])) {
@@ -221,8 +233,9 @@ PYBIND11_MODULE(_qmx, m) {
   ce.def(py::init<const std::vector<std::string>&>());
   bind_engine(ce);
   py::class_<HipEngine> he(m, "HipEngine");
-  he.def(py::init<const std::vector<std::string>&, int, int, int, int>(), py::arg("tags"), py::arg("device"),
-         py::arg("tile_bytes") = 16384, py::arg("max_slots") = 8192, py::arg("content_cap") = 1 << 20);
+  he.def(py::init<const std::vector<std::string>&, int, int, int, int, int>(), py::arg("tags"), py::arg("device"),
+         py::arg("tile_bytes") = 16384, py::arg("max_slots") = 8192, py::arg("content_cap") = 1 << 20,
+         py::arg("lanes") = 1);
   bind_engine(he);
   he.def("kernel_stats", &HipEngine::kernel_stats);
 }

@@ -346,40 +346,71 @@ int HostEngine::submit_finalize(const std::vector<int>& slots, bool strip, bool 
 
 bool HostEngine::has_work() {
   std::lock_guard<std::mutex> g(mu_);
-  return !dirty_.empty() || !fin_.empty();
+  if (!fin_.empty()) return true;
+  for (int s : dirty_)
+    if (!meta_[s].busy) return true;
+  return false;
 }
 
-void HostEngine::tick(int64_t created, std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres) {
+bool HostEngine::tick(int64_t created, std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres, int lane,
+                      std::vector<int>* taken) {
   std::vector<Work> work;
   std::vector<FinalizeReq> fin;
   {
     std::lock_guard<std::mutex> g(mu_);
+    std::vector<int> keep;
     for (int s : pending_free_) {
+      if (meta_[s].busy) {  // still in flight on another lane: free it once settled
+        keep.push_back(s);
+        continue;
+      }
       on_free(s);
       free_.push_back(s);
     }
-    pending_free_.clear();
+    pending_free_.swap(keep);
+    keep.clear();
     work.reserve(dirty_.size());
     for (int s : dirty_) {
       Meta& m = meta_[s];
+      if (m.busy && m.live) {  // this stream's previous tick is not settled: next time
+        keep.push_back(s);
+        continue;
+      }
       m.dirty = false;
       if (!m.live) continue;
       Work w{s, std::string(), m.eof, m.fresh};
       w.data.swap(m.incoming);
       m.fresh = false;
+      m.busy = true;
       work.push_back(std::move(w));
     }
-    dirty_.clear();
+    dirty_.swap(keep);
     fin.swap(fin_);
-    ++ticks_;
+    if (!work.empty() || !fin.empty()) ++ticks_;
   }
-  if (!work.empty()) process(work, created, results);
-  for (auto& r : results) bytes_out_ += r.sse.size();
-  if (!fin.empty()) finalize(fin, fres);
+  if (work.empty() && fin.empty()) return false;
+  if (!work.empty()) process(work, created, results, lane);
+  size_t out = 0;
+  for (auto& r : results) out += r.sse.size();
+  std::vector<int> slots;
+  std::vector<int>& tk = taken ? *taken : slots;
+  for (auto& w : work) tk.push_back(w.slot);
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    bytes_out_ += out;
+  }
+  if (!fin.empty()) finalize(fin, fres, lane);
+  if (!taken) settle(slots);
+  return true;
+}
+
+void HostEngine::settle(const std::vector<int>& taken) {
+  std::lock_guard<std::mutex> g(mu_);
+  for (int s : taken) meta_[s].busy = false;
 }
 
 std::string HostEngine::text(int slot) {
-  if (slot < 0 || slot >= (int)core_.size()) return std::string();
+  if (slot < 0 || slot >= (int)nslots()) return std::string();
   const SlotCore& c = core_[slot];
   return c.aborted ? std::string() : c.content;
 }
@@ -393,7 +424,7 @@ std::unordered_map<std::string, double> HostEngine::stats() {
 // --------------------------------------------------------------------------------
 // CpuEngine
 // --------------------------------------------------------------------------------
-void CpuEngine::process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results) {
+void CpuEngine::process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results, int /*lane*/) {
   for (auto& w : work) {
     SlotCore& c = core_[w.slot];
     bool was_closed = c.done || c.aborted;
@@ -404,7 +435,7 @@ void CpuEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
   }
 }
 
-void CpuEngine::finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out) {
+void CpuEngine::finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out, int /*lane*/) {
   for (auto& r : reqs) {
     std::vector<std::string> texts;
     for (int s : r.slots) texts.push_back(text(s));

@@ -11,6 +11,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -94,7 +95,15 @@ class HostEngine {
   int submit_finalize(const std::vector<int>& slots, bool strip, bool texts, const std::string& joiner,
                       int64_t created);
   bool has_work();
-  void tick(int64_t created, std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres);
+  // One tick over every dirty slot that is not in flight on another lane.  `lane` picks the
+  // engine's per-thread launch resources (HipEngine: stream + arenas), so several tick
+  // threads can have kernels in flight at once over disjoint slot sets.  With `taken`, the
+  // slots stay busy (excluded from other lanes' ticks) until settle(*taken) — the caller
+  // routes the results first, so a stream's outputs are delivered in order.  Returns false
+  // when there was nothing to do.
+  bool tick(int64_t created, std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres, int lane = 0,
+            std::vector<int>* taken = nullptr);
+  void settle(const std::vector<int>& taken);
   virtual std::string text(int slot);
   virtual std::unordered_map<std::string, double> stats();
 
@@ -108,8 +117,8 @@ class HostEngine {
     bool fresh;
   };
   // engine-specific batch processing
-  virtual void process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results) = 0;
-  virtual void finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out) = 0;
+  virtual void process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results, int lane) = 0;
+  virtual void finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out, int lane) = 0;
   virtual void on_free(int /*slot*/) {}
 
   struct Meta {
@@ -118,13 +127,20 @@ class HostEngine {
     bool eof = false;
     bool fresh = true;
     bool closed = false;  // DONE/ABORTED reported
+    bool busy = false;    // taken by an unsettled tick (in flight on some lane)
     std::string incoming;
   };
 
   TagSet ts_;
   std::mutex mu_;
-  std::vector<Meta> meta_;
-  std::vector<SlotCore> core_;  // host state (CPU engine; HIP engine: flags + fallback)
+  // deques: open() appends under mu_ while tick lanes hold references to other slots'
+  // entries outside the lock (a vector would reallocate under them)
+  std::deque<Meta> meta_;
+  std::deque<SlotCore> core_;  // host state (CPU engine; HIP engine: flags + fallback)
+  size_t nslots() {
+    std::lock_guard<std::mutex> g(mu_);
+    return core_.size();
+  }
   std::vector<int> free_, pending_free_;
   std::vector<int> dirty_;
   std::vector<FinalizeReq> fin_;
@@ -137,8 +153,8 @@ class CpuEngine : public HostEngine {
   explicit CpuEngine(const std::vector<std::string>& tags) : HostEngine(tags) {}
 
  protected:
-  void process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results) override;
-  void finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out) override;
+  void process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results, int lane) override;
+  void finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out, int lane) override;
 };
 
 // Shared by both engines' host-side finalisation.

@@ -10,6 +10,10 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <memory>
+#include <mutex>
+
 #include "qmx_engine.h"
 
 namespace qmx {
@@ -61,42 +65,62 @@ struct FinResult {
   uint32_t text_len[8];              // texts-kind: per-text stripped lengths
 };
 
+// Launch resources of one tick lane: a tick thread owns a lane (HIP stream, events,
+// host-mapped in/out arenas, work/result descriptors, counters), so several lanes can have
+// tick kernels in flight at once over disjoint slot sets (HostEngine busy flags).
+struct TickLane {
+  std::mutex mu;  // held by the lane's tick for its whole process(); kernel_stats() reads under it
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, evb = nullptr;
+  KParams params;
+  uint8_t* h_in = nullptr;
+  size_t in_cap = 0;
+  uint8_t* h_out = nullptr;
+  size_t out_cap = 0;
+  WorkItem* h_items = nullptr;
+  WorkResult* h_res = nullptr;
+  size_t items_cap = 0;
+  unsigned long long* h_dbg = nullptr;
+  size_t dbg_cap = 0;
+  // counters (summed over lanes by kernel_stats)
+  uint64_t launches = 0, items = 0, h2d_bytes = 0, d2h_bytes = 0;
+  uint64_t s3_full = 0, s3_tpl = 0, s3_events = 0, stage_n = 0;  // QMX_STAGE_TIMING: S3 path counters
+  double kernel_ms = 0.0, host_prep_us = 0, gpu_wait_us = 0, process_us = 0;  // host-side tick breakdown
+  double stage_us[16] = {0};
+  double clk_cycles = 0, clk_us = 0;
+};
+
 class HipEngine : public HostEngine {
  public:
-  HipEngine(const std::vector<std::string>& tags, int device, int tile_bytes, int max_slots, int content_cap);
+  HipEngine(const std::vector<std::string>& tags, int device, int tile_bytes, int max_slots, int content_cap,
+            int lanes = 1);
   ~HipEngine() override;
   std::string text(int slot) override;
   std::unordered_map<std::string, double> kernel_stats();
+  int lanes() const { return (int)lanes_.size(); }
 
  protected:
-  void process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results) override;
-  void finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out) override;
+  void process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results, int lane) override;
+  void finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out, int lane) override;
   void on_free(int slot) override;
 
  private:
   void escalate(int slot, bool fresh);
   void finalize_host(const FinalizeReq& r, std::vector<FinalizeRes>& out);
-  void wait_stream();
-  void ensure_in(size_t bytes);
-  void ensure_out(size_t bytes);
-  void build_params(int64_t created);
+  void wait_stream(TickLane& L);
+  void ensure_in(TickLane& L, size_t bytes);
+  void ensure_out(TickLane& L, size_t bytes);
+  void build_params(TickLane& L, int64_t created);
   std::string device_content(int slot, uint32_t len);
 
   int device_;
   int tile_;
   int max_slots_;
   uint32_t content_cap_;
-  hipStream_t stream_ = nullptr;
-  KParams params_;
-  // host-mapped arenas
-  uint8_t* h_in_ = nullptr;
-  size_t in_cap_ = 0;
-  uint8_t* h_out_ = nullptr;
-  size_t out_cap_ = 0;
-  WorkItem* h_items_ = nullptr;
-  WorkResult* h_res_ = nullptr;
-  size_t items_cap_ = 0;
-  // finalize arenas
+  KParams base_params_;  // tag patterns (each lane's copy also gets the tick's envelopes)
+  std::vector<std::unique_ptr<TickLane>> lanes_;
+  // finalize arenas: one finalize at a time (fin_mu_), on the calling lane's stream
+  std::mutex fin_mu_;
   FinItem* h_fin_ = nullptr;
   size_t fin_cap_ = 0;
   FinResult* h_finres_ = nullptr;
@@ -114,22 +138,14 @@ class HipEngine : public HostEngine {
   // device-resident
   DevSlot* d_state_ = nullptr;
   uint8_t* d_content_ = nullptr;
-  // host mirrors
+  // host mirrors (per slot; a slot is only touched by the lane it is busy on)
   std::vector<uint8_t> host_mode_;       // slot escalated to the host path
   std::vector<uint32_t> content_len_;    // device content bytes per slot
   // stats
-  uint64_t launches_ = 0, items_ = 0, escalations_ = 0, fin_launches_ = 0, fin_items_ = 0, fin_host_ = 0;
-  double kernel_ms_ = 0.0, fin_ms_ = 0.0;
-  uint64_t h2d_bytes_ = 0, d2h_bytes_ = 0;
-  uint64_t s3_full_ = 0, s3_tpl_ = 0, s3_events_ = 0;  // QMX_STAGE_TIMING: S3 path counters
-  double host_prep_us_ = 0, gpu_wait_us_ = 0, process_us_ = 0;  // host-side tick breakdown
-  int spin_us_ = 0;  // QMX_WAIT_SPIN_US: yield-poll before the blocking wait  // zero-copy arena traffic (device reads / host reads)
-  unsigned long long* h_dbg_ = nullptr;
-  size_t dbg_cap_ = 0;
-  double stage_us_[16] = {0};
-  uint64_t stage_n_ = 0;
-  double clk_cycles_ = 0, clk_us_ = 0;
-  hipEvent_t ev0_ = nullptr, ev1_ = nullptr, evb_ = nullptr;
+  std::atomic<uint64_t> escalations_{0}, fin_host_{0};
+  uint64_t fin_launches_ = 0, fin_items_ = 0;  // under fin_mu_
+  double fin_ms_ = 0.0;
+  int spin_us_ = 0;  // QMX_WAIT_SPIN_US: yield-poll before the blocking wait
 };
 
 }  // namespace qmx

@@ -1212,48 +1212,39 @@ static void put(char* dst, int cap, int* len, const std::string& s) {
   *len = (int)s.size();
 }
 
-// Wait for this engine's stream without pinning a core: the io loops share the CPU with
-// the tick threads.  A blocking-sync event sleeps on the completion interrupt: measured on
-// MI355X (tools/probes/launch_bench.hip) launch+wait = 11 us, vs 18 us spinning
+// Wait for a lane's stream without pinning a core: the io loops share the CPU with the tick
+// threads.  A blocking-sync event sleeps on the completion interrupt: measured on MI355X
+// (tools/probes/launch_bench.hip) launch+wait = 11 us, vs 18 us spinning
 // hipStreamSynchronize (one core burnt per engine) and 77 us polling with sleep_for.
-void HipEngine::wait_stream() {
-  HIP_CHECK(hipEventRecord(evb_, stream_));
+void HipEngine::wait_stream(TickLane& L) {
+  HIP_CHECK(hipEventRecord(L.evb, L.stream));
   if (spin_us_ > 0) {  // optional: yield-poll for the expected kernel time before sleeping
     const auto t0 = std::chrono::steady_clock::now();
-    while (hipEventQuery(evb_) == hipErrorNotReady) {
+    while (hipEventQuery(L.evb) == hipErrorNotReady) {
       if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_)) break;
       sched_yield();
     }
   }
-  HIP_CHECK(hipEventSynchronize(evb_));
+  HIP_CHECK(hipEventSynchronize(L.evb));
 }
 
 HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_bytes, int max_slots,
-                     int content_cap)
+                     int content_cap, int lanes)
     : HostEngine(tags),
       device_(device),
       tile_(std::min(std::max(tile_bytes, 1024), TILE_MAX) & ~15),
       max_slots_(max_slots),
       content_cap_((uint32_t)content_cap) {
   HIP_CHECK(hipSetDevice(device_));
-  HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-  HIP_CHECK(hipEventCreate(&ev0_));
-  HIP_CHECK(hipEventCreate(&ev1_));
-  HIP_CHECK(hipEventCreateWithFlags(&evb_, hipEventBlockingSync | hipEventDisableTiming));
   if (const char* sp = getenv("QMX_WAIT_SPIN_US")) spin_us_ = atoi(sp);
   HIP_CHECK(hipMalloc(&d_state_, sizeof(DevSlot) * (size_t)max_slots_));
   HIP_CHECK(hipMemset(d_state_, 0, sizeof(DevSlot) * (size_t)max_slots_));
   HIP_CHECK(hipMalloc(&d_content_, (size_t)content_cap_ * (size_t)max_slots_));
 
-  ensure_in(8u << 20);
-  ensure_out(32u << 20);
-  items_cap_ = 4096;
-  HIP_CHECK(hipHostMalloc((void**)&h_items_, sizeof(WorkItem) * items_cap_, hipHostMallocMapped));
-  HIP_CHECK(hipHostMalloc((void**)&h_res_, sizeof(WorkResult) * items_cap_, hipHostMallocMapped));
-  std::memset(&params_, 0, sizeof(params_));
-  params_.ts = ts_;
-  params_.npat = 2 * ts_.n;
-  for (int p = 0; p < params_.npat; ++p) {
+  std::memset(&base_params_, 0, sizeof(base_params_));
+  base_params_.ts = ts_;
+  base_params_.npat = 2 * ts_.n;
+  for (int p = 0; p < base_params_.npat; ++p) {
     int E = 0;
     for (int j = 0; j < pattern_len(ts_, p); ++j) {
       uint8_t b = pattern_byte(ts_, p, j);
@@ -1261,24 +1252,42 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
               : b == '<' ? 37 : b == '/' ? 38 : b == '>' ? 39 : b == '_' ? 40 : b == '-' ? 41 : b == ':' ? 42 : 63;
       E += (q & 7) * (q & 7) + (q >> 3) * (q >> 3);
     }
-    params_.pat_E[p] = E;
+    base_params_.pat_E[p] = E;
   }
-  params_.content_cap = content_cap_;
-
+  base_params_.content_cap = content_cap_;
+  for (int i = 0; i < std::max(1, lanes); ++i) {
+    std::unique_ptr<TickLane> L(new TickLane());
+    HIP_CHECK(hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreate(&L->ev0));
+    HIP_CHECK(hipEventCreate(&L->ev1));
+    HIP_CHECK(hipEventCreateWithFlags(&L->evb, hipEventBlockingSync | hipEventDisableTiming));
+    L->params = base_params_;
+    ensure_in(*L, 8u << 20);
+    ensure_out(*L, 32u << 20);
+    L->items_cap = 4096;
+    HIP_CHECK(hipHostMalloc((void**)&L->h_items, sizeof(WorkItem) * L->items_cap, hipHostMallocMapped));
+    HIP_CHECK(hipHostMalloc((void**)&L->h_res, sizeof(WorkResult) * L->items_cap, hipHostMallocMapped));
+    lanes_.push_back(std::move(L));
+  }
   host_mode_.assign(max_slots_, 0);
   content_len_.assign(max_slots_, 0);
 }
 
 HipEngine::~HipEngine() {
-  if (stream_) hipStreamSynchronize(stream_);
-  if (h_in_) hipHostFree(h_in_);
-  if (h_out_) hipHostFree(h_out_);
-  if (h_items_) hipHostFree(h_items_);
-  if (h_res_) hipHostFree(h_res_);
-  if (h_dbg_) hipHostFree(h_dbg_);
+  for (auto& L : lanes_) {
+    if (L->stream) hipStreamSynchronize(L->stream);
+    if (L->h_in) hipHostFree(L->h_in);
+    if (L->h_out) hipHostFree(L->h_out);
+    if (L->h_items) hipHostFree(L->h_items);
+    if (L->h_res) hipHostFree(L->h_res);
+    if (L->h_dbg) hipHostFree(L->h_dbg);
+    if (L->ev0) hipEventDestroy(L->ev0);
+    if (L->ev1) hipEventDestroy(L->ev1);
+    if (L->evb) hipEventDestroy(L->evb);
+    if (L->stream) hipStreamDestroy(L->stream);
+  }
   if (d_state_) hipFree(d_state_);
   if (d_content_) hipFree(d_content_);
-
   if (h_fin_) hipHostFree(h_fin_);
   if (h_finres_) hipHostFree(h_finres_);
   if (h_fint_) hipHostFree(h_fint_);
@@ -1286,31 +1295,28 @@ HipEngine::~HipEngine() {
   if (h_fout_) hipHostFree(h_fout_);
   if (d_join_) hipFree(d_join_);
   if (d_fout_) hipFree(d_fout_);
-  if (ev0_) hipEventDestroy(ev0_);
-  if (ev1_) hipEventDestroy(ev1_);
-  if (evb_) hipEventDestroy(evb_);
-  if (stream_) hipStreamDestroy(stream_);
 }
 
-void HipEngine::ensure_in(size_t bytes) {
-  if (bytes <= in_cap_) return;
-  if (h_in_) HIP_CHECK(hipHostFree(h_in_));
-  in_cap_ = std::max(bytes, in_cap_ * 2);
-  HIP_CHECK(hipHostMalloc((void**)&h_in_, in_cap_ + 64, hipHostMallocMapped));
+void HipEngine::ensure_in(TickLane& L, size_t bytes) {
+  if (bytes <= L.in_cap) return;
+  if (L.h_in) HIP_CHECK(hipHostFree(L.h_in));
+  L.in_cap = std::max(bytes, L.in_cap * 2);
+  HIP_CHECK(hipHostMalloc((void**)&L.h_in, L.in_cap + 64, hipHostMallocMapped));
 }
-void HipEngine::ensure_out(size_t bytes) {
-  if (bytes <= out_cap_) return;
-  if (h_out_) HIP_CHECK(hipHostFree(h_out_));
-  out_cap_ = std::max(bytes, out_cap_ * 2);
-  HIP_CHECK(hipHostMalloc((void**)&h_out_, out_cap_ + 64, hipHostMallocMapped));
+void HipEngine::ensure_out(TickLane& L, size_t bytes) {
+  if (bytes <= L.out_cap) return;
+  if (L.h_out) HIP_CHECK(hipHostFree(L.h_out));
+  L.out_cap = std::max(bytes, L.out_cap * 2);
+  HIP_CHECK(hipHostMalloc((void**)&L.h_out, L.out_cap + 64, hipHostMallocMapped));
 }
 
-void HipEngine::build_params(int64_t created) {
-  put(params_.pre1, sizeof(params_.pre1), &params_.pre1_len, "data: {\"id\": \"chatcmpl-parallel-");
-  put(params_.pre2, sizeof(params_.pre2), &params_.pre2_len,
+void HipEngine::build_params(TickLane& L, int64_t created) {
+  KParams& P = L.params;
+  put(P.pre1, sizeof(P.pre1), &P.pre1_len, "data: {\"id\": \"chatcmpl-parallel-");
+  put(P.pre2, sizeof(P.pre2), &P.pre2_len,
       "\", \"object\": \"chat.completion.chunk\", \"created\": " + std::to_string(created) +
           ", \"model\": \"parallel-proxy\", \"choices\": [{\"index\": 0, \"delta\": {\"content\": \"");
-  put(params_.suf, sizeof(params_.suf), &params_.suf_len, kDeltaSuffix);
+  put(P.suf, sizeof(P.suf), &P.suf_len, kDeltaSuffix);
 }
 
 void HipEngine::on_free(int slot) {
@@ -1345,14 +1351,16 @@ void HipEngine::escalate(int slot, bool fresh) {
 }
 
 std::string HipEngine::text(int slot) {
-  if (slot < 0 || slot >= (int)core_.size()) return std::string();
+  if (slot < 0 || slot >= (int)nslots()) return std::string();
   const SlotCore& c = core_[slot];
   if (c.aborted) return std::string();
   if (slot >= max_slots_ || host_mode_[slot]) return c.content;
   return device_content(slot, content_len_[slot]);
 }
 
-void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results) {
+void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results, int lane) {
+  TickLane& L = *lanes_[(size_t)lane % lanes_.size()];
+  std::lock_guard<std::mutex> lg(L.mu);  // a lane is driven by one thread; kernel_stats() reads under it
   using HC = std::chrono::steady_clock;
   const auto tp0 = HC::now();
   struct Pending {
@@ -1372,14 +1380,14 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
     in_need += (sub + 15) & ~(size_t)15;
     out_need += ((12 * sub + 1024) + 15) & ~(size_t)15;
   }
-  ensure_in(in_need + 64);
-  ensure_out(out_need + 64);
-  if (work.size() > items_cap_) {
-    hipHostFree(h_items_);
-    hipHostFree(h_res_);
-    items_cap_ = work.size() * 2;
-    HIP_CHECK(hipHostMalloc((void**)&h_items_, sizeof(WorkItem) * items_cap_, hipHostMallocMapped));
-    HIP_CHECK(hipHostMalloc((void**)&h_res_, sizeof(WorkResult) * items_cap_, hipHostMallocMapped));
+  ensure_in(L, in_need + 64);
+  ensure_out(L, out_need + 64);
+  if (work.size() > L.items_cap) {
+    hipHostFree(L.h_items);
+    hipHostFree(L.h_res);
+    L.items_cap = work.size() * 2;
+    HIP_CHECK(hipHostMalloc((void**)&L.h_items, sizeof(WorkItem) * L.items_cap, hipHostMallocMapped));
+    HIP_CHECK(hipHostMalloc((void**)&L.h_res, sizeof(WorkResult) * L.items_cap, hipHostMallocMapped));
   }
   size_t in_off = 0, out_off = 0;
   int n = 0;
@@ -1424,9 +1432,9 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
     bool eof_sent = w.eof && sub == tot;
     // copy carry + data prefix into the arena
     size_t a = std::min(cl, sub);
-    std::memcpy(h_in_ + in_off, c.carry.data(), a);
-    if (sub > a) std::memcpy(h_in_ + in_off + a, w.data.data(), sub - a);
-    WorkItem& it = h_items_[n];
+    std::memcpy(L.h_in + in_off, c.carry.data(), a);
+    if (sub > a) std::memcpy(L.h_in + in_off + a, w.data.data(), sub - a);
+    WorkItem& it = L.h_items[n];
     it.slot = (uint32_t)slot;
     it.in_off = (uint32_t)in_off;
     it.in_len = (uint32_t)sub;
@@ -1442,60 +1450,60 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
     ++n;
   }
   if (n > 0) {
-    build_params(created);
-    params_.dbg = nullptr;
+    build_params(L, created);
+    L.params.dbg = nullptr;
     if (getenv("QMX_STAGE_TIMING")) {
-      if (dbg_cap_ < (size_t)n) {
-        if (h_dbg_) hipHostFree(h_dbg_);
-        dbg_cap_ = std::max((size_t)n, items_cap_);
-        HIP_CHECK(hipHostMalloc((void**)&h_dbg_, sizeof(unsigned long long) * 16 * dbg_cap_, hipHostMallocMapped));
+      if (L.dbg_cap < (size_t)n) {
+        if (L.h_dbg) hipHostFree(L.h_dbg);
+        L.dbg_cap = std::max((size_t)n, L.items_cap);
+        HIP_CHECK(hipHostMalloc((void**)&L.h_dbg, sizeof(unsigned long long) * 16 * L.dbg_cap, hipHostMallocMapped));
       }
-      std::memset(h_dbg_, 0, sizeof(unsigned long long) * 16 * n);
-      params_.dbg = h_dbg_;
+      std::memset(L.h_dbg, 0, sizeof(unsigned long long) * 16 * n);
+      L.params.dbg = L.h_dbg;
     }
     const auto tp1 = HC::now();
-    host_prep_us_ += std::chrono::duration<double, std::micro>(tp1 - tp0).count();
+    L.host_prep_us += std::chrono::duration<double, std::micro>(tp1 - tp0).count();
     roctxRangePushA("qmx_tick");  // rocprofv3 --marker-trace: one range per tick launch + wait
-    h2d_bytes_ += in_off;
-    HIP_CHECK(hipEventRecord(ev0_, stream_));
-    hipLaunchKernelGGL(qmx_tick_kernel, dim3(n), dim3(BS), 0, stream_, h_items_, h_in_, h_out_, h_res_, d_state_,
-                       d_content_, params_);
+    L.h2d_bytes += in_off;
+    HIP_CHECK(hipEventRecord(L.ev0, L.stream));
+    hipLaunchKernelGGL(qmx_tick_kernel, dim3(n), dim3(BS), 0, L.stream, L.h_items, L.h_in, L.h_out, L.h_res, d_state_,
+                       d_content_, L.params);
     HIP_CHECK(hipGetLastError());
-    HIP_CHECK(hipEventRecord(ev1_, stream_));
-    wait_stream();
+    HIP_CHECK(hipEventRecord(L.ev1, L.stream));
+    wait_stream(L);
     roctxRangePop();
-    gpu_wait_us_ += std::chrono::duration<double, std::micro>(HC::now() - tp1).count();
+    L.gpu_wait_us += std::chrono::duration<double, std::micro>(HC::now() - tp1).count();
     float ms = 0.f;
-    hipEventElapsedTime(&ms, ev0_, ev1_);
-    kernel_ms_ += ms;
-    ++launches_;
-    items_ += n;
-    if (params_.dbg) {
+    hipEventElapsedTime(&ms, L.ev0, L.ev1);
+    L.kernel_ms += ms;
+    ++L.launches;
+    L.items += n;
+    if (L.params.dbg) {
       for (int i = 0; i < n; ++i) {
-        const unsigned long long* d = h_dbg_ + 16 * i;
+        const unsigned long long* d = L.h_dbg + 16 * i;
         if (d[12] > d[11] && d[10] > d[0]) {
-          clk_cycles_ += (double)(d[12] - d[11]);
-          clk_us_ += (double)(d[10] - d[0]) * 0.01;
+          L.clk_cycles += (double)(d[12] - d[11]);
+          L.clk_us += (double)(d[10] - d[0]) * 0.01;
         }
         int prev = 0;
         for (int k = 1; k < 11; ++k) {
           if (!d[k]) continue;
-          stage_us_[k] += (double)(d[k] - d[prev]) * 0.01;  // 100 MHz ticks -> us
+          L.stage_us[k] += (double)(d[k] - d[prev]) * 0.01;  // 100 MHz ticks -> us
           prev = k;
         }
       }
-      stage_n_ += n;
+      L.stage_n += n;
       for (int i = 0; i < n; ++i) {
-        s3_full_ += h_dbg_[16 * i + 13];
-        s3_tpl_ += h_dbg_[16 * i + 14];
-        s3_events_ += h_dbg_[16 * i + 15];
+        L.s3_full += L.h_dbg[16 * i + 13];
+        L.s3_tpl += L.h_dbg[16 * i + 14];
+        L.s3_events += L.h_dbg[16 * i + 15];
       }
     }
   }
   for (int i = 0; i < n; ++i) {
     Pending& p = pend[i];
     SlotCore& c = core_[p.slot];
-    const WorkResult r = h_res_[i];
+    const WorkResult r = L.h_res[i];
     Work& w = *p.w;
     // rebuild the unconsumed remainder: (carry + data)[consumed:]
     auto remainder = [&](size_t consumed) {
@@ -1540,8 +1548,8 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
       }
     }
     std::string sse;
-    d2h_bytes_ += r.out_len;
-    if (r.out_len) sse.assign((const char*)h_out_ + h_items_[i].out_off, r.out_len);
+    L.d2h_bytes += r.out_len;
+    if (r.out_len) sse.assign((const char*)L.h_out + L.h_items[i].out_off, r.out_len);
     if (!sse.empty() || flags) results.push_back({p.slot, std::move(sse), flags});
   }
   if (!requeue.empty()) {
@@ -1553,7 +1561,7 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
       dirty_.push_back(s);
     }
   }
-  process_us_ += std::chrono::duration<double, std::micro>(HC::now() - tp0).count();
+  L.process_us += std::chrono::duration<double, std::micro>(HC::now() - tp0).count();
 }
 
 void HipEngine::finalize_host(const FinalizeReq& r, std::vector<FinalizeRes>& out) {
@@ -1579,14 +1587,17 @@ static void grow_device(uint8_t** p, size_t* cap, size_t need) {
   HIP_CHECK(hipMalloc((void**)p, *cap + 64));
 }
 
-void HipEngine::finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out) {
+void HipEngine::finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out, int lane) {
+  std::lock_guard<std::mutex> fg(fin_mu_);  // finalize arenas are shared by the lanes
+  TickLane& L = *lanes_[(size_t)lane % lanes_.size()];
+  const int nsl = (int)nslots();
   // Sessions whose texts are all HBM-resident run on the GPU (K3+K4+K5); a session with an
   // escalated (host-path) stream, or > 8 texts in texts-kind, is finalized on the host.
   std::vector<const FinalizeReq*> gpu;
   size_t ntext = 0, in_bytes = 0;
   for (auto& r : reqs) {
     bool dev = !(r.texts && r.slots.size() > 8);
-    for (int s : r.slots) dev = dev && s >= 0 && s < max_slots_ && s < (int)core_.size() && !host_mode_[s];
+    for (int s : r.slots) dev = dev && s >= 0 && s < max_slots_ && s < nsl && !host_mode_[s];
     if (!dev) {
       finalize_host(r, out);
       continue;
@@ -1642,15 +1653,15 @@ void HipEngine::finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes
   grow_device(&d_fout_, &dfout_cap_, out_off + 16);
   grow_mapped(&h_fout_, &fout_cap_, out_off + 16);
   roctxRangePushA("qmx_finalize");
-  HIP_CHECK(hipEventRecord(ev0_, stream_));
-  hipLaunchKernelGGL(qmx_finalize_kernel, dim3(n), dim3(BS), 0, stream_, h_fin_, h_fint_, h_fin_in_, d_content_,
+  HIP_CHECK(hipEventRecord(L.ev0, L.stream));
+  hipLaunchKernelGGL(qmx_finalize_kernel, dim3(n), dim3(BS), 0, L.stream, h_fin_, h_fint_, h_fin_in_, d_content_,
                      content_cap_, d_join_, d_fout_, h_fout_, h_finres_, ts_);
   HIP_CHECK(hipGetLastError());
-  HIP_CHECK(hipEventRecord(ev1_, stream_));
-  wait_stream();
+  HIP_CHECK(hipEventRecord(L.ev1, L.stream));
+  wait_stream(L);
   roctxRangePop();
   float ms = 0.f;
-  hipEventElapsedTime(&ms, ev0_, ev1_);
+  hipEventElapsedTime(&ms, L.ev0, L.ev1);
   fin_ms_ += ms;
   ++fin_launches_;
   fin_items_ += n;
@@ -1682,18 +1693,36 @@ void HipEngine::finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes
 }
 
 std::unordered_map<std::string, double> HipEngine::kernel_stats() {
-  std::unordered_map<std::string, double> m{{"launches", (double)launches_}, {"items", (double)items_},
-                                             {"kernel_ms", kernel_ms_}, {"escalations", (double)escalations_},
-                                             {"fin_launches", (double)fin_launches_}, {"stage_items", (double)stage_n_},
-                                             {"fin_items", (double)fin_items_}, {"fin_host", (double)fin_host_},
-                                             {"fin_ms", fin_ms_}, {"h2d_bytes", (double)h2d_bytes_},
-                                             {"d2h_bytes", (double)d2h_bytes_},
-                                             {"s3_full_parses", (double)s3_full_}, {"s3_template_hits", (double)s3_tpl_},
-                                             {"s3_events", (double)s3_events_},
-                                             {"host_prep_us", host_prep_us_}, {"gpu_wait_us", gpu_wait_us_},
-                                             {"process_us", process_us_}};
-  for (int k = 1; k < 11; ++k) m["stage" + std::to_string(k) + "_us"] = stage_us_[k];
-  m["shader_mhz"] = clk_us_ > 0 ? clk_cycles_ / clk_us_ : 0.0;
+  std::unordered_map<std::string, double> m;
+  double stage[16] = {0}, cyc = 0, cus = 0;
+  for (auto& Lp : lanes_) {
+    TickLane& L = *Lp;
+    std::lock_guard<std::mutex> lg(L.mu);
+    m["launches"] += (double)L.launches;
+    m["items"] += (double)L.items;
+    m["kernel_ms"] += L.kernel_ms;
+    m["stage_items"] += (double)L.stage_n;
+    m["h2d_bytes"] += (double)L.h2d_bytes;
+    m["d2h_bytes"] += (double)L.d2h_bytes;
+    m["s3_full_parses"] += (double)L.s3_full;
+    m["s3_template_hits"] += (double)L.s3_tpl;
+    m["s3_events"] += (double)L.s3_events;
+    m["host_prep_us"] += L.host_prep_us;
+    m["gpu_wait_us"] += L.gpu_wait_us;
+    m["process_us"] += L.process_us;
+    for (int k = 1; k < 11; ++k) stage[k] += L.stage_us[k];
+    cyc += L.clk_cycles;
+    cus += L.clk_us;
+  }
+  for (int k = 1; k < 11; ++k) m["stage" + std::to_string(k) + "_us"] = stage[k];
+  m["shader_mhz"] = cus > 0 ? cyc / cus : 0.0;
+  m["escalations"] = (double)escalations_.load();
+  m["fin_host"] = (double)fin_host_.load();
+  m["lanes"] = (double)lanes_.size();
+  std::lock_guard<std::mutex> fg(fin_mu_);
+  m["fin_launches"] = (double)fin_launches_;
+  m["fin_items"] = (double)fin_items_;
+  m["fin_ms"] = fin_ms_;
   return m;
 }
 

@@ -463,27 +463,38 @@ class Verifier {
 };
 
 // --------------------------------------------------------------------------------------
-// GPU hub: ONE HIP engine per process shared by every io loop.  A single tick thread batches
-// the pending bytes of all loops' streams into one launch of the fused tick kernel (the
-// SURVEY's "pack pending upstream bytes of ALL active streams on this rank"), then routes
-// each stream's results back to the loop that owns it (per-loop queue + eventfd).
+// GPU hub: ONE HIP engine per process shared by every io loop (the SURVEY's "pack pending
+// upstream bytes of ALL active streams on this rank").  `tick_lanes` tick threads each own
+// a lane of the engine (HIP stream + host-mapped arenas): a lane takes every dirty stream
+// that is not in flight on another lane, launches the fused tick kernel, waits, routes each
+// stream's results to the loop that owns it (per-loop queue + eventfd) and only then
+// settles its streams — so a stream's outputs stay in order while a second lane already
+// has the next kernel in flight for the bytes that arrived meanwhile (the tick kernel is
+// latency-bound: two launches in flight cost the GPU nothing and halve the tick period).
 // --------------------------------------------------------------------------------------
 class GpuHub {
  public:
   using Sink = std::function<void(ResultBatch&&)>;
   GpuHub(const ServerCfg& cfg, int nloops) : cfg_(cfg), sinks_(nloops) {
+    lanes_ = std::max(1, std::min(cfg.tick_lanes, 8));
     if (cfg.engine == "hip")
-      eng_.reset(new HipEngine(cfg.tags, cfg.device, cfg.tile, cfg.max_slots, cfg.content_cap));
+      eng_.reset(new HipEngine(cfg.tags, cfg.device, cfg.tile, cfg.max_slots, cfg.content_cap, lanes_));
     else
       eng_.reset(new CpuEngine(cfg.tags));  // shared CPU engine: exercises the hub routing on CPU
     if (cfg.verify) ver_.reset(new Verifier(cfg.tags));
   }
   ~GpuHub() {
-    stop_ = true;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
     cv_.notify_all();
-    if (th_.joinable()) th_.join();
+    for (auto& t : th_)
+      if (t.joinable()) t.join();
   }
-  void start() { th_ = std::thread([this] { run(); }); }
+  void start() {
+    for (int i = 0; i < lanes_; ++i) th_.emplace_back([this, i] { run(i); });
+  }
   void attach(int loop, Sink s) { sinks_[loop] = std::move(s); }
   int open(int loop, int index, bool f, bool e) {
     int slot = eng_->open(index, f, e);
@@ -509,7 +520,7 @@ class GpuHub {
   }
   int submit(int loop, const std::vector<int>& slots, bool strip, bool texts, const std::string& joiner,
              int64_t created) {
-    std::lock_guard<std::mutex> g(omu_);  // the id must be routable before the tick thread sees it
+    std::lock_guard<std::mutex> g(omu_);  // the id must be routable before a tick lane sees it
     int id = eng_->submit_finalize(slots, strip, texts, joiner, created);
     fin_owner_[id] = loop;
     if (ver_) ver_->submit(id, slots, strip, texts, joiner, created);
@@ -520,7 +531,7 @@ class GpuHub {
       std::lock_guard<std::mutex> g(mu_);
       work_ = true;
     }
-    cv_.notify_one();
+    cv_.notify_one();  // an idle lane, if any: a busy lane re-checks for work when it settles
   }
   std::unordered_map<std::string, double> snapshot() {
     std::lock_guard<std::mutex> g(smu_);
@@ -528,22 +539,23 @@ class GpuHub {
   }
 
  private:
-  void run() {
+  void run(int lane) {
     if (cfg_.engine == "hip") hipSetDevice(cfg_.device);
-    double last_snap = 0;
     std::vector<ResultBatch> per(sinks_.size());
-    while (!stop_) {
+    std::vector<int> taken;
+    while (true) {
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait_for(lk, std::chrono::milliseconds(2), [this] { return work_ || stop_; });
+        if (stop_) break;
         work_ = false;
       }
-      if (stop_) break;
-      while (eng_->has_work()) {
+      while (true) {
         ResultBatch rb;
+        taken.clear();
         const double tt = now_s();
         const int64_t created = (int64_t)time(nullptr);
-        eng_->tick(created, rb.r, rb.f);
+        if (!eng_->tick(created, rb.r, rb.f, lane, &taken)) break;  // nothing this lane may take
         h_tick.observe(now_s() - tt);
         if (ver_) ver_->check(created, rb.r, rb.f);
         c_ticks++;
@@ -566,30 +578,34 @@ class GpuHub {
           if (sinks_[l]) sinks_[l](std::move(per[l]));
           per[l] = ResultBatch();
         }
-        if (tt - last_snap > 0.05) {
+        eng_->settle(taken);  // after routing: a stream's next results cannot overtake these
+        if (tt - last_snap_.load() > 0.05) {
+          last_snap_.store(tt);
           std::unordered_map<std::string, double> m;
           for (auto& kv : eng_->stats()) m["qmx_engine_" + kv.first] = kv.second;
           if (auto* h = dynamic_cast<HipEngine*>(eng_.get()))
             for (auto& kv : h->kernel_stats()) m["qmx_kernel_" + kv.first] = kv.second;
           std::lock_guard<std::mutex> g(smu_);
           snap_.swap(m);
-          last_snap = tt;
         }
+        if (stop_) break;
       }
     }
   }
   const ServerCfg& cfg_;
+  int lanes_ = 1;
   std::unique_ptr<HostEngine> eng_;
   std::unique_ptr<Verifier> ver_;
   std::vector<Sink> sinks_;
   std::mutex mu_, omu_, smu_;
   std::condition_variable cv_;
   bool work_ = false;
-  std::atomic<bool> stop_{false};
+  std::atomic<bool> stop_{false};  // set under mu_ (cv predicate); lanes also poll it between ticks
+  std::atomic<double> last_snap_{0.0};
   std::vector<int> owner_;                  // slot → io loop
   std::unordered_map<int, int> fin_owner_;  // finalize id → io loop
   std::unordered_map<std::string, double> snap_;
-  std::thread th_;
+  std::vector<std::thread> th_;
 };
 
 // --------------------------------------------------------------------------------------

@@ -1,9 +1,11 @@
 // qmx_server.h — native data plane: epoll HTTP/1.1 proxy front-end + upstream client.
 //
 // One process per GPU; T io threads per process, each owning an SO_REUSEPORT listener, its
-// client/upstream connections, keep-alive upstream pools, and its own stream engine (for
-// `hip`: its own HIP stream + device-resident slot arena, driven by a companion tick
-// thread so socket I/O overlaps the fused tick kernel).  Semantics mirror the FastAPI
+// client/upstream connections and keep-alive upstream pools.  Stream processing: for `hip`
+// one shared engine per process (the GPU hub) whose tick lanes — threads, each with its own
+// HIP stream and host-mapped arenas — keep up to `tick_lanes` fused tick kernels in flight
+// over disjoint stream sets while the io loops keep reading sockets; for `cpu` one engine
+// per io loop, ticked inline.  Semantics mirror the FastAPI
 // conformance app (quorum_amd/server/app.py) and quorum's handler
 // (src/quorum/oai_proxy.py:959-1408).
 #pragma once
@@ -33,6 +35,7 @@ struct ServerCfg {
   // engine
   std::string engine = "cpu";
   int shared_engine = -1;  // one engine per process shared by all io loops (-1: auto = hip only)
+  int tick_lanes = 2;      // shared engine: tick threads, each with its own HIP stream + arenas
   int device = 0;
   int tile = 16384, max_slots = 4096, content_cap = 1 << 20;
   // config

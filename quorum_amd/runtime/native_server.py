@@ -66,6 +66,7 @@ def native_config(cfg: Dict[str, Any], host: str, port: int, engine: str, device
         "backends": backends,
         "drain_s": float(rt.drain_timeout), "verify": bool(rt.verify),
         "shared_engine": -1 if rt.shared_engine in ("auto", None) else int(bool(rt.shared_engine)),
+        "tick_lanes": int(rt.tick_lanes),
         "ca_file": _ca_bundle(), "tls_verify": os.environ.get("QMX_TLS_VERIFY", "1") not in ("0", "false"), "ready_file": (os.environ["QMX_READY_FILE"] + f".{os.getpid()}") if os.environ.get("QMX_READY_FILE") else "",
         **cluster_config(rt, port, engine),
     }

@@ -64,8 +64,11 @@ def spawn_workers(config: str, host: str, port: int, workers: int, engine: str, 
     procs = []
     e = dict(os.environ if env is None else env)
     e.setdefault("PYTHONUNBUFFERED", "1")
-    # one HIP stream per io loop: give them hardware queues of their own (HIP defaults to 4;
-    # measured on MI355X with 8 loops: 96k -> 117k req/s, p99 TTFT 0.88 -> 0.60 ms)
+    # workers run `python -m quorum_amd.serve`: the package must import from any cwd
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e["PYTHONPATH"] = os.pathsep.join([root] + [x for x in e.get("PYTHONPATH", "").split(os.pathsep) if x])
+    # per-loop engines (runtime.shared_engine: false) each own a HIP stream: give them
+    # hardware queues of their own (HIP defaults to 4)
     e.setdefault("GPU_MAX_HW_QUEUES", str(min(16, max(4, threads))))
     for _ in range(workers if impl == "python" else 1):
         if impl == "native":

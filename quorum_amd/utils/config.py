@@ -216,6 +216,8 @@ class RuntimeConfig:
     verify:    debug mode: a shadow CPU oracle engine checks every stream and final (QMX_VERIFY=1)
     shared_engine: "auto" (one engine per process shared by all io loops for hip, per-loop
                engines for cpu) | true | false (QMX_SHARED_ENGINE=0/1)
+    tick_lanes: shared engine: tick threads with a kernel in flight each (own HIP stream and
+               arenas, disjoint stream sets) — QMX_TICK_LANES
     """
 
     engine: str = "auto"
@@ -231,6 +233,7 @@ class RuntimeConfig:
     drain_timeout: float = 10.0
     verify: bool = False
     shared_engine: Any = "auto"
+    tick_lanes: int = 2
     log_content: bool = False
 
     @classmethod
@@ -245,5 +248,7 @@ class RuntimeConfig:
             rt["verify"] = os.environ["QMX_VERIFY"] not in ("0", "", "false")
         if os.environ.get("QMX_SHARED_ENGINE"):
             rt["shared_engine"] = os.environ["QMX_SHARED_ENGINE"] not in ("0", "false")
+        if os.environ.get("QMX_TICK_LANES"):
+            rt["tick_lanes"] = int(os.environ["QMX_TICK_LANES"])
         known = {k: v for k, v in rt.items() if k in cls.__dataclass_fields__}
         return cls(**known)

@@ -111,11 +111,12 @@ class LiveUpstream:
 
 @contextlib.contextmanager
 def native_server(cfg: Dict[str, Any], engine: str = "cpu", threads: int = 1, env_key: str = "",
-                  verify: bool = False, shared: Optional[bool] = None):
+                  verify: bool = False, shared: Optional[bool] = None, lanes: Optional[int] = None):
     """Run the C++ data plane in-process (background thread) for one config.
 
     verify: run the shadow CPU-oracle engine (server_counters()['verify_mismatches']).
-    shared: one engine per process shared by all io loops (None = the config's default)."""
+    shared: one engine per process shared by all io loops (None = the config's default).
+    lanes: tick lanes of the shared engine (None = the config's default)."""
     import http.client
     import os
 
@@ -130,6 +131,8 @@ def native_server(cfg: Dict[str, Any], engine: str = "cpu", threads: int = 1, en
     d["verify"] = verify
     if shared is not None:
         d["shared_engine"] = int(shared)
+    if lanes is not None:
+        d["tick_lanes"] = int(lanes)
     th = threading.Thread(target=ext.run_server, args=(d,), daemon=True)
     th.start()
     t0 = time.time()

@@ -8,7 +8,7 @@ import random
 import pytest
 
 from quorum_amd.ops import native, reference as ref
-from quorum_amd.ops.engine import F_ABORTED, FinalizeRequest
+from quorum_amd.ops.engine import F_ABORTED, F_DONE, FinalizeRequest
 from quorum_amd.ops.native import NativeEngine
 
 import engine_harness as H
@@ -199,3 +199,65 @@ def test_hip_engine_stats(ext):
     st = eng._e.kernel_stats()
     assert st["launches"] >= 1 and st["items"] >= 1
     eng.release(slot)
+
+
+def test_hip_two_lanes_concurrent(ext):
+    """Two tick lanes (own HIP stream + host-mapped arenas each) driven by two threads while
+    a third feeds: a stream in flight on one lane is skipped by the other until settled, so
+    every stream's SSE, flags and final content equal the CPU engine's."""
+    import threading
+    import time
+
+    rng = random.Random(4242)
+    tags = ["think", "reason"]
+    raw = [H.rand_stream(rng, abort_p=0.02) for _ in range(48)]
+    streams = [H.split_random(rng, r, rng.choice([7, 40, 300])) for r in raw]
+    n = len(streams)
+    cpu, _, _ = H.run_engine(NativeEngine("cpu", tags), streams, [True] * n, [True] * n, random.Random(1))
+    hip = _hip(tags, lanes=2)
+    slots = [hip.open(i % 7, True, True) for i in range(n)]
+    out = {s: [] for s in slots}
+    flags = {s: 0 for s in slots}
+    lock = threading.Lock()
+    fed = threading.Event()
+    lanes_seen = set()
+
+    def lane_loop(lane):
+        while True:
+            res, _fres, taken = hip._e.tick_unsettled(H.CREATED, lane)
+            with lock:
+                for slot, data, fl in res:
+                    out[slot].append(data)
+                    flags[slot] |= fl
+                if taken:
+                    lanes_seen.add(lane)
+            hip._e.settle(taken)
+            if not taken:
+                if fed.is_set() and not hip.has_work():
+                    return
+                time.sleep(0.0002)
+
+    ths = [threading.Thread(target=lane_loop, args=(i,)) for i in range(2)]
+    for t in ths:
+        t.start()
+    cur = [0] * n
+    while any(c <= len(s) for c, s in zip(cur, streams)):
+        for i, chunks in enumerate(streams):
+            if cur[i] < len(chunks):
+                hip.feed(slots[i], chunks[cur[i]])
+            elif cur[i] == len(chunks):
+                hip.finish(slots[i])
+            cur[i] += 1
+        time.sleep(0.0003)
+    fed.set()
+    for t in ths:
+        t.join(timeout=60)
+        assert not t.is_alive()
+    for i, s in enumerate(slots):
+        assert flags[s] & (F_DONE | F_ABORTED) == cpu[i][1], ("flags", i, raw[i])
+        assert b"".join(out[s]) == cpu[i][0], ("sse", i, raw[i])
+        if not flags[s] & F_ABORTED:
+            assert hip.text(s) == cpu[i][2], ("content", i)
+    st = hip._e.kernel_stats()
+    assert st["lanes"] == 2 and st["launches"] >= 2, st
+    assert lanes_seen == {0, 1}

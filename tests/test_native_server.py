@@ -332,11 +332,12 @@ def _per_stream(evs):
     return per
 
 
-@pytest.mark.parametrize("threads", [1, 4])
-def test_native_shared_engine_many_loops(threads):
+@pytest.mark.parametrize("threads,lanes", [(1, 1), (4, 1), (4, 3)])
+def test_native_shared_engine_many_loops(threads, lanes):
     """One engine per process shared by every io loop (the GPU-hub topology, here with the
-    CPU engine): concurrent sessions land on different loops, the hub's tick thread routes
-    each stream's results back to its owning loop, and the shadow oracle sees no mismatch."""
+    CPU engine): concurrent sessions land on different loops, the hub's tick lanes take
+    disjoint stream sets, route each stream's results back to its owning loop before
+    settling it, and the shadow oracle sees no mismatch."""
     import concurrent.futures as cf
 
     ext = native.require()
@@ -352,7 +353,7 @@ def test_native_shared_engine_many_loops(threads):
         with native_server(cfg) as port:
             ref = _norm_sse(httpx.post(f"http://127.0.0.1:{port}/chat/completions", json=req, headers=AUTH,
                                        timeout=30).text)
-        with native_server(cfg, threads=threads, verify=True, shared=True) as port:
+        with native_server(cfg, threads=threads, verify=True, shared=True, lanes=lanes) as port:
             def one(_):
                 with httpx.Client(base_url=f"http://127.0.0.1:{port}") as cl:
                     return [_norm_sse(cl.post("/chat/completions", json=req, headers=AUTH, timeout=30).text)
