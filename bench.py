@@ -125,6 +125,35 @@ def scrape(port):
     return out
 
 
+def cpu_seconds(pid: int) -> float:
+    """utime + stime of a live process (all its threads), from /proc."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            fields = f.read().rsplit(")", 1)[1].split()
+        return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
+    except (OSError, IndexError, ValueError):
+        return 0.0
+
+
+def cpu_snapshot(mock_procs, proxy_procs):
+    import resource
+
+    return {"proxy": sum(cpu_seconds(p.pid) for p in proxy_procs),
+            "mocks": sum(cpu_seconds(p.pid) for p in mock_procs),
+            "loadgen": resource.getrusage(resource.RUSAGE_CHILDREN).ru_utime
+            + resource.getrusage(resource.RUSAGE_CHILDREN).ru_stime}
+
+
+def cpu_breakdown(c0, c1, requests, elapsed):
+    """CPU time per 1k completed requests by component (proxy / mock backends / load
+    generator) over the timed region: the proxied-req/s metric shares the box's cores with
+    the synthetic harness, so this says where the CPU goes."""
+    d = {k: c1[k] - c0[k] for k in c0}
+    out = {f"{k}_cpu_ms_per_1k_req": round(1e6 * v / max(requests, 1), 2) for k, v in d.items()}
+    out["cores_busy"] = {k: round(v / elapsed, 2) for k, v in d.items()} if elapsed else {}
+    return out
+
+
 def breakdown(m0, m1, elapsed):
     d = {k: m1.get(k, 0.0) - m0.get(k, 0.0) for k in m1}
     launches = d.get("qmx_kernel_launches", 0.0)
@@ -212,8 +241,10 @@ def main() -> int:
             dist.broadcast_object_list(nonce, src=0)
             env.update({"QMX_XCHG_NONCE": nonce[0], "QMX_XCHG_PORT": str(args.port + 7),
                         "QMX_RANK": str(rank), "QMX_WORLD": str(world)})
-        procs += spawn_workers(cfg_path, "127.0.0.1", args.port, args.workers, engine,
+        mock_procs = list(procs)
+        proxy_procs = spawn_workers(cfg_path, "127.0.0.1", args.port, args.workers, engine,
                                local_rank if use_cuda else None, impl=args.impl, threads=args.threads, env=env)
+        procs += proxy_procs
         if not wait_healthy("127.0.0.1", args.port, 180):
             raise RuntimeError("proxy did not become healthy")
         if dist is not None:
@@ -226,6 +257,7 @@ def main() -> int:
         if use_cuda:
             torch.cuda.synchronize()
         m0 = scrape(args.port)
+        c0 = cpu_snapshot(mock_procs, proxy_procs)
         t0 = time.perf_counter()
         stats = loadgen(bin_dir, args.port, args.conns, args.steps * args.batch, args.lg_threads, args.timeout)
         if use_cuda:
@@ -233,7 +265,9 @@ def main() -> int:
         if dist is not None:
             dist.barrier()
         elapsed = time.perf_counter() - t0
+        c1 = cpu_snapshot(mock_procs, proxy_procs)
         bd = breakdown(m0, scrape(args.port), elapsed) if args.impl == "native" else {}
+        bd.update(cpu_breakdown(c0, c1, stats["completed"], elapsed))
         local = [elapsed, float(stats["completed"]), float(stats["ttft_p50_ms"]), float(stats["ttft_p99_ms"]),
                  float(stats["errors"] + stats["non200"]), float(stats["ttfb_p50_ms"]), float(stats["lat_p50_ms"])]
         if dist is not None:

@@ -172,12 +172,37 @@ def build_sanitized(verbose: bool = False) -> list:
         return out
 
 
+# ThreadSanitizer build of the data plane (host code only): io loops, the shared engine's tick
+# lanes, verify shadow, metrics — the threads that share slot tables and result queues.
+TSAN_FLAGS = ["-Xarch_host", "-fsanitize=thread", "-Xarch_host", "-fno-omit-frame-pointer"]
+
+
+def build_tsan(verbose: bool = False) -> Path:
+    """TSan host build -> quorum_amd/bin/qmx_server_tsan."""
+    with _BuildLock():
+        BIN.mkdir(exist_ok=True)
+        srcs, libs = SAN_TARGETS["qmx_server_asan"]
+        b = BIN / "qmx_server_tsan"
+        paths = [PKG / x for x in srcs]
+        newest_hdr = max((h.stat().st_mtime for h in CSRC.glob("*.h")), default=0)
+        if b.exists() and b.stat().st_mtime > max([newest_hdr] + [x.stat().st_mtime for x in paths]):
+            return b
+        cmd = [hipcc(), "-x", "hip", f"--offload-arch={ARCH}", "-O1", "-g", "-std=c++17", f"-I{CSRC}"] + TSAN_FLAGS + \
+            [str(x) for x in paths] + ["-o", str(b), "-fsanitize=thread"] + libs
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"tsan build failed\n{r.stderr[-4000:]}")
+        return b
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--jobs", type=int, default=3)
     ap.add_argument("-v", "--verbose", action="store_true")
-    ap.add_argument("--sanitize", action="store_true", help="also build the ASan/UBSan host binaries")
+    ap.add_argument("--sanitize", action="store_true", help="also build the ASan/UBSan and TSan host binaries")
     args = ap.parse_args(argv)
     path = build(args.debug, args.jobs, args.verbose)
     print(path)
@@ -186,6 +211,7 @@ def main(argv=None) -> int:
     if args.sanitize:
         for t in build_sanitized(args.verbose):
             print(t)
+        print(build_tsan(args.verbose))
     return 0
 
 

@@ -149,3 +149,67 @@ def test_server_asan_traffic(san_bins, tmp_path):
         drop_srv.close()
         live.close()
     assert not errs, errs
+
+
+def test_server_tsan_shared_engine_lanes(tmp_path):
+    """ThreadSanitizer build of the data plane: 4 io loops share one engine with 3 tick lanes
+    (the GPU-hub topology, CPU engine) plus the verify shadow, under concurrent clients with
+    aborting and failing backends.  Any data race report fails the test."""
+    import concurrent.futures as cf
+
+    from quorum_amd.ops import build
+    from quorum_amd.runtime.native_server import native_config
+
+    tsan = build.build_tsan()
+    live = LiveUpstream()
+    stream = sse_stream(["Hel", "lo <think>x</think> wor", "ld"])
+    null_stream = [sse_chunk({"content": "a"}), sse_chunk({"content": None}), b"data: [DONE]\n\n"]
+    ports = [live.serve("ok", ("stream", 200, stream)), live.serve("null", ("stream", 200, null_stream)),
+             live.serve("e500", ("json", 500, {"error": {"message": "boom"}}))]
+    urls = [f"http://127.0.0.1:{p}/v1" for p in ports]
+    block = {"separator": "\n--\n", "hide_intermediate_think": True, "hide_final_think": True,
+             "thinking_tags": ["think"], "skip_final_aggregation": False}
+    cfg = cfg_parallel(3, block=block)
+    for b, u in zip(cfg["primary_backends"], urls):
+        b["url"] = u
+    port = free_port()
+    d = native_config(cfg, "127.0.0.1", port, "cpu", 0, 4)
+    d.update(env_api_key="", shared_engine=1, tick_lanes=3, verify=True)
+    path = tmp_path / "tsan.json"
+    path.write_text(json.dumps(d))
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=0:second_deadlock_stack=1:report_signal_unsafe=0")
+    srv = subprocess.Popen([str(tsan), str(path)], stderr=subprocess.PIPE, env=env)
+    try:
+        t0 = time.time()
+        while time.time() - t0 < 60:
+            try:
+                if httpx.get(f"http://127.0.0.1:{port}/health", timeout=1).status_code == 200:
+                    break
+            except httpx.HTTPError:
+                time.sleep(0.1)
+        req = {"messages": [{"role": "user", "content": "q"}], "stream": True}
+
+        def client(i):
+            with httpx.Client(base_url=f"http://127.0.0.1:{port}") as c:
+                for k in range(12):
+                    body = req if (i + k) % 3 else {"messages": req["messages"]}
+                    r = c.post("/chat/completions", json=body, headers={"Authorization": "Bearer k"}, timeout=60)
+                    assert r.status_code in (200, 500)
+                    if body.get("stream"):
+                        assert r.text.rstrip().endswith("data: [DONE]")
+            return True
+
+        with cf.ThreadPoolExecutor(8) as ex:
+            assert all(ex.map(client, range(8)))
+        assert httpx.get(f"http://127.0.0.1:{port}/metrics").status_code == 200
+    finally:
+        srv.send_signal(signal.SIGINT)
+        try:
+            _, err = srv.communicate(timeout=60)
+        except subprocess.TimeoutExpired:
+            srv.kill()
+            _, err = srv.communicate()
+        live.close()
+    err = err.decode(errors="replace")
+    assert "ThreadSanitizer" not in err, err[-6000:]
+    assert srv.returncode == 0, err[-3000:]
