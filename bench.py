@@ -222,6 +222,8 @@ def main() -> int:
 
     qbuild.build()
     bin_dir = os.path.dirname(str(qbuild.build_tools()[0]))
+    from quorum_amd.parallel.exchange import exchange_env
+    from quorum_amd.parallel.topology import summary as link_summary
     from quorum_amd.serve import spawn_workers, wait_healthy
 
     procs = []
@@ -239,8 +241,7 @@ def main() -> int:
         if args.placement == "spread" and world > 1:
             nonce = [str(time.time_ns()) if rank == 0 else None]
             dist.broadcast_object_list(nonce, src=0)
-            env.update({"QMX_XCHG_NONCE": nonce[0], "QMX_XCHG_PORT": str(args.port + 7),
-                        "QMX_RANK": str(rank), "QMX_WORLD": str(world)})
+            env.update(exchange_env(rank, world, args.port, nonce[0]))
         mock_procs = list(procs)
         proxy_procs = spawn_workers(cfg_path, "127.0.0.1", args.port, args.workers, engine,
                                local_rank if use_cuda else None, impl=args.impl, threads=args.threads, env=env)
@@ -303,7 +304,8 @@ def main() -> int:
                                           + (f" + ep{world} (backend streams spread over ranks, "
                                                 f"{'RCCL' if engine == 'hip' else 'TCP'} all-gather exchange)"
                                              if args.placement == "spread" and world > 1 else ""),
-                           "impl": args.impl, "engine": engine, "conns_per_rank": args.conns},
+                           "impl": args.impl, "engine": engine, "conns_per_rank": args.conns,
+                           "gpu_links": {k: v for k, v in link_summary().items() if k != "links_per_gpu"}},
                 "p50_ttft_ms": round(p50, 3),
                 "p99_ttft_ms": round(max(r[3] for r in rows), 3),
                 "p50_ttfb_ms": round(statistics.median(r[5] for r in rows), 3),

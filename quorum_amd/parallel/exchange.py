@@ -1,0 +1,55 @@
+"""Cross-rank settings of the native exchange (SURVEY §2.3 R1, §2.4 EP, §5.8).
+
+With ``runtime.placement: spread`` a session's N backend streams run on ranks
+owner..owner+N-1 (mod world) — the expert-parallel analog of quorum's backend fan-out
+(``oai_proxy.py:547-550``) — and the worker ranks send deltas and final texts back to the
+owner through lock-step all-gather rounds (``csrc/qmx_exchange.cpp``):
+
+* ``rccl``: ``ncclAllGather`` over xGMI on a dedicated HIP stream, a fixed-size slot per
+  rank plus a padded second phase for larger rounds (one collective per round, never per
+  session: KB payloads are latency-bound on the per-link-bound ring);
+* ``tcp``: the same protocol over a localhost TCP hub (CPU-only tests, no GPU).
+
+Every rank must agree on the transport, the rendezvous port and the RCCL unique-id file:
+:func:`exchange_env` builds them once (launcher / bench) and :func:`cluster_config` turns
+them into the native server's settings.
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Any, Dict, Mapping, Optional
+
+from .topology import RankEnv
+
+
+def exchange_env(rank: int, world: int, port: int, nonce: Optional[str] = None) -> Dict[str, str]:
+    """Environment for rank ``rank`` of a ``world``-rank node serving on ``port``.  The nonce
+    keys the RCCL unique-id file, so concurrent deployments on one host never collide; all
+    ranks of one deployment must get the same nonce."""
+    return {"QMX_RANK": str(rank), "QMX_WORLD": str(world), "QMX_XCHG_NONCE": nonce or str(time.time_ns()),
+            "QMX_XCHG_PORT": str(port + 7)}
+
+
+def cluster_config(placement: str, exchange: str, round_us: int, timeout: float, port: int, engine: str,
+                   env: Optional[Mapping[str, str]] = None) -> Dict[str, Any]:
+    """Rank / placement / exchange settings of the native server (env wins: QMX_RANK,
+    QMX_WORLD, QMX_XCHG_*).  ``exchange: auto`` = RCCL with the HIP engine, else TCP."""
+    e = os.environ if env is None else env
+    r = RankEnv.from_env(e)
+    xchg = e.get("QMX_XCHG", exchange)
+    if xchg == "auto":
+        xchg = "rccl" if engine == "hip" else "tcp"
+    if xchg not in ("rccl", "tcp"):
+        raise ValueError(f"runtime.exchange {xchg!r}: expected 'auto', 'rccl' or 'tcp'")
+    if placement not in ("local", "spread"):
+        raise ValueError(f"runtime.placement {placement!r}: expected 'local' or 'spread'")
+    nonce = e.get("QMX_XCHG_NONCE", "0")
+    return {
+        "rank": r.rank, "world": r.world, "placement": placement, "xchg": xchg,
+        "xchg_addr": e.get("QMX_XCHG_ADDR", "127.0.0.1"),
+        "xchg_port": int(e.get("QMX_XCHG_PORT", str(port + 7))),
+        "xchg_id_file": e.get("QMX_XCHG_ID_FILE", f"/tmp/qmx_xchg_{port}_{nonce}.id"),
+        "xchg_round_us": int(e.get("QMX_XCHG_ROUND_US", str(round_us))),
+        "xchg_timeout": float(e.get("QMX_XCHG_TIMEOUT", str(timeout))),
+    }

@@ -85,24 +85,13 @@ def _ca_bundle() -> str:
 
 
 def cluster_config(rt: RuntimeConfig, port: int, engine: str) -> Dict[str, Any]:
-    """Rank / placement / exchange settings (env wins: QMX_RANK, QMX_WORLD, QMX_XCHG_*)."""
-    env = os.environ
-    rank = int(env.get("QMX_RANK", env.get("RANK", "0")))
-    world = int(env.get("QMX_WORLD", env.get("WORLD_SIZE", "1")))
-    xchg = env.get("QMX_XCHG", rt.exchange)
-    if xchg == "auto":
-        xchg = "rccl" if engine == "hip" else "tcp"
-    if rt.placement not in ("local", "spread"):
-        raise NativeUnsupported(f"runtime.placement {rt.placement!r}: expected 'local' or 'spread'")
-    nonce = env.get("QMX_XCHG_NONCE", "0")
-    return {
-        "rank": rank, "world": world, "placement": rt.placement, "xchg": xchg,
-        "xchg_addr": env.get("QMX_XCHG_ADDR", "127.0.0.1"),
-        "xchg_port": int(env.get("QMX_XCHG_PORT", str(port + 7))),
-        "xchg_id_file": env.get("QMX_XCHG_ID_FILE", f"/tmp/qmx_xchg_{port}_{nonce}.id"),
-        "xchg_round_us": int(env.get("QMX_XCHG_ROUND_US", str(rt.exchange_round_us))),
-        "xchg_timeout": float(env.get("QMX_XCHG_TIMEOUT", str(rt.exchange_timeout))),
-    }
+    """Rank / placement / exchange settings (:func:`quorum_amd.parallel.exchange.cluster_config`)."""
+    from ..parallel.exchange import cluster_config as _cc
+
+    try:
+        return _cc(rt.placement, rt.exchange, rt.exchange_round_us, rt.exchange_timeout, port, engine)
+    except ValueError as exc:
+        raise NativeUnsupported(str(exc)) from exc
 
 
 def run_native(config: str, host: str, port: int, engine: str, device: Optional[int], threads: int) -> int:

@@ -259,30 +259,9 @@ def main(argv=None) -> int:
 
 
 def launch_ranks(argv, args) -> int:
-    """Node launcher: one rank per GPU on the shared SO_REUSEPORT port (DP session sharding);
-    with ``runtime.placement: spread`` the ranks also exchange backend streams (RCCL).
-    SIGHUP / SIGTERM are forwarded to every rank's supervisor."""
-    nonce = str(time.time_ns())
-    procs = []
-    for r in range(args.gpus):
-        env = dict(os.environ, QMX_RANK=str(r), QMX_WORLD=str(args.gpus), LOCAL_RANK=str(r), QMX_XCHG_NONCE=nonce)
-        cmd = [sys.executable, "-m", "quorum_amd.serve"] + [a for a in (argv or sys.argv[1:])]
-        if args.device is None:
-            cmd += ["--device", str(r)]
-        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
+    from .parallel.launcher import launch_ranks as _launch
 
-    def fwd(sig, _frame):
-        for p in procs:
-            try:
-                os.kill(p.pid, sig)
-            except OSError:
-                pass
-    for sig in (signal.SIGHUP, signal.SIGTERM, signal.SIGINT):
-        signal.signal(sig, fwd)
-    rc = 0
-    for p in procs:
-        rc = p.wait() or rc
-    return rc
+    return _launch(argv if argv is not None else sys.argv[1:], args.gpus, args.device is None, args.port)
 
 
 if __name__ == "__main__":
