@@ -1,0 +1,18 @@
+// qmx_prof.h — in-process CPU sampling profiler for the native data plane.
+//
+// QMX_PROF=<path> (%p = pid): SIGPROF every QMX_PROF_US (default 500) microseconds of *process* CPU
+// time (ITIMER_PROF: user + system, all threads); the handler records the interrupted
+// thread's call stack into a preallocated ring (async-signal-safe: no allocation, one
+// atomic slot claim).  prof_stop() writes one line per sample, frames as
+// "module+0xoffset", for offline symbolisation (tools/cpuprof.py → llvm-symbolizer).
+// A syscall shows up as its libc wrapper frame (the signal lands on the return to user
+// space), so the profile splits the proxy's CPU into socket I/O, epoll, locking, HTTP /
+// JSON handling and engine host work.  Not for production: one timer per process.
+#pragma once
+
+namespace qmx {
+
+void prof_start();  // no-op unless QMX_PROF is set (idempotent)
+void prof_stop();   // stop sampling, write the profile
+
+}  // namespace qmx

@@ -32,6 +32,7 @@
 #include "qmx_exchange.h"
 #include "qmx_hip.h"
 #include "qmx_json.h"
+#include "qmx_prof.h"
 
 namespace qmx {
 namespace {
@@ -260,6 +261,8 @@ struct Client {
   bool keepalive = true;
   bool dead = false;         // error: close now
   bool close_after = false;  // graceful: close once output is flushed
+  bool queued = false;       // in the loop's end-of-iteration flush list
+  bool want_out = false;     // EPOLLOUT armed (socket buffer was full)
 };
 
 enum UpMode { UP_ENGINE, UP_BUFFER, UP_PASS };
@@ -683,13 +686,14 @@ class Loop {
           if (it != clients_.end() && !it->second->sess && !it->second->dead) process_requests(it->second.get());
         }
       }
-      if (!pending_close_.empty()) reap_clients();
       double t = now_s();
       if (t - last_sweep > 0.1) {
         sweep_timeouts(t);
         last_sweep = t;
         snapshot();  // own CPU engine (the GPU hub snapshots the shared HIP engine)
       }
+      if (!flushq_.empty()) flush_queued();
+      if (!pending_close_.empty()) reap_clients();
     }
   }
 
@@ -852,6 +856,7 @@ class Loop {
       Client* c = kv.second.get();
       if (!c->sess && c->in.empty() && c->out_off >= c->out.size()) mark_close(c);
     }
+    if (!flushq_.empty()) flush_queued();
     if (!pending_close_.empty()) reap_clients();
     return (sessions_.empty() && clients_.empty()) || t > drain_deadline_;
   }
@@ -911,25 +916,53 @@ class Loop {
     close(c->fd);
     clients_.erase(c->fd);
   }
+  // Output is corked per loop iteration: everything written to a client while handling one
+  // batch of epoll events and tick results (SSE headers + role event, several streams'
+  // deltas, the last delta + [DONE]) leaves in ONE send at the end of the iteration.  A
+  // loopback send runs the receiver's TCP input path in the sender's context, so sends —
+  // not parsing — dominated the proxy's CPU profile (tools/cpuprof.py: __send 38%).
   void write_client(Client* c, const std::string& data) {
     if (c->dead) return;
     if (c->out.size() == c->out_off) {
       c->out.clear();
       c->out_off = 0;
-      ssize_t w = send(c->fd, data.data(), data.size(), MSG_NOSIGNAL);
-      if (w == (ssize_t)data.size()) return;
-      if (w < 0) {
-        if (errno != EAGAIN && errno != EWOULDBLOCK) {
-          c->dead = true;
-          return;
-        }
-        w = 0;
-      }
-      c->out.assign(data, w, std::string::npos);
-      mod(c->fd, EPOLLIN | EPOLLOUT, tag(3, c->fd));
-      return;
     }
     c->out += data;
+    if (!c->queued && !c->want_out) {
+      c->queued = true;
+      flushq_.push_back(c->fd);
+    }
+  }
+  void flush_queued() {
+    std::vector<int> fds;
+    fds.swap(flushq_);
+    for (int fd : fds) {
+      auto it = clients_.find(fd);
+      if (it == clients_.end()) continue;
+      Client* c = it->second.get();
+      c->queued = false;
+      if (c->dead || c->want_out) continue;
+      while (c->out_off < c->out.size()) {
+        ssize_t w = send(c->fd, c->out.data() + c->out_off, c->out.size() - c->out_off, MSG_NOSIGNAL);
+        if (w > 0) {
+          c->out_off += w;
+          continue;
+        }
+        if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+          c->want_out = true;
+          mod(c->fd, EPOLLIN | EPOLLOUT, tag(3, c->fd));
+        } else {
+          c->dead = true;
+          pending_close_.push_back(c->fd);
+        }
+        break;
+      }
+      if (c->out_off >= c->out.size()) {
+        c->out.clear();
+        c->out_off = 0;
+        if (c->close_after) pending_close_.push_back(c->fd);
+      }
+    }
   }
   void flush_client(Client* c) {
     while (c->out_off < c->out.size()) {
@@ -944,6 +977,7 @@ class Loop {
     }
     c->out.clear();
     c->out_off = 0;
+    c->want_out = false;
     mod(c->fd, EPOLLIN, tag(3, c->fd));
     if (c->close_after) pending_close_.push_back(c->fd);
   }
@@ -2213,6 +2247,7 @@ class Loop {
   std::unordered_map<int, SSL*> idle_ssl_;  // pooled https connections
   SSL_CTX* tls_ = nullptr;                  // https upstreams (peer + host verification, as httpx)
   std::vector<int> pending_close_, pending_requests_;
+  std::vector<int> flushq_;  // clients with corked output (flushed at the end of each iteration)
 };
 
 void on_signal(int sig) {
@@ -2224,6 +2259,7 @@ void on_signal(int sig) {
 
 int run_server(const ServerCfg& cfg0) {
   ServerCfg cfg = cfg0;
+  prof_start();  // QMX_PROF=<path>: CPU sampling profile of this process (qmx_prof.h)
   bool any_https = false;
   for (auto& b : cfg.backends) {
     if (!b.valid || b.host.empty()) continue;
@@ -2299,6 +2335,7 @@ int run_server(const ServerCfg& cfg0) {
     });
   }
   for (auto& t : ts) t.join();
+  prof_stop();
   if (xch) {
     xch->request_stop();  // keeps taking part in rounds until every rank has stopped
     xch->join();

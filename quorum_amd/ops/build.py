@@ -20,7 +20,8 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent.parent
 CSRC = PKG / "csrc"
 BUILD = PKG.parent / "build" / "qmx"
-SOURCES = ["qmx_engine.cpp", "qmx_json.cpp", "qmx_server.cpp", "qmx_exchange.cpp", "qmx_hip.hip", "bindings.cpp"]
+SOURCES = ["qmx_engine.cpp", "qmx_json.cpp", "qmx_server.cpp", "qmx_exchange.cpp", "qmx_prof.cpp", "qmx_hip.hip",
+           "bindings.cpp"]
 ARCH = os.environ.get("QMX_ARCH", "gfx950")
 
 
@@ -138,7 +139,7 @@ SAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=und
 SAN_TARGETS = {
     "qmx_fuzz_asan": (["tools/csrc/fuzz_host.cpp", "csrc/qmx_engine.cpp", "csrc/qmx_json.cpp"], []),
     "qmx_server_asan": (["tools/csrc/server_main.cpp", "csrc/qmx_server.cpp", "csrc/qmx_engine.cpp",
-                         "csrc/qmx_json.cpp", "csrc/qmx_exchange.cpp", "csrc/qmx_hip.hip"],
+                         "csrc/qmx_json.cpp", "csrc/qmx_exchange.cpp", "csrc/qmx_prof.cpp", "csrc/qmx_hip.hip"],
                         ["-L/opt/rocm/lib", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", "-lssl", "-lcrypto",
                          "-Wl,-rpath,/opt/rocm/lib", "-pthread"]),
 }
