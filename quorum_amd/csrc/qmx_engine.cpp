@@ -307,6 +307,29 @@ int HostEngine::open(int index, bool filter, bool emit) {
 
 void HostEngine::feed(int slot, const std::string& data) {
   std::lock_guard<std::mutex> g(mu_);
+  feed_locked(slot, data);
+}
+
+void HostEngine::finish(int slot) {
+  std::lock_guard<std::mutex> g(mu_);
+  finish_locked(slot);
+}
+
+void HostEngine::release(int slot) {
+  std::lock_guard<std::mutex> g(mu_);
+  release_locked(slot);
+}
+
+void HostEngine::apply_ops(const std::vector<EngineOp>& ops) {
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto& op : ops) {
+    if (op.kind == EngineOp::FEED) feed_locked(op.slot, op.data);
+    else if (op.kind == EngineOp::FINISH) finish_locked(op.slot);
+    else release_locked(op.slot);
+  }
+}
+
+void HostEngine::feed_locked(int slot, const std::string& data) {
   if (slot < 0 || slot >= (int)meta_.size() || !meta_[slot].live) return;
   Meta& m = meta_[slot];
   m.incoming += data;
@@ -317,8 +340,7 @@ void HostEngine::feed(int slot, const std::string& data) {
   }
 }
 
-void HostEngine::finish(int slot) {
-  std::lock_guard<std::mutex> g(mu_);
+void HostEngine::finish_locked(int slot) {
   if (slot < 0 || slot >= (int)meta_.size() || !meta_[slot].live) return;
   Meta& m = meta_[slot];
   m.eof = true;
@@ -328,8 +350,7 @@ void HostEngine::finish(int slot) {
   }
 }
 
-void HostEngine::release(int slot) {
-  std::lock_guard<std::mutex> g(mu_);
+void HostEngine::release_locked(int slot) {
   if (slot < 0 || slot >= (int)meta_.size() || !meta_[slot].live) return;
   meta_[slot].live = false;
   meta_[slot].incoming.clear();

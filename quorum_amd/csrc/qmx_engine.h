@@ -63,6 +63,15 @@ struct SlotCore {
 void process_slot(const TagSet& ts, SlotCore& s, const uint8_t* data, size_t n, bool eof,
                   int64_t created, std::string& out);
 
+// One deferred slot operation: io loops batch their feed / finish / release calls of an
+// event-loop iteration and hand them over under ONE engine lock (apply_ops).
+struct EngineOp {
+  enum Kind : int { FEED = 0, FINISH = 1, RELEASE = 2 };
+  int kind;
+  int slot;
+  std::string data;
+};
+
 struct SlotResult {
   int slot;
   std::string sse;
@@ -92,6 +101,7 @@ class HostEngine {
   void feed(int slot, const std::string& data);
   void finish(int slot);
   void release(int slot);
+  void apply_ops(const std::vector<EngineOp>& ops);  // in order, one lock
   int submit_finalize(const std::vector<int>& slots, bool strip, bool texts, const std::string& joiner,
                       int64_t created);
   bool has_work();
@@ -120,6 +130,10 @@ class HostEngine {
   virtual void process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results, int lane) = 0;
   virtual void finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out, int lane) = 0;
   virtual void on_free(int /*slot*/) {}
+
+  void feed_locked(int slot, const std::string& data);
+  void finish_locked(int slot);
+  void release_locked(int slot);
 
   struct Meta {
     bool live = false;

@@ -23,6 +23,7 @@ struct WorkItem {
 };
 struct WorkResult {
   uint32_t consumed, out_len, status, content_len;
+  uint32_t seq;  // written last (system-scope release): the lane's tick sequence number
 };
 constexpr int kTplBytes = 320;  // per-stream event shape template (qmx_lex.h TPL_*)
 struct DevSlot {
@@ -88,6 +89,11 @@ struct TickLane {
   double kernel_ms = 0.0, host_prep_us = 0, gpu_wait_us = 0, process_us = 0;  // host-side tick breakdown
   double stage_us[16] = {0};
   double clk_cycles = 0, clk_us = 0;
+  // completion by polling the kernel-published sequence numbers (HipEngine::wait_results)
+  uint32_t seq = 0;
+  double ema_us = 40.0;  // launch-to-results time, smoothed
+  bool timing_pending = false;
+  uint64_t poll_fallbacks = 0;
 };
 
 class HipEngine : public HostEngine {
@@ -108,6 +114,8 @@ class HipEngine : public HostEngine {
   void escalate(int slot, bool fresh);
   void finalize_host(const FinalizeReq& r, std::vector<FinalizeRes>& out);
   void wait_stream(TickLane& L);
+  void wait_results(TickLane& L, int n, uint32_t seq);
+  void collect_timing(TickLane& L);
   void ensure_in(TickLane& L, size_t bytes);
   void ensure_out(TickLane& L, size_t bytes);
   void build_params(TickLane& L, int64_t created);
@@ -146,6 +154,8 @@ class HipEngine : public HostEngine {
   uint64_t fin_launches_ = 0, fin_items_ = 0;  // under fin_mu_
   double fin_ms_ = 0.0;
   int spin_us_ = 0;  // QMX_WAIT_SPIN_US: yield-poll before the blocking wait
+  bool poll_ = true;  // QMX_WAIT=event: wait on a blocking-sync HIP event instead of polling
+  int poll_us_ = 6;   // QMX_POLL_US: poll period once the expected kernel time has passed
 };
 
 }  // namespace qmx

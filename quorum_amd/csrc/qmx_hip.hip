@@ -24,6 +24,8 @@
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <sched.h>
+#include <sys/prctl.h>
+#include <time.h>
 
 #include <chrono>
 #include <thread>
@@ -300,10 +302,10 @@ __device__ inline int hold_cut(const Smem& s, const uint8_t* Z, int ncand, int n
 // ------------------------------------------------------------------------------------
 // the fused tick kernel
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict__ items,
-                                                      const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
-                                                      WorkResult* __restrict__ res, DevSlot* __restrict__ state,
-                                                      uint8_t* __restrict__ content, KParams Pk) {
+__device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, const uint8_t* __restrict__ in,
+                                          uint8_t* __restrict__ out, WorkResult* __restrict__ res,
+                                          DevSlot* __restrict__ state, uint8_t* __restrict__ content,
+                                          const KParams& Pk) {
   __shared__ Smem s;
   __shared__ KParams P;  // kernel args staged in LDS: lane-divergent pattern/envelope reads
   __shared__ uint16_t TKP[BS / 64][TOK_CAP];  // per-wave token buffers (positions)
@@ -1002,6 +1004,22 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
   }
 }
 
+// Every workgroup publishes its result last: all threads fence their host-mapped stores
+// (output SSE, result record) at system scope, then thread 0 stores the tick's sequence
+// number into the record.  The host polls these sequence numbers instead of waiting on a
+// HIP event: no interrupt round trip and no HSA spin-wait per tick (tools/cpuprof.py: the
+// blocked event wait spun inside libhsa-runtime for most of each kernel's duration).
+// Every early exit of tick_body is block-uniform, so every thread reaches the fence.
+__global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict__ items,
+                                                      const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                      WorkResult* __restrict__ res, DevSlot* __restrict__ state,
+                                                      uint8_t* __restrict__ content, KParams Pk, uint32_t seq) {
+  tick_body(items, in, out, res, state, content, Pk);
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(&res[blockIdx.x].seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ------------------------------------------------------------------------------------
 // the finalize kernel: K3 think_strip_final + K4 join_pack + K5 sse_encode, one workgroup
 // per session request, texts read straight from the HBM-resident content arena
@@ -1228,6 +1246,51 @@ void HipEngine::wait_stream(TickLane& L) {
   HIP_CHECK(hipEventSynchronize(L.evb));
 }
 
+// Results published by the tick kernel itself (qmx_tick_kernel's sequence numbers): sleep
+// most of the expected kernel time (EMA), then poll every poll_us_ with a 1 us timer slack.
+// A launch that has not published after 4x the EMA + 2 ms waits on its event (surfaces a
+// fault; correct even if host-mapped visibility misbehaved: counted in poll_fallbacks).
+void HipEngine::wait_results(TickLane& L, int n, uint32_t seq) {
+  using HC = std::chrono::steady_clock;
+  static thread_local bool slack = (prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0), true);
+  (void)slack;
+  const auto t0 = HC::now();
+  auto nap = [](double us) {
+    if (us < 1) return;
+    timespec ts{0, (long)(us * 1000)};
+    nanosleep(&ts, nullptr);
+  };
+  auto done = [&](int& i) {
+    while (i < n && __atomic_load_n(&L.h_res[i].seq, __ATOMIC_ACQUIRE) == seq) ++i;
+    return i == n;
+  };
+  int i = 0;
+  nap(0.6 * L.ema_us - 6.0);
+  while (!done(i)) {
+    const double el = std::chrono::duration<double, std::micro>(HC::now() - t0).count();
+    if (el > 4.0 * L.ema_us + 2000.0) {
+      HIP_CHECK(hipEventSynchronize(L.ev1));  // throws on a kernel fault
+      ++L.poll_fallbacks;
+      break;  // the stream has drained: every result is final
+    }
+    if (el < spin_us_) {
+      sched_yield();
+      continue;
+    }
+    nap(poll_us_);
+  }
+  const double tot = std::chrono::duration<double, std::micro>(HC::now() - t0).count();
+  L.ema_us = 0.85 * L.ema_us + 0.15 * std::min(tot, 2000.0);
+}
+
+void HipEngine::collect_timing(TickLane& L) {
+  if (!L.timing_pending) return;
+  L.timing_pending = false;
+  HIP_CHECK(hipEventSynchronize(L.ev1));  // long complete when called for the previous launch
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, L.ev0, L.ev1) == hipSuccess) L.kernel_ms += ms;
+}
+
 HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_bytes, int max_slots,
                      int content_cap, int lanes)
     : HostEngine(tags),
@@ -1237,6 +1300,8 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
       content_cap_((uint32_t)content_cap) {
   HIP_CHECK(hipSetDevice(device_));
   if (const char* sp = getenv("QMX_WAIT_SPIN_US")) spin_us_ = atoi(sp);
+  if (const char* w = getenv("QMX_WAIT")) poll_ = std::string(w) != "event";
+  if (const char* pu = getenv("QMX_POLL_US")) poll_us_ = std::max(1, atoi(pu));
   HIP_CHECK(hipMalloc(&d_state_, sizeof(DevSlot) * (size_t)max_slots_));
   HIP_CHECK(hipMemset(d_state_, 0, sizeof(DevSlot) * (size_t)max_slots_));
   HIP_CHECK(hipMalloc(&d_content_, (size_t)content_cap_ * (size_t)max_slots_));
@@ -1465,17 +1530,23 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
     L.host_prep_us += std::chrono::duration<double, std::micro>(tp1 - tp0).count();
     roctxRangePushA("qmx_tick");  // rocprofv3 --marker-trace: one range per tick launch + wait
     L.h2d_bytes += in_off;
+    collect_timing(L);  // the previous launch's kernel time (its events are reused now)
     HIP_CHECK(hipEventRecord(L.ev0, L.stream));
+    const uint32_t seq = ++L.seq;
     hipLaunchKernelGGL(qmx_tick_kernel, dim3(n), dim3(BS), 0, L.stream, L.h_items, L.h_in, L.h_out, L.h_res, d_state_,
-                       d_content_, L.params);
+                       d_content_, L.params, seq);
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipEventRecord(L.ev1, L.stream));
-    wait_stream(L);
+    if (poll_) {
+      wait_results(L, n, seq);
+      L.timing_pending = true;
+    } else {
+      wait_stream(L);
+      L.timing_pending = true;
+      collect_timing(L);
+    }
     roctxRangePop();
     L.gpu_wait_us += std::chrono::duration<double, std::micro>(HC::now() - tp1).count();
-    float ms = 0.f;
-    hipEventElapsedTime(&ms, L.ev0, L.ev1);
-    L.kernel_ms += ms;
     ++L.launches;
     L.items += n;
     if (L.params.dbg) {
@@ -1652,6 +1723,10 @@ void HipEngine::finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes
   grow_device(&d_join_, &join_cap_, join_off + 16);
   grow_device(&d_fout_, &dfout_cap_, out_off + 16);
   grow_mapped(&h_fout_, &fout_cap_, out_off + 16);
+  {
+    std::lock_guard<std::mutex> lg(L.mu);
+    collect_timing(L);
+  }
   roctxRangePushA("qmx_finalize");
   HIP_CHECK(hipEventRecord(L.ev0, L.stream));
   hipLaunchKernelGGL(qmx_finalize_kernel, dim3(n), dim3(BS), 0, L.stream, h_fin_, h_fint_, h_fin_in_, d_content_,
@@ -1710,6 +1785,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["host_prep_us"] += L.host_prep_us;
     m["gpu_wait_us"] += L.gpu_wait_us;
     m["process_us"] += L.process_us;
+    m["poll_fallbacks"] += (double)L.poll_fallbacks;
     for (int k = 1; k < 11; ++k) stage[k] += L.stage_us[k];
     cyc += L.clk_cycles;
     cus += L.clk_us;

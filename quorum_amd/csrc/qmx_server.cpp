@@ -280,6 +280,7 @@ struct Up {
   double last_io = 0, deadline = 0, timeout = 60, t_open = 0;
   SSL* ssl = nullptr;     // https backend
   bool tls_hs = false;    // handshake in progress
+  bool out_armed = false;  // EPOLLOUT registered (connect / a send that hit EAGAIN)
 };
 
 struct BState {
@@ -370,6 +371,13 @@ class Verifier {
     rmap_.erase(it->second.shadow);
     cpu_.release(it->second.shadow);
     map_.erase(it);
+  }
+  void apply_ops(const std::vector<EngineOp>& ops) {
+    for (auto& op : ops) {
+      if (op.kind == EngineOp::FEED) feed(op.slot, op.data);
+      else if (op.kind == EngineOp::FINISH) finish(op.slot);
+      else release(op.slot);
+    }
   }
   void submit(int fid, const std::vector<int>& slots, bool strip, bool texts, const std::string& joiner,
               int64_t created) {
@@ -521,6 +529,10 @@ class GpuHub {
     eng_->release(slot);
     if (ver_) ver_->release(slot);
   }
+  void apply_ops(const std::vector<EngineOp>& ops) {
+    eng_->apply_ops(ops);
+    if (ver_) ver_->apply_ops(ops);
+  }
   int submit(int loop, const std::vector<int>& slots, bool strip, bool texts, const std::string& joiner,
              int64_t created) {
     std::lock_guard<std::mutex> g(omu_);  // the id must be routable before a tick lane sees it
@@ -670,14 +682,12 @@ class Loop {
     std::vector<epoll_event> evs(512);
     double last_sweep = now_s();
     while (!g_stop.load()) {
-      int n = epoll_wait(ep_, evs.data(), (int)evs.size(), 50);
+      // inline engine with work queued by the last iteration (e.g. a finalize submitted
+      // while applying tick results): poll instead of sleeping
+      const int to = (!hub_ && kick_) ? 0 : 50;
+      int n = epoll_wait(ep_, evs.data(), (int)evs.size(), to);
       for (int i = 0; i < n; ++i) dispatch(evs[i]);
       if (g_drain.load() && drain_step()) break;
-      if (!hub_ && eng_->has_work()) tick_inline();
-      if (hub_ && kick_) {
-        kick_ = false;
-        hub_->kick();
-      }
       if (!pending_requests_.empty()) {
         std::vector<int> fds;
         fds.swap(pending_requests_);
@@ -691,6 +701,17 @@ class Loop {
         sweep_timeouts(t);
         last_sweep = t;
         snapshot();  // own CPU engine (the GPU hub snapshots the shared HIP engine)
+      }
+      flush_ops();
+      if (!hub_) {
+        if (kick_ || eng_->has_work()) {
+          kick_ = false;
+          tick_inline();
+          flush_ops();  // releases queued while applying the results
+        }
+      } else if (kick_) {
+        kick_ = false;
+        hub_->kick();
       }
       if (!flushq_.empty()) flush_queued();
       if (!pending_close_.empty()) reap_clients();
@@ -753,6 +774,7 @@ class Loop {
     if (kind == 4) {
       auto it = ups_.find(fd);
       if (it != ups_.end()) on_up(it->second.get(), e.events);
+      else on_parked(fd);
       return;
     }
   }
@@ -816,20 +838,22 @@ class Loop {
     if (ver_) ver_->open(slot, index, f, e);
     return slot;
   }
-  void e_feed(int slot, const std::string& d) {
-    if (hub_) return hub_->feed(slot, d);
-    eng_->feed(slot, d);
-    if (ver_) ver_->feed(slot, d);
-  }
-  void e_finish(int slot) {
-    if (hub_) return hub_->finish(slot);
-    eng_->finish(slot);
-    if (ver_) ver_->finish(slot);
-  }
-  void e_release(int slot) {
-    if (hub_) return hub_->release(slot);
-    eng_->release(slot);
-    if (ver_) ver_->release(slot);
+  // feed / finish / release are queued in order and handed to the engine once per loop
+  // iteration (flush_ops: one engine lock instead of one per upstream read — with the
+  // shared engine, 8+ loops and the tick lanes otherwise contend on it per call)
+  void e_feed(int slot, const std::string& d) { ops_.push_back(EngineOp{EngineOp::FEED, slot, d}); }
+  void e_finish(int slot) { ops_.push_back(EngineOp{EngineOp::FINISH, slot, std::string()}); }
+  void e_release(int slot) { ops_.push_back(EngineOp{EngineOp::RELEASE, slot, std::string()}); }
+  void flush_ops() {
+    if (ops_.empty()) return;
+    if (hub_) {
+      hub_->apply_ops(ops_);
+    } else {
+      eng_->apply_ops(ops_);
+      if (ver_) ver_->apply_ops(ops_);
+    }
+    ops_.clear();
+    kick_ = true;
   }
   int e_submit(const std::vector<int>& slots, bool strip, bool texts, const std::string& joiner, int64_t created) {
     if (hub_) return hub_->submit(idx_, slots, strip, texts, joiner, created);
@@ -1197,6 +1221,10 @@ class Loop {
     while (!pool.empty() && fd < 0) {
       fd = pool.back();
       pool.pop_back();
+      if (!parked_.count(fd)) {  // closed while parked (on_parked): stale entry
+        fd = -1;
+        continue;
+      }
       u->reused = true;
       auto it = idle_ssl_.find(fd);
       if (it != idle_ssl_.end()) {
@@ -1217,6 +1245,7 @@ class Loop {
       c_up_conns++;
       u->fd = fd;
       add(fd, EPOLLIN | EPOLLOUT, tag(4, fd));
+      u->out_armed = true;
       if (be.https) {
         u->ssl = SSL_new(tls_);
         SSL_set_fd(u->ssl, fd);
@@ -1228,8 +1257,8 @@ class Loop {
         u->tls_hs = true;
       }
     } else {
-      u->fd = fd;
-      add(fd, EPOLLIN | EPOLLOUT, tag(4, fd));
+      u->fd = fd;  // pooled: still registered for EPOLLIN (no epoll_ctl on the reuse path)
+      parked_.erase(fd);
     }
     Up* p = u.get();
     ups_[fd] = std::move(u);
@@ -1264,8 +1293,14 @@ class Loop {
           continue;
         }
         int e = SSL_get_error(u->ssl, w);
-        if (e == SSL_ERROR_WANT_WRITE) return mod(u->fd, EPOLLIN | EPOLLOUT, tag(4, u->fd));
-        if (e == SSL_ERROR_WANT_READ) return mod(u->fd, EPOLLIN, tag(4, u->fd));
+        if (e == SSL_ERROR_WANT_WRITE) {
+          u->out_armed = true;
+          return mod(u->fd, EPOLLIN | EPOLLOUT, tag(4, u->fd));
+        }
+        if (e == SSL_ERROR_WANT_READ) {
+          u->out_armed = false;
+          return mod(u->fd, EPOLLIN, tag(4, u->fd));
+        }
         if (u->reused && !u->got_bytes) return retry_fresh(u);  // stale pooled TLS connection
         c_fail_connect++;
         return up_error(u, "All connection attempts failed");
@@ -1276,11 +1311,20 @@ class Loop {
         u->last_io = now_s();
         continue;
       }
-      if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) return;
+      if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+        if (!u->out_armed) {
+          u->out_armed = true;
+          mod(u->fd, EPOLLIN | EPOLLOUT, tag(4, u->fd));
+        }
+        return;
+      }
       c_fail_connect++;
       return up_error(u, "All connection attempts failed");
     }
-    mod(u->fd, EPOLLIN, tag(4, u->fd));
+    if (u->out_armed) {
+      u->out_armed = false;
+      mod(u->fd, EPOLLIN, tag(4, u->fd));
+    }
   }
   // read what the socket (or the TLS layer) has: >0 bytes, 0 would block, -1 eof/error
   ssize_t up_read(Up* u, char* buf, size_t n) {
@@ -1366,9 +1410,11 @@ class Loop {
   }
   void drop_up(Up* u, bool reuse) {
     int fd = u->fd;
-    if (reuse && !u->rp.close && !u->tls_hs) {
-      epoll_ctl(ep_, EPOLL_CTL_DEL, fd, nullptr);  // parked: re-armed when reused
+    if (reuse && !u->rp.close && !u->tls_hs && !u->out_armed) {
+      // parked, still registered for EPOLLIN: a keep-alive upstream sends nothing unasked,
+      // so readiness while parked means it closed (on_parked); reuse needs no epoll_ctl
       idle_[u->backend].push_back(fd);
+      parked_[fd] = u->backend;
       if (u->ssl) idle_ssl_[fd] = u->ssl;  // the TLS session stays with the pooled socket
     } else {
       epoll_ctl(ep_, EPOLL_CTL_DEL, fd, nullptr);
@@ -1377,6 +1423,21 @@ class Loop {
     }
     u->ssl = nullptr;
     ups_.erase(fd);
+  }
+  // readiness on a parked keep-alive socket: the upstream closed it (or broke protocol)
+  void on_parked(int fd) {
+    auto it = parked_.find(fd);
+    if (it == parked_.end()) return;
+    auto& pool = idle_[it->second];
+    pool.erase(std::remove(pool.begin(), pool.end(), fd), pool.end());
+    parked_.erase(it);
+    auto s = idle_ssl_.find(fd);
+    if (s != idle_ssl_.end()) {
+      SSL_free(s->second);
+      idle_ssl_.erase(s);
+    }
+    epoll_ctl(ep_, EPOLL_CTL_DEL, fd, nullptr);
+    close(fd);
   }
   void up_error(Up* u, const std::string& msg) {
     Session* s = u->sess;
@@ -2245,9 +2306,11 @@ class Loop {
   std::map<std::pair<uint64_t, int>, Session*> shadow_;     // worker streams by (owner key, bi)
   std::vector<std::vector<int>> idle_;
   std::unordered_map<int, SSL*> idle_ssl_;  // pooled https connections
+  std::unordered_map<int, int> parked_;     // pooled fd -> backend (registered, EPOLLIN)
   SSL_CTX* tls_ = nullptr;                  // https upstreams (peer + host verification, as httpx)
   std::vector<int> pending_close_, pending_requests_;
   std::vector<int> flushq_;  // clients with corked output (flushed at the end of each iteration)
+  std::vector<EngineOp> ops_;  // engine feed / finish / release of this iteration (flush_ops)
 };
 
 void on_signal(int sig) {

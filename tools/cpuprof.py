@@ -12,6 +12,7 @@ from __future__ import annotations
 import argparse
 import collections
 import json
+import os
 import re
 import shutil
 import subprocess
@@ -33,17 +34,33 @@ CATEGORIES = [
 ]
 
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def local_module(mod: str) -> str:
+    """A profile taken on the GPU box names modules under its own repo copy: map our own
+    binaries back to this tree (they are the same files — the box runs the shipped .so)."""
+    if os.path.exists(mod):
+        return mod
+    base = os.path.basename(mod)
+    for cand in (os.path.join(ROOT, "quorum_amd", base), os.path.join(ROOT, "quorum_amd", "bin", base)):
+        if os.path.exists(cand):
+            return cand
+    return mod
+
+
 def symbolize(frames):
     by_mod = collections.defaultdict(set)
     for fr in frames:
         mod, _, off = fr.rpartition("+")
         by_mod[mod].add(off)
     names = {}
-    for mod, offs in by_mod.items():
+    for mod0, offs in by_mod.items():
         offs = sorted(offs)
+        mod = local_module(mod0)
         if mod in ("?", "") or not shutil.which(SYMBOLIZER) and not SYMBOLIZER.startswith("/"):
             for o in offs:
-                names[f"{mod}+{o}"] = f"{mod}+{o}"
+                names[f"{mod0}+{o}"] = f"{mod0}+{o}"
             continue
         try:
             out = subprocess.run([SYMBOLIZER, f"--obj={mod}", "-C", "--no-inlines", "--functions=linkage"],
@@ -54,7 +71,7 @@ def symbolize(frames):
         short = mod.rsplit("/", 1)[-1]
         for o, blk in zip(offs, blocks + [[]] * (len(offs) - len(blocks))):
             fn = blk[0] if blk else "??"
-            names[f"{mod}+{o}"] = f"{fn} [{short}]" if fn != "??" else f"?? [{short}+{o}]"
+            names[f"{mod0}+{o}"] = f"{fn} [{short}]" if fn != "??" else f"?? [{short}+{o}]"
     return names
 
 
