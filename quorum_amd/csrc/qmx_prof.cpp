@@ -5,7 +5,9 @@
 #include <errno.h>
 #include <execinfo.h>
 #include <signal.h>
+#include <sys/syscall.h>
 #include <sys/time.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -31,6 +33,7 @@ Sample* g_ring = nullptr;
 std::atomic<size_t> g_next{0};
 std::atomic<bool> g_on{false};
 std::string g_path;
+int g_us = 500;
 
 void on_prof(int, siginfo_t*, void*) {
   if (!g_on.load(std::memory_order_relaxed)) return;
@@ -57,14 +60,30 @@ void prof_start() {
   sa.sa_flags = SA_SIGINFO | SA_RESTART;
   sigemptyset(&sa.sa_mask);
   sigaction(SIGPROF, &sa, nullptr);
-  int us = 500;
-  if (const char* e = getenv("QMX_PROF_US")) us = std::max(50, atoi(e));
+  if (const char* e = getenv("QMX_PROF_US")) g_us = std::max(50, atoi(e));
   itimerval tv{};
-  tv.it_interval.tv_sec = us / 1000000;
-  tv.it_interval.tv_usec = us % 1000000;
+  tv.it_interval.tv_sec = g_us / 1000000;
+  tv.it_interval.tv_usec = g_us % 1000000;
   tv.it_value = tv.it_interval;
   g_on.store(true);
   setitimer(ITIMER_PROF, &tv, nullptr);
+}
+
+void prof_thread() {
+  // A process-wide ITIMER_PROF fires at most once per scheduler tick however many threads
+  // burn CPU; a per-thread CPU-time timer per hot thread samples each of them fully.
+  if (!g_on.load()) return;
+  sigevent sev{};
+  sev.sigev_notify = SIGEV_THREAD_ID;
+  sev.sigev_signo = SIGPROF;
+  sev._sigev_un._tid = (pid_t)syscall(SYS_gettid);
+  timer_t t;
+  if (timer_create(CLOCK_THREAD_CPUTIME_ID, &sev, &t) != 0) return;
+  itimerspec its{};
+  its.it_interval.tv_sec = g_us / 1000000;
+  its.it_interval.tv_nsec = (long)(g_us % 1000000) * 1000;
+  its.it_value = its.it_interval;
+  timer_settime(t, 0, &its, nullptr);  // lives until the thread exits (profiling only)
 }
 
 void prof_stop() {

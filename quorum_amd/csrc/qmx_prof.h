@@ -12,7 +12,8 @@
 
 namespace qmx {
 
-void prof_start();  // no-op unless QMX_PROF is set (idempotent)
+void prof_start();   // no-op unless QMX_PROF is set (idempotent)
+void prof_thread();  // add a per-thread CPU-time sampler for the calling thread (if on)
 void prof_stop();   // stop sampling, write the profile
 
 }  // namespace qmx

@@ -555,6 +555,7 @@ class GpuHub {
 
  private:
   void run(int lane) {
+    prof_thread();
     if (cfg_.engine == "hip") hipSetDevice(cfg_.device);
     std::vector<ResultBatch> per(sinks_.size());
     std::vector<int> taken;
@@ -671,6 +672,7 @@ class Loop {
   }
 
   void run() {
+    prof_thread();
     setup();
     if (++g_ready == cfg_.threads && !cfg_.ready_file.empty()) {
       FILE* f = fopen(cfg_.ready_file.c_str(), "w");  // supervisor: this generation is serving
