@@ -41,6 +41,9 @@ struct KParams {
   TagSet ts;
   int npat;
   int32_t pat_E[2 * kMaxTags];  // Σ_j m(q0²+q1²) per pattern (match iff dot == -E)
+  // MFMA B operand (patterns × window features) per lane, built once on the host:
+  // lane l = pattern (l & 15), feature group (l >> 4): 0: -2·q0, 1: -2·q1, 2/3: mask
+  alignas(16) int8_t bfrag[64 * 16];
   uint32_t content_cap;
   int pre1_len, pre2_len, suf_len;
   char pre1[48];

@@ -197,22 +197,11 @@ __device__ inline int code_of(uint8_t b) {
   }
 }
 
-// B operand (patterns × window features), built once per wave: lane l = pattern (l&15),
-// feature group (l>>4): 0: -2·q0, 1: -2·q1, 2/3: mask (pairs with d0², d1² in A).
+// B operand (patterns × window features): host-built per lane (KParams::bfrag), one
+// 16-byte LDS read per lane instead of per-byte pattern decoding.
 __device__ inline v4i build_pattern_frag(const KParams& P) {
-  int l = threadIdx.x & 63, t = l & 15, kg = l >> 4;
-  int8_t bytes[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    int v = 0;
-    if (t < P.npat && j < pattern_len(P.ts, t)) {
-      int q = code_of(pattern_byte(P.ts, t, j));
-      v = kg == 0 ? -2 * (q & 7) : kg == 1 ? -2 * (q >> 3) : 1;
-    }
-    bytes[j] = (int8_t)v;
-  }
   v4i b;
-  __builtin_memcpy(&b, bytes, 16);
+  __builtin_memcpy(&b, &P.bfrag[(threadIdx.x & 63) * 16], 16);
   return b;
 }
 
@@ -222,10 +211,19 @@ __device__ inline void mfma_match_group(const uint8_t* Z, int Zn, const uint16_t
   int l = threadIdx.x & 63, r = l & 15, kg = l >> 4;
   int c = g * 16 + r;
   int p = c < ncand ? (int)cand[c] : -1;
+  // the 16-byte window from two aligned-word LDS reads (Z is 8-byte aligned with >= 24
+  // readable bytes past Zn), bytes past Zn get code 0
+  uint64_t w0 = 0, w1 = 0;
+  const int nv = p >= 0 ? min(16, Zn - p) : 0;
+  if (nv > 0) {
+    w0 = lds_window8(Z, p, Zn);
+    w1 = lds_window8(Z, p + 8, Zn);
+  }
   int8_t bytes[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    int code = (p >= 0 && p + j < Zn) ? code_of(Z[p + j]) : 0;
+    const uint8_t zb = (uint8_t)((j < 8 ? w0 : w1) >> ((j & 7) * 8));
+    int code = j < nv ? code_of(zb) : 0;
     int d0 = code & 7, d1 = code >> 3;
     bytes[j] = (int8_t)(kg == 0 ? d0 : kg == 1 ? d1 : kg == 2 ? d0 * d0 : d1 * d1);
   }
@@ -395,10 +393,11 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     int flen = in_len - start;
     int C = (flen + BS - 1) / BS;
     int lo = min(start + tid * C, in_len), hi = min(lo + C, in_len);
+    const uint8_t* rd = s.A;  // independent byte reads pipeline (a cached-word reader measured slower)
     bool all_nl = true;
     int trail = 0;
     for (int p = lo; p < hi; ++p) {
-      if (s.A[p] == '\n') ++trail;
+      if (rd[p] == '\n') ++trail;
       else { trail = 0; all_nl = false; }
     }
     int2 run = all_nl ? make_int2(1, hi - lo) : make_int2(0, trail);
@@ -407,8 +406,8 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     int r = ex.y;
     int cnt = 0;
     for (int p = lo; p < hi; ++p) {
-      if (s.A[p] == '\n') {
-        if (!(r & 1) && p + 1 < in_len && s.A[p + 1] == '\n') ++cnt;
+      if (rd[p] == '\n') {
+        if (!(r & 1) && p + 1 < in_len && rd[p + 1] == '\n') ++cnt;
         ++r;
       } else {
         r = 0;
@@ -418,8 +417,8 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     int k = block_excl_sum(cnt, s.scr, &nsep);
     r = ex.y;
     for (int p = lo; p < hi; ++p) {
-      if (s.A[p] == '\n') {
-        if (!(r & 1) && p + 1 < in_len && s.A[p + 1] == '\n') {
+      if (rd[p] == '\n') {
+        if (!(r & 1) && p + 1 < in_len && rd[p + 1] == '\n') {
           if (k < MAX_EV) s.ev_b[k] = (uint16_t)p;
           if (k + 1 < MAX_EV) s.ev_a[k + 1] = (uint16_t)(p + 2);
           atomicMax(&s.v[V_LASTSEP], p);
@@ -1320,6 +1319,22 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
     base_params_.pat_E[p] = E;
   }
   base_params_.content_cap = content_cap_;
+  auto code_host = [](uint8_t b) {
+    return (b >= 'a' && b <= 'z') ? b - 'a' + 1 : (b >= 'A' && b <= 'Z') ? b - 'A' + 1
+           : (b >= '0' && b <= '9') ? 27 + b - '0' : b == '<' ? 37 : b == '/' ? 38 : b == '>' ? 39
+           : b == '_' ? 40 : b == '-' ? 41 : b == ':' ? 42 : 63;
+  };
+  for (int l = 0; l < 64; ++l) {
+    const int t = l & 15, kg = l >> 4;
+    for (int j = 0; j < 16; ++j) {
+      int v = 0;
+      if (t < base_params_.npat && j < pattern_len(ts_, t)) {
+        const int q = code_host(pattern_byte(ts_, t, j));
+        v = kg == 0 ? -2 * (q & 7) : kg == 1 ? -2 * (q >> 3) : 1;
+      }
+      base_params_.bfrag[l * 16 + j] = (int8_t)v;
+    }
+  }
   for (int i = 0; i < std::max(1, lanes); ++i) {
     std::unique_ptr<TickLane> L(new TickLane());
     HIP_CHECK(hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking));
