@@ -959,6 +959,23 @@ class Loop {
       flushq_.push_back(c->fd);
     }
   }
+  // HTTP chunk framing appended straight into the corked output (no temporary string)
+  void write_chunk(Client* c, const std::string& data) {
+    if (c->dead || data.empty()) return;
+    if (c->out.size() == c->out_off) {
+      c->out.clear();
+      c->out_off = 0;
+    }
+    char h[24];
+    const int n = snprintf(h, sizeof(h), "%zx\r\n", data.size());
+    c->out.append(h, n);
+    c->out += data;
+    c->out.append("\r\n", 2);
+    if (!c->queued && !c->want_out) {
+      c->queued = true;
+      flushq_.push_back(c->fd);
+    }
+  }
   void flush_queued() {
     std::vector<int> fds;
     fds.swap(flushq_);
@@ -1615,7 +1632,7 @@ class Loop {
 
   // ---------------------------------------------------------------- parallel streaming
   void send_chunk(Session* s, const std::string& data) {
-    if (s->cl) write_client(s->cl, chunk(data));
+    if (s->cl) write_chunk(s->cl, data);
   }
   // content-bearing events: the first one closes the session's TTFT span
   void send_content(Session* s, const std::string& data) {

@@ -76,15 +76,28 @@ def _props(path: Path) -> Dict[str, int]:
     return out
 
 
-def gpu_links(root: Path = KFD_TOPOLOGY) -> List[Link]:
-    """Direct GPU↔GPU links (CPU nodes and GPU↔CPU links are left out)."""
+def _gpu_nodes(root: Path) -> Dict[int, int]:
+    """KFD node id -> GPU index (KFD node order = HIP device order; CPU nodes have no SIMDs)."""
     if not root.is_dir():
-        return []
+        return {}
     nodes = sorted((p for p in root.iterdir() if p.name.isdigit()), key=lambda p: int(p.name))
     gpu_of: Dict[int, int] = {}
     for p in nodes:
-        if _props(p / "properties").get("simd_count", 0) > 0:  # CPU nodes have no SIMDs
+        if _props(p / "properties").get("simd_count", 0) > 0:
             gpu_of[int(p.name)] = len(gpu_of)
+    return gpu_of
+
+
+def gpu_count(root: Path = KFD_TOPOLOGY) -> int:
+    return len(_gpu_nodes(root))
+
+
+def gpu_links(root: Path = KFD_TOPOLOGY) -> List[Link]:
+    """Direct GPU↔GPU links (CPU nodes and GPU↔CPU links are left out)."""
+    gpu_of = _gpu_nodes(root)
+    if not gpu_of:
+        return []
+    nodes = sorted((p for p in root.iterdir() if p.name.isdigit()), key=lambda p: int(p.name))
     links: List[Link] = []
     for p in nodes:
         src = int(p.name)
@@ -103,12 +116,16 @@ def gpu_links(root: Path = KFD_TOPOLOGY) -> List[Link]:
     return links
 
 
-def summary(links: Optional[List[Link]] = None) -> Dict[str, object]:
-    """Per-GPU direct-link counts by kind, and whether the GPUs form a full xGMI mesh."""
-    links = gpu_links() if links is None else links
-    gpus = sorted({x.src for x in links} | {x.dst for x in links})
-    per: Dict[int, Dict[str, int]] = {g: {} for g in gpus}
+def summary(links: Optional[List[Link]] = None, n_gpus: Optional[int] = None,
+            root: Path = KFD_TOPOLOGY) -> Dict[str, object]:
+    """GPU count, per-GPU direct-link counts by kind, and whether the GPUs form a full xGMI
+    mesh (a single GPU trivially does)."""
+    links = gpu_links(root) if links is None else links
+    if n_gpus is None:
+        n_gpus = gpu_count(root) if root.is_dir() else len({x.src for x in links} | {x.dst for x in links})
+    per: Dict[int, Dict[str, int]] = {g: {} for g in range(n_gpus)}
     for x in links:
+        per.setdefault(x.src, {})
         per[x.src][x.kind] = per[x.src].get(x.kind, 0) + 1
-    full = bool(gpus) and all(per[g].get("xgmi", 0) >= len(gpus) - 1 for g in gpus)
-    return {"gpus": len(gpus), "links_per_gpu": per, "full_xgmi_mesh": full}
+    full = n_gpus > 0 and all(per[g].get("xgmi", 0) >= n_gpus - 1 for g in range(n_gpus))
+    return {"gpus": n_gpus, "links_per_gpu": per, "full_xgmi_mesh": full}

@@ -38,15 +38,18 @@ def test_kfd_full_xgmi_mesh(tmp_path):
     _fake_kfd(tmp_path, 8)
     links = topology.gpu_links(tmp_path)
     assert len(links) == 8 * 7 and {x.kind for x in links} == {"xgmi"}
-    s = topology.summary(links)
+    assert topology.gpu_count(tmp_path) == 8
+    s = topology.summary(root=tmp_path)
     assert s["gpus"] == 8 and s["full_xgmi_mesh"] and s["links_per_gpu"][0] == {"xgmi": 7}
 
 
 def test_kfd_pcie_only_and_missing(tmp_path):
-    _fake_kfd(tmp_path, 2, kind=2)
-    assert not topology.summary(topology.gpu_links(tmp_path))["full_xgmi_mesh"]
+    _fake_kfd(tmp_path / "two", 2, kind=2)
+    assert not topology.summary(root=tmp_path / "two")["full_xgmi_mesh"]
+    _fake_kfd(tmp_path / "one", 1)
+    assert topology.summary(root=tmp_path / "one") == {"gpus": 1, "links_per_gpu": {0: {}}, "full_xgmi_mesh": True}
     assert topology.gpu_links(tmp_path / "nope") == []
-    assert topology.summary([]) == {"gpus": 0, "links_per_gpu": {}, "full_xgmi_mesh": False}
+    assert topology.summary(root=tmp_path / "nope") == {"gpus": 0, "links_per_gpu": {}, "full_xgmi_mesh": False}
 
 
 def test_exchange_settings_agree_across_ranks():
