@@ -262,6 +262,8 @@ struct Client {
   bool dead = false;         // error: close now
   bool close_after = false;  // graceful: close once output is flushed
   bool queued = false;       // in the loop's end-of-iteration flush list
+  int served = 0;            // requests handled on this connection
+  double t_accept = 0;
   bool want_out = false;     // EPOLLOUT armed (socket buffer was full)
 };
 
@@ -873,6 +875,7 @@ class Loop {
       draining_ = true;
       drain_deadline_ = t + cfg_.drain_s;
       if (lfd_ >= 0) {
+        on_accept();  // connections already queued on this listener are served, not reset
         epoll_ctl(ep_, EPOLL_CTL_DEL, lfd_, nullptr);
         close(lfd_);
         lfd_ = -1;
@@ -880,7 +883,10 @@ class Loop {
     }
     for (auto& kv : clients_) {
       Client* c = kv.second.get();
-      if (!c->sess && c->in.empty() && c->out_off >= c->out.size()) mark_close(c);
+      // idle keep-alive connections close; a connection accepted but whose request has not
+      // arrived yet gets a grace period (closing it would drop that request)
+      const bool idle = !c->sess && c->in.empty() && c->out_off >= c->out.size();
+      if (idle && (c->served > 0 || t - c->t_accept > 1.0)) mark_close(c);
     }
     if (!flushq_.empty()) flush_queued();
     if (!pending_close_.empty()) reap_clients();
@@ -896,6 +902,7 @@ class Loop {
       setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
       auto c = std::make_unique<Client>();
       c->fd = fd;
+      c->t_accept = now_s();
       add(fd, EPOLLIN, tag(3, fd));
       clients_[fd] = std::move(c);
       c_clients++;
@@ -1122,6 +1129,7 @@ class Loop {
       return respond(c, 404, "application/json", "{\"detail\":\"Not Found\"}");
     if (method != "POST") return respond(c, 405, "application/json", "{\"detail\":\"Method Not Allowed\"}");
     c_requests++;
+    c->served++;
     auto s = std::make_unique<Session>();
     s->t0 = now_s();
     std::string perr;
