@@ -207,13 +207,19 @@ def main() -> int:
     import torch
 
     use_cuda = torch.cuda.is_available()
+    n_dev = torch.cuda.device_count() if use_cuda else 0
+    # one rank per GPU (the driver's node runs); a rehearsal with more ranks than GPUs maps
+    # ranks onto the visible GPUs and keeps the bench's own bookkeeping group on gloo (RCCL
+    # refuses two ranks on one GPU)
+    device = local_rank % n_dev if n_dev else None
+    coll_cuda = use_cuda and n_dev >= world
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
 
-        dist.init_process_group("nccl" if use_cuda else "gloo")
+        dist.init_process_group("nccl" if coll_cuda else "gloo")
     if use_cuda:
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(device)
     engine = args.engine
     if engine == "auto":
         engine = "hip" if use_cuda else "cpu"
@@ -244,7 +250,7 @@ def main() -> int:
             env.update(exchange_env(rank, world, args.port, nonce[0]))
         mock_procs = list(procs)
         proxy_procs = spawn_workers(cfg_path, "127.0.0.1", args.port, args.workers, engine,
-                               local_rank if use_cuda else None, impl=args.impl, threads=args.threads, env=env)
+                               device, impl=args.impl, threads=args.threads, env=env)
         procs += proxy_procs
         if not wait_healthy("127.0.0.1", args.port, 180):
             raise RuntimeError("proxy did not become healthy")
@@ -272,7 +278,7 @@ def main() -> int:
         local = [elapsed, float(stats["completed"]), float(stats["ttft_p50_ms"]), float(stats["ttft_p99_ms"]),
                  float(stats["errors"] + stats["non200"]), float(stats["ttfb_p50_ms"]), float(stats["lat_p50_ms"])]
         if dist is not None:
-            t = torch.tensor(local, dtype=torch.float64, device="cuda" if use_cuda else "cpu")
+            t = torch.tensor(local, dtype=torch.float64, device="cuda" if coll_cuda else "cpu")
             gathered = [torch.zeros_like(t) for _ in range(world)]
             dist.all_gather(gathered, t)
             rows = [g.cpu().tolist() for g in gathered]
