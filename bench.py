@@ -70,6 +70,18 @@ def _kill(procs):
                 pass
 
 
+def available_cores() -> int:
+    """CPU cores this job may use: the cgroup CPU quota if one is set, else the affinity set
+    (``nproc`` on a GPU box shows the whole machine)."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    return len(os.sched_getaffinity(0))
+
+
 def write_config(path: str, mock_ports, skip_final: bool, tile: int, sc=None, placement="local") -> None:
     import yaml
 
@@ -186,7 +198,9 @@ def main() -> int:
     ap.add_argument("--impl", default=os.environ.get("QMX_BENCH_IMPL", "native"), choices=["native", "python"])
     ap.add_argument("--engine", default=os.environ.get("QMX_BENCH_ENGINE", "auto"))
     ap.add_argument("--workers", type=int, default=4, help="python impl: proxy processes per rank")
-    ap.add_argument("--threads", type=int, default=8, help="native impl: io threads per rank")
+    ap.add_argument("--threads", type=int, default=0,
+                    help="native impl: io threads per rank (0: min(8, cores / (2 x ranks)), at least 2 — "
+                         "the node's cores are shared by every rank's proxy, mocks and load generator)")
     ap.add_argument("--lg-threads", type=int, default=2)
     ap.add_argument("--mock-threads", type=int, default=2)
     ap.add_argument("--skip-final", type=int, default=1)
@@ -203,6 +217,8 @@ def main() -> int:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.threads <= 0:
+        args.threads = max(2, min(8, available_cores() // (2 * world)))
 
     import torch
 
@@ -254,6 +270,7 @@ def main() -> int:
         procs += proxy_procs
         if not wait_healthy("127.0.0.1", args.port, 180):
             raise RuntimeError("proxy did not become healthy")
+        xchg_kind = os.environ.get("QMX_XCHG", "rccl" if engine == "hip" else "tcp")
         if dist is not None:
             dist.barrier()
         # warmup
@@ -308,9 +325,10 @@ def main() -> int:
                            "global_batch": args.batch * world, "seq_len": 26,
                            "parallelism": f"dp{world} (sessions sharded over GPUs via SO_REUSEPORT)"
                                           + (f" + ep{world} (backend streams spread over ranks, "
-                                                f"{'RCCL' if engine == 'hip' else 'TCP'} all-gather exchange)"
+                                                f"{xchg_kind.upper()} all-gather exchange)"
                                              if args.placement == "spread" and world > 1 else ""),
                            "impl": args.impl, "engine": engine, "conns_per_rank": args.conns,
+                           "io_threads_per_rank": args.threads,
                            "gpu_links": {k: v for k, v in link_summary().items() if k != "links_per_gpu"}},
                 "p50_ttft_ms": round(p50, 3),
                 "p99_ttft_ms": round(max(r[3] for r in rows), 3),
