@@ -47,6 +47,13 @@ SCENARIOS = {
                     faults={1: ["--fail-rate", "0.3", "--drop-rate", "0.2", "--null-rate", "0.1"]},
                     baseline=6.9, desc="2 mock backends, backend 2 injects 30% HTTP 500 / 20% mid-stream "
                                        "disconnect / 10% content:null; 2 s timeout"),
+    # steady-state serving shape: backends pace their events (10 ms apart, like a decoding
+    # LLM), many concurrent sessions, each tick sees a few events of many streams.  TTFT is
+    # bounded below by the mock's own first-content time (5 events x 10 ms = 50 ms).
+    "paced": dict(n=2, strategy="concatenate", hide_final=False, skip=True, faults={}, timeout=30,
+                  mock_args=["--delay-us", "10000"], conns=1024, baseline=None,
+                  desc="2 mock backends pacing events 10 ms apart (first content at 50 ms), 1024 sessions "
+                       "in flight, streaming concatenate + hide_intermediate_think"),
 }
 
 
@@ -212,6 +219,8 @@ def main() -> int:
                     help="spread: a session's backend streams run on consecutive ranks (RCCL exchange)")
     args = ap.parse_args()
     sc = SCENARIOS[args.scenario]
+    if "conns" in sc and args.conns == 64:  # scenario default unless set explicitly
+        args.conns = sc["conns"]
     skip_final = bool(args.skip_final) if args.scenario == "headline" else sc["skip"]
 
     rank = int(os.environ.get("RANK", "0"))
@@ -255,7 +264,7 @@ def main() -> int:
         for i, p in enumerate(mock_ports):
             procs.append(subprocess.Popen([os.path.join(bin_dir, "qmx_mock"), "--port", str(p), "--threads",
                                            str(args.mock_threads), "--tokens", "20", "--think", "1"]
-                                          + sc["faults"].get(i, []),
+                                          + sc.get("mock_args", []) + sc["faults"].get(i, []),
                                           stderr=subprocess.DEVNULL, start_new_session=True))
         cfg_path = os.path.join(tmp, "config.yaml")
         write_config(cfg_path, mock_ports, skip_final, args.tile, sc, args.placement)
@@ -317,7 +326,7 @@ def main() -> int:
                 "ms_per_step": round(1000.0 * max_el / args.steps, 3),
                 "higher_is_better": True,
                 "scaling": "weak",
-                "vs_baseline": round(value / sc["baseline"], 3),
+                "vs_baseline": round(value / sc["baseline"], 3) if sc["baseline"] else None,
                 "dtype": "bytes (utf-8 SSE text; no float compute)",
                 "data": "synthetic: C++ mock backends (role + 4 split <think> fragments + 20 tokens + stop + "
                         "[DONE]) and C++ closed-loop load generator",

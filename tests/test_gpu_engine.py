@@ -261,3 +261,19 @@ def test_hip_two_lanes_concurrent(ext):
     st = hip._e.kernel_stats()
     assert st["lanes"] == 2 and st["launches"] >= 2, st
     assert lanes_seen == {0, 1}
+
+
+def test_hip_completion_modes(ext, monkeypatch):
+    """Tick completion by polling the kernel-published sequence numbers (default) must never
+    need the event fallback; the blocking-event mode (QMX_WAIT=event) gives the same bytes."""
+    _check(7001, 40)
+    eng = _hip(["think"])
+    slot = eng.open(0, True, True)
+    for i in range(20):
+        eng.feed(slot, H.event_bytes(random.Random(i), "x<think>y</think>z" * (i % 3)))
+        eng.tick(H.CREATED)
+    st = eng._e.kernel_stats()
+    assert st["launches"] >= 10 and st["poll_fallbacks"] == 0, st
+    eng.release(slot)
+    monkeypatch.setenv("QMX_WAIT", "event")
+    _check(7002, 40)
