@@ -11,11 +11,12 @@
 #pragma once
 #include <stdint.h>
 
-#include <deque>
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <stdexcept>
 #include <unordered_set>
 #include <vector>
 
@@ -92,6 +93,30 @@ struct FinalizeRes {
   std::vector<std::string> texts;
 };
 
+// Append-only slot table with stable element addresses AND a never-moving index: chunks
+// of 256 elements hang off a fixed pointer table, so a tick lane can index slot i
+// (operator[]) while an io loop appends under the engine lock (a std::deque's block map
+// may be reallocated by push_back underneath a concurrent reader).
+template <class T>
+class SlotTable {
+ public:
+  static constexpr int kShift = 8, kChunk = 1 << kShift, kMaxChunks = 4096;  // 1M slots
+  SlotTable() : chunks_(new std::unique_ptr<T[]>[kMaxChunks]) {}
+  T& operator[](size_t i) { return chunks_[i >> kShift][i & (kChunk - 1)]; }
+  const T& operator[](size_t i) const { return chunks_[i >> kShift][i & (kChunk - 1)]; }
+  size_t size() const { return n_.load(std::memory_order_acquire); }
+  void emplace_back() {  // caller serialises appends
+    const size_t n = n_.load(std::memory_order_relaxed);
+    if ((n >> kShift) >= (size_t)kMaxChunks) throw std::length_error("slot table full");
+    if ((n & (kChunk - 1)) == 0) chunks_[n >> kShift].reset(new T[kChunk]());
+    n_.store(n + 1, std::memory_order_release);
+  }
+
+ private:
+  std::unique_ptr<std::unique_ptr<T[]>[]> chunks_;
+  std::atomic<size_t> n_{0};
+};
+
 class HostEngine {
  public:
   explicit HostEngine(const std::vector<std::string>& tags);
@@ -147,14 +172,10 @@ class HostEngine {
 
   TagSet ts_;
   std::mutex mu_;
-  // deques: open() appends under mu_ while tick lanes hold references to other slots'
-  // entries outside the lock (a vector would reallocate under them)
-  std::deque<Meta> meta_;
-  std::deque<SlotCore> core_;  // host state (CPU engine; HIP engine: flags + fallback)
-  size_t nslots() {
-    std::lock_guard<std::mutex> g(mu_);
-    return core_.size();
-  }
+  // open() appends under mu_ while tick lanes index other slots outside the lock
+  SlotTable<Meta> meta_;
+  SlotTable<SlotCore> core_;  // host state (CPU engine; HIP engine: flags + fallback)
+  size_t nslots() const { return core_.size(); }
   std::vector<int> free_, pending_free_;
   std::vector<int> dirty_;
   std::vector<FinalizeReq> fin_;
