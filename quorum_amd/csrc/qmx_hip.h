@@ -24,6 +24,8 @@ struct WorkItem {
 struct WorkResult {
   uint32_t consumed, out_len, status, content_len;
   uint32_t seq;  // written last (system-scope release): the lane's tick sequence number
+  uint32_t pad;
+  uint64_t t0, t1;  // s_memrealtime (100 MHz) at workgroup start / end: kernel span per tick
 };
 constexpr int kTplBytes = 320;  // per-stream event shape template (qmx_lex.h TPL_*)
 struct DevSlot {

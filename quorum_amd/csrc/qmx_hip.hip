@@ -1013,7 +1013,12 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
                                                       const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                       WorkResult* __restrict__ res, DevSlot* __restrict__ state,
                                                       uint8_t* __restrict__ content, KParams Pk, uint32_t seq) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   tick_body(items, in, out, res, state, content, Pk);
+  if (threadIdx.x == 0) {
+    res[blockIdx.x].t0 = t0;
+    res[blockIdx.x].t1 = __builtin_amdgcn_s_memrealtime();
+  }
   __threadfence_system();
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(&res[blockIdx.x].seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1247,7 +1252,7 @@ void HipEngine::wait_stream(TickLane& L) {
 
 // Results published by the tick kernel itself (qmx_tick_kernel's sequence numbers): sleep
 // most of the expected kernel time (EMA), then poll every poll_us_ with a 1 us timer slack.
-// A launch that has not published after 4x the EMA + 2 ms waits on its event (surfaces a
+// A launch that has not published after 4x the EMA + 2 ms synchronises its stream (surfaces a
 // fault; correct even if host-mapped visibility misbehaved: counted in poll_fallbacks).
 void HipEngine::wait_results(TickLane& L, int n, uint32_t seq) {
   using HC = std::chrono::steady_clock;
@@ -1268,7 +1273,7 @@ void HipEngine::wait_results(TickLane& L, int n, uint32_t seq) {
   while (!done(i)) {
     const double el = std::chrono::duration<double, std::micro>(HC::now() - t0).count();
     if (el > 4.0 * L.ema_us + 2000.0) {
-      HIP_CHECK(hipEventSynchronize(L.ev1));  // throws on a kernel fault
+      HIP_CHECK(hipStreamSynchronize(L.stream));  // throws on a kernel fault
       ++L.poll_fallbacks;
       break;  // the stream has drained: every result is final
     }
@@ -1545,17 +1550,22 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
     L.host_prep_us += std::chrono::duration<double, std::micro>(tp1 - tp0).count();
     roctxRangePushA("qmx_tick");  // rocprofv3 --marker-trace: one range per tick launch + wait
     L.h2d_bytes += in_off;
-    collect_timing(L);  // the previous launch's kernel time (its events are reused now)
-    HIP_CHECK(hipEventRecord(L.ev0, L.stream));
     const uint32_t seq = ++L.seq;
+    if (!poll_) HIP_CHECK(hipEventRecord(L.ev0, L.stream));
     hipLaunchKernelGGL(qmx_tick_kernel, dim3(n), dim3(BS), 0, L.stream, L.h_items, L.h_in, L.h_out, L.h_res, d_state_,
                        d_content_, L.params, seq);
     HIP_CHECK(hipGetLastError());
-    HIP_CHECK(hipEventRecord(L.ev1, L.stream));
     if (poll_) {
+      // one HIP call per tick: completion and kernel span both come from the result records
       wait_results(L, n, seq);
-      L.timing_pending = true;
+      uint64_t a = ~0ull, b = 0;
+      for (int i = 0; i < n; ++i) {
+        a = std::min(a, L.h_res[i].t0);
+        b = std::max(b, L.h_res[i].t1);
+      }
+      if (b > a) L.kernel_ms += (double)(b - a) * 1e-5;  // 100 MHz ticks -> ms
     } else {
+      HIP_CHECK(hipEventRecord(L.ev1, L.stream));
       wait_stream(L);
       L.timing_pending = true;
       collect_timing(L);
