@@ -35,7 +35,7 @@ struct ServerCfg {
   // engine
   std::string engine = "cpu";
   int shared_engine = -1;  // one engine per process shared by all io loops (-1: auto = hip only)
-  int tick_lanes = 1;      // shared engine: tick threads, each with its own HIP stream + arenas
+  int tick_lanes = 2;      // shared engine: tick threads, each with its own HIP stream + arenas
   int device = 0;
   int tile = 16384, max_slots = 4096, content_cap = 1 << 20;
   // config

@@ -233,7 +233,7 @@ class RuntimeConfig:
     drain_timeout: float = 10.0
     verify: bool = False
     shared_engine: Any = "auto"
-    tick_lanes: int = 1
+    tick_lanes: int = 2
     log_content: bool = False
 
     @classmethod

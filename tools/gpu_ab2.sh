@@ -13,7 +13,7 @@ run() {  # name, env..., args
   python3 -c "import json,sys; d=json.load(open('$OUT/$name.json')); b=d['breakdown_one_rank']; print('$name', d['value'], d['p50_ttft_ms'], d['p99_ttft_ms'], b.get('streams_per_tick'), b.get('tick_wall_us_avg'), b.get('tick_kernel_us_avg'), b.get('tick_host_prep_us_avg'), b.get('tick_launch_wait_us_avg'), b.get('tick_process_us_avg'), b.get('proxy_cpu_ms_per_1k_req'))"
 }
 for rep in 1 2 3; do
-  run hip_$rep python bench.py --steps 10 --warmup 2 || exit 1
+  run hip_$rep python bench.py --steps 10 --warmup 2 && run hip_l2_$rep QMX_TICK_LANES=2 python bench.py --steps 10 --warmup 2 || exit 1
   if [ $rep -le 2 ]; then run cpu_$rep python bench.py --engine cpu --steps 10 --warmup 2 || exit 1; fi
 done
 run prof QMX_PROF=$PWD/$OUT/cpu_hip.%p.txt python bench.py --steps 30 --warmup 2 || exit 1
