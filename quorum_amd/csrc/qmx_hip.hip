@@ -712,55 +712,95 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     }
     __syncthreads();
     QMX_STAMP(6);
-    // token compaction (4 candidates per thread)
-    {
-      int loc = 0, flags[4];
+    if (ncand <= 64) {
+      // common case (a few '<' in the tile): wave 0 alone compacts the tokens by ballot and
+      // runs the depth scan with wave shuffles — one barrier instead of five.  Candidates
+      // are in position order and non-tokens are the scan identity (0,0), so the lane-order
+      // exclusive prefix at a token lane is its depth before the token.
+      if (tid < 64) {
+        const int lane = tid;
+        const int id = lane < ncand ? (int)s.cand_tok[lane] : 0;
+        const uint64_t m = __ballot(id != 0);
+        const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+        const int k = __popcll(m & below);
+        DepthOp op;
+        int2 x = id > 0 ? make_int2(1, 1) : id < 0 ? make_int2(-1, 0) : make_int2(0, 0);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        int c = tid * 4 + i;
-        flags[i] = loc;
-        loc += (c < ncand && s.cand_tok[c] != 0) ? 1 : 0;
-      }
-      int tot;
-      int base = block_excl_sum(loc, s.scr, &tot);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        int c = tid * 4 + i;
-        if (c < ncand && s.cand_tok[c] != 0) {
-          int k = base + flags[i];
-          int id = s.cand_tok[c];
-          s.tok_pos[k] = s.cand[c];
+        for (int o = 1; o < 64; o <<= 1) {
+          int2 y;
+          y.x = __shfl_up(x.x, o, 64);
+          y.y = __shfl_up(x.y, o, 64);
+          if (lane >= o) x = op(y, x);
+        }
+        int2 ex;
+        ex.x = __shfl_up(x.x, 1, 64);
+        ex.y = __shfl_up(x.y, 1, 64);
+        if (lane == 0) ex = make_int2(0, 0);
+        if (id != 0) {
+          s.tok_pos[k] = s.cand[lane];
           s.tok_id[k] = (int8_t)id;
           s.tok_len[k] = (uint8_t)tok_plen(P, id);
+          s.tok_dep[k] = (int16_t)max(depth0 + ex.x, ex.y);
+        }
+        if (lane == 63) {
+          const int nt = __popcll(m);
+          s.v[V_NTOK] = nt;
+          s.tok_dep[nt] = (int16_t)max(depth0 + x.x, x.y);
         }
       }
-      ntok = tot;
-    }
-    __syncthreads();
-    // depth scan over tokens: open (1,1), close (-1,0)
-    {
-      int2 loc = make_int2(0, 0);
-      int2 pre[4];
-      DepthOp op;
+      __syncthreads();
+      ntok = s.v[V_NTOK];
+    } else {
+      // token compaction (4 candidates per thread)
+      {
+        int loc = 0, flags[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        int k = tid * 4 + i;
-        pre[i] = loc;
-        if (k < ntok) loc = op(loc, s.tok_id[k] > 0 ? make_int2(1, 1) : make_int2(-1, 0));
-      }
-      int2 tot;
-      int2 base = block_excl_pair(loc, make_int2(0, 0), op, s.scr, &tot);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        int k = tid * 4 + i;
-        if (k < ntok) {
-          int2 f = op(base, pre[i]);
-          s.tok_dep[k] = (int16_t)max(depth0 + f.x, f.y);
+        for (int i = 0; i < 4; ++i) {
+          int c = tid * 4 + i;
+          flags[i] = loc;
+          loc += (c < ncand && s.cand_tok[c] != 0) ? 1 : 0;
         }
+        int tot;
+        int base = block_excl_sum(loc, s.scr, &tot);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          int c = tid * 4 + i;
+          if (c < ncand && s.cand_tok[c] != 0) {
+            int k = base + flags[i];
+            int id = s.cand_tok[c];
+            s.tok_pos[k] = s.cand[c];
+            s.tok_id[k] = (int8_t)id;
+            s.tok_len[k] = (uint8_t)tok_plen(P, id);
+          }
+        }
+        ntok = tot;
       }
-      if (tid == 0) s.tok_dep[ntok] = (int16_t)max(depth0 + tot.x, tot.y);
+      __syncthreads();
+      // depth scan over tokens: open (1,1), close (-1,0)
+      {
+        int2 loc = make_int2(0, 0);
+        int2 pre[4];
+        DepthOp op;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          int k = tid * 4 + i;
+          pre[i] = loc;
+          if (k < ntok) loc = op(loc, s.tok_id[k] > 0 ? make_int2(1, 1) : make_int2(-1, 0));
+        }
+        int2 tot;
+        int2 base = block_excl_pair(loc, make_int2(0, 0), op, s.scr, &tot);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          int k = tid * 4 + i;
+          if (k < ntok) {
+            int2 f = op(base, pre[i]);
+            s.tok_dep[k] = (int16_t)max(depth0 + f.x, f.y);
+          }
+        }
+        if (tid == 0) s.tok_dep[ntok] = (int16_t)max(depth0 + tot.x, tot.y);
+      }
+      __syncthreads();
     }
-    __syncthreads();
     // cuts per delta + new tail
     for (int j = tid; j < ndelta; j += BS) {
       int q;
