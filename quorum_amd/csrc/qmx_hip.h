@@ -91,6 +91,7 @@ struct TickLane {
   // counters (summed over lanes by kernel_stats)
   uint64_t launches = 0, items = 0, h2d_bytes = 0, d2h_bytes = 0;
   uint64_t s3_full = 0, s3_tpl = 0, s3_events = 0, stage_n = 0;  // QMX_STAGE_TIMING: S3 path counters
+  uint64_t s3_cyc_full = 0, s3_cyc_tpl = 0, s3_cyc_lex = 0;  // S3 wave cycles: full parse / templates / lexer
   double kernel_ms = 0.0, host_prep_us = 0, gpu_wait_us = 0, process_us = 0;  // host-side tick breakdown
   double stage_us[16] = {0};
   double clk_cycles = 0, clk_us = 0;

@@ -54,7 +54,8 @@ constexpr int TILE_MAX = 16384;
 constexpr int MAX_EV = 512;  // events per tile (more → WS_MORE requeue); keeps LDS < 80 KiB (2 WG/CU)
 constexpr int MAX_CAND = 1024;
 constexpr int PAD = 16;
-constexpr int TOK_CAP = 512;  // tokens per wave (an event with more → scalar fallback)
+constexpr int TOK_CAP = 512;
+constexpr int kDbg = 20;  // QMX_STAGE_TIMING record per work item: stamps 0-12, S3 counters 13-17  // tokens per wave (an event with more → scalar fallback)
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 
@@ -62,7 +63,7 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 #define QMX_STAMP(k)                                               \
   do {                                                             \
     if (Pk.dbg != nullptr && threadIdx.x == 0)                     \
-      Pk.dbg[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+      Pk.dbg[blockIdx.x * kDbg + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
 struct Smem {
@@ -92,7 +93,7 @@ static_assert(TPL_BYTES == kTplBytes, "template size");
 enum : int {
   V_START = 0, V_NSEP, V_LASTSEP, V_ABORT, V_NEV, V_CONSUMED, V_STATUS, V_NDELTA, V_YLEN, V_NCAND,
   V_NTOK, V_BAIL, V_DEPTH0, V_TAILLEN, V_NEWTAIL, V_NEWDEPTH, V_WLEN, V_NEMIT, V_ETOT, V_OUTLEN,
-  V_TPLPRE, V_TPLSUF, V_TPLK, V_NEXTEV, V_NFULL, V_NTPL
+  V_TPLPRE, V_TPLSUF, V_TPLK, V_NEXTEV, V_NFULL, V_NTPL, V_CFULL, V_CTPL, V_CLEX
 };
 
 // LDS byte reader that fetches one aligned 64-bit word per 8 sequential bytes: a byte-serial
@@ -312,7 +313,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   const int tid = threadIdx.x;
   for (int i = tid; i < (int)(sizeof(KParams) / 4); i += BS) ((uint32_t*)&P)[i] = ((const uint32_t*)&Pk)[i];
   QMX_STAMP(0);
-  if (Pk.dbg != nullptr && threadIdx.x == 0) Pk.dbg[blockIdx.x * 16 + 11] = __builtin_amdgcn_s_memtime();
+  if (Pk.dbg != nullptr && threadIdx.x == 0) Pk.dbg[blockIdx.x * kDbg + 11] = __builtin_amdgcn_s_memtime();
   const WorkItem it = items[blockIdx.x];
   const int in_len = (int)it.in_len;
   const bool eof = it.flags & WF_EOF;
@@ -330,7 +331,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     s.v[V_STATUS] = 0;
     s.v[V_TPLK] = -1;
     s.v[V_NEXTEV] = 0;
-    s.v[V_NFULL] = s.v[V_NTPL] = 0;
+    s.v[V_NFULL] = s.v[V_NTPL] = s.v[V_CFULL] = s.v[V_CTPL] = s.v[V_CLEX] = 0;
     for (int q = 0; q < BS / 64; ++q) wtpl[q][0] = -1;
     if (fresh) {
       s.v[V_DEPTH0] = 0;
@@ -500,6 +501,9 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       int kind = EV_SKIP, sa = 0, sb = 0, body = -1;
       bool slow = false, lexed = false;
       int nt = 0;
+      const bool probe = Pk.dbg != nullptr;
+      const uint64_t c0 = probe ? __builtin_amdgcn_s_memtime() : 0;
+      uint64_t c1 = 0;
       if (tp > 0 && e1 - e0 >= tp + ts && wave_tpl_match(s.A, e0, e1, s.tpl, tp, ts) &&
           (body = wave_str_body(s.A, e0 + tp, e1 - ts)) >= 0) {
         kind = EV_CONTENT;  // same shape as this stream's last parsed content event
@@ -521,11 +525,14 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
             if (lane == 0) atomicAdd(&s.v[V_NTPL], 1);
           }
         }
+        if (probe) c1 = __builtin_amdgcn_s_memtime();
         if (kind != EV_CONTENT && lit_at(s.A, e0, e1, QMX_LIT("data: "))) {
           int a = e0 + 6, b = e1;
           ustrip(s.A, &a, &b);
           if (!(b - a == 6 && lit_at(s.A, a, b, QMX_LIT("[DONE]")))) {
+            const uint64_t cl0 = probe ? __builtin_amdgcn_s_memtime() : 0;
             nt = wave_lex(s.A, a, b, TKP[w], TKT[w], 0, TOK_CAP);
+            if (probe && lane == 0) atomicAdd(&s.v[V_CLEX], (int)(__builtin_amdgcn_s_memtime() - cl0));
             if (lane == 0) atomicAdd(&s.v[V_NFULL], 1);
             if (nt == -LEX_COMPLEX) {
               slow = true;
@@ -555,6 +562,15 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
               }
             }
           }
+        }
+      }
+      if (probe && lane == 0) {
+        const uint64_t c2 = __builtin_amdgcn_s_memtime();
+        if (c1) {
+          atomicAdd(&s.v[V_CTPL], (int)(c1 - c0));
+          atomicAdd(&s.v[V_CFULL], (int)(c2 - c1));
+        } else {
+          atomicAdd(&s.v[V_CTPL], (int)(c2 - c0));
         }
       }
       if (lane == 0) {
@@ -1032,10 +1048,13 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   }
   QMX_STAMP(10);
   if (Pk.dbg != nullptr && threadIdx.x == 0) {
-    Pk.dbg[blockIdx.x * 16 + 12] = __builtin_amdgcn_s_memtime();
-    Pk.dbg[blockIdx.x * 16 + 13] = (unsigned long long)s.v[V_NFULL];  // S3: events fully parsed
-    Pk.dbg[blockIdx.x * 16 + 14] = (unsigned long long)s.v[V_NTPL];   // S3: template hits
-    Pk.dbg[blockIdx.x * 16 + 15] = (unsigned long long)nev;
+    Pk.dbg[blockIdx.x * kDbg + 12] = __builtin_amdgcn_s_memtime();
+    Pk.dbg[blockIdx.x * kDbg + 13] = (unsigned long long)s.v[V_NFULL];  // S3: events fully parsed
+    Pk.dbg[blockIdx.x * kDbg + 14] = (unsigned long long)s.v[V_NTPL];   // S3: template hits
+    Pk.dbg[blockIdx.x * kDbg + 15] = (unsigned long long)nev;
+    Pk.dbg[blockIdx.x * kDbg + 16] = (unsigned long long)s.v[V_CFULL];  // S3 cycles: full parses (sum over waves)
+    Pk.dbg[blockIdx.x * kDbg + 17] = (unsigned long long)s.v[V_CTPL];   // S3 cycles: template checks
+    Pk.dbg[blockIdx.x * kDbg + 18] = (unsigned long long)s.v[V_CLEX];   // S3 cycles: wave_lex part of full
   }
   if (tid == 0) {
     WorkResult r{(uint32_t)s.v[V_CONSUMED], (uint32_t)out_len, (uint32_t)s.v[V_STATUS], new_clen};
@@ -1581,9 +1600,9 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
       if (L.dbg_cap < (size_t)n) {
         if (L.h_dbg) hipHostFree(L.h_dbg);
         L.dbg_cap = std::max((size_t)n, L.items_cap);
-        HIP_CHECK(hipHostMalloc((void**)&L.h_dbg, sizeof(unsigned long long) * 16 * L.dbg_cap, hipHostMallocMapped));
+        HIP_CHECK(hipHostMalloc((void**)&L.h_dbg, sizeof(unsigned long long) * kDbg * L.dbg_cap, hipHostMallocMapped));
       }
-      std::memset(L.h_dbg, 0, sizeof(unsigned long long) * 16 * n);
+      std::memset(L.h_dbg, 0, sizeof(unsigned long long) * kDbg * n);
       L.params.dbg = L.h_dbg;
     }
     const auto tp1 = HC::now();
@@ -1616,7 +1635,7 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
     L.items += n;
     if (L.params.dbg) {
       for (int i = 0; i < n; ++i) {
-        const unsigned long long* d = L.h_dbg + 16 * i;
+        const unsigned long long* d = L.h_dbg + kDbg * i;
         if (d[12] > d[11] && d[10] > d[0]) {
           L.clk_cycles += (double)(d[12] - d[11]);
           L.clk_us += (double)(d[10] - d[0]) * 0.01;
@@ -1630,9 +1649,12 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
       }
       L.stage_n += n;
       for (int i = 0; i < n; ++i) {
-        L.s3_full += L.h_dbg[16 * i + 13];
-        L.s3_tpl += L.h_dbg[16 * i + 14];
-        L.s3_events += L.h_dbg[16 * i + 15];
+        L.s3_full += L.h_dbg[kDbg * i + 13];
+        L.s3_tpl += L.h_dbg[kDbg * i + 14];
+        L.s3_events += L.h_dbg[kDbg * i + 15];
+        L.s3_cyc_full += L.h_dbg[kDbg * i + 16];
+        L.s3_cyc_tpl += L.h_dbg[kDbg * i + 17];
+        L.s3_cyc_lex += L.h_dbg[kDbg * i + 18];
       }
     }
   }
@@ -1847,6 +1869,9 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["s3_full_parses"] += (double)L.s3_full;
     m["s3_template_hits"] += (double)L.s3_tpl;
     m["s3_events"] += (double)L.s3_events;
+    m["s3_cycles_full"] += (double)L.s3_cyc_full;
+    m["s3_cycles_template"] += (double)L.s3_cyc_tpl;
+    m["s3_cycles_lex"] += (double)L.s3_cyc_lex;
     m["host_prep_us"] += L.host_prep_us;
     m["gpu_wait_us"] += L.gpu_wait_us;
     m["process_us"] += L.process_us;
