@@ -20,6 +20,7 @@ import os
 from typing import Any, Dict, List, Optional
 
 from ..server.transport import UpstreamPool, call_backend
+from ..utils.logging_setup import log_content, redact
 from ..utils.config import (DEFAULT_PROMPT_TEMPLATE, DEFAULT_QUERY_FORMAT,
                             DEFAULT_SOURCE_LABEL_FORMAT, AggregateSettings)
 
@@ -98,10 +99,16 @@ async def aggregate_responses(
         return separator.join(source_responses)
     body = {"model": aggregator_backend.get("model", ""),
             "messages": [{"role": "user", "content": prompt}], "stream": False}
+    aggregation_logger.info("aggregator call to %s, headers %s", aggregator_backend.get("name"), redact(clean))
+    if log_content():
+        aggregation_logger.info("aggregator prompt: %s", prompt)
     try:
         res = await call_backend(aggregator_backend, json.dumps(body).encode(), clean, 60.0, pool=pool)
         if res["status_code"] == 200:
-            return res["content"]["choices"][0]["message"]["content"]
+            out = res["content"]["choices"][0]["message"]["content"]
+            if log_content():
+                aggregation_logger.info("aggregator result: %s", out)
+            return out
         aggregation_logger.error("aggregator backend failed: status %s", res["status_code"])
     except Exception as exc:  # noqa: BLE001
         aggregation_logger.error("error calling aggregator backend: %s", exc)

@@ -40,9 +40,13 @@ def run_worker(config: str, host: str, port: int, engine: str, device: Optional[
 
     from .server.app import create_app
     from .utils.config import RuntimeConfig, load_config
+    from .utils.logging_setup import from_env, set_log_content
 
+    from_env()
     cfg = load_config(config)
     rt = RuntimeConfig.from_config(cfg)
+    if rt.log_content:
+        set_log_content(True)
     if engine:
         rt.engine = engine
     if device is not None:

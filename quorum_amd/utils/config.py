@@ -218,6 +218,8 @@ class RuntimeConfig:
                engines for cpu) | true | false (QMX_SHARED_ENGINE=0/1)
     tick_lanes: shared engine: tick threads with a kernel in flight each (own HIP stream and
                arenas, disjoint stream sets) — QMX_TICK_LANES
+    log_content: allow prompts / per-backend answers in the ``aggregation`` log (off: user
+               data; see utils/logging_setup.py) — QMX_LOG_CONTENT
     """
 
     engine: str = "auto"
