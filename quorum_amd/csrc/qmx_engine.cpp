@@ -320,10 +320,13 @@ void HostEngine::release(int slot) {
   release_locked(slot);
 }
 
-void HostEngine::apply_ops(const std::vector<EngineOp>& ops) {
+void HostEngine::apply_ops(std::vector<EngineOp>& ops, bool move_data) {
   std::lock_guard<std::mutex> g(mu_);
   for (auto& op : ops) {
-    if (op.kind == EngineOp::FEED) feed_locked(op.slot, op.data);
+    if (op.kind == EngineOp::FEED) {
+      if (move_data) feed_locked_move(op.slot, op.data);
+      else feed_locked(op.slot, op.data);
+    }
     else if (op.kind == EngineOp::FINISH) finish_locked(op.slot);
     else release_locked(op.slot);
   }
@@ -334,6 +337,20 @@ void HostEngine::feed_locked(int slot, const std::string& data) {
   Meta& m = meta_[slot];
   m.incoming += data;
   bytes_in_ += data.size();
+  if (!m.dirty) {
+    m.dirty = true;
+    dirty_.push_back(slot);
+  }
+}
+
+// Same as feed_locked, but an empty backlog takes the payload's buffer instead of a copy
+// (the common case: the previous tick consumed everything), shortening the lock hold.
+void HostEngine::feed_locked_move(int slot, std::string& data) {
+  if (slot < 0 || slot >= (int)meta_.size() || !meta_[slot].live) return;
+  if (!meta_[slot].incoming.empty()) return feed_locked(slot, data);
+  bytes_in_ += data.size();
+  meta_[slot].incoming.swap(data);
+  Meta& m = meta_[slot];
   if (!m.dirty) {
     m.dirty = true;
     dirty_.push_back(slot);

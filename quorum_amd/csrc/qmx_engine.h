@@ -126,7 +126,8 @@ class HostEngine {
   void feed(int slot, const std::string& data);
   void finish(int slot);
   void release(int slot);
-  void apply_ops(const std::vector<EngineOp>& ops);  // in order, one lock
+  // in order, one lock; move_data: FEED payloads may be moved out of ops (the caller is done with them)
+  void apply_ops(std::vector<EngineOp>& ops, bool move_data = false);
   int submit_finalize(const std::vector<int>& slots, bool strip, bool texts, const std::string& joiner,
                       int64_t created);
   bool has_work();
@@ -157,6 +158,7 @@ class HostEngine {
   virtual void on_free(int /*slot*/) {}
 
   void feed_locked(int slot, const std::string& data);
+  void feed_locked_move(int slot, std::string& data);
   void finish_locked(int slot);
   void release_locked(int slot);
 

@@ -531,9 +531,9 @@ class GpuHub {
     eng_->release(slot);
     if (ver_) ver_->release(slot);
   }
-  void apply_ops(const std::vector<EngineOp>& ops) {
-    eng_->apply_ops(ops);
+  void apply_ops(std::vector<EngineOp>& ops) {
     if (ver_) ver_->apply_ops(ops);
+    eng_->apply_ops(ops, true);
   }
   int submit(int loop, const std::vector<int>& slots, bool strip, bool texts, const std::string& joiner,
              int64_t created) {
@@ -853,8 +853,8 @@ class Loop {
     if (hub_) {
       hub_->apply_ops(ops_);
     } else {
-      eng_->apply_ops(ops_);
       if (ver_) ver_->apply_ops(ops_);
+      eng_->apply_ops(ops_, true);
     }
     ops_.clear();
     kick_ = true;
