@@ -89,6 +89,31 @@ def available_cores() -> int:
     return len(os.sched_getaffinity(0))
 
 
+def pin_rank(torch, world: int, local_rank: int, n_dev: int):
+    """One rank per GPU on a multi-socket node: bind this rank (and the proxy, mocks and load
+    generator it spawns) to its GPU's NUMA node, splitting the node's cores between the ranks
+    whose GPUs hang off it (parallel/topology.py).  Skipped for one rank, for rehearsals
+    with more ranks than GPUs, when NUMA information is missing or would strand cores, and
+    with QMX_BENCH_PIN=0."""
+    if world <= 1 or n_dev == 0 or os.environ.get("QMX_BENCH_PIN", "1") == "0":
+        return None
+    from quorum_amd.parallel.topology import pci_numa_node, plan_rank_cpus
+
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if n_dev < local_world:
+        return None
+    nodes = []
+    for r in range(local_world):
+        pr = torch.cuda.get_device_properties(r)
+        nodes.append(pci_numa_node(pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id))
+    allowed = sorted(os.sched_getaffinity(0))
+    plan = plan_rank_cpus(nodes, allowed)
+    if plan is None or not plan[local_rank]:
+        return {"numa_nodes": nodes, "pinned": False}
+    os.sched_setaffinity(0, plan[local_rank])
+    return {"numa_nodes": nodes, "pinned": True, "cpus": len(plan[local_rank])}
+
+
 def write_config(path: str, mock_ports, skip_final: bool, tile: int, sc=None, placement="local") -> None:
     import yaml
 
@@ -245,6 +270,7 @@ def main() -> int:
         dist.init_process_group("nccl" if coll_cuda else "gloo")
     if use_cuda:
         torch.cuda.set_device(device)
+    pinning = pin_rank(torch, world, local_rank, n_dev)
     engine = args.engine
     if engine == "auto":
         engine = "hip" if use_cuda else "cpu"
@@ -337,7 +363,7 @@ def main() -> int:
                                                 f"{xchg_kind.upper()} all-gather exchange)"
                                              if args.placement == "spread" and world > 1 else ""),
                            "impl": args.impl, "engine": engine, "conns_per_rank": args.conns,
-                           "io_threads_per_rank": args.threads,
+                           "io_threads_per_rank": args.threads, "cpu_pinning": pinning,
                            "gpu_links": {k: v for k, v in link_summary().items() if k != "links_per_gpu"}},
                 "p50_ttft_ms": round(p50, 3),
                 "p99_ttft_ms": round(max(r[3] for r in rows), 3),

@@ -22,7 +22,7 @@ import time
 from typing import List, Sequence
 
 from .exchange import exchange_env
-from .topology import summary
+from .topology import gpu_numa_nodes, plan_rank_cpus, summary
 
 log = logging.getLogger("qmx.launcher")
 
@@ -48,9 +48,20 @@ def launch_ranks(argv: Sequence[str], gpus: int, bind_devices: bool, port: int) 
     if topo["gpus"]:
         log.info("GPU links: %s (full xGMI mesh: %s)", topo["links_per_gpu"], topo["full_xgmi_mesh"])
     nonce = str(time.time_ns())
+    # bind each rank to its GPU's NUMA node when the KFD/PCI topology says where it is
+    # (QMX_PIN=0 disables; device-pinned or rehearsal launches are left alone)
+    plan = None
+    if bind_devices and os.environ.get("QMX_PIN", "1") != "0":
+        nodes = gpu_numa_nodes()
+        if len(nodes) >= gpus:
+            plan = plan_rank_cpus(nodes[:gpus], sorted(os.sched_getaffinity(0)))
+    if plan:
+        log.info("rank CPU sets: %s", [len(c) for c in plan])
     procs: List[subprocess.Popen] = []
-    for cmd, env in rank_commands(argv, gpus, bind_devices, port, nonce):
-        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
+    for r, (cmd, env) in enumerate(rank_commands(argv, gpus, bind_devices, port, nonce)):
+        cpus = plan[r] if plan else None
+        pre = (lambda c=cpus: os.sched_setaffinity(0, c)) if cpus else None
+        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True, preexec_fn=pre))
 
     def fwd(sig, _frame):
         for p in procs:

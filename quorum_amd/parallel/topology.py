@@ -129,3 +129,97 @@ def summary(links: Optional[List[Link]] = None, n_gpus: Optional[int] = None,
         per[x.src][x.kind] = per[x.src].get(x.kind, 0) + 1
     full = n_gpus > 0 and all(per[g].get("xgmi", 0) >= n_gpus - 1 for g in range(n_gpus))
     return {"gpus": n_gpus, "links_per_gpu": per, "full_xgmi_mesh": full}
+
+
+# ---- NUMA placement of a rank's host threads ------------------------------------------
+# On an 8-GPU node each GPU hangs off one socket's PCIe root; a rank's io loops, tick lanes
+# (which poll the GPU's mapped result records) and — in bench.py — its load generator and
+# mock backends talk over loopback TCP, so keeping them on the GPU's NUMA node keeps both
+# the socket traffic and the mapped-memory polling socket-local.
+PCI_DEVICES = Path("/sys/bus/pci/devices")
+NUMA_NODES = Path("/sys/devices/system/node")
+CPU_DEVICES = Path("/sys/devices/system/cpu")
+
+
+def parse_cpulist(s: str) -> List[int]:
+    """``0-3,8,10-11`` -> [0, 1, 2, 3, 8, 10, 11]."""
+    out: List[int] = []
+    for part in s.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out.extend(range(int(a), int(b or a) + 1))
+    return out
+
+
+def pci_numa_node(domain: int, bus: int, device: int, function: int = 0, root: Path = PCI_DEVICES) -> int:
+    """NUMA node of a PCI function (-1 when unknown or single-node)."""
+    try:
+        return int((root / f"{domain:04x}:{bus:02x}:{device:02x}.{function}" / "numa_node").read_text().strip())
+    except (OSError, ValueError):
+        return -1
+
+
+def node_cpus(node: int, root: Path = NUMA_NODES) -> List[int]:
+    try:
+        return parse_cpulist((root / f"node{node}" / "cpulist").read_text())
+    except (OSError, ValueError):
+        return []
+
+
+def _core_key(cpu: int, root: Path) -> tuple:
+    t = root / f"cpu{cpu}" / "topology"
+    try:
+        return (int((t / "physical_package_id").read_text()), int((t / "core_id").read_text()))
+    except (OSError, ValueError):
+        return (-1, cpu)
+
+
+def rank_cpus(gpu_nodes: List[int], local_rank: int, allowed: Optional[List[int]] = None,
+              node_root: Path = NUMA_NODES, cpu_root: Path = CPU_DEVICES) -> Optional[List[int]]:
+    """CPUs for ``local_rank`` given the NUMA node of every local rank's GPU: the ranks whose
+    GPUs share a node split that node's allowed CPUs by whole physical cores (SMT siblings
+    stay together), in rank order.  None when the node is unknown or has too few cores."""
+    node = gpu_nodes[local_rank] if 0 <= local_rank < len(gpu_nodes) else -1
+    if node < 0:
+        return None
+    ok = set(allowed) if allowed is not None else None
+    cpus = [c for c in node_cpus(node, node_root) if ok is None or c in ok]
+    peers = [r for r, n in enumerate(gpu_nodes) if n == node]
+    cores: Dict[tuple, List[int]] = {}
+    for c in cpus:
+        cores.setdefault(_core_key(c, cpu_root), []).append(c)
+    keys = sorted(cores, key=lambda k: min(cores[k]))
+    if len(keys) < len(peers):
+        return None
+    k = peers.index(local_rank)
+    lo, hi = k * len(keys) // len(peers), (k + 1) * len(keys) // len(peers)
+    return sorted(c for key in keys[lo:hi] for c in cores[key])
+
+
+def gpu_numa_nodes(root: Path = KFD_TOPOLOGY, pci_root: Path = PCI_DEVICES) -> List[int]:
+    """NUMA node of every GPU in KFD order, from the KFD node's PCI address (``domain`` +
+    ``location_id`` = bus << 8 | devfn) — no HIP call, so a launcher can plan before any
+    rank touches the GPU.  -1 where unknown."""
+    out: List[int] = []
+    gpu_of = _gpu_nodes(root)
+    for node in sorted(gpu_of, key=gpu_of.get):
+        pr = _props(root / str(node) / "properties")
+        loc = pr.get("location_id", -1)
+        out.append(pci_numa_node(pr.get("domain", 0), loc >> 8, (loc >> 3) & 31, loc & 7, pci_root)
+                   if loc >= 0 else -1)
+    return out
+
+
+def plan_rank_cpus(gpu_nodes: List[int], allowed: List[int], min_cover: float = 0.9,
+                   node_root: Path = NUMA_NODES, cpu_root: Path = CPU_DEVICES) -> Optional[List[List[int]]]:
+    """Every local rank's CPU set (see :func:`rank_cpus`), or None when any rank's node is
+    unknown or the sets would leave more than ``1 - min_cover`` of the allowed CPUs idle
+    (e.g. firmware reporting every GPU on node 0 of a two-socket box): pinning must never
+    strand cores the unpinned scheduler would use."""
+    sets = [rank_cpus(gpu_nodes, r, allowed, node_root, cpu_root) for r in range(len(gpu_nodes))]
+    if not sets or any(s is None for s in sets):
+        return None
+    if sum(len(s) for s in sets) < min_cover * len(allowed):
+        return None
+    return sets

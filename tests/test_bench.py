@@ -73,3 +73,32 @@ def test_bench_two_ranks_torchrun(tmp_path):
     res = _check(lines[0], 2, 2, 1)
     assert res["config"]["global_batch"] == 256
     assert res["config"]["parallelism"].startswith("dp2")
+
+
+def test_pin_rank_numa_plan(monkeypatch):
+    """bench.pin_rank: ranks bound to their GPU's NUMA node (fake device properties and
+    topology); skipped for one rank, rehearsals with more ranks than GPUs, and opt-out."""
+    import importlib.util
+    from types import SimpleNamespace
+
+    from quorum_amd.parallel import topology
+
+    spec = importlib.util.spec_from_file_location("qmx_bench_mod", BENCH)
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    buses = [0x05, 0x15, 0x65, 0x75, 0x85, 0x95, 0xE5, 0xF5]
+    fake_torch = SimpleNamespace(cuda=SimpleNamespace(get_device_properties=lambda r: SimpleNamespace(
+        pci_domain_id=0, pci_bus_id=buses[r], pci_device_id=0)))
+    monkeypatch.setattr(topology, "pci_numa_node", lambda d, b, dev, f=0: 0 if b < 0x80 else 1)
+    got = {}
+    monkeypatch.setattr(topology, "plan_rank_cpus",
+                        lambda nodes, allowed: [[r] for r in range(len(nodes))] if len(set(nodes)) == 2 else None)
+    monkeypatch.setattr(os, "sched_setaffinity", lambda pid, cpus: got.setdefault("cpus", list(cpus)))
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    monkeypatch.delenv("QMX_BENCH_PIN", raising=False)
+    r = bench.pin_rank(fake_torch, 8, 5, 8)
+    assert r == {"numa_nodes": [0, 0, 0, 0, 1, 1, 1, 1], "pinned": True, "cpus": 1} and got["cpus"] == [5]
+    assert bench.pin_rank(fake_torch, 1, 0, 8) is None
+    assert bench.pin_rank(fake_torch, 8, 0, 1) is None  # more ranks than GPUs
+    monkeypatch.setenv("QMX_BENCH_PIN", "0")
+    assert bench.pin_rank(fake_torch, 8, 0, 8) is None

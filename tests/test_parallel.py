@@ -52,6 +52,74 @@ def test_kfd_pcie_only_and_missing(tmp_path):
     assert topology.summary(root=tmp_path / "nope") == {"gpus": 0, "links_per_gpu": {}, "full_xgmi_mesh": False}
 
 
+def _fake_numa(root, nodes, smt=2):
+    """nodes: {node: n_physical_cores}; logical cpu numbering as on a 2-socket EPYC box:
+    physical cores first (node by node), SMT siblings after them."""
+    total = sum(nodes.values())
+    first = 0
+    for node, n in sorted(nodes.items()):
+        cpus = []
+        for i in range(n):
+            for t in range(smt):
+                cpu = first + i + t * total
+                cpus.append(cpu)
+                topo = root / "cpu" / f"cpu{cpu}" / "topology"
+                topo.mkdir(parents=True)
+                (topo / "physical_package_id").write_text(f"{node}\n")
+                (topo / "core_id").write_text(f"{i}\n")
+        d = root / "node" / f"node{node}"
+        d.mkdir(parents=True)
+        cpus.sort()
+        # kernel format: ranges
+        runs, start = [], cpus[0]
+        for a, b in zip(cpus, cpus[1:] + [None]):
+            if b != a + 1:
+                runs.append(f"{start}-{a}" if a != start else str(a))
+                start = b
+        (d / "cpulist").write_text(",".join(runs) + "\n")
+        first += n
+
+
+def test_cpulist_and_pci_numa(tmp_path):
+    assert topology.parse_cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
+    dev = tmp_path / "pci" / "0000:75:00.0"
+    dev.mkdir(parents=True)
+    (dev / "numa_node").write_text("1\n")
+    assert topology.pci_numa_node(0, 0x75, 0, root=tmp_path / "pci") == 1
+    assert topology.pci_numa_node(0, 0x76, 0, root=tmp_path / "pci") == -1
+
+
+def test_rank_cpus_split_by_numa_node(tmp_path):
+    _fake_numa(tmp_path, {0: 8, 1: 8})  # 2 sockets x 8 cores x 2 threads = cpus 0-31
+    nodes = [0, 0, 0, 0, 1, 1, 1, 1]  # GPUs 0-3 on socket 0, 4-7 on socket 1
+    kw = dict(node_root=tmp_path / "node", cpu_root=tmp_path / "cpu")
+    sets = [topology.rank_cpus(nodes, r, **kw) for r in range(8)]
+    assert sets[0] == [0, 1, 16, 17] and sets[3] == [6, 7, 22, 23] and sets[4] == [8, 9, 24, 25]
+    flat = [c for s in sets for c in s]
+    assert sorted(flat) == list(range(32))  # disjoint, covering every cpu
+    # restricted affinity set; unknown node; more ranks than cores
+    assert topology.rank_cpus(nodes, 0, allowed=[0, 1, 2, 3, 16], **kw) == [0, 16]
+    assert topology.rank_cpus([-1, -1], 0, **kw) is None
+    assert topology.rank_cpus([0] * 9, 0, **kw) is None
+    # the plan refuses to strand a socket (every GPU reported on node 0)
+    allowed = list(range(32))
+    assert topology.plan_rank_cpus(nodes, allowed, **kw) == sets
+    assert topology.plan_rank_cpus([0] * 8, allowed, **kw) is None
+    assert topology.plan_rank_cpus([0, -1], allowed, **kw) is None
+
+
+def test_gpu_numa_nodes_from_kfd(tmp_path):
+    _fake_kfd(tmp_path / "kfd", 2)
+    for g, (bus, node) in enumerate([(0x05, 0), (0xE5, 1)], start=1):
+        pp = tmp_path / "kfd" / str(g) / "properties"
+        pp.write_text(pp.read_text() + f"domain 0\nlocation_id {bus << 8}\n")
+        dev = tmp_path / "pci" / f"0000:{bus:02x}:00.0"
+        dev.mkdir(parents=True)
+        (dev / "numa_node").write_text(f"{node}\n")
+    assert topology.gpu_numa_nodes(tmp_path / "kfd", tmp_path / "pci") == [0, 1]
+    assert topology.gpu_numa_nodes(tmp_path / "none", tmp_path / "pci") == []
+
+
 def test_exchange_settings_agree_across_ranks():
     cfgs = []
     for r in range(4):
