@@ -270,7 +270,10 @@ def main() -> int:
         dist.init_process_group("nccl" if coll_cuda else "gloo")
     if use_cuda:
         torch.cuda.set_device(device)
-    pinning = pin_rank(torch, world, local_rank, n_dev)
+    try:
+        pinning = pin_rank(torch, world, local_rank, n_dev)
+    except (OSError, RuntimeError, ValueError, AttributeError) as e:  # placement is an optimisation only
+        pinning = {"pinned": False, "error": repr(e)}
     engine = args.engine
     if engine == "auto":
         engine = "hip" if use_cuda else "cpu"
