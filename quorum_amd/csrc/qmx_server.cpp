@@ -16,6 +16,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -83,15 +84,46 @@ Hist h_ttft, h_latency, h_tick, h_upstream_ttfb;
 using Clock = std::chrono::steady_clock;
 inline double now_s() { return std::chrono::duration<double>(Clock::now().time_since_epoch()).count(); }
 
-std::string lower(std::string s) {
-  for (auto& c : s) c = (char)tolower((unsigned char)c);
-  return s;
+// Header block [p, p+n) ("k: v\r\n" lines, no start line): calls f(lower(trim(k)), trim(v)) per line that
+// has a colon, building each key and value string once (no per-line/per-field temporaries).
+template <class F>
+void for_each_header(const char* p, size_t n, F&& f) {
+  auto ws = [](char ch) { return ch == ' ' || ch == '\t'; };
+  size_t pos = 0;
+  while (pos < n) {
+    const char* e0 = (const char*)memmem(p + pos, n - pos, "\r\n", 2);
+    size_t e = e0 ? (size_t)(e0 - p) : n;
+    const char* colon = (const char*)memchr(p + pos, ':', e - pos);
+    if (colon) {
+      size_t ka = pos, kb = (size_t)(colon - p);
+      while (ka < kb && ws(p[ka])) ++ka;
+      while (kb > ka && (ws(p[kb - 1]) || p[kb - 1] == '\r')) --kb;
+      size_t va = (size_t)(colon - p) + 1, vb = e;
+      while (va < vb && ws(p[va])) ++va;
+      while (vb > va && (ws(p[vb - 1]) || p[vb - 1] == '\r')) --vb;
+      std::string k(p + ka, kb - ka);
+      for (auto& ch : k) ch = (char)tolower((unsigned char)ch);
+      f(std::move(k), std::string(p + va, vb - va));
+    }
+    pos = e + 2;
+  }
 }
-std::string trim(const std::string& s) {
-  size_t a = 0, b = s.size();
-  while (a < b && (s[a] == ' ' || s[a] == '\t')) ++a;
-  while (b > a && (s[b - 1] == ' ' || s[b - 1] == '\t' || s[b - 1] == '\r')) --b;
-  return s.substr(a, b - a);
+// ASCII case-insensitive equality / substring search of a lower-case needle
+bool ieq(const std::string& s, const char* lw) {
+  size_t n = strlen(lw);
+  if (s.size() != n) return false;
+  for (size_t i = 0; i < n; ++i)
+    if ((char)tolower((unsigned char)s[i]) != lw[i]) return false;
+  return true;
+}
+bool icontains(const std::string& s, const char* lw) {
+  size_t n = strlen(lw);
+  for (size_t i = 0; i + n <= s.size(); ++i) {
+    size_t j = 0;
+    while (j < n && (char)tolower((unsigned char)s[i + j]) == lw[j]) ++j;
+    if (j == n) return true;
+  }
+  return false;
 }
 const char* reason(int st) {
   switch (st) {
@@ -159,31 +191,24 @@ struct RespParser {
       if (phase == 0) {
         size_t he = buf.find("\r\n\r\n", i);
         if (he == std::string::npos) break;
-        std::string head = buf.substr(i, he - i);
+        const char* hp = buf.data() + i;
+        size_t hn = he - i;
         i = he + 4;
-        size_t le = head.find("\r\n");
-        std::string sl = head.substr(0, le);
-        if (sl.size() < 12 || sl.compare(0, 5, "HTTP/") != 0) return -1;
-        status = atoi(sl.c_str() + 9);
+        const char* le0 = (const char*)memmem(hp, hn, "\r\n", 2);
+        size_t le = le0 ? (size_t)(le0 - hp) : hn;
+        if (le < 12 || memcmp(hp, "HTTP/", 5) != 0) return -1;
+        status = atoi(std::string(hp + 9, le - 9).c_str());
         bool chunked = false, has_len = false;
-        size_t pos = le == std::string::npos ? head.size() : le + 2;
-        while (pos < head.size()) {
-          size_t e = head.find("\r\n", pos);
-          if (e == std::string::npos) e = head.size();
-          std::string line = head.substr(pos, e - pos);
-          size_t c = line.find(':');
-          if (c != std::string::npos) {
-            std::string k = lower(trim(line.substr(0, c))), v = trim(line.substr(c + 1));
-            if (k == "transfer-encoding" && lower(v).find("chunked") != std::string::npos) chunked = true;
-            if (k == "content-length") {
-              has_len = true;
-              remaining = atol(v.c_str());
-            }
-            if (k == "connection" && lower(v) == "close") close = true;
-            headers.emplace_back(k, v);
+        size_t pos = le0 ? le + 2 : hn;
+        for_each_header(hp + pos, hn - pos, [&](std::string&& k, std::string&& v) {
+          if (k == "transfer-encoding" && icontains(v, "chunked")) chunked = true;
+          if (k == "content-length") {
+            has_len = true;
+            remaining = atol(v.c_str());
           }
-          pos = e + 2;
-        }
+          if (k == "connection" && ieq(v, "close")) close = true;
+          headers.emplace_back(std::move(k), std::move(v));
+        });
         if (status == 204 || status == 304) phase = 7;
         else if (chunked) phase = 2;
         else if (has_len) phase = remaining > 0 ? 1 : 7;
@@ -1051,28 +1076,20 @@ class Loop {
       std::string method = rl.substr(0, sp1), target = rl.substr(sp1 + 1, sp2 - sp1 - 1),
                   version = rl.substr(sp2 + 1);
       std::vector<std::pair<std::string, std::string>> hdrs;
+      hdrs.reserve(12);
       size_t pos = le == std::string::npos ? head.size() : le + 2;
       long clen = 0;
       bool chunked = false;
       bool keepalive = version != "HTTP/1.0";
-      while (pos < head.size()) {
-        size_t e = head.find("\r\n", pos);
-        if (e == std::string::npos) e = head.size();
-        std::string line = head.substr(pos, e - pos);
-        size_t colon = line.find(':');
-        if (colon != std::string::npos) {
-          std::string k = lower(trim(line.substr(0, colon))), v = trim(line.substr(colon + 1));
-          if (k == "content-length") clen = atol(v.c_str());
-          if (k == "transfer-encoding" && lower(v).find("chunked") != std::string::npos) chunked = true;
-          if (k == "connection") {
-            std::string lv = lower(v);
-            if (lv == "close") keepalive = false;
-            if (lv == "keep-alive") keepalive = true;
-          }
-          hdrs.emplace_back(k, v);
+      for_each_header(head.data() + pos, head.size() - std::min(pos, head.size()), [&](std::string&& k, std::string&& v) {
+        if (k == "content-length") clen = atol(v.c_str());
+        if (k == "transfer-encoding" && icontains(v, "chunked")) chunked = true;
+        if (k == "connection") {
+          if (ieq(v, "close")) keepalive = false;
+          if (ieq(v, "keep-alive")) keepalive = true;
         }
-        pos = e + 2;
-      }
+        hdrs.emplace_back(std::move(k), std::move(v));
+      });
       std::string body;
       size_t used;
       if (chunked) {
@@ -1148,6 +1165,7 @@ class Loop {
     bool streaming = sv && sv->truthy();
     // forward all headers but host; auth fallback/normalisation; content-type default (quorum :972-1008)
     bool has_auth = false, has_ctype = false;
+    s->fwd.reserve(hdrs.size() + 2);
     for (auto& h : hdrs) {
       if (h.first == "host") continue;
       if (h.first == "authorization") {
@@ -1223,11 +1241,21 @@ class Loop {
   }
   std::string build_req(const BackendCfg& be, const std::vector<std::pair<std::string, std::string>>& hdrs,
                         const std::string& body) {
-    std::string r = "POST " + be.path + "/chat/completions HTTP/1.1\r\nhost: " + be.host +
-                    (be.port != (be.https ? 443 : 80) ? ":" + std::to_string(be.port) : std::string()) + "\r\n";
-    for (auto& h : hdrs) r += h.first + ": " + h.second + "\r\n";
-    r += "content-length: " + std::to_string(body.size()) + "\r\n\r\n";
-    r += body;
+    // one reserved buffer, appended in place (the request line + headers were ~10 temporaries)
+    size_t n = be.path.size() + be.host.size() + body.size() + 96;
+    for (auto& h : hdrs) n += h.first.size() + h.second.size() + 4;
+    std::string r;
+    r.reserve(n);
+    r.append("POST ").append(be.path).append("/chat/completions HTTP/1.1\r\nhost: ").append(be.host);
+    char num[24];
+    if (be.port != (be.https ? 443 : 80)) {
+      r += ':';
+      r.append(num, (size_t)snprintf(num, sizeof num, "%d", be.port));
+    }
+    r.append("\r\n");
+    for (auto& h : hdrs) r.append(h.first).append(": ").append(h.second).append("\r\n");
+    r.append("content-length: ").append(num, (size_t)snprintf(num, sizeof num, "%zu", body.size())).append("\r\n\r\n");
+    r.append(body);
     return r;
   }
   Up* open_up(Session* s, int bi, int backend, UpMode mode, std::string req, double timeout) {
