@@ -367,3 +367,47 @@ def test_native_shared_engine_many_loops(threads, lanes):
     after = ext.server_counters()
     assert after["verify_checked"] - before["verify_checked"] >= 48 * 3
     assert after["verify_mismatches"] == before["verify_mismatches"]
+
+
+def _raw_http(port, data: bytes) -> bytes:
+    import socket
+
+    with socket.create_connection(("127.0.0.1", port), timeout=10) as s:
+        s.sendall(data)
+        out = b""
+        while True:
+            b = s.recv(65536)
+            if not b:
+                return out
+            out += b
+
+
+def test_native_header_block_edge_cases():
+    """Client request headers: case-insensitive names, tab / no-space / trailing-space values,
+    a `Transfer-Encoding: Chunked` body and `Connection: Close`; forwarded headers reach the
+    upstream trimmed, the hop-by-hop ones do not (qmx_server.cpp for_each_header)."""
+    live = LiveUpstream()
+    p1 = live.serve("b1", ("json", 200, completion("hi")))
+    cfg = {"primary_backends": [{"name": "a", "url": f"http://127.0.0.1:{p1}/v1", "model": "m"}],
+           "settings": {"timeout": 5}}
+    body = json.dumps({"messages": MSG}).encode()
+    half = len(body) // 2
+    chunked = b"%x\r\n%s\r\n%x\r\n%s\r\n0\r\n\r\n" % (half, body[:half], len(body) - half, body[half:])
+    req = (b"POST /v1/chat/completions HTTP/1.1\r\nHOST: x\r\nAuthorization:\tBearer k1  \r\n"
+           b"X-Custom:val ue\t\r\nTransfer-Encoding: Chunked\r\nCONTENT-TYPE: application/json\r\n"
+           b"Accept-Encoding: gzip\r\nConnection: Close\r\n\r\n" + chunked)
+    try:
+        with native_server(cfg) as port:
+            out = _raw_http(port, req)  # the server closes after one response (Connection: Close)
+            head, _, rest = out.partition(b"\r\n\r\n")
+            assert head.startswith(b"HTTP/1.1 200"), head
+            assert b'"hi"' in rest
+        assert len(live.calls) == 1
+        h = live.calls[0]["headers"]
+        assert h["authorization"] == "Bearer k1"
+        assert h["x-custom"] == "val ue"
+        assert h["content-type"] == "application/json"
+        assert "accept-encoding" not in h and "transfer-encoding" not in h
+        assert live.calls[0]["body"]["messages"] == MSG
+    finally:
+        live.close()
