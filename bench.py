@@ -37,8 +37,11 @@ BASELINE_RPS = 9.1  # reference, 2 backends, same config, 16 client
 # BASELINE.json configs.  "headline" is the driver's metric; the others are measured with
 # --scenario (reference numbers from BASELINE.md where one exists for that shape).
 SCENARIOS = {
+    # headline: 16384 requests per step so the timed window (one load-generator run) is ~2 s
+    # and its start/connect/drain is amortised (MI355X A/B, profiles/r1n_batch_ab.txt: 4/4
+    # pairs higher, mean 180k vs 153k req/s against 4096 per step)
     "headline": dict(n=2, strategy="concatenate", hide_final=False, skip=True, faults={}, timeout=30,
-                     baseline=9.1, desc="2 mock backends, streaming concatenate, hide_intermediate_think"),
+                     batch=16384, baseline=9.1, desc="2 mock backends, streaming concatenate, hide_intermediate_think"),
     "aggregate4": dict(n=4, strategy="aggregate", hide_final=False, skip=False, faults={}, timeout=30,
                        baseline=3.8, desc="4 mock backends, streaming aggregate strategy (LLM4 also aggregates)"),
     "highqps8": dict(n=8, strategy="concatenate", hide_final=True, skip=True, faults={}, timeout=30,
@@ -225,7 +228,8 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4096, help="requests per step per rank")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="requests per step per rank (0: the scenario's default, 16384 headline / 4096 others)")
     ap.add_argument("--conns", type=int, default=64, help="concurrent client connections per rank")
     ap.add_argument("--impl", default=os.environ.get("QMX_BENCH_IMPL", "native"), choices=["native", "python"])
     ap.add_argument("--engine", default=os.environ.get("QMX_BENCH_ENGINE", "auto"))
@@ -246,6 +250,8 @@ def main() -> int:
     sc = SCENARIOS[args.scenario]
     if "conns" in sc and args.conns == 64:  # scenario default unless set explicitly
         args.conns = sc["conns"]
+    if args.batch <= 0:
+        args.batch = sc.get("batch", 4096)
     skip_final = bool(args.skip_final) if args.scenario == "headline" else sc["skip"]
 
     rank = int(os.environ.get("RANK", "0"))
