@@ -713,7 +713,7 @@ class Loop {
     while (!g_stop.load()) {
       // inline engine with work queued by the last iteration (e.g. a finalize submitted
       // while applying tick results): poll instead of sleeping
-      const int to = (!hub_ && kick_) ? 0 : 50;
+      const int to = (!hub_ && kick_) ? 0 : deferq_.empty() ? 50 : 1;
       int n = epoll_wait(ep_, evs.data(), (int)evs.size(), to);
       for (int i = 0; i < n; ++i) dispatch(evs[i]);
       if (g_drain.load() && drain_step()) break;
@@ -742,9 +742,28 @@ class Loop {
         kick_ = false;
         hub_->kick();
       }
+      if (!deferq_.empty()) release_deferred(now_s());
       if (!flushq_.empty()) flush_queued();
       if (!pending_close_.empty()) reap_clients();
     }
+  }
+  // deferred heads whose deadline passed are queued for this iteration's flush; entries whose
+  // client was queued by later output (or closed) are dropped
+  void release_deferred(double t) {
+    size_t k = 0;
+    for (size_t i = 0; i < deferq_.size(); ++i) {
+      auto it = clients_.find(deferq_[i].first);
+      if (it == clients_.end()) continue;
+      Client* c = it->second.get();
+      if (c->queued || c->want_out || c->dead || c->out_off >= c->out.size()) continue;
+      if (deferq_[i].second <= t || g_drain.load()) {
+        c->queued = true;
+        flushq_.push_back(c->fd);
+        continue;
+      }
+      deferq_[k++] = deferq_[i];
+    }
+    deferq_.resize(k);
   }
 
  private:
@@ -1684,9 +1703,15 @@ class Loop {
     s->filter = cfg_.hide_intermediate;
     s->emit = !cfg_.suppress;
     if (const JVal* sup = s->body.get("suppress_individual_responses")) s->emit = !sup->truthy();
+    const bool defer = role_defer_s_ > 0 && s->cl && !s->cl->queued && !s->cl->want_out;
     write_client(s->cl, kSseHdr);
     send_chunk(s, chunk_event_json("chatcmpl-parallel", (int64_t)time(nullptr), "\"parallel-proxy\"",
                                    "{\"role\": \"assistant\"}", "null"));
+    if (defer && s->cl->queued && !flushq_.empty() && flushq_.back() == s->cl->fd) {
+      flushq_.pop_back();  // un-queue: the first content (or the deadline) sends it
+      s->cl->queued = false;
+      deferq_.emplace_back(s->cl->fd, now_s() + role_defer_s_);
+    }
     s->bs.resize(valid.size());
     // spread placement (EP analog): backend i of a session owned by rank r runs on rank
     // (r + i) % world; its deltas and final text come back through the exchange (R1)
@@ -2365,6 +2390,14 @@ class Loop {
   SSL_CTX* tls_ = nullptr;                  // https upstreams (peer + host verification, as httpx)
   std::vector<int> pending_close_, pending_requests_;
   std::vector<int> flushq_;  // clients with corked output (flushed at the end of each iteration)
+  // parallel streams: the SSE head + role event wait (corked, not queued) for the first
+  // content of the same session or this deadline, whichever comes first — one client send
+  // per request instead of two when the tick answers within it (QMX_ROLE_DEFER_US, 0: off)
+  std::vector<std::pair<int, double>> deferq_;
+  const double role_defer_s_ = [] {
+    const char* e = getenv("QMX_ROLE_DEFER_US");
+    return (e ? atof(e) : 1000.0) * 1e-6;
+  }();
   std::vector<EngineOp> ops_;  // engine feed / finish / release of this iteration (flush_ops)
 };
 

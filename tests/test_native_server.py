@@ -411,3 +411,34 @@ def test_native_header_block_edge_cases():
         assert live.calls[0]["body"]["messages"] == MSG
     finally:
         live.close()
+
+
+def test_native_role_event_not_held_behind_slow_upstream():
+    """The parallel SSE head + role event is corked until the first content or a 1 ms deadline
+    (QMX_ROLE_DEFER_US): a slow upstream must not hold it back."""
+    import time
+
+    live = LiveUpstream()
+    slow = [sse_chunk({"role": "assistant"}), 0.8, sse_chunk({"content": "late"}), sse_chunk({}, finish="stop"),
+            b"data: [DONE]\n\n"]
+    p1 = live.serve("b1", ("stream", 200, slow))
+    p2 = live.serve("b2", ("stream", 200, slow))
+    cfg = cfg_parallel(2, block=dict(CONCAT, skip_final_aggregation=True))
+    cfg["primary_backends"][0]["url"] = f"http://127.0.0.1:{p1}/v1"
+    cfg["primary_backends"][1]["url"] = f"http://127.0.0.1:{p2}/v1"
+    try:
+        with native_server(cfg) as port:
+            with httpx.Client(base_url=f"http://127.0.0.1:{port}", timeout=30) as cl:
+                t0 = time.perf_counter()
+                with cl.stream("POST", "/v1/chat/completions", json={"messages": MSG, "stream": True},
+                               headers=AUTH) as r:
+                    it = r.iter_raw()
+                    first = next(it)
+                    t_first = time.perf_counter() - t0
+                    rest = b"".join(it)
+        assert b'"role": "assistant"' in first and b"late" not in first
+        assert t_first < 0.5, t_first  # the upstream's content comes 0.8 s in
+        evs = _norm_sse((first + rest).decode())
+        assert evs[-1] == "[DONE]"
+    finally:
+        live.close()
