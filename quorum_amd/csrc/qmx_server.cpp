@@ -665,15 +665,10 @@ class Loop {
         {
           std::lock_guard<std::mutex> g(rmu_);
           rq_.push_back(std::move(rb));
-          rq_pending_.store(true);
         }
-        // wake the loop only if it is (about to be) parked in epoll_wait: an awake loop takes
-        // the batch at the end of its iteration (Dekker pair with the store/load in run())
-        if (evfd_always_ || sleeping_.exchange(false)) {
-          uint64_t one = 1;
-          ssize_t w = write(evfd_, &one, 8);
-          (void)w;
-        }
+        uint64_t one = 1;
+        ssize_t w = write(evfd_, &one, 8);
+        (void)w;
       });
   }
   void attach_tls(SSL_CTX* t) { tls_ = t; }
@@ -718,18 +713,9 @@ class Loop {
     while (!g_stop.load()) {
       // inline engine with work queued by the last iteration (e.g. a finalize submitted
       // while applying tick results): poll instead of sleeping
-      int to = (!hub_ && kick_) ? 0 : deferq_.empty() ? 50 : 1;
-      if (hub_) {
-        sleeping_.store(true);
-        if (rq_pending_.load()) {
-          sleeping_.store(false);
-          to = 0;
-        }
-      }
+      const int to = (!hub_ && kick_) ? 0 : deferq_.empty() ? 50 : 1;
       int n = epoll_wait(ep_, evs.data(), (int)evs.size(), to);
-      if (hub_) sleeping_.store(false);
       for (int i = 0; i < n; ++i) dispatch(evs[i]);
-      if (hub_ && rq_pending_.load(std::memory_order_relaxed)) take_results();
       if (g_drain.load() && drain_step()) break;
       if (!pending_requests_.empty()) {
         std::vector<int> fds;
@@ -857,14 +843,10 @@ class Loop {
     uint64_t v;
     ssize_t r = read(evfd_, &v, 8);
     (void)r;
-    take_results();
-  }
-  void take_results() {
     std::vector<ResultBatch> q;
     {
       std::lock_guard<std::mutex> g(rmu_);
       q.swap(rq_);
-      rq_pending_.store(false);
     }
     for (auto& rb : q) apply(rb);
   }
@@ -2385,8 +2367,6 @@ class Loop {
   bool kick_ = false;
   std::mutex rmu_;
   std::vector<ResultBatch> rq_;
-  std::atomic<bool> rq_pending_{false}, sleeping_{false};
-  const bool evfd_always_ = getenv("QMX_EVFD_ALWAYS") != nullptr;  // A/B: wake on every batch
   std::unordered_map<int, std::unique_ptr<Client>> clients_;
   std::unordered_map<int, std::unique_ptr<Up>> ups_;
   std::unordered_map<Session*, std::unique_ptr<Session>> sessions_;
