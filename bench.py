@@ -294,13 +294,17 @@ def main() -> int:
 
     procs = []
     tmp = tempfile.mkdtemp(prefix=f"qmx_bench_r{rank}_")
+    restarts = 0
     try:
         mock_ports = [args.port + 100 + rank * 10 + i for i in range(sc["n"])]
+
+        def spawn_mock(i, p):
+            return subprocess.Popen([os.path.join(bin_dir, "qmx_mock"), "--port", str(p), "--threads",
+                                     str(args.mock_threads), "--tokens", "20", "--think", "1"]
+                                    + sc.get("mock_args", []) + sc["faults"].get(i, []),
+                                    stderr=subprocess.DEVNULL, start_new_session=True)
         for i, p in enumerate(mock_ports):
-            procs.append(subprocess.Popen([os.path.join(bin_dir, "qmx_mock"), "--port", str(p), "--threads",
-                                           str(args.mock_threads), "--tokens", "20", "--think", "1"]
-                                          + sc.get("mock_args", []) + sc["faults"].get(i, []),
-                                          stderr=subprocess.DEVNULL, start_new_session=True))
+            procs.append(spawn_mock(i, p))
         cfg_path = os.path.join(tmp, "config.yaml")
         write_config(cfg_path, mock_ports, skip_final, args.tile, sc, args.placement)
         env = dict(os.environ)
@@ -320,6 +324,26 @@ def main() -> int:
         # warmup
         if args.warmup > 0:
             loadgen(bin_dir, args.port, args.conns, args.warmup * args.batch, args.lg_threads, args.timeout)
+        # a server process that died during warmup is reported (stderr + "restarts" in the JSON
+        # line) and started again once, so the timed steps measure a live stack
+        dead = [(i, q.returncode) for i, q in enumerate(mock_procs + proxy_procs) if q.poll() is not None]
+        if dead:
+            print(f"bench rank {rank}: server process(es) exited during warmup (index, code): {dead}",
+                  file=sys.stderr, flush=True)
+            restarts += len(dead)
+            for i, _ in dead:
+                if i < len(mock_procs):
+                    mock_procs[i] = spawn_mock(i, mock_ports[i])
+                    procs.append(mock_procs[i])
+            if any(i >= len(mock_procs) for i, _ in dead):
+                _kill(proxy_procs)
+                proxy_procs = spawn_workers(cfg_path, "127.0.0.1", args.port, args.workers, engine,
+                                            device, impl=args.impl, threads=args.threads, env=env)
+                procs += proxy_procs
+            if not wait_healthy("127.0.0.1", args.port, 180):
+                raise RuntimeError("proxy did not become healthy after restart")
+            loadgen(bin_dir, args.port, args.conns, max(1, args.warmup) * args.batch, args.lg_threads,
+                    args.timeout)
         if dist is not None:
             dist.barrier()
         if use_cuda:
@@ -337,7 +361,8 @@ def main() -> int:
         bd = breakdown(m0, scrape(args.port), elapsed) if args.impl == "native" else {}
         bd.update(cpu_breakdown(c0, c1, stats["completed"], elapsed))
         local = [elapsed, float(stats["completed"]), float(stats["ttft_p50_ms"]), float(stats["ttft_p99_ms"]),
-                 float(stats["errors"] + stats["non200"]), float(stats["ttfb_p50_ms"]), float(stats["lat_p50_ms"])]
+                 float(stats["errors"] + stats["non200"]), float(stats["ttfb_p50_ms"]), float(stats["lat_p50_ms"]),
+                 float(restarts)]
         if dist is not None:
             t = torch.tensor(local, dtype=torch.float64, device="cuda" if coll_cuda else "cpu")
             gathered = [torch.zeros_like(t) for _ in range(world)]
@@ -379,6 +404,7 @@ def main() -> int:
                 "p50_ttfb_ms": round(statistics.median(r[5] for r in rows), 3),
                 "p50_latency_ms": round(statistics.median(r[6] for r in rows), 3),
                 "errors": int(sum(r[4] for r in rows)),
+                "server_restarts_in_warmup": int(sum(r[7] for r in rows)),
                 "baseline_p50_ttft_ms_16_clients": 1605,
                 # one rank proxy process counters over the timed region (SURVEY §5.1 time breakdown;
                 # with N>1 the shared port answers from any rank)
