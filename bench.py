@@ -60,10 +60,6 @@ SCENARIOS = {
 }
 
 
-def _free_port_block(base: int) -> int:
-    return base
-
-
 def _kill(procs):
     for p in procs:
         try:
@@ -142,13 +138,84 @@ def write_config(path: str, mock_ports, skip_final: bool, tile: int, sc=None, pl
         yaml.safe_dump(cfg, f)
 
 
-def loadgen(bin_dir, port, conns, requests, threads, timeout):
-    out = subprocess.run([os.path.join(bin_dir, "qmx_loadgen"), "--port", str(port), "--conns", str(conns),
-                          "--requests", str(requests), "--threads", str(threads), "--timeout", str(timeout),
-                          "--path", "/v1/chat/completions"], capture_output=True, text=True, timeout=timeout + 60)
+def mock_expected(bin_dir) -> dict:
+    """What a client must see from one mock backend (qmx_mock --print-expected): the streamed
+    content outside the think block, and the non-streaming message content."""
+    out = subprocess.run([os.path.join(bin_dir, "qmx_mock"), "--print-expected", "1", "--tokens", "20", "--think", "1"],
+                         capture_output=True, text=True, timeout=30, check=True)
+    return json.loads(out.stdout)
+
+
+def expect_spec(path: str, sc: dict, skip_final: bool, exp: dict, path_prefix: str = "chatcmpl-parallel") -> None:
+    """Write qmx_loadgen's --expect file for a scenario: the exact event contract every
+    response must satisfy (role first, [DONE] last, per-backend content, final event)."""
+    sep = "\n" + "\n-------------\n"  # streaming final joiner: "\n" + separator (oai_proxy.py:834-841)
+    text = exp["stream_text"]
+    faulty = set(sc["faults"])
+    lines = ["role 1", "done 1"]
+    for i in range(sc["n"]):
+        mode = "prefix" if i in faulty else "exact"
+        lines.append(f"stream {path_prefix}-{i} {mode} {text.encode().hex()}")
+    if skip_final:
+        lines.append("final absent")
+    elif sc["strategy"] == "aggregate":
+        lines.append("final any " + exp["message"].encode().hex())  # the aggregator's answer, verbatim
+    else:
+        good = [i for i in range(sc["n"]) if i not in faulty]
+        opts = {sep.join([text] * len(good))}
+        if faulty:  # a faulty backend contributes its text only when its stream succeeded
+            opts.add(sep.join([text] * (len(good) + len(faulty))))
+        lines.append("final any " + " ".join(sorted(o.encode().hex() for o in opts)))
+    lines.append("error absent")
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+def loadgen(bin_dir, port, conns, requests, threads, timeout, expect=None, path="/v1/chat/completions"):
+    cmd = [os.path.join(bin_dir, "qmx_loadgen"), "--port", str(port), "--conns", str(conns),
+           "--requests", str(requests), "--threads", str(threads), "--timeout", str(timeout),
+           "--path", path]
+    if expect:
+        cmd += ["--expect", expect]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout + 60)
     if out.returncode != 0:
         raise RuntimeError(f"loadgen failed: {out.stderr}")
+    if out.stderr.strip():
+        print(out.stderr.strip()[-3000:], file=sys.stderr, flush=True)  # the first invalid responses
     return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def exit_status(p) -> dict:
+    """How a harness process ended (None: still running)."""
+    rc = p.poll()
+    if rc is None:
+        return {"pid": p.pid, "running": True}
+    d = {"pid": p.pid, "running": False, "returncode": rc}
+    if rc < 0:
+        try:
+            d["signal"] = signal.Signals(-rc).name
+        except ValueError:
+            d["signal"] = -rc
+    return d
+
+
+def spawn_reference(ref_root: str, tmp: str, cfg_path: str, port: int) -> subprocess.Popen:
+    """The reference proxy, UNMODIFIED, from a scratch copy: quorum reads
+    <copy>/config.yaml (oai_proxy.py:46) and writes <copy>/logs/ (oai_proxy.py:20-37); one
+    uvicorn worker as in its Makefile (run-prod, Makefile:7).  Same mocks and load
+    generator as the native proxy: the same-harness baseline BASELINE.md asks for."""
+    import shutil
+
+    copy = os.path.join(tmp, "refcopy")
+    shutil.copytree(os.path.join(ref_root, "src"), os.path.join(copy, "src"))
+    shutil.copy(cfg_path, os.path.join(copy, "config.yaml"))
+    env = dict(os.environ)
+    env["PYTHONPATH"] = os.path.join(copy, "src")
+    env.setdefault("OPENAI_API_KEY", "bench")
+    return subprocess.Popen([sys.executable, "-m", "uvicorn", "quorum.oai_proxy:app", "--host", "127.0.0.1",
+                             "--port", str(port), "--workers", "1", "--log-level", "warning"],
+                            cwd=copy, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                            start_new_session=True)
 
 
 def scrape(port):
@@ -231,7 +298,11 @@ def main() -> int:
     ap.add_argument("--batch", type=int, default=0,
                     help="requests per step per rank (0: the scenario's default, 16384 headline / 4096 others)")
     ap.add_argument("--conns", type=int, default=64, help="concurrent client connections per rank")
-    ap.add_argument("--impl", default=os.environ.get("QMX_BENCH_IMPL", "native"), choices=["native", "python"])
+    ap.add_argument("--impl", default=os.environ.get("QMX_BENCH_IMPL", "native"),
+                    choices=["native", "python", "reference"],
+                    help="reference: the unmodified upstream proxy (scratch copy of --ref-root) under uvicorn, "
+                         "same mocks and load generator (same-harness baseline)")
+    ap.add_argument("--ref-root", default=os.environ.get("QMX_REF_ROOT", "/root/reference"))
     ap.add_argument("--engine", default=os.environ.get("QMX_BENCH_ENGINE", "auto"))
     ap.add_argument("--workers", type=int, default=4, help="python impl: proxy processes per rank")
     ap.add_argument("--threads", type=int, default=0,
@@ -250,8 +321,11 @@ def main() -> int:
     sc = SCENARIOS[args.scenario]
     if "conns" in sc and args.conns == 64:  # scenario default unless set explicitly
         args.conns = sc["conns"]
+    if args.impl == "reference" and args.conns == 64:
+        args.conns = 16  # the survey's reference rows (16 clients)
     if args.batch <= 0:
-        args.batch = sc.get("batch", 4096)
+        # the reference serves ~9 req/s: 64 requests per step keeps a default run in minutes
+        args.batch = 64 if args.impl == "reference" else sc.get("batch", 4096)
     skip_final = bool(args.skip_final) if args.scenario == "headline" else sc["skip"]
 
     rank = int(os.environ.get("RANK", "0"))
@@ -294,75 +368,80 @@ def main() -> int:
 
     procs = []
     tmp = tempfile.mkdtemp(prefix=f"qmx_bench_r{rank}_")
-    restarts = 0
+    ok = True
     try:
         mock_ports = [args.port + 100 + rank * 10 + i for i in range(sc["n"])]
-
-        def spawn_mock(i, p):
-            return subprocess.Popen([os.path.join(bin_dir, "qmx_mock"), "--port", str(p), "--threads",
-                                     str(args.mock_threads), "--tokens", "20", "--think", "1"]
-                                    + sc.get("mock_args", []) + sc["faults"].get(i, []),
-                                    stderr=subprocess.DEVNULL, start_new_session=True)
         for i, p in enumerate(mock_ports):
-            procs.append(spawn_mock(i, p))
+            procs.append(subprocess.Popen([os.path.join(bin_dir, "qmx_mock"), "--port", str(p), "--threads",
+                                           str(args.mock_threads), "--tokens", "20", "--think", "1"]
+                                          + sc.get("mock_args", []) + sc["faults"].get(i, []),
+                                          stderr=subprocess.DEVNULL, start_new_session=True))
         cfg_path = os.path.join(tmp, "config.yaml")
         write_config(cfg_path, mock_ports, skip_final, args.tile, sc, args.placement)
+        spec_path = os.path.join(tmp, "expect.txt")
+        expect_spec(spec_path, sc, skip_final, mock_expected(bin_dir))
         env = dict(os.environ)
         if args.placement == "spread" and world > 1:
             nonce = [str(time.time_ns()) if rank == 0 else None]
             dist.broadcast_object_list(nonce, src=0)
             env.update(exchange_env(rank, world, args.port, nonce[0]))
         mock_procs = list(procs)
-        proxy_procs = spawn_workers(cfg_path, "127.0.0.1", args.port, args.workers, engine,
-                               device, impl=args.impl, threads=args.threads, env=env)
+        proxy_port = args.port
+        if args.impl == "reference":
+            proxy_port = args.port + rank  # uvicorn binds without SO_REUSEPORT: a port per rank
+            proxy_procs = [spawn_reference(args.ref_root, tmp, cfg_path, proxy_port)]
+        else:
+            proxy_procs = spawn_workers(cfg_path, "127.0.0.1", args.port, args.workers, engine,
+                                        device, impl=args.impl, threads=args.threads, env=env)
         procs += proxy_procs
-        if not wait_healthy("127.0.0.1", args.port, 180):
-            raise RuntimeError("proxy did not become healthy")
+        if not wait_healthy("127.0.0.1", proxy_port, 180):
+            raise RuntimeError(f"proxy did not become healthy: {[exit_status(p) for p in proxy_procs]}")
         xchg_kind = os.environ.get("QMX_XCHG", "rccl" if engine == "hip" else "tcp")
         if dist is not None:
             dist.barrier()
-        # warmup
+        # the reference has no /v1 prefix (oai_proxy.py:959); qmx serves both
+        path = "/chat/completions" if args.impl == "reference" else "/v1/chat/completions"
+        warm = {}
         if args.warmup > 0:
-            loadgen(bin_dir, args.port, args.conns, args.warmup * args.batch, args.lg_threads, args.timeout)
-        # a server process that died during warmup is reported (stderr + "restarts" in the JSON
-        # line) and started again once, so the timed steps measure a live stack
-        dead = [(i, q.returncode) for i, q in enumerate(mock_procs + proxy_procs) if q.poll() is not None]
-        if dead:
-            print(f"bench rank {rank}: server process(es) exited during warmup (index, code): {dead}",
-                  file=sys.stderr, flush=True)
-            restarts += len(dead)
-            for i, _ in dead:
-                if i < len(mock_procs):
-                    mock_procs[i] = spawn_mock(i, mock_ports[i])
-                    procs.append(mock_procs[i])
-            if any(i >= len(mock_procs) for i, _ in dead):
-                _kill(proxy_procs)
-                proxy_procs = spawn_workers(cfg_path, "127.0.0.1", args.port, args.workers, engine,
-                                            device, impl=args.impl, threads=args.threads, env=env)
-                procs += proxy_procs
-            if not wait_healthy("127.0.0.1", args.port, 180):
-                raise RuntimeError("proxy did not become healthy after restart")
-            loadgen(bin_dir, args.port, args.conns, max(1, args.warmup) * args.batch, args.lg_threads,
-                    args.timeout)
+            warm = loadgen(bin_dir, proxy_port, args.conns, args.warmup * args.batch, args.lg_threads, args.timeout,
+                           spec_path, path)
+
+        def casualties():
+            return [dict(exit_status(q), role="mock" if i < len(mock_procs) else "proxy")
+                    for i, q in enumerate(mock_procs + proxy_procs) if q.poll() is not None]
+
+        dead_warm = casualties()  # a process that died in warmup fails the run (no silent restart)
+        if dead_warm:
+            print(f"bench rank {rank}: server process(es) exited during warmup: {dead_warm}", file=sys.stderr,
+                  flush=True)
         if dist is not None:
             dist.barrier()
         if use_cuda:
             torch.cuda.synchronize()
-        m0 = scrape(args.port)
+        m0 = scrape(proxy_port) if args.impl == "native" else {}
         c0 = cpu_snapshot(mock_procs, proxy_procs)
         t0 = time.perf_counter()
-        stats = loadgen(bin_dir, args.port, args.conns, args.steps * args.batch, args.lg_threads, args.timeout)
+        stats = loadgen(bin_dir, proxy_port, args.conns, args.steps * args.batch, args.lg_threads, args.timeout,
+                        spec_path, path)
         if use_cuda:
             torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
         elapsed = time.perf_counter() - t0
         c1 = cpu_snapshot(mock_procs, proxy_procs)
-        bd = breakdown(m0, scrape(args.port), elapsed) if args.impl == "native" else {}
+        bd = breakdown(m0, scrape(proxy_port), elapsed) if args.impl == "native" else {}
         bd.update(cpu_breakdown(c0, c1, stats["completed"], elapsed))
+        dead = casualties()
+        if dead and not dead_warm:
+            print(f"bench rank {rank}: server process(es) exited during the timed steps: {dead}", file=sys.stderr,
+                  flush=True)
+        bad = (stats["invalid"] + stats["no_content"] + stats["errors"] + stats["non200"]
+               + warm.get("invalid", 0) + warm.get("errors", 0) + warm.get("non200", 0) + len(dead)
+               + (args.steps * args.batch - stats["completed"]))
         local = [elapsed, float(stats["completed"]), float(stats["ttft_p50_ms"]), float(stats["ttft_p99_ms"]),
                  float(stats["errors"] + stats["non200"]), float(stats["ttfb_p50_ms"]), float(stats["lat_p50_ms"]),
-                 float(restarts)]
+                 float(len(dead)), float(stats["invalid"]), float(stats["no_content"]), float(stats["validated"]),
+                 float(bad)]
         if dist is not None:
             t = torch.tensor(local, dtype=torch.float64, device="cuda" if coll_cuda else "cpu")
             gathered = [torch.zeros_like(t) for _ in range(world)]
@@ -370,11 +449,13 @@ def main() -> int:
             rows = [g.cpu().tolist() for g in gathered]
         else:
             rows = [local]
+        ok = all(r[11] == 0 for r in rows)
         if rank == 0:
             max_el = max(r[0] for r in rows)
             total = sum(r[1] for r in rows)
             value = total / max_el
             p50 = statistics.median(r[2] for r in rows)
+            baseline = sc["baseline"] if args.impl != "reference" else None
             res = {
                 "metric": "proxied req/sec (whole node) + p50 TTFT, 2-backend concatenate stream at 1/2/4/8 GPU"
                           if args.scenario == "headline" else f"proxied req/sec (whole node) + p50 TTFT, {args.scenario}",
@@ -386,17 +467,19 @@ def main() -> int:
                 "ms_per_step": round(1000.0 * max_el / args.steps, 3),
                 "higher_is_better": True,
                 "scaling": "weak",
-                "vs_baseline": round(value / sc["baseline"], 3) if sc["baseline"] else None,
+                "vs_baseline": round(value / baseline, 3) if baseline else None,
                 "dtype": "bytes (utf-8 SSE text; no float compute)",
                 "data": "synthetic: C++ mock backends (role + 4 split <think> fragments + 20 tokens + stop + "
-                        "[DONE]) and C++ closed-loop load generator",
+                        "[DONE]) and C++ closed-loop load generator; every response validated against the "
+                        "expected event contract",
                 "config": {"model": f"{sc['desc']}, skip_final_aggregation={skip_final}",
                            "global_batch": args.batch * world, "seq_len": 26,
                            "parallelism": f"dp{world} (sessions sharded over GPUs via SO_REUSEPORT)"
                                           + (f" + ep{world} (backend streams spread over ranks, "
-                                                f"{xchg_kind.upper()} all-gather exchange)"
+                                                f"{xchg_kind.upper()} exchange)"
                                              if args.placement == "spread" and world > 1 else ""),
-                           "impl": args.impl, "engine": engine, "conns_per_rank": args.conns,
+                           "impl": args.impl, "engine": engine if args.impl != "reference" else "reference",
+                           "conns_per_rank": args.conns,
                            "io_threads_per_rank": args.threads, "cpu_pinning": pinning,
                            "gpu_links": {k: v for k, v in link_summary().items() if k != "links_per_gpu"}},
                 "p50_ttft_ms": round(p50, 3),
@@ -404,17 +487,28 @@ def main() -> int:
                 "p50_ttfb_ms": round(statistics.median(r[5] for r in rows), 3),
                 "p50_latency_ms": round(statistics.median(r[6] for r in rows), 3),
                 "errors": int(sum(r[4] for r in rows)),
-                "server_restarts_in_warmup": int(sum(r[7] for r in rows)),
+                # validation: every completed response is checked by the load generator
+                "validated": int(sum(r[10] for r in rows)),
+                "invalid": int(sum(r[8] for r in rows)),
+                "no_content": int(sum(r[9] for r in rows)),
+                "processes_exited": int(sum(r[7] for r in rows)),
+                "valid": ok,
                 "baseline_p50_ttft_ms_16_clients": 1605,
                 # one rank proxy process counters over the timed region (SURVEY §5.1 time breakdown;
                 # with N>1 the shared port answers from any rank)
                 "breakdown_one_rank": bd,
             }
+            if dead or dead_warm:
+                res["exited"] = dead or dead_warm
             print(json.dumps(res), flush=True)
     finally:
         _kill(procs)
         if dist is not None:
             dist.destroy_process_group()
+    if not ok:
+        print("bench: INVALID run (responses failed validation, requests missing, or a server process "
+              "exited): see 'invalid' / 'exited' in the JSON line", file=sys.stderr, flush=True)
+        return 1
     return 0
 
 

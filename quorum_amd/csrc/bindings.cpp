@@ -37,7 +37,8 @@ struct PyStripper {
   py::bytes strip(const std::string& s) { return py::bytes(strip_final(ts, (const uint8_t*)s.data(), s.size())); }
 };
 
-py::tuple tick_to_py(HostEngine& e, int64_t created, int lane = 0, std::vector<int>* taken = nullptr) {
+py::tuple tick_to_py(HostEngine& e, int64_t created, int lane = 0, std::vector<int>* taken = nullptr,
+                     bool with_gen = false) {
   std::vector<SlotResult> results;
   std::vector<FinalizeRes> fres;
   {
@@ -45,7 +46,10 @@ py::tuple tick_to_py(HostEngine& e, int64_t created, int lane = 0, std::vector<i
     e.tick(created, results, fres, lane, taken);
   }
   py::list r;
-  for (auto& x : results) r.append(py::make_tuple(x.slot, py::bytes(x.sse), x.flags));
+  for (auto& x : results) {
+    if (with_gen) r.append(py::make_tuple(x.slot, py::bytes(x.sse), x.flags, x.gen));
+    else r.append(py::make_tuple(x.slot, py::bytes(x.sse), x.flags));
+  }
   py::list f;
   for (auto& x : fres) {
     if (x.kind == 0) {
@@ -63,7 +67,14 @@ py::tuple tick_to_py(HostEngine& e, int64_t created, int lane = 0, std::vector<i
 
 template <class E>
 void bind_engine(py::class_<E>& c) {
-  c.def("open", &E::open, py::arg("index"), py::arg("filter"), py::arg("emit"))
+  c.def("open", [](E& e, int index, bool filter, bool emit) { return e.open(index, filter, emit); },
+        py::arg("index"), py::arg("filter"), py::arg("emit"))
+      // (slot, generation): a slot's results carry the generation of the open() they belong to
+      .def("open_gen", [](E& e, int index, bool filter, bool emit) {
+        uint32_t g = 0;
+        int slot = e.open(index, filter, emit, &g);
+        return py::make_tuple(slot, g);
+      })
       .def("feed", [](E& e, int slot, const py::bytes& b) { e.feed(slot, std::string(b)); })
       .def("finish", &E::finish)
       .def("release", &E::release)
@@ -76,6 +87,12 @@ void bind_engine(py::class_<E>& c) {
       .def("tick_unsettled", [](E& e, int64_t created, int lane) {
         std::vector<int> taken;
         py::tuple t = tick_to_py(e, created, lane, &taken);
+        return py::make_tuple(t[0], t[1], taken);
+      })
+      // same, results as (slot, sse, flags, generation)
+      .def("tick_unsettled_gen", [](E& e, int64_t created, int lane) {
+        std::vector<int> taken;
+        py::tuple t = tick_to_py(e, created, lane, &taken, true);
         return py::make_tuple(t[0], t[1], taken);
       })
       .def("settle", [](E& e, const std::vector<int>& taken) {

@@ -283,7 +283,7 @@ void finalize_texts(const TagSet& ts, const std::vector<std::string>& texts, con
 // --------------------------------------------------------------------------------
 HostEngine::HostEngine(const std::vector<std::string>& tags) : ts_(make_tagset(tags)) {}
 
-int HostEngine::open(int index, bool filter, bool emit) {
+int HostEngine::open(int index, bool filter, bool emit, uint32_t* gen) {
   std::lock_guard<std::mutex> g(mu_);
   int slot;
   if (!free_.empty()) {
@@ -295,8 +295,11 @@ int HostEngine::open(int index, bool filter, bool emit) {
     core_.emplace_back();
   }
   Meta& m = meta_[slot];
+  const uint32_t ng = m.gen + 1;
   m = Meta();
   m.live = true;
+  m.gen = ng;
+  if (gen) *gen = ng;
   SlotCore& c = core_[slot];
   c = SlotCore();
   c.index = index;
@@ -436,6 +439,9 @@ bool HostEngine::tick(int64_t created, std::vector<SlotResult>& results, std::ve
   {
     std::lock_guard<std::mutex> g(mu_);
     bytes_out_ += out;
+    // a taken slot stays busy until settled, so it cannot be re-opened meanwhile: its
+    // generation is the one the results belong to
+    for (auto& r : results) r.gen = meta_[r.slot].gen;
   }
   if (!fin.empty()) finalize(fin, fres, lane);
   if (!taken) settle(slots);

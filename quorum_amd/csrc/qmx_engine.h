@@ -77,6 +77,10 @@ struct SlotResult {
   int slot;
   std::string sse;
   int flags;
+  // open() generation of the slot this result belongs to: a slot released while its tick
+  // is in flight can be re-opened by another session before the result is applied; the
+  // consumer drops results whose generation is not the one it opened (stamped by tick()).
+  uint32_t gen = 0;
 };
 struct FinalizeReq {
   int id;
@@ -122,7 +126,8 @@ class HostEngine {
   explicit HostEngine(const std::vector<std::string>& tags);
   virtual ~HostEngine() = default;
 
-  int open(int index, bool filter, bool emit);
+  // returns the slot; *gen (optional) receives the slot's open generation (SlotResult::gen)
+  int open(int index, bool filter, bool emit, uint32_t* gen = nullptr);
   void feed(int slot, const std::string& data);
   void finish(int slot);
   void release(int slot);
@@ -169,6 +174,7 @@ class HostEngine {
     bool fresh = true;
     bool closed = false;  // DONE/ABORTED reported
     bool busy = false;    // taken by an unsettled tick (in flight on some lane)
+    uint32_t gen = 0;     // bumped by every open()
     std::string incoming;
   };
 

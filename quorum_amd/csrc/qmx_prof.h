@@ -16,4 +16,14 @@ void prof_start();   // no-op unless QMX_PROF is set (idempotent)
 void prof_thread();  // add a per-thread CPU-time sampler for the calling thread (if on)
 void prof_stop();   // stop sampling, write the profile
 
+// Fatal-signal reporting (SIGSEGV / SIGBUS / SIGFPE / SIGILL / SIGABRT and std::terminate):
+// writes "qmx fatal: <signal> in thread <tid>" plus the faulting thread's backtrace
+// (module+offset frames, symbolise with tools/cpuprof.py or llvm-symbolizer) to stderr on
+// an alternate signal stack, then hands the signal to the previously installed handler
+// (Python's faulthandler in a worker process) or the default action, so the exit status
+// still reports the signal.  Idempotent; installs an alternate stack for the caller only
+// (crash_thread() adds one per thread).
+void crash_handler_install();
+void crash_thread();
+
 }  // namespace qmx

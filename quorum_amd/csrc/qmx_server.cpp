@@ -288,6 +288,7 @@ struct Client {
   bool close_after = false;  // graceful: close once output is flushed
   bool queued = false;       // in the loop's end-of-iteration flush list
   int served = 0;            // requests handled on this connection
+  uint64_t serial = 0;       // per-loop connection serial (fd numbers are reused)
   double t_accept = 0;
   bool want_out = false;     // EPOLLOUT armed (socket buffer was full)
 };
@@ -374,9 +375,10 @@ std::atomic<uint64_t> c_verify_checked{0}, c_verify_mismatch{0};
 class Verifier {
  public:
   explicit Verifier(const std::vector<std::string>& tags) : cpu_(tags) {}
-  void open(int slot, int index, bool f, bool e) {
+  void open(int slot, uint32_t gen, int index, bool f, bool e) {
     std::lock_guard<std::mutex> g(mu_);
     Track t;
+    t.gen = gen;
     t.shadow = cpu_.open(index, f, e);
     rmap_[t.shadow] = slot;
     map_[slot] = std::move(t);
@@ -422,7 +424,7 @@ class Verifier {
     std::lock_guard<std::mutex> g(mu_);
     for (auto& x : r) {
       auto it = map_.find(x.slot);
-      if (it == map_.end()) continue;
+      if (it == map_.end() || it->second.gen != x.gen) continue;  // stale: slot re-opened
       it->second.acc[0] += x.sse;
       it->second.term[0] |= x.flags & (RF_DONE | RF_ABORTED);
     }
@@ -468,6 +470,7 @@ class Verifier {
  private:
   struct Track {
     int shadow = -1;
+    uint32_t gen = 0;
     std::string acc[2];
     int term[2] = {0, 0};
     bool compared = false;
@@ -534,14 +537,14 @@ class GpuHub {
     for (int i = 0; i < lanes_; ++i) th_.emplace_back([this, i] { run(i); });
   }
   void attach(int loop, Sink s) { sinks_[loop] = std::move(s); }
-  int open(int loop, int index, bool f, bool e) {
-    int slot = eng_->open(index, f, e);
+  int open(int loop, int index, bool f, bool e, uint32_t* gen) {
+    int slot = eng_->open(index, f, e, gen);
     {
       std::lock_guard<std::mutex> g(omu_);
       if ((int)owner_.size() <= slot) owner_.resize(slot + 1024, -1);
       owner_[slot] = loop;
     }
-    if (ver_) ver_->open(slot, index, f, e);
+    if (ver_) ver_->open(slot, *gen, index, f, e);
     return slot;
   }
   void feed(int slot, const std::string& d) {
@@ -583,6 +586,7 @@ class GpuHub {
  private:
   void run(int lane) {
     prof_thread();
+    crash_thread();
     if (cfg_.engine == "hip") hipSetDevice(cfg_.device);
     std::vector<ResultBatch> per(sinks_.size());
     std::vector<int> taken;
@@ -700,6 +704,7 @@ class Loop {
 
   void run() {
     prof_thread();
+    crash_thread();
     setup();
     if (++g_ready == cfg_.threads && !cfg_.ready_file.empty()) {
       FILE* f = fopen(cfg_.ready_file.c_str(), "w");  // supervisor: this generation is serving
@@ -752,11 +757,12 @@ class Loop {
   void release_deferred(double t) {
     size_t k = 0;
     for (size_t i = 0; i < deferq_.size(); ++i) {
-      auto it = clients_.find(deferq_[i].first);
+      auto it = clients_.find(deferq_[i].fd);
       if (it == clients_.end()) continue;
       Client* c = it->second.get();
+      if (c->serial != deferq_[i].serial) continue;  // fd closed and reused by a new connection
       if (c->queued || c->want_out || c->dead || c->out_off >= c->out.size()) continue;
-      if (deferq_[i].second <= t || g_drain.load()) {
+      if (deferq_[i].deadline <= t || g_drain.load()) {
         c->queued = true;
         flushq_.push_back(c->fd);
         continue;
@@ -853,9 +859,13 @@ class Loop {
   void apply(ResultBatch& rb) {
     for (auto& r : rb.r) {
       auto it = slot_owner_.find(r.slot);
-      if (it == slot_owner_.end()) continue;
-      Session* s = it->second.first;
-      int bi = it->second.second;
+      // a result of an earlier session on this slot (ended while its tick was in flight; the
+      // slot was freed and re-opened before this batch was applied) is dropped
+      if (it == slot_owner_.end() || it->second.gen != r.gen) continue;
+      Session* s = it->second.s;
+      int bi = it->second.bi;
+      if (fault_drop_every_ > 0 && !r.sse.empty() && ++fault_n_ % fault_drop_every_ == 0)
+        r.sse.clear();  // QMX_FAULT_DROP_DELTA: fault injection (the bench's validator must notice)
       if (!r.sse.empty()) {
         if (s->kind == K_REMOTE) post_owner(s, X_DATA, 0, 0, r.sse);
         else if (s->cl) send_content(s, r.sse);
@@ -880,10 +890,17 @@ class Loop {
   }
   void kick() { kick_ = true; }
   // engine calls, mirrored into the verify shadow when enabled
-  int e_open(int index, bool f, bool e) {
-    if (hub_) return hub_->open(idx_, index, f, e);
-    int slot = eng_->open(index, f, e);
-    if (ver_) ver_->open(slot, index, f, e);
+  // opens an engine slot for stream `bi` of session s and registers its owner
+  int e_open(Session* s, int bi, int index, bool f, bool e) {
+    uint32_t gen = 0;
+    int slot;
+    if (hub_) {
+      slot = hub_->open(idx_, index, f, e, &gen);
+    } else {
+      slot = eng_->open(index, f, e, &gen);
+      if (ver_) ver_->open(slot, gen, index, f, e);
+    }
+    slot_owner_[slot] = SlotOwner{s, bi, gen};
     return slot;
   }
   // feed / finish / release are queued in order and handed to the engine once per loop
@@ -946,6 +963,7 @@ class Loop {
       setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
       auto c = std::make_unique<Client>();
       c->fd = fd;
+      c->serial = ++next_serial_;
       c->t_accept = now_s();
       add(fd, EPOLLIN, tag(3, fd));
       clients_[fd] = std::move(c);
@@ -1710,7 +1728,7 @@ class Loop {
     if (defer && s->cl->queued && !flushq_.empty() && flushq_.back() == s->cl->fd) {
       flushq_.pop_back();  // un-queue: the first content (or the deadline) sends it
       s->cl->queued = false;
-      deferq_.emplace_back(s->cl->fd, now_s() + role_defer_s_);
+      deferq_.push_back(Deferred{s->cl->fd, s->cl->serial, now_s() + role_defer_s_});
     }
     s->bs.resize(valid.size());
     // spread placement (EP analog): backend i of a session owned by rank r runs on rank
@@ -1728,8 +1746,7 @@ class Loop {
         s->remote_n++;
         continue;
       }
-      s->bs[i].slot = e_open((int)i, s->filter, s->emit);
-      slot_owner_[s->bs[i].slot] = {s, (int)i};
+      s->bs[i].slot = e_open(s, (int)i, (int)i, s->filter, s->emit);
     }
     for (size_t i = 0; i < valid.size(); ++i) {
       std::string body, msg;
@@ -1871,8 +1888,7 @@ class Loop {
         s->emit = (m.flags & 2) != 0;
         s->bs.resize(1);
         s->bs[0].backend = m.a;
-        s->bs[0].slot = e_open(m.bi, s->filter, s->emit);
-        slot_owner_[s->bs[0].slot] = {s, 0};
+        s->bs[0].slot = e_open(s, 0, m.bi, s->filter, s->emit);
         shadow_[{m.skey, m.bi}] = s;
         c_remote_streams++;
         Up* u = (m.a >= 0 && m.a < (int)cfg_.backends.size())
@@ -2370,7 +2386,12 @@ class Loop {
   std::unordered_map<int, std::unique_ptr<Client>> clients_;
   std::unordered_map<int, std::unique_ptr<Up>> ups_;
   std::unordered_map<Session*, std::unique_ptr<Session>> sessions_;
-  std::unordered_map<int, std::pair<Session*, int>> slot_owner_;
+  struct SlotOwner {
+    Session* s;
+    int bi;
+    uint32_t gen;  // open generation: results of an earlier owner of the slot are dropped
+  };
+  std::unordered_map<int, SlotOwner> slot_owner_;
   std::unordered_map<int, std::pair<Session*, int>> fin_owner_;  // fin id → (session, bs index | -1)
   // spread placement
   Exchange* xch_ = nullptr;
@@ -2393,12 +2414,24 @@ class Loop {
   // parallel streams: the SSE head + role event wait (corked, not queued) for the first
   // content of the same session or this deadline, whichever comes first — one client send
   // per request instead of two when the tick answers within it (QMX_ROLE_DEFER_US, 0: off)
-  std::vector<std::pair<int, double>> deferq_;
+  struct Deferred {
+    int fd;
+    uint64_t serial;  // the connection the head belongs to (its fd may be reused after a close)
+    double deadline;
+  };
+  std::vector<Deferred> deferq_;
+  uint64_t next_serial_ = 0;
   const double role_defer_s_ = [] {
     const char* e = getenv("QMX_ROLE_DEFER_US");
     return (e ? atof(e) : 1000.0) * 1e-6;
   }();
   std::vector<EngineOp> ops_;  // engine feed / finish / release of this iteration (flush_ops)
+  // fault injection (tests): drop every Nth stream result's SSE bytes before it is sent
+  const long fault_drop_every_ = [] {
+    const char* e = getenv("QMX_FAULT_DROP_DELTA");
+    return e ? atol(e) : 0L;
+  }();
+  long fault_n_ = 0;
 };
 
 void on_signal(int sig) {
@@ -2410,6 +2443,7 @@ void on_signal(int sig) {
 
 int run_server(const ServerCfg& cfg0) {
   ServerCfg cfg = cfg0;
+  crash_handler_install();  // a native fault leaves a backtrace on stderr, not a silent exit
   prof_start();  // QMX_PROF=<path>: CPU sampling profile of this process (qmx_prof.h)
   bool any_https = false;
   for (auto& b : cfg.backends) {

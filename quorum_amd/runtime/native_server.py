@@ -95,7 +95,13 @@ def cluster_config(rt: RuntimeConfig, port: int, engine: str) -> Dict[str, Any]:
 
 
 def run_native(config: str, host: str, port: int, engine: str, device: Optional[int], threads: int) -> int:
+    import faulthandler
+
     from ..ops import native
+
+    # a native fault is reported by the server's own handler (module+offset backtrace),
+    # which then chains to this one for the Python side of the stack
+    faulthandler.enable(all_threads=True)
 
     ext = native.require()
     cfg = load_config(config)

@@ -11,12 +11,15 @@ Replaces the reference's 100 ms polling loop (``src/quorum/oai_proxy.py:554-747`
 from __future__ import annotations
 
 import asyncio
+import logging
 import time
 from concurrent.futures import ThreadPoolExecutor
 from typing import Dict, List, Optional
 
 from ..ops.engine import F_ABORTED, F_DONE, FinalizeRequest
 from ..utils import metrics
+
+_log = logging.getLogger("qmx.ticker")
 
 
 class SessionStreams:
@@ -65,6 +68,7 @@ class Ticker:
             ThreadPoolExecutor(max_workers=1, thread_name_prefix="qmx-tick") if engine.offload else None)
         self._task = loop.create_task(self._run())
         self.ticks = 0
+        self.failures = 0  # engine ticks that raised (the ticker survives them)
 
     # session API ------------------------------------------------------------
     def open_session(self, n: int, filter_think: bool, emit: bool) -> SessionStreams:
@@ -110,11 +114,17 @@ class Ticker:
                 else:
                     results, fres = self.engine.tick(created)
             except Exception as exc:  # noqa: BLE001 - never kill the ticker; fail the waiters
+                self.failures += 1
+                _log.error("engine tick failed (%s); failing the sessions in flight", exc)
                 for fut in self._futures.values():
                     if not fut.done():
                         fut.set_exception(exc)
                 self._futures.clear()
-                raise
+                # the batch's outputs are lost: end every live stream (as failed) so no
+                # session waits for results that will never come; new sessions keep working
+                for slot, owner in list(self._owners.items()):
+                    owner.fail(slot)
+                continue  # the next feed wakes the ticker again (no busy retry of a failing tick)
             self.ticks += 1
             metrics.observe_tick(time.perf_counter() - t0, len(results))
             for slot, data, flags in results:

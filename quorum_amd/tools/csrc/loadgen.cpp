@@ -1,12 +1,31 @@
-// qmx_loadgen — closed-loop HTTP/1.1 load generator for OpenAI-style streaming endpoints.
+// qmx_loadgen — closed-loop HTTP/1.1 load generator for OpenAI-style streaming endpoints,
+// with per-response validation.
 //
 // C keep-alive connections (spread over T epoll threads) each issue POST requests back to
 // back until R requests have completed.  Per request it records TTFB (first SSE `data:`
 // byte), TTFT (first SSE event carrying a non-empty "content") and total latency, parsing
 // chunked or content-length bodies incrementally.  Prints one JSON line of statistics.
 //
+// Validation (--expect FILE): every completed response is checked against the expected
+// event contract of the proxy (quorum's progress_streaming_aggregator, reference
+// src/quorum/oai_proxy.py:530-885): status 200, the role event first, `data: [DONE]` last
+// and exactly once, every event well-formed JSON-in-SSE with a known id, per-backend
+// concatenated delta content equal to (or, for a stream allowed to fail, a prefix of) the
+// text the mock backend streams, and the final event absent / one of the allowed texts.
+// A response that fails any check counts in "invalid" (the first few are printed to
+// stderr); completed = valid + invalid.  Spec file, one directive per line, texts hex:
+//     role 1                       role event first (id chatcmpl-parallel)
+//     done 1                       [DONE] last
+//     stream <id> exact|prefix <hex>
+//     final absent | final any <hex> [<hex> ...]
+//     error allowed|absent         the all-failed "error" event
+//
+// --abort-rate P: a request is abandoned (socket closed mid-stream, right after its first
+// content event) with probability P — client-abort churn for the data plane's session
+// teardown paths; abandoned requests are counted in "aborted", not "completed".
+//
 //   qmx_loadgen --port 8000 --conns 64 --requests 5000 [--threads 2] [--path /v1/chat/completions]
-//               [--body-file req.json] [--stream 1]
+//               [--body-file req.json] [--stream 1] [--expect spec.txt] [--abort-rate 0]
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netinet/in.h>
@@ -24,6 +43,7 @@
 #include <cstring>
 #include <fstream>
 #include <mutex>
+#include <random>
 #include <sstream>
 #include <string>
 #include <thread>
@@ -31,6 +51,20 @@
 
 namespace {
 using Clock = std::chrono::steady_clock;
+
+struct StreamSpec {
+  std::string id;
+  bool exact = true;
+  std::string text;
+};
+struct Spec {
+  bool on = false;
+  bool role = true, done = true;
+  std::vector<StreamSpec> streams;
+  bool final_absent = true;
+  std::vector<std::string> final_any;
+  bool error_allowed = false;
+};
 
 struct Opts {
   std::string host = "127.0.0.1";
@@ -42,9 +76,12 @@ struct Opts {
   std::string body;
   bool stream = true;
   double timeout_s = 60;
+  double abort_rate = 0.0;
+  Spec spec;
 } g;
 
-std::atomic<long> g_issued{0}, g_done{0}, g_errors{0}, g_non200{0}, g_no_content{0};
+std::atomic<long> g_issued{0}, g_done{0}, g_errors{0}, g_non200{0}, g_no_content{0}, g_invalid{0},
+    g_aborted{0}, g_validated{0};
 std::mutex g_mu;
 std::vector<double> g_ttft, g_ttfb, g_lat;
 
@@ -60,7 +97,9 @@ struct Conn {
   long chunk_left = -1;
   int status = 0;
   bool got_data = false, got_content = false;
+  bool abort_this = false;
   std::string tail;  // SSE scan carry
+  std::string body;  // decoded body (validation)
   Clock::time_point t0, t_data, t_content;
   bool active = false;
 };
@@ -81,8 +120,317 @@ int connect_to() {
   return fd;
 }
 
+// ---------------------------------------------------------------------------------------
+// validation: a small strict JSON reader for the proxy's SSE events
+// ---------------------------------------------------------------------------------------
+struct JR {
+  const char* p;
+  const char* e;
+  bool ok = true;
+  void ws() {
+    while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) ++p;
+  }
+  bool lit(const char* s) {
+    size_t n = strlen(s);
+    if ((size_t)(e - p) < n || memcmp(p, s, n) != 0) return ok = false;
+    p += n;
+    return true;
+  }
+  static int hexv(char c) {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+  }
+  static void put_utf8(uint32_t cp, std::string& o) {
+    if (cp < 0x80) {
+      o.push_back((char)cp);
+    } else if (cp < 0x800) {
+      o.push_back((char)(0xC0 | (cp >> 6)));
+      o.push_back((char)(0x80 | (cp & 0x3F)));
+    } else if (cp < 0x10000) {
+      o.push_back((char)(0xE0 | (cp >> 12)));
+      o.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+      o.push_back((char)(0x80 | (cp & 0x3F)));
+    } else {
+      o.push_back((char)(0xF0 | (cp >> 18)));
+      o.push_back((char)(0x80 | ((cp >> 12) & 0x3F)));
+      o.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+      o.push_back((char)(0x80 | (cp & 0x3F)));
+    }
+  }
+  bool u4(uint32_t* v) {
+    if (e - p < 4) return ok = false;
+    uint32_t x = 0;
+    for (int i = 0; i < 4; ++i) {
+      int h = hexv(p[i]);
+      if (h < 0) return ok = false;
+      x = x * 16 + (uint32_t)h;
+    }
+    p += 4;
+    *v = x;
+    return true;
+  }
+  // string → UTF-8 (lone surrogates encoded as WTF-8, as the proxy's json.loads would keep them)
+  bool str(std::string* out) {
+    ws();
+    if (p >= e || *p != '"') return ok = false;
+    ++p;
+    while (p < e) {
+      const char c = *p++;
+      if (c == '"') return true;
+      if ((unsigned char)c < 0x20) return ok = false;
+      if (c != '\\') {
+        if (out) out->push_back(c);
+        continue;
+      }
+      if (p >= e) return ok = false;
+      const char d = *p++;
+      char r = 0;
+      switch (d) {
+        case '"': r = '"'; break;
+        case '\\': r = '\\'; break;
+        case '/': r = '/'; break;
+        case 'b': r = '\b'; break;
+        case 'f': r = '\f'; break;
+        case 'n': r = '\n'; break;
+        case 'r': r = '\r'; break;
+        case 't': r = '\t'; break;
+        case 'u': {
+          uint32_t cp;
+          if (!u4(&cp)) return false;
+          if (cp >= 0xD800 && cp < 0xDC00 && e - p >= 6 && p[0] == '\\' && p[1] == 'u') {
+            const char* save = p;
+            p += 2;
+            uint32_t lo;
+            if (u4(&lo) && lo >= 0xDC00 && lo < 0xE000) {
+              cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+            } else {
+              ok = true;
+              p = save;
+            }
+          }
+          if (out) put_utf8(cp, *out);
+          continue;
+        }
+        default: return ok = false;
+      }
+      if (out) out->push_back(r);
+    }
+    return ok = false;
+  }
+  bool skip_value(int depth = 0) {
+    ws();
+    if (p >= e || depth > 32) return ok = false;
+    if (*p == '"') return str(nullptr);
+    if (*p == '{' || *p == '[') {
+      const char close = *p == '{' ? '}' : ']';
+      const bool obj = *p == '{';
+      ++p;
+      ws();
+      if (p < e && *p == close) {
+        ++p;
+        return true;
+      }
+      while (true) {
+        if (obj) {
+          if (!str(nullptr)) return false;
+          ws();
+          if (p >= e || *p++ != ':') return ok = false;
+        }
+        if (!skip_value(depth + 1)) return false;
+        ws();
+        if (p < e && *p == ',') {
+          ++p;
+          continue;
+        }
+        if (p < e && *p == close) {
+          ++p;
+          return true;
+        }
+        return ok = false;
+      }
+    }
+    const char* s = p;
+    while (p < e && (isalnum((unsigned char)*p) || *p == '-' || *p == '+' || *p == '.')) ++p;
+    return p > s ? true : (ok = false);
+  }
+};
+
+struct Ev {
+  std::string id, content, finish;
+  bool has_content = false, has_role = false, content_null = false;
+};
+
+// {"id": ..., "choices": [{"delta": {"role"?, "content"?}, "finish_reason": ...}], ...}
+bool parse_event(const char* p, const char* e, Ev& ev) {
+  JR r{p, e};
+  r.ws();
+  if (!r.lit("{")) return false;
+  bool have_choices = false;
+  while (true) {
+    std::string key;
+    if (!r.str(&key)) return false;
+    r.ws();
+    if (!r.lit(":")) return false;
+    r.ws();
+    if (key == "id") {
+      if (!r.str(&ev.id)) return false;
+    } else if (key == "choices") {
+      if (!r.lit("[")) return false;
+      r.ws();
+      if (!r.lit("{")) return false;
+      while (true) {
+        std::string k2;
+        if (!r.str(&k2)) return false;
+        r.ws();
+        if (!r.lit(":")) return false;
+        r.ws();
+        if (k2 == "delta") {
+          if (!r.lit("{")) return false;
+          r.ws();
+          if (r.p < r.e && *r.p == '}') {
+            ++r.p;
+          } else {
+            while (true) {
+              std::string k3;
+              if (!r.str(&k3)) return false;
+              r.ws();
+              if (!r.lit(":")) return false;
+              r.ws();
+              if (k3 == "content") {
+                if (r.p < r.e && *r.p == 'n') {
+                  if (!r.lit("null")) return false;
+                  ev.content_null = true;
+                } else {
+                  if (!r.str(&ev.content)) return false;
+                  ev.has_content = true;
+                }
+              } else if (k3 == "role") {
+                ev.has_role = true;
+                if (!r.skip_value()) return false;
+              } else if (!r.skip_value()) {
+                return false;
+              }
+              r.ws();
+              if (r.p < r.e && *r.p == ',') {
+                ++r.p;
+                continue;
+              }
+              if (!r.lit("}")) return false;
+              break;
+            }
+          }
+        } else if (k2 == "finish_reason") {
+          if (r.p < r.e && *r.p == '"') {
+            if (!r.str(&ev.finish)) return false;
+          } else if (!r.lit("null")) {
+            return false;
+          }
+        } else if (!r.skip_value()) {
+          return false;
+        }
+        r.ws();
+        if (r.p < r.e && *r.p == ',') {
+          ++r.p;
+          continue;
+        }
+        if (!r.lit("}")) return false;
+        break;
+      }
+      r.ws();
+      if (!r.lit("]")) return false;  // exactly one choice
+      have_choices = true;
+    } else if (!r.skip_value()) {
+      return false;
+    }
+    r.ws();
+    if (r.p < r.e && *r.p == ',') {
+      ++r.p;
+      continue;
+    }
+    if (!r.lit("}")) return false;
+    break;
+  }
+  r.ws();
+  return r.p == r.e && have_choices && !ev.id.empty();
+}
+
+// returns "" when the response satisfies the spec, else a short reason
+std::string validate(int status, const std::string& body) {
+  const Spec& S = g.spec;
+  if (status != 200) return "status " + std::to_string(status);
+  std::vector<std::string> acc(S.streams.size());
+  std::vector<int> nev(S.streams.size(), 0);
+  bool saw_done = false, saw_final = false, saw_error = false;
+  std::string final_text;
+  size_t pos = 0;
+  int k = 0;
+  while (pos < body.size()) {
+    size_t j = body.find("\n\n", pos);
+    if (j == std::string::npos) return "trailing bytes after the last event";
+    const char* a = body.data() + pos;
+    const char* b = body.data() + j;
+    pos = j + 2;
+    if (saw_done) return "event after [DONE]";
+    if (b - a < 6 || memcmp(a, "data: ", 6) != 0) return "event without 'data: '";
+    a += 6;
+    if (b - a == 6 && memcmp(a, "[DONE]", 6) == 0) {
+      saw_done = true;
+      ++k;
+      continue;
+    }
+    Ev ev;
+    if (!parse_event(a, b, ev)) return "malformed event " + std::to_string(k);
+    if (k == 0 && S.role) {
+      if (ev.id != "chatcmpl-parallel" || !ev.has_role || ev.has_content) return "first event is not the role event";
+      ++k;
+      continue;
+    }
+    ++k;
+    if (ev.id == "chatcmpl-parallel-final") {
+      if (saw_final) return "two final events";
+      if (ev.finish != "stop" || !ev.has_content) return "bad final event";
+      saw_final = true;
+      final_text = ev.content;
+      continue;
+    }
+    if (ev.id == "error") {
+      saw_error = true;
+      continue;
+    }
+    size_t si = 0;
+    while (si < S.streams.size() && S.streams[si].id != ev.id) ++si;
+    if (si == S.streams.size()) return "unexpected event id " + ev.id;
+    if (!ev.has_content || ev.content.empty()) return "delta event without content (" + ev.id + ")";
+    if (saw_final) return "delta after the final event";
+    acc[si] += ev.content;
+    ++nev[si];
+  }
+  if (S.done && !saw_done) return "no [DONE]";
+  if (S.role && k == 0) return "empty body";
+  for (size_t si = 0; si < S.streams.size(); ++si) {
+    const StreamSpec& ss = S.streams[si];
+    if (ss.exact ? acc[si] != ss.text : ss.text.compare(0, acc[si].size(), acc[si]) != 0 ||
+                                            acc[si].size() > ss.text.size())
+      return "content of " + ss.id + " differs (" + std::to_string(acc[si].size()) + " B, " +
+             std::to_string(nev[si]) + " events)";
+  }
+  if (saw_error && !S.error_allowed) return "unexpected error event";
+  if (S.final_absent) {
+    if (saw_final) return "unexpected final event";
+  } else if (!saw_error || saw_final) {
+    if (!saw_final) return "no final event";
+    if (std::find(S.final_any.begin(), S.final_any.end(), final_text) == S.final_any.end())
+      return "final content differs (" + std::to_string(final_text.size()) + " B)";
+  }
+  return std::string();
+}
+
 // scan decoded body bytes for SSE markers
 void scan_sse(Conn& c, const char* p, size_t n, Clock::time_point now) {
+  if (g.spec.on) c.body.append(p, n);
+  if (c.got_data && c.got_content) return;
   std::string s = c.tail;
   s.append(p, n);
   if (!c.got_data && s.find("data:") != std::string::npos) {
@@ -108,6 +456,8 @@ void scan_sse(Conn& c, const char* p, size_t n, Clock::time_point now) {
   c.tail = s.size() > 16 ? s.substr(s.size() - 16) : s;
 }
 
+thread_local std::mt19937_64 t_rng(12345);
+
 bool start_request(Conn& c) {
   long k = g_issued.fetch_add(1);
   if (k >= g.requests) {
@@ -121,7 +471,9 @@ bool start_request(Conn& c) {
   c.chunk_left = -1;
   c.status = 0;
   c.got_data = c.got_content = false;
+  c.abort_this = g.abort_rate > 0 && std::uniform_real_distribution<double>(0, 1)(t_rng) < g.abort_rate;
   c.tail.clear();
+  c.body.clear();
   c.t0 = Clock::now();
   c.active = true;
   return true;
@@ -135,6 +487,17 @@ void finish_request(Conn& c, std::vector<double>& ttft, std::vector<double>& ttf
   if (c.got_data) ttfb.push_back(ms(c.t_data));
   if (c.got_content) ttft.push_back(ms(c.t_content));
   else g_no_content++;
+  if (g.spec.on) {
+    g_validated++;
+    std::string why = validate(c.status, c.body);
+    if (!why.empty()) {
+      const long n = g_invalid.fetch_add(1);
+      if (n < 5)
+        fprintf(stderr, "qmx_loadgen: invalid response (%s): %.600s\n", why.c_str(),
+                c.body.size() > 600 ? (c.body.substr(0, 300) + " ... " + c.body.substr(c.body.size() - 280)).c_str()
+                                    : c.body.c_str());
+    }
+  }
   g_done++;
   c.phase = 0;
 }
@@ -156,6 +519,10 @@ bool parse(Conn& c, bool* done) {
       c.in.erase(0, he + 4);
       c.phase = c.chunked ? 2 : 3;
       c.chunk_left = -1;
+      if (!c.chunked && c.remaining == 0) {
+        *done = true;
+        return true;
+      }
       continue;
     }
     if (c.phase == 3) {
@@ -170,22 +537,16 @@ bool parse(Conn& c, bool* done) {
       return true;
     }
     if (c.phase == 2) {
-      if (c.chunk_left < 0) {
+      if (c.chunk_left < 0 && c.chunk_left != -2) {
         size_t le = c.in.find("\r\n");
         if (le == std::string::npos) return true;
         long sz = strtol(c.in.c_str(), nullptr, 16);
         c.in.erase(0, le + 2);
         if (sz == 0) {
-          // trailer: expect "\r\n"
-          if (c.in.size() < 2) {
-            c.chunk_left = -2;
-            return true;
-          }
-          c.in.erase(0, 2);
-          *done = true;
-          return true;
+          c.chunk_left = -2;  // trailer: expect "\r\n"
+        } else {
+          c.chunk_left = sz;
         }
-        c.chunk_left = sz;
       }
       if (c.chunk_left == -2) {
         if (c.in.size() < 2) return true;
@@ -198,15 +559,9 @@ bool parse(Conn& c, bool* done) {
       c.in.erase(0, take);
       c.chunk_left -= take;
       if (c.chunk_left > 0) return true;
-      if (c.in.size() < 2) {
-        c.chunk_left = 0;
-        if (c.in.empty()) return true;
-      }
-      if (c.chunk_left == 0) {
-        if (c.in.size() < 2) return true;
-        c.in.erase(0, 2);
-        c.chunk_left = -1;
-      }
+      if (c.in.size() < 2) return true;  // chunk_left == 0: its CRLF has not arrived yet
+      c.in.erase(0, 2);
+      c.chunk_left = -1;
       continue;
     }
     return true;
@@ -214,12 +569,25 @@ bool parse(Conn& c, bool* done) {
 }
 
 void worker(int tid, int nconns, Clock::time_point deadline) {
+  t_rng.seed(12345 + 7919 * tid);
   int ep = epoll_create1(0);
   std::vector<Conn> cs(nconns);
   std::vector<double> ttft, ttfb, lat;
   std::string req = "POST " + g.path + " HTTP/1.1\r\nHost: " + g.host + "\r\ncontent-type: application/json\r\n"
                     "authorization: Bearer bench\r\ncontent-length: " + std::to_string(g.body.size()) + "\r\n\r\n" + g.body;
   int live = 0;
+  auto reconnect = [&](Conn& c, uint32_t idx) -> bool {
+    epoll_ctl(ep, EPOLL_CTL_DEL, c.fd, nullptr);
+    close(c.fd);
+    c.in.clear();
+    c.fd = connect_to();
+    if (c.fd < 0) return false;
+    epoll_event e{};
+    e.events = EPOLLIN | EPOLLOUT;
+    e.data.u32 = idx;
+    epoll_ctl(ep, EPOLL_CTL_ADD, c.fd, &e);
+    return true;
+  };
   for (int i = 0; i < nconns; ++i) {
     cs[i].fd = connect_to();
     if (cs[i].fd < 0) {
@@ -238,7 +606,8 @@ void worker(int tid, int nconns, Clock::time_point deadline) {
   while (live > 0 && Clock::now() < deadline) {
     int n = epoll_wait(ep, evs.data(), (int)evs.size(), 100);
     for (int k = 0; k < n; ++k) {
-      Conn& c = cs[evs[k].data.u32];
+      const uint32_t idx = evs[k].data.u32;
+      Conn& c = cs[idx];
       if (!c.active) continue;
       bool dead = false;
       if (evs[k].events & EPOLLOUT) {
@@ -253,7 +622,7 @@ void worker(int tid, int nconns, Clock::time_point deadline) {
         if (c.req_off >= c.req.size()) {
           epoll_event e{};
           e.events = EPOLLIN;
-          e.data.u32 = evs[k].data.u32;
+          e.data.u32 = idx;
           epoll_ctl(ep, EPOLL_CTL_MOD, c.fd, &e);
         }
       }
@@ -273,6 +642,18 @@ void worker(int tid, int nconns, Clock::time_point deadline) {
             dead = true;
             break;
           }
+          if (!done && c.abort_this && c.got_content) {
+            // client abort: hang up mid-stream, then carry on with a fresh connection
+            g_aborted++;
+            if (!reconnect(c, idx)) {
+              c.active = false;
+              --live;
+            } else if (!start_request(c)) {
+              --live;
+            }
+            dead = false;
+            break;
+          }
           if (!done) break;
           finish_request(c, ttft, ttfb, lat);
           done = false;
@@ -282,30 +663,24 @@ void worker(int tid, int nconns, Clock::time_point deadline) {
           }
           epoll_event e{};
           e.events = EPOLLIN | EPOLLOUT;
-          e.data.u32 = evs[k].data.u32;
+          e.data.u32 = idx;
           epoll_ctl(ep, EPOLL_CTL_MOD, c.fd, &e);
           if (c.in.empty()) break;
         }
       }
       if (dead && c.active) {
         g_errors++;
-        epoll_ctl(ep, EPOLL_CTL_DEL, c.fd, nullptr);
-        close(c.fd);
-        c.in.clear();
-        c.fd = connect_to();
-        if (c.fd < 0) {
+        if (!reconnect(c, idx)) {
           c.active = false;
           --live;
           continue;
         }
-        epoll_event e{};
-        e.events = EPOLLIN | EPOLLOUT;
-        e.data.u32 = evs[k].data.u32;
-        epoll_ctl(ep, EPOLL_CTL_ADD, c.fd, &e);
         c.req_off = 0;
         c.phase = 1;
         c.t0 = Clock::now();
         c.got_data = c.got_content = false;
+        c.tail.clear();
+        c.body.clear();
       }
     }
   }
@@ -324,11 +699,53 @@ double pct(std::vector<double>& v, double p) {
   return v[i];
 }
 
+std::string unhex(const std::string& h) {
+  std::string o;
+  for (size_t i = 0; i + 1 < h.size(); i += 2) o.push_back((char)(JR::hexv(h[i]) * 16 + JR::hexv(h[i + 1])));
+  return o;
+}
+
+bool load_spec(const std::string& path) {
+  std::ifstream f(path);
+  if (!f) return false;
+  std::string line;
+  Spec& S = g.spec;
+  S.on = true;
+  while (std::getline(f, line)) {
+    std::istringstream ss(line);
+    std::string kw;
+    if (!(ss >> kw) || kw[0] == '#') continue;
+    if (kw == "role") ss >> S.role;
+    else if (kw == "done") ss >> S.done;
+    else if (kw == "stream") {
+      StreamSpec st;
+      std::string mode, hex;
+      ss >> st.id >> mode >> hex;
+      st.exact = mode == "exact";
+      st.text = unhex(hex);
+      S.streams.push_back(st);
+    } else if (kw == "final") {
+      std::string mode, hex;
+      ss >> mode;
+      S.final_absent = mode == "absent";
+      while (ss >> hex) S.final_any.push_back(hex == "-" ? std::string() : unhex(hex));
+    } else if (kw == "error") {
+      std::string m;
+      ss >> m;
+      S.error_allowed = m == "allowed";
+    } else {
+      fprintf(stderr, "qmx_loadgen: unknown spec directive %s\n", kw.c_str());
+      return false;
+    }
+  }
+  return true;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
   signal(SIGPIPE, SIG_IGN);
-  std::string body_file;
+  std::string body_file, spec_file;
   for (int i = 1; i + 1 < argc; i += 2) {
     std::string k = argv[i], v = argv[i + 1];
     if (k == "--host") g.host = v;
@@ -340,6 +757,12 @@ int main(int argc, char** argv) {
     else if (k == "--body-file") body_file = v;
     else if (k == "--stream") g.stream = atoi(v.c_str()) != 0;
     else if (k == "--timeout") g.timeout_s = atof(v.c_str());
+    else if (k == "--expect") spec_file = v;
+    else if (k == "--abort-rate") g.abort_rate = atof(v.c_str());
+  }
+  if (!spec_file.empty() && !load_spec(spec_file)) {
+    fprintf(stderr, "qmx_loadgen: cannot read spec %s\n", spec_file.c_str());
+    return 2;
   }
   if (!body_file.empty()) {
     std::ifstream f(body_file);
@@ -360,11 +783,12 @@ int main(int argc, char** argv) {
   }
   for (auto& t : ts) t.join();
   double el = std::chrono::duration<double>(Clock::now() - t0).count();
-  printf("{\"completed\": %ld, \"errors\": %ld, \"non200\": %ld, \"no_content\": %ld, \"elapsed_s\": %.6f, "
+  printf("{\"completed\": %ld, \"errors\": %ld, \"non200\": %ld, \"no_content\": %ld, \"invalid\": %ld, "
+         "\"validated\": %ld, \"aborted\": %ld, \"elapsed_s\": %.6f, "
          "\"rps\": %.3f, \"ttft_p50_ms\": %.3f, \"ttft_p90_ms\": %.3f, \"ttft_p99_ms\": %.3f, "
          "\"ttfb_p50_ms\": %.3f, \"lat_p50_ms\": %.3f, \"lat_p99_ms\": %.3f, \"conns\": %d}\n",
-         g_done.load(), g_errors.load(), g_non200.load(), g_no_content.load(), el, g_done.load() / el,
-         pct(g_ttft, 50), pct(g_ttft, 90), pct(g_ttft, 99), pct(g_ttfb, 50), pct(g_lat, 50), pct(g_lat, 99),
-         g.conns);
+         g_done.load(), g_errors.load(), g_non200.load(), g_no_content.load(), g_invalid.load(), g_validated.load(),
+         g_aborted.load(), el, g_done.load() / el, pct(g_ttft, 50), pct(g_ttft, 90), pct(g_ttft, 99), pct(g_ttfb, 50),
+         pct(g_lat, 50), pct(g_lat, 99), g.conns);
   return 0;
 }

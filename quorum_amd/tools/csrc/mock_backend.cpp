@@ -7,6 +7,8 @@
 // --drop-rate (close mid-stream), --null-rate (content:null event).
 //
 //   qmx_mock --port 9101 [--threads 2] [--tokens 20] [--think 1] [--delay-us 0]
+//   qmx_mock --print-expected 1 [--tokens 20] [--think 1]   # JSON: what clients should see
+//       {"stream_text": <content outside the think block>, "message": <non-stream content>}
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netinet/in.h>
@@ -56,6 +58,8 @@ std::string chunk(const std::string& s) {
 }
 
 std::vector<std::string> g_events;  // SSE events of one streamed response
+std::string g_visible;              // concatenated content outside the think block
+std::string g_message;              // non-streaming message content
 std::string g_stream_all;           // full chunked streamed response (no delay path)
 std::string g_json_resp;            // non-streaming response
 const char* kStreamHdr =
@@ -80,6 +84,8 @@ void build_responses() {
     full += w;
     g_events.push_back(sse_event("{\"content\": \"" + w + "\"}"));
   }
+  g_visible = full;
+  g_message = std::string(g.think ? "<think>let me reason</think>" : "") + full;
   g_events.push_back(sse_event("{}", "\"stop\""));
   g_events.push_back("data: [DONE]\n\n");
   g_stream_all = kStreamHdr;
@@ -307,6 +313,7 @@ void worker(int tid) {
 
 int main(int argc, char** argv) {
   signal(SIGPIPE, SIG_IGN);
+  bool print_expected = false;
   for (int i = 1; i + 1 < argc; i += 2) {
     std::string k = argv[i], v = argv[i + 1];
     if (k == "--port") g.port = atoi(v.c_str());
@@ -319,8 +326,16 @@ int main(int argc, char** argv) {
     else if (k == "--null-rate") g.null_rate = atof(v.c_str());
     else if (k == "--stall-ms") g.stall_ms = atol(v.c_str());
     else if (k == "--name") g.name = v;
+    else if (k == "--print-expected") print_expected = atoi(v.c_str()) != 0;
   }
   build_responses();
+  if (print_expected) {
+    auto js = [](const std::string& x) {  // the texts are ASCII without quotes / backslashes
+      return "\"" + x + "\"";
+    };
+    printf("{\"stream_text\": %s, \"message\": %s}\n", js(g_visible).c_str(), js(g_message).c_str());
+    return 0;
+  }
   std::vector<std::thread> ts;
   for (int t = 0; t < g.threads; ++t) ts.emplace_back(worker, t);
   fprintf(stderr, "qmx_mock listening on 127.0.0.1:%d (%d threads)\n", g.port, g.threads);

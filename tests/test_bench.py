@@ -102,3 +102,31 @@ def test_pin_rank_numa_plan(monkeypatch):
     assert bench.pin_rank(fake_torch, 8, 0, 1) is None  # more ranks than GPUs
     monkeypatch.setenv("QMX_BENCH_PIN", "0")
     assert bench.pin_rank(fake_torch, 8, 0, 8) is None
+
+
+def test_bench_fails_on_invalid_responses(tmp_path):
+    """A proxy that drops one delta in 50 (QMX_FAULT_DROP_DELTA) must fail the bench: the
+    load generator validates every response, so a broken engine cannot score."""
+    port = _free_port()
+    env = dict(_env(), QMX_FAULT_DROP_DELTA="50")
+    r = subprocess.run([sys.executable, BENCH, "--steps", "1", "--warmup", "0", "--batch", "200", "--threads", "2",
+                        "--conns", "8", "--port", str(port)],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 1, r.stdout[-2000:]
+    res = json.loads(_json_lines(r.stdout)[0])
+    assert res["invalid"] > 0 and res["valid"] is False
+    assert "invalid response" in r.stderr
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/src/quorum"), reason="reference checkout not present")
+def test_bench_reference_same_harness(tmp_path):
+    """--impl reference: the unmodified upstream proxy (scratch copy) behind the same mocks,
+    load generator and validator — its responses satisfy the same event contract."""
+    port = _free_port()
+    r = subprocess.run([sys.executable, BENCH, "--impl", "reference", "--steps", "1", "--warmup", "0", "--batch", "16",
+                        "--conns", "4", "--port", str(port)],
+                       cwd=str(tmp_path), env=_env(), capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(_json_lines(r.stdout)[0])
+    assert res["config"]["impl"] == "reference" and res["validated"] == 16 and res["invalid"] == 0
+    assert res["vs_baseline"] is None

@@ -213,3 +213,62 @@ def test_server_tsan_shared_engine_lanes(tmp_path):
     err = err.decode(errors="replace")
     assert "ThreadSanitizer" not in err, err[-6000:]
     assert srv.returncode == 0, err[-3000:]
+
+
+def test_server_asan_abort_churn_shared_engine(san_bins, tmp_path):
+    """ASan/UBSan data plane, shared engine with 3 tick lanes over 3 io loops (the GPU-hub
+    topology, CPU engine), driven by the validating load generator with 30% of clients
+    hanging up mid-stream (session teardown while ticks are in flight, slot reuse): no
+    sanitizer report, no invalid response, clean shutdown."""
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from quorum_amd.ops import build
+    from quorum_amd.runtime.native_server import native_config
+
+    bin_dir = os.path.dirname(str(build.build_tools()[0]))
+    mports = [free_port(), free_port()]
+    mocks = [subprocess.Popen([os.path.join(bin_dir, "qmx_mock"), "--port", str(p), "--threads", "1",
+                               "--delay-us", "200"], stderr=subprocess.DEVNULL) for p in mports]
+    cfg = cfg_parallel(2, block={"separator": "\n--\n", "hide_intermediate_think": True,
+                                 "thinking_tags": ["think", "reason", "reasoning", "thought"],
+                                 "skip_final_aggregation": True})
+    for b, p in zip(cfg["primary_backends"], mports):
+        b["url"] = f"http://127.0.0.1:{p}/v1"
+    port = free_port()
+    d = native_config(cfg, "127.0.0.1", port, "cpu", 0, 3)
+    d.update(env_api_key="", shared_engine=1, tick_lanes=3)
+    path = tmp_path / "churn.json"
+    path.write_text(json.dumps(d))
+    spec = tmp_path / "spec.txt"
+    text = bench.mock_expected(bin_dir)["stream_text"].encode().hex()
+    spec.write_text(f"role 1\ndone 1\nstream chatcmpl-parallel-0 exact {text}\n"
+                    f"stream chatcmpl-parallel-1 exact {text}\nfinal absent\nerror absent\n")
+    srv = subprocess.Popen([str(san_bins["qmx_server_asan"]), str(path)], stderr=subprocess.PIPE,
+                           env=dict(os.environ, **ASAN_ENV))
+    try:
+        t0 = time.time()
+        while time.time() - t0 < 30:
+            try:
+                if httpx.get(f"http://127.0.0.1:{port}/health", timeout=1).status_code == 200:
+                    break
+            except httpx.HTTPError:
+                time.sleep(0.05)
+        out = subprocess.run([os.path.join(bin_dir, "qmx_loadgen"), "--port", str(port), "--conns", "32",
+                              "--requests", "2000", "--threads", "2", "--timeout", "120", "--expect", str(spec),
+                              "--abort-rate", "0.3"], capture_output=True, text=True, timeout=200)
+        r = json.loads(out.stdout.strip().splitlines()[-1])
+    finally:
+        srv.send_signal(signal.SIGINT)
+        try:
+            _, err = srv.communicate(timeout=30)
+        except subprocess.TimeoutExpired:
+            srv.kill()
+            _, err = srv.communicate()
+        for m in mocks:
+            m.kill()
+            m.wait()
+    err = err.decode(errors="replace")
+    assert srv.returncode == 0 and "AddressSanitizer" not in err and "runtime error" not in err, err[-4000:]
+    assert r["aborted"] > 200 and r["invalid"] == 0 and r["errors"] == 0, (r, out.stderr[-2000:])
