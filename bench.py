@@ -32,7 +32,12 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-BASELINE_RPS = 9.1  # reference, 2 backends, same config, 16 clients
+# BASELINE.md "same harness" rows: the unmodified reference proxy measured on the MI355X box
+# by this bench (--impl reference: same C++ mocks, load generator, validator, 16 clients;
+# profiles/r2/reference_same_harness_*.json).  Scenarios without such a row fall back to the
+# survey's 8-vCPU container numbers and say so in the JSON line.
+BASELINE_SOURCE_SAME = "reference proxy, same box + same harness (bench.py --impl reference)"
+BASELINE_SOURCE_SURVEY = "reference proxy, survey container (8 vCPU, Python harness; SURVEY §6)"
 
 # BASELINE.json configs.  "headline" is the driver's metric; the others are measured with
 # --scenario (reference numbers from BASELINE.md where one exists for that shape).
@@ -41,7 +46,8 @@ SCENARIOS = {
     # and its start/connect/drain is amortised (MI355X A/B, profiles/r1n_batch_ab.txt: 4/4
     # pairs higher, mean 180k vs 153k req/s against 4096 per step)
     "headline": dict(n=2, strategy="concatenate", hide_final=False, skip=True, faults={}, timeout=30,
-                     batch=16384, baseline=9.1, desc="2 mock backends, streaming concatenate, hide_intermediate_think"),
+                     batch=16384, baseline=21.071, baseline_ttft_ms=619.6, baseline_source=BASELINE_SOURCE_SAME,
+                     desc="2 mock backends, streaming concatenate, hide_intermediate_think"),
     "aggregate4": dict(n=4, strategy="aggregate", hide_final=False, skip=False, faults={}, timeout=30,
                        baseline=3.8, desc="4 mock backends, streaming aggregate strategy (LLM4 also aggregates)"),
     "highqps8": dict(n=8, strategy="concatenate", hide_final=True, skip=True, faults={}, timeout=30,
@@ -302,13 +308,19 @@ def main() -> int:
                     choices=["native", "python", "reference"],
                     help="reference: the unmodified upstream proxy (scratch copy of --ref-root) under uvicorn, "
                          "same mocks and load generator (same-harness baseline)")
-    ap.add_argument("--ref-root", default=os.environ.get("QMX_REF_ROOT", "/root/reference"))
+    ap.add_argument("--ref-root", default=os.environ.get("QMX_REF_ROOT") or next(
+        (d for d in ("/root/reference", os.path.join(ROOT, ".refstage")) if os.path.isdir(os.path.join(d, "src"))),
+        "/root/reference"),
+        help="reference checkout (its src/ is copied to a scratch dir); .refstage/ is a git-ignored staging "
+             "copy for GPU boxes, which have no /root/reference")
     ap.add_argument("--engine", default=os.environ.get("QMX_BENCH_ENGINE", "auto"))
     ap.add_argument("--workers", type=int, default=4, help="python impl: proxy processes per rank")
     ap.add_argument("--threads", type=int, default=0,
                     help="native impl: io threads per rank (0: min(8, cores / (2 x ranks)), at least 2 — "
                          "the node's cores are shared by every rank's proxy, mocks and load generator)")
-    ap.add_argument("--lg-threads", type=int, default=2)
+    # 3 load-generator threads: every response is validated (the envelope fast path costs
+    # ~2-5 us per response), two threads saturate near 110k req/s on the MI355X box
+    ap.add_argument("--lg-threads", type=int, default=3)
     ap.add_argument("--mock-threads", type=int, default=2)
     ap.add_argument("--skip-final", type=int, default=1)
     ap.add_argument("--tile", type=int, default=16384)
@@ -468,6 +480,8 @@ def main() -> int:
                 "higher_is_better": True,
                 "scaling": "weak",
                 "vs_baseline": round(value / baseline, 3) if baseline else None,
+                "baseline_req_s": baseline,
+                "baseline_source": sc.get("baseline_source", BASELINE_SOURCE_SURVEY) if baseline else None,
                 "dtype": "bytes (utf-8 SSE text; no float compute)",
                 "data": "synthetic: C++ mock backends (role + 4 split <think> fragments + 20 tokens + stop + "
                         "[DONE]) and C++ closed-loop load generator; every response validated against the "
@@ -493,7 +507,7 @@ def main() -> int:
                 "no_content": int(sum(r[9] for r in rows)),
                 "processes_exited": int(sum(r[7] for r in rows)),
                 "valid": ok,
-                "baseline_p50_ttft_ms_16_clients": 1605,
+                "baseline_p50_ttft_ms": sc.get("baseline_ttft_ms"),
                 # one rank proxy process counters over the timed region (SURVEY §5.1 time breakdown;
                 # with N>1 the shared port answers from any rank)
                 "breakdown_one_rank": bd,

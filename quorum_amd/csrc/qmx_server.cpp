@@ -1179,6 +1179,14 @@ class Loop {
     if (q != std::string::npos) target.resize(q);
     if (method == "GET" && target == "/health") return respond(c, 200, "application/json", "{\"status\":\"healthy\"}");
     if (method == "GET" && target == "/metrics") return respond(c, 200, "text/plain; version=0.0.4", metrics_text());
+    if (method == "GET" && target == "/openapi.json" && !cfg_.openapi_json.empty())
+      return respond(c, 200, "application/json", cfg_.openapi_json);
+    if (method == "GET" && target == "/docs" && !cfg_.docs_html.empty())
+      return respond(c, 200, "text/html; charset=utf-8", cfg_.docs_html);
+    if (method == "GET" && target == "/docs/oauth2-redirect" && !cfg_.oauth2_redirect_html.empty())
+      return respond(c, 200, "text/html; charset=utf-8", cfg_.oauth2_redirect_html);
+    if (method == "GET" && target == "/redoc" && !cfg_.redoc_html.empty())
+      return respond(c, 200, "text/html; charset=utf-8", cfg_.redoc_html);
     if (target != "/chat/completions" && target != "/v1/chat/completions")
       return respond(c, 404, "application/json", "{\"detail\":\"Not Found\"}");
     if (method != "POST") return respond(c, 405, "application/json", "{\"detail\":\"Method Not Allowed\"}");
@@ -1218,13 +1226,18 @@ class Loop {
       s->fwd.push_back(h);
     }
     if (!has_auth) {
-      if (cfg_.env_api_key.empty()) {
+      std::string env_key = cfg_.env_api_key;
+      if (cfg_.api_key_from_env) {  // per request, like os.environ.get (a rotated key applies at once)
+        const char* e = getenv("OPENAI_API_KEY");
+        env_key = e ? e : "";
+      }
+      if (env_key.empty()) {
         c_errors++;
         return respond(c, 401, "application/json",
                        err_json("Authorization header is required and OPENAI_API_KEY environment variable is not set",
                                 "auth_error"));
       }
-      s->auth = "Bearer " + cfg_.env_api_key;
+      s->auth = "Bearer " + env_key;
     }
     s->fwd.emplace_back("Authorization", s->auth);
     if (!has_ctype) s->fwd.emplace_back("Content-Type", "application/json");

@@ -50,7 +50,11 @@ struct ServerCfg {
   std::string aggregator_name;  // empty = none
   std::string prompt_template, intermediate_separator, query_format, source_label_format;
   bool include_original_query = true, include_source_names = false;
-  std::string env_api_key;
+  std::string env_api_key;         // static OPENAI_API_KEY (tests; api_key_from_env = false)
+  bool api_key_from_env = false;   // read OPENAI_API_KEY per request, as quorum (oai_proxy.py:981)
+  // FastAPI's default documentation routes of the reference app (oai_proxy.py:70): the
+  // documents are rendered once by the launcher from the conformance app; empty = 404
+  std::string openapi_json, docs_html, redoc_html, oauth2_redirect_html;
   bool install_signals = true;
   // multi-rank: one process per GPU.  placement "local" = DP session sharding only;
   // "spread" = a session's backend streams run on ranks owner..owner+N-1 (qmx_exchange.h)

@@ -25,6 +25,36 @@ SOURCES = ["qmx_engine.cpp", "qmx_json.cpp", "qmx_server.cpp", "qmx_exchange.cpp
 ARCH = os.environ.get("QMX_ARCH", "gfx950")
 
 
+def _digest(*parts) -> str:
+    """Build key: every input that changes the output (source and header bytes, the exact
+    command line with its flags and target arch, the compiler binary)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for p in parts:
+        if isinstance(p, Path):
+            h.update(p.read_bytes())
+        else:
+            h.update(str(p).encode())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def _compiler_id(cc: str) -> str:
+    real = os.path.realpath(cc)
+    st = os.stat(real)
+    return f"{real}:{st.st_size}:{int(st.st_mtime)}"
+
+
+def _fresh(out: Path, key: str) -> bool:
+    k = out.with_name(out.name + ".key")
+    return out.exists() and k.exists() and k.read_text() == key
+
+
+def _stamp(out: Path, key: str) -> None:
+    out.with_name(out.name + ".key").write_text(key)
+
+
 def hipcc() -> str:
     for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
         if cand and os.path.exists(cand):
@@ -73,33 +103,38 @@ def _build(debug: bool = False, jobs: int = 3, verbose: bool = False) -> Path:
     BUILD.mkdir(parents=True, exist_ok=True)
     flags = _flags(debug)
     out = ext_path()
-    headers = list(CSRC.glob("*.h"))
-    newest_hdr = max((h.stat().st_mtime for h in headers), default=0)
+    headers = sorted(CSRC.glob("*.h"))
+    cid = _compiler_id(cc)
 
-    def obj(src: str) -> Path:
+    def obj(src: str):
         s = CSRC / src
         o = BUILD / (src + ".o")
-        if o.exists() and o.stat().st_mtime > max(s.stat().st_mtime, newest_hdr):
-            return o
         cmd = [cc, "-x", "hip", "-c", str(s), "-o", str(o)] + flags
+        key = _digest(cid, " ".join(cmd), s, *headers)  # content + flags + arch, not mtimes
+        if _fresh(o, key):
+            return o, key
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"compile failed: {src}\n{r.stdout}\n{r.stderr}")
-        return o
+        _stamp(o, key)
+        return o, key
 
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(obj, SOURCES))
-    if out.exists() and out.stat().st_mtime > max(o.stat().st_mtime for o in objs):
-        return out
+        built = list(ex.map(obj, SOURCES))
+    objs = [o for o, _ in built]
     cmd = [cc, "-shared", "-o", str(out)] + [str(o) for o in objs] + [
         f"--offload-arch={ARCH}", "-fPIC", "-L/opt/rocm/lib", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", "-lssl", "-lcrypto", "-Wl,-rpath,/opt/rocm/lib"]
+    key = _digest(cid, " ".join(cmd), *[k for _, k in built])
+    if _fresh(out, key):
+        return out
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed\n{r.stdout}\n{r.stderr}")
+    _stamp(out, key)
     return out
 
 
@@ -121,14 +156,16 @@ def _build_tools(verbose: bool = False) -> list:
         s = PKG / "tools" / "csrc" / src
         b = BIN / name
         out.append(b)
-        if b.exists() and b.stat().st_mtime > s.stat().st_mtime:
-            continue
         cmd = [cxx, "-O2", "-std=c++17", "-pthread", str(s), "-o", str(b)]
+        key = _digest(_compiler_id(cxx), " ".join(cmd), s)
+        if _fresh(b, key):
+            continue
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"tool build failed: {src}\n{r.stderr}")
+        _stamp(b, key)
     return out
 
 
@@ -150,22 +187,24 @@ def build_sanitized(verbose: bool = False) -> list:
     with _BuildLock():
         BIN.mkdir(exist_ok=True)
         cc = hipcc()
-        newest_hdr = max((h.stat().st_mtime for h in CSRC.glob("*.h")), default=0)
+        headers = sorted(CSRC.glob("*.h"))
         out = []
 
         def one(item):
             name, (srcs, libs) = item
             b = BIN / name
             paths = [PKG / x for x in srcs]
-            if b.exists() and b.stat().st_mtime > max([newest_hdr] + [x.stat().st_mtime for x in paths]):
-                return b
             cmd = [cc, "-x", "hip", f"--offload-arch={ARCH}", "-O1", "-g", "-std=c++17", f"-I{CSRC}"] + SAN_FLAGS + \
                 [str(x) for x in paths] + ["-o", str(b), "-fsanitize=address", "-fsanitize=undefined"] + libs
+            key = _digest(_compiler_id(cc), " ".join(cmd), *paths, *headers)
+            if _fresh(b, key):
+                return b
             if verbose:
                 print(" ".join(cmd), flush=True)
             r = subprocess.run(cmd, capture_output=True, text=True)
             if r.returncode != 0:
                 raise RuntimeError(f"sanitizer build failed: {name}\n{r.stderr[-4000:]}")
+            _stamp(b, key)
             return b
 
         with cf.ThreadPoolExecutor(max_workers=2) as ex:
@@ -185,16 +224,18 @@ def build_tsan(verbose: bool = False) -> Path:
         srcs, libs = SAN_TARGETS["qmx_server_asan"]
         b = BIN / "qmx_server_tsan"
         paths = [PKG / x for x in srcs]
-        newest_hdr = max((h.stat().st_mtime for h in CSRC.glob("*.h")), default=0)
-        if b.exists() and b.stat().st_mtime > max([newest_hdr] + [x.stat().st_mtime for x in paths]):
-            return b
-        cmd = [hipcc(), "-x", "hip", f"--offload-arch={ARCH}", "-O1", "-g", "-std=c++17", f"-I{CSRC}"] + TSAN_FLAGS + \
+        cc = hipcc()
+        cmd = [cc, "-x", "hip", f"--offload-arch={ARCH}", "-O1", "-g", "-std=c++17", f"-I{CSRC}"] + TSAN_FLAGS + \
             [str(x) for x in paths] + ["-o", str(b), "-fsanitize=thread"] + libs
+        key = _digest(_compiler_id(cc), " ".join(cmd), *paths, *sorted(CSRC.glob("*.h")))
+        if _fresh(b, key):
+            return b
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"tsan build failed\n{r.stderr[-4000:]}")
+        _stamp(b, key)
         return b
 
 

@@ -62,13 +62,38 @@ def native_config(cfg: Dict[str, Any], host: str, port: int, engine: str, device
         "source_label_format": str(agg.source_label_format),
         "include_original_query": bool(agg.include_original_query),
         "include_source_names": bool(agg.include_source_names),
-        "env_api_key": os.environ.get("OPENAI_API_KEY", ""),
+        "env_api_key": "", "api_key_from_env": True,  # per request, as quorum (oai_proxy.py:981)
         "backends": backends,
         "drain_s": float(rt.drain_timeout), "verify": bool(rt.verify),
         "shared_engine": -1 if rt.shared_engine in ("auto", None) else int(bool(rt.shared_engine)),
         "tick_lanes": int(rt.tick_lanes),
         "ca_file": _ca_bundle(), "tls_verify": os.environ.get("QMX_TLS_VERIFY", "1") not in ("0", "false"), "ready_file": (os.environ["QMX_READY_FILE"] + f".{os.getpid()}") if os.environ.get("QMX_READY_FILE") else "",
         **cluster_config(rt, port, engine),
+        **doc_routes(cfg),
+    }
+
+
+def doc_routes(cfg: Dict[str, Any]) -> Dict[str, str]:
+    """FastAPI's default /openapi.json, /docs, /docs/oauth2-redirect and /redoc of the
+    reference app (``FastAPI(title="OpenAI API Proxy")``, oai_proxy.py:70), rendered once from
+    the conformance app so the native front-end serves the same documents."""
+    try:
+        import json
+
+        from fastapi.openapi.docs import get_redoc_html, get_swagger_ui_html, get_swagger_ui_oauth2_redirect_html
+
+        from ..server.app import create_app
+    except ImportError:  # fastapi absent: the routes 404, as any unknown path
+        return {}
+    app = create_app(lambda: cfg)
+    return {
+        "openapi_json": json.dumps(app.openapi(), separators=(",", ":")),
+        "docs_html": get_swagger_ui_html(openapi_url=app.openapi_url, title=f"{app.title} - Swagger UI",
+                                         oauth2_redirect_url=app.swagger_ui_oauth2_redirect_url,
+                                         init_oauth=app.swagger_ui_init_oauth,
+                                         swagger_ui_parameters=app.swagger_ui_parameters).body.decode(),
+        "oauth2_redirect_html": get_swagger_ui_oauth2_redirect_html().body.decode(),
+        "redoc_html": get_redoc_html(openapi_url=app.openapi_url, title=f"{app.title} - ReDoc").body.decode(),
     }
 
 

@@ -85,11 +85,39 @@ std::atomic<long> g_issued{0}, g_done{0}, g_errors{0}, g_non200{0}, g_no_content
 std::mutex g_mu;
 std::vector<double> g_ttft, g_ttfb, g_lat;
 
+// receive buffer consumed from the front by offset (no memmove per HTTP chunk)
+struct InBuf {
+  std::string s;
+  size_t off = 0;
+  const char* data() const { return s.data() + off; }
+  size_t size() const { return s.size() - off; }
+  bool empty() const { return off >= s.size(); }
+  void clear() {
+    s.clear();
+    off = 0;
+  }
+  void append(const char* p, size_t n) {
+    if (off > 0 && off * 2 > s.size()) {
+      s.erase(0, off);
+      off = 0;
+    }
+    s.append(p, n);
+  }
+  void erase_front(size_t n) {
+    off += n;
+    if (off >= s.size()) clear();
+  }
+  size_t find(const char* pat) const {
+    const size_t k = s.find(pat, off);
+    return k == std::string::npos ? k : k - off;
+  }
+};
+
 struct Conn {
   int fd = -1;
   std::string req;
   size_t req_off = 0;
-  std::string in;
+  InBuf in;
   // response parse state
   int phase = 0;  // 0 idle, 1 headers, 2 body-chunked, 3 body-length
   bool chunked = false;
@@ -177,6 +205,10 @@ struct JR {
     if (p >= e || *p != '"') return ok = false;
     ++p;
     while (p < e) {
+      const char* run = p;  // plain bytes are appended in one go
+      while (p < e && *p != '"' && *p != '\\' && (unsigned char)*p >= 0x20) ++p;
+      if (out && p > run) out->append(run, p - run);
+      if (p >= e) break;
       const char c = *p++;
       if (c == '"') return true;
       if ((unsigned char)c < 0x20) return ok = false;
@@ -356,6 +388,69 @@ bool parse_event(const char* p, const char* e, Ev& ev) {
   return r.p == r.e && have_choices && !ev.id.empty();
 }
 
+// Fast path: the proxy's own envelope (json.dumps of quorum's event dicts, oai_proxy.py:530-541,
+// 629-646, 847-860) matched literally around one strictly scanned JSON string — a strict
+// subset of what parse_event accepts, with the same result; anything else takes the full
+// parser.  Keeps validation off the load generator's critical CPU (it shares the box).
+// kind: 1 role, 2 delta/final content (appended to *content), 0 no match.
+int fast_event(const char* a, const char* b, std::string* id, std::string* content_out, bool* final_stop) {
+  static const char kP0[] = "{\"id\": \"";
+  static const char kP1[] = "\", \"object\": \"chat.completion.chunk\", \"created\": ";
+  static const char kP2[] = ", \"model\": \"parallel-proxy\", \"choices\": [{\"index\": 0, \"delta\": {";
+  static const char kRole[] = "\"role\": \"assistant\"}, \"finish_reason\": null}]}";
+  static const char kCont[] = "\"content\": ";
+  static const char kEndNull[] = "}, \"finish_reason\": null}]}";
+  static const char kEndStop[] = "}, \"finish_reason\": \"stop\"}]}";
+  auto eat = [&](const char* lit, size_t n) {
+    if ((size_t)(b - a) < n || memcmp(a, lit, n) != 0) return false;
+    a += n;
+    return true;
+  };
+  if (!eat(kP0, sizeof(kP0) - 1)) return 0;
+  const char* q = (const char*)memchr(a, '"', b - a);
+  if (!q) return 0;
+  for (const char* x = a; x < q; ++x)
+    if (*x == '\\' || (unsigned char)*x < 0x20) return 0;
+  id->assign(a, q - a);
+  a = q;
+  if (!eat(kP1, sizeof(kP1) - 1)) return 0;
+  const char* d = a;
+  while (a < b && *a >= '0' && *a <= '9') ++a;
+  if (a == d) return 0;
+  if (!eat(kP2, sizeof(kP2) - 1)) return 0;
+  if (eat(kRole, sizeof(kRole) - 1)) return a == b ? 1 : 0;
+  if (!eat(kCont, sizeof(kCont) - 1)) return 0;
+  const size_t n0 = content_out->size();
+  {
+    // escape-free string (the common case): one memchr, one check pass, one append
+    const char* q2 = a < b && *a == '"' ? (const char*)memchr(a + 1, '"', b - a - 1) : nullptr;
+    bool plain = q2 != nullptr;
+    for (const char* x = a + 1; plain && x < q2; ++x) plain = *x != '\\' && (unsigned char)*x >= 0x20;
+    if (plain) {
+      content_out->append(a + 1, q2 - a - 1);
+      a = q2 + 1;
+    } else {
+      JR r{a, b};
+      if (!r.str(content_out) || !r.ok) {
+        content_out->resize(n0);
+        return 0;
+      }
+      a = r.p;
+    }
+  }
+  const size_t left = (size_t)(b - a);
+  if (left == sizeof(kEndNull) - 1 && memcmp(a, kEndNull, left) == 0) {
+    *final_stop = false;
+    return 2;
+  }
+  if (left == sizeof(kEndStop) - 1 && memcmp(a, kEndStop, left) == 0) {
+    *final_stop = true;
+    return 2;
+  }
+  content_out->resize(n0);
+  return 0;
+}
+
 // returns "" when the response satisfies the spec, else a short reason
 std::string validate(int status, const std::string& body) {
   const Spec& S = g.spec;
@@ -364,6 +459,7 @@ std::string validate(int status, const std::string& body) {
   std::vector<int> nev(S.streams.size(), 0);
   bool saw_done = false, saw_final = false, saw_error = false;
   std::string final_text;
+  std::string fid, fcontent;
   size_t pos = 0;
   int k = 0;
   while (pos < body.size()) {
@@ -381,6 +477,26 @@ std::string validate(int status, const std::string& body) {
       continue;
     }
     Ev ev;
+    {
+      // fast path: content goes straight into its stream's accumulator
+      fcontent.clear();
+      bool stop = false;
+      const int kind = fast_event(a, b, &fid, &fcontent, &stop);
+      if (kind == 1 && k == 0 && S.role && fid == "chatcmpl-parallel") {
+        ++k;
+        continue;
+      }
+      if (kind == 2 && !stop && !fcontent.empty() && !saw_final && k > 0) {
+        size_t si = 0;
+        while (si < S.streams.size() && S.streams[si].id != fid) ++si;
+        if (si < S.streams.size()) {
+          acc[si] += fcontent;
+          ++nev[si];
+          ++k;
+          continue;
+        }
+      }
+    }
     if (!parse_event(a, b, ev)) return "malformed event " + std::to_string(k);
     if (k == 0 && S.role) {
       if (ev.id != "chatcmpl-parallel" || !ev.has_role || ev.has_content) return "first event is not the role event";
@@ -474,6 +590,7 @@ bool start_request(Conn& c) {
   c.abort_this = g.abort_rate > 0 && std::uniform_real_distribution<double>(0, 1)(t_rng) < g.abort_rate;
   c.tail.clear();
   c.body.clear();
+  if (g.spec.on) c.body.reserve(16384);
   c.t0 = Clock::now();
   c.active = true;
   return true;
@@ -510,13 +627,13 @@ bool parse(Conn& c, bool* done) {
     if (c.phase == 1) {
       size_t he = c.in.find("\r\n\r\n");
       if (he == std::string::npos) return true;
-      std::string h = c.in.substr(0, he);
+      std::string h(c.in.data(), he);
       c.status = atoi(h.c_str() + 9);
       for (auto& ch : h) ch = (char)tolower(ch);
       c.chunked = h.find("transfer-encoding: chunked") != std::string::npos;
       size_t p = h.find("content-length:");
       c.remaining = p != std::string::npos ? strtol(h.c_str() + p + 15, nullptr, 10) : 0;
-      c.in.erase(0, he + 4);
+      c.in.erase_front(he + 4);
       c.phase = c.chunked ? 2 : 3;
       c.chunk_left = -1;
       if (!c.chunked && c.remaining == 0) {
@@ -528,7 +645,7 @@ bool parse(Conn& c, bool* done) {
     if (c.phase == 3) {
       size_t take = std::min((size_t)c.remaining, c.in.size());
       if (take) scan_sse(c, c.in.data(), take, now);
-      c.in.erase(0, take);
+      c.in.erase_front(take);
       c.remaining -= take;
       if (c.remaining == 0) {
         *done = true;
@@ -540,8 +657,8 @@ bool parse(Conn& c, bool* done) {
       if (c.chunk_left < 0 && c.chunk_left != -2) {
         size_t le = c.in.find("\r\n");
         if (le == std::string::npos) return true;
-        long sz = strtol(c.in.c_str(), nullptr, 16);
-        c.in.erase(0, le + 2);
+        long sz = strtol(c.in.data(), nullptr, 16);
+        c.in.erase_front(le + 2);
         if (sz == 0) {
           c.chunk_left = -2;  // trailer: expect "\r\n"
         } else {
@@ -550,17 +667,17 @@ bool parse(Conn& c, bool* done) {
       }
       if (c.chunk_left == -2) {
         if (c.in.size() < 2) return true;
-        c.in.erase(0, 2);
+        c.in.erase_front(2);
         *done = true;
         return true;
       }
       size_t take = std::min((size_t)c.chunk_left, c.in.size());
       if (take) scan_sse(c, c.in.data(), take, now);
-      c.in.erase(0, take);
+      c.in.erase_front(take);
       c.chunk_left -= take;
       if (c.chunk_left > 0) return true;
       if (c.in.size() < 2) return true;  // chunk_left == 0: its CRLF has not arrived yet
-      c.in.erase(0, 2);
+      c.in.erase_front(2);
       c.chunk_left = -1;
       continue;
     }
@@ -763,6 +880,22 @@ int main(int argc, char** argv) {
   if (!spec_file.empty() && !load_spec(spec_file)) {
     fprintf(stderr, "qmx_loadgen: cannot read spec %s\n", spec_file.c_str());
     return 2;
+  }
+  if (const char* vb = getenv("QMX_LOADGEN_VALIDATE_BENCH")) {  // FILE:N — validator cost per body
+    std::string f(vb);
+    const size_t c = f.rfind(':');
+    std::ifstream in(f.substr(0, c));
+    std::stringstream ss;
+    ss << in.rdbuf();
+    const std::string body = ss.str();
+    const long n = atol(f.c_str() + c + 1);
+    auto t0 = Clock::now();
+    long bad = 0;
+    for (long i = 0; i < n; ++i) bad += !validate(200, body).empty();
+    const double us = std::chrono::duration<double, std::micro>(Clock::now() - t0).count() / n;
+    printf("{\"validate_us\": %.3f, \"bytes\": %zu, \"invalid\": %ld, \"why\": \"%s\"}\n", us, body.size(), bad,
+           validate(200, body).c_str());
+    return 0;
   }
   if (!body_file.empty()) {
     std::ifstream f(body_file);

@@ -76,6 +76,11 @@ int main(int argc, char** argv) {
   c.include_original_query = gb(d, "include_original_query", true);
   c.include_source_names = gb(d, "include_source_names", false);
   c.env_api_key = gs(d, "env_api_key", "");
+  c.api_key_from_env = gb(d, "api_key_from_env", false);
+  c.openapi_json = gs(d, "openapi_json", "");
+  c.docs_html = gs(d, "docs_html", "");
+  c.redoc_html = gs(d, "redoc_html", "");
+  c.oauth2_redirect_html = gs(d, "oauth2_redirect_html", "");
   c.rank = gi(d, "rank", 0);
   c.world = gi(d, "world", 1);
   c.placement = gs(d, "placement", "local");

@@ -111,7 +111,8 @@ class LiveUpstream:
 
 @contextlib.contextmanager
 def native_server(cfg: Dict[str, Any], engine: str = "cpu", threads: int = 1, env_key: str = "",
-                  verify: bool = False, shared: Optional[bool] = None, lanes: Optional[int] = None):
+                  verify: bool = False, shared: Optional[bool] = None, lanes: Optional[int] = None,
+                  key_from_env: bool = False):
     """Run the C++ data plane in-process (background thread) for one config.
 
     verify: run the shadow CPU-oracle engine (server_counters()['verify_mismatches']).
@@ -128,6 +129,7 @@ def native_server(cfg: Dict[str, Any], engine: str = "cpu", threads: int = 1, en
     d = native_config(cfg, "127.0.0.1", port, engine, 0, threads)
     d["install_signals"] = False
     d["env_api_key"] = env_key
+    d["api_key_from_env"] = key_from_env  # default: the test's key, not the shared process env
     d["verify"] = verify
     if shared is not None:
         d["shared_engine"] = int(shared)

@@ -442,3 +442,42 @@ def test_native_role_event_not_held_behind_slow_upstream():
         assert evs[-1] == "[DONE]"
     finally:
         live.close()
+
+
+def test_native_api_key_read_per_request(monkeypatch):
+    """quorum reads OPENAI_API_KEY on every request (oai_proxy.py:981): a key set (or
+    removed) after the server started applies to the next request."""
+    live = LiveUpstream()
+    p1 = live.serve("b1", ("json", 200, completion("hi")))
+    cfg = {"primary_backends": [{"name": "LLM1", "url": f"http://127.0.0.1:{p1}/v1", "model": "m"}],
+           "settings": {"timeout": 30}}
+    req = {"messages": MSG}
+    try:
+        with native_server(cfg, key_from_env=True) as port:
+            url = f"http://127.0.0.1:{port}/chat/completions"
+            assert httpx.post(url, json=req, timeout=30).status_code == 401
+            monkeypatch.setenv("OPENAI_API_KEY", "rotated-key")
+            r = httpx.post(url, json=req, timeout=30)
+            assert r.status_code == 200
+            assert live.calls[-1]["headers"]["authorization"] == "Bearer rotated-key"
+            monkeypatch.delenv("OPENAI_API_KEY")
+            r = httpx.post(url, json=req, timeout=30)
+            assert r.status_code == 401 and r.json()["error"]["type"] == "auth_error"
+    finally:
+        live.close()
+
+
+def test_native_serves_fastapi_doc_routes():
+    """FastAPI's default documentation routes of the reference app (oai_proxy.py:70)."""
+    from quorum_amd.server.app import create_app
+
+    cfg = {"primary_backends": [{"name": "LLM1", "url": "http://127.0.0.1:9/v1", "model": "m"}],
+           "settings": {"timeout": 30}}
+    with native_server(cfg) as port:
+        base = f"http://127.0.0.1:{port}"
+        r = httpx.get(base + "/openapi.json")
+        assert r.status_code == 200 and r.json() == create_app(lambda: cfg).openapi()
+        assert r.json()["info"]["title"] == "OpenAI API Proxy"
+        for path, marker in (("/docs", "swagger-ui"), ("/redoc", "redoc"), ("/docs/oauth2-redirect", "oauth2")):
+            r = httpx.get(base + path)
+            assert r.status_code == 200 and r.headers["content-type"].startswith("text/html") and marker in r.text

@@ -94,6 +94,7 @@ def test_server_asan_traffic(san_bins, tmp_path):
             port = free_port()
             d = native_config(cfg, "127.0.0.1", port, "cpu", 0, 2)
             d["env_api_key"] = ""
+            d["api_key_from_env"] = False
             path = tmp_path / f"{name}.json"
             path.write_text(json.dumps(d))
             srv = subprocess.Popen([str(san_bins["qmx_server_asan"]), str(path)], stderr=subprocess.PIPE,
@@ -174,7 +175,7 @@ def test_server_tsan_shared_engine_lanes(tmp_path):
         b["url"] = u
     port = free_port()
     d = native_config(cfg, "127.0.0.1", port, "cpu", 0, 4)
-    d.update(env_api_key="", shared_engine=1, tick_lanes=3, verify=True)
+    d.update(env_api_key="", api_key_from_env=False, shared_engine=1, tick_lanes=3, verify=True)
     path = tmp_path / "tsan.json"
     path.write_text(json.dumps(d))
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=0:second_deadlock_stack=1:report_signal_unsafe=0")
@@ -238,7 +239,7 @@ def test_server_asan_abort_churn_shared_engine(san_bins, tmp_path):
         b["url"] = f"http://127.0.0.1:{p}/v1"
     port = free_port()
     d = native_config(cfg, "127.0.0.1", port, "cpu", 0, 3)
-    d.update(env_api_key="", shared_engine=1, tick_lanes=3)
+    d.update(env_api_key="", api_key_from_env=False, shared_engine=1, tick_lanes=3)
     path = tmp_path / "churn.json"
     path.write_text(json.dumps(d))
     spec = tmp_path / "spec.txt"

@@ -1,0 +1,120 @@
+#!/bin/bash
+# One parameterised MI355X session for gpurun: each argument is a step, run in order, each
+# under its own time limit; the first failing step ends the session (no retries, nothing
+# else touches the GPU after a fault / abort / timeout).
+#
+#   gpurun -- 'bash tools/gpu_session.sh TAG step [step ...]'
+#
+# steps:
+#   tests                 pytest -m gpu (HIP engine vs C++ oracle, HIP server with verify mode)
+#   smoke                 __graft_entry__.smoke()
+#   bench[=N]             headline bench.py N times (default 1)            -> bench_<i>.json
+#   bench:ARGS            one bench.py run with extra args (commas = spaces) -> bench_<slug>.json
+#   ab:NAME:ENV:ARGS      one bench.py run under extra env (commas = spaces) -> ab_<NAME>.json
+#   scenarios             aggregate4, highqps8, failure, paced (10 steps each)
+#   reference             the upstream proxy under the same harness (bench.py --impl reference)
+#   prof                  rocprofv3 --kernel-trace --stats of a short headline bench
+#   pmc:C1,C2,...         rocprofv3 --pmc pass (one block-limited counter set) on kbench
+#   kbench                tools/kbench.py in-kernel stage split (QMX_STAGE_TIMING)
+#   multirank=N           bench.py under torch.distributed.run with N ranks sharing GPU 0
+#   spread=N              same, --placement spread over the TCP exchange
+#   cpuprof               headline bench with the in-process CPU profiler on the proxy
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+TAG=${1:?tag}; shift
+OUT=gpurun_out/$TAG
+mkdir -p $OUT/prof
+
+summ() {  # one line per bench JSON
+  python3 - "$1" "$2" <<'EOF'
+import json, sys
+name, path = sys.argv[1], sys.argv[2]
+lines = [l for l in open(path) if l.startswith("{")]
+if not lines:
+    print(name, "no JSON line"); sys.exit(0)
+d = json.loads(lines[-1]); b = d.get("breakdown_one_rank", {})
+print(name, d["value"], "p50ttft", d.get("p50_ttft_ms"), "valid", d.get("valid"), d.get("validated"),
+      "inv", d.get("invalid"), "nocont", d.get("no_content"), "kern", b.get("tick_kernel_us_avg"),
+      "tickwall", b.get("tick_wall_us_avg"), "spt", b.get("streams_per_tick"), "fin", b.get("finalize_launches"),
+      "proxy_cpu", b.get("proxy_cpu_ms_per_1k_req"), "lg_cpu", b.get("loadgen_cpu_ms_per_1k_req"))
+EOF
+}
+bench() {  # name timeout env... -- args...
+  local name=$1 to=$2; shift 2
+  local envs=()
+  while [ "$1" != "--" ]; do envs+=("$1"); shift; done; shift
+  timeout -k 10 $to env "${envs[@]}" python bench.py "$@" > $OUT/$name.json 2> $OUT/$name.err
+  local rc=$?
+  summ $name $OUT/$name.json
+  if [ $rc -ne 0 ]; then echo "step $name failed rc=$rc"; tail -25 $OUT/$name.err; return 1; fi
+}
+torchrun_bench() {  # name nproc args...
+  local name=$1 np=$2; shift 2
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $np --master-addr 127.0.0.1 \
+    --master-port $((29500 + RANDOM % 500)) bench.py --gpus $np "$@" > $OUT/$name.json 2> $OUT/$name.err
+  local rc=$?
+  summ $name $OUT/$name.json
+  if [ $rc -ne 0 ]; then echo "step $name failed rc=$rc"; tail -30 $OUT/$name.err; return 1; fi
+}
+
+for step in "$@"; do
+  echo "== $step ($(date +%T))"
+  case $step in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        > $OUT/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -40 $OUT/gpu_tests.log; exit 1; }
+      tail -3 $OUT/gpu_tests.log ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 \
+        || { echo "smoke failed"; tail -20 $OUT/smoke.log; exit 1; }
+      tail -1 $OUT/smoke.log ;;
+    bench|bench=*)
+      n=${step#bench}; n=${n#=}; n=${n:-1}
+      for i in $(seq 1 $n); do bench bench_$i 300 QMX_NOP=1 -- || exit 1; done ;;
+    bench:*)
+      a=${step#bench:}; slug=$(echo "$a" | tr -c 'a-zA-Z0-9' '_')
+      bench bench_$slug 300 QMX_NOP=1 -- ${a//,/ } || exit 1 ;;
+    ab:*)
+      rest=${step#ab:}; name=${rest%%:*}; rest=${rest#*:}; envs=${rest%%:*}; a=${rest#*:}
+      bench ab_$name 300 ${envs//,/ } -- ${a//,/ } || exit 1 ;;
+    scenarios)
+      for SC in aggregate4 highqps8 failure paced; do
+        bench sc_$SC 300 QMX_NOP=1 -- --scenario $SC --steps 10 --warmup 2 || exit 1
+      done ;;
+    reference)
+      bench reference 600 QMX_NOP=1 -- --impl reference --steps 10 --warmup 1 --batch 64 || exit 1 ;;
+    prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o native --output-format csv -- \
+        python3 bench.py --steps 5 --warmup 1 > $OUT/bench_prof.json 2> $OUT/bench_prof.err \
+        || { echo "prof failed"; tail -10 $OUT/bench_prof.err; exit 1; }
+      summ prof $OUT/bench_prof.json
+      find $OUT/prof -name '*kernel_stats.csv' -exec head -5 {} \; ;;
+    pmc:*)
+      ctr=${step#pmc:}; slug=$(echo "$ctr" | tr -c 'a-zA-Z0-9' '_' | cut -c1-60)
+      timeout -s KILL 120 rocprofv3 --pmc ${ctr//,/ } -d $OUT/pmc_$slug -o pmc --output-format csv -- \
+        python3 tools/kbench.py --slots 256 --iters 10 > $OUT/pmc_$slug.log 2>&1 \
+        || { echo "pmc $ctr failed"; tail -10 $OUT/pmc_$slug.log; exit 1; }
+      python3 tools/pmc_summary.py $OUT/pmc_$slug > $OUT/pmc_$slug.md 2>&1; cat $OUT/pmc_$slug.md | head -30 ;;
+    kbench)
+      QMX_STAGE_TIMING=1 timeout -k 10 300 python tools/kbench.py --slots 1,22,64,256 --iters 20 > $OUT/kbench.jsonl 2>&1 \
+        || { echo "kbench failed"; tail -5 $OUT/kbench.jsonl; exit 1; }
+      python3 -c "
+import json
+for l in open('$OUT/kbench.jsonl'):
+    if not l.startswith('{'): continue
+    d=json.loads(l); st=d.get('stage_us_per_item',{})
+    print(d.get('filter'),d.get('emit'),d['slots'],d['wall_us_p50'],d['kernel_us_avg'],[st.get('stage%d_us'%k) for k in range(1,11)])
+" ;;
+    multirank=*)
+      n=${step#multirank=}; torchrun_bench multirank_$n $n --steps 5 --warmup 1 --threads 4 || exit 1 ;;
+    spread=*)
+      n=${step#spread=}; QMX_XCHG=tcp torchrun_bench spread_$n $n --steps 5 --warmup 1 --threads 4 --placement spread || exit 1 ;;
+    cpuprof)
+      bench cpuprof 300 QMX_PROF=$PWD/$OUT/cpu_hip.%p.txt -- --steps 20 --warmup 2 || exit 1
+      for f in $OUT/cpu_hip.*.txt; do python3 tools/cpuprof.py $f --top 30 --json $f.json > $f.summary 2>&1 || true; done
+      head -30 $OUT/cpu_hip.*.summary ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "all done"
