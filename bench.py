@@ -288,7 +288,11 @@ def breakdown(m0, m1, elapsed):
         "tick_launch_wait_us_avg": round(d.get("qmx_kernel_gpu_wait_us", 0.0) / launches, 1) if launches else None,
         "tick_process_us_avg": round(d.get("qmx_kernel_process_us", 0.0) / launches, 1) if launches else None,
         "gpu_busy_frac": round(d.get("qmx_kernel_kernel_ms", 0.0) / 1000 / elapsed, 4) if elapsed else None,
-        "finalize_launches": int(d.get("qmx_kernel_fin_launches", 0.0)),
+        # finalize (K3 strip + K4 join + K5 encode) rides the tick launches: requests folded into
+        # them, and launches of its own (always 0 since r2)
+        "finalize_items_fused": int(d.get("qmx_kernel_fin_items", 0.0)),
+        "finalize_separate_launches": int(d.get("qmx_kernel_fin_separate_launches", 0.0)),
+        "finalize_host": int(d.get("qmx_kernel_fin_host", 0.0)),
         "h2d_MB": round(d.get("qmx_kernel_h2d_bytes", 0.0) / 1e6, 2),
         "d2h_MB": round(d.get("qmx_kernel_d2h_bytes", 0.0) / 1e6, 2),
         "escalations": int(d.get("qmx_kernel_escalations", 0.0)),

@@ -430,7 +430,7 @@ bool HostEngine::tick(int64_t created, std::vector<SlotResult>& results, std::ve
     if (!work.empty() || !fin.empty()) ++ticks_;
   }
   if (work.empty() && fin.empty()) return false;
-  if (!work.empty()) process(work, created, results, lane);
+  run_tick(work, fin, created, results, fres, lane);
   size_t out = 0;
   for (auto& r : results) out += r.sse.size();
   std::vector<int> slots;
@@ -443,7 +443,6 @@ bool HostEngine::tick(int64_t created, std::vector<SlotResult>& results, std::ve
     // generation is the one the results belong to
     for (auto& r : results) r.gen = meta_[r.slot].gen;
   }
-  if (!fin.empty()) finalize(fin, fres, lane);
   if (!taken) settle(slots);
   return true;
 }
@@ -468,7 +467,8 @@ std::unordered_map<std::string, double> HostEngine::stats() {
 // --------------------------------------------------------------------------------
 // CpuEngine
 // --------------------------------------------------------------------------------
-void CpuEngine::process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results, int /*lane*/) {
+void CpuEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin, int64_t created,
+                         std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres, int /*lane*/) {
   for (auto& w : work) {
     SlotCore& c = core_[w.slot];
     bool was_closed = c.done || c.aborted;
@@ -477,15 +477,12 @@ void CpuEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
     int flags = (c.done ? RF_DONE : 0) | (c.aborted ? RF_ABORTED : 0);
     if (!out.empty() || (flags && !was_closed)) results.push_back({w.slot, std::move(out), flags});
   }
-}
-
-void CpuEngine::finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out, int /*lane*/) {
-  for (auto& r : reqs) {
+  for (auto& r : fin) {
     std::vector<std::string> texts;
     for (int s : r.slots) texts.push_back(text(s));
     FinalizeRes fr;
     finalize_texts(ts_, texts, r, fr);
-    out.push_back(std::move(fr));
+    fres.push_back(std::move(fr));
   }
 }
 

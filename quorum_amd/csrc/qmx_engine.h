@@ -157,9 +157,10 @@ class HostEngine {
     bool eof;
     bool fresh;
   };
-  // engine-specific batch processing
-  virtual void process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results, int lane) = 0;
-  virtual void finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out, int lane) = 0;
+  // engine-specific batch processing: the tick's stream work AND its finalize requests
+  // (HipEngine: one fused launch for both; CpuEngine: sequentially)
+  virtual void run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin, int64_t created,
+                        std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres, int lane) = 0;
   virtual void on_free(int /*slot*/) {}
 
   void feed_locked(int slot, const std::string& data);
@@ -196,8 +197,8 @@ class CpuEngine : public HostEngine {
   explicit CpuEngine(const std::vector<std::string>& tags) : HostEngine(tags) {}
 
  protected:
-  void process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results, int lane) override;
-  void finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out, int lane) override;
+  void run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin, int64_t created,
+                std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres, int lane) override;
 };
 
 // Shared by both engines' host-side finalisation.

@@ -54,7 +54,8 @@ struct KParams {
   unsigned long long* dbg;  // optional per-stage stamps [item][16] (QMX_STAGE_TIMING=1)
 };
 
-// Finalize (K3 strip + K4 join + K5 encode) work: one workgroup per session request.
+// Finalize (K3 strip + K4 join + K5 encode) work: one workgroup of the fused tick launch
+// per session request.
 struct FinItem {
   uint32_t first_text, n_texts;     // into the FinText array
   uint32_t flags;                   // 1 strip, 2 texts-kind (no join / encode)
@@ -62,13 +63,16 @@ struct FinItem {
   uint32_t out_off, out_cap;        // device + host output offset (16-B aligned), capacity
   uint32_t joiner_off, joiner_len;  // in the finalize input arena
   uint32_t pre_off, pre_len, suf_off, suf_len;
+  uint32_t seg_off, seg_cap;        // kept-segment scratch (device), entries
+  uint32_t tl_off;                  // texts-kind: per-text stripped lengths at text_len[tl_off..]
 };
 struct FinText {
   uint32_t slot, len;
 };
 struct FinResult {
   uint32_t out_len, status, n_kept;  // status 1: escalate to the host path
-  uint32_t text_len[8];              // texts-kind: per-text stripped lengths
+  uint32_t seq;                      // written last (system-scope release), as WorkResult::seq
+  uint64_t t0, t1;                   // s_memrealtime at workgroup start / end
 };
 
 // Launch resources of one tick lane: a tick thread owns a lane (HIP stream, events,
@@ -95,6 +99,26 @@ struct TickLane {
   double kernel_ms = 0.0, host_prep_us = 0, gpu_wait_us = 0, process_us = 0;  // host-side tick breakdown
   double stage_us[16] = {0};
   double clk_cycles = 0, clk_us = 0;
+  // finalize arenas (fused into this lane's tick launches)
+  FinItem* h_fin = nullptr;
+  size_t fin_cap = 0;
+  FinResult* h_finres = nullptr;
+  size_t finres_cap = 0;
+  FinText* h_fint = nullptr;
+  size_t fint_cap = 0;
+  uint8_t* h_fin_in = nullptr;
+  size_t fin_in_cap = 0;
+  uint8_t* h_fout = nullptr;
+  size_t fout_cap = 0;
+  uint32_t* h_tl = nullptr;
+  size_t tl_cap = 0;
+  uint8_t* d_join = nullptr;
+  size_t join_cap = 0;
+  uint8_t* d_fout = nullptr;
+  size_t dfout_cap = 0;
+  uint8_t* d_segs = nullptr;  // int2 entries
+  size_t segs_cap = 0;        // bytes
+  uint64_t fin_launches = 0, fin_items = 0, fin_host = 0;  // launches that carried finalize work
   // completion by polling the kernel-published sequence numbers (HipEngine::wait_results)
   uint32_t seq = 0;
   double ema_us = 40.0;  // launch-to-results time, smoothed
@@ -112,15 +136,19 @@ class HipEngine : public HostEngine {
   int lanes() const { return (int)lanes_.size(); }
 
  protected:
-  void process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results, int lane) override;
-  void finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out, int lane) override;
+  void run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin, int64_t created,
+                std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres, int lane) override;
   void on_free(int slot) override;
 
  private:
   void escalate(int slot, bool fresh);
   void finalize_host(const FinalizeReq& r, std::vector<FinalizeRes>& out);
+  // finalize items of this tick → the lane's arenas; returns the GPU ones (others: host path)
+  std::vector<const FinalizeReq*> prep_finalize(TickLane& L, std::vector<FinalizeReq>& fin,
+                                                std::vector<const FinalizeReq*>& host);
+  void collect_finalize(TickLane& L, const std::vector<const FinalizeReq*>& gpu, std::vector<FinalizeRes>& out);
   void wait_stream(TickLane& L);
-  void wait_results(TickLane& L, int n, uint32_t seq);
+  void wait_results(TickLane& L, int n, int m, uint32_t seq);
   void collect_timing(TickLane& L);
   void ensure_in(TickLane& L, size_t bytes);
   void ensure_out(TickLane& L, size_t bytes);
@@ -133,22 +161,6 @@ class HipEngine : public HostEngine {
   uint32_t content_cap_;
   KParams base_params_;  // tag patterns (each lane's copy also gets the tick's envelopes)
   std::vector<std::unique_ptr<TickLane>> lanes_;
-  // finalize arenas: one finalize at a time (fin_mu_), on the calling lane's stream
-  std::mutex fin_mu_;
-  FinItem* h_fin_ = nullptr;
-  size_t fin_cap_ = 0;
-  FinResult* h_finres_ = nullptr;
-  size_t finres_cap_ = 0;
-  FinText* h_fint_ = nullptr;
-  size_t fint_cap_ = 0;
-  uint8_t* h_fin_in_ = nullptr;
-  size_t fin_in_cap_ = 0;
-  uint8_t* h_fout_ = nullptr;
-  size_t fout_cap_ = 0;
-  uint8_t* d_join_ = nullptr;
-  size_t join_cap_ = 0;
-  uint8_t* d_fout_ = nullptr;
-  size_t dfout_cap_ = 0;
   // device-resident
   DevSlot* d_state_ = nullptr;
   uint8_t* d_content_ = nullptr;
@@ -157,8 +169,6 @@ class HipEngine : public HostEngine {
   std::vector<uint32_t> content_len_;    // device content bytes per slot
   // stats
   std::atomic<uint64_t> escalations_{0}, fin_host_{0};
-  uint64_t fin_launches_ = 0, fin_items_ = 0;  // under fin_mu_
-  double fin_ms_ = 0.0;
   int spin_us_ = 0;  // QMX_WAIT_SPIN_US: yield-poll before the blocking wait
   bool poll_ = true;  // QMX_WAIT=event: wait on a blocking-sync HIP event instead of polling
   int poll_us_ = 6;   // QMX_POLL_US: poll period once the expected kernel time has passed

@@ -301,15 +301,24 @@ __device__ inline int hold_cut(const Smem& s, const uint8_t* Z, int ncand, int n
 // ------------------------------------------------------------------------------------
 // the fused tick kernel
 // ------------------------------------------------------------------------------------
+// LDS of a tick workgroup (the fused kernel overlays it with the finalize workgroup's)
+struct TickShared {
+  Smem s;
+  KParams P;                                   // kernel args staged in LDS: lane-divergent reads
+  uint16_t TKP[BS / 64][TOK_CAP];              // per-wave token buffers (positions)
+  alignas(8) uint8_t TKT[BS / 64][TOK_CAP];    // token bytes (type | key id | flags)
+  int wtpl[BS / 64][4];  // S3: per-wave in-tile templates {p0, tp, s0, ts} (p0 < 0: none)
+};
+
 __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, const uint8_t* __restrict__ in,
                                           uint8_t* __restrict__ out, WorkResult* __restrict__ res,
                                           DevSlot* __restrict__ state, uint8_t* __restrict__ content,
-                                          const KParams& Pk) {
-  __shared__ Smem s;
-  __shared__ KParams P;  // kernel args staged in LDS: lane-divergent pattern/envelope reads
-  __shared__ uint16_t TKP[BS / 64][TOK_CAP];  // per-wave token buffers (positions)
-  __shared__ alignas(8) uint8_t TKT[BS / 64][TOK_CAP];  // token bytes (type | key id | flags)
-  __shared__ int wtpl[BS / 64][4];  // S3: per-wave in-tile templates {p0, tp, s0, ts} (p0 < 0: none)
+                                          const KParams& Pk, TickShared& U) {
+  Smem& s = U.s;
+  KParams& P = U.P;
+  auto& TKP = U.TKP;
+  auto& TKT = U.TKT;
+  auto& wtpl = U.wtpl;
   const int tid = threadIdx.x;
   for (int i = tid; i < (int)(sizeof(KParams) / 4); i += BS) ((uint32_t*)&P)[i] = ((const uint32_t*)&Pk)[i];
   QMX_STAMP(0);
@@ -1062,84 +1071,57 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   }
 }
 
-// Every workgroup publishes its result last: all threads fence their host-mapped stores
-// (output SSE, result record) at system scope, then thread 0 stores the tick's sequence
-// number into the record.  The host polls these sequence numbers instead of waiting on a
-// HIP event: no interrupt round trip and no HSA spin-wait per tick (tools/cpuprof.py: the
-// blocked event wait spun inside libhsa-runtime for most of each kernel's duration).
-// Every early exit of tick_body is block-uniform, so every thread reaches the fence.
-__global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict__ items,
-                                                      const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
-                                                      WorkResult* __restrict__ res, DevSlot* __restrict__ state,
-                                                      uint8_t* __restrict__ content, KParams Pk, uint32_t seq) {
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  tick_body(items, in, out, res, state, content, Pk);
-  if (threadIdx.x == 0) {
-    res[blockIdx.x].t0 = t0;
-    res[blockIdx.x].t1 = __builtin_amdgcn_s_memrealtime();
-  }
-  __threadfence_system();
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(&res[blockIdx.x].seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // ------------------------------------------------------------------------------------
-// the finalize kernel: K3 think_strip_final + K4 join_pack + K5 sse_encode, one workgroup
-// per session request, texts read straight from the HBM-resident content arena
-// (reference oai_proxy.py:120-139 strip, :834-860 join + final event)
+// finalize body: K3 think_strip_final + K4 join_pack + K5 sse_encode for one session
+// request, texts read straight from the HBM-resident content arena (reference
+// oai_proxy.py:120-139 strip, :834-860 join + final event, :406-423 texts for the aggregator)
 // ------------------------------------------------------------------------------------
-constexpr int FIN_TOK_MAX = 4096;  // tag tokens per text staged in LDS (more → host path)
-constexpr int FIN_SEG_MAX = FIN_TOK_MAX / 2 + 2;
+constexpr int FIN_TOK = 4096;   // tag tokens of one tokenisation window staged in LDS
+constexpr int FIN_WIN = 8192;   // window bytes: a token is >= 3 bytes, so <= 2731 tokens per window
+constexpr int FIN_BIG = 256;    // kept segments at least this long are copied by the whole workgroup
 
-struct FinSmem {
-  int32_t tpos[FIN_TOK_MAX];
-  int8_t tkid[FIN_TOK_MAX];  // +(t+1) open, -(t+1) close
-  uint8_t tlen[FIN_TOK_MAX];
-  int32_t seg_a[FIN_SEG_MAX], seg_b[FIN_SEG_MAX], seg_o[FIN_SEG_MAX + 1];
-  int32_t scr[2 * (BS / 64)];  // block scans: one (pair) partial per wave
-  int32_t v[4];
+struct FinShared {
+  int32_t tpos[FIN_TOK];
+  int8_t tkid[FIN_TOK];  // +(t+1) open, -(t+1) close
+  uint8_t tlen[FIN_TOK];
+  int32_t scr[2 * (BS / 64)];
+  int32_t v[16];
+  int32_t last_close[kMaxTags];  // start of the last close token of each tag in the text
 };
+enum : int { FV_CUR = 0, FV_PEND, FV_SEGA, FV_NSEG, FV_NTOK, FV_S0, FV_S1, FV_NBIG, FV_OVF };
 
-__global__ __launch_bounds__(BS) void qmx_finalize_kernel(const FinItem* __restrict__ items,
-                                                          const FinText* __restrict__ texts,
-                                                          const uint8_t* __restrict__ fin_in,
-                                                          const uint8_t* __restrict__ content, uint32_t content_cap,
-                                                          uint8_t* __restrict__ join_buf, uint8_t* __restrict__ out_dev,
-                                                          uint8_t* __restrict__ out_host, FinResult* __restrict__ res,
-                                                          TagSet ts) {
-  __shared__ FinSmem f;
+// Interval selection of re.sub("<(t)>.*?</\1>", "", IGNORECASE|DOTALL): leftmost open whose
+// tag closes later (re tries every start position, so an open that never closes is just
+// skipped), its interval ends at the FIRST close of the same tag after it, the scan resumes
+// there.  Blockwise over tokenisation windows with the (cursor, pending-tag) state carried
+// between them; within a window wave 0 walks 64 tokens per step by ballot: each selection is
+// one ballot + find-first + shuffle (no per-token thread-serial loop, no token-count cap).
+// Kept segments (text between selected intervals) go to segs[]; returns their count, -1 if
+// more than cap (host path).  Block-uniform.
+__device__ __forceinline__ int fin_select(const uint8_t* __restrict__ src, int n, const TagSet& ts, int2* __restrict__ segs, int cap,
+                          FinShared& F) {
   const int tid = threadIdx.x;
-  const FinItem it = items[blockIdx.x];
-  const bool strip = it.flags & 1, as_texts = it.flags & 2;
-  uint8_t* J = join_buf + it.join_off;
-  int jl = 0, nk = 0;
-  uint32_t tlens[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  auto bail = [&]() {
-    if (tid == 0) {
-      FinResult r;
-      r.out_len = 0;
-      r.status = 1;
-      r.n_kept = 0;
-      res[blockIdx.x] = r;
-    }
-  };
-  for (uint32_t i = 0; i < it.n_texts; ++i) {
-    const FinText ft = texts[it.first_text + i];
-    const int n = (int)ft.len;
-    if (n == 0) continue;  // empty texts are not kept (nor joined)
-    if (as_texts && nk >= 8) {
-      bail();
-      return;
-    }
-    const uint8_t* src = content + (size_t)ft.slot * content_cap;
-    if (nk > 0 && !as_texts) {
-      for (uint32_t k = tid; k < it.joiner_len; k += BS) J[jl + k] = fin_in[it.joiner_off + k];
-      jl += (int)it.joiner_len;
-    }
-    if (strip) {
-      // K3a: tag tokens (contiguous byte range per thread, compacted in order)
-      const int C = (n + BS - 1) / BS;
-      const int lo = min(tid * C, n), hi = min(lo + C, n);
+  if (tid < kMaxTags) F.last_close[tid] = -1;
+  if (tid == 0) {
+    F.v[FV_CUR] = 0;
+    F.v[FV_PEND] = 0;
+    F.v[FV_SEGA] = 0;
+    F.v[FV_NSEG] = 0;
+    F.v[FV_OVF] = 0;
+  }
+  __syncthreads();
+  for (int p = tid; p < n; p += BS) {  // pass 0: which opens can close at all
+    if (src[p] != '<' || p + 1 >= n || src[p + 1] != '/') continue;
+    int L = 0;
+    const int id = match_at(src, n, p, ts, &L);
+    if (id < 0) atomicMax(&F.last_close[-id - 1], p);
+  }
+  __syncthreads();
+  for (int w0 = 0; w0 < n; w0 += FIN_WIN) {
+    const int w1 = min(n, w0 + FIN_WIN);
+    {  // tokens starting in [w0, w1), compacted in position order
+      const int C = (w1 - w0 + BS - 1) / BS;
+      const int lo = min(w0 + tid * C, w1), hi = min(lo + C, w1);
       int cnt = 0;
       for (int p = lo; p < hi; ++p) {
         if (src[p] != '<') continue;
@@ -1147,102 +1129,194 @@ __global__ __launch_bounds__(BS) void qmx_finalize_kernel(const FinItem* __restr
         cnt += match_at(src, n, p, ts, &L) != 0;
       }
       int tot;
-      int k = block_excl_sum(cnt, f.scr, &tot);
-      if (tot > FIN_TOK_MAX) {
-        bail();
-        return;
-      }
+      int k = block_excl_sum(cnt, F.scr, &tot);
       for (int p = lo; p < hi && cnt > 0; ++p) {
         if (src[p] != '<') continue;
         int L = 0;
         const int id = match_at(src, n, p, ts, &L);
         if (id == 0) continue;
-        f.tpos[k] = p;
-        f.tkid[k] = (int8_t)id;
-        f.tlen[k] = (uint8_t)L;
+        F.tpos[k] = p;
+        F.tkid[k] = (int8_t)id;
+        F.tlen[k] = (uint8_t)L;
         ++k;
       }
-      __syncthreads();
-      // K3b: leftmost-first, non-greedy, same-tag intervals (regex <(t)>.*?</\1>), then
-      // str.strip() across the kept segments.  Per-tag close pointers only move forward.
-      if (tid == 0) {
-        int cp[kMaxTags];
-        for (int t = 0; t < kMaxTags; ++t) cp[t] = 0;
-        int pos = 0, ns = 0;
-        for (int q = 0; q < tot; ++q) {
-          const int id = f.tkid[q];
-          if (id <= 0 || f.tpos[q] < pos) continue;
-          int j = max(cp[id - 1], q + 1);
-          while (j < tot && f.tkid[j] != -id) ++j;
-          cp[id - 1] = j;
-          if (j >= tot) continue;
-          f.seg_a[ns] = pos;
-          f.seg_b[ns] = f.tpos[q];
-          ++ns;
-          pos = f.tpos[j] + f.tlen[j];
-          q = j;
-        }
-        f.seg_a[ns] = pos;
-        f.seg_b[ns] = n;
-        ++ns;
-        int s0 = 0;
-        for (; s0 < ns; ++s0) {
-          while (f.seg_a[s0] < f.seg_b[s0]) {
-            const int w = ws_at(src, f.seg_a[s0], f.seg_b[s0]);
-            if (w <= 0) break;
-            f.seg_a[s0] += w;
-          }
-          if (f.seg_a[s0] < f.seg_b[s0]) break;
-        }
-        int s1 = ns - 1;
-        for (; s1 >= s0; --s1) {
-          while (f.seg_b[s1] > f.seg_a[s1]) {
-            const int w = ws_before(src, f.seg_a[s1], f.seg_b[s1]);
-            if (w <= 0) break;
-            f.seg_b[s1] -= w;
-          }
-          if (f.seg_b[s1] > f.seg_a[s1]) break;
-        }
-        int m = 0, off = 0;
-        for (int q = s0; q <= s1; ++q) {
-          f.seg_a[m] = f.seg_a[q];
-          f.seg_b[m] = f.seg_b[q];
-          f.seg_o[m] = off;
-          off += f.seg_b[q] - f.seg_a[q];
-          ++m;
-        }
-        f.seg_o[m] = off;
-        f.v[0] = m;
-      }
-    } else if (tid == 0) {
-      f.seg_a[0] = 0;
-      f.seg_b[0] = n;
-      f.seg_o[0] = 0;
-      f.seg_o[1] = n;
-      f.v[0] = 1;
+      if (tid == 0) F.v[FV_NTOK] = tot;
     }
     __syncthreads();
-    // K4: copy the kept segments into the join buffer
-    const int nseg = f.v[0];
-    for (int q = 0; q < nseg; ++q) {
-      const int a = f.seg_a[q], len = f.seg_b[q] - a, o = jl + f.seg_o[q];
-      for (int x = tid; x < len; x += BS) J[o + x] = src[a + x];
+    if (tid < 64) {
+      const int lane = tid;
+      const int ntok = F.v[FV_NTOK];
+      int cur = F.v[FV_CUR], pend = F.v[FV_PEND], sega = F.v[FV_SEGA], nseg = F.v[FV_NSEG];
+      for (int c0 = 0; c0 < ntok; c0 += 64) {
+        const int k = c0 + lane;
+        const bool valid = k < ntok;
+        const int pos = valid ? F.tpos[k] : 0x7fffffff;
+        const int id = valid ? (int)F.tkid[k] : 0;
+        const int end = pos + (valid ? (int)F.tlen[k] : 0);
+        const bool can_open = id > 0 && F.last_close[id - 1] >= end;
+        while (true) {
+          uint64_t m;
+          if (pend != 0) {
+            m = __ballot(valid && id == -pend && pos >= cur);
+            if (m == 0) break;
+            const int L = __ffsll((unsigned long long)m) - 1;
+            cur = __shfl(end, L, 64);
+            pend = 0;
+            sega = cur;
+          } else {
+            m = __ballot(can_open && pos >= cur);
+            if (m == 0) break;
+            const int L = __ffsll((unsigned long long)m) - 1;
+            const int po = __shfl(pos, L, 64);
+            if (po > sega) {
+              if (lane == 0 && nseg < cap) segs[nseg] = make_int2(sega, po);
+              ++nseg;
+            }
+            pend = __shfl(id, L, 64);
+            cur = __shfl(end, L, 64);
+          }
+        }
+      }
+      if (lane == 0) {
+        F.v[FV_CUR] = cur;
+        F.v[FV_PEND] = pend;
+        F.v[FV_SEGA] = sega;
+        F.v[FV_NSEG] = nseg;
+      }
     }
-    const int tl = f.seg_o[nseg];
-    if (as_texts) tlens[nk] = (uint32_t)tl;
-    jl += tl;
-    ++nk;
-    __syncthreads();  // LDS token/segment arrays are reused by the next text
+    __syncthreads();
+  }
+  // an open is only taken when its tag closes later, so no interval is left pending
+  if (tid == 0) {
+    int nseg = F.v[FV_NSEG];
+    const int sega = F.v[FV_SEGA];
+    if (n > sega) {
+      if (nseg < cap) segs[nseg] = make_int2(sega, n);
+      ++nseg;
+    }
+    F.v[FV_NSEG] = nseg;
   }
   __syncthreads();
-  uint8_t* O = out_dev + it.out_off;
+  const int nseg = F.v[FV_NSEG];
+  return nseg > cap ? -1 : nseg;
+}
+
+struct FinArgs {
+  const FinItem* items;
+  const FinText* texts;
+  const uint8_t* fin_in;   // joiners + final-event envelopes (host-mapped)
+  uint8_t* join;           // device join buffer
+  uint8_t* out_dev;        // device encode buffer
+  uint8_t* out_host;       // host-mapped output
+  FinResult* res;          // host-mapped result records
+  uint32_t* text_len;      // host-mapped per-text stripped lengths (texts-kind)
+  int2* segs;              // device kept-segment scratch
+};
+
+__device__ __forceinline__ void fin_body(const FinArgs& fa, int j, const uint8_t* __restrict__ content, uint32_t content_cap,
+                         const TagSet& ts, FinShared& F) {
+  const int tid = threadIdx.x;
+  const FinItem it = fa.items[j];
+  const bool strip = it.flags & 1, as_texts = it.flags & 2;
+  uint8_t* J = fa.join + it.join_off;
+  int2* segs = fa.segs + it.seg_off;
+  int jl = 0, nk = 0;
+  auto bail = [&]() {
+    if (tid == 0) {
+      FinResult r{};
+      r.status = 1;
+      fa.res[j] = r;
+    }
+  };
+  for (uint32_t i = 0; i < it.n_texts; ++i) {
+    const FinText ft = fa.texts[it.first_text + i];
+    const int n = (int)ft.len;
+    if (n == 0) continue;  // empty texts are not kept (nor joined)
+    const uint8_t* src = content + (size_t)ft.slot * content_cap;
+    if (nk > 0 && !as_texts) {
+      for (uint32_t k = tid; k < it.joiner_len; k += BS) J[jl + k] = fa.fin_in[it.joiner_off + k];
+      jl += (int)it.joiner_len;
+    }
+    int nseg = 1;
+    if (strip) {
+      nseg = fin_select(src, n, ts, segs, (int)it.seg_cap, F);
+      if (nseg < 0) {
+        bail();
+        return;
+      }
+    } else if (tid == 0) {
+      segs[0] = make_int2(0, n);
+    }
+    __syncthreads();
+    if (tid == 0) {  // str.strip() over the kept text: whitespace at the outer segment ends
+      int s0 = 0, s1 = nseg - 1;
+      if (strip) {
+        for (; s0 < nseg; ++s0) {
+          int2 g = segs[s0];
+          while (g.x < g.y) {
+            const int w = ws_at(src, g.x, g.y);
+            if (w <= 0) break;
+            g.x += w;
+          }
+          segs[s0] = g;
+          if (g.x < g.y) break;
+        }
+        for (; s1 >= s0; --s1) {
+          int2 g = segs[s1];
+          while (g.y > g.x) {
+            const int w = ws_before(src, g.x, g.y);
+            if (w <= 0) break;
+            g.y -= w;
+          }
+          segs[s1] = g;
+          if (g.y > g.x) break;
+        }
+      }
+      F.v[FV_S0] = s0;
+      F.v[FV_S1] = s1;
+    }
+    __syncthreads();
+    // K4: kept segments → join buffer (short ones by one thread each, long ones by all)
+    const int s0 = F.v[FV_S0], s1 = F.v[FV_S1];
+    int run = 0;
+    for (int c0 = s0; c0 <= s1; c0 += BS) {
+      const int q = c0 + tid;
+      const int2 g = q <= s1 ? segs[q] : make_int2(0, 0);
+      const int len = g.y - g.x;
+      if (tid == 0) F.v[FV_NBIG] = 0;
+      int tot;
+      const int dst = jl + run + block_excl_sum(len, F.scr, &tot);  // (its barriers order the reset)
+      if (len >= FIN_BIG) {
+        const int b = atomicAdd(&F.v[FV_NBIG], 1);
+        F.tpos[3 * b] = g.x;  // tokens are dead by now: reuse as the big-segment list
+        F.tpos[3 * b + 1] = len;
+        F.tpos[3 * b + 2] = dst;
+      } else {
+        for (int x = 0; x < len; ++x) J[dst + x] = src[g.x + x];
+      }
+      __syncthreads();
+      const int nbig = F.v[FV_NBIG];
+      for (int b = 0; b < nbig; ++b) {
+        const int a = F.tpos[3 * b], l = F.tpos[3 * b + 1], d = F.tpos[3 * b + 2];
+        for (int x = tid; x < l; x += BS) J[d + x] = src[a + x];
+      }
+      __syncthreads();
+      run += tot;
+    }
+    if (as_texts && tid == 0) fa.text_len[it.tl_off + nk] = (uint32_t)run;
+    jl += run;
+    ++nk;
+    __syncthreads();  // LDS token / state arrays are reused by the next text
+  }
+  __syncthreads();
+  uint8_t* O = fa.out_dev + it.out_off;
   int out_len = 0;
   const uint8_t* src_out = J;
   if (as_texts) {
     out_len = jl;
   } else if (nk > 0) {
     // K5: ensure_ascii JSON escape of the joined text inside the final-event envelope
-    for (uint32_t k = tid; k < it.pre_len; k += BS) O[k] = fin_in[it.pre_off + k];
+    for (uint32_t k = tid; k < it.pre_len; k += BS) O[k] = fa.fin_in[it.pre_off + k];
     const int C = (jl + BS - 1) / BS;
     int lo = min(tid * C, jl), hi = min(lo + C, jl);
     while (lo < jl && is_cont(J[lo])) ++lo;  // code points starting in [lo, hi): both bounds
@@ -1255,7 +1329,7 @@ __global__ __launch_bounds__(BS) void qmx_finalize_kernel(const FinItem* __restr
       el += escaped_len_cp(cpv);
     }
     int tot;
-    int o = (int)it.pre_len + block_excl_sum(el, f.scr, &tot);
+    int o = (int)it.pre_len + block_excl_sum(el, F.scr, &tot);
     out_len = (int)it.pre_len + tot + (int)it.suf_len;
     if ((uint32_t)out_len > it.out_cap) {
       bail();
@@ -1266,21 +1340,63 @@ __global__ __launch_bounds__(BS) void qmx_finalize_kernel(const FinItem* __restr
       p += wtf8_decode(J, p, jl, &cpv);
       o += escape_cp(cpv, O + o);
     }
-    for (uint32_t k = tid; k < it.suf_len; k += BS) O[it.pre_len + tot + k] = fin_in[it.suf_off + k];
+    for (uint32_t k = tid; k < it.suf_len; k += BS) O[it.pre_len + tot + k] = fa.fin_in[it.suf_off + k];
     src_out = O;
   }
   __syncthreads();
   // coalesced 16-B stores into the host-mapped output arena
-  uint4* dst = (uint4*)(out_host + it.out_off);
+  uint4* dst = (uint4*)(fa.out_host + it.out_off);
   const uint4* sv = (const uint4*)src_out;
   for (int k = tid; k * 16 < out_len; k += BS) dst[k] = sv[k];
   if (tid == 0) {
-    FinResult r;
+    FinResult r{};
     r.out_len = (uint32_t)out_len;
     r.status = 0;
     r.n_kept = (uint32_t)nk;
-    for (int q = 0; q < 8; ++q) r.text_len[q] = tlens[q];
-    res[blockIdx.x] = r;
+    fa.res[j] = r;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// the fused kernel: workgroups [0, n_tick) run one stream tile each, [n_tick, grid) one
+// finalize request each — one launch per tick for both (their LDS overlays: a workgroup is
+// one or the other).  Every workgroup publishes its result record last: all threads fence
+// their host-mapped stores (output, result record) at system scope, then thread 0 stores the
+// tick's sequence number into the record.  The host polls these sequence numbers instead of
+// waiting on a HIP event (no interrupt round trip, no HSA spin-wait per tick).  Every early
+// exit of tick_body / fin_body is block-uniform, so every thread reaches the fence.
+// ------------------------------------------------------------------------------------
+union TickLds {
+  TickShared t;
+  FinShared f;
+};
+
+__global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict__ items,
+                                                      const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                      WorkResult* __restrict__ res, DevSlot* __restrict__ state,
+                                                      uint8_t* __restrict__ content, KParams Pk, uint32_t seq,
+                                                      uint32_t n_tick, FinArgs fa) {
+  __shared__ TickLds U;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  if (blockIdx.x < n_tick) {
+    tick_body(items, in, out, res, state, content, Pk, U.t);
+    if (threadIdx.x == 0) {
+      res[blockIdx.x].t0 = t0;
+      res[blockIdx.x].t1 = __builtin_amdgcn_s_memrealtime();
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(&res[blockIdx.x].seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  } else {
+    const int j = (int)(blockIdx.x - n_tick);
+    fin_body(fa, j, content, Pk.content_cap, Pk.ts, U.f);
+    if (threadIdx.x == 0) {
+      fa.res[j].t0 = t0;
+      fa.res[j].t1 = __builtin_amdgcn_s_memrealtime();
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(&fa.res[j].seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -1313,7 +1429,7 @@ void HipEngine::wait_stream(TickLane& L) {
 // most of the expected kernel time (EMA), then poll every poll_us_ with a 1 us timer slack.
 // A launch that has not published after 4x the EMA + 2 ms synchronises its stream (surfaces a
 // fault; correct even if host-mapped visibility misbehaved: counted in poll_fallbacks).
-void HipEngine::wait_results(TickLane& L, int n, uint32_t seq) {
+void HipEngine::wait_results(TickLane& L, int n, int m, uint32_t seq) {
   using HC = std::chrono::steady_clock;
   static thread_local bool slack = (prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0), true);
   (void)slack;
@@ -1325,7 +1441,8 @@ void HipEngine::wait_results(TickLane& L, int n, uint32_t seq) {
   };
   auto done = [&](int& i) {
     while (i < n && __atomic_load_n(&L.h_res[i].seq, __ATOMIC_ACQUIRE) == seq) ++i;
-    return i == n;
+    while (i >= n && i < n + m && __atomic_load_n(&L.h_finres[i - n].seq, __ATOMIC_ACQUIRE) == seq) ++i;
+    return i == n + m;
   };
   int i = 0;
   nap(0.6 * L.ema_us - 6.0);
@@ -1425,6 +1542,15 @@ HipEngine::~HipEngine() {
     if (L->h_items) hipHostFree(L->h_items);
     if (L->h_res) hipHostFree(L->h_res);
     if (L->h_dbg) hipHostFree(L->h_dbg);
+    if (L->h_fin) hipHostFree(L->h_fin);
+    if (L->h_finres) hipHostFree(L->h_finres);
+    if (L->h_fint) hipHostFree(L->h_fint);
+    if (L->h_fin_in) hipHostFree(L->h_fin_in);
+    if (L->h_fout) hipHostFree(L->h_fout);
+    if (L->h_tl) hipHostFree(L->h_tl);
+    if (L->d_join) hipFree(L->d_join);
+    if (L->d_fout) hipFree(L->d_fout);
+    if (L->d_segs) hipFree(L->d_segs);
     if (L->ev0) hipEventDestroy(L->ev0);
     if (L->ev1) hipEventDestroy(L->ev1);
     if (L->evb) hipEventDestroy(L->evb);
@@ -1432,13 +1558,6 @@ HipEngine::~HipEngine() {
   }
   if (d_state_) hipFree(d_state_);
   if (d_content_) hipFree(d_content_);
-  if (h_fin_) hipHostFree(h_fin_);
-  if (h_finres_) hipHostFree(h_finres_);
-  if (h_fint_) hipHostFree(h_fint_);
-  if (h_fin_in_) hipHostFree(h_fin_in_);
-  if (h_fout_) hipHostFree(h_fout_);
-  if (d_join_) hipFree(d_join_);
-  if (d_fout_) hipFree(d_fout_);
 }
 
 void HipEngine::ensure_in(TickLane& L, size_t bytes) {
@@ -1502,7 +1621,8 @@ std::string HipEngine::text(int slot) {
   return device_content(slot, content_len_[slot]);
 }
 
-void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<SlotResult>& results, int lane) {
+void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin, int64_t created,
+                         std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres, int lane) {
   TickLane& L = *lanes_[(size_t)lane % lanes_.size()];
   std::lock_guard<std::mutex> lg(L.mu);  // a lane is driven by one thread; kernel_stats() reads under it
   using HC = std::chrono::steady_clock;
@@ -1593,7 +1713,11 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
     pend.push_back({slot, cl, sub, eof_sent, &w});
     ++n;
   }
-  if (n > 0) {
+  // finalize requests ride the same launch: workgroups [n, n + m)
+  std::vector<const FinalizeReq*> fin_host;
+  const std::vector<const FinalizeReq*> fin_gpu = prep_finalize(L, fin, fin_host);
+  const int m = (int)fin_gpu.size();
+  if (n + m > 0) {
     build_params(L, created);
     L.params.dbg = nullptr;
     if (getenv("QMX_STAGE_TIMING")) {
@@ -1611,16 +1735,23 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
     L.h2d_bytes += in_off;
     const uint32_t seq = ++L.seq;
     if (!poll_) HIP_CHECK(hipEventRecord(L.ev0, L.stream));
-    hipLaunchKernelGGL(qmx_tick_kernel, dim3(n), dim3(BS), 0, L.stream, L.h_items, L.h_in, L.h_out, L.h_res, d_state_,
-                       d_content_, L.params, seq);
+    FinArgs fa{L.h_fin, L.h_fint, L.h_fin_in, L.d_join, L.d_fout, L.h_fout, L.h_finres, L.h_tl, (int2*)L.d_segs};
+    hipLaunchKernelGGL(qmx_tick_kernel, dim3(n + m), dim3(BS), 0, L.stream, L.h_items, L.h_in, L.h_out, L.h_res,
+                       d_state_, d_content_, L.params, seq, (uint32_t)n, fa);
     HIP_CHECK(hipGetLastError());
+    // sessions the GPU does not finalize (escalated streams) are finalized here meanwhile
+    for (const FinalizeReq* r : fin_host) finalize_host(*r, fres);
     if (poll_) {
       // one HIP call per tick: completion and kernel span both come from the result records
-      wait_results(L, n, seq);
+      wait_results(L, n, m, seq);
       uint64_t a = ~0ull, b = 0;
       for (int i = 0; i < n; ++i) {
         a = std::min(a, L.h_res[i].t0);
         b = std::max(b, L.h_res[i].t1);
+      }
+      for (int i = 0; i < m; ++i) {
+        a = std::min(a, L.h_finres[i].t0);
+        b = std::max(b, L.h_finres[i].t1);
       }
       if (b > a) L.kernel_ms += (double)(b - a) * 1e-5;  // 100 MHz ticks -> ms
     } else {
@@ -1633,6 +1764,10 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
     L.gpu_wait_us += std::chrono::duration<double, std::micro>(HC::now() - tp1).count();
     ++L.launches;
     L.items += n;
+    if (m > 0) {
+      ++L.fin_launches;
+      L.fin_items += m;
+    }
     if (L.params.dbg) {
       for (int i = 0; i < n; ++i) {
         const unsigned long long* d = L.h_dbg + kDbg * i;
@@ -1710,6 +1845,9 @@ void HipEngine::process(std::vector<Work>& work, int64_t created, std::vector<Sl
     if (r.out_len) sse.assign((const char*)L.h_out + L.h_items[i].out_off, r.out_len);
     if (!sse.empty() || flags) results.push_back({p.slot, std::move(sse), flags});
   }
+  if (m > 0) collect_finalize(L, fin_gpu, fres);
+  if (n + m == 0)
+    for (const FinalizeReq* r : fin_host) finalize_host(*r, fres);
   if (!requeue.empty()) {
     std::lock_guard<std::mutex> g(mu_);
     for (int s : requeue) {
@@ -1745,104 +1883,100 @@ static void grow_device(uint8_t** p, size_t* cap, size_t need) {
   HIP_CHECK(hipMalloc((void**)p, *cap + 64));
 }
 
-void HipEngine::finalize(std::vector<FinalizeReq>& reqs, std::vector<FinalizeRes>& out, int lane) {
-  std::lock_guard<std::mutex> fg(fin_mu_);  // finalize arenas are shared by the lanes
-  TickLane& L = *lanes_[(size_t)lane % lanes_.size()];
-  const int nsl = (int)nslots();
-  // Sessions whose texts are all HBM-resident run on the GPU (K3+K4+K5); a session with an
-  // escalated (host-path) stream, or > 8 texts in texts-kind, is finalized on the host.
+// Finalize items of a tick, staged in the lane's arenas for the fused launch.  Sessions whose
+// texts are all HBM-resident run on the GPU (K3+K4+K5 workgroups); a session with an
+// escalated (host-path) stream is finalized on the host.
+std::vector<const FinalizeReq*> HipEngine::prep_finalize(TickLane& L, std::vector<FinalizeReq>& reqs,
+                                                         std::vector<const FinalizeReq*>& host) {
   std::vector<const FinalizeReq*> gpu;
+  if (reqs.empty()) return gpu;
+  const int nsl = (int)nslots();
   size_t ntext = 0, in_bytes = 0;
   for (auto& r : reqs) {
-    bool dev = !(r.texts && r.slots.size() > 8);
+    bool dev = true;
     for (int s : r.slots) dev = dev && s >= 0 && s < max_slots_ && s < nsl && !host_mode_[s];
     if (!dev) {
-      finalize_host(r, out);
+      host.push_back(&r);
       continue;
     }
     gpu.push_back(&r);
     ntext += r.slots.size();
     in_bytes += ((r.joiner.size() + 15) & ~(size_t)15) + 256 + 64;
   }
-  if (gpu.empty()) return;
+  if (gpu.empty()) return gpu;
   const int n = (int)gpu.size();
-  grow_mapped(&h_fin_, &fin_cap_, (size_t)n);
-  grow_mapped(&h_finres_, &finres_cap_, (size_t)n);
-  grow_mapped(&h_fint_, &fint_cap_, ntext);
-  grow_mapped(&h_fin_in_, &fin_in_cap_, in_bytes);
-  size_t join_off = 0, out_off = 0, in_off = 0, t_off = 0;
+  grow_mapped(&L.h_fin, &L.fin_cap, (size_t)n);
+  grow_mapped(&L.h_finres, &L.finres_cap, (size_t)n);
+  grow_mapped(&L.h_fint, &L.fint_cap, ntext);
+  grow_mapped(&L.h_tl, &L.tl_cap, ntext);
+  grow_mapped(&L.h_fin_in, &L.fin_in_cap, in_bytes);
+  size_t join_off = 0, out_off = 0, in_off = 0, t_off = 0, seg_off = 0;
   const std::string suf = kFinalSuffix;
-  std::vector<size_t> caps(n);
   for (int i = 0; i < n; ++i) {
     const FinalizeReq& r = *gpu[i];
-    FinItem& it = h_fin_[i];
-    size_t total = 0;
+    FinItem& it = L.h_fin[i];
+    size_t total = 0, longest = 0;
     it.first_text = (uint32_t)t_off;
     it.n_texts = (uint32_t)r.slots.size();
+    it.tl_off = (uint32_t)t_off;
     for (int s : r.slots) {
       const uint32_t len = core_[s].aborted ? 0u : content_len_[s];
-      h_fint_[t_off++] = FinText{(uint32_t)s, len};
+      L.h_fint[t_off++] = FinText{(uint32_t)s, len};
       total += len;
+      longest = std::max(longest, (size_t)len);
     }
     if (r.slots.size() > 1) total += (r.slots.size() - 1) * r.joiner.size();
     const std::string pre = r.texts ? std::string() : final_prefix(r.created);
     it.flags = (r.strip ? 1u : 0u) | (r.texts ? 2u : 0u);
     it.joiner_off = (uint32_t)in_off;
     it.joiner_len = (uint32_t)r.joiner.size();
-    std::memcpy(h_fin_in_ + in_off, r.joiner.data(), r.joiner.size());
+    std::memcpy(L.h_fin_in + in_off, r.joiner.data(), r.joiner.size());
     in_off += (r.joiner.size() + 15) & ~(size_t)15;
     it.pre_off = (uint32_t)in_off;
     it.pre_len = (uint32_t)pre.size();
-    std::memcpy(h_fin_in_ + in_off, pre.data(), pre.size());
+    std::memcpy(L.h_fin_in + in_off, pre.data(), pre.size());
     in_off += (pre.size() + 15) & ~(size_t)15;
     it.suf_off = (uint32_t)in_off;
     it.suf_len = (uint32_t)suf.size();
-    std::memcpy(h_fin_in_ + in_off, suf.data(), suf.size());
+    std::memcpy(L.h_fin_in + in_off, suf.data(), suf.size());
     in_off += (suf.size() + 15) & ~(size_t)15;
     it.join_off = (uint32_t)join_off;
     join_off += (total + 15) & ~(size_t)15;
+    // kept segments of one text: an interval spans >= 7 bytes ("<t></t>"), so <= len/7 + 2
+    it.seg_off = (uint32_t)seg_off;
+    it.seg_cap = r.strip ? (uint32_t)(longest / 4 + 4) : 1u;
+    seg_off += it.seg_cap;
     const size_t cap = r.texts ? total : 6 * total + pre.size() + suf.size();
     it.out_off = (uint32_t)out_off;
     it.out_cap = (uint32_t)cap;
-    caps[i] = cap;
     out_off += (cap + 15) & ~(size_t)15;
   }
-  grow_device(&d_join_, &join_cap_, join_off + 16);
-  grow_device(&d_fout_, &dfout_cap_, out_off + 16);
-  grow_mapped(&h_fout_, &fout_cap_, out_off + 16);
-  {
-    std::lock_guard<std::mutex> lg(L.mu);
-    collect_timing(L);
-  }
-  roctxRangePushA("qmx_finalize");
-  HIP_CHECK(hipEventRecord(L.ev0, L.stream));
-  hipLaunchKernelGGL(qmx_finalize_kernel, dim3(n), dim3(BS), 0, L.stream, h_fin_, h_fint_, h_fin_in_, d_content_,
-                     content_cap_, d_join_, d_fout_, h_fout_, h_finres_, ts_);
-  HIP_CHECK(hipGetLastError());
-  HIP_CHECK(hipEventRecord(L.ev1, L.stream));
-  wait_stream(L);
-  roctxRangePop();
-  float ms = 0.f;
-  hipEventElapsedTime(&ms, L.ev0, L.ev1);
-  fin_ms_ += ms;
-  ++fin_launches_;
-  fin_items_ += n;
-  for (int i = 0; i < n; ++i) {
+  grow_device(&L.d_join, &L.join_cap, join_off + 16);
+  grow_device(&L.d_fout, &L.dfout_cap, out_off + 16);
+  grow_device(&L.d_segs, &L.segs_cap, seg_off * sizeof(int2) + 16);
+  grow_mapped(&L.h_fout, &L.fout_cap, out_off + 16);
+  return gpu;
+}
+
+void HipEngine::collect_finalize(TickLane& L, const std::vector<const FinalizeReq*>& gpu,
+                                 std::vector<FinalizeRes>& out) {
+  for (size_t i = 0; i < gpu.size(); ++i) {
     const FinalizeReq& r = *gpu[i];
-    const FinResult fr = h_finres_[i];
+    const FinResult fr = L.h_finres[i];
     if (fr.status) {
       finalize_host(r, out);
       continue;
     }
     FinalizeRes res;
     res.id = r.id;
-    const char* base = (const char*)h_fout_ + h_fin_[i].out_off;
+    const char* base = (const char*)L.h_fout + L.h_fin[i].out_off;
     if (r.texts) {
       res.kind = 2;
       size_t o = 0;
       for (uint32_t k = 0; k < fr.n_kept; ++k) {
-        res.texts.emplace_back(base + o, fr.text_len[k]);
-        o += fr.text_len[k];
+        const uint32_t tl = L.h_tl[L.h_fin[i].tl_off + k];
+        res.texts.emplace_back(base + o, tl);
+        o += tl;
       }
     } else if (fr.n_kept == 0) {
       res.kind = 0;
@@ -1876,6 +2010,8 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["gpu_wait_us"] += L.gpu_wait_us;
     m["process_us"] += L.process_us;
     m["poll_fallbacks"] += (double)L.poll_fallbacks;
+    m["fin_launches"] += (double)L.fin_launches;  // tick launches that also carried finalize work
+    m["fin_items"] += (double)L.fin_items;
     for (int k = 1; k < 11; ++k) stage[k] += L.stage_us[k];
     cyc += L.clk_cycles;
     cus += L.clk_us;
@@ -1885,10 +2021,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   m["escalations"] = (double)escalations_.load();
   m["fin_host"] = (double)fin_host_.load();
   m["lanes"] = (double)lanes_.size();
-  std::lock_guard<std::mutex> fg(fin_mu_);
-  m["fin_launches"] = (double)fin_launches_;
-  m["fin_items"] = (double)fin_items_;
-  m["fin_ms"] = fin_ms_;
+  m["fin_separate_launches"] = 0.0;  // finalize no longer has a launch (or a wait) of its own
   return m;
 }
 

@@ -190,6 +190,34 @@ def test_hip_finalize_kernel_matches_cpu(ext, seed):
     assert st["fin_items"] >= 1, st  # the GPU path ran (texts-kind with 9+ texts falls back)
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_hip_finalize_long_texts_many_texts_on_gpu(ext, seed):
+    """K3 without host bail-outs: texts of ~100 KB carrying > 4096 tag tokens (unclosed opens,
+    cross-type closes, nesting) and texts-kind requests with more than 8 texts all finalize
+    on the GPU (fin_host stays 0) and match the C++ host algorithms byte for byte."""
+    rng = random.Random(900 + seed)
+    tags = ["think", "reason", "reasoning", "thought"]
+    streams = []
+    for k in range(12):
+        n_events = 130 if k < 2 else rng.randint(1, 3)  # 130 x 200 pieces: ~100 KB of content
+        evs = ["".join(rng.choice(FIN_PIECES) for _ in range(200)) for _ in range(n_events)]
+        if k == 0:
+            assert "".join(evs).count("<") > 4096
+        streams.append([b"".join(H.event_bytes(rng, t) for t in evs[i:i + 8]) for i in range(0, n_events, 8)])
+    m = len(streams)
+    filt = [False] * m
+    for strip in (True, False):
+        c = H.run_engine(NativeEngine("cpu", tags), streams, filt, [True] * m, random.Random(1),
+                         strip_final=strip, joiner="\n--\n")
+        eng = _hip(tags, content_cap=1 << 18, max_slots=64)
+        g = H.run_engine(eng, streams, filt, [True] * m, random.Random(1), strip_final=strip, joiner="\n--\n")
+        assert c[1] == g[1], strip
+        assert c[2] == g[2], strip
+        st = eng._e.kernel_stats()
+        assert st["fin_items"] >= 2 and st["fin_host"] == 0 and st["escalations"] == 0, st
+        assert st["fin_separate_launches"] == 0, st  # finalize rides the tick launch
+
+
 def test_hip_engine_stats(ext):
     eng = _hip(["think"])
     slot = eng.open(0, True, True)
