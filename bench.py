@@ -300,6 +300,66 @@ def breakdown(m0, m1, elapsed):
     }
 
 
+def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports, dist, n_dev):
+    """Outside the timed region, N > 1: expert-parallel placement end to end.  A second proxy
+    set on port + 50 runs the headline backends with ``placement: spread`` and the final
+    event on (skip_final_aggregation: false), so backend 1 of every session runs on the next
+    rank: its deltas cross the TCP mesh, its final text moves HBM → HBM by an RCCL
+    ncclSend/ncclRecv round (rank 0 orders the rounds), and the owner's fused finalize kernel
+    merges it.  Every response is validated; the exchange counters say which path moved
+    the finals.  Failures are reported, never hidden, and do not touch the headline numbers."""
+    from quorum_amd.parallel.exchange import exchange_env
+    from quorum_amd.serve import spawn_workers, wait_healthy
+
+    port = args.port + 50
+    out = {"ok": False}
+    procs = []
+    try:
+        nonce = [str(time.time_ns()) if rank == 0 else None]
+        dist.broadcast_object_list(nonce, src=0)
+        env = dict(os.environ, **exchange_env(rank, world, port, nonce[0]))
+        if n_dev < world or engine != "hip":
+            env["QMX_XCHG"] = "tcp"  # ranks sharing a GPU (rehearsal): RCCL needs one GPU per rank
+        cfg = os.path.join(tmp, "config_spread.yaml")
+        write_config(cfg, mock_ports, False, args.tile, sc, "spread")
+        spec = os.path.join(tmp, "expect_spread.txt")
+        expect_spec(spec, sc, False, mock_expected(bin_dir))
+        procs = spawn_workers(cfg, "127.0.0.1", port, 1, engine, device, impl="native", threads=args.threads,
+                              env=env)
+        if not wait_healthy("127.0.0.1", port, 120):
+            raise RuntimeError("spread proxy did not become healthy")
+        dist.barrier()
+        want_rccl = env.get("QMX_XCHG", "rccl") == "rccl"
+        t0 = time.time()
+        while True:  # the mesh (and, on GPUs, the RCCL communicator) formed on every rank
+            m = scrape(port)
+            if m.get("qmx_exchange_healthy") == 1.0 and (not want_rccl or m.get("qmx_exchange_rccl_active") == 1.0):
+                break
+            if time.time() - t0 > 90:
+                raise RuntimeError(f"exchange did not form: {({k: v for k, v in m.items() if 'exchange' in k})}")
+            time.sleep(0.2)
+        dist.barrier()
+        m0 = scrape(port)
+        st = loadgen(bin_dir, port, 32, 2048, 2, 120, spec)
+        time.sleep(0.2)
+        m1 = scrape(port)
+        d = {k: m1.get(k, 0.0) - m0.get(k, 0.0) for k in m1 if "exchange" in k or "remote_streams" in k}
+        out = {"ok": st["invalid"] == 0 and st["errors"] == 0 and st["completed"] == 2048,
+               "transport": "rccl" if want_rccl else "tcp", "requests": st["completed"], "invalid": st["invalid"],
+               "p50_ttft_ms": st["ttft_p50_ms"], "p50_latency_ms": st["lat_p50_ms"], "req_s": st["rps"],
+               "remote_streams": d.get("qmx_remote_streams_total", 0.0),
+               "rccl_rounds": d.get("qmx_exchange_rounds_total", 0.0),
+               "rccl_final_bytes": d.get("qmx_exchange_bulk_bytes_total", 0.0),
+               "mesh_finals": d.get("qmx_exchange_mesh_finals_total", 0.0),
+               "mesh_messages": d.get("qmx_exchange_messages_total", 0.0),
+               "epochs": m1.get("qmx_exchange_epochs_total", 0.0)}
+    except Exception as e:  # noqa: BLE001 - reported in the JSON line
+        out["error"] = repr(e)[:300]
+    finally:
+        _kill(procs)
+    return out
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -331,6 +391,8 @@ def main() -> int:
     ap.add_argument("--port", type=int, default=int(os.environ.get("QMX_BENCH_PORT", "18000")))
     ap.add_argument("--timeout", type=float, default=300)
     ap.add_argument("--scenario", default="headline", choices=sorted(SCENARIOS))
+    ap.add_argument("--spread-check", type=int, default=1,
+                    help="N > 1: after the timed steps, validate spread placement (RCCL finals) end to end")
     ap.add_argument("--placement", default="local", choices=["local", "spread"],
                     help="spread: a session's backend streams run on consecutive ranks (RCCL exchange)")
     args = ap.parse_args()
@@ -454,6 +516,14 @@ def main() -> int:
         bad = (stats["invalid"] + stats["no_content"] + stats["errors"] + stats["non200"]
                + warm.get("invalid", 0) + warm.get("errors", 0) + warm.get("non200", 0) + len(dead)
                + (args.steps * args.batch - stats["completed"]))
+        spread = None
+        if (dist is not None and world > 1 and args.spread_check and args.impl == "native"
+                and args.placement == "local"):
+            spread = spread_check(args, SCENARIOS["headline"], rank, world, engine, device, bin_dir, tmp,
+                                  mock_ports, dist, n_dev)
+            spread_rows = [None] * world
+            dist.all_gather_object(spread_rows, spread)
+            spread = spread_rows
         local = [elapsed, float(stats["completed"]), float(stats["ttft_p50_ms"]), float(stats["ttft_p99_ms"]),
                  float(stats["errors"] + stats["non200"]), float(stats["ttfb_p50_ms"]), float(stats["lat_p50_ms"]),
                  float(len(dead)), float(stats["invalid"]), float(stats["no_content"]), float(stats["validated"]),
@@ -518,6 +588,8 @@ def main() -> int:
             }
             if dead or dead_warm:
                 res["exited"] = dead or dead_warm
+            if spread is not None:  # outside the timed region; per rank
+                res["spread_check"] = {"ok": all(r.get("ok") for r in spread), "per_rank": spread}
             print(json.dumps(res), flush=True)
     finally:
         _kill(procs)

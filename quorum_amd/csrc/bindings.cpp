@@ -7,6 +7,10 @@
 #include "qmx_hip.h"
 #include "qmx_json.h"
 #include <chrono>
+#include <condition_variable>
+#include <map>
+#include <mutex>
+#include <thread>
 
 #include "qmx_exchange.h"
 #include "qmx_server.h"
@@ -174,59 +178,141 @@ PYBIND11_MODULE(_qmx, m) {
   });
   m.def("server_counters", &server_counters);
   m.def("rccl_unique_id", &rccl_unique_id_hex);
-  // Transport self-test: `rounds` all-gathers of random payloads (some larger than the fixed
-  // slot, exercising the padded second phase); every rank must receive every rank's bytes.
+  // Exchange self-test: every rank sends every other rank `rounds` delta messages over the
+  // mesh and `rounds` final texts through the bulk plane (RCCL p2p rounds from HBM into HBM
+  // sinks with transport=rccl, the mesh with tcp); receivers verify every byte.
   m.def("exchange_selftest", [](const py::dict& d, int rounds) {
     XOptions o;
     auto gs = [&](const char* k, std::string& v) { if (d.contains(k)) v = py::cast<std::string>(d[k]); };
     auto gi = [&](const char* k, int& v) { if (d.contains(k)) v = py::cast<int>(d[k]); };
     gi("rank", o.rank); gi("world", o.world); gs("transport", o.transport); gs("addr", o.addr);
-    gi("port", o.port); gs("id_file", o.id_file); gi("device", o.device);
+    gi("port", o.port); gi("device", o.device);
+    if (d.contains("timeout")) o.timeout_s = py::cast<double>(d["timeout"]);
+    const bool dev = o.transport == "rccl";
+    auto payload = [](int r, int src, int dst, int kind) {
+      uint64_t x = 1234567 ^ ((uint64_t)r * 1000003ull) ^ ((uint64_t)src * 7919ull) ^ ((uint64_t)dst * 104729ull) ^
+                   ((uint64_t)kind << 40);
+      size_t n = kind ? 1 + (x % 20000) : 1 + (x % 3000);
+      std::string s(n, '\0');
+      for (size_t i = 0; i < n; ++i) {
+        x = x * 6364136223846793005ull + 1442695040888963407ull;
+        s[i] = (char)(x >> 56);
+      }
+      return s;
+    };
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<XMsg> got;
     bool ok = true;
-    int bad = 0, fail_round = -1;
-    double t_small = 0, t_big = 0;
-    int n_small = 0, n_big = 0;
+    int bad = 0, n_data = 0, n_bulk = 0, n_sent = 0;
+    double data_us = 0, wall = 0;
+    uint64_t rounds_done = 0, mesh_finals = 0, epochs = 0;
     {
       py::gil_scoped_release nogil;
-      auto tr = o.transport == "rccl" ? make_rccl_transport(o) : make_tcp_transport(o);
-      std::vector<std::string> all;
-      std::vector<uint32_t> fl;
-      const uint64_t seed = 1234567;
-      for (int r = 0; r < rounds && ok; ++r) {
-        // every rank derives every rank's payload from (round, rank): receivers can verify
-        auto payload = [&](int rk) {
-          uint64_t x = seed ^ ((uint64_t)r * 1000003ull) ^ ((uint64_t)rk * 7919ull);
-          size_t n = (r % 5 == 4) ? 20000 + (x % 5000) : (x % 3000);
-          std::string s(n, '\0');
-          for (size_t i = 0; i < n; ++i) {
-            x = x * 6364136223846793005ull + 1442695040888963407ull;
-            s[i] = (char)(x >> 56);
-          }
-          return s;
-        };
-        std::string mine = payload(o.rank);
-        auto t0 = std::chrono::steady_clock::now();
-        if (!tr->allgather(mine, (uint32_t)r, all, fl)) {
+      std::vector<void*> bufs;
+      auto dalloc = [&](size_t n) -> void* {
+        void* p = nullptr;
+        if (hipSetDevice(o.device) != hipSuccess || hipMalloc(&p, std::max<size_t>(n, 16)) != hipSuccess) return nullptr;
+        bufs.push_back(p);
+        return p;
+      };
+      Exchange x(o, 1, [&](int, std::vector<XMsg>&& v) {
+        std::lock_guard<std::mutex> g(mu);
+        for (auto& m : v) got.push_back(std::move(m));
+        cv.notify_all();
+      });
+      // sinks first: a bulk that finds no sink is dropped
+      std::map<std::pair<int, int>, void*> sinks;
+      for (int r = 0; r < rounds; ++r)
+        for (int src = 0; src < o.world; ++src) {
+          if (src == o.rank) continue;
+          const size_t n = payload(r, src, o.rank, 1).size();
+          void* p = dev ? dalloc(n) : nullptr;
+          sinks[{r, src}] = p;
+          x.expect_bulk((uint64_t)(r + 1), src, p, n);
+        }
+      const auto t0 = std::chrono::steady_clock::now();
+      auto secs = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
+      while (!x.healthy() || (dev && !x.rccl_active())) {
+        if (secs() > o.timeout_s) {
           ok = false;
-          fail_round = r;
           break;
         }
-        double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-        if (r % 5 == 4) {
-          t_big += us;
-          ++n_big;
-        } else {
-          t_small += us;
-          ++n_small;
-        }
-        for (int rk = 0; rk < o.world; ++rk)
-          if (all[rk] != payload(rk) || fl[rk] != (uint32_t)r) ++bad;
+        std::this_thread::sleep_for(std::chrono::milliseconds(5));
       }
+      const auto t1 = std::chrono::steady_clock::now();
+      for (int r = 0; r < rounds && ok; ++r)
+        for (int p = 0; p < o.world; ++p) {
+          if (p == o.rank) continue;
+          XMsg m;
+          m.type = X_DATA;
+          m.dst_rank = p;
+          m.src_rank = o.rank;
+          m.skey = (uint64_t)(r + 1);
+          m.bi = o.rank;
+          m.payload = payload(r, o.rank, p, 0);
+          x.post(std::move(m));
+          std::string b = payload(r, o.rank, p, 1);
+          void* src = nullptr;
+          if (dev) {
+            src = dalloc(b.size());
+            if (!src || hipMemcpy(src, b.data(), b.size(), hipMemcpyHostToDevice) != hipSuccess) ok = false;
+          }
+          XMsg h;
+          h.dst_rank = p;
+          h.src_rank = o.rank;
+          h.skey = (uint64_t)(r + 1);
+          h.bi = o.rank;
+          h.flags = XF_TEXT;
+          x.send_bulk(std::move(h), src, b.size(), [b] { return b; });
+        }
+      const int want = rounds * (o.world - 1);
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        while (ok) {
+          for (auto& m : got) {
+            if (m.type == X_DATA) {
+              ++n_data;
+              if (m.payload != payload((int)m.skey - 1, m.bi, o.rank, 0)) ++bad;
+              if (n_data == want) data_us = 1e6 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+            } else if (m.type == X_BULK) {
+              ++n_bulk;
+              const std::string exp = payload((int)m.skey - 1, m.bi, o.rank, 1);
+              std::string have = m.payload;
+              if (have.empty() && m.a > 0) {  // RCCL: in the HBM sink
+                have.assign((size_t)m.a, '\0');
+                void* sp = sinks[{(int)m.skey - 1, m.bi}];
+                if (!sp || hipMemcpy(&have[0], sp, have.size(), hipMemcpyDeviceToHost) != hipSuccess) have.clear();
+              }
+              if (have != exp) ++bad;
+            } else if (m.type == X_SENT) {
+              ++n_sent;
+            }
+          }
+          got.clear();
+          if (n_data >= want && n_bulk >= want && n_sent >= want) break;
+          if (secs() > o.timeout_s) {
+            ok = false;
+            break;
+          }
+          cv.wait_for(lk, std::chrono::milliseconds(20));
+        }
+      }
+      wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+      rounds_done = x.rounds();
+      mesh_finals = x.mesh_bulk();
+      epochs = x.epochs();
+      // linger so peers still waiting for our bytes get them, then stop
+      std::this_thread::sleep_for(std::chrono::milliseconds(300));
+      x.request_stop();
+      x.join();
+      for (void* p : bufs) hipFree(p);
     }
     return py::dict(py::arg("ok") = ok && bad == 0, py::arg("bad") = bad, py::arg("rounds") = rounds,
-                    py::arg("fail_round") = fail_round,
-                    py::arg("small_round_us") = n_small ? t_small / n_small : 0.0,
-                    py::arg("large_round_us") = n_big ? t_big / n_big : 0.0);
+                    py::arg("data") = n_data, py::arg("bulk") = n_bulk, py::arg("sent") = n_sent,
+                    py::arg("data_wall_us") = data_us, py::arg("wall_s") = wall,
+                    py::arg("rccl_rounds") = rounds_done, py::arg("mesh_finals") = mesh_finals,
+                    py::arg("epochs") = epochs);
   });
   m.def("stop_server", &stop_server);
   m.def("json_roundtrip", [](const py::bytes& b) -> py::object {

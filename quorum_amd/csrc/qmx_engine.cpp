@@ -458,6 +458,16 @@ std::string HostEngine::text(int slot) {
   return c.aborted ? std::string() : c.content;
 }
 
+size_t HostEngine::content_size(int slot) {
+  if (slot < 0 || slot >= (int)nslots()) return 0;
+  return core_[slot].content.size();
+}
+
+void HostEngine::set_remote_content(int slot, const std::string* bytes, size_t len) {
+  if (slot < 0 || slot >= (int)nslots()) return;
+  core_[slot].content = bytes ? *bytes : std::string(len, '\0');
+}
+
 std::unordered_map<std::string, double> HostEngine::stats() {
   std::lock_guard<std::mutex> g(mu_);
   return {{"ticks", (double)ticks_}, {"bytes_in", (double)bytes_in_}, {"bytes_out", (double)bytes_out_},

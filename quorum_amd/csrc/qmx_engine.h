@@ -147,6 +147,16 @@ class HostEngine {
   void settle(const std::vector<int>& taken);
   virtual std::string text(int slot);
   virtual std::unordered_map<std::string, double> stats();
+  // Spread placement (qmx_exchange.h): a stream whose final text another rank produced.
+  // content_device_ptr: the slot's HBM content area (nullptr: host engine / host path);
+  // content_size: filtered content bytes so far; set_remote_content: the slot's content
+  // becomes `len` bytes — *bytes if given, else already written into the HBM area.
+  virtual void* content_device_ptr(int /*slot*/, size_t* cap) {
+    *cap = 0;
+    return nullptr;
+  }
+  virtual size_t content_size(int slot);
+  virtual void set_remote_content(int slot, const std::string* bytes, size_t len);
 
   const TagSet& tagset() const { return ts_; }
 

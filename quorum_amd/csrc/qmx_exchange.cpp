@@ -1,21 +1,25 @@
-// qmx_exchange.cpp — lock-step all-gather rounds over RCCL (xGMI) or a TCP hub.
+// qmx_exchange.cpp — TCP mesh (control + deltas) and RCCL point-to-point rounds (final
+// texts, HBM to HBM) for spread placement; see qmx_exchange.h.
 #include "qmx_exchange.h"
 
 #include <arpa/inet.h>
+#include <errno.h>
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <rccl/rccl.h>
-#include <sys/socket.h>
 #include <sched.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
-#include <fstream>
-#include <sstream>
+#include <deque>
 #include <stdexcept>
 
 namespace qmx {
@@ -34,187 +38,39 @@ struct WireHdr {
   int32_t a, b;
   uint32_t len;
 };
+// one bulk transfer of a round manifest
+struct WireEntry {
+  int32_t src, dst;
+  uint64_t skey;
+  int32_t bi, b;
+  uint32_t len;
+  uint16_t src_loop, dst_loop;
+  uint8_t flags, pad[3];
+};
 #pragma pack(pop)
 
-void serialize(const std::vector<XMsg>& ms, std::string& out) {
-  for (const XMsg& m : ms) {
-    WireHdr h{m.type, m.flags, m.dst_loop, m.src_loop, 0, m.dst_rank, m.src_rank, m.bi, m.skey, m.a, m.b,
-              (uint32_t)m.payload.size()};
-    out.append((const char*)&h, sizeof(h));
-    out += m.payload;
-  }
-}
-
-bool parse_for(const std::string& buf, int rank, std::vector<XMsg>& out) {
-  size_t p = 0;
-  while (p + sizeof(WireHdr) <= buf.size()) {
-    WireHdr h;
-    std::memcpy(&h, buf.data() + p, sizeof(h));
-    p += sizeof(h);
-    if (p + h.len > buf.size()) return false;
-    if (h.dst_rank == rank) {
-      XMsg m;
-      m.type = h.type;
-      m.flags = h.flags;
-      m.dst_loop = h.dst_loop;
-      m.src_loop = h.src_loop;
-      m.dst_rank = h.dst_rank;
-      m.src_rank = h.src_rank;
-      m.bi = h.bi;
-      m.skey = h.skey;
-      m.a = h.a;
-      m.b = h.b;
-      m.payload.assign(buf.data() + p, h.len);
-      out.push_back(std::move(m));
-    }
-    p += h.len;
-  }
-  return p == buf.size();
-}
-
-// ------------------------------------------------------------------------------ TCP hub
-bool send_all(int fd, const void* p, size_t n) {
-  const char* c = (const char*)p;
-  while (n) {
-    ssize_t w = send(fd, c, n, MSG_NOSIGNAL);
-    if (w <= 0) {
-      if (w < 0 && errno == EINTR) continue;
-      return false;
-    }
-    c += w;
-    n -= (size_t)w;
-  }
-  return true;
-}
-bool recv_all(int fd, void* p, size_t n) {
-  char* c = (char*)p;
-  while (n) {
-    ssize_t r = recv(fd, c, n, 0);
-    if (r <= 0) {
-      if (r < 0 && errno == EINTR) continue;
-      return false;
-    }
-    c += r;
-    n -= (size_t)r;
-  }
-  return true;
-}
-void set_timeouts(int fd, double s) {
-  timeval tv{};
-  tv.tv_sec = (time_t)s;
-  tv.tv_usec = (suseconds_t)((s - (double)tv.tv_sec) * 1e6);
-  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
-  setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
-  int one = 1;
-  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
-}
-
-class TcpX : public XTransport {
- public:
-  explicit TcpX(const XOptions& o) : o_(o), fds_(o.world, -1) {
-    sockaddr_in a{};
-    a.sin_family = AF_INET;
-    a.sin_port = htons((uint16_t)o.port);
-    inet_pton(AF_INET, o.addr.c_str(), &a.sin_addr);
-    const double t_end = now_s() + o.timeout_s;
-    if (o.rank == 0) {
-      int l = socket(AF_INET, SOCK_STREAM, 0);
-      int one = 1;
-      setsockopt(l, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
-      if (bind(l, (sockaddr*)&a, sizeof(a)) != 0 || listen(l, 64) != 0) {
-        close(l);
-        throw std::runtime_error("exchange: hub bind failed: " + std::string(strerror(errno)));
-      }
-      set_timeouts(l, o.timeout_s);
-      for (int got = 1; got < o.world;) {
-        int fd = accept(l, nullptr, nullptr);
-        if (fd < 0) {
-          if (errno == EINTR) continue;
-          close(l);
-          throw std::runtime_error("exchange: peers did not connect");
-        }
-        set_timeouts(fd, o.timeout_s);
-        int32_t r = -1;
-        if (!recv_all(fd, &r, 4) || r <= 0 || r >= o.world || fds_[r] >= 0) {
-          close(fd);
-          continue;
-        }
-        fds_[r] = fd;
-        ++got;
-      }
-      close(l);
-    } else {
-      int fd = -1;
-      while (true) {
-        fd = socket(AF_INET, SOCK_STREAM, 0);
-        if (connect(fd, (sockaddr*)&a, sizeof(a)) == 0) break;
-        close(fd);
-        fd = -1;
-        if (now_s() > t_end) throw std::runtime_error("exchange: cannot reach hub");
-        usleep(20000);
-      }
-      set_timeouts(fd, o.timeout_s);
-      int32_t r = o.rank;
-      if (!send_all(fd, &r, 4)) throw std::runtime_error("exchange: hub handshake failed");
-      fds_[0] = fd;
-    }
-  }
-  ~TcpX() override {
-    for (int fd : fds_)
-      if (fd >= 0) close(fd);
-  }
-  bool allgather(const std::string& mine, uint32_t flags, std::vector<std::string>& all,
-                 std::vector<uint32_t>& all_flags) override {
-    const int W = o_.world;
-    all.assign(W, std::string());
-    all_flags.assign(W, 0);
-    if (o_.rank != 0) {
-      uint32_t h[2] = {(uint32_t)mine.size(), flags};
-      if (!send_all(fds_[0], h, 8) || !send_all(fds_[0], mine.data(), mine.size())) return false;
-      std::vector<uint32_t> hs(2 * W);
-      if (!recv_all(fds_[0], hs.data(), 8 * W)) return false;
-      for (int r = 0; r < W; ++r) {
-        all[r].resize(hs[2 * r]);
-        all_flags[r] = hs[2 * r + 1];
-        if (hs[2 * r] && !recv_all(fds_[0], &all[r][0], hs[2 * r])) return false;
-      }
-      return true;
-    }
-    all[0] = mine;
-    all_flags[0] = flags;
-    for (int r = 1; r < W; ++r) {
-      uint32_t h[2];
-      if (!recv_all(fds_[r], h, 8)) return false;
-      all[r].resize(h[0]);
-      all_flags[r] = h[1];
-      if (h[0] && !recv_all(fds_[r], &all[r][0], h[0])) return false;
-    }
-    std::string blob;
-    for (int r = 0; r < W; ++r) {
-      uint32_t h[2] = {(uint32_t)all[r].size(), all_flags[r]};
-      blob.append((const char*)h, 8);
-    }
-    for (int r = 0; r < W; ++r) blob += all[r];
-    for (int r = 1; r < W; ++r)
-      if (!send_all(fds_[r], blob.data(), blob.size())) return false;
-    return true;
-  }
-
- private:
-  XOptions o_;
-  std::vector<int> fds_;
+// mesh-internal frame types (never delivered to the io loops)
+enum : uint8_t {
+  F_HELLO = 100,     // a = sender rank (first frame of a connection)
+  F_ANNOUNCE = 101,  // worker → rank 0: payload = one WireEntry (a bulk waiting for a round)
+  F_MANIFEST = 102,  // rank 0 → involved rank: a = round, b = epoch, flags 1 = fall back to the mesh
+  F_EPOCH = 103,     // rank 0 → all: a = epoch (0: RCCL down everywhere), payload = unique id hex
+  F_BULK_MESH = 104, // worker → owner: the final text's bytes over the mesh
+  F_RCCL_DOWN = 105, // any rank → rank 0: my communicator failed (a = epoch)
 };
 
-// ------------------------------------------------------------------------------ RCCL
-#define XHIP(x)                                                                            \
-  do {                                                                                     \
-    hipError_t e_ = (x);                                                                   \
-    if (e_ != hipSuccess) throw std::runtime_error(std::string("exchange HIP: ") + hipGetErrorString(e_)); \
-  } while (0)
-#define XNCCL(x)                                                                           \
-  do {                                                                                     \
-    ncclResult_t r_ = (x);                                                                 \
-    if (r_ != ncclSuccess) throw std::runtime_error(std::string("exchange RCCL: ") + ncclGetErrorString(r_)); \
+std::string frame(const XMsg& m) {
+  WireHdr h{m.type, m.flags, m.dst_loop, m.src_loop, 0, m.dst_rank, m.src_rank, m.bi, m.skey, m.a, m.b,
+            (uint32_t)m.payload.size()};
+  std::string s((const char*)&h, sizeof(h));
+  s += m.payload;
+  return s;
+}
+
+#define XHIP(x)                                                                                                  \
+  do {                                                                                                           \
+    hipError_t e_ = (x);                                                                                         \
+    if (e_ != hipSuccess) throw std::runtime_error(std::string("exchange HIP: ") + hipGetErrorString(e_));       \
   } while (0)
 
 std::string to_hex(const ncclUniqueId& id) {
@@ -234,231 +90,865 @@ bool from_hex(const std::string& s, ncclUniqueId* id) {
   return true;
 }
 
-class RcclX : public XTransport {
- public:
-  static constexpr size_t kSlot = 8192;  // fixed per-rank slot of the first all-gather
-
-  explicit RcclX(const XOptions& o) : o_(o) {
-    XHIP(hipSetDevice(o.device));
-    ncclUniqueId id;
-    if (o.rank == 0) {
-      XNCCL(ncclGetUniqueId(&id));
-      std::string tmp = o.id_file + ".tmp";
-      {
-        std::ofstream f(tmp);
-        f << to_hex(id);
-      }
-      if (rename(tmp.c_str(), o.id_file.c_str()) != 0) throw std::runtime_error("exchange: cannot publish RCCL id");
-    } else {
-      const double t_end = now_s() + o.timeout_s;
-      while (true) {
-        std::ifstream f(o.id_file);
-        std::string s;
-        if (f && (f >> s) && from_hex(s, &id)) break;
-        if (now_s() > t_end) throw std::runtime_error("exchange: RCCL id not published");
-        usleep(20000);
-      }
-    }
-    XHIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
-    XNCCL(ncclCommInitRank(&comm_, o.world, id, o.rank));
-    XHIP(hipMalloc(&d_s1_, kSlot));
-    XHIP(hipMalloc(&d_r1_, kSlot * o.world));
-    XHIP(hipHostMalloc((void**)&h_s1_, kSlot));
-    XHIP(hipHostMalloc((void**)&h_r1_, kSlot * o.world));
-  }
-  ~RcclX() override {
-    if (comm_) {
-      if (aborted_) ncclCommAbort(comm_);
-      else ncclCommDestroy(comm_);
-    }
-    if (st_) hipStreamDestroy(st_);
-    hipFree(d_s1_);
-    hipFree(d_r1_);
-    hipFree(d_s2_);
-    hipFree(d_r2_);
-    hipHostFree(h_s1_);
-    hipHostFree(h_r1_);
-    hipHostFree(h_s2_);
-    hipHostFree(h_r2_);
-  }
-  bool wait() {
-    const double t_end = now_s() + o_.timeout_s;
-    while (true) {
-      hipError_t e = hipStreamQuery(st_);
-      if (e == hipSuccess) return true;
-      if (e != hipErrorNotReady || now_s() > t_end) {
-        ncclCommAbort(comm_);  // a peer died or stalled: fail fast, survivors go local
-        comm_ = nullptr;
-        aborted_ = true;
-        return false;
-      }
-      // yield while the round is young (collectives take tens of us), then back off
-      if (now_s() - (t_end - o_.timeout_s) < 5e-4) sched_yield();
-      else usleep(50);
-    }
-  }
-  bool allgather(const std::string& mine, uint32_t flags, std::vector<std::string>& all,
-                 std::vector<uint32_t>& all_flags) override {
-    if (!comm_) return false;
-    const int W = o_.world;
-    const size_t cap = kSlot - 8;
-    uint32_t h[2] = {(uint32_t)mine.size(), flags};
-    std::memcpy(h_s1_, h, 8);
-    const size_t n1 = std::min(mine.size(), cap);
-    if (mine.size() <= cap) std::memcpy(h_s1_ + 8, mine.data(), n1);
-    try {
-      XHIP(hipMemcpyAsync(d_s1_, h_s1_, 8 + (mine.size() <= cap ? n1 : 0), hipMemcpyHostToDevice, st_));
-      XNCCL(ncclAllGather(d_s1_, d_r1_, kSlot, ncclUint8, comm_, st_));
-      XHIP(hipMemcpyAsync(h_r1_, d_r1_, kSlot * W, hipMemcpyDeviceToHost, st_));
-    } catch (const std::exception& e) {
-      fprintf(stderr, "%s\n", e.what());
-      return false;
-    }
-    if (!wait()) return false;
-    all.assign(W, std::string());
-    all_flags.assign(W, 0);
-    size_t M = 0;
-    for (int r = 0; r < W; ++r) {
-      uint32_t hr[2];
-      std::memcpy(hr, h_r1_ + r * kSlot, 8);
-      all_flags[r] = hr[1];
-      if (hr[0] <= cap) all[r].assign((const char*)h_r1_ + r * kSlot + 8, hr[0]);
-      else M = std::max(M, (size_t)hr[0]);
-    }
-    if (M == 0) return true;
-    // phase 2: padded all-gather of the large buffers (every rank knows M from phase 1)
-    try {
-      if (M > cap2_) {
-        hipFree(d_s2_);
-        hipFree(d_r2_);
-        hipHostFree(h_s2_);
-        hipHostFree(h_r2_);
-        cap2_ = std::max(M, cap2_ * 2);
-        XHIP(hipMalloc(&d_s2_, cap2_));
-        XHIP(hipMalloc(&d_r2_, cap2_ * W));
-        XHIP(hipHostMalloc((void**)&h_s2_, cap2_));
-        XHIP(hipHostMalloc((void**)&h_r2_, cap2_ * W));
-      }
-      if (mine.size() > cap) {
-        std::memcpy(h_s2_, mine.data(), mine.size());
-        XHIP(hipMemcpyAsync(d_s2_, h_s2_, mine.size(), hipMemcpyHostToDevice, st_));
-      }
-      XNCCL(ncclAllGather(d_s2_, d_r2_, M, ncclUint8, comm_, st_));
-      XHIP(hipMemcpyAsync(h_r2_, d_r2_, M * W, hipMemcpyDeviceToHost, st_));
-    } catch (const std::exception& e) {
-      fprintf(stderr, "%s\n", e.what());
-      return false;
-    }
-    if (!wait()) return false;
-    for (int r = 0; r < W; ++r) {
-      uint32_t hr[2];
-      std::memcpy(hr, h_r1_ + r * kSlot, 8);
-      if (hr[0] > cap) all[r].assign((const char*)h_r2_ + r * M, hr[0]);
-    }
-    return true;
-  }
-
- private:
-  XOptions o_;
-  ncclComm_t comm_ = nullptr;
-  hipStream_t st_ = nullptr;
-  bool aborted_ = false;
-  uint8_t *d_s1_ = nullptr, *d_r1_ = nullptr, *h_s1_ = nullptr, *h_r1_ = nullptr;
-  uint8_t *d_s2_ = nullptr, *d_r2_ = nullptr, *h_s2_ = nullptr, *h_r2_ = nullptr;
-  size_t cap2_ = 0;
-};
-
 }  // namespace
 
-std::unique_ptr<XTransport> make_tcp_transport(const XOptions& o) { return std::unique_ptr<XTransport>(new TcpX(o)); }
-std::unique_ptr<XTransport> make_rccl_transport(const XOptions& o) {
-  return std::unique_ptr<XTransport>(new RcclX(o));
-}
 std::string rccl_unique_id_hex() {
   ncclUniqueId id;
-  XNCCL(ncclGetUniqueId(&id));
+  if (ncclGetUniqueId(&id) != ncclSuccess) throw std::runtime_error("ncclGetUniqueId failed");
   return to_hex(id);
 }
 
-// ------------------------------------------------------------------------------ Exchange
+// ----------------------------------------------------------------------------------------
+struct Exchange::Impl {
+  struct Peer {
+    int fd = -1;
+    bool up = false, hello = false, dialing = false, want_out = false;
+    double next_dial = 0;
+    std::string in, out;
+    size_t out_off = 0;
+    PeerStats st;
+  };
+  struct Send {  // worker side: a final text waiting for its round
+    XMsg hdr;
+    const void* dev = nullptr;
+    size_t len = 0;
+    std::function<std::string()> host;
+  };
+  struct Sink {
+    void* dev = nullptr;
+    size_t cap = 0;
+  };
+  struct Manifest {
+    int round = 0, epoch = 0;
+    bool fallback = false;
+    std::vector<WireEntry> es;
+  };
+  using Key = std::pair<uint64_t, int>;
+
+  Exchange* X;
+  int ep = -1, lfd = -1, evfd = -1;
+  std::vector<Peer> peers;
+  std::mutex omu;                       // outgoing frames posted by other threads
+  std::vector<std::string> posted;      // per peer
+  std::vector<std::pair<int, std::string>> local_frames;  // frames addressed to this rank itself
+  std::atomic<uint64_t> up_mask_bits{0};
+
+  // bulk state
+  std::mutex bmu;
+  std::condition_variable bcv;
+  std::map<Key, Send> sends;
+  std::map<Key, Sink> sinks;
+  std::deque<Manifest> manifests;
+  int pending_epoch = 0;  // bulk thread: (re)form the communicator for this epoch
+  std::string pending_id;
+  bool drop_comm = false;
+  // coordinator (rank 0, mesh thread only)
+  std::vector<WireEntry> ann;
+  double ann_deadline = 0;
+  int round_no = 0, epoch_no = 0;
+  bool epoch_live = false;  // an epoch is formed (or forming) and not reported down
+  bool ever_all_up = false;
+  double next_epoch_at = 0;  // retry backoff after an epoch / communicator failure
+  int epoch_failures = 0;
+
+  explicit Impl(Exchange* x) : X(x) {}
+
+  // ------------------------------------------------------------------ mesh plumbing
+  void wake() {
+    uint64_t one = 1;
+    ssize_t w = write(evfd, &one, 8);
+    (void)w;
+  }
+  void enqueue(int peer, std::string&& f) {  // any thread
+    {
+      std::lock_guard<std::mutex> g(omu);
+      if (peer == X->o_.rank) local_frames.emplace_back(peer, std::move(f));
+      else posted[peer] += f;
+    }
+    wake();
+  }
+  void arm(Peer& p, int r, bool out) {
+    epoll_event e{};
+    e.events = EPOLLIN | (out ? EPOLLOUT : 0);
+    e.data.u64 = (uint64_t)(r + 1);
+    epoll_ctl(ep, EPOLL_CTL_MOD, p.fd, &e);
+  }
+  void set_nodelay(int fd) {
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  }
+  void mark_down(int r) {
+    Peer& p = peers[r];
+    if (p.fd >= 0) {
+      epoll_ctl(ep, EPOLL_CTL_DEL, p.fd, nullptr);
+      close(p.fd);
+    }
+    const bool was_up = p.up;
+    p.fd = -1;
+    p.up = p.hello = p.dialing = p.want_out = false;
+    p.in.clear();
+    p.out.clear();
+    p.out_off = 0;
+    p.next_dial = now_s() + 0.1;
+    if (was_up) {
+      up_mask_bits.fetch_and(~(1ull << r));
+      for (int l = 0; l < X->nloops_; ++l) {
+        std::vector<XMsg> v(1);
+        v[0].type = X_DOWN;
+        v[0].a = r;
+        X->deliver_(l, std::move(v));
+      }
+      bcv.notify_all();  // a bulk round waiting on this peer gives up at once
+      if (X->o_.rank == 0 && X->o_.transport == "rccl") rccl_down_everywhere();
+    }
+  }
+  void mark_up(int r) {
+    Peer& p = peers[r];
+    p.up = true;
+    p.st.connects++;
+    if (p.st.connects > 1) X->rejoins_++;
+    up_mask_bits.fetch_or(1ull << r);
+    // flush what was posted for this peer while it was down: nothing (frames posted to a
+    // down peer are dropped: their sessions were failed by X_DOWN)
+    {
+      std::lock_guard<std::mutex> g(omu);
+      posted[r].clear();
+    }
+    for (int l = 0; l < X->nloops_; ++l) {
+      std::vector<XMsg> v(1);
+      v[0].type = X_UP;
+      v[0].a = r;
+      X->deliver_(l, std::move(v));
+    }
+  }
+  bool all_up() const {
+    for (int r = 0; r < X->o_.world; ++r)
+      if (r != X->o_.rank && !peers[r].up) return false;
+    return true;
+  }
+  void dial(int r) {
+    Peer& p = peers[r];
+    int fd = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK, 0);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons((uint16_t)(X->o_.port + r));
+    inet_pton(AF_INET, X->o_.addr.c_str(), &a.sin_addr);
+    int rc = connect(fd, (sockaddr*)&a, sizeof(a));
+    if (rc != 0 && errno != EINPROGRESS) {
+      close(fd);
+      p.next_dial = now_s() + 0.1;
+      return;
+    }
+    set_nodelay(fd);
+    p.fd = fd;
+    p.dialing = true;
+    epoll_event e{};
+    e.events = EPOLLIN | EPOLLOUT;
+    e.data.u64 = (uint64_t)(r + 1);
+    epoll_ctl(ep, EPOLL_CTL_ADD, fd, &e);
+    XMsg h;
+    h.type = F_HELLO;
+    h.a = X->o_.rank;
+    p.out = frame(h);
+    p.out_off = 0;
+    p.want_out = true;
+  }
+  void flush(int r) {
+    Peer& p = peers[r];
+    while (p.fd >= 0 && p.out_off < p.out.size()) {
+      ssize_t w = send(p.fd, p.out.data() + p.out_off, p.out.size() - p.out_off, MSG_NOSIGNAL);
+      if (w > 0) {
+        p.out_off += (size_t)w;
+        continue;
+      }
+      if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+        if (!p.want_out) {
+          p.want_out = true;
+          arm(p, r, true);
+        }
+        return;
+      }
+      return mark_down(r);
+    }
+    if (p.fd >= 0) {
+      p.out.clear();
+      p.out_off = 0;
+      if (p.want_out) {
+        p.want_out = false;
+        arm(p, r, false);
+      }
+    }
+  }
+  void take_posted() {
+    std::vector<std::pair<int, std::string>> loc;
+    {
+      std::lock_guard<std::mutex> g(omu);
+      for (int r = 0; r < X->o_.world; ++r) {
+        if (posted[r].empty()) continue;
+        Peer& p = peers[r];
+        if (p.up) {
+          if (p.out_off == p.out.size()) {
+            p.out.clear();
+            p.out_off = 0;
+          }
+          p.out += posted[r];
+        }
+        posted[r].clear();
+      }
+      loc.swap(local_frames);
+    }
+    for (auto& f : loc) on_frames(X->o_.rank, f.second);
+    for (int r = 0; r < X->o_.world; ++r)
+      if (peers[r].up && peers[r].out_off < peers[r].out.size() && !peers[r].want_out) flush(r);
+  }
+  // parse every complete frame in `buf` (from peer r)
+  void on_frames(int r, std::string& buf) {
+    size_t p = 0;
+    std::vector<std::vector<XMsg>> per(X->nloops_);
+    while (buf.size() - p >= sizeof(WireHdr)) {
+      WireHdr h;
+      std::memcpy(&h, buf.data() + p, sizeof(h));
+      if (buf.size() - p - sizeof(h) < h.len) break;
+      XMsg m;
+      m.type = h.type;
+      m.flags = h.flags;
+      m.dst_loop = h.dst_loop;
+      m.src_loop = h.src_loop;
+      m.dst_rank = h.dst_rank;
+      m.src_rank = h.src_rank;
+      m.bi = h.bi;
+      m.skey = h.skey;
+      m.a = h.a;
+      m.b = h.b;
+      m.payload.assign(buf.data() + p + sizeof(h), h.len);
+      p += sizeof(h) + h.len;
+      if (r != X->o_.rank) {
+        peers[r].st.msgs_in++;
+        peers[r].st.bytes_in += m.payload.size();
+      }
+      X->msgs_++;
+      X->bytes_ += m.payload.size();
+      if (m.type < F_HELLO) {
+        per[m.dst_loop % X->nloops_].push_back(std::move(m));
+        continue;
+      }
+      on_internal(r, std::move(m), per);
+    }
+    buf.erase(0, p);
+    for (int l = 0; l < X->nloops_; ++l)
+      if (!per[l].empty()) X->deliver_(l, std::move(per[l]));
+  }
+  void on_internal(int r, XMsg&& m, std::vector<std::vector<XMsg>>& per) {
+    switch (m.type) {
+      case F_BULK_MESH: {  // the final text's bytes: deliver as X_BULK with the payload
+        X->mesh_bulk_++;
+        m.type = X_BULK;
+        m.a = (int32_t)m.payload.size();
+        per[m.dst_loop % X->nloops_].push_back(std::move(m));
+        return;
+      }
+      case F_ANNOUNCE: {  // coordinator: a bulk waiting for a round
+        if (X->o_.rank != 0 || m.payload.size() != sizeof(WireEntry)) return;
+        WireEntry e;
+        std::memcpy(&e, m.payload.data(), sizeof(e));
+        if (ann.empty()) ann_deadline = now_s() + X->o_.batch_us * 1e-6;
+        ann.push_back(e);
+        return;
+      }
+      case F_MANIFEST: {
+        Manifest mf;
+        mf.round = m.a;
+        mf.epoch = m.b;
+        mf.fallback = m.flags & 1;
+        const size_t n = m.payload.size() / sizeof(WireEntry);
+        mf.es.resize(n);
+        if (n) std::memcpy(mf.es.data(), m.payload.data(), n * sizeof(WireEntry));
+        {
+          std::lock_guard<std::mutex> g(bmu);
+          manifests.push_back(std::move(mf));
+        }
+        bcv.notify_all();
+        return;
+      }
+      case F_EPOCH: {
+        {
+          std::lock_guard<std::mutex> g(bmu);
+          if (m.a == 0) {
+            drop_comm = true;  // RCCL is down somewhere: everyone drops to the mesh
+            pending_epoch = 0;
+          } else {
+            pending_epoch = m.a;
+            pending_id = m.payload;
+          }
+        }
+        if (m.a == 0) X->rccl_ok_.store(false);
+        bcv.notify_all();
+        return;
+      }
+      case F_RCCL_DOWN:
+        if (X->o_.rank == 0 && m.a == epoch_no) rccl_down_everywhere();
+        return;
+      default:
+        (void)r;
+        return;
+    }
+  }
+  // coordinator: RCCL is unusable (a round failed, a peer left): every rank drops its
+  // communicator; a new epoch forms once every rank is up again
+  void rccl_down_everywhere() {
+    if (!epoch_live) return;
+    epoch_live = false;
+    // back off before the next epoch: 0.5 s, 1 s, 2 s, ... 60 s (a communicator that cannot
+    // form — e.g. two ranks on one GPU in a rehearsal — must not be retried in a tight loop)
+    next_epoch_at = now_s() + std::min(60.0, 0.5 * (double)(1 << std::min(epoch_failures, 7)));
+    ++epoch_failures;
+    XMsg e;
+    e.type = F_EPOCH;
+    e.a = 0;
+    for (int r = 0; r < X->o_.world; ++r) {
+      e.dst_rank = r;
+      if (r == X->o_.rank || peers[r].up) enqueue(r, frame(e));
+    }
+  }
+  void maybe_new_epoch() {
+    if (X->o_.rank != 0 || X->o_.transport != "rccl" || epoch_live || !all_up() || now_s() < next_epoch_at) return;
+    std::string id;
+    try {
+      id = rccl_unique_id_hex();
+    } catch (const std::exception& ex) {
+      fprintf(stderr, "qmx exchange: %s\n", ex.what());
+      return;
+    }
+    epoch_live = true;
+    ++epoch_no;
+    XMsg e;
+    e.type = F_EPOCH;
+    e.a = epoch_no;
+    e.payload = id;
+    for (int r = 0; r < X->o_.world; ++r) {
+      e.dst_rank = r;
+      enqueue(r, frame(e));
+    }
+  }
+  // coordinator: turn the batched announcements into a round; each involved rank gets its
+  // own entries in round order (per-pair order identical on both ends)
+  void form_round() {
+    if (ann.empty()) return;
+    const bool fallback = !epoch_live;
+    ++round_no;
+    std::map<int, std::vector<WireEntry>> part;
+    for (const WireEntry& e : ann) {
+      if (fallback) {
+        part[e.src].push_back(e);  // only the sender acts: it ships the bytes over the mesh
+        continue;
+      }
+      part[e.src].push_back(e);
+      part[e.dst].push_back(e);
+    }
+    ann.clear();
+    for (auto& kv : part) {
+      XMsg m;
+      m.type = F_MANIFEST;
+      m.a = round_no;
+      m.b = epoch_no;
+      m.flags = fallback ? 1 : 0;
+      m.dst_rank = kv.first;
+      m.payload.assign((const char*)kv.second.data(), kv.second.size() * sizeof(WireEntry));
+      enqueue(kv.first, frame(m));
+    }
+  }
+};
+
+// ----------------------------------------------------------------------------------------
 Exchange::Exchange(const XOptions& o, int nloops, Deliver deliver)
-    : o_(o), nloops_(nloops), deliver_(std::move(deliver)) {
-  th_ = std::thread([this] { run(); });
+    : o_(o), nloops_(nloops), deliver_(std::move(deliver)), im_(new Impl(this)) {
+  im_->peers.resize(o_.world);
+  im_->posted.resize(o_.world);
+  im_->ep = epoll_create1(0);
+  im_->evfd = eventfd(0, EFD_NONBLOCK);
+  epoll_event e{};
+  e.events = EPOLLIN;
+  e.data.u64 = 1ull << 40;  // eventfd
+  epoll_ctl(im_->ep, EPOLL_CTL_ADD, im_->evfd, &e);
+  im_->lfd = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK, 0);
+  int one = 1;
+  setsockopt(im_->lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons((uint16_t)(o_.port + o_.rank));
+  inet_pton(AF_INET, o_.addr.c_str(), &a.sin_addr);
+  if (bind(im_->lfd, (sockaddr*)&a, sizeof(a)) != 0 || listen(im_->lfd, 64) != 0) {
+    fprintf(stderr, "qmx exchange (rank %d): mesh listen on %d failed: %s — spread placement disabled\n", o_.rank,
+            o_.port + o_.rank, strerror(errno));
+    close(im_->lfd);
+    im_->lfd = -1;
+  } else {
+    e.events = EPOLLIN;
+    e.data.u64 = 1ull << 41;  // listener
+    epoll_ctl(im_->ep, EPOLL_CTL_ADD, im_->lfd, &e);
+  }
+  mesh_th_ = std::thread([this] { mesh_loop(); });
+  if (o_.transport == "rccl") bulk_th_ = std::thread([this] { bulk_loop(); });
 }
+
 Exchange::~Exchange() {
   request_stop();
   join();
-}
-void Exchange::post(XMsg&& m) {
-  if (stop_.load()) return;
-  std::lock_guard<std::mutex> g(mu_);
-  out_.push_back(std::move(m));
-}
-void Exchange::request_stop() {
-  stop_.store(true);
-  cv_.notify_all();
-}
-void Exchange::join() {
-  if (th_.joinable()) th_.join();
+  for (auto& p : im_->peers)
+    if (p.fd >= 0) close(p.fd);
+  if (im_->lfd >= 0) close(im_->lfd);
+  if (im_->evfd >= 0) close(im_->evfd);
+  if (im_->ep >= 0) close(im_->ep);
 }
 
-void Exchange::run() {
-  std::unique_ptr<XTransport> tr;
-  auto down = [&]() {
-    healthy_.store(false);
-    for (int l = 0; l < nloops_; ++l) {
-      std::vector<XMsg> v(1);
-      v[0].type = X_DOWN;
-      deliver_(l, std::move(v));
+void Exchange::post(XMsg&& m) {
+  if (stop_.load() || m.dst_rank < 0 || m.dst_rank >= o_.world) return;
+  const int r = m.dst_rank;
+  im_->enqueue(r, frame(m));
+}
+
+bool Exchange::peer_up(int r) const {
+  if (r == o_.rank) return true;
+  return r >= 0 && r < o_.world && ((im_->up_mask_bits.load() >> r) & 1ull);
+}
+
+void Exchange::send_bulk(XMsg&& hdr, const void* dev, size_t len, std::function<std::string()> host) {
+  const int dst = hdr.dst_rank;
+  if (rccl_active() && dev != nullptr && len > 0) {
+    WireEntry e{};
+    e.src = o_.rank;
+    e.dst = dst;
+    e.skey = hdr.skey;
+    e.bi = hdr.bi;
+    e.b = hdr.b;
+    e.len = (uint32_t)len;
+    e.src_loop = hdr.src_loop;
+    e.dst_loop = hdr.dst_loop;
+    e.flags = hdr.flags;
+    {
+      std::lock_guard<std::mutex> g(im_->bmu);
+      Impl::Send s;
+      s.hdr = hdr;
+      s.dev = dev;
+      s.len = len;
+      s.host = std::move(host);
+      im_->sends[{hdr.skey, hdr.bi}] = std::move(s);
+    }
+    XMsg a;
+    a.type = F_ANNOUNCE;
+    a.dst_rank = 0;
+    a.src_rank = o_.rank;
+    a.payload.assign((const char*)&e, sizeof(e));
+    im_->enqueue(0, frame(a));
+    return;
+  }
+  // mesh: the bytes ride the owner's connection right behind the stream's deltas
+  XMsg m = std::move(hdr);
+  const int src_loop = m.src_loop;
+  m.type = F_BULK_MESH;
+  m.payload = len ? host() : std::string();
+  XMsg sent;
+  sent.type = X_SENT;
+  sent.skey = m.skey;
+  sent.bi = m.bi;
+  sent.dst_loop = (uint16_t)src_loop;
+  post(std::move(m));
+  std::vector<XMsg> v;
+  v.push_back(std::move(sent));
+  deliver_(src_loop % nloops_, std::move(v));
+}
+
+void Exchange::expect_bulk(uint64_t skey, int bi, void* dev, size_t cap) {
+  std::lock_guard<std::mutex> g(im_->bmu);
+  im_->sinks[{skey, bi}] = Impl::Sink{dev, cap};
+}
+void Exchange::forget_bulk(uint64_t skey, int bi) {
+  std::lock_guard<std::mutex> g(im_->bmu);
+  im_->sinks.erase({skey, bi});
+}
+
+void Exchange::request_stop() {
+  stop_.store(true);
+  if (im_ && im_->evfd >= 0) im_->wake();
+  if (im_) im_->bcv.notify_all();
+}
+void Exchange::join() {
+  if (mesh_th_.joinable()) mesh_th_.join();
+  if (bulk_th_.joinable()) bulk_th_.join();
+}
+
+// ------------------------------------------------------------------ the mesh thread
+void Exchange::mesh_loop() {
+  Impl& I = *im_;
+  if (I.lfd < 0) {
+    std::vector<XMsg> v(1);
+    v[0].type = X_DOWN;
+    v[0].a = -1;
+    for (int l = 0; l < nloops_; ++l) deliver_(l, std::vector<XMsg>(v));
+    return;
+  }
+  for (int r = 0; r < o_.world; ++r) I.peers[r].next_dial = 0;
+  std::vector<epoll_event> evs(64);
+  std::vector<int> pending;  // accepted sockets waiting for their hello
+  std::map<int, std::string> pend_in;
+  char buf[65536];
+  while (!stop_.load()) {
+    const double t = now_s();
+    // the higher rank dials; retry every 100 ms while a lower peer is down
+    for (int r = 0; r < o_.rank; ++r) {
+      Impl::Peer& p = I.peers[r];
+      if (p.fd < 0 && t >= p.next_dial) I.dial(r);
+    }
+    int to = 20;
+    if (o_.rank == 0 && !I.ann.empty()) to = std::max(0, (int)((I.ann_deadline - t) * 1000));
+    int n = epoll_wait(I.ep, evs.data(), (int)evs.size(), to);
+    for (int i = 0; i < n; ++i) {
+      const uint64_t tag = evs[i].data.u64;
+      if (tag == (1ull << 40)) {
+        uint64_t v;
+        ssize_t rd = read(I.evfd, &v, 8);
+        (void)rd;
+        continue;
+      }
+      if (tag == (1ull << 41)) {
+        while (true) {
+          int fd = accept4(I.lfd, nullptr, nullptr, SOCK_NONBLOCK);
+          if (fd < 0) break;
+          I.set_nodelay(fd);
+          epoll_event e{};
+          e.events = EPOLLIN;
+          e.data.u64 = (1ull << 42) | (uint32_t)fd;
+          epoll_ctl(I.ep, EPOLL_CTL_ADD, fd, &e);
+          pending.push_back(fd);
+        }
+        continue;
+      }
+      if (tag & (1ull << 42)) {  // an accepted connection: its hello names the peer
+        const int fd = (int)(uint32_t)tag;
+        std::string& in = pend_in[fd];
+        bool dead = false;
+        while (true) {
+          ssize_t r = recv(fd, buf, sizeof(buf), 0);
+          if (r > 0) {
+            in.append(buf, r);
+            continue;
+          }
+          if (r == 0 || (errno != EAGAIN && errno != EWOULDBLOCK)) dead = true;
+          break;
+        }
+        if (!dead && in.size() >= sizeof(WireHdr)) {
+          WireHdr h;
+          std::memcpy(&h, in.data(), sizeof(h));
+          const int pr = h.a;
+          if (h.type != F_HELLO || pr <= o_.rank || pr >= o_.world) {
+            dead = true;
+          } else {
+            Impl::Peer& p = I.peers[pr];
+            if (p.fd >= 0) I.mark_down(pr);  // a re-joined peer replaces its dead connection
+            p.fd = fd;
+            p.in = in.substr(sizeof(WireHdr) + h.len);
+            epoll_event e{};
+            e.events = EPOLLIN;
+            e.data.u64 = (uint64_t)(pr + 1);
+            epoll_ctl(I.ep, EPOLL_CTL_MOD, fd, &e);
+            pend_in.erase(fd);
+            pending.erase(std::remove(pending.begin(), pending.end(), fd), pending.end());
+            I.mark_up(pr);
+            if (!p.in.empty()) I.on_frames(pr, p.in);
+            continue;
+          }
+        }
+        if (dead) {
+          epoll_ctl(I.ep, EPOLL_CTL_DEL, fd, nullptr);
+          close(fd);
+          pend_in.erase(fd);
+          pending.erase(std::remove(pending.begin(), pending.end(), fd), pending.end());
+        }
+        continue;
+      }
+      const int r = (int)tag - 1;
+      if (r < 0 || r >= o_.world) continue;
+      Impl::Peer& p = I.peers[r];
+      if (p.fd < 0) continue;
+      if (p.dialing && (evs[i].events & (EPOLLOUT | EPOLLERR | EPOLLHUP))) {
+        int err = 0;
+        socklen_t el = sizeof(err);
+        getsockopt(p.fd, SOL_SOCKET, SO_ERROR, &err, &el);
+        if (err != 0) {
+          I.mark_down(r);
+          continue;
+        }
+        p.dialing = false;
+        I.mark_up(r);  // our hello is queued first in p.out
+      }
+      if (evs[i].events & EPOLLOUT) I.flush(r);
+      if (p.fd < 0) continue;
+      if (evs[i].events & (EPOLLIN | EPOLLHUP | EPOLLERR)) {
+        bool dead = false;
+        while (true) {
+          ssize_t rr = recv(p.fd, buf, sizeof(buf), 0);
+          if (rr > 0) {
+            p.in.append(buf, rr);
+            continue;
+          }
+          if (rr == 0 || (errno != EAGAIN && errno != EWOULDBLOCK)) dead = true;
+          break;
+        }
+        if (!p.in.empty()) I.on_frames(r, p.in);
+        if (dead) I.mark_down(r);
+      }
+    }
+    I.take_posted();
+    if (!healthy_.load() && I.all_up()) {
+      healthy_.store(true);  // every peer reached once: sessions may spread from now on
+      I.ever_all_up = true;
+    }
+    if (o_.rank == 0) {
+      I.maybe_new_epoch();
+      if (!I.ann.empty() && now_s() >= I.ann_deadline) {
+        I.form_round();
+        I.take_posted();
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ the bulk (RCCL) thread
+void Exchange::bulk_loop() {
+  Impl& I = *im_;
+  ncclComm_t comm = nullptr;
+  int epoch = 0;
+  hipStream_t st = nullptr;
+  uint8_t* scratch = nullptr;
+  size_t scratch_cap = 0;
+  try {
+    XHIP(hipSetDevice(o_.device));
+    XHIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  } catch (const std::exception& e) {
+    fprintf(stderr, "qmx exchange (rank %d): %s — bulk transfers use the mesh\n", o_.rank, e.what());
+    return;
+  }
+  auto drop = [&](bool report) {
+    if (comm) ncclCommAbort(comm);
+    comm = nullptr;
+    rccl_ok_.store(false);
+    if (report && epoch > 0) {
+      XMsg m;
+      m.type = F_RCCL_DOWN;
+      m.a = epoch;
+      m.dst_rank = 0;
+      I.enqueue(0, frame(m));
     }
   };
-  try {
-    tr = o_.transport == "rccl" ? make_rccl_transport(o_) : make_tcp_transport(o_);
-  } catch (const std::exception& e) {
-    fprintf(stderr, "qmx exchange (rank %d): %s — spread placement disabled\n", o_.rank, e.what());
-    return down();
-  }
-  healthy_.store(true);  // sessions start placing streams on other ranks from now on
-  int idle = 0;
-  std::vector<std::string> all;
-  std::vector<uint32_t> fl;
-  while (true) {
-    std::vector<XMsg> batch;
-    bool stopping;
-    {
-      std::unique_lock<std::mutex> lk(mu_);
-      // Every rank paces identically (idle is derived from the gathered totals), so the
-      // lock-step collective is not held up by a sleeping peer for long.
-      const int us = idle > 64 ? 1000 : o_.round_us;
-      cv_.wait_for(lk, std::chrono::microseconds(us), [this] { return stop_.load(); });
-      batch.swap(out_);
-      stopping = stop_.load();
+  // wait for the communicator's pending operation (non-blocking communicator)
+  auto comm_ready = [&](double deadline) {
+    while (true) {
+      ncclResult_t ae = ncclSuccess;
+      if (ncclCommGetAsyncError(comm, &ae) != ncclSuccess) return false;
+      if (ae == ncclSuccess) return true;
+      if (ae != ncclInProgress || now_s() > deadline || stop_.load()) return false;
+      std::this_thread::sleep_for(std::chrono::microseconds(100));
     }
-    std::string mine;
-    serialize(batch, mine);
+  };
+  auto mesh_fallback = [&](const WireEntry& e) {
+    Impl::Send s;
+    {
+      std::lock_guard<std::mutex> g(I.bmu);
+      auto it = I.sends.find({e.skey, e.bi});
+      if (it == I.sends.end()) return;
+      s = std::move(it->second);
+      I.sends.erase(it);
+    }
+    XMsg m = s.hdr;
+    m.type = F_BULK_MESH;
+    m.payload = s.len ? s.host() : std::string();
+    post(std::move(m));
+    mesh_bulk_++;
+    std::vector<XMsg> v(1);
+    v[0].type = X_SENT;
+    v[0].skey = e.skey;
+    v[0].bi = e.bi;
+    v[0].dst_loop = e.src_loop;
+    deliver_(e.src_loop % nloops_, std::move(v));
+  };
+  while (!stop_.load()) {
+    Impl::Manifest mf;
+    int want_epoch = 0;
+    std::string id;
+    bool dropc = false;
+    {
+      std::unique_lock<std::mutex> lk(I.bmu);
+      I.bcv.wait_for(lk, std::chrono::milliseconds(50), [&] {
+        return stop_.load() || !I.manifests.empty() || I.drop_comm || (I.pending_epoch && I.pending_epoch != epoch);
+      });
+      if (stop_.load()) break;
+      dropc = I.drop_comm;
+      I.drop_comm = false;
+      if (I.pending_epoch && I.pending_epoch != epoch) {
+        want_epoch = I.pending_epoch;
+        id = I.pending_id;
+      }
+      if (!I.manifests.empty()) {
+        mf = std::move(I.manifests.front());
+        I.manifests.pop_front();
+      }
+    }
+    if (dropc) {
+      drop(false);
+      epoch = 0;
+    }
+    if (want_epoch) {  // (re)form the world communicator
+      drop(false);
+      ncclUniqueId uid;
+      if (from_hex(id, &uid)) {
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;
+        ncclResult_t r = ncclCommInitRankConfig(&comm, o_.world, uid, o_.rank, &cfg);
+        if ((r == ncclSuccess || r == ncclInProgress) && comm_ready(now_s() + o_.timeout_s)) {
+          epoch = want_epoch;
+          rccl_epoch_.store((uint64_t)epoch);
+          rccl_ok_.store(true);
+        } else {
+          fprintf(stderr, "qmx exchange (rank %d): RCCL epoch %d did not form — bulk uses the mesh\n", o_.rank,
+                  want_epoch);
+          epoch = want_epoch;
+          drop(true);
+        }
+      }
+    }
+    if (mf.es.empty() && !mf.fallback) continue;
+    if (mf.fallback || !comm || mf.epoch != epoch) {
+      for (const WireEntry& e : mf.es)
+        if (e.src == o_.rank) mesh_fallback(e);
+      // a receive whose sender falls back arrives over the mesh (F_BULK_MESH)
+      continue;
+    }
+    // one group: this rank's sends and receives of the round, in manifest order
     const double t0 = now_s();
-    if (!tr->allgather(mine, stopping ? 1u : 0u, all, fl)) {
-      fprintf(stderr, "qmx exchange (rank %d): round failed — falling back to local placement\n", o_.rank);
-      return down();
+    std::vector<std::pair<const WireEntry*, Impl::Send>> my_sends;
+    std::vector<std::pair<const WireEntry*, size_t>> my_recvs;  // (entry, staging offset)
+    bool ok = true;
+    size_t recv_off = 0;
+    {
+      size_t scratch_need = 256;
+      for (const WireEntry& e : mf.es)
+        if (e.dst == o_.rank) scratch_need += (e.len + 255) & ~(size_t)255;
+      if (scratch_need > scratch_cap) {
+        if (scratch) hipFree(scratch);
+        scratch_cap = std::max(scratch_need, scratch_cap * 2);
+        if (hipMalloc(&scratch, scratch_cap) != hipSuccess) {
+          scratch = nullptr;
+          scratch_cap = 0;
+          ok = false;
+        }
+      }
+    }
+    if (ok && ncclGroupStart() != ncclSuccess) ok = false;
+    for (const WireEntry& e : mf.es) {
+      if (!ok) break;
+      if (e.src == o_.rank) {
+        Impl::Send s;
+        {
+          std::lock_guard<std::mutex> g(I.bmu);
+          auto it = I.sends.find({e.skey, e.bi});
+          if (it != I.sends.end()) {
+            s = std::move(it->second);
+            I.sends.erase(it);
+          }
+        }
+        const void* src = s.dev ? s.dev : scratch + scratch_cap - 256;  // (a vanished send still matches)
+        ncclResult_t r = ncclSend(src, e.len, ncclUint8, e.dst, comm, st);
+        ok = r == ncclSuccess || r == ncclInProgress;
+        my_sends.emplace_back(&e, std::move(s));
+      } else if (e.dst == o_.rank) {
+        // into this rank's staging area (one slot per receive of the round): the owner may
+        // release the destination slot while the round is in flight; the copy into its HBM
+        // content slot happens under the sink lock once the data is here
+        ncclResult_t r = ncclRecv(scratch + recv_off, e.len, ncclUint8, e.src, comm, st);
+        ok = r == ncclSuccess || r == ncclInProgress;
+        my_recvs.emplace_back(&e, recv_off);
+        recv_off += (e.len + 255) & ~(size_t)255;
+      }
+    }
+    if (ok) {
+      ncclResult_t r = ncclGroupEnd();
+      ok = (r == ncclSuccess || r == ncclInProgress) && comm_ready(now_s() + o_.timeout_s);
+    }
+    // completion: poll the stream; give up at the timeout or as soon as a peer of the round
+    // leaves the mesh (its socket closed)
+    while (ok) {
+      hipError_t e = hipStreamQuery(st);
+      if (e == hipSuccess) break;
+      bool peer_gone = false;
+      for (const WireEntry& w : mf.es) {
+        const int p = w.src == o_.rank ? w.dst : w.src;
+        if (!peer_up(p)) peer_gone = true;
+      }
+      bool dropped;
+      {
+        std::lock_guard<std::mutex> g(I.bmu);
+        dropped = I.drop_comm;  // rank 0 declared RCCL down (another rank's round failed)
+      }
+      if (e != hipErrorNotReady || peer_gone || dropped || now_s() - t0 > o_.timeout_s || stop_.load()) {
+        ok = false;
+        break;
+      }
+      if (now_s() - t0 < 5e-4) sched_yield();
+      else std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
     busy_us_.store(busy_us_.load() + 1e6 * (now_s() - t0));
-    rounds_++;
-    size_t total = 0;
-    bool all_stop = true;
-    std::vector<std::vector<XMsg>> per(nloops_);
-    for (int r = 0; r < (int)all.size(); ++r) {
-      total += all[r].size();
-      all_stop = all_stop && (fl[r] & 1);
-      std::vector<XMsg> got;
-      if (!parse_for(all[r], o_.rank, got)) continue;
-      for (auto& m : got) per[m.dst_loop % nloops_].push_back(std::move(m));
+    if (!ok) {
+      fprintf(stderr, "qmx exchange (rank %d): RCCL round %d failed — communicator dropped, bulk uses the mesh\n",
+              o_.rank, mf.round);
+      drop(true);
+      hipStreamSynchronize(st);  // the aborted communicator's kernels have been flushed
+      for (auto& s : my_sends) {  // resend over the mesh (a receiver may see it twice: it dedups)
+        if (!s.second.host) continue;
+        std::lock_guard<std::mutex> g(I.bmu);
+        I.sends[{s.first->skey, s.first->bi}] = std::move(s.second);
+      }
+      for (auto& s : my_sends) mesh_fallback(*s.first);
+      continue;
     }
-    bytes_ += total;
-    for (int l = 0; l < nloops_; ++l)
-      if (!per[l].empty()) deliver_(l, std::move(per[l]));
-    idle = total ? 0 : idle + 1;
-    if (all_stop) break;
+    rounds_++;
+    for (auto& s : my_sends) {
+      bulk_bytes_ += s.first->len;
+      std::vector<XMsg> v(1);
+      v[0].type = X_SENT;
+      v[0].skey = s.first->skey;
+      v[0].bi = s.first->bi;
+      v[0].dst_loop = s.first->src_loop;
+      deliver_(s.first->src_loop % nloops_, std::move(v));
+    }
+    for (auto& rcv : my_recvs) {
+      const WireEntry& e = *rcv.first;
+      bulk_bytes_ += e.len;
+      {
+        std::lock_guard<std::mutex> g(I.bmu);
+        auto it = I.sinks.find({e.skey, e.bi});
+        if (it == I.sinks.end() || !it->second.dev || it->second.cap < e.len) continue;  // session gone
+        // HBM → HBM into the owner's shadow slot; complete before the lock drops, so a
+        // forget_bulk() that returns guarantees no later write into a released slot
+        if (e.len && (hipMemcpyAsync(it->second.dev, scratch + rcv.second, e.len, hipMemcpyDeviceToDevice, st) !=
+                          hipSuccess ||
+                      hipStreamSynchronize(st) != hipSuccess))
+          continue;
+      }
+      std::vector<XMsg> v(1);
+      v[0].type = X_BULK;
+      v[0].flags = e.flags;
+      v[0].skey = e.skey;
+      v[0].bi = e.bi;
+      v[0].a = (int32_t)e.len;  // already in the owner's HBM content arena
+      v[0].b = e.b;
+      v[0].src_rank = e.src;
+      v[0].dst_loop = e.dst_loop;
+      deliver_(e.dst_loop % nloops_, std::move(v));
+    }
   }
+  if (comm) ncclCommAbort(comm);
+  if (scratch) hipFree(scratch);
+  if (st) hipStreamDestroy(st);
 }
 
 }  // namespace qmx

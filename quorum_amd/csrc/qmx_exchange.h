@@ -1,25 +1,33 @@
-// qmx_exchange.h — cross-rank message exchange for spread (EP-style) backend placement.
+// qmx_exchange.h — cross-rank messaging for spread (EP-style) backend placement.
 //
 // One process per GPU.  With `placement: spread`, a session's N backend streams run on
 // ranks owner, owner+1, ... (mod world): each worker rank opens the upstream connection
-// from its own keep-alive pool and runs the stream through its own GPU tick kernel; the
-// encoded SSE deltas and the stripped final text come back to the session owner.
+// from its own keep-alive pool and runs the stream through its own GPU tick kernel.
 //
-// Transport = lock-step rounds of an all-gather: every rank contributes
-// one buffer per round holding all its outgoing messages; receivers keep the messages
-// addressed to them.  Round = ONE fixed-slot all-gather (header + up to kSlot bytes per
-// rank) in the common case, plus a padded all-gather of max_len bytes when any rank has
-// more (lengths travel in the first one).  Backends:
-//   rccl — ncclAllGather on a dedicated HIP stream over xGMI (device buffers, pinned
-//          staging); a round that does not complete within the timeout aborts the
-//          communicator (rank death) and the survivors fall back to local placement.
-//   tcp  — hub at rank 0 (CPU tests, no GPU).
-// Messages are tiny (KB) and rounds are latency-bound, so the design batches every
-// message of a round into one collective rather than issuing per-session operations.
+// Two planes, both event-driven (nothing moves while every rank is idle):
+//  * mesh — a TCP connection per rank pair (rank r listens on port + r; the higher rank
+//    dials).  Control messages (open / cancel / final flags) and the encoded SSE deltas
+//    travel point to point, owner <-> worker, never through a collective: they are on the
+//    TTFT path (SURVEY §7.4 hard part 5).  A dropped connection marks the peer down (its
+//    streams fail, new sessions stop placing streams there); the higher rank redials every
+//    100 ms, so a restarted rank re-joins the mesh without any coordination.
+//  * bulk — a stream's final text goes from the worker's HBM content arena straight into the
+//    owner's HBM content arena (the owner's "shadow" slot for that stream) with ncclSend /
+//    ncclRecv over xGMI, so the owner's own fused finalize kernel (K3 strip, K4 join, K5
+//    encode) merges local and remote streams alike.  RCCL point-to-point
+//    needs both ends to post matching operations in the same per-pair order: rank 0
+//    coordinates — workers announce (owner, length) over the mesh, rank 0 batches the
+//    announcements into numbered rounds and sends each involved rank its part of the round
+//    manifest; every rank executes rounds in order, one ncclGroupStart/End per round with
+//    only its own sends and receives.  A peer that never answers aborts the communicator
+//    (a round timeout); bulk transfers then fall back to the mesh (host bytes) until rank 0
+//    re-forms the communicator over the ranks that are up (a new "epoch").  transport=tcp
+//    (CPU tests, no GPU) sends bulk bytes over the mesh only.
 #pragma once
 #include <atomic>
 #include <condition_variable>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -28,8 +36,18 @@
 
 namespace qmx {
 
-enum XType : uint8_t { X_OPEN = 1, X_DATA = 2, X_FINAL = 3, X_CANCEL = 4, X_DOWN = 5 };
-// X_FINAL flags
+enum XType : uint8_t {
+  X_OPEN = 1,    // owner → worker: run stream bi of session skey (payload: upstream request)
+  X_DATA = 2,    // worker → owner: encoded SSE deltas of the stream
+  X_FINAL = 3,   // worker → owner: stream over without a bulk text (flags below)
+  X_CANCEL = 4,  // owner → worker: session gone, stop the stream
+  X_DOWN = 5,    // exchange → loops: peer `a` is unreachable (a = -1: the whole exchange)
+  X_BULK = 6,    // exchange → owner loop: the stream's final text arrived (a = length, b = data
+                 //   messages sent before it; payload = the bytes when not written to HBM)
+  X_SENT = 7,    // exchange → worker loop: the bulk left (flags XF_FAILED if it could not)
+  X_UP = 8,      // exchange → loops: peer `a` (re)joined the mesh
+};
+// X_FINAL / X_BULK / X_SENT flags
 enum : uint8_t { XF_TEXT = 1, XF_ABORTED = 2, XF_FAILED = 4 };
 
 struct XMsg {
@@ -46,52 +64,67 @@ struct XOptions {
   int rank = 0, world = 1;
   std::string transport = "tcp";  // tcp | rccl
   std::string addr = "127.0.0.1";
-  int port = 0;                   // tcp hub port
-  std::string id_file;            // rccl: rank 0 writes the unique id here, others read it
+  int port = 0;                   // mesh: rank r listens on port + r
   int device = 0;
-  int round_us = 200;             // pacing between rounds while traffic flows
-  double timeout_s = 30.0;        // a round slower than this = peer failure
+  int batch_us = 50;              // rank 0: announcements arriving within this window share a round
+  double timeout_s = 30.0;        // bulk round / epoch formation slower than this = peer failure
 };
 
-class XTransport {
- public:
-  virtual ~XTransport() = default;
-  // All-gather `mine` (+ flag bits); returns false on failure (peer death / timeout).
-  virtual bool allgather(const std::string& mine, uint32_t flags, std::vector<std::string>& all,
-                         std::vector<uint32_t>& all_flags) = 0;
+// the mesh's view of one peer
+struct PeerStats {
+  bool up = false;
+  uint64_t msgs_out = 0, msgs_in = 0, bytes_out = 0, bytes_in = 0, connects = 0;
 };
-
-std::unique_ptr<XTransport> make_tcp_transport(const XOptions& o);
-std::unique_ptr<XTransport> make_rccl_transport(const XOptions& o);
-std::string rccl_unique_id_hex();  // for launchers that distribute the id themselves
 
 class Exchange {
  public:
   using Deliver = std::function<void(int loop, std::vector<XMsg>&&)>;
   Exchange(const XOptions& o, int nloops, Deliver deliver);
   ~Exchange();
-  void post(XMsg&& m);       // thread-safe
-  void request_stop();       // the thread exits once every rank has requested stop
+  void post(XMsg&& m);  // thread-safe: control / delta message to m.dst_rank over the mesh
+  // Worker: ship stream (hdr.skey, hdr.bi)'s final text to hdr.dst_rank.  `dev` points at
+  // `len` bytes in HBM that stay valid until X_SENT comes back to hdr.src_loop; `host`
+  // produces the bytes for the mesh fallback.  hdr.flags / hdr.b travel with it.
+  void send_bulk(XMsg&& hdr, const void* dev, size_t len, std::function<std::string()> host);
+  // Owner: a bulk for (skey, bi) lands at `dev` (HBM, capacity `cap`); nullptr / a mesh
+  // transfer delivers the bytes in X_BULK's payload instead.
+  void expect_bulk(uint64_t skey, int bi, void* dev, size_t cap);
+  void forget_bulk(uint64_t skey, int bi);
+  void request_stop();
   void join();
-  bool healthy() const { return healthy_.load(); }  // false until connected and after a failure
+  bool healthy() const { return healthy_.load(); }  // the mesh formed once and is running
+  bool peer_up(int r) const;
   int rank() const { return o_.rank; }
   int world() const { return o_.world; }
-  uint64_t rounds() const { return rounds_.load(); }
-  uint64_t bytes() const { return bytes_.load(); }
-  double busy_us() const { return busy_us_.load(); }
+  bool rccl_active() const { return rccl_epoch_.load() > 0 && rccl_ok_.load(); }
+  // counters (/metrics)
+  uint64_t rounds() const { return rounds_.load(); }        // RCCL bulk rounds executed here
+  uint64_t bytes() const { return bytes_.load(); }          // mesh payload bytes sent + received
+  uint64_t bulk_bytes() const { return bulk_bytes_.load(); }  // final-text bytes moved by RCCL
+  uint64_t mesh_bulk() const { return mesh_bulk_.load(); }  // finals moved over the mesh
+  uint64_t msgs() const { return msgs_.load(); }            // mesh messages sent + received
+  uint64_t epochs() const { return rccl_epoch_.load(); }    // RCCL communicators formed
+  uint64_t rejoins() const { return rejoins_.load(); }      // peer (re)connections after the first
+  double busy_us() const { return busy_us_.load(); }        // time inside RCCL rounds
+
+  struct Impl;
 
  private:
-  void run();
   XOptions o_;
   int nloops_;
   Deliver deliver_;
-  std::mutex mu_;
-  std::condition_variable cv_;
-  std::vector<XMsg> out_;
-  std::atomic<bool> stop_{false}, healthy_{false};  // healthy once the transport is up
-  std::atomic<uint64_t> rounds_{0}, bytes_{0};
+  std::unique_ptr<Impl> im_;
+  std::atomic<bool> stop_{false}, healthy_{false}, rccl_ok_{false};
+  std::atomic<uint64_t> rounds_{0}, bytes_{0}, bulk_bytes_{0}, mesh_bulk_{0}, msgs_{0}, rccl_epoch_{0}, rejoins_{0};
   std::atomic<double> busy_us_{0};
-  std::thread th_;
+  std::thread mesh_th_, bulk_th_;
+  void mesh_loop();
+  void bulk_loop();
+  friend struct Impl;
 };
+
+// RCCL point-to-point self-test over the same round machinery (bindings / GPU tests):
+// every rank sends `rounds` payloads to every other rank and checks what it receives.
+std::string rccl_unique_id_hex();
 
 }  // namespace qmx

@@ -132,6 +132,9 @@ class HipEngine : public HostEngine {
             int lanes = 1);
   ~HipEngine() override;
   std::string text(int slot) override;
+  void* content_device_ptr(int slot, size_t* cap) override;
+  size_t content_size(int slot) override;
+  void set_remote_content(int slot, const std::string* bytes, size_t len) override;
   std::unordered_map<std::string, double> kernel_stats();
   int lanes() const { return (int)lanes_.size(); }
 

@@ -1591,9 +1591,42 @@ void HipEngine::on_free(int slot) {
 
 std::string HipEngine::device_content(int slot, uint32_t len) {
   std::string out(len, '\0');
-  if (len)
+  if (len) {
+    HIP_CHECK(hipSetDevice(device_));  // io loops / exchange threads call this too
     HIP_CHECK(hipMemcpy(&out[0], d_content_ + (size_t)slot * content_cap_, len, hipMemcpyDeviceToHost));
+  }
   return out;
+}
+
+void* HipEngine::content_device_ptr(int slot, size_t* cap) {
+  *cap = 0;
+  if (slot < 0 || slot >= max_slots_ || slot >= (int)nslots() || host_mode_[slot]) return nullptr;
+  *cap = content_cap_;
+  return d_content_ + (size_t)slot * content_cap_;
+}
+
+size_t HipEngine::content_size(int slot) {
+  if (slot < 0 || slot >= (int)nslots()) return 0;
+  if (slot >= max_slots_ || host_mode_[slot]) return core_[slot].content.size();
+  return content_len_[slot];
+}
+
+// Spread placement: a remote stream's final text in this (owner) rank's shadow slot.  From
+// RCCL it is already in the slot's HBM area (bytes == nullptr); over the mesh it is copied
+// there (or kept on the host when it does not fit), so the fused finalize reads it like
+// any local stream.
+void HipEngine::set_remote_content(int slot, const std::string* bytes, size_t len) {
+  if (slot < 0 || slot >= (int)nslots()) return;
+  if (slot >= max_slots_ || (bytes && len > content_cap_)) {
+    if (slot < max_slots_) host_mode_[slot] = 1;
+    core_[slot].content = bytes ? *bytes : std::string();
+    return;
+  }
+  if (bytes && len) {
+    HIP_CHECK(hipSetDevice(device_));
+    HIP_CHECK(hipMemcpy(d_content_ + (size_t)slot * content_cap_, bytes->data(), len, hipMemcpyHostToDevice));
+  }
+  content_len_[slot] = (uint32_t)len;
 }
 
 void HipEngine::escalate(int slot, bool fresh) {

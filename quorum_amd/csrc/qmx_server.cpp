@@ -313,10 +313,11 @@ struct Up {
 
 struct BState {
   int backend = -1;
-  int slot = -1;
+  int slot = -1;          // engine slot (spread: the owner's shadow slot of a remote stream)
   int remote = -1;        // spread placement: rank running this stream (-1 = local)
-  bool has_text = false;  // per-stream final text (spread sessions)
-  std::string ftext;
+  int rx_data = 0;        // spread: delta messages received from the worker
+  bool bulk_waiting = false;  // spread: the final text arrived before some of its deltas
+  XMsg bulk_msg;
   Up* up = nullptr;
   int state = 0;  // 0 running, 1 done, 2 failed
   int status = 0;
@@ -352,9 +353,11 @@ struct Session {
   double t0 = 0;
   // spread placement
   uint64_t skey = 0;  // owner: key under which workers address this session
-  int remote_n = 0, fin_pending = 0;
+  int remote_n = 0;
   int owner_rank = -1, owner_loop = 0, shadow_bi = 0;  // worker (K_REMOTE)
   uint64_t owner_skey = 0;
+  int data_sent = 0;          // worker: delta messages posted to the owner
+  bool bulk_pending = false;  // worker: the final text is in flight (the slot must stay)
   bool first_content = false;  // TTFT recorded
 };
 
@@ -537,16 +540,17 @@ class GpuHub {
     for (int i = 0; i < lanes_; ++i) th_.emplace_back([this, i] { run(i); });
   }
   void attach(int loop, Sink s) { sinks_[loop] = std::move(s); }
-  int open(int loop, int index, bool f, bool e, uint32_t* gen) {
+  int open(int loop, int index, bool f, bool e, uint32_t* gen, bool verify = true) {
     int slot = eng_->open(index, f, e, gen);
     {
       std::lock_guard<std::mutex> g(omu_);
       if ((int)owner_.size() <= slot) owner_.resize(slot + 1024, -1);
       owner_[slot] = loop;
     }
-    if (ver_) ver_->open(slot, *gen, index, f, e);
+    if (ver_ && verify) ver_->open(slot, *gen, index, f, e);
     return slot;
   }
+  HostEngine& engine() { return *eng_; }
   void feed(int slot, const std::string& d) {
     eng_->feed(slot, d);
     if (ver_) ver_->feed(slot, d);
@@ -867,7 +871,10 @@ class Loop {
       if (fault_drop_every_ > 0 && !r.sse.empty() && ++fault_n_ % fault_drop_every_ == 0)
         r.sse.clear();  // QMX_FAULT_DROP_DELTA: fault injection (the bench's validator must notice)
       if (!r.sse.empty()) {
-        if (s->kind == K_REMOTE) post_owner(s, X_DATA, 0, 0, r.sse);
+        if (s->kind == K_REMOTE) {
+          post_owner(s, X_DATA, 0, 0, r.sse);
+          s->data_sent++;
+        }
         else if (s->cl) send_content(s, r.sse);
       }
       if ((r.flags & RF_ABORTED)) c_stream_aborts++;
@@ -889,16 +896,18 @@ class Loop {
     }
   }
   void kick() { kick_ = true; }
+  HostEngine& eng() { return hub_ ? hub_->engine() : *eng_; }
   // engine calls, mirrored into the verify shadow when enabled
   // opens an engine slot for stream `bi` of session s and registers its owner
-  int e_open(Session* s, int bi, int index, bool f, bool e) {
+  // verify = false: a spread owner's shadow slot (its content comes from another rank)
+  int e_open(Session* s, int bi, int index, bool f, bool e, bool verify = true) {
     uint32_t gen = 0;
     int slot;
     if (hub_) {
-      slot = hub_->open(idx_, index, f, e, &gen);
+      slot = hub_->open(idx_, index, f, e, &gen, verify);
     } else {
       slot = eng_->open(index, f, e, &gen);
-      if (ver_) ver_->open(slot, gen, index, f, e);
+      if (ver_ && verify) ver_->open(slot, gen, index, f, e);
     }
     slot_owner_[slot] = SlotOwner{s, bi, gen};
     return slot;
@@ -1754,9 +1763,16 @@ class Loop {
     for (size_t i = 0; i < valid.size(); ++i) {
       s->bs[i].backend = valid[i];
       const int target = spread ? (xch_->rank() + (int)i) % xch_->world() : -1;
-      if (spread && target != xch_->rank()) {
+      if (spread && target != xch_->rank() && xch_->peer_up(target)) {
         s->bs[i].remote = target;
         s->remote_n++;
+        // the owner's shadow slot: the remote stream's final text lands in its HBM content
+        // area (RCCL, HBM to HBM), so this rank's fused finalize merges remote and local
+        // streams alike; it is never fed upstream bytes
+        s->bs[i].slot = e_open(s, (int)i, (int)i, false, false, false);
+        size_t cap = 0;
+        void* dev = eng().content_device_ptr(s->bs[i].slot, &cap);
+        xch_->expect_bulk(s->skey, (int)i, dev, cap);
         continue;
       }
       s->bs[i].slot = e_open(s, (int)i, (int)i, s->filter, s->emit);
@@ -1797,57 +1813,40 @@ class Loop {
   }
   void begin_final(Session* s) {
     s->stage = 1;
-    if (s->kind == K_REMOTE) {  // worker: hand the stream's (stripped) final text to the owner
+    if (s->kind == K_REMOTE) {  // worker: ship the stream's final text to the owner
       const BState& b = s->bs[0];
-      if (b.aborted || cfg_.skip_final) {
+      const size_t len = b.aborted || cfg_.skip_final ? 0 : eng().content_size(b.slot);
+      if (len == 0) {
         post_owner(s, X_FINAL, b.aborted ? XF_ABORTED : 0, 0, std::string());
         return end_session(s);
       }
-      s->fin_id = e_submit({b.slot}, cfg_.hide_final, true, std::string(), (int64_t)time(nullptr));
-      fin_owner_[s->fin_id] = {s, -1};
-      kick();
+      // HBM content slot → the owner's shadow slot (RCCL p2p round), or its bytes over the
+      // mesh; the slot stays ours until X_SENT says the transfer has left
+      XMsg h;
+      h.flags = XF_TEXT;
+      h.dst_rank = s->owner_rank;
+      h.src_rank = xch_->rank();
+      h.dst_loop = (uint16_t)s->owner_loop;
+      h.src_loop = (uint16_t)idx_;
+      h.bi = s->shadow_bi;
+      h.skey = s->owner_skey;
+      h.b = s->data_sent;  // the owner applies the final after this many deltas
+      size_t cap = 0;
+      const void* dev = eng().content_device_ptr(b.slot, &cap);
+      HostEngine* e = &eng();
+      const int slot = b.slot;
+      s->bulk_pending = true;
+      xch_->send_bulk(std::move(h), dev, len, [e, slot] { return e->text(slot); });
       return;
     }
     if (cfg_.skip_final) return finish_stream(s);
-    if (s->remote_n > 0) {  // owner of a spread session: per-stream texts, merged in backend order
-      for (int i = 0; i < (int)s->bs.size(); ++i) {
-        const BState& b = s->bs[i];
-        if (b.remote >= 0 || b.state != 1 || b.aborted) continue;
-        int id = e_submit({b.slot}, cfg_.hide_final, true, std::string(), (int64_t)time(nullptr));
-        fin_owner_[id] = {s, i};
-        s->fin_pending++;
-      }
-      if (s->fin_pending == 0) return merge_final(s);
-      kick();
-      return;
-    }
+    // (spread owners included: remote streams' texts sit in their shadow slots)
     std::vector<int> g = good_slots(s);
     bool texts = !cfg_.aggregator_name.empty();
     s->fin_texts = texts;
     s->fin_id = e_submit(g, cfg_.hide_final, texts, "\n" + cfg_.separator, (int64_t)time(nullptr));
     fin_owner_[s->fin_id] = {s, -1};
     kick();
-  }
-  // spread session: every stream's final text is in (local finalize or X_FINAL from a worker)
-  void merge_final(Session* s) {
-    std::vector<std::string> texts;
-    for (auto& b : s->bs)
-      if (b.state == 1 && !b.aborted && b.has_text) texts.push_back(b.ftext);
-    if (texts.empty()) {
-      send_chunk(s, error_event());
-      return finish_stream(s);
-    }
-    if (!cfg_.aggregator_name.empty()) {
-      s->texts = std::move(texts);
-      s->fin_texts = true;
-      return start_aggregator(s, "\n" + cfg_.separator);
-    }
-    std::string j = joined(texts, "\n" + cfg_.separator);
-    std::string ev = final_prefix((int64_t)time(nullptr));
-    escape_append((const uint8_t*)j.data(), j.size(), ev);
-    ev += kFinalSuffix;
-    send_chunk(s, ev);
-    finish_stream(s);
   }
   void post_owner(Session* s, uint8_t type, uint8_t flags, int a, const std::string& payload) {
     if (!xch_) return;
@@ -1874,16 +1873,19 @@ class Loop {
       in.swap(xin_);
     }
     for (auto& m : in) {
+      if (m.type == X_UP) continue;  // a peer (re)joined: new sessions may place streams there
       if (m.type == X_DOWN) {
-        // exchange failed (peer death / timeout): fail remote streams, drop worker streams
+        // peer m.a (or, a = -1, every peer) is unreachable: fail the streams it runs for
+        // our sessions, drop the streams we run for its sessions (a worker whose final
+        // text is in flight waits for X_SENT, which the exchange always sends)
         std::vector<Session*> owners, shadows;
         for (auto& kv : rsess_) owners.push_back(kv.second);
         for (auto& kv : shadow_) shadows.push_back(kv.second);
         for (Session* s : shadows)
-          if (sessions_.count(s)) end_session(s);
+          if (sessions_.count(s) && (m.a < 0 || s->owner_rank == m.a) && !s->bulk_pending) end_session(s);
         for (Session* s : owners) {
           for (int i = 0; i < (int)s->bs.size() && sessions_.count(s); ++i)
-            if (s->bs[i].remote >= 0 && s->bs[i].state == 0)
+            if (s->bs[i].remote >= 0 && (m.a < 0 || s->bs[i].remote == m.a) && s->bs[i].state == 0)
               fail_backend(s, i, 500, "rank exchange failed", "proxy_error");
         }
         continue;
@@ -1910,21 +1912,40 @@ class Loop {
         else s->bs[0].up = u;
         continue;
       }
-      if (m.type == X_CANCEL) {
+      if (m.type == X_CANCEL || m.type == X_SENT) {  // worker side
         auto it = shadow_.find({m.skey, m.bi});
-        if (it != shadow_.end()) end_session(it->second);
+        if (it == shadow_.end()) continue;
+        Session* s = it->second;
+        if (m.type == X_SENT) s->bulk_pending = false;
+        if (!s->bulk_pending) end_session(s);  // a cancel during the transfer ends it at X_SENT
         continue;
       }
       auto it = rsess_.find(m.skey);
       if (it == rsess_.end()) continue;
       Session* s = it->second;
       if (m.bi < 0 || m.bi >= (int)s->bs.size()) continue;
+      BState& b = s->bs[m.bi];
       if (m.type == X_DATA) {
+        b.rx_data++;
         if (s->cl) send_content(s, m.payload);
+        if (b.bulk_waiting && b.rx_data >= b.bulk_msg.b) {
+          b.bulk_waiting = false;
+          XMsg bm = std::move(b.bulk_msg);
+          remote_final(s, m.bi, bm);
+        }
+        continue;
+      }
+      if (m.type == X_BULK) {
+        if (b.state != 0) continue;  // a duplicate (RCCL round failed after delivering)
+        if (b.rx_data < m.b) {  // deltas still in flight on the mesh: apply it after them
+          b.bulk_waiting = true;
+          b.bulk_msg = std::move(m);
+          continue;
+        }
+        remote_final(s, m.bi, m);
         continue;
       }
       if (m.type == X_FINAL) {
-        BState& b = s->bs[m.bi];
         if (b.state != 0) continue;
         if (m.flags & XF_FAILED) {
           fail_backend(s, m.bi, m.a, m.payload, "proxy_error");
@@ -1932,27 +1953,27 @@ class Loop {
         }
         b.state = 1;
         b.aborted = (m.flags & XF_ABORTED) != 0;
-        b.has_text = (m.flags & XF_TEXT) != 0;
-        b.ftext = std::move(m.payload);
         s->finished++;
         if (s->stage == 0 && s->finished == (int)s->bs.size()) begin_final(s);
       }
     }
   }
-  void on_finalized(Session* s, FinalizeRes& f, int bi) {
-    if (s->kind == K_NONSTREAM) return;  // not used
-    if (s->kind == K_REMOTE) {
-      const bool has = !f.texts.empty();
-      post_owner(s, X_FINAL, has ? XF_TEXT : 0, 0, has ? f.texts[0] : std::string());
-      return end_session(s);
-    }
-    if (bi >= 0) {
-      BState& b = s->bs[bi];
-      b.has_text = !f.texts.empty();
-      if (b.has_text) b.ftext = std::move(f.texts[0]);
-      if (--s->fin_pending == 0) merge_final(s);
-      return;
-    }
+  // owner: a remote stream's final text is in (HBM already, or the mesh payload)
+  void remote_final(Session* s, int bi, XMsg& m) {
+    BState& b = s->bs[bi];
+    if (b.state != 0) return;
+    // over the mesh the bytes are in the payload; an RCCL round already wrote them to HBM
+    // (a final text is never empty: an empty one travels as X_FINAL)
+    const bool bytes = !m.payload.empty();
+    eng().set_remote_content(b.slot, bytes ? &m.payload : nullptr, bytes ? m.payload.size() : (size_t)m.a);
+    xch_->forget_bulk(s->skey, bi);
+    b.state = 1;
+    b.aborted = false;
+    s->finished++;
+    if (s->stage == 0 && s->finished == (int)s->bs.size()) begin_final(s);
+  }
+  void on_finalized(Session* s, FinalizeRes& f, int /*bi*/) {
+    if (s->kind == K_NONSTREAM || s->kind == K_REMOTE) return;  // not used
     if (!s->fin_texts) {
       if (f.kind == 1) send_chunk(s, f.event);
       else send_chunk(s, error_event());
@@ -2313,11 +2334,15 @@ class Loop {
         xch_->post(std::move(m));
       }
     }
-    for (auto& b : s->bs) {
+    for (int i = 0; i < (int)s->bs.size(); ++i) {
+      BState& b = s->bs[i];
       if (b.up) {
         drop_up(b.up, false);
         b.up = nullptr;
       }
+      // a shadow slot: no RCCL round may write into it once released (forget_bulk waits
+      // for a copy in progress)
+      if (b.remote >= 0 && xch_ && s->skey) xch_->forget_bulk(s->skey, i);
       if (b.slot >= 0) {
         slot_owner_.erase(b.slot);
         e_release(b.slot);
@@ -2329,10 +2354,6 @@ class Loop {
       s->agg = nullptr;
     }
     if (s->fin_id >= 0) fin_owner_.erase(s->fin_id);
-    for (auto it = fin_owner_.begin(); s->fin_pending > 0 && it != fin_owner_.end();) {
-      if (it->second.first == s) it = fin_owner_.erase(it);
-      else ++it;
-    }
     Client* c = s->cl;
     sessions_.erase(s);
     if (c) {
@@ -2369,10 +2390,19 @@ class Loop {
     h_tick.render(m, "qmx_tick_seconds");
     h_upstream_ttfb.render(m, "qmx_upstream_ttfb_seconds");
     if (xch_) {
-      put("qmx_exchange_rounds_total", (double)xch_->rounds());
-      put("qmx_exchange_bytes_total", (double)xch_->bytes());
+      put("qmx_exchange_rounds_total", (double)xch_->rounds());  // RCCL p2p rounds (final texts)
+      put("qmx_exchange_bytes_total", (double)xch_->bytes());    // mesh payload bytes
+      put("qmx_exchange_messages_total", (double)xch_->msgs());  // mesh messages (control + deltas)
+      put("qmx_exchange_bulk_bytes_total", (double)xch_->bulk_bytes());  // final texts, HBM to HBM
+      put("qmx_exchange_mesh_finals_total", (double)xch_->mesh_bulk());  // final texts over the mesh
+      put("qmx_exchange_epochs_total", (double)xch_->epochs());
+      put("qmx_exchange_rejoins_total", (double)xch_->rejoins());
       put("qmx_exchange_busy_us_total", xch_->busy_us());
       put("qmx_exchange_healthy", xch_->healthy() ? 1.0 : 0.0);
+      put("qmx_exchange_rccl_active", xch_->rccl_active() ? 1.0 : 0.0);
+      int up = 0;
+      for (int r = 0; r < xch_->world(); ++r) up += xch_->peer_up(r);
+      put("qmx_exchange_peers_up", (double)up);
     }
     // engine/kernel stats summed over every io loop's engine (snapshots taken by their tick threads)
     std::map<std::string, double> tot;
@@ -2512,9 +2542,8 @@ int run_server(const ServerCfg& cfg0) {
     o.transport = cfg.xchg;
     o.addr = cfg.xchg_addr;
     o.port = cfg.xchg_port;
-    o.id_file = cfg.xchg_id_file;
     o.device = cfg.device;
-    o.round_us = cfg.xchg_round_us;
+    o.batch_us = cfg.xchg_round_us;
     o.timeout_s = cfg.xchg_timeout;
     std::vector<Loop*> lp;
     for (auto& l : loops) lp.push_back(l.get());

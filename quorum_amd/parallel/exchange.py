@@ -2,17 +2,21 @@
 
 With ``runtime.placement: spread`` a session's N backend streams run on ranks
 owner..owner+N-1 (mod world) — the expert-parallel analog of quorum's backend fan-out
-(``oai_proxy.py:547-550``) — and the worker ranks send deltas and final texts back to the
-owner through lock-step all-gather rounds (``csrc/qmx_exchange.cpp``):
+(``oai_proxy.py:547-550``).  The exchange (``csrc/qmx_exchange.cpp``) has two planes, both
+event-driven (an idle node exchanges nothing):
 
-* ``rccl``: ``ncclAllGather`` over xGMI on a dedicated HIP stream, a fixed-size slot per
-  rank plus a padded second phase for larger rounds (one collective per round, never per
-  session: KB payloads are latency-bound on the per-link-bound ring);
-* ``tcp``: the same protocol over a localhost TCP hub (CPU-only tests, no GPU).
+* mesh: one TCP connection per rank pair (rank r listens on ``QMX_XCHG_PORT + r``) for
+  control messages and the encoded SSE deltas — point to point, never on a collective,
+  because they sit on the TTFT path; a restarted rank re-joins by redialling;
+* bulk (``rccl``): each stream's final text moves from the worker's HBM content arena into
+  the owner's HBM shadow slot with ``ncclSend``/``ncclRecv`` over xGMI, in rounds rank 0
+  orders (so both ends of every pair post matching operations), and the owner's fused
+  finalize kernel merges remote and local texts.  ``tcp`` (CPU tests) moves the bytes over
+  the mesh instead, as does ``rccl`` while its communicator is (re)forming.
 
-Every rank must agree on the transport, the rendezvous port and the RCCL unique-id file:
-:func:`exchange_env` builds them once (launcher / bench) and :func:`cluster_config` turns
-them into the native server's settings.
+Every rank must agree on the transport and the mesh base port: :func:`exchange_env` builds
+them once (launcher / bench) and :func:`cluster_config` turns them into the native
+server's settings.
 """
 from __future__ import annotations
 
@@ -24,9 +28,9 @@ from .topology import RankEnv
 
 
 def exchange_env(rank: int, world: int, port: int, nonce: Optional[str] = None) -> Dict[str, str]:
-    """Environment for rank ``rank`` of a ``world``-rank node serving on ``port``.  The nonce
-    keys the RCCL unique-id file, so concurrent deployments on one host never collide; all
-    ranks of one deployment must get the same nonce."""
+    """Environment for rank ``rank`` of a ``world``-rank node serving on ``port``: the mesh
+    listens on ``port + 7 + rank``.  The nonce names the deployment (all ranks of one
+    deployment get the same one)."""
     return {"QMX_RANK": str(rank), "QMX_WORLD": str(world), "QMX_XCHG_NONCE": nonce or str(time.time_ns()),
             "QMX_XCHG_PORT": str(port + 7)}
 
@@ -49,7 +53,8 @@ def cluster_config(placement: str, exchange: str, round_us: int, timeout: float,
         "rank": r.rank, "world": r.world, "placement": placement, "xchg": xchg,
         "xchg_addr": e.get("QMX_XCHG_ADDR", "127.0.0.1"),
         "xchg_port": int(e.get("QMX_XCHG_PORT", str(port + 7))),
-        "xchg_id_file": e.get("QMX_XCHG_ID_FILE", f"/tmp/qmx_xchg_{port}_{nonce}.id"),
+        "xchg_id_file": "",  # the RCCL unique id travels over the mesh (rank 0 → all)
+        # rank 0 batches bulk announcements arriving within this window into one round
         "xchg_round_us": int(e.get("QMX_XCHG_ROUND_US", str(round_us))),
         "xchg_timeout": float(e.get("QMX_XCHG_TIMEOUT", str(timeout))),
     }

@@ -25,6 +25,30 @@ def free_port() -> int:
     return p
 
 
+def free_port_block(n: int) -> int:
+    """Base of n consecutive bindable ports, below the ephemeral range (the exchange mesh
+    listens on base + rank; an ephemeral base would collide with sockets the kernel hands
+    out next, e.g. to tests running in parallel)."""
+    import random
+
+    rng = random.Random()
+    for _ in range(200):
+        base = rng.randrange(20000, 30000 - n)
+        socks = []
+        try:
+            for k in range(n):
+                s = socket.socket()
+                s.bind(("127.0.0.1", base + k))
+                socks.append(s)
+            return base
+        except OSError:
+            continue
+        finally:
+            for s in socks:
+                s.close()
+    raise RuntimeError("no free port block")
+
+
 class _Handler(BaseHTTPRequestHandler):
     protocol_version = "HTTP/1.1"
 

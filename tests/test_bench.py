@@ -18,9 +18,20 @@ KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "
 
 
 def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    """A bench base port below the ephemeral range: the bench also binds base + 7.. (mesh),
+    base + 50.. (spread check) and base + 100.. (mocks)."""
+    import random
+
+    for _ in range(200):
+        base = random.randrange(20000, 29000)
+        try:
+            for off in (0, 7, 8, 50, 57, 58, 100, 101, 110, 111):
+                with socket.socket() as s:
+                    s.bind(("127.0.0.1", base + off))
+            return base
+        except OSError:
+            continue
+    raise RuntimeError("no free port block")
 
 
 def _env():

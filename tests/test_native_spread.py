@@ -21,7 +21,7 @@ import pytest
 from quorum_amd.ops import native
 
 from conftest import cfg_parallel, completion, sse_chunk, sse_stream
-from live_upstream import LiveUpstream, free_port, native_server
+from live_upstream import LiveUpstream, free_port, free_port_block, native_server
 
 pytestmark = pytest.mark.skipif(not native.available(), reason="native extension not built")
 
@@ -46,7 +46,7 @@ def native_cluster(cfg, world: int, placement: str = "spread"):
     cfg = copy.deepcopy(cfg)
     cfg.setdefault("runtime", {})["placement"] = placement
     ports = [free_port() for _ in range(world)]
-    xport = free_port()
+    xport = free_port_block(world)  # the mesh: rank r listens on xport + r
     threads = []
     for r in range(world):
         env = {"QMX_RANK": str(r), "QMX_WORLD": str(world), "QMX_XCHG": "tcp", "QMX_XCHG_PORT": str(xport),
@@ -72,6 +72,14 @@ def native_cluster(cfg, world: int, placement: str = "spread"):
                 if httpx.get(f"http://127.0.0.1:{p}/health", timeout=1).status_code == 200:
                     break
             except httpx.HTTPError:
+                time.sleep(0.02)
+    if placement == "spread":  # sessions spread only once every rank's mesh is complete
+        for p in ports:
+            t0 = time.time()
+            while time.time() - t0 < 20:
+                m = httpx.get(f"http://127.0.0.1:{p}/metrics").text
+                if f"qmx_exchange_peers_up {float(world):f}" in m and "qmx_exchange_healthy 1.000000" in m:
+                    break
                 time.sleep(0.02)
     try:
         yield ports
@@ -199,7 +207,7 @@ def test_exchange_transport_selftest_tcp():
     """Raw transport: 3 ranks, 60 all-gather rounds with payloads below and above the fixed
     first-phase slot; every rank must receive every rank's exact bytes and flags."""
     ext = native.require()
-    port = free_port()
+    port = free_port_block(3)
     res = {}
 
     def run(r):
@@ -210,3 +218,37 @@ def test_exchange_transport_selftest_tcp():
     for t in ts:
         t.join(timeout=60)
     assert len(res) == 3 and all(v["ok"] for v in res.values()), res
+
+
+def test_idle_cluster_exchanges_nothing():
+    """Event-driven exchange: once the traffic stops, a 3-rank cluster sends no mesh message
+    and runs no bulk round (the r1 design paced all-gather rounds forever)."""
+    behs = [("stream", 200, sse_stream(["x"])), ("stream", 200, sse_stream(["y"])), ("stream", 200, sse_stream(["z"]))]
+    live, ports = _live({f"b{i + 1}": b for i, b in enumerate(behs)})
+    try:
+        cfg = _cfg(3, CONCAT, "concatenate", [f"http://127.0.0.1:{ports[f'b{i + 1}']}/v1" for i in range(3)])
+        req = {"messages": MSG, "stream": True}
+
+        def snap(cports):
+            tot = {}
+            for p in cports:
+                for ln in httpx.get(f"http://127.0.0.1:{p}/metrics").text.splitlines():
+                    if ln.startswith("qmx_exchange_"):
+                        k, v = ln.split()
+                        tot[k] = tot.get(k, 0.0) + float(v)
+            return tot
+
+        with native_cluster(cfg, 3) as cports:
+            for p in cports:
+                assert httpx.post(f"http://127.0.0.1:{p}/chat/completions", json=req, headers=AUTH,
+                                  timeout=30).status_code == 200
+            time.sleep(0.3)
+            a = snap(cports)
+            time.sleep(1.0)
+            b = snap(cports)
+        assert a["qmx_exchange_messages_total"] > 0  # the traffic did use the mesh
+        assert b["qmx_exchange_messages_total"] == a["qmx_exchange_messages_total"], (a, b)
+        assert b["qmx_exchange_rounds_total"] == a["qmx_exchange_rounds_total"] == 0  # tcp: no RCCL rounds
+        assert b["qmx_exchange_peers_up"] == 9  # 3 ranks x 3
+    finally:
+        live.close()

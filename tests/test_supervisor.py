@@ -19,7 +19,7 @@ import yaml
 from quorum_amd.ops import native
 
 from conftest import cfg_parallel, sse_stream
-from live_upstream import LiveUpstream, free_port
+from live_upstream import LiveUpstream, free_port, free_port_block
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 AUTH = {"Authorization": "Bearer k"}
@@ -186,7 +186,7 @@ def test_launcher_two_ranks_spread(tmp_path):
     with open(cfg, "w") as f:
         yaml.safe_dump(c, f)
     port = free_port()
-    env = dict(os.environ, PYTHONPATH=ROOT, QMX_XCHG_PORT=str(free_port()))
+    env = dict(os.environ, PYTHONPATH=ROOT, QMX_XCHG_PORT=str(free_port_block(2)))
     env.pop("QMX_RANK", None)
     sup = subprocess.Popen([sys.executable, "-m", "quorum_amd.serve", "--impl", "native", "--engine", "cpu",
                             "--gpus", "2", "--config", cfg, "--port", str(port), "--threads", "1"], cwd=ROOT,
@@ -229,7 +229,7 @@ def test_rank_death_survivors_keep_serving(tmp_path):
     with open(cfg, "w") as f:
         yaml.safe_dump(c, f)
     port = free_port()
-    env = dict(os.environ, PYTHONPATH=ROOT, QMX_XCHG_PORT=str(free_port()))
+    env = dict(os.environ, PYTHONPATH=ROOT, QMX_XCHG_PORT=str(free_port_block(2)))
     env.pop("QMX_RANK", None)
     sup = subprocess.Popen([sys.executable, "-m", "quorum_amd.serve", "--impl", "native", "--engine", "cpu",
                             "--gpus", "2", "--config", cfg, "--port", str(port), "--threads", "1"], cwd=ROOT,
@@ -268,6 +268,80 @@ def test_rank_death_survivors_keep_serving(tmp_path):
         assert len(finals) - n_before > 5
     finally:
         stop.set()
+        os.kill(sup.pid, signal.SIGTERM)
+        try:
+            sup.wait(timeout=40)
+        except subprocess.TimeoutExpired:
+            os.killpg(sup.pid, signal.SIGKILL)
+        live.close()
+
+
+def test_rank_restart_exchange_reforms(tmp_path):
+    """SURVEY §5.3 re-join: rank 1's worker is killed, its supervisor restarts it, the new
+    process dials the mesh again (the higher rank redials) and spread placement resumes —
+    streams run on rank 1 again, rank 0 counts the re-join, and every answer is complete."""
+    if not native.available():
+        pytest.skip("native extension not built")
+    live = LiveUpstream()
+    pa = live.serve("a", ("stream", 200, sse_stream(["AAA"])))
+    pb = live.serve("b", ("stream", 200, sse_stream(["BBB"])))
+    cfg = str(tmp_path / "config.yaml")
+    _write(cfg, [f"http://127.0.0.1:{pa}/v1", f"http://127.0.0.1:{pb}/v1"])
+    with open(cfg) as f:
+        c = yaml.safe_load(f)
+    c["runtime"]["placement"] = "spread"
+    with open(cfg, "w") as f:
+        yaml.safe_dump(c, f)
+    port = free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT, QMX_XCHG_PORT=str(free_port_block(2)))
+    env.pop("QMX_RANK", None)
+    sup = subprocess.Popen([sys.executable, "-m", "quorum_amd.serve", "--impl", "native", "--engine", "cpu",
+                            "--gpus", "2", "--config", cfg, "--port", str(port), "--threads", "1"], cwd=ROOT,
+                           env=env, start_new_session=True)
+
+    def metric(text, name):
+        for ln in text.splitlines():
+            if ln.startswith(name + " "):
+                return float(ln.split()[1])
+        return 0.0
+
+    def scrape_all(n=12):  # the shared port answers from either rank
+        out = []
+        for _ in range(n):
+            with httpx.Client() as cl:  # a fresh connection: another SO_REUSEPORT pick
+                out.append(cl.get(f"http://127.0.0.1:{port}/metrics").text)
+        return out
+
+    try:
+        _wait(port, lambda r: _final(r.text) == "AAA\n\n--\nBBB")
+        t0 = time.time()  # both ranks up and meshed before the kill
+        while not all(metric(m, "qmx_exchange_peers_up") == 2 for m in scrape_all(6)):
+            assert time.time() - t0 < 30, "mesh never formed"
+            time.sleep(0.2)
+        ranks = subprocess.run(["pgrep", "-P", str(sup.pid)], capture_output=True, text=True).stdout.split()
+        assert len(ranks) == 2
+        victims = subprocess.run(["pgrep", "-P", ranks[1]], capture_output=True, text=True).stdout.split()
+        assert victims
+        for v in victims:
+            os.kill(int(v), signal.SIGKILL)
+        # the restarted worker re-joins: both ranks see 2 peers up, rank 0 counted a re-join
+        t0 = time.time()
+        while time.time() - t0 < 30:
+            ms = scrape_all(6)
+            if all(metric(m, "qmx_exchange_peers_up") == 2 for m in ms) and \
+                    max(metric(m, "qmx_exchange_rejoins_total") for m in ms) >= 1:
+                break
+            time.sleep(0.3)
+        else:
+            raise AssertionError("exchange did not re-form")
+        for _ in range(40):
+            r = _post(port)
+            assert r.status_code == 200 and _final(r.text) == "AAA\n\n--\nBBB"
+        # streams are spread onto the new rank-1 process again (its own counter starts at 0)
+        ms = scrape_all()
+        assert all(metric(m, "qmx_remote_streams_total") >= 1 for m in ms), [metric(m, "qmx_remote_streams_total")
+                                                                             for m in ms]
+    finally:
         os.kill(sup.pid, signal.SIGTERM)
         try:
             sup.wait(timeout=40)
