@@ -223,9 +223,10 @@ PYBIND11_MODULE(_qmx, m) {
       });
       // sinks first: a bulk that finds no sink is dropped
       std::map<std::pair<int, int>, void*> sinks;
+      const bool loop1 = o.world == 1;  // one rank: everything goes to itself (RCCL send/recv to self)
       for (int r = 0; r < rounds; ++r)
         for (int src = 0; src < o.world; ++src) {
-          if (src == o.rank) continue;
+          if (src == o.rank && !loop1) continue;
           const size_t n = payload(r, src, o.rank, 1).size();
           void* p = dev ? dalloc(n) : nullptr;
           sinks[{r, src}] = p;
@@ -243,7 +244,7 @@ PYBIND11_MODULE(_qmx, m) {
       const auto t1 = std::chrono::steady_clock::now();
       for (int r = 0; r < rounds && ok; ++r)
         for (int p = 0; p < o.world; ++p) {
-          if (p == o.rank) continue;
+          if (p == o.rank && !loop1) continue;
           XMsg m;
           m.type = X_DATA;
           m.dst_rank = p;
@@ -266,7 +267,7 @@ PYBIND11_MODULE(_qmx, m) {
           h.flags = XF_TEXT;
           x.send_bulk(std::move(h), src, b.size(), [b] { return b; });
         }
-      const int want = rounds * (o.world - 1);
+      const int want = rounds * (loop1 ? 1 : o.world - 1);
       {
         std::unique_lock<std::mutex> lk(mu);
         while (ok) {

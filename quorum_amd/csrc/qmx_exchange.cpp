@@ -443,7 +443,7 @@ struct Exchange::Impl {
         continue;
       }
       part[e.src].push_back(e);
-      part[e.dst].push_back(e);
+      if (e.dst != e.src) part[e.dst].push_back(e);  // (loopback: one entry, both halves)
     }
     ann.clear();
     for (auto& kv : part) {
@@ -860,7 +860,8 @@ void Exchange::bulk_loop() {
         ncclResult_t r = ncclSend(src, e.len, ncclUint8, e.dst, comm, st);
         ok = r == ncclSuccess || r == ncclInProgress;
         my_sends.emplace_back(&e, std::move(s));
-      } else if (e.dst == o_.rank) {
+      }
+      if (ok && e.dst == o_.rank) {  // (a loopback entry — self-test — has both halves here)
         // into this rank's staging area (one slot per receive of the round): the owner may
         // release the destination slot while the round is in flight; the copy into its HBM
         // content slot happens under the sink lock once the data is here
