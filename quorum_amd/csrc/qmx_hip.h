@@ -36,6 +36,16 @@ struct DevSlot {
   uint8_t tail[kMaxTail];
 };
 
+// Per-backend event shape template (cross-stream): written by the first workgroup of a
+// launch that parses a content event of that backend index, read by the lane's next launch
+constexpr int kBackendTpl = 16;  // backend indices with a table entry
+struct BackendTpl {
+  alignas(16) uint8_t tpl[kTplBytes];
+  uint16_t pre, suf;  // 0: none yet
+  uint32_t claim;     // launch sequence number of the last writer
+  uint32_t pad[2];
+};
+
 enum WorkFlags : uint32_t { WF_EOF = 1, WF_FILTER = 2, WF_EMIT = 4, WF_STARTED = 8, WF_FRESH = 16 };
 enum WorkStatus : uint32_t { WS_DONE = 1, WS_ABORTED = 2, WS_STARTED = 4, WS_ESCALATE = 8, WS_MORE = 16 };
 
@@ -83,6 +93,11 @@ struct TickLane {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evb = nullptr;
   KParams params;
+  KParams* d_params = nullptr;  // device copy read by the kernel
+  BackendTpl* d_btpl = nullptr;  // [2][kBackendTpl]: launch parity double buffer
+  KParams* h_params = nullptr;  // pinned staging for its upload
+  int64_t params_created = -1;
+  bool params_dirty = true;
   uint8_t* h_in = nullptr;
   size_t in_cap = 0;
   uint8_t* h_out = nullptr;

@@ -313,7 +313,8 @@ struct TickShared {
 __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, const uint8_t* __restrict__ in,
                                           uint8_t* __restrict__ out, WorkResult* __restrict__ res,
                                           DevSlot* __restrict__ state, uint8_t* __restrict__ content,
-                                          const KParams& Pk, TickShared& U) {
+                                          const KParams& Pk, TickShared& U, const BackendTpl* __restrict__ btpl_rd,
+                                          BackendTpl* __restrict__ btpl_wr, uint32_t seq) {
   Smem& s = U.s;
   KParams& P = U.P;
   auto& TKP = U.TKP;
@@ -345,15 +346,28 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     if (fresh) {
       s.v[V_DEPTH0] = 0;
       s.v[V_TAILLEN] = 0;
-      s.v[V_TPLPRE] = s.v[V_TPLSUF] = 0;
     } else {
       s.v[V_DEPTH0] = state[it.slot].depth;
       s.v[V_TAILLEN] = state[it.slot].tail_len;
-      s.v[V_TPLPRE] = state[it.slot].tpl_pre;
-      s.v[V_TPLSUF] = state[it.slot].tpl_suf;
     }
   }
-  if (!fresh && tid < TPL_BYTES / 16) ((uint4*)s.tpl)[tid] = ((const uint4*)state[it.slot].tpl)[tid];
+  // Event shape template: the stream's own (earlier ticks), else its backend's — published
+  // by any stream of the same backend index in this lane's previous launch (a fresh burst
+  // of a new session then matches its content events at once instead of lexing the first
+  // ones; a template is only ever a real parsed event's bytes around its content string,
+  // and a match re-validates the string, so whose it is never changes a result)
+  const bool own_tpl = !fresh && state[it.slot].tpl_pre != 0;
+  const BackendTpl* bt = (!own_tpl && btpl_rd != nullptr && it.index < (uint32_t)kBackendTpl)
+                             ? &btpl_rd[it.index] : nullptr;
+  const bool borrow = bt != nullptr && bt->pre != 0;
+  if (tid == 0) {
+    s.v[V_TPLPRE] = own_tpl ? state[it.slot].tpl_pre : borrow ? bt->pre : 0;
+    s.v[V_TPLSUF] = own_tpl ? state[it.slot].tpl_suf : borrow ? bt->suf : 0;
+  }
+  if (tid < TPL_BYTES / 16) {
+    if (own_tpl) ((uint4*)s.tpl)[tid] = ((const uint4*)state[it.slot].tpl)[tid];
+    else if (borrow) ((uint4*)s.tpl)[tid] = ((const uint4*)bt->tpl)[tid];
+  }
   __syncthreads();
   QMX_STAMP(1);
   const int tail_len = filt ? s.v[V_TAILLEN] : 0;
@@ -623,6 +637,31 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       if (tid == 0) {
         ds.tpl_pre = (uint16_t)pre;
         ds.tpl_suf = (uint16_t)suf;
+      }
+      // publish it for this backend index: the first workgroup of the launch to claim the
+      // entry writes it; the lane's next launch reads it (a kernel boundary in between)
+      int won = 0;
+      if (tid == 0 && btpl_wr != nullptr && it.index < (uint32_t)kBackendTpl) {
+        uint32_t* claim = &btpl_wr[it.index].claim;
+        uint32_t old = __hip_atomic_load(claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        won = old != seq && atomicCAS(claim, old, seq) == old;
+      }
+      won = __syncthreads_or(won);
+      if (won) {
+        BackendTpl& bw = btpl_wr[it.index];
+        if (tid < pre) bw.tpl[tid] = s.A[e0 + tid];
+        if (tid < suf) bw.tpl[TPL_PRE_MAX + tid] = s.A[e1 - suf + tid];
+        if (tid == 0) {
+          bw.pre = (uint16_t)pre;
+          bw.suf = (uint16_t)suf;
+        }
+      }
+    } else if (borrow) {  // keep the backend's template as the stream's own
+      DevSlot& ds = state[it.slot];
+      if (tid < TPL_BYTES / 16) ((uint4*)ds.tpl)[tid] = ((const uint4*)s.tpl)[tid];
+      if (tid == 0) {
+        ds.tpl_pre = (uint16_t)s.v[V_TPLPRE];
+        ds.tpl_suf = (uint16_t)s.v[V_TPLSUF];
       }
     } else if (fresh && tid == 0) {
       state[it.slot].tpl_pre = state[it.slot].tpl_suf = 0;
@@ -997,12 +1036,13 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       const int w1 = min(w0 + WIN, out_len);
       // envelopes: fully parallel over (emitted event, envelope byte)
       {
-        char dg[3];
-        int v = it.index;
-        for (int i = ndig - 1; i >= 0; --i) {
-          dg[i] = (char)('0' + v % 10);
-          v /= 10;
-        }
+        // the index digits, most significant first, as registers (a local array indexed by
+        // a loop variable lands in scratch)
+        const int ix = (int)it.index;
+        const uint32_t dg_packed = ndig == 1 ? (uint32_t)('0' + ix)
+                                 : ndig == 2 ? (uint32_t)('0' + ix / 10) | ((uint32_t)('0' + ix % 10) << 8)
+                                             : (uint32_t)('0' + ix / 100) | ((uint32_t)('0' + (ix / 10) % 10) << 8) |
+                                                   ((uint32_t)('0' + ix % 10) << 16);
         for (int idx = tid; idx < n_emit * EVL; idx += BS) {
           int k = idx / EVL, bpos = idx - k * EVL;
           int j = s.ejx[k];
@@ -1011,7 +1051,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
           if (bpos < PRE) {
             o = k * EVL + (j ? (int)s.epos[j - 1] : 0) + bpos;
             ch = bpos < P.pre1_len ? (uint8_t)P.pre1[bpos]
-                 : bpos < P.pre1_len + ndig ? (uint8_t)dg[bpos - P.pre1_len]
+                 : bpos < P.pre1_len + ndig ? (uint8_t)(dg_packed >> (8 * (bpos - P.pre1_len)))
                                             : (uint8_t)P.pre2[bpos - P.pre1_len - ndig];
           } else {
             o = k * EVL + PRE + (int)s.epos[j] + (bpos - PRE);
@@ -1374,12 +1414,17 @@ union TickLds {
 __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict__ items,
                                                       const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                       WorkResult* __restrict__ res, DevSlot* __restrict__ state,
-                                                      uint8_t* __restrict__ content, KParams Pk, uint32_t seq,
-                                                      uint32_t n_tick, FinArgs fa) {
+                                                      uint8_t* __restrict__ content, const KParams* __restrict__ Pkp,
+                                                      uint32_t seq, uint32_t n_tick, FinArgs fa,
+                                                      const BackendTpl* __restrict__ btpl_rd,
+                                                      BackendTpl* __restrict__ btpl_wr) {
   __shared__ TickLds U;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  // tag patterns, MFMA B operand and SSE envelopes: in device memory (uploaded by the lane
+  // when they change, ~once a second), not a 1.5 KB by-value kernel argument per launch
+  const KParams& Pk = *Pkp;
   if (blockIdx.x < n_tick) {
-    tick_body(items, in, out, res, state, content, Pk, U.t);
+    tick_body(items, in, out, res, state, content, Pk, U.t, btpl_rd, btpl_wr, seq);
     if (threadIdx.x == 0) {
       res[blockIdx.x].t0 = t0;
       res[blockIdx.x].t1 = __builtin_amdgcn_s_memrealtime();
@@ -1523,6 +1568,10 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
     HIP_CHECK(hipEventCreate(&L->ev1));
     HIP_CHECK(hipEventCreateWithFlags(&L->evb, hipEventBlockingSync | hipEventDisableTiming));
     L->params = base_params_;
+    HIP_CHECK(hipMalloc((void**)&L->d_params, sizeof(KParams)));
+    HIP_CHECK(hipMalloc((void**)&L->d_btpl, sizeof(BackendTpl) * 2 * kBackendTpl));
+    HIP_CHECK(hipMemset(L->d_btpl, 0, sizeof(BackendTpl) * 2 * kBackendTpl));
+    HIP_CHECK(hipHostMalloc((void**)&L->h_params, sizeof(KParams), hipHostMallocDefault));
     ensure_in(*L, 8u << 20);
     ensure_out(*L, 32u << 20);
     L->items_cap = 4096;
@@ -1542,6 +1591,9 @@ HipEngine::~HipEngine() {
     if (L->h_items) hipHostFree(L->h_items);
     if (L->h_res) hipHostFree(L->h_res);
     if (L->h_dbg) hipHostFree(L->h_dbg);
+    if (L->d_params) hipFree(L->d_params);
+    if (L->d_btpl) hipFree(L->d_btpl);
+    if (L->h_params) hipHostFree(L->h_params);
     if (L->h_fin) hipHostFree(L->h_fin);
     if (L->h_finres) hipHostFree(L->h_finres);
     if (L->h_fint) hipHostFree(L->h_fint);
@@ -1751,7 +1803,12 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
   const std::vector<const FinalizeReq*> fin_gpu = prep_finalize(L, fin, fin_host);
   const int m = (int)fin_gpu.size();
   if (n + m > 0) {
-    build_params(L, created);
+    if (created != L.params_created) {  // envelopes carry the second: rebuilt + uploaded once a second
+      build_params(L, created);
+      L.params_created = created;
+      L.params_dirty = true;
+    }
+    unsigned long long* const dbg0 = L.params.dbg;
     L.params.dbg = nullptr;
     if (getenv("QMX_STAGE_TIMING")) {
       if (L.dbg_cap < (size_t)n) {
@@ -1762,6 +1819,12 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
       std::memset(L.h_dbg, 0, sizeof(unsigned long long) * kDbg * n);
       L.params.dbg = L.h_dbg;
     }
+    if (L.params.dbg != dbg0) L.params_dirty = true;
+    if (L.params_dirty) {  // stream-ordered before the launch; the pinned copy is not touched
+      std::memcpy(L.h_params, &L.params, sizeof(KParams));  // again until this tick completed
+      HIP_CHECK(hipMemcpyAsync(L.d_params, L.h_params, sizeof(KParams), hipMemcpyHostToDevice, L.stream));
+      L.params_dirty = false;
+    }
     const auto tp1 = HC::now();
     L.host_prep_us += std::chrono::duration<double, std::micro>(tp1 - tp0).count();
     roctxRangePushA("qmx_tick");  // rocprofv3 --marker-trace: one range per tick launch + wait
@@ -1770,7 +1833,8 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
     if (!poll_) HIP_CHECK(hipEventRecord(L.ev0, L.stream));
     FinArgs fa{L.h_fin, L.h_fint, L.h_fin_in, L.d_join, L.d_fout, L.h_fout, L.h_finres, L.h_tl, (int2*)L.d_segs};
     hipLaunchKernelGGL(qmx_tick_kernel, dim3(n + m), dim3(BS), 0, L.stream, L.h_items, L.h_in, L.h_out, L.h_res,
-                       d_state_, d_content_, L.params, seq, (uint32_t)n, fa);
+                       d_state_, d_content_, L.d_params, seq, (uint32_t)n, fa,
+                       L.d_btpl + (size_t)((seq - 1) & 1) * kBackendTpl, L.d_btpl + (size_t)(seq & 1) * kBackendTpl);
     HIP_CHECK(hipGetLastError());
     // sessions the GPU does not finalize (escalated streams) are finalized here meanwhile
     for (const FinalizeReq* r : fin_host) finalize_host(*r, fres);

@@ -179,6 +179,7 @@ std::string chunk_event_json(const char* id, int64_t created, const std::string&
 struct RespParser {
   int phase = 0;  // 0 headers, 1 length body, 2 chunk size, 3 chunk data, 4 chunk crlf, 5 trailers, 6 until close, 7 done
   int status = 0;
+  bool keep_headers = true;  // engine-fed streams need only status + framing (no per-header strings)
   std::vector<std::pair<std::string, std::string>> headers;
   long remaining = 0;
   bool close = false;
@@ -207,7 +208,7 @@ struct RespParser {
             remaining = atol(v.c_str());
           }
           if (k == "connection" && ieq(v, "close")) close = true;
-          headers.emplace_back(std::move(k), std::move(v));
+          if (keep_headers) headers.emplace_back(std::move(k), std::move(v));
         });
         if (status == 204 || status == 304) phase = 7;
         else if (chunked) phase = 2;
@@ -346,6 +347,10 @@ struct Session {
   std::vector<std::string> texts;
   Up* agg = nullptr;
   // single-stream passthrough
+  // body with "model" replaced = mpre + dumps(model) + mpost (built once per request,
+  // reused for every backend whose config model overrides the request's)
+  bool msplit = false;
+  std::string mpre, mpost;
   std::string first_buf;
   bool first_decided = false, saw_done = false, pass_started = false;
   std::string done_tail;
@@ -1002,6 +1007,9 @@ class Loop {
         ssize_t r = recv(c->fd, buf, sizeof(buf), 0);
         if (r > 0) {
           c->in.append(buf, r);
+          // a short read drained the socket: epoll is level-triggered, so skip the recv
+          // that would only return EAGAIN (one syscall per request saved)
+          if (r < (ssize_t)sizeof(buf)) break;
           continue;
         }
         if (r == 0 || (errno != EAGAIN && errno != EWOULDBLOCK)) c->dead = true;
@@ -1284,9 +1292,36 @@ class Loop {
       return false;
     }
     if (!be.model.empty()) {
-      JVal j = s->body;
-      j.set("model", JVal::str(be.model));
-      out = json_dumps(j);
+      // json.dumps of the body after body["model"] = model (quorum :161-163): the key keeps
+      // its position, a new key goes last — serialised once per request around the value
+      if (!s->msplit) {
+        s->msplit = true;
+        const auto& items = s->body.o;
+        size_t k = 0;
+        while (k < items.size() && items[k].first != "model") ++k;
+        std::string& pre = s->mpre;
+        pre.reserve(s->raw.size() + 32);
+        pre.push_back('{');
+        for (size_t i = 0; i < k; ++i) {
+          if (i) pre += ", ";
+          json_dump_str(items[i].first, pre);
+          pre += ": ";
+          json_dump(items[i].second, pre);
+        }
+        if (k > 0) pre += ", ";
+        pre += "\"model\": ";
+        for (size_t i = k + 1; i < items.size(); ++i) {
+          s->mpost += ", ";
+          json_dump_str(items[i].first, s->mpost);
+          s->mpost += ": ";
+          json_dump(items[i].second, s->mpost);
+        }
+        s->mpost.push_back('}');
+      }
+      out.reserve(s->mpre.size() + be.model.size() + s->mpost.size() + 8);
+      out = s->mpre;
+      json_dump_str(be.model, out);
+      out += s->mpost;
       return true;
     }
     if (!s->body.get("model")) {
@@ -1324,6 +1359,7 @@ class Loop {
     u->sess = s;
     u->bi = bi;
     u->mode = mode;
+    u->rp.keep_headers = mode != UP_ENGINE;
     u->req = std::move(req);
     u->timeout = timeout;
     u->last_io = now_s();
@@ -1490,6 +1526,10 @@ class Loop {
             c_fail_protocol++;
             return up_error(u, "invalid HTTP response");
           }
+          // plain TCP, short read: drained (level-triggered epoll reports more data); a
+          // complete response needs no EAGAIN probe either.  TLS keeps reading: its
+          // records can sit decrypted inside the SSL object with the socket empty.
+          if (!u->ssl && (r < (ssize_t)sizeof(buf) || u->rp.done())) break;
           continue;
         }
         if (r < 0) eof = true;
@@ -1616,7 +1656,7 @@ class Loop {
     int status = u->rp.status;
     UpMode mode = u->mode;
     std::string body = std::move(u->body);
-    auto rh = u->rp.headers;
+    auto rh = std::move(u->rp.headers);
     drop_up(u, reusable);
     if (bi >= 0) s->bs[bi].up = nullptr;
     else s->agg = nullptr;
@@ -1744,9 +1784,15 @@ class Loop {
     s->emit = !cfg_.suppress;
     if (const JVal* sup = s->body.get("suppress_individual_responses")) s->emit = !sup->truthy();
     const bool defer = role_defer_s_ > 0 && s->cl && !s->cl->queued && !s->cl->want_out;
-    write_client(s->cl, kSseHdr);
-    send_chunk(s, chunk_event_json("chatcmpl-parallel", (int64_t)time(nullptr), "\"parallel-proxy\"",
-                                   "{\"role\": \"assistant\"}", "null"));
+    // SSE head + chunked role event (quorum :530-541): identical within a second, cached
+    const int64_t now_sec = (int64_t)time(nullptr);
+    if (now_sec != role_sec_) {
+      role_sec_ = now_sec;
+      role_head_ = kSseHdr;
+      role_head_ += chunk(chunk_event_json("chatcmpl-parallel", now_sec, "\"parallel-proxy\"",
+                                           "{\"role\": \"assistant\"}", "null"));
+    }
+    write_client(s->cl, role_head_);
     if (defer && s->cl->queued && !flushq_.empty() && flushq_.back() == s->cl->fd) {
       flushq_.pop_back();  // un-queue: the first content (or the deadline) sends it
       s->cl->queued = false;
@@ -2469,6 +2515,8 @@ class Loop {
     return (e ? atof(e) : 1000.0) * 1e-6;
   }();
   std::vector<EngineOp> ops_;  // engine feed / finish / release of this iteration (flush_ops)
+  int64_t role_sec_ = -1;      // second of the cached SSE head + role event
+  std::string role_head_;
   // fault injection (tests): drop every Nth stream result's SSE bytes before it is sent
   const long fault_drop_every_ = [] {
     const char* e = getenv("QMX_FAULT_DROP_DELTA");

@@ -95,7 +95,8 @@ for step in "$@"; do
       timeout -s KILL 120 rocprofv3 --pmc ${ctr//,/ } -d $OUT/pmc_$slug -o pmc --output-format csv -- \
         python3 tools/kbench.py --slots 256 --iters 10 > $OUT/pmc_$slug.log 2>&1 \
         || { echo "pmc $ctr failed"; tail -10 $OUT/pmc_$slug.log; exit 1; }
-      python3 tools/pmc_summary.py $OUT/pmc_$slug > $OUT/pmc_$slug.md 2>&1; cat $OUT/pmc_$slug.md | head -30 ;;
+      python3 tools/pmc_summary.py $(find $OUT/pmc_$slug -name '*counter_collection.csv') > $OUT/pmc_$slug.md 2>&1
+      grep -v rocclr $OUT/pmc_$slug.md | head -30 ;;
     kbench)
       QMX_STAGE_TIMING=1 timeout -k 10 300 python tools/kbench.py --slots 1,22,64,256 --iters 20 > $OUT/kbench.jsonl 2>&1 \
         || { echo "kbench failed"; tail -5 $OUT/kbench.jsonl; exit 1; }
@@ -111,7 +112,7 @@ for l in open('$OUT/kbench.jsonl'):
     spread=*)
       n=${step#spread=}; QMX_XCHG=tcp torchrun_bench spread_$n $n --steps 5 --warmup 1 --threads 4 --placement spread || exit 1 ;;
     cpuprof)
-      bench cpuprof 300 QMX_PROF=$PWD/$OUT/cpu_hip.%p.txt -- --steps 20 --warmup 2 || exit 1
+      bench cpuprof 300 QMX_PROF=$PWD/$OUT/cpu_hip.%p.txt QMX_PROF_US=100 -- --steps 20 --warmup 2 || exit 1
       for f in $OUT/cpu_hip.*.txt; do python3 tools/cpuprof.py $f --top 30 --json $f.json > $f.summary 2>&1 || true; done
       head -30 $OUT/cpu_hip.*.summary ;;
     *) echo "unknown step $step"; exit 2 ;;
