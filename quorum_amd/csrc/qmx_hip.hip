@@ -413,7 +413,63 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   QMX_STAMP(2);
 
   // ---- S2: framing -----------------------------------------------------------------
-  {
+  // Common case (8-byte aligned start): each thread takes an 8-byte-multiple chunk with
+  // ds_read_b64 loads and works on a 32-bit newline mask (SWAR byte compare) — byte loops
+  // over stride-C chunks were bank-conflicted LDS reads, three passes over every byte.
+  const int flen0 = in_len - start;
+  const int C8 = (((flen0 + BS - 1) / BS) + 7) & ~7;
+  if ((start & 7) == 0 && C8 <= 32) {
+    const int lo = min(start + tid * C8, in_len), hi = min(lo + C8, in_len);
+    const int len = hi - lo;
+    uint32_t nm = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q * 8 < len) {
+        const uint64_t w = *(const uint64_t*)&s.A[lo + 8 * q];  // A has 64 B of padding
+        const uint64_t x = w ^ 0x0a0a0a0a0a0a0a0aull;
+        const uint64_t y = (((x & 0x7f7f7f7f7f7f7f7full) + 0x7f7f7f7f7f7f7f7full) | x) & 0x8080808080808080ull;
+        const uint64_t zb = ~y & 0x8080808080808080ull;  // high bit of every '\n' byte
+        nm |= (uint32_t)(((zb >> 7) * 0x0102040810204080ull) >> 56) << (8 * q);
+      }
+    }
+    const uint32_t valid = len >= 32 ? 0xffffffffu : ((1u << len) - 1u);
+    nm &= valid;
+    const uint32_t inv = ~nm & valid;
+    const bool all_nl = inv == 0;
+    const int trail = all_nl ? len : len - 32 + __clz(inv);  // newlines at the chunk's end
+    const bool next_nl = hi < in_len && s.A[hi] == '\n';
+    int2 run = all_nl ? make_int2(1, len) : make_int2(0, trail);
+    int2 tot2;
+    int2 ex = block_excl_pair(run, make_int2(1, 0), RunOp(), s.scr, &tot2);
+    // separators: "\n" at an even position of its newline run, followed by a "\n"
+    auto each_sep = [&](auto&& f) {
+      uint32_t m = nm;
+      while (m) {
+        const int r0 = __ffs(m) - 1;
+        const uint32_t rest = ~(m >> r0);
+        const int L = rest == 0 ? 32 - r0 : __ffs(rest) - 1;  // run length in the chunk
+        const int c = r0 == 0 ? ex.y : 0;                     // newlines just before it
+        const bool ext = r0 + L == len && next_nl;            // the run continues past lo + len
+        for (int i = 0; i < L; ++i)
+          if (!((c + i) & 1) && (i + 1 < L || ext)) f(lo + r0 + i);
+        m &= ~(L >= 32 ? 0xffffffffu : (((1u << L) - 1u) << r0));
+      }
+    };
+    int cnt = 0;
+    each_sep([&](int) { ++cnt; });
+    int nsep;
+    int k = block_excl_sum(cnt, s.scr, &nsep);
+    each_sep([&](int p) {
+      if (k < MAX_EV) s.ev_b[k] = (uint16_t)p;
+      if (k + 1 < MAX_EV) s.ev_a[k + 1] = (uint16_t)(p + 2);
+      atomicMax(&s.v[V_LASTSEP], p);
+      ++k;
+    });
+    if (tid == 0) {
+      s.ev_a[0] = (uint16_t)start;
+      s.v[V_NSEP] = nsep;
+    }
+  } else {
     int flen = in_len - start;
     int C = (flen + BS - 1) / BS;
     int lo = min(start + tid * C, in_len), hi = min(lo + C, in_len);
@@ -747,17 +803,38 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       s.v[V_NEWDEPTH] = depth0;
     }
   } else if (filt && ndelta > 0) {
-    // candidates
+    // candidates: per-thread 8-byte-multiple chunks of Z (16-B aligned) as ds_read_b64
+    // words, a 32-bit '<' mask per thread (SWAR compare), popcount + ordered compaction
     {
-      int C = (Zn + BS - 1) / BS;
-      int lo = min(tid * C, Zn), hi = min(lo + C, Zn);
-      int cnt = 0;
-      for (int p = lo; p < hi; ++p) cnt += Z[p] == '<';
-      int tot;
-      int k = block_excl_sum(cnt, s.scr, &tot);
-      if (tot <= MAX_CAND)
-        for (int p = lo; p < hi; ++p)
-          if (Z[p] == '<') s.cand[k++] = (uint16_t)p;
+      const int C8 = (((Zn + BS - 1) / BS) + 7) & ~7;
+      int cnt = 0, tot;
+      if (C8 <= 32) {
+        const int lo = min(tid * C8, Zn), hi = min(lo + C8, Zn), len = hi - lo;
+        uint32_t lm = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (q * 8 < len) {
+            const uint64_t w = *(const uint64_t*)&Z[lo + 8 * q];  // B has >= 48 B past Zn
+            const uint64_t x = w ^ 0x3c3c3c3c3c3c3c3cull;
+            const uint64_t y = (((x & 0x7f7f7f7f7f7f7f7full) + 0x7f7f7f7f7f7f7f7full) | x) & 0x8080808080808080ull;
+            const uint64_t zb = ~y & 0x8080808080808080ull;
+            lm |= (uint32_t)(((zb >> 7) * 0x0102040810204080ull) >> 56) << (8 * q);
+          }
+        }
+        lm &= len >= 32 ? 0xffffffffu : ((1u << len) - 1u);
+        cnt = __popc(lm);
+        int k = block_excl_sum(cnt, s.scr, &tot);
+        if (tot <= MAX_CAND)
+          for (uint32_t m = lm; m; m &= m - 1) s.cand[k++] = (uint16_t)(lo + __ffs(m) - 1);
+      } else {
+        const int C = (Zn + BS - 1) / BS;
+        const int lo = min(tid * C, Zn), hi = min(lo + C, Zn);
+        for (int p = lo; p < hi; ++p) cnt += Z[p] == '<';
+        int k = block_excl_sum(cnt, s.scr, &tot);
+        if (tot <= MAX_CAND)
+          for (int p = lo; p < hi; ++p)
+            if (Z[p] == '<') s.cand[k++] = (uint16_t)p;
+      }
       ncand = tot;
     }
     if (ncand > MAX_CAND) {
