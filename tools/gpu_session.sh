@@ -13,6 +13,7 @@
 #   ab:NAME:ENV:ARGS      one bench.py run under extra env (commas = spaces) -> ab_<NAME>.json
 #   scenarios             aggregate4, highqps8, failure, paced (10 steps each)
 #   reference             the upstream proxy under the same harness (bench.py --impl reference)
+#   refscenarios          the same for aggregate4, highqps8, failure
 #   prof                  rocprofv3 --kernel-trace --stats of a short headline bench
 #   pmc:C1,C2,...         rocprofv3 --pmc pass (one block-limited counter set) on kbench
 #   kbench                tools/kbench.py in-kernel stage split (QMX_STAGE_TIMING)
@@ -84,6 +85,10 @@ for step in "$@"; do
       done ;;
     reference)
       bench reference 600 QMX_NOP=1 -- --impl reference --steps 10 --warmup 1 --batch 64 || exit 1 ;;
+    refscenarios)  # the upstream proxy on every BASELINE scenario, same harness
+      for SC in aggregate4 highqps8 failure; do
+        bench ref_$SC 600 QMX_NOP=1 -- --impl reference --scenario $SC --steps 5 --warmup 1 --batch 32 || exit 1
+      done ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o native --output-format csv -- \
         python3 bench.py --steps 5 --warmup 1 > $OUT/bench_prof.json 2> $OUT/bench_prof.err \
@@ -108,9 +113,9 @@ for l in open('$OUT/kbench.jsonl'):
     print(d.get('filter'),d.get('emit'),d['slots'],d['wall_us_p50'],d['kernel_us_avg'],[st.get('stage%d_us'%k) for k in range(1,11)])
 " ;;
     multirank=*)
-      n=${step#multirank=}; torchrun_bench multirank_$n $n --steps 5 --warmup 1 --threads 4 || exit 1 ;;
+      n=${step#multirank=}; torchrun_bench multirank_$n $n --steps 5 --warmup 1 --threads 2 --batch 4096 || exit 1 ;;
     spread=*)
-      n=${step#spread=}; QMX_XCHG=tcp torchrun_bench spread_$n $n --steps 5 --warmup 1 --threads 4 --placement spread || exit 1 ;;
+      n=${step#spread=}; QMX_XCHG=tcp torchrun_bench spread_$n $n --steps 5 --warmup 1 --threads 2 --batch 4096 --placement spread || exit 1 ;;
     cpuprof)
       bench cpuprof 300 QMX_PROF=$PWD/$OUT/cpu_hip.%p.txt QMX_PROF_US=100 -- --steps 20 --warmup 2 || exit 1
       for f in $OUT/cpu_hip.*.txt; do python3 tools/cpuprof.py $f --top 30 --json $f.json > $f.summary 2>&1 || true; done
