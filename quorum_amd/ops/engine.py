@@ -20,7 +20,6 @@ Reference counterpart: the per-backend loop of ``progress_streaming_aggregator``
 """
 from __future__ import annotations
 
-import json
 import logging
 import re
 import threading
@@ -187,6 +186,3 @@ def make_engine(kind: str, tags: Sequence[str], device: Optional[int] = None, **
         _NATIVE_CACHE[key] = eng
     return eng
 
-
-def dumps_event_text(text: str) -> str:
-    return json.dumps(text)
