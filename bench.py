@@ -40,7 +40,7 @@ BASELINE_SOURCE_SAME = "reference proxy, same box + same harness (bench.py --imp
 BASELINE_SOURCE_SURVEY = "reference proxy, survey container (8 vCPU, Python harness; SURVEY §6)"
 
 # BASELINE.json configs.  "headline" is the driver's metric; the others are measured with
-# --scenario (reference numbers from BASELINE.md where one exists for that shape).
+# --scenario; every one with a reference number has it from the same harness.
 SCENARIOS = {
     # headline: 16384 requests per step so the timed window (one load-generator run) is ~2 s
     # and its start/connect/drain is amortised (MI355X A/B, profiles/r1n_batch_ab.txt: 4/4
@@ -49,12 +49,15 @@ SCENARIOS = {
                      batch=16384, baseline=21.071, baseline_ttft_ms=619.6, baseline_source=BASELINE_SOURCE_SAME,
                      desc="2 mock backends, streaming concatenate, hide_intermediate_think"),
     "aggregate4": dict(n=4, strategy="aggregate", hide_final=False, skip=False, faults={}, timeout=30,
-                       baseline=3.8, desc="4 mock backends, streaming aggregate strategy (LLM4 also aggregates)"),
+                       baseline=10.09, baseline_ttft_ms=1191.9, baseline_source=BASELINE_SOURCE_SAME,
+                       desc="4 mock backends, streaming aggregate strategy (LLM4 also aggregates)"),
     "highqps8": dict(n=8, strategy="concatenate", hide_final=True, skip=True, faults={}, timeout=30,
-                     baseline=2.4, desc="8 mock backends, streaming, hide_final_think + skip_final_aggregation"),
+                     baseline=6.695, baseline_ttft_ms=2183.2, baseline_source=BASELINE_SOURCE_SAME,
+                     desc="8 mock backends, streaming, hide_final_think + skip_final_aggregation"),
     "failure": dict(n=2, strategy="concatenate", hide_final=False, skip=False, timeout=2,
                     faults={1: ["--fail-rate", "0.3", "--drop-rate", "0.2", "--null-rate", "0.1"]},
-                    baseline=6.9, desc="2 mock backends, backend 2 injects 30% HTTP 500 / 20% mid-stream "
+                    baseline=21.14, baseline_ttft_ms=620.5, baseline_source=BASELINE_SOURCE_SAME,
+                    desc="2 mock backends, backend 2 injects 30% HTTP 500 / 20% mid-stream "
                                        "disconnect / 10% content:null; 2 s timeout"),
     # steady-state serving shape: backends pace their events (10 ms apart, like a decoding
     # LLM), many concurrent sessions, each tick sees a few events of many streams.  TTFT is
@@ -414,13 +417,14 @@ def main() -> int:
 
     import torch
 
-    use_cuda = torch.cuda.is_available()
-    n_dev = torch.cuda.device_count() if use_cuda else 0
+    n_dev = torch.cuda.device_count()  # counts without initialising HIP
     # one rank per GPU (the driver's node runs); a rehearsal with more ranks than GPUs maps
-    # ranks onto the visible GPUs and keeps the bench's own bookkeeping group on gloo (RCCL
-    # refuses two ranks on one GPU)
+    # ranks onto the visible GPUs, keeps the bench's own bookkeeping group on gloo (RCCL
+    # refuses two ranks on one GPU) and keeps the bench processes themselves off the GPU:
+    # they do no GPU work (the native workers do), and a box admits 16 GPU processes
+    use_cuda = n_dev >= world and n_dev > 0 and torch.cuda.is_available()
     device = local_rank % n_dev if n_dev else None
-    coll_cuda = use_cuda and n_dev >= world
+    coll_cuda = use_cuda
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
@@ -434,7 +438,7 @@ def main() -> int:
         pinning = {"pinned": False, "error": repr(e)}
     engine = args.engine
     if engine == "auto":
-        engine = "hip" if use_cuda else "cpu"
+        engine = "hip" if n_dev else "cpu"
 
     from quorum_amd.ops import build as qbuild
 
@@ -519,6 +523,7 @@ def main() -> int:
         spread = None
         if (dist is not None and world > 1 and args.spread_check and args.impl == "native"
                 and args.placement == "local"):
+            _kill(proxy_procs)  # done measuring; the check brings up its own proxy set
             spread = spread_check(args, SCENARIOS["headline"], rank, world, engine, device, bin_dir, tmp,
                                   mock_ports, dist, n_dev)
             spread_rows = [None] * world
