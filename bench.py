@@ -238,7 +238,7 @@ def scrape(port):
     except Exception:  # noqa: BLE001
         return out
     for ln in txt.splitlines():
-        if not ln or ln[0] == "#" or "{" in ln:
+        if not ln or ln[0] == "#" or ("{" in ln and not ln.startswith("qmx_syscalls_total")):
             continue
         k, _, v = ln.rpartition(" ")
         try:
@@ -299,6 +299,10 @@ def breakdown(m0, m1, elapsed):
         "h2d_MB": round(d.get("qmx_kernel_h2d_bytes", 0.0) / 1e6, 2),
         "d2h_MB": round(d.get("qmx_kernel_d2h_bytes", 0.0) / 1e6, 2),
         "escalations": int(d.get("qmx_kernel_escalations", 0.0)),
+        # io-loop syscalls per request (sends to clients / upstreams, recvs, epoll, wakeups)
+        "syscalls_per_req": {k.split('"')[1]: round(v / d["qmx_requests_total"], 2)
+                             for k, v in d.items() if k.startswith("qmx_syscalls_total")}
+        if d.get("qmx_requests_total") else {},
         "exchange_rounds": int(d.get("qmx_exchange_rounds_total", 0.0)),
     }
 
@@ -417,7 +421,9 @@ def main() -> int:
 
     import torch
 
-    n_dev = torch.cuda.device_count()  # counts without initialising HIP
+    # QMX_BENCH_NDEV: a rehearsal names the GPU count itself, so the bench processes never
+    # open the device (a box counts every process holding it open)
+    n_dev = int(os.environ["QMX_BENCH_NDEV"]) if os.environ.get("QMX_BENCH_NDEV") else torch.cuda.device_count()
     # one rank per GPU (the driver's node runs); a rehearsal with more ranks than GPUs maps
     # ranks onto the visible GPUs, keeps the bench's own bookkeeping group on gloo (RCCL
     # refuses two ranks on one GPU) and keeps the bench processes themselves off the GPU:

@@ -2,6 +2,7 @@
 #include "qmx_engine.h"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <stdexcept>
 
@@ -136,10 +137,19 @@ void escape_append(const uint8_t* y, size_t n, std::string& out) {
     out.append((const char*)buf, k);
   }
 }
+static void delta_prefix_append(int index, int64_t created, std::string& out) {
+  char b[224];
+  const int n = snprintf(b, sizeof(b),
+                         "data: {\"id\": \"chatcmpl-parallel-%d\", \"object\": \"chat.completion.chunk\", "
+                         "\"created\": %lld, \"model\": \"parallel-proxy\", \"choices\": [{\"index\": 0, "
+                         "\"delta\": {\"content\": \"",
+                         index, (long long)created);
+  out.append(b, (size_t)n);
+}
 std::string delta_prefix(int index, int64_t created) {
-  return "data: {\"id\": \"chatcmpl-parallel-" + std::to_string(index) +
-         "\", \"object\": \"chat.completion.chunk\", \"created\": " + std::to_string(created) +
-         ", \"model\": \"parallel-proxy\", \"choices\": [{\"index\": 0, \"delta\": {\"content\": \"";
+  std::string s;
+  delta_prefix_append(index, created, s);
+  return s;
 }
 std::string final_prefix(int64_t created) {
   return "data: {\"id\": \"chatcmpl-parallel-final\", \"object\": \"chat.completion.chunk\", \"created\": " +
@@ -194,15 +204,16 @@ static void handle_event(const TagSet& ts, SlotCore& s, const uint8_t* e, int m,
     s.aborted = true;
     return;
   }
-  int dl = json_unescape(e, r.str_a, r.str_b, nullptr);
-  std::string c(dl, '\0');
+  const int dl = json_unescape(e, r.str_a, r.str_b, nullptr);
+  thread_local std::string c;  // unescaped content (reused: no allocation per event)
+  c.resize((size_t)dl);
   json_unescape(e, r.str_a, r.str_b, (uint8_t*)&c[0]);
   scratch.clear();
   if (s.filter) filter_feed(ts, s.fs, (const uint8_t*)c.data(), c.size(), scratch);
-  else scratch.swap(c);
+  else scratch.assign(c);
   s.content += scratch;
   if (!scratch.empty() && s.emit) {
-    out += delta_prefix(s.index, created);
+    delta_prefix_append(s.index, created, out);
     escape_append((const uint8_t*)scratch.data(), scratch.size(), out);
     out += kDeltaSuffix;
   }
@@ -229,13 +240,19 @@ void process_slot(const TagSet& ts, SlotCore& s, const uint8_t* data, size_t n, 
     }
     s.started = true;
   }
-  std::string scratch;
+  thread_local std::string scratch;
+  int from = pos;  // no separator starts before `from` (memchr for '\n', then check the next byte)
   while (!s.aborted) {
-    const void* hit = memmem(x + pos, (size_t)(N - pos), "\n\n", 2);  // leftmost separator
-    if (!hit) break;
-    const int j = (int)((const uint8_t*)hit - x);
-    handle_event(ts, s, x + pos, j - pos, created, out, scratch);
-    pos = j + 2;
+    const void* nl = from < N ? memchr(x + from, '\n', (size_t)(N - from)) : nullptr;
+    if (!nl) break;
+    const int j = (int)((const uint8_t*)nl - x);
+    if (j + 1 >= N) break;
+    if (x[j + 1] != '\n') {
+      from = j + 1;
+      continue;
+    }
+    handle_event(ts, s, x + pos, j - pos, created, out, scratch);  // leftmost separator
+    pos = from = j + 2;
   }
   if (s.aborted) {
     s.carry.clear();

@@ -1,6 +1,7 @@
 // qmx_exchange.cpp — TCP mesh (control + deltas) and RCCL point-to-point rounds (final
 // texts, HBM to HBM) for spread placement; see qmx_exchange.h.
 #include "qmx_exchange.h"
+#include "qmx_prof.h"
 
 #include <arpa/inet.h>
 #include <errno.h>
@@ -579,6 +580,8 @@ void Exchange::join() {
 
 // ------------------------------------------------------------------ the mesh thread
 void Exchange::mesh_loop() {
+  prof_thread();
+  crash_thread();
   Impl& I = *im_;
   if (I.lfd < 0) {
     std::vector<XMsg> v(1);
@@ -715,6 +718,8 @@ void Exchange::mesh_loop() {
 
 // ------------------------------------------------------------------ the bulk (RCCL) thread
 void Exchange::bulk_loop() {
+  prof_thread();
+  crash_thread();
   Impl& I = *im_;
   ncclComm_t comm = nullptr;
   int epoch = 0;

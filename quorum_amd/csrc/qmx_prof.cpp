@@ -209,12 +209,11 @@ void prof_start() {
   sigemptyset(&sa.sa_mask);
   sigaction(SIGPROF, &sa, nullptr);
   if (const char* e = getenv("QMX_PROF_US")) g_us = std::max(50, atoi(e));
-  itimerval tv{};
-  tv.it_interval.tv_sec = g_us / 1000000;
-  tv.it_interval.tv_usec = g_us % 1000000;
-  tv.it_value = tv.it_interval;
+  // Only per-thread CPU-time timers (prof_thread, armed by every hot thread): a process-wide
+  // ITIMER_PROF signal may be delivered to any thread, including one blocked in a join, and
+  // would charge its stack with CPU it never used.  The kernel checks thread CPU timers at
+  // the scheduler tick, so the effective rate is at most HZ per thread whatever g_us says.
   g_on.store(true);
-  setitimer(ITIMER_PROF, &tv, nullptr);
 }
 
 void prof_thread() {
@@ -236,8 +235,6 @@ void prof_thread() {
 
 void prof_stop() {
   if (!g_ring || !g_on.exchange(false)) return;
-  itimerval off{};
-  setitimer(ITIMER_PROF, &off, nullptr);
   FILE* f = fopen(g_path.c_str(), "w");
   if (!f) return;
   const size_t n = std::min(g_next.load(), kMaxSamples);

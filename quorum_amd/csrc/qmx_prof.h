@@ -1,13 +1,14 @@
 // qmx_prof.h — in-process CPU sampling profiler for the native data plane.
 //
-// QMX_PROF=<path> (%p = pid): SIGPROF every QMX_PROF_US (default 500) microseconds of *process* CPU
-// time (ITIMER_PROF: user + system, all threads); the handler records the interrupted
-// thread's call stack into a preallocated ring (async-signal-safe: no allocation, one
-// atomic slot claim).  prof_stop() writes one line per sample, frames as
+// QMX_PROF=<path> (%p = pid): SIGPROF every QMX_PROF_US (default 500) microseconds of each hot
+// thread's own CPU time (a CLOCK_THREAD_CPUTIME_ID timer per thread that calls prof_thread();
+// the kernel checks them at the scheduler tick, so at most HZ samples per thread per second);
+// the handler records the interrupted thread's call stack into a preallocated ring
+// (async-signal-safe: no allocation, one atomic slot claim).  prof_stop() writes one line per sample, frames as
 // "module+0xoffset", for offline symbolisation (tools/cpuprof.py → llvm-symbolizer).
 // A syscall shows up as its libc wrapper frame (the signal lands on the return to user
 // space), so the profile splits the proxy's CPU into socket I/O, epoll, locking, HTTP /
-// JSON handling and engine host work.  Not for production: one timer per process.
+// JSON handling and engine host work.  Not for production.
 #pragma once
 
 namespace qmx {

@@ -688,6 +688,10 @@ class Loop {
   void attach_loops(const std::vector<Loop*>* ls) { loops_ = ls; }
   std::mutex smu_;
   std::unordered_map<std::string, double> snap_;  // engine stats snapshot (read by /metrics on any loop)
+  // syscalls issued by this loop's thread (single writer; /metrics reads them from any loop)
+  enum { SC_CLIENT_SEND, SC_UP_SEND, SC_RECV, SC_EPOLL_WAIT, SC_EPOLL_CTL, SC_WAKE_READ, SC_N };
+  std::atomic<uint64_t> sc_[SC_N] = {};
+  void cnt(int i) { sc_[i].store(sc_[i].load(std::memory_order_relaxed) + 1, std::memory_order_relaxed); }
   void snapshot() {
     if (!eng_) return;
     std::unordered_map<std::string, double> m;
@@ -729,6 +733,7 @@ class Loop {
       // while applying tick results): poll instead of sleeping
       const int to = (!hub_ && kick_) ? 0 : deferq_.empty() ? 50 : 1;
       int n = epoll_wait(ep_, evs.data(), (int)evs.size(), to);
+      cnt(SC_EPOLL_WAIT);
       for (int i = 0; i < n; ++i) dispatch(evs[i]);
       if (g_drain.load() && drain_step()) break;
       if (!pending_requests_.empty()) {
@@ -815,12 +820,14 @@ class Loop {
     e.events = ev;
     e.data.u64 = t;
     epoll_ctl(ep_, EPOLL_CTL_ADD, fd, &e);
+    cnt(SC_EPOLL_CTL);
   }
   void mod(int fd, uint32_t ev, uint64_t t) {
     epoll_event e{};
     e.events = ev;
     e.data.u64 = t;
     epoll_ctl(ep_, EPOLL_CTL_MOD, fd, &e);
+    cnt(SC_EPOLL_CTL);
   }
 
   void dispatch(const epoll_event& e) {
@@ -857,6 +864,7 @@ class Loop {
   void on_results() {
     uint64_t v;
     ssize_t r = read(evfd_, &v, 8);
+    cnt(SC_WAKE_READ);
     (void)r;
     std::vector<ResultBatch> q;
     {
@@ -952,6 +960,7 @@ class Loop {
       if (lfd_ >= 0) {
         on_accept();  // connections already queued on this listener are served, not reset
         epoll_ctl(ep_, EPOLL_CTL_DEL, lfd_, nullptr);
+        cnt(SC_EPOLL_CTL);
         close(lfd_);
         lfd_ = -1;
       }
@@ -1005,6 +1014,7 @@ class Loop {
       char buf[65536];
       while (true) {
         ssize_t r = recv(c->fd, buf, sizeof(buf), 0);
+        cnt(SC_RECV);
         if (r > 0) {
           c->in.append(buf, r);
           // a short read drained the socket: epoll is level-triggered, so skip the recv
@@ -1025,6 +1035,7 @@ class Loop {
       abort_session(c->sess);
     }
     epoll_ctl(ep_, EPOLL_CTL_DEL, c->fd, nullptr);
+    cnt(SC_EPOLL_CTL);
     close(c->fd);
     clients_.erase(c->fd);
   }
@@ -1073,6 +1084,7 @@ class Loop {
       if (c->dead || c->want_out) continue;
       while (c->out_off < c->out.size()) {
         ssize_t w = send(c->fd, c->out.data() + c->out_off, c->out.size() - c->out_off, MSG_NOSIGNAL);
+        cnt(SC_CLIENT_SEND);
         if (w > 0) {
           c->out_off += w;
           continue;
@@ -1096,6 +1108,7 @@ class Loop {
   void flush_client(Client* c) {
     while (c->out_off < c->out.size()) {
       ssize_t w = send(c->fd, c->out.data() + c->out_off, c->out.size() - c->out_off, MSG_NOSIGNAL);
+      cnt(SC_CLIENT_SEND);
       if (w > 0) {
         c->out_off += w;
         continue;
@@ -1456,6 +1469,7 @@ class Loop {
         return up_error(u, "All connection attempts failed");
       }
       ssize_t w = send(u->fd, u->req.data() + u->req_off, u->req.size() - u->req_off, MSG_NOSIGNAL);
+      cnt(SC_UP_SEND);
       if (w > 0) {
         u->req_off += w;
         u->last_io = now_s();
@@ -1480,6 +1494,7 @@ class Loop {
   ssize_t up_read(Up* u, char* buf, size_t n) {
     if (!u->ssl) {
       ssize_t r = recv(u->fd, buf, n, 0);
+      cnt(SC_RECV);
       if (r > 0) return r;
       if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) return 0;
       return -1;
@@ -1572,6 +1587,7 @@ class Loop {
       if (u->ssl) idle_ssl_[fd] = u->ssl;  // the TLS session stays with the pooled socket
     } else {
       epoll_ctl(ep_, EPOLL_CTL_DEL, fd, nullptr);
+      cnt(SC_EPOLL_CTL);
       if (u->ssl) SSL_free(u->ssl);
       close(fd);
     }
@@ -1591,6 +1607,7 @@ class Loop {
       idle_ssl_.erase(s);
     }
     epoll_ctl(ep_, EPOLL_CTL_DEL, fd, nullptr);
+    cnt(SC_EPOLL_CTL);
     close(fd);
   }
   void up_error(Up* u, const std::string& msg) {
@@ -1912,6 +1929,7 @@ class Loop {
   void on_xmsgs() {
     uint64_t v;
     ssize_t r = read(xfd_, &v, 8);
+    cnt(SC_WAKE_READ);
     (void)r;
     std::vector<XMsg> in;
     {
@@ -2459,6 +2477,12 @@ class Loop {
     if (hub_)
       for (auto& kv : hub_->snapshot()) tot[kv.first] += kv.second;
     for (auto& kv : tot) put(kv.first.c_str(), kv.second);
+    static const char* sc_names[SC_N] = {"client_send", "upstream_send", "recv", "epoll_wait", "epoll_ctl", "wake_read"};
+    for (int i = 0; i < SC_N; ++i) {
+      uint64_t v = 0;
+      for (Loop* l : *loops_) v += l->sc_[i].load(std::memory_order_relaxed);
+      m += std::string("qmx_syscalls_total{op=\"") + sc_names[i] + "\"} " + std::to_string(v) + "\n";
+    }
     return m;
   }
 

@@ -96,6 +96,7 @@ def summarize(path: str, top: int = 40):
     self_c = collections.Counter()
     cat_c = collections.Counter()
     incl = collections.Counter()
+    callers = collections.defaultdict(collections.Counter)  # category -> first qmx frame above it
     for st in stacks:
         fns = [names.get(fr, fr) for fr in st]
         # drop the handler and the sigreturn trampoline above the interrupted frame
@@ -107,7 +108,11 @@ def summarize(path: str, top: int = 40):
         self_c[fns[0]] += 1
         # the category of a sample = the innermost frame that matches one (libc wrappers first)
         cats = [category(x) for x in fns]
-        cat_c[next((c for c in cats if not c.startswith("other")), cats[0])] += 1
+        cat = next((c for c in cats if not c.startswith("other")), cats[0])
+        cat_c[cat] += 1
+        own = next((x for x in fns if "[_qmx" in x or "[qmx_" in x), None)
+        if own is not None and own != fns[0]:
+            callers[cat][own.split(" [")[0]] += 1
         for x in set(fns):
             if "qmx" in x or "Loop" in x:
                 incl[x] += 1
@@ -115,7 +120,9 @@ def summarize(path: str, top: int = 40):
     return {"samples": n,
             "by_category_pct": {k: pct(v) for k, v in cat_c.most_common()},
             "self_top_pct": {k: pct(v) for k, v in self_c.most_common(top)},
-            "inclusive_qmx_pct": {k: pct(v) for k, v in incl.most_common(top)}}
+            "inclusive_qmx_pct": {k: pct(v) for k, v in incl.most_common(top)},
+            # which of our functions issued the library time of each category
+            "callers_pct": {c: {k: pct(v) for k, v in cc.most_common(12)} for c, cc in callers.items()}}
 
 
 def main(argv=None) -> int:
@@ -123,6 +130,8 @@ def main(argv=None) -> int:
     ap.add_argument("profiles", nargs="+")
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--callers", action="append", default=[],
+                    help="print our functions that issued a category's time (e.g. allocator)")
     a = ap.parse_args(argv)
     res = {p: summarize(p, a.top) for p in a.profiles}
     for p, r in res.items():
@@ -133,6 +142,10 @@ def main(argv=None) -> int:
         print("-- self (%)")
         for k, v in list(r["self_top_pct"].items())[:a.top]:
             print(f"  {v:6.2f}  {k}")
+        for cat in a.callers:
+            print(f"-- callers of {cat} (%)")
+            for k, v in r["callers_pct"].get(cat, {}).items():
+                print(f"  {v:6.2f}  {k[:150]}")
     if a.json:
         with open(a.json, "w") as f:
             json.dump(res, f, indent=1)

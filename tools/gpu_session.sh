@@ -52,7 +52,7 @@ bench() {  # name timeout env... -- args...
 }
 torchrun_bench() {  # name nproc args...
   local name=$1 np=$2; shift 2
-  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $np --master-addr 127.0.0.1 \
+  QMX_BENCH_NDEV=${QMX_BENCH_NDEV:-1} timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $np --master-addr 127.0.0.1 \
     --master-port $((29500 + RANDOM % 500)) bench.py --gpus $np "$@" > $OUT/$name.json 2> $OUT/$name.err
   local rc=$?
   summ $name $OUT/$name.json
