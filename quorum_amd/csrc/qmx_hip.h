@@ -85,6 +85,9 @@ struct FinResult {
   uint64_t t0, t1;                   // s_memrealtime at workgroup start / end
 };
 
+struct PDoor;  // persistent mode: host-mapped doorbell (qmx_hip.hip)
+struct PCtl;   // persistent mode: device control block
+
 // Launch resources of one tick lane: a tick thread owns a lane (HIP stream, events,
 // host-mapped in/out arenas, work/result descriptors, counters), so several lanes can have
 // tick kernels in flight at once over disjoint slot sets (HostEngine busy flags).
@@ -139,6 +142,13 @@ struct TickLane {
   double ema_us = 40.0;  // launch-to-results time, smoothed
   bool timing_pending = false;
   uint64_t poll_fallbacks = 0;
+  // persistent mode (QMX_PERSISTENT=1): the lane's long-lived grid and its doorbell
+  PDoor* h_door = nullptr;
+  PCtl* d_ctl = nullptr;
+  bool p_running = false;
+  uint32_t p_gen = 0;
+  double p_last_post = 0;  // steady clock, seconds
+  uint64_t p_launches = 0, p_ticks = 0;
 };
 
 class HipEngine : public HostEngine {
@@ -172,6 +182,15 @@ class HipEngine : public HostEngine {
   void ensure_out(TickLane& L, size_t bytes);
   void build_params(TickLane& L, int64_t created);
   std::string device_content(int slot, uint32_t len);
+  uint32_t next_seq(TickLane& L);
+  void ensure_persistent(TickLane& L);
+  void stop_persistent(TickLane& L);
+  // arenas replaced by a larger one: freed at destruction (a free may wait for the device,
+  // which a persistent grid would hold up)
+  void retire_host(void* p);
+  void retire_dev(void* p);
+  std::vector<void*> grave_host_, grave_dev_;
+  std::mutex grave_mu_;
 
   int device_;
   int tile_;
@@ -190,6 +209,15 @@ class HipEngine : public HostEngine {
   int spin_us_ = 0;  // QMX_WAIT_SPIN_US: yield-poll before the blocking wait
   bool poll_ = true;  // QMX_WAIT=event: wait on a blocking-sync HIP event instead of polling
   int poll_us_ = 6;   // QMX_POLL_US: poll period once the expected kernel time has passed
+  bool persistent_ = false;  // QMX_PERSISTENT=1: a long-lived grid per lane, ticks posted by doorbell
+  int p_grid_ = 64;          // QMX_PERSISTENT_WG: workgroups per lane grid (1 per CU: 256 VGPRs)
+  int p_idle_ms_ = 50;       // the grid exits after this long without a tick
+
+ public:
+  bool persistent() const { return persistent_; }
+  // off for spread placement: remote final texts land in the content arena by RCCL / DMA,
+  // outside the grid's release / acquire protocol
+  void set_persistent(bool on);
 };
 
 }  // namespace qmx

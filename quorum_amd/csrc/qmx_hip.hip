@@ -63,7 +63,7 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 #define QMX_STAMP(k)                                               \
   do {                                                             \
     if (Pk.dbg != nullptr && threadIdx.x == 0)                     \
-      Pk.dbg[blockIdx.x * kDbg + (k)] = __builtin_amdgcn_s_memrealtime(); \
+      Pk.dbg[bi * kDbg + (k)] = __builtin_amdgcn_s_memrealtime();      \
   } while (0)
 
 struct Smem {
@@ -314,7 +314,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
                                           uint8_t* __restrict__ out, WorkResult* __restrict__ res,
                                           DevSlot* __restrict__ state, uint8_t* __restrict__ content,
                                           const KParams& Pk, TickShared& U, const BackendTpl* __restrict__ btpl_rd,
-                                          BackendTpl* __restrict__ btpl_wr, uint32_t seq) {
+                                          BackendTpl* __restrict__ btpl_wr, uint32_t seq, const int bi) {
   Smem& s = U.s;
   KParams& P = U.P;
   auto& TKP = U.TKP;
@@ -323,8 +323,8 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   const int tid = threadIdx.x;
   for (int i = tid; i < (int)(sizeof(KParams) / 4); i += BS) ((uint32_t*)&P)[i] = ((const uint32_t*)&Pk)[i];
   QMX_STAMP(0);
-  if (Pk.dbg != nullptr && threadIdx.x == 0) Pk.dbg[blockIdx.x * kDbg + 11] = __builtin_amdgcn_s_memtime();
-  const WorkItem it = items[blockIdx.x];
+  if (Pk.dbg != nullptr && threadIdx.x == 0) Pk.dbg[bi * kDbg + 11] = __builtin_amdgcn_s_memtime();
+  const WorkItem it = items[bi];
   const int in_len = (int)it.in_len;
   const bool eof = it.flags & WF_EOF;
   const bool filt = it.flags & WF_FILTER;
@@ -405,7 +405,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     }
     if (tid == 0) {
       WorkResult r{(uint32_t)s.v[V_CONSUMED], 0u, (uint32_t)s.v[V_STATUS], it.content_len};
-      res[blockIdx.x] = r;
+      res[bi] = r;
     }
     return;
   }
@@ -840,7 +840,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     if (ncand > MAX_CAND) {
       if (tid == 0) {
         WorkResult r{0u, 0u, (uint32_t)WS_ESCALATE, it.content_len};
-        res[blockIdx.x] = r;
+        res[bi] = r;
       }
       return;  // uniform: every thread saw the same total
     }
@@ -1078,7 +1078,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   if ((uint32_t)out_len > it.out_cap || new_clen > P.content_cap) {
     if (tid == 0) {
       WorkResult r{0u, 0u, (uint32_t)WS_ESCALATE, it.content_len};
-      res[blockIdx.x] = r;
+      res[bi] = r;
     }
     return;
   }
@@ -1174,17 +1174,17 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   }
   QMX_STAMP(10);
   if (Pk.dbg != nullptr && threadIdx.x == 0) {
-    Pk.dbg[blockIdx.x * kDbg + 12] = __builtin_amdgcn_s_memtime();
-    Pk.dbg[blockIdx.x * kDbg + 13] = (unsigned long long)s.v[V_NFULL];  // S3: events fully parsed
-    Pk.dbg[blockIdx.x * kDbg + 14] = (unsigned long long)s.v[V_NTPL];   // S3: template hits
-    Pk.dbg[blockIdx.x * kDbg + 15] = (unsigned long long)nev;
-    Pk.dbg[blockIdx.x * kDbg + 16] = (unsigned long long)s.v[V_CFULL];  // S3 cycles: full parses (sum over waves)
-    Pk.dbg[blockIdx.x * kDbg + 17] = (unsigned long long)s.v[V_CTPL];   // S3 cycles: template checks
-    Pk.dbg[blockIdx.x * kDbg + 18] = (unsigned long long)s.v[V_CLEX];   // S3 cycles: wave_lex part of full
+    Pk.dbg[bi * kDbg + 12] = __builtin_amdgcn_s_memtime();
+    Pk.dbg[bi * kDbg + 13] = (unsigned long long)s.v[V_NFULL];  // S3: events fully parsed
+    Pk.dbg[bi * kDbg + 14] = (unsigned long long)s.v[V_NTPL];   // S3: template hits
+    Pk.dbg[bi * kDbg + 15] = (unsigned long long)nev;
+    Pk.dbg[bi * kDbg + 16] = (unsigned long long)s.v[V_CFULL];  // S3 cycles: full parses (sum over waves)
+    Pk.dbg[bi * kDbg + 17] = (unsigned long long)s.v[V_CTPL];   // S3 cycles: template checks
+    Pk.dbg[bi * kDbg + 18] = (unsigned long long)s.v[V_CLEX];   // S3 cycles: wave_lex part of full
   }
   if (tid == 0) {
     WorkResult r{(uint32_t)s.v[V_CONSUMED], (uint32_t)out_len, (uint32_t)s.v[V_STATUS], new_clen};
-    res[blockIdx.x] = r;
+    res[bi] = r;
   }
 }
 
@@ -1488,29 +1488,26 @@ union TickLds {
   FinShared f;
 };
 
-__global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict__ items,
-                                                      const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
-                                                      WorkResult* __restrict__ res, DevSlot* __restrict__ state,
-                                                      uint8_t* __restrict__ content, const KParams* __restrict__ Pkp,
-                                                      uint32_t seq, uint32_t n_tick, FinArgs fa,
-                                                      const BackendTpl* __restrict__ btpl_rd,
-                                                      BackendTpl* __restrict__ btpl_wr) {
-  __shared__ TickLds U;
+// One work item of a tick: k < n_tick a stream tile, else finalize request k - n_tick.
+// Publishes the item's result record last (fence + sequence number).
+__device__ __forceinline__ void run_item(int k, const WorkItem* __restrict__ items, const uint8_t* __restrict__ in,
+                                         uint8_t* __restrict__ out, WorkResult* __restrict__ res,
+                                         DevSlot* __restrict__ state, uint8_t* __restrict__ content,
+                                         const KParams& Pk, uint32_t seq, uint32_t n_tick, const FinArgs& fa,
+                                         const BackendTpl* __restrict__ btpl_rd, BackendTpl* __restrict__ btpl_wr,
+                                         TickLds& U) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  // tag patterns, MFMA B operand and SSE envelopes: in device memory (uploaded by the lane
-  // when they change, ~once a second), not a 1.5 KB by-value kernel argument per launch
-  const KParams& Pk = *Pkp;
-  if (blockIdx.x < n_tick) {
-    tick_body(items, in, out, res, state, content, Pk, U.t, btpl_rd, btpl_wr, seq);
+  if ((uint32_t)k < n_tick) {
+    tick_body(items, in, out, res, state, content, Pk, U.t, btpl_rd, btpl_wr, seq, k);
     if (threadIdx.x == 0) {
-      res[blockIdx.x].t0 = t0;
-      res[blockIdx.x].t1 = __builtin_amdgcn_s_memrealtime();
+      res[k].t0 = t0;
+      res[k].t1 = __builtin_amdgcn_s_memrealtime();
     }
     __threadfence_system();
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(&res[blockIdx.x].seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) __hip_atomic_store(&res[k].seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   } else {
-    const int j = (int)(blockIdx.x - n_tick);
+    const int j = (int)(k - n_tick);
     fin_body(fa, j, content, Pk.content_cap, Pk.ts, U.f);
     if (threadIdx.x == 0) {
       fa.res[j].t0 = t0;
@@ -1519,6 +1516,149 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
     __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(&fa.res[j].seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+__global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict__ items,
+                                                      const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                      WorkResult* __restrict__ res, DevSlot* __restrict__ state,
+                                                      uint8_t* __restrict__ content, const KParams* __restrict__ Pkp,
+                                                      uint32_t seq, uint32_t n_tick, FinArgs fa,
+                                                      const BackendTpl* __restrict__ btpl_rd,
+                                                      BackendTpl* __restrict__ btpl_wr) {
+  __shared__ TickLds U;
+  // tag patterns, MFMA B operand and SSE envelopes: in device memory (uploaded by the lane
+  // when they change, ~once a second), not a 1.5 KB by-value kernel argument per launch
+  run_item((int)blockIdx.x, items, in, out, res, state, content, *Pkp, seq, n_tick, fa, btpl_rd, btpl_wr, U);
+}
+
+// ------------------------------------------------------------------------------------
+// Persistent mode (QMX_PERSISTENT=1): one long-lived grid per tick lane replaces the launch
+// per tick.  The host posts a tick by writing its arguments (TickDesc) into a host-mapped
+// doorbell and then its sequence number; workgroup 0 polls the doorbell (relaxed system-
+// scope loads with s_sleep, one PCIe read in flight) and relays the tick into a device-
+// memory control block, which the other workgroups poll (relaxed agent-scope loads: no cache
+// invalidation per poll).  On a new tick every workgroup takes one acquire fence (system
+// scope: host-written items / tile bytes and other XCDs' slot state become visible), then
+// runs items blockIdx.x, blockIdx.x + grid, ... exactly like the one-shot kernel, result
+// records included, so the host's completion polling is unchanged.
+// Exit conditions every wave reaches: a posted tick with stop set; or workgroup 0 idle for
+// idle_ticks (s_memrealtime, 100 MHz) — it then raises the control block's exit word for
+// this launch generation; or (safety net) any workgroup idle for 2 x idle_ticks.  The host
+// never posts to a grid that may be idling out (HipEngine::ensure_persistent), and stops it
+// before anything that would wait for the device.
+// ------------------------------------------------------------------------------------
+template <class T>
+__device__ __forceinline__ T* uni(T* p) {  // a wave-uniform pointer held in SGPRs
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (T*)(((uint64_t)hi << 32) | lo);
+}
+
+struct TickDesc {
+  const WorkItem* items;
+  const uint8_t* in;
+  uint8_t* out;
+  WorkResult* res;
+  KParams* params;            // device copy read by the items
+  const KParams* params_src;  // non-null: host-mapped new parameters, copied into `params` first
+  const BackendTpl* btpl_rd;
+  BackendTpl* btpl_wr;
+  FinArgs fa;
+  uint32_t seq, n_tick, n_fin, stop;
+};
+struct PDoor {  // host-mapped: written by the host, polled by workgroup 0
+  TickDesc d;
+  alignas(64) uint32_t posted;
+};
+struct PCtl {  // device memory: written by workgroup 0, polled by the others
+  TickDesc d;
+  alignas(64) uint32_t seq;
+  uint32_t exit_gen;
+};
+
+__global__ __launch_bounds__(BS) void qmx_tick_persistent(const PDoor* __restrict__ door, PCtl* __restrict__ ctl,
+                                                          DevSlot* __restrict__ state, uint8_t* __restrict__ content,
+                                                          uint32_t seq0, uint32_t gen, uint32_t idle_ticks) {
+  __shared__ TickLds U;
+  __shared__ TickDesc D;
+  __shared__ uint32_t cmd;  // new tick's sequence number, 0: exit
+  uint32_t last = seq0;     // the value the host posted last before this launch
+  const bool relay = blockIdx.x == 0;
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const uint64_t t_idle = __builtin_amdgcn_s_memrealtime();
+      const uint64_t limit = relay ? (uint64_t)idle_ticks : 2ull * idle_ticks;
+      uint32_t c = 0;
+      for (;;) {
+        if (relay) {
+          const uint32_t v = __hip_atomic_load(&door->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          if ((int32_t)(v - last) > 0) {  // newer only: a control word left by an earlier launch is older
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the descriptor written before `posted`
+            const uint32_t* src = (const uint32_t*)&door->d;
+            uint32_t* dst = (uint32_t*)&D;
+            for (int i = 0; i < (int)(sizeof(TickDesc) / 4); ++i) dst[i] = src[i];
+            c = v;
+            break;
+          }
+        } else {
+          const uint32_t v = __hip_atomic_load(&ctl->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((int32_t)(v - last) > 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            D = ctl->d;
+            c = v;
+            break;
+          }
+          if (__hip_atomic_load(&ctl->exit_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t_idle > limit) {
+          if (relay) __hip_atomic_store(&ctl->exit_gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+      }
+      cmd = c;
+    }
+    __syncthreads();
+    const uint32_t c = cmd;
+    if (relay && c != 0) {
+      // new kernel parameters (about once a second): copied by this workgroup's threads, then
+      // the tick is published to the other workgroups (agent-scope release)
+      if (D.params_src != nullptr && !D.stop)
+        for (int i = threadIdx.x; i < (int)(sizeof(KParams) / 4); i += BS)
+          ((uint32_t*)D.params)[i] = ((const uint32_t*)D.params_src)[i];
+      __threadfence();
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        ctl->d = D;
+        __hip_atomic_store(&ctl->seq, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (c == 0 || D.stop) return;  // D is block-uniform (LDS, written before the barrier)
+    last = c;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope, every thread: see the header
+    // descriptor fields read from LDS land in VGPRs: make them wave-uniform scalars again
+    // (as kernel arguments are), or every address derived from them costs vector registers
+    FinArgs fa;
+    fa.items = uni(D.fa.items);
+    fa.texts = uni(D.fa.texts);
+    fa.fin_in = uni(D.fa.fin_in);
+    fa.join = uni(D.fa.join);
+    fa.out_dev = uni(D.fa.out_dev);
+    fa.out_host = uni(D.fa.out_host);
+    fa.res = uni(D.fa.res);
+    fa.text_len = uni(D.fa.text_len);
+    fa.segs = uni(D.fa.segs);
+    const uint32_t n_tick = __builtin_amdgcn_readfirstlane(D.n_tick);
+    const int total = (int)(n_tick + __builtin_amdgcn_readfirstlane(D.n_fin));
+    const uint32_t seq = __builtin_amdgcn_readfirstlane(D.seq);
+    for (int k = (int)blockIdx.x; k < total; k += (int)gridDim.x) {
+      run_item(k, uni(D.items), uni(D.in), uni(D.out), uni(D.res), state, content, *uni(D.params), seq, n_tick, fa,
+               uni(D.btpl_rd), uni(D.btpl_wr), U);
+      __syncthreads();  // LDS is reused by the next item
+    }
+    __syncthreads();  // D / cmd are rewritten by thread 0 for the next tick
   }
 }
 
@@ -1571,9 +1711,12 @@ void HipEngine::wait_results(TickLane& L, int n, int m, uint32_t seq) {
   while (!done(i)) {
     const double el = std::chrono::duration<double, std::micro>(HC::now() - t0).count();
     if (el > 4.0 * L.ema_us + 2000.0) {
-      HIP_CHECK(hipStreamSynchronize(L.stream));  // throws on a kernel fault
+      if (L.p_running) stop_persistent(L);  // the grid leaves after this tick; throws on a fault
+      else HIP_CHECK(hipStreamSynchronize(L.stream));  // throws on a kernel fault
       ++L.poll_fallbacks;
-      break;  // the stream has drained: every result is final
+      // the stream has drained: every result is final — or the tick was never run
+      if (!done(i)) throw std::runtime_error("tick results missing after the lane drained (seq " + std::to_string(seq) + ")");
+      break;
     }
     if (el < spin_us_) {
       sched_yield();
@@ -1604,6 +1747,9 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
   if (const char* sp = getenv("QMX_WAIT_SPIN_US")) spin_us_ = atoi(sp);
   if (const char* w = getenv("QMX_WAIT")) poll_ = std::string(w) != "event";
   if (const char* pu = getenv("QMX_POLL_US")) poll_us_ = std::max(1, atoi(pu));
+  if (const char* pe = getenv("QMX_PERSISTENT")) persistent_ = atoi(pe) != 0;
+  if (const char* pw = getenv("QMX_PERSISTENT_WG")) p_grid_ = std::min(std::max(8, atoi(pw)), 1024);
+  if (const char* pi = getenv("QMX_PERSISTENT_IDLE_MS")) p_idle_ms_ = std::min(std::max(5, atoi(pi)), 1000);
   HIP_CHECK(hipMalloc(&d_state_, sizeof(DevSlot) * (size_t)max_slots_));
   HIP_CHECK(hipMemset(d_state_, 0, sizeof(DevSlot) * (size_t)max_slots_));
   HIP_CHECK(hipMalloc(&d_content_, (size_t)content_cap_ * (size_t)max_slots_));
@@ -1648,7 +1794,11 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
     HIP_CHECK(hipMalloc((void**)&L->d_params, sizeof(KParams)));
     HIP_CHECK(hipMalloc((void**)&L->d_btpl, sizeof(BackendTpl) * 2 * kBackendTpl));
     HIP_CHECK(hipMemset(L->d_btpl, 0, sizeof(BackendTpl) * 2 * kBackendTpl));
-    HIP_CHECK(hipHostMalloc((void**)&L->h_params, sizeof(KParams), hipHostMallocDefault));
+    HIP_CHECK(hipHostMalloc((void**)&L->h_params, sizeof(KParams), hipHostMallocMapped));
+    HIP_CHECK(hipHostMalloc((void**)&L->h_door, sizeof(PDoor), hipHostMallocMapped));
+    std::memset((void*)L->h_door, 0, sizeof(PDoor));
+    HIP_CHECK(hipMalloc((void**)&L->d_ctl, sizeof(PCtl)));
+    HIP_CHECK(hipMemset(L->d_ctl, 0, sizeof(PCtl)));
     ensure_in(*L, 8u << 20);
     ensure_out(*L, 32u << 20);
     L->items_cap = 4096;
@@ -1662,7 +1812,13 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
 
 HipEngine::~HipEngine() {
   for (auto& L : lanes_) {
+    try {
+      stop_persistent(*L);
+    } catch (const std::exception&) {
+    }
     if (L->stream) hipStreamSynchronize(L->stream);
+    if (L->h_door) hipHostFree(L->h_door);
+    if (L->d_ctl) hipFree(L->d_ctl);
     if (L->h_in) hipHostFree(L->h_in);
     if (L->h_out) hipHostFree(L->h_out);
     if (L->h_items) hipHostFree(L->h_items);
@@ -1685,19 +1841,73 @@ HipEngine::~HipEngine() {
     if (L->evb) hipEventDestroy(L->evb);
     if (L->stream) hipStreamDestroy(L->stream);
   }
+  for (void* p : grave_host_) hipHostFree(p);
+  for (void* p : grave_dev_) hipFree(p);
   if (d_state_) hipFree(d_state_);
   if (d_content_) hipFree(d_content_);
 }
 
+void HipEngine::retire_host(void* p) {
+  std::lock_guard<std::mutex> g(grave_mu_);
+  grave_host_.push_back(p);
+}
+void HipEngine::retire_dev(void* p) {
+  std::lock_guard<std::mutex> g(grave_mu_);
+  grave_dev_.push_back(p);
+}
+
+void HipEngine::set_persistent(bool on) {
+  if (!on)
+    for (auto& L : lanes_) {
+      std::lock_guard<std::mutex> lg(L->mu);
+      stop_persistent(*L);
+    }
+  persistent_ = on;
+}
+
+uint32_t HipEngine::next_seq(TickLane& L) {
+  if (++L.seq == 0) ++L.seq;  // 0 never names a tick (fresh result records hold it)
+  return L.seq;
+}
+
+static double steady_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// The lane's grid is running and will see the next post: launch it when it is not running,
+// and replace it when it has been idle long enough that it may be exiting (the host never
+// posts to a grid within reach of its idle limit).
+void HipEngine::ensure_persistent(TickLane& L) {
+  if (L.p_running && steady_s() - L.p_last_post > 0.4e-3 * p_idle_ms_) stop_persistent(L);
+  if (L.p_running) return;
+  hipLaunchKernelGGL(qmx_tick_persistent, dim3(p_grid_), dim3(BS), 0, L.stream, (const PDoor*)L.h_door, L.d_ctl,
+                     d_state_, d_content_, L.seq, ++L.p_gen, (uint32_t)p_idle_ms_ * 100000u);
+  HIP_CHECK(hipGetLastError());
+  L.p_running = true;
+  L.p_last_post = steady_s();
+  ++L.p_launches;
+}
+
+// Post a stop tick and wait for the grid to leave (it finishes the tick it is on first).
+void HipEngine::stop_persistent(TickLane& L) {
+  if (!L.p_running) return;
+  const uint32_t s = next_seq(L);
+  L.h_door->d.stop = 1;
+  L.h_door->d.seq = s;
+  __atomic_store_n(&L.h_door->posted, s, __ATOMIC_RELEASE);
+  L.p_running = false;
+  HIP_CHECK(hipStreamSynchronize(L.stream));
+}
+
 void HipEngine::ensure_in(TickLane& L, size_t bytes) {
   if (bytes <= L.in_cap) return;
-  if (L.h_in) HIP_CHECK(hipHostFree(L.h_in));
+  if (L.h_in) retire_host(L.h_in);
   L.in_cap = std::max(bytes, L.in_cap * 2);
   HIP_CHECK(hipHostMalloc((void**)&L.h_in, L.in_cap + 64, hipHostMallocMapped));
 }
 void HipEngine::ensure_out(TickLane& L, size_t bytes) {
   if (bytes <= L.out_cap) return;
-  if (L.h_out) HIP_CHECK(hipHostFree(L.h_out));
+  if (L.h_out) retire_host(L.h_out);
   L.out_cap = std::max(bytes, L.out_cap * 2);
   HIP_CHECK(hipHostMalloc((void**)&L.h_out, L.out_cap + 64, hipHostMallocMapped));
 }
@@ -1809,8 +2019,8 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
   ensure_in(L, in_need + 64);
   ensure_out(L, out_need + 64);
   if (work.size() > L.items_cap) {
-    hipHostFree(L.h_items);
-    hipHostFree(L.h_res);
+    retire_host(L.h_items);
+    retire_host(L.h_res);
     L.items_cap = work.size() * 2;
     HIP_CHECK(hipHostMalloc((void**)&L.h_items, sizeof(WorkItem) * L.items_cap, hipHostMallocMapped));
     HIP_CHECK(hipHostMalloc((void**)&L.h_res, sizeof(WorkResult) * L.items_cap, hipHostMallocMapped));
@@ -1889,7 +2099,7 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
     L.params.dbg = nullptr;
     if (getenv("QMX_STAGE_TIMING")) {
       if (L.dbg_cap < (size_t)n) {
-        if (L.h_dbg) hipHostFree(L.h_dbg);
+        if (L.h_dbg) retire_host(L.h_dbg);
         L.dbg_cap = std::max((size_t)n, L.items_cap);
         HIP_CHECK(hipHostMalloc((void**)&L.h_dbg, sizeof(unsigned long long) * kDbg * L.dbg_cap, hipHostMallocMapped));
       }
@@ -1897,22 +2107,47 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
       L.params.dbg = L.h_dbg;
     }
     if (L.params.dbg != dbg0) L.params_dirty = true;
-    if (L.params_dirty) {  // stream-ordered before the launch; the pinned copy is not touched
-      std::memcpy(L.h_params, &L.params, sizeof(KParams));  // again until this tick completed
-      HIP_CHECK(hipMemcpyAsync(L.d_params, L.h_params, sizeof(KParams), hipMemcpyHostToDevice, L.stream));
+    const bool new_params = L.params_dirty;
+    if (L.params_dirty) {  // the pinned copy is not touched again until this tick completed
+      std::memcpy(L.h_params, &L.params, sizeof(KParams));
+      // one-shot launches: a stream-ordered upload; persistent: the grid copies it itself
+      if (!persistent_) HIP_CHECK(hipMemcpyAsync(L.d_params, L.h_params, sizeof(KParams), hipMemcpyHostToDevice, L.stream));
       L.params_dirty = false;
     }
     const auto tp1 = HC::now();
     L.host_prep_us += std::chrono::duration<double, std::micro>(tp1 - tp0).count();
     roctxRangePushA("qmx_tick");  // rocprofv3 --marker-trace: one range per tick launch + wait
     L.h2d_bytes += in_off;
-    const uint32_t seq = ++L.seq;
+    const bool persist = persistent_ && poll_;
+    if (persist) ensure_persistent(L);  // before the tick's sequence number: a relaunch starts from L.seq
+    const uint32_t seq = next_seq(L);
+    const uint32_t par = L.launches & 1;  // backend template table: read last tick's half, write the other
     if (!poll_) HIP_CHECK(hipEventRecord(L.ev0, L.stream));
     FinArgs fa{L.h_fin, L.h_fint, L.h_fin_in, L.d_join, L.d_fout, L.h_fout, L.h_finres, L.h_tl, (int2*)L.d_segs};
-    hipLaunchKernelGGL(qmx_tick_kernel, dim3(n + m), dim3(BS), 0, L.stream, L.h_items, L.h_in, L.h_out, L.h_res,
-                       d_state_, d_content_, L.d_params, seq, (uint32_t)n, fa,
-                       L.d_btpl + (size_t)((seq - 1) & 1) * kBackendTpl, L.d_btpl + (size_t)(seq & 1) * kBackendTpl);
-    HIP_CHECK(hipGetLastError());
+    if (persist) {
+      TickDesc& d = L.h_door->d;  // host-mapped: plain stores, then the release store of `posted`
+      d.items = L.h_items;
+      d.in = L.h_in;
+      d.out = L.h_out;
+      d.res = L.h_res;
+      d.params = L.d_params;
+      d.params_src = new_params ? L.h_params : nullptr;
+      d.btpl_rd = L.d_btpl + (size_t)(par ^ 1) * kBackendTpl;
+      d.btpl_wr = L.d_btpl + (size_t)par * kBackendTpl;
+      d.fa = fa;
+      d.seq = seq;
+      d.n_tick = (uint32_t)n;
+      d.n_fin = (uint32_t)m;
+      d.stop = 0;
+      __atomic_store_n(&L.h_door->posted, seq, __ATOMIC_RELEASE);
+      L.p_last_post = steady_s();
+      ++L.p_ticks;
+    } else {
+      hipLaunchKernelGGL(qmx_tick_kernel, dim3(n + m), dim3(BS), 0, L.stream, L.h_items, L.h_in, L.h_out, L.h_res,
+                         d_state_, d_content_, L.d_params, seq, (uint32_t)n, fa,
+                         L.d_btpl + (size_t)(par ^ 1) * kBackendTpl, L.d_btpl + (size_t)par * kBackendTpl);
+      HIP_CHECK(hipGetLastError());
+    }
     // sessions the GPU does not finalize (escalated streams) are finalized here meanwhile
     for (const FinalizeReq* r : fin_host) finalize_host(*r, fres);
     if (poll_) {
@@ -2044,15 +2279,15 @@ void HipEngine::finalize_host(const FinalizeReq& r, std::vector<FinalizeRes>& ou
 }
 
 template <class T>
-static void grow_mapped(T** p, size_t* cap, size_t need) {
+static void grow_mapped(HipEngine* e, T** p, size_t* cap, size_t need, void (HipEngine::*retire)(void*)) {
   if (need <= *cap) return;
-  if (*p) HIP_CHECK(hipHostFree(*p));
+  if (*p) (e->*retire)(*p);
   *cap = std::max(need, *cap * 2);
   HIP_CHECK(hipHostMalloc((void**)p, sizeof(T) * *cap + 64, hipHostMallocMapped));
 }
-static void grow_device(uint8_t** p, size_t* cap, size_t need) {
+static void grow_device(HipEngine* e, uint8_t** p, size_t* cap, size_t need, void (HipEngine::*retire)(void*)) {
   if (need <= *cap) return;
-  if (*p) HIP_CHECK(hipFree(*p));
+  if (*p) (e->*retire)(*p);
   *cap = std::max(need, *cap * 2);
   HIP_CHECK(hipMalloc((void**)p, *cap + 64));
 }
@@ -2079,11 +2314,11 @@ std::vector<const FinalizeReq*> HipEngine::prep_finalize(TickLane& L, std::vecto
   }
   if (gpu.empty()) return gpu;
   const int n = (int)gpu.size();
-  grow_mapped(&L.h_fin, &L.fin_cap, (size_t)n);
-  grow_mapped(&L.h_finres, &L.finres_cap, (size_t)n);
-  grow_mapped(&L.h_fint, &L.fint_cap, ntext);
-  grow_mapped(&L.h_tl, &L.tl_cap, ntext);
-  grow_mapped(&L.h_fin_in, &L.fin_in_cap, in_bytes);
+  grow_mapped(this, &L.h_fin, &L.fin_cap, (size_t)n, &HipEngine::retire_host);
+  grow_mapped(this, &L.h_finres, &L.finres_cap, (size_t)n, &HipEngine::retire_host);
+  grow_mapped(this, &L.h_fint, &L.fint_cap, ntext, &HipEngine::retire_host);
+  grow_mapped(this, &L.h_tl, &L.tl_cap, ntext, &HipEngine::retire_host);
+  grow_mapped(this, &L.h_fin_in, &L.fin_in_cap, in_bytes, &HipEngine::retire_host);
   size_t join_off = 0, out_off = 0, in_off = 0, t_off = 0, seg_off = 0;
   const std::string suf = kFinalSuffix;
   for (int i = 0; i < n; ++i) {
@@ -2125,10 +2360,10 @@ std::vector<const FinalizeReq*> HipEngine::prep_finalize(TickLane& L, std::vecto
     it.out_cap = (uint32_t)cap;
     out_off += (cap + 15) & ~(size_t)15;
   }
-  grow_device(&L.d_join, &L.join_cap, join_off + 16);
-  grow_device(&L.d_fout, &L.dfout_cap, out_off + 16);
-  grow_device(&L.d_segs, &L.segs_cap, seg_off * sizeof(int2) + 16);
-  grow_mapped(&L.h_fout, &L.fout_cap, out_off + 16);
+  grow_device(this, &L.d_join, &L.join_cap, join_off + 16, &HipEngine::retire_dev);
+  grow_device(this, &L.d_fout, &L.dfout_cap, out_off + 16, &HipEngine::retire_dev);
+  grow_device(this, &L.d_segs, &L.segs_cap, seg_off * sizeof(int2) + 16, &HipEngine::retire_dev);
+  grow_mapped(this, &L.h_fout, &L.fout_cap, out_off + 16, &HipEngine::retire_host);
   return gpu;
 }
 
@@ -2169,6 +2404,8 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     TickLane& L = *Lp;
     std::lock_guard<std::mutex> lg(L.mu);
     m["launches"] += (double)L.launches;
+    m["persistent_grids"] += (double)L.p_launches;  // persistent mode: grid launches (ticks ride doorbells)
+    m["persistent_ticks"] += (double)L.p_ticks;
     m["items"] += (double)L.items;
     m["kernel_ms"] += L.kernel_ms;
     m["stage_items"] += (double)L.stage_n;

@@ -526,9 +526,13 @@ class GpuHub {
   using Sink = std::function<void(ResultBatch&&)>;
   GpuHub(const ServerCfg& cfg, int nloops) : cfg_(cfg), sinks_(nloops) {
     lanes_ = std::max(1, std::min(cfg.tick_lanes, 8));
-    if (cfg.engine == "hip")
-      eng_.reset(new HipEngine(cfg.tags, cfg.device, cfg.tile, cfg.max_slots, cfg.content_cap, lanes_));
-    else
+    if (cfg.engine == "hip") {
+      HipEngine* he = new HipEngine(cfg.tags, cfg.device, cfg.tile, cfg.max_slots, cfg.content_cap, lanes_);
+      eng_.reset(he);
+      // spread placement writes remote final texts into the content arena with RCCL / DMA:
+      // one-shot launches (each launch's acquire) keep those visible
+      if (cfg.world > 1 && cfg.placement == "spread" && he->persistent()) he->set_persistent(false);
+    } else
       eng_.reset(new CpuEngine(cfg.tags));  // shared CPU engine: exercises the hub routing on CPU
     if (cfg.verify) ver_.reset(new Verifier(cfg.tags));
   }

@@ -7,6 +7,7 @@
 #
 # steps:
 #   tests                 pytest -m gpu (HIP engine vs C++ oracle, HIP server with verify mode)
+#   pytest:F1,F2          selected GPU test files only
 #   smoke                 __graft_entry__.smoke()
 #   bench[=N]             headline bench.py N times (default 1)            -> bench_<i>.json
 #   bench:ARGS            one bench.py run with extra args (commas = spaces) -> bench_<slug>.json
@@ -66,6 +67,13 @@ for step in "$@"; do
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
         > $OUT/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -40 $OUT/gpu_tests.log; exit 1; }
       tail -3 $OUT/gpu_tests.log ;;
+    pytest:*)  # selected GPU test files (commas = spaces), before the full suite
+      f=${step#pytest:}; slug=$(echo "$f" | tr -c 'a-zA-Z0-9' '_' | cut -c1-60)
+      timeout -k 10 600 python -u -m pytest ${f//,/ } -x -v --timeout 120 --timeout-method thread \
+        > $OUT/pytest_$slug.log 2>&1 || { echo "pytest $f failed"; tail -40 $OUT/pytest_$slug.log; exit 1; }
+      tail -3 $OUT/pytest_$slug.log ;;
+    fdprobe)  # which bench-rank step opens a GPU device file
+      timeout -k 10 120 python tools/probes/fd_probe.py > $OUT/fdprobe.log 2>&1; cat $OUT/fdprobe.log ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 \
         || { echo "smoke failed"; tail -20 $OUT/smoke.log; exit 1; }
