@@ -1571,6 +1571,10 @@ struct TickDesc {
 struct PDoor {  // host-mapped: written by the host, polled by workgroup 0
   TickDesc d;
   alignas(64) uint32_t posted;
+  // written by workgroup 0 (diagnostics: the host reports them when a tick goes missing)
+  alignas(64) uint32_t relayed;  // last tick relayed
+  uint32_t exits;                // last grid exit: reason << 16 | launch generation (1 idle, 2 stop)
+  uint32_t idle_limit_hit_us;    // the idle time that triggered the last idle exit, us
 };
 struct PCtl {  // device memory: written by workgroup 0, polled by the others
   TickDesc d;
@@ -1578,7 +1582,10 @@ struct PCtl {  // device memory: written by workgroup 0, polled by the others
   uint32_t exit_gen;
 };
 
-__global__ __launch_bounds__(BS) void qmx_tick_persistent(const PDoor* __restrict__ door, PCtl* __restrict__ ctl,
+// `door` / `ctl` are neither const nor __restrict__ and their words are read with atomic
+// loads: a readonly noalias kernel argument may be read through the scalar cache, which no
+// acquire fence invalidates — the next tick's descriptor would come back stale.
+__global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* door, PCtl* ctl,
                                                           DevSlot* __restrict__ state, uint8_t* __restrict__ content,
                                                           uint32_t seq0, uint32_t gen, uint32_t idle_ticks) {
   __shared__ TickLds U;
@@ -1596,9 +1603,10 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(const PDoor* __restric
           const uint32_t v = __hip_atomic_load(&door->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           if ((int32_t)(v - last) > 0) {  // newer only: a control word left by an earlier launch is older
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the descriptor written before `posted`
-            const uint32_t* src = (const uint32_t*)&door->d;
+            uint32_t* src = (uint32_t*)&door->d;
             uint32_t* dst = (uint32_t*)&D;
-            for (int i = 0; i < (int)(sizeof(TickDesc) / 4); ++i) dst[i] = src[i];
+            for (int i = 0; i < (int)(sizeof(TickDesc) / 4); ++i)
+              dst[i] = __hip_atomic_load(&src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             c = v;
             break;
           }
@@ -1606,14 +1614,22 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(const PDoor* __restric
           const uint32_t v = __hip_atomic_load(&ctl->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if ((int32_t)(v - last) > 0) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            D = ctl->d;
+            uint32_t* src = (uint32_t*)&ctl->d;
+            uint32_t* dst = (uint32_t*)&D;
+            for (int i = 0; i < (int)(sizeof(TickDesc) / 4); ++i)
+              dst[i] = __hip_atomic_load(&src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             c = v;
             break;
           }
           if (__hip_atomic_load(&ctl->exit_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) break;
         }
-        if (__builtin_amdgcn_s_memrealtime() - t_idle > limit) {
-          if (relay) __hip_atomic_store(&ctl->exit_gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t idle = __builtin_amdgcn_s_memrealtime() - t_idle;
+        if (idle > limit) {
+          if (relay) {
+            __hip_atomic_store(&ctl->exit_gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&door->idle_limit_hit_us, (uint32_t)(idle / 100), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&door->exits, (1u << 16) | (gen & 0xffffu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
           break;
         }
         __builtin_amdgcn_s_sleep(8);
@@ -1627,11 +1643,17 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(const PDoor* __restric
       // the tick is published to the other workgroups (agent-scope release)
       if (D.params_src != nullptr && !D.stop)
         for (int i = threadIdx.x; i < (int)(sizeof(KParams) / 4); i += BS)
-          ((uint32_t*)D.params)[i] = ((const uint32_t*)D.params_src)[i];
+          ((uint32_t*)D.params)[i] =
+              __hip_atomic_load((uint32_t*)D.params_src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __threadfence();
       __syncthreads();
       if (threadIdx.x == 0) {
-        ctl->d = D;
+        __hip_atomic_store(&door->relayed, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (D.stop) __hip_atomic_store(&door->exits, (2u << 16) | (gen & 0xffffu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        uint32_t* src = (uint32_t*)&D;
+        uint32_t* dst = (uint32_t*)&ctl->d;
+        for (int i = 0; i < (int)(sizeof(TickDesc) / 4); ++i)
+          __hip_atomic_store(&dst[i], src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&ctl->seq, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -1654,6 +1676,11 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(const PDoor* __restric
     const int total = (int)(n_tick + __builtin_amdgcn_readfirstlane(D.n_fin));
     const uint32_t seq = __builtin_amdgcn_readfirstlane(D.seq);
     for (int k = (int)blockIdx.x; k < total; k += (int)gridDim.x) {
+      // a visible clobber: the host rewrites items, tile bytes and finalize descriptors
+      // between ticks, so none of them may be read through the scalar cache as
+      // launch-invariant data (which the compiler does for uniform addresses it proves
+      // unclobbered within the kernel)
+      asm volatile("" ::: "memory");
       run_item(k, uni(D.items), uni(D.in), uni(D.out), uni(D.res), state, content, *uni(D.params), seq, n_tick, fa,
                uni(D.btpl_rd), uni(D.btpl_wr), U);
       __syncthreads();  // LDS is reused by the next item
@@ -1710,12 +1737,23 @@ void HipEngine::wait_results(TickLane& L, int n, int m, uint32_t seq) {
   nap(0.6 * L.ema_us - 6.0);
   while (!done(i)) {
     const double el = std::chrono::duration<double, std::micro>(HC::now() - t0).count();
-    if (el > 4.0 * L.ema_us + 2000.0) {
+    // a persistent grid is only stopped to surface a fault: a tick it has not reached yet
+    // (first launch loading the code object, a long finalize) would be lost to the stop
+    if (el > (L.p_running ? 1e6 : 4.0 * L.ema_us + 2000.0)) {
       if (L.p_running) stop_persistent(L);  // the grid leaves after this tick; throws on a fault
       else HIP_CHECK(hipStreamSynchronize(L.stream));  // throws on a kernel fault
       ++L.poll_fallbacks;
       // the stream has drained: every result is final — or the tick was never run
-      if (!done(i)) throw std::runtime_error("tick results missing after the lane drained (seq " + std::to_string(seq) + ")");
+      if (!done(i)) {
+        std::string why = "tick results missing after the lane drained (seq " + std::to_string(seq) + ", " +
+                          std::to_string(i) + "/" + std::to_string(n + m) + " published";
+        if (L.h_door)
+          why += "; grid: relayed " + std::to_string(__atomic_load_n(&L.h_door->relayed, __ATOMIC_ACQUIRE)) +
+                 ", exits " + std::to_string(L.h_door->exits) + ", last idle exit after " +
+                 std::to_string(L.h_door->idle_limit_hit_us) + " us, launches " + std::to_string(L.p_launches) +
+                 ", posted " + std::to_string(L.h_door->posted);
+        throw std::runtime_error(why + ")");
+      }
       break;
     }
     if (el < spin_us_) {
@@ -1880,7 +1918,7 @@ static double steady_s() {
 void HipEngine::ensure_persistent(TickLane& L) {
   if (L.p_running && steady_s() - L.p_last_post > 0.4e-3 * p_idle_ms_) stop_persistent(L);
   if (L.p_running) return;
-  hipLaunchKernelGGL(qmx_tick_persistent, dim3(p_grid_), dim3(BS), 0, L.stream, (const PDoor*)L.h_door, L.d_ctl,
+  hipLaunchKernelGGL(qmx_tick_persistent, dim3(p_grid_), dim3(BS), 0, L.stream, L.h_door, L.d_ctl,
                      d_state_, d_content_, L.seq, ++L.p_gen, (uint32_t)p_idle_ms_ * 100000u);
   HIP_CHECK(hipGetLastError());
   L.p_running = true;
@@ -2006,9 +2044,14 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
     bool eof_sent;
     Work* w;
   };
-  std::vector<Pending> pend;
-  pend.reserve(work.size());
-  std::vector<int> requeue;
+  // per-thread scratch reused from tick to tick (a lane is driven by one thread at a time)
+  thread_local std::vector<Pending> pend;
+  thread_local std::vector<int> requeue;
+  thread_local std::vector<Work*> order;
+  thread_local std::vector<Work*> b[8];
+  pend.clear();
+  requeue.clear();
+  order.clear();
   size_t in_need = 0, out_need = 0;
   for (auto& w : work) {
     size_t tot = core_[w.slot].carry.size() + w.data.size();
@@ -2030,10 +2073,8 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
   // XCD-aware item order: the dispatcher hands workgroup i to XCD i % 8, so item i gets a
   // stream with slot % 8 == i % 8 where possible — a stream's DevSlot state, template and
   // content-arena tail stay in one XCD's L2 from tick to tick.  Host-path streams first.
-  std::vector<Work*> order;
-  order.reserve(work.size());
   {
-    std::vector<Work*> b[8];
+    for (auto& q : b) q.clear();
     for (auto& w : work) {
       if (w.slot >= max_slots_ || host_mode_[w.slot]) order.push_back(&w);
       else b[w.slot & 7].push_back(&w);
@@ -2207,24 +2248,23 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
     SlotCore& c = core_[p.slot];
     const WorkResult r = L.h_res[i];
     Work& w = *p.w;
-    // rebuild the unconsumed remainder: (carry + data)[consumed:]
-    auto remainder = [&](size_t consumed) {
-      std::string rem;
-      size_t cl = p.carry_len;
+    // the unconsumed remainder (carry + data)[consumed:] becomes the carry, in place
+    auto keep_remainder = [&](size_t consumed) {
+      const size_t cl = p.carry_len;
       if (consumed < cl) {
-        rem.assign(c.carry, consumed, std::string::npos);
-        rem += w.data;
+        c.carry.erase(0, consumed);
+        c.carry += w.data;
       } else {
-        rem.assign(w.data, consumed - cl, std::string::npos);
+        c.carry.assign(w.data, consumed - cl, std::string::npos);
       }
-      return rem;
     };
     bool no_progress = (r.status & WS_ESCALATE) ||
                        (p.submitted == (size_t)tile_ && r.consumed == 0 && !(r.status & (WS_DONE | WS_ABORTED)));
     if (no_progress) {
       escalate(p.slot, w.fresh);
-      std::string all = remainder(0);
-      c.carry.clear();
+      keep_remainder(0);
+      std::string all;
+      all.swap(c.carry);
       bool was_closed = c.done || c.aborted;
       std::string o;
       process_slot(ts_, c, (const uint8_t*)all.data(), all.size(), w.eof, created, o);
@@ -2240,7 +2280,7 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
       c.carry.clear();
       flags |= RF_ABORTED;
     } else {
-      c.carry = remainder(r.consumed);
+      keep_remainder(r.consumed);
       if (r.status & WS_DONE) {
         c.done = true;
         c.carry.clear();
