@@ -80,7 +80,7 @@ def test_persistent_two_lanes(persistent):
     n = len(streams)
     cpu = H.run_engine(NativeEngine("cpu", tags), streams, [True] * n, [True] * n, random.Random(2))
     eng = NativeEngine("hip", tags, device=0, lanes=2)
-    slots = [eng.open(i % 5, True, True) for i in range(n)]
+    slots = [eng.open(i % 7, True, True) for i in range(n)]  # the harness's backend indices
     out = {s: b"" for s in slots}
     cur = [0] * n
     lane = 0
