@@ -1593,8 +1593,11 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* door, PCtl* ctl
   __shared__ uint32_t cmd;  // new tick's sequence number, 0: exit
   uint32_t last = seq0;     // the value the host posted last before this launch
   const bool relay = blockIdx.x == 0;
+  constexpr int kWords = (int)(sizeof(TickDesc) / 4);
+  static_assert(kWords <= 64, "the descriptor is copied by one wave, a word per lane");
+  const int tid = threadIdx.x;
   for (;;) {
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
       const uint64_t t_idle = __builtin_amdgcn_s_memrealtime();
       const uint64_t limit = relay ? (uint64_t)idle_ticks : 2ull * idle_ticks;
       uint32_t c = 0;
@@ -1602,22 +1605,12 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* door, PCtl* ctl
         if (relay) {
           const uint32_t v = __hip_atomic_load(&door->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           if ((int32_t)(v - last) > 0) {  // newer only: a control word left by an earlier launch is older
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the descriptor written before `posted`
-            uint32_t* src = (uint32_t*)&door->d;
-            uint32_t* dst = (uint32_t*)&D;
-            for (int i = 0; i < (int)(sizeof(TickDesc) / 4); ++i)
-              dst[i] = __hip_atomic_load(&src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             c = v;
             break;
           }
         } else {
           const uint32_t v = __hip_atomic_load(&ctl->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if ((int32_t)(v - last) > 0) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            uint32_t* src = (uint32_t*)&ctl->d;
-            uint32_t* dst = (uint32_t*)&D;
-            for (int i = 0; i < (int)(sizeof(TickDesc) / 4); ++i)
-              dst[i] = __hip_atomic_load(&src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             c = v;
             break;
           }
@@ -1638,28 +1631,44 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* door, PCtl* ctl
     }
     __syncthreads();
     const uint32_t c = cmd;
-    if (relay && c != 0) {
+    if (c == 0) return;
+    // the descriptor: a word per lane of wave 0, all loads in flight at once (one round trip
+    // to host memory / the coherence point, not one per word)
+    if (tid < kWords) {
+      uint32_t w;
+      if (relay) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // written by the host before `posted`
+        w = __hip_atomic_load((uint32_t*)&door->d + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      } else {
+        // system scope (not just agent): this is also the workgroup's acquire of the tick's
+        // host-written items / tile bytes and of other XCDs' slot state — one cache
+        // invalidation per workgroup (the caches are per CU / per XCD), not one per wave
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        w = __hip_atomic_load((uint32_t*)&ctl->d + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      ((uint32_t*)&D)[tid] = w;
+    }
+    __syncthreads();
+    if (relay) {
       // new kernel parameters (about once a second): copied by this workgroup's threads, then
       // the tick is published to the other workgroups (agent-scope release)
       if (D.params_src != nullptr && !D.stop)
-        for (int i = threadIdx.x; i < (int)(sizeof(KParams) / 4); i += BS)
+        for (int i = tid; i < (int)(sizeof(KParams) / 4); i += BS)
           ((uint32_t*)D.params)[i] =
               __hip_atomic_load((uint32_t*)D.params_src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (tid < kWords)
+        __hip_atomic_store((uint32_t*)&ctl->d + tid, ((const uint32_t*)&D)[tid], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
       __threadfence();
       __syncthreads();
-      if (threadIdx.x == 0) {
+      if (tid == 0) {
         __hip_atomic_store(&door->relayed, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (D.stop) __hip_atomic_store(&door->exits, (2u << 16) | (gen & 0xffffu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        uint32_t* src = (uint32_t*)&D;
-        uint32_t* dst = (uint32_t*)&ctl->d;
-        for (int i = 0; i < (int)(sizeof(TickDesc) / 4); ++i)
-          __hip_atomic_store(&dst[i], src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&ctl->seq, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    if (c == 0 || D.stop) return;  // D is block-uniform (LDS, written before the barrier)
-    last = c;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope, every thread: see the header
+    if (D.stop) return;  // D is block-uniform (LDS, written before the barrier)
+    last = c;  // (the tick's acquire: wave 0's fence above, ordered before every wave by the barrier)
     // descriptor fields read from LDS land in VGPRs: make them wave-uniform scalars again
     // (as kernel arguments are), or every address derived from them costs vector registers
     FinArgs fa;

@@ -1136,23 +1136,28 @@ class Loop {
         if (c->in.size() > (1 << 20)) c->dead = true;
         return;
       }
-      std::string head = c->in.substr(0, he);
-      size_t le = head.find("\r\n");
-      std::string rl = head.substr(0, le);
-      size_t sp1 = rl.find(' '), sp2 = rl.rfind(' ');
-      if (sp1 == std::string::npos || sp2 == sp1) {
+      // request line and headers parsed in place (no copy of the head)
+      const char* head = c->in.data();
+      const size_t le0 = c->in.find("\r\n");
+      const size_t le = le0 == std::string::npos || le0 > he ? he : le0;
+      const char* sp1p = (const char*)memchr(head, ' ', le);
+      const char* sp2p = (const char*)memrchr(head, ' ', le);
+      if (!sp1p || sp2p == sp1p) {
         c->dead = true;
         return;
       }
-      std::string method = rl.substr(0, sp1), target = rl.substr(sp1 + 1, sp2 - sp1 - 1),
-                  version = rl.substr(sp2 + 1);
+      const size_t sp1 = (size_t)(sp1p - head), sp2 = (size_t)(sp2p - head);
+      thread_local std::string method, target;
+      method.assign(head, sp1);
+      target.assign(head + sp1 + 1, sp2 - sp1 - 1);
+      const bool http10 = le - sp2 - 1 == 8 && memcmp(head + sp2 + 1, "HTTP/1.0", 8) == 0;
       std::vector<std::pair<std::string, std::string>> hdrs;
       hdrs.reserve(12);
-      size_t pos = le == std::string::npos ? head.size() : le + 2;
+      const size_t pos = le + 2;
       long clen = 0;
       bool chunked = false;
-      bool keepalive = version != "HTTP/1.0";
-      for_each_header(head.data() + pos, head.size() - std::min(pos, head.size()), [&](std::string&& k, std::string&& v) {
+      bool keepalive = !http10;
+      for_each_header(head + std::min(pos, he), he - std::min(pos, he), [&](std::string&& k, std::string&& v) {
         if (k == "content-length") clen = atol(v.c_str());
         if (k == "transfer-encoding" && icontains(v, "chunked")) chunked = true;
         if (k == "connection") {
@@ -1257,7 +1262,7 @@ class Loop {
       if (h.first == "content-length" || h.first == "transfer-encoding" || h.first == "connection" ||
           h.first == "keep-alive" || h.first == "te" || h.first == "upgrade" || h.first == "accept-encoding")
         continue;
-      s->fwd.push_back(h);
+      s->fwd.push_back(std::move(h));  // hdrs is not read again
     }
     if (!has_auth) {
       std::string env_key = cfg_.env_api_key;
@@ -1275,9 +1280,12 @@ class Loop {
     }
     s->fwd.emplace_back("Authorization", s->auth);
     if (!has_ctype) s->fwd.emplace_back("Content-Type", "application/json");
-    std::vector<int> valid;
-    for (int i = 0; i < (int)cfg_.backends.size(); ++i)
-      if (cfg_.backends[i].valid) valid.push_back(i);
+    if (!valid_init_) {
+      valid_init_ = true;
+      for (int i = 0; i < (int)cfg_.backends.size(); ++i)
+        if (cfg_.backends[i].valid) valid_.push_back(i);
+    }
+    const std::vector<int>& valid = valid_;
     if (valid.empty())
       return respond(c, 500, "application/json", err_json("No valid backends configured", "configuration_error"));
     if (!s->body.get("model")) {
@@ -2517,6 +2525,8 @@ class Loop {
   const std::vector<Loop*>* loops_ = nullptr;
   double last_snap_ = 0;
   int xfd_ = -1;
+  std::vector<int> valid_;  // backends with a URL (config order), computed once
+  bool valid_init_ = false;
   std::mutex xmu_;
   std::vector<XMsg> xin_;
   uint64_t next_skey_ = 1;

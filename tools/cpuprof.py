@@ -27,7 +27,7 @@ CATEGORIES = [
     ("accept/close/socket", r"accept|^close$|__close|socket|setsockopt|connect"),
     ("allocator", r"malloc|free|operator new|operator delete|_int_malloc|_int_free|realloc|cfree"),
     ("memcpy/memmove/memset", r"memcpy|memmove|memset|memchr|memmem|memcmp|strlen"),
-    ("HIP runtime", r"^hip|amd::|roc|hsa_|Hip|libamdhip64|libhsa"),
+    ("HIP runtime", r"^hip|amd::|^roc|hsa_|^Hip|libamdhip64|libhsa"),
     ("json", r"json|JVal|py_float_repr"),
     ("engine host", r"HostEngine|CpuEngine|HipEngine|process_slot|filter_feed|classify|escape|strip_final|finalize"),
     ("http/proxy", r"qmx::|Loop::|Session|http|parse"),

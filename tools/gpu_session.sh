@@ -120,6 +120,14 @@ for l in open('$OUT/kbench.jsonl'):
     d=json.loads(l); st=d.get('stage_us_per_item',{})
     print(d.get('filter'),d.get('emit'),d['slots'],d['wall_us_p50'],d['kernel_us_avg'],[st.get('stage%d_us'%k) for k in range(1,11)])
 " ;;
+    gpuprocs=*)  # which processes hold the GPU during an N-rank rehearsal (N <= 4 keeps it under the limit)
+      n=${step#gpuprocs=}
+      python tools/probes/gpu_procs.py $OUT/gpuprocs_$n.txt 60 &
+      mon=$!
+      torchrun_bench gpuprocs_$n $n --steps 5 --warmup 1 --threads 2 --batch 4096; rc=$?
+      kill $mon 2>/dev/null; wait $mon 2>/dev/null
+      cat $OUT/gpuprocs_$n.txt
+      [ $rc -eq 0 ] || exit 1 ;;
     multirank=*)
       n=${step#multirank=}; torchrun_bench multirank_$n $n --steps 5 --warmup 1 --threads 2 --batch 4096 || exit 1 ;;
     spread=*)
