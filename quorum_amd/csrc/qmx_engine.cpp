@@ -311,17 +311,29 @@ int HostEngine::open(int index, bool filter, bool emit, uint32_t* gen) {
     meta_.emplace_back();
     core_.emplace_back();
   }
+  // reset in place: a reused slot keeps its (small) buffers, so a new session costs no
+  // allocation under the engine lock
+  auto recycle = [](std::string& x) {
+    if (x.capacity() > (64u << 10)) std::string().swap(x);
+    else x.clear();
+  };
   Meta& m = meta_[slot];
-  const uint32_t ng = m.gen + 1;
-  m = Meta();
+  m.gen += 1;
   m.live = true;
-  m.gen = ng;
-  if (gen) *gen = ng;
+  m.dirty = m.eof = m.closed = m.busy = false;
+  m.fresh = true;
+  recycle(m.incoming);
+  if (gen) *gen = m.gen;
   SlotCore& c = core_[slot];
-  c = SlotCore();
-  c.index = index;
   c.filter = filter;
   c.emit = emit;
+  c.started = c.aborted = c.done = false;
+  c.index = index;
+  recycle(c.carry);
+  c.fs = FilterState();
+  recycle(c.content);
+  recycle(c.tpl_pre);
+  recycle(c.tpl_suf);
   return slot;
 }
 
@@ -412,11 +424,16 @@ bool HostEngine::has_work() {
 
 bool HostEngine::tick(int64_t created, std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres, int lane,
                       std::vector<int>* taken) {
-  std::vector<Work> work;
-  std::vector<FinalizeReq> fin;
+  // per-thread scratch reused from tick to tick (a tick thread drives one lane)
+  thread_local std::vector<Work> work;
+  thread_local std::vector<FinalizeReq> fin;
+  thread_local std::vector<int> keep, slots;
+  work.clear();
+  fin.clear();
+  keep.clear();
+  slots.clear();
   {
     std::lock_guard<std::mutex> g(mu_);
-    std::vector<int> keep;
     for (int s : pending_free_) {
       if (meta_[s].busy) {  // still in flight on another lane: free it once settled
         keep.push_back(s);
@@ -450,7 +467,6 @@ bool HostEngine::tick(int64_t created, std::vector<SlotResult>& results, std::ve
   run_tick(work, fin, created, results, fres, lane);
   size_t out = 0;
   for (auto& r : results) out += r.sse.size();
-  std::vector<int> slots;
   std::vector<int>& tk = taken ? *taken : slots;
   for (auto& w : work) tk.push_back(w.slot);
   {
