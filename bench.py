@@ -69,6 +69,25 @@ SCENARIOS = {
 }
 
 
+def _gpu_held() -> bool:
+    """Does this process hold the GPU (a KFD process entry or an open device file)?"""
+    if os.path.exists(f"/sys/class/kfd/kfd/proc/{os.getpid()}"):
+        return True
+    try:
+        for fd in os.listdir("/proc/self/fd"):
+            t = os.readlink(f"/proc/self/fd/{fd}")
+            if t == "/dev/kfd" or t.startswith("/dev/dri/"):
+                return True
+    except OSError:
+        pass
+    return False
+
+
+def _trace(stage: str) -> None:
+    if os.environ.get("QMX_BENCH_FDTRACE"):
+        print(f"bench rank {os.environ.get('RANK', '0')}: {stage}: gpu held {_gpu_held()}", file=sys.stderr, flush=True)
+
+
 def _kill(procs):
     for p in procs:
         try:
@@ -421,6 +440,7 @@ def main() -> int:
 
     import torch
 
+    _trace("import torch")
     # QMX_BENCH_NDEV: a rehearsal names the GPU count itself, so the bench processes never
     # open the device (a box counts every process holding it open)
     n_dev = int(os.environ["QMX_BENCH_NDEV"]) if os.environ.get("QMX_BENCH_NDEV") else torch.cuda.device_count()
@@ -429,6 +449,7 @@ def main() -> int:
     # refuses two ranks on one GPU) and keeps the bench processes themselves off the GPU:
     # they do no GPU work (the native workers do), and a box admits 16 GPU processes
     use_cuda = n_dev >= world and n_dev > 0 and torch.cuda.is_available()
+    _trace("device count")
     device = local_rank % n_dev if n_dev else None
     coll_cuda = use_cuda
     dist = None
@@ -436,6 +457,7 @@ def main() -> int:
         import torch.distributed as dist  # noqa: F811
 
         dist.init_process_group("nccl" if coll_cuda else "gloo")
+    _trace("init_process_group")
     if use_cuda:
         torch.cuda.set_device(device)
     try:
@@ -482,9 +504,11 @@ def main() -> int:
             proxy_procs = spawn_workers(cfg_path, "127.0.0.1", args.port, args.workers, engine,
                                         device, impl=args.impl, threads=args.threads, env=env)
         procs += proxy_procs
+        _trace("workers spawned")
         if not wait_healthy("127.0.0.1", proxy_port, 180):
             raise RuntimeError(f"proxy did not become healthy: {[exit_status(p) for p in proxy_procs]}")
         xchg_kind = os.environ.get("QMX_XCHG", "rccl" if engine == "hip" else "tcp")
+        _trace("healthy")
         if dist is not None:
             dist.barrier()
         # the reference has no /v1 prefix (oai_proxy.py:959); qmx serves both

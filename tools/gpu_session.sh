@@ -8,6 +8,7 @@
 # steps:
 #   tests                 pytest -m gpu (HIP engine vs C++ oracle, HIP server with verify mode)
 #   pytest:F1,F2          selected GPU test files only
+#   envtests:V=X,...      the whole GPU suite under extra env
 #   smoke                 __graft_entry__.smoke()
 #   bench[=N]             headline bench.py N times (default 1)            -> bench_<i>.json
 #   bench:ARGS            one bench.py run with extra args (commas = spaces) -> bench_<slug>.json
@@ -67,6 +68,11 @@ for step in "$@"; do
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
         > $OUT/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -40 $OUT/gpu_tests.log; exit 1; }
       tail -3 $OUT/gpu_tests.log ;;
+    envtests:*)  # the whole GPU suite under extra env (commas = spaces), e.g. envtests:QMX_PERSISTENT=1
+      e=${step#envtests:}; slug=$(echo "$e" | tr -c 'a-zA-Z0-9' '_' | cut -c1-60)
+      env ${e//,/ } timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        > $OUT/gpu_tests_$slug.log 2>&1 || { echo "gpu tests ($e) failed"; tail -40 $OUT/gpu_tests_$slug.log; exit 1; }
+      tail -3 $OUT/gpu_tests_$slug.log ;;
     pytest:*)  # selected GPU test files (commas = spaces), before the full suite
       f=${step#pytest:}; slug=$(echo "$f" | tr -c 'a-zA-Z0-9' '_' | cut -c1-60)
       timeout -k 10 600 python -u -m pytest ${f//,/ } -x -v --timeout 120 --timeout-method thread \
@@ -124,7 +130,8 @@ for l in open('$OUT/kbench.jsonl'):
       n=${step#gpuprocs=}
       python tools/probes/gpu_procs.py $OUT/gpuprocs_$n.txt 60 &
       mon=$!
-      torchrun_bench gpuprocs_$n $n --steps 5 --warmup 1 --threads 2 --batch 4096; rc=$?
+      QMX_BENCH_FDTRACE=1 torchrun_bench gpuprocs_$n $n --steps 5 --warmup 1 --threads 2 --batch 4096; rc=$?
+      grep "gpu held" $OUT/gpuprocs_$n.err | sort | uniq -c | head -20
       kill $mon 2>/dev/null; wait $mon 2>/dev/null
       cat $OUT/gpuprocs_$n.txt
       [ $rc -eq 0 ] || exit 1 ;;
