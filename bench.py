@@ -88,6 +88,25 @@ def _trace(stage: str) -> None:
         print(f"bench rank {os.environ.get('RANK', '0')}: {stage}: gpu held {_gpu_held()}", file=sys.stderr, flush=True)
 
 
+def _trace_watch() -> None:
+    """QMX_BENCH_FDTRACE: report the main thread's stack when this process first holds the GPU."""
+    if not os.environ.get("QMX_BENCH_FDTRACE"):
+        return
+    import threading
+    import traceback
+
+    main = threading.main_thread().ident
+
+    def watch():
+        while not _gpu_held():
+            time.sleep(0.05)
+        fr = sys._current_frames().get(main)
+        print(f"bench rank {os.environ.get('RANK', '0')}: GPU first held at:\n" + "".join(traceback.format_stack(fr)),
+              file=sys.stderr, flush=True)
+
+    threading.Thread(target=watch, daemon=True).start()
+
+
 def _kill(procs):
     for p in procs:
         try:
@@ -438,6 +457,7 @@ def main() -> int:
     if args.threads <= 0:
         args.threads = max(2, min(8, available_cores() // (2 * world)))
 
+    _trace_watch()
     import torch
 
     _trace("import torch")

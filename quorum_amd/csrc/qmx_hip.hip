@@ -60,10 +60,12 @@ constexpr int kDbg = 20;  // QMX_STAGE_TIMING record per work item: stamps 0-12,
 typedef int v4i __attribute__((ext_vector_type(4)));
 
 // optional per-stage wall-clock stamps (s_memrealtime, 100 MHz) written by thread 0
+// (reads the LDS copy P of the kernel parameters: a persistent grid's parameters are not
+// launch-invariant, so reading them from memory at every use would cost vector registers)
 #define QMX_STAMP(k)                                               \
   do {                                                             \
-    if (Pk.dbg != nullptr && threadIdx.x == 0)                     \
-      Pk.dbg[bi * kDbg + (k)] = __builtin_amdgcn_s_memrealtime();      \
+    if (P.dbg != nullptr && threadIdx.x == 0)                      \
+      P.dbg[bi * kDbg + (k)] = __builtin_amdgcn_s_memrealtime();       \
   } while (0)
 
 struct Smem {
@@ -322,9 +324,20 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   auto& wtpl = U.wtpl;
   const int tid = threadIdx.x;
   for (int i = tid; i < (int)(sizeof(KParams) / 4); i += BS) ((uint32_t*)&P)[i] = ((const uint32_t*)&Pk)[i];
-  QMX_STAMP(0);
+  if (Pk.dbg != nullptr && threadIdx.x == 0) Pk.dbg[bi * kDbg + 0] = __builtin_amdgcn_s_memrealtime();
   if (Pk.dbg != nullptr && threadIdx.x == 0) Pk.dbg[bi * kDbg + 11] = __builtin_amdgcn_s_memtime();
-  const WorkItem it = items[bi];
+  // the work item is wave-uniform: keep its fields in scalar registers (a one-shot launch
+  // reads it through the scalar cache anyway; a persistent grid loads it per tick with
+  // vector loads, and every address derived from VGPR copies would cost vector registers)
+  WorkItem it = items[bi];
+  it.slot = __builtin_amdgcn_readfirstlane(it.slot);
+  it.in_off = __builtin_amdgcn_readfirstlane(it.in_off);
+  it.in_len = __builtin_amdgcn_readfirstlane(it.in_len);
+  it.out_off = __builtin_amdgcn_readfirstlane(it.out_off);
+  it.out_cap = __builtin_amdgcn_readfirstlane(it.out_cap);
+  it.flags = __builtin_amdgcn_readfirstlane(it.flags);
+  it.index = __builtin_amdgcn_readfirstlane(it.index);
+  it.content_len = __builtin_amdgcn_readfirstlane(it.content_len);
   const int in_len = (int)it.in_len;
   const bool eof = it.flags & WF_EOF;
   const bool filt = it.flags & WF_FILTER;
@@ -580,7 +593,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       int kind = EV_SKIP, sa = 0, sb = 0, body = -1;
       bool slow = false, lexed = false;
       int nt = 0;
-      const bool probe = Pk.dbg != nullptr;
+      const bool probe = P.dbg != nullptr;
       const uint64_t c0 = probe ? __builtin_amdgcn_s_memtime() : 0;
       uint64_t c1 = 0;
       if (tp > 0 && e1 - e0 >= tp + ts && wave_tpl_match(s.A, e0, e1, s.tpl, tp, ts) &&
@@ -1173,14 +1186,14 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     }
   }
   QMX_STAMP(10);
-  if (Pk.dbg != nullptr && threadIdx.x == 0) {
-    Pk.dbg[bi * kDbg + 12] = __builtin_amdgcn_s_memtime();
-    Pk.dbg[bi * kDbg + 13] = (unsigned long long)s.v[V_NFULL];  // S3: events fully parsed
-    Pk.dbg[bi * kDbg + 14] = (unsigned long long)s.v[V_NTPL];   // S3: template hits
-    Pk.dbg[bi * kDbg + 15] = (unsigned long long)nev;
-    Pk.dbg[bi * kDbg + 16] = (unsigned long long)s.v[V_CFULL];  // S3 cycles: full parses (sum over waves)
-    Pk.dbg[bi * kDbg + 17] = (unsigned long long)s.v[V_CTPL];   // S3 cycles: template checks
-    Pk.dbg[bi * kDbg + 18] = (unsigned long long)s.v[V_CLEX];   // S3 cycles: wave_lex part of full
+  if (P.dbg != nullptr && threadIdx.x == 0) {
+    P.dbg[bi * kDbg + 12] = __builtin_amdgcn_s_memtime();
+    P.dbg[bi * kDbg + 13] = (unsigned long long)s.v[V_NFULL];  // S3: events fully parsed
+    P.dbg[bi * kDbg + 14] = (unsigned long long)s.v[V_NTPL];   // S3: template hits
+    P.dbg[bi * kDbg + 15] = (unsigned long long)nev;
+    P.dbg[bi * kDbg + 16] = (unsigned long long)s.v[V_CFULL];  // S3 cycles: full parses (sum over waves)
+    P.dbg[bi * kDbg + 17] = (unsigned long long)s.v[V_CTPL];   // S3 cycles: template checks
+    P.dbg[bi * kDbg + 18] = (unsigned long long)s.v[V_CLEX];   // S3 cycles: wave_lex part of full
   }
   if (tid == 0) {
     WorkResult r{(uint32_t)s.v[V_CONSUMED], (uint32_t)out_len, (uint32_t)s.v[V_STATUS], new_clen};
@@ -1204,6 +1217,7 @@ struct FinShared {
   int32_t scr[2 * (BS / 64)];
   int32_t v[16];
   int32_t last_close[kMaxTags];  // start of the last close token of each tag in the text
+  TagSet ts;                     // the tag set, staged from the kernel parameters
 };
 enum : int { FV_CUR = 0, FV_PEND, FV_SEGA, FV_NSEG, FV_NTOK, FV_S0, FV_S1, FV_NBIG, FV_OVF };
 
@@ -1331,8 +1345,11 @@ struct FinArgs {
 };
 
 __device__ __forceinline__ void fin_body(const FinArgs& fa, int j, const uint8_t* __restrict__ content, uint32_t content_cap,
-                         const TagSet& ts, FinShared& F) {
+                         const TagSet& ts_mem, FinShared& F) {
   const int tid = threadIdx.x;
+  for (int i = tid; i < (int)(sizeof(TagSet) / 4); i += BS) ((uint32_t*)&F.ts)[i] = ((const uint32_t*)&ts_mem)[i];
+  __syncthreads();
+  const TagSet& ts = F.ts;
   const FinItem it = fa.items[j];
   const bool strip = it.flags & 1, as_texts = it.flags & 2;
   uint8_t* J = fa.join + it.join_off;
@@ -2157,18 +2174,20 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
       L.params.dbg = L.h_dbg;
     }
     if (L.params.dbg != dbg0) L.params_dirty = true;
+    // persistent grid (needs polled completion) or a one-shot launch for this tick
+    const bool persist = persistent_ && poll_;
+    if (!persist && L.p_running) stop_persistent(L);  // mode switched: the grid must not hold the stream
     const bool new_params = L.params_dirty;
     if (L.params_dirty) {  // the pinned copy is not touched again until this tick completed
       std::memcpy(L.h_params, &L.params, sizeof(KParams));
       // one-shot launches: a stream-ordered upload; persistent: the grid copies it itself
-      if (!persistent_) HIP_CHECK(hipMemcpyAsync(L.d_params, L.h_params, sizeof(KParams), hipMemcpyHostToDevice, L.stream));
+      if (!persist) HIP_CHECK(hipMemcpyAsync(L.d_params, L.h_params, sizeof(KParams), hipMemcpyHostToDevice, L.stream));
       L.params_dirty = false;
     }
     const auto tp1 = HC::now();
     L.host_prep_us += std::chrono::duration<double, std::micro>(tp1 - tp0).count();
     roctxRangePushA("qmx_tick");  // rocprofv3 --marker-trace: one range per tick launch + wait
     L.h2d_bytes += in_off;
-    const bool persist = persistent_ && poll_;
     if (persist) ensure_persistent(L);  // before the tick's sequence number: a relaunch starts from L.seq
     const uint32_t seq = next_seq(L);
     const uint32_t par = L.launches & 1;  // backend template table: read last tick's half, write the other

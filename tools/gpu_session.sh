@@ -131,7 +131,7 @@ for l in open('$OUT/kbench.jsonl'):
       python tools/probes/gpu_procs.py $OUT/gpuprocs_$n.txt 60 &
       mon=$!
       QMX_BENCH_FDTRACE=1 torchrun_bench gpuprocs_$n $n --steps 5 --warmup 1 --threads 2 --batch 4096; rc=$?
-      grep "gpu held" $OUT/gpuprocs_$n.err | sort | uniq -c | head -20
+      grep -A30 "GPU first held" $OUT/gpuprocs_$n.err | head -40
       kill $mon 2>/dev/null; wait $mon 2>/dev/null
       cat $OUT/gpuprocs_$n.txt
       [ $rc -eq 0 ] || exit 1 ;;
