@@ -88,6 +88,18 @@ def _trace(stage: str) -> None:
         print(f"bench rank {os.environ.get('RANK', '0')}: {stage}: gpu held {_gpu_held()}", file=sys.stderr, flush=True)
 
 
+def _barrier(dist, on_gpu: bool) -> None:
+    """dist.barrier(), but a rehearsal's gloo group synchronises with a CPU all-reduce:
+    gloo's barrier() touches the CUDA device (it picks a device for its work), and a box
+    counts every process holding the GPU."""
+    if on_gpu:
+        dist.barrier()
+    else:
+        import torch
+
+        dist.all_reduce(torch.zeros(1))
+
+
 def _trace_watch() -> None:
     """QMX_BENCH_FDTRACE: report the main thread's stack when this process first holds the GPU."""
     if not os.environ.get("QMX_BENCH_FDTRACE"):
@@ -373,7 +385,7 @@ def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports
                               env=env)
         if not wait_healthy("127.0.0.1", port, 120):
             raise RuntimeError("spread proxy did not become healthy")
-        dist.barrier()
+        _barrier(dist, n_dev >= world)
         want_rccl = env.get("QMX_XCHG", "rccl") == "rccl"
         t0 = time.time()
         while True:  # the mesh (and, on GPUs, the RCCL communicator) formed on every rank
@@ -383,7 +395,7 @@ def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports
             if time.time() - t0 > 90:
                 raise RuntimeError(f"exchange did not form: {({k: v for k, v in m.items() if 'exchange' in k})}")
             time.sleep(0.2)
-        dist.barrier()
+        _barrier(dist, n_dev >= world)
         m0 = scrape(port)
         st = loadgen(bin_dir, port, 32, 2048, 2, 120, spec)
         time.sleep(0.2)
@@ -530,7 +542,7 @@ def main() -> int:
         xchg_kind = os.environ.get("QMX_XCHG", "rccl" if engine == "hip" else "tcp")
         _trace("healthy")
         if dist is not None:
-            dist.barrier()
+            _barrier(dist, coll_cuda)
         # the reference has no /v1 prefix (oai_proxy.py:959); qmx serves both
         path = "/chat/completions" if args.impl == "reference" else "/v1/chat/completions"
         warm = {}
@@ -547,7 +559,7 @@ def main() -> int:
             print(f"bench rank {rank}: server process(es) exited during warmup: {dead_warm}", file=sys.stderr,
                   flush=True)
         if dist is not None:
-            dist.barrier()
+            _barrier(dist, coll_cuda)
         if use_cuda:
             torch.cuda.synchronize()
         m0 = scrape(proxy_port) if args.impl == "native" else {}
@@ -558,7 +570,7 @@ def main() -> int:
         if use_cuda:
             torch.cuda.synchronize()
         if dist is not None:
-            dist.barrier()
+            _barrier(dist, coll_cuda)
         elapsed = time.perf_counter() - t0
         c1 = cpu_snapshot(mock_procs, proxy_procs)
         bd = breakdown(m0, scrape(proxy_port), elapsed) if args.impl == "native" else {}

@@ -209,7 +209,7 @@ class HipEngine : public HostEngine {
   int spin_us_ = 0;  // QMX_WAIT_SPIN_US: yield-poll before the blocking wait
   bool poll_ = true;  // QMX_WAIT=event: wait on a blocking-sync HIP event instead of polling
   int poll_us_ = 6;   // QMX_POLL_US: poll period once the expected kernel time has passed
-  bool persistent_ = false;  // QMX_PERSISTENT=1: a long-lived grid per lane, ticks posted by doorbell
+  bool persistent_ = true;   // a long-lived grid per lane, ticks posted by doorbell (QMX_PERSISTENT=0: a launch per tick)
   int p_grid_ = 64;          // QMX_PERSISTENT_WG: workgroups per lane grid (1 per CU: 256 VGPRs)
   int p_idle_ms_ = 50;       // the grid exits after this long without a tick
 

@@ -1,5 +1,6 @@
-"""GPU: persistent tick mode (QMX_PERSISTENT=1) — one long-lived grid per lane, ticks posted
-through a host-mapped doorbell instead of a launch each (qmx_hip.hip qmx_tick_persistent).
+"""GPU: persistent tick mode (the default; QMX_PERSISTENT=0 launches per tick) — one
+long-lived grid per lane, ticks posted through a host-mapped doorbell instead of a launch
+each (qmx_hip.hip qmx_tick_persistent).
 
 Every result must equal the C++ CPU engine's, as in one-shot mode, including ticks with more
 items than the grid has workgroups (a workgroup loops over items), fused finalize work,
@@ -100,3 +101,14 @@ def test_persistent_two_lanes(persistent):
         assert out[s] == cpu[0][i][0], i
     st = eng._e.kernel_stats()
     assert st["persistent_grids"] >= 2 and st["poll_fallbacks"] == 0, st
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_oneshot_mode_matches_cpu(monkeypatch, seed):
+    """QMX_PERSISTENT=0: the launch-per-tick path stays exact (rocprof kernel stats and the
+    stage-timing benchmark use it)."""
+    e = native.require()
+    assert e.device_count() > 0
+    monkeypatch.setenv("QMX_PERSISTENT", "0")
+    st = _check(8400 + seed, 30)
+    assert st["persistent_grids"] == 0 and st["launches"] >= 1 and st["poll_fallbacks"] == 0, st

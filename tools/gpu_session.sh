@@ -104,20 +104,21 @@ for step in "$@"; do
         bench ref_$SC 600 QMX_NOP=1 -- --impl reference --scenario $SC --steps 5 --warmup 1 --batch 32 || exit 1
       done ;;
     prof)
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o native --output-format csv -- \
+      # one-shot launches: a persistent grid is one long dispatch per lane, no per-tick kernel stats
+      QMX_PERSISTENT=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o native --output-format csv -- \
         python3 bench.py --steps 5 --warmup 1 > $OUT/bench_prof.json 2> $OUT/bench_prof.err \
         || { echo "prof failed"; tail -10 $OUT/bench_prof.err; exit 1; }
       summ prof $OUT/bench_prof.json
       find $OUT/prof -name '*kernel_stats.csv' -exec head -5 {} \; ;;
     pmc:*)
       ctr=${step#pmc:}; slug=$(echo "$ctr" | tr -c 'a-zA-Z0-9' '_' | cut -c1-60)
-      timeout -s KILL 120 rocprofv3 --pmc ${ctr//,/ } -d $OUT/pmc_$slug -o pmc --output-format csv -- \
+      QMX_PERSISTENT=0 timeout -s KILL 120 rocprofv3 --pmc ${ctr//,/ } -d $OUT/pmc_$slug -o pmc --output-format csv -- \
         python3 tools/kbench.py --slots 256 --iters 10 > $OUT/pmc_$slug.log 2>&1 \
         || { echo "pmc $ctr failed"; tail -10 $OUT/pmc_$slug.log; exit 1; }
       python3 tools/pmc_summary.py $(find $OUT/pmc_$slug -name '*counter_collection.csv') > $OUT/pmc_$slug.md 2>&1
       grep -v rocclr $OUT/pmc_$slug.md | head -30 ;;
     kbench)
-      QMX_STAGE_TIMING=1 timeout -k 10 300 python tools/kbench.py --slots 1,22,64,256 --iters 20 > $OUT/kbench.jsonl 2>&1 \
+      QMX_PERSISTENT=0 QMX_STAGE_TIMING=1 timeout -k 10 300 python tools/kbench.py --slots 1,22,64,256 --iters 20 > $OUT/kbench.jsonl 2>&1 \
         || { echo "kbench failed"; tail -5 $OUT/kbench.jsonl; exit 1; }
       python3 -c "
 import json
