@@ -523,6 +523,8 @@ def main() -> int:
         spec_path = os.path.join(tmp, "expect.txt")
         expect_spec(spec_path, sc, skip_final, mock_expected(bin_dir))
         env = dict(os.environ)
+        if n_dev:  # processes sharing this rank's GPU (persistent tick grids need it alone)
+            env["QMX_GPU_SHARERS"] = str(max(1, -(-int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) // n_dev)))
         if args.placement == "spread" and world > 1:
             nonce = [str(time.time_ns()) if rank == 0 else None]
             dist.broadcast_object_list(nonce, src=0)

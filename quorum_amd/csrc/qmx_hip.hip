@@ -1597,6 +1597,7 @@ struct PCtl {  // device memory: written by workgroup 0, polled by the others
   TickDesc d;
   alignas(64) uint32_t seq;
   uint32_t exit_gen;
+  alignas(64) uint32_t next[4];  // item counters, tick seq & 3 (reset by the relay before publishing)
 };
 
 // `door` / `ctl` are neither const nor __restrict__ and their words are read with atomic
@@ -1676,6 +1677,7 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* door, PCtl* ctl
       if (tid < kWords)
         __hip_atomic_store((uint32_t*)&ctl->d + tid, ((const uint32_t*)&D)[tid], __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0) __hip_atomic_store(&ctl->next[c & 3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __threadfence();
       __syncthreads();
       if (tid == 0) {
@@ -1701,7 +1703,14 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* door, PCtl* ctl
     const uint32_t n_tick = __builtin_amdgcn_readfirstlane(D.n_tick);
     const int total = (int)(n_tick + __builtin_amdgcn_readfirstlane(D.n_fin));
     const uint32_t seq = __builtin_amdgcn_readfirstlane(D.seq);
-    for (int k = (int)blockIdx.x; k < total; k += (int)gridDim.x) {
+    // items are claimed from the tick's counter, not dealt by workgroup index: a workgroup
+    // that is not resident (the CUs are shared with other grids / kernels) holds up nothing
+    for (;;) {
+      if (tid == 0) cmd = __hip_atomic_fetch_add(&ctl->next[seq & 3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const int k = (int)cmd;
+      __syncthreads();  // cmd is rewritten by the next claim
+      if (k >= total) break;
       // a visible clobber: the host rewrites items, tile bytes and finalize descriptors
       // between ticks, so none of them may be read through the scalar cache as
       // launch-invariant data (which the compiler does for uniform addresses it proves
@@ -1811,6 +1820,9 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
   if (const char* sp = getenv("QMX_WAIT_SPIN_US")) spin_us_ = atoi(sp);
   if (const char* w = getenv("QMX_WAIT")) poll_ = std::string(w) != "event";
   if (const char* pu = getenv("QMX_POLL_US")) poll_us_ = std::max(1, atoi(pu));
+  // a persistent grid assumes its process owns the GPU: grids of several processes on one
+  // device (a rehearsal with more ranks than GPUs) need not all be resident at once
+  if (const char* gs = getenv("QMX_GPU_SHARERS")) persistent_ = atoi(gs) <= 1;
   if (const char* pe = getenv("QMX_PERSISTENT")) persistent_ = atoi(pe) != 0;
   if (const char* pw = getenv("QMX_PERSISTENT_WG")) p_grid_ = std::min(std::max(8, atoi(pw)), 1024);
   if (const char* pi = getenv("QMX_PERSISTENT_IDLE_MS")) p_idle_ms_ = std::min(std::max(5, atoi(pi)), 1000);
