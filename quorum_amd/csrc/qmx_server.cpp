@@ -932,7 +932,7 @@ class Loop {
   // feed / finish / release are queued in order and handed to the engine once per loop
   // iteration (flush_ops: one engine lock instead of one per upstream read — with the
   // shared engine, 8+ loops and the tick lanes otherwise contend on it per call)
-  void e_feed(int slot, const std::string& d) { ops_.push_back(EngineOp{EngineOp::FEED, slot, d}); }
+  void e_feed_move(int slot, std::string& d) { ops_.push_back(EngineOp{EngineOp::FEED, slot, std::move(d)}); }
   void e_finish(int slot) { ops_.push_back(EngineOp{EngineOp::FINISH, slot, std::string()}); }
   void e_release(int slot) { ops_.push_back(EngineOp{EngineOp::RELEASE, slot, std::string()}); }
   void flush_ops() {
@@ -1669,10 +1669,11 @@ class Loop {
       }
     }
   }
-  void on_up_body(Up* u, const std::string& body) {
+  // `body` is the caller's scratch: its bytes may be moved out
+  void on_up_body(Up* u, std::string& body) {
     Session* s = u->sess;
     if (u->rp.status == 200 && u->mode == UP_ENGINE) {
-      e_feed(s->bs[u->bi].slot, body);
+      e_feed_move(s->bs[u->bi].slot, body);  // the engine takes the buffer (no copy)
       kick();
       return;
     }
