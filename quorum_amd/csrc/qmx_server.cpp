@@ -741,7 +741,8 @@ class Loop {
       for (int i = 0; i < n; ++i) dispatch(evs[i]);
       if (g_drain.load() && drain_step()) break;
       if (!pending_requests_.empty()) {
-        std::vector<int> fds;
+        std::vector<int>& fds = scratch_fds_;  // swapped each iteration: both buffers keep their capacity
+        fds.clear();
         fds.swap(pending_requests_);
         for (int fd : fds) {
           auto it = clients_.find(fd);
@@ -870,7 +871,8 @@ class Loop {
     ssize_t r = read(evfd_, &v, 8);
     cnt(SC_WAKE_READ);
     (void)r;
-    std::vector<ResultBatch> q;
+    std::vector<ResultBatch>& q = scratch_rq_;
+    q.clear();
     {
       std::lock_guard<std::mutex> g(rmu_);
       q.swap(rq_);
@@ -1078,7 +1080,8 @@ class Loop {
     }
   }
   void flush_queued() {
-    std::vector<int> fds;
+    std::vector<int>& fds = scratch_flush_;
+    fds.clear();
     fds.swap(flushq_);
     for (int fd : fds) {
       auto it = clients_.find(fd);
@@ -2527,6 +2530,8 @@ class Loop {
   double last_snap_ = 0;
   int xfd_ = -1;
   std::vector<int> valid_;  // backends with a URL (config order), computed once
+  std::vector<int> scratch_fds_, scratch_flush_;  // per-iteration lists, capacity kept
+  std::vector<ResultBatch> scratch_rq_;
   bool valid_init_ = false;
   std::mutex xmu_;
   std::vector<XMsg> xin_;
