@@ -208,7 +208,7 @@ class HipEngine : public HostEngine {
   std::atomic<uint64_t> escalations_{0}, fin_host_{0};
   int spin_us_ = 0;  // QMX_WAIT_SPIN_US: yield-poll before the blocking wait
   bool poll_ = true;  // QMX_WAIT=event: wait on a blocking-sync HIP event instead of polling
-  int poll_us_ = 2;   // QMX_POLL_US: poll period once the expected kernel time has passed (MI355X A/B: 2 beats 6)
+  int poll_us_ = 1;   // QMX_POLL_US: poll period once the expected kernel time has passed (MI355X A/Bs: 2 beats 6, 1 beats 2)
   bool persistent_ = true;   // a long-lived grid per lane, ticks posted by doorbell (QMX_PERSISTENT=0: a launch per tick)
   int p_grid_ = 64;          // QMX_PERSISTENT_WG: workgroups per lane grid (1 per CU: 256 VGPRs)
   int p_idle_ms_ = 50;       // the grid exits after this long without a tick
