@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <functional>
 #include <memory>
 #include <mutex>
 
@@ -176,7 +177,8 @@ class HipEngine : public HostEngine {
                                                 std::vector<const FinalizeReq*>& host);
   void collect_finalize(TickLane& L, const std::vector<const FinalizeReq*>& gpu, std::vector<FinalizeRes>& out);
   void wait_stream(TickLane& L);
-  void wait_results(TickLane& L, int n, int m, uint32_t seq);
+  // polls the tick's result records; on_item(i) as stream result i is seen published (in order)
+  void wait_results(TickLane& L, int n, int m, uint32_t seq, const std::function<void(int)>& on_item);
   void collect_timing(TickLane& L);
   void ensure_in(TickLane& L, size_t bytes);
   void ensure_out(TickLane& L, size_t bytes);

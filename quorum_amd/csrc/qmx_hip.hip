@@ -1753,7 +1753,7 @@ void HipEngine::wait_stream(TickLane& L) {
 // most of the expected kernel time (EMA), then poll every poll_us_ with a 1 us timer slack.
 // A launch that has not published after 4x the EMA + 2 ms synchronises its stream (surfaces a
 // fault; correct even if host-mapped visibility misbehaved: counted in poll_fallbacks).
-void HipEngine::wait_results(TickLane& L, int n, int m, uint32_t seq) {
+void HipEngine::wait_results(TickLane& L, int n, int m, uint32_t seq, const std::function<void(int)>& on_item) {
   using HC = std::chrono::steady_clock;
   static thread_local bool slack = (prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0), true);
   (void)slack;
@@ -1764,7 +1764,7 @@ void HipEngine::wait_results(TickLane& L, int n, int m, uint32_t seq) {
     nanosleep(&ts, nullptr);
   };
   auto done = [&](int& i) {
-    while (i < n && __atomic_load_n(&L.h_res[i].seq, __ATOMIC_ACQUIRE) == seq) ++i;
+    while (i < n && __atomic_load_n(&L.h_res[i].seq, __ATOMIC_ACQUIRE) == seq) on_item(i++);
     while (i >= n && i < n + m && __atomic_load_n(&L.h_finres[i - n].seq, __ATOMIC_ACQUIRE) == seq) ++i;
     return i == n + m;
   };
@@ -2164,6 +2164,60 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
     pend.push_back({slot, cl, sub, eof_sent, &w});
     ++n;
   }
+  // one stream's result → slot state + SSE; run as each result record is published (the
+  // host's share of a tick overlaps the kernel's stragglers), the rest after the wait
+  int n_done = 0;
+  auto process_item = [&](int i) {
+    Pending& p = pend[i];
+    SlotCore& c = core_[p.slot];
+    const WorkResult r = L.h_res[i];
+    Work& w = *p.w;
+    // the unconsumed remainder (carry + data)[consumed:] becomes the carry, in place
+    auto keep_remainder = [&](size_t consumed) {
+      const size_t cl = p.carry_len;
+      if (consumed < cl) {
+        c.carry.erase(0, consumed);
+        c.carry += w.data;
+      } else {
+        c.carry.assign(w.data, consumed - cl, std::string::npos);
+      }
+    };
+    bool no_progress = (r.status & WS_ESCALATE) ||
+                       (p.submitted == (size_t)tile_ && r.consumed == 0 && !(r.status & (WS_DONE | WS_ABORTED)));
+    if (no_progress) {
+      escalate(p.slot, w.fresh);
+      keep_remainder(0);
+      std::string all;
+      all.swap(c.carry);
+      bool was_closed = c.done || c.aborted;
+      std::string o;
+      process_slot(ts_, c, (const uint8_t*)all.data(), all.size(), w.eof, created, o);
+      int flags = (c.done ? RF_DONE : 0) | (c.aborted ? RF_ABORTED : 0) | RF_ESCALATED;
+      if (!o.empty() || ((flags & (RF_DONE | RF_ABORTED)) && !was_closed)) results.push_back({p.slot, std::move(o), flags});
+      return;
+    }
+    if (r.status & WS_STARTED) c.started = true;
+    content_len_[p.slot] = r.content_len;
+    int flags = 0;
+    if (r.status & WS_ABORTED) {
+      c.aborted = true;
+      c.carry.clear();
+      flags |= RF_ABORTED;
+    } else {
+      keep_remainder(r.consumed);
+      if (r.status & WS_DONE) {
+        c.done = true;
+        c.carry.clear();
+        flags |= RF_DONE;
+      } else if ((r.status & WS_MORE) || p.submitted < p.carry_len + w.data.size()) {
+        requeue.push_back(p.slot);  // unprocessed bytes (or a pending EOF) remain
+      }
+    }
+    std::string sse;
+    L.d2h_bytes += r.out_len;
+    if (r.out_len) sse.assign((const char*)L.h_out + L.h_items[i].out_off, r.out_len);
+    if (!sse.empty() || flags) results.push_back({p.slot, std::move(sse), flags});
+  };
   // finalize requests ride the same launch: workgroups [n, n + m)
   std::vector<const FinalizeReq*> fin_host;
   const std::vector<const FinalizeReq*> fin_gpu = prep_finalize(L, fin, fin_host);
@@ -2233,7 +2287,9 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
     for (const FinalizeReq* r : fin_host) finalize_host(*r, fres);
     if (poll_) {
       // one HIP call per tick: completion and kernel span both come from the result records
-      wait_results(L, n, m, seq);
+      wait_results(L, n, m, seq, [&](int i) {
+        if (i == n_done) process_item(n_done++);
+      });
       uint64_t a = ~0ull, b = 0;
       for (int i = 0; i < n; ++i) {
         a = std::min(a, L.h_res[i].t0);
@@ -2283,57 +2339,7 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
       }
     }
   }
-  for (int i = 0; i < n; ++i) {
-    Pending& p = pend[i];
-    SlotCore& c = core_[p.slot];
-    const WorkResult r = L.h_res[i];
-    Work& w = *p.w;
-    // the unconsumed remainder (carry + data)[consumed:] becomes the carry, in place
-    auto keep_remainder = [&](size_t consumed) {
-      const size_t cl = p.carry_len;
-      if (consumed < cl) {
-        c.carry.erase(0, consumed);
-        c.carry += w.data;
-      } else {
-        c.carry.assign(w.data, consumed - cl, std::string::npos);
-      }
-    };
-    bool no_progress = (r.status & WS_ESCALATE) ||
-                       (p.submitted == (size_t)tile_ && r.consumed == 0 && !(r.status & (WS_DONE | WS_ABORTED)));
-    if (no_progress) {
-      escalate(p.slot, w.fresh);
-      keep_remainder(0);
-      std::string all;
-      all.swap(c.carry);
-      bool was_closed = c.done || c.aborted;
-      std::string o;
-      process_slot(ts_, c, (const uint8_t*)all.data(), all.size(), w.eof, created, o);
-      int flags = (c.done ? RF_DONE : 0) | (c.aborted ? RF_ABORTED : 0) | RF_ESCALATED;
-      if (!o.empty() || ((flags & (RF_DONE | RF_ABORTED)) && !was_closed)) results.push_back({p.slot, std::move(o), flags});
-      continue;
-    }
-    if (r.status & WS_STARTED) c.started = true;
-    content_len_[p.slot] = r.content_len;
-    int flags = 0;
-    if (r.status & WS_ABORTED) {
-      c.aborted = true;
-      c.carry.clear();
-      flags |= RF_ABORTED;
-    } else {
-      keep_remainder(r.consumed);
-      if (r.status & WS_DONE) {
-        c.done = true;
-        c.carry.clear();
-        flags |= RF_DONE;
-      } else if ((r.status & WS_MORE) || p.submitted < p.carry_len + w.data.size()) {
-        requeue.push_back(p.slot);  // unprocessed bytes (or a pending EOF) remain
-      }
-    }
-    std::string sse;
-    L.d2h_bytes += r.out_len;
-    if (r.out_len) sse.assign((const char*)L.h_out + L.h_items[i].out_off, r.out_len);
-    if (!sse.empty() || flags) results.push_back({p.slot, std::move(sse), flags});
-  }
+  for (; n_done < n; ++n_done) process_item(n_done);  // the rest (event wait, stage timing)
   if (m > 0) collect_finalize(L, fin_gpu, fres);
   if (n + m == 0)
     for (const FinalizeReq* r : fin_host) finalize_host(*r, fres);

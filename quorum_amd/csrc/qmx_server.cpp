@@ -184,21 +184,34 @@ struct RespParser {
   long remaining = 0;
   bool close = false;
   std::string buf;
-  // returns -1 on protocol error; appends body bytes to out
+  // returns -1 on protocol error; appends body bytes to out.  Parses straight from the read
+  // buffer when nothing is pending (the common case): only an unconsumed tail is copied.
   int feed(const char* p, size_t n, std::string& out) {
-    buf.append(p, n);
+    const char* d = p;
+    size_t len = n;
+    if (!buf.empty()) {
+      buf.append(p, n);
+      d = buf.data();
+      len = buf.size();
+    }
+    out.reserve(out.size() + n);  // at most n body bytes arrive with n bytes
+    auto find = [&](const char* pat, size_t pl, size_t from) -> size_t {
+      const void* f = from <= len ? memmem(d + from, len - from, pat, pl) : nullptr;
+      return f ? (size_t)((const char*)f - d) : std::string::npos;
+    };
     size_t i = 0;
     while (phase != 7) {
       if (phase == 0) {
-        size_t he = buf.find("\r\n\r\n", i);
+        size_t he = find("\r\n\r\n", 4, i);
         if (he == std::string::npos) break;
-        const char* hp = buf.data() + i;
+        const char* hp = d + i;
         size_t hn = he - i;
         i = he + 4;
         const char* le0 = (const char*)memmem(hp, hn, "\r\n", 2);
         size_t le = le0 ? (size_t)(le0 - hp) : hn;
         if (le < 12 || memcmp(hp, "HTTP/", 5) != 0) return -1;
-        status = atoi(std::string(hp + 9, le - 9).c_str());
+        status = 0;
+        for (size_t k = 9; k < le && hp[k] >= '0' && hp[k] <= '9'; ++k) status = status * 10 + (hp[k] - '0');
         bool chunked = false, has_len = false;
         size_t pos = le0 ? le + 2 : hn;
         for_each_header(hp + pos, hn - pos, [&](std::string&& k, std::string&& v) {
@@ -220,29 +233,29 @@ struct RespParser {
         continue;
       }
       if (phase == 1) {
-        size_t take = std::min((size_t)remaining, buf.size() - i);
-        out.append(buf, i, take);
+        size_t take = std::min((size_t)remaining, len - i);
+        out.append(d + i, take);
         i += take;
         remaining -= take;
         if (remaining == 0) phase = 7;
         break;
       }
       if (phase == 6) {
-        out.append(buf, i, std::string::npos);
-        i = buf.size();
+        out.append(d + i, len - i);
+        i = len;
         break;
       }
       if (phase == 2) {
-        size_t le = buf.find("\r\n", i);
+        size_t le = find("\r\n", 2, i);
         if (le == std::string::npos) break;
-        remaining = strtol(buf.c_str() + i, nullptr, 16);
+        remaining = strtol(d + i, nullptr, 16);  // stops at the CR
         i = le + 2;
         phase = remaining == 0 ? 5 : 3;
         continue;
       }
       if (phase == 3) {
-        size_t take = std::min((size_t)remaining, buf.size() - i);
-        out.append(buf, i, take);
+        size_t take = std::min((size_t)remaining, len - i);
+        out.append(d + i, take);
         i += take;
         remaining -= take;
         if (remaining > 0) break;
@@ -250,13 +263,13 @@ struct RespParser {
         continue;
       }
       if (phase == 4) {
-        if (buf.size() - i < 2) break;
+        if (len - i < 2) break;
         i += 2;
         phase = 2;
         continue;
       }
       if (phase == 5) {
-        size_t le = buf.find("\r\n", i);
+        size_t le = find("\r\n", 2, i);
         if (le == std::string::npos) break;
         bool empty = le == i;
         i = le + 2;
@@ -264,7 +277,8 @@ struct RespParser {
         continue;
       }
     }
-    buf.erase(0, i);
+    if (d == p) buf.assign(p + i, n - i);  // the unconsumed tail only
+    else buf.erase(0, i);
     return 0;
   }
   bool done() const { return phase == 7; }
