@@ -311,6 +311,25 @@ int HostEngine::open(int index, bool filter, bool emit, uint32_t* gen) {
     meta_.emplace_back();
     core_.emplace_back();
   }
+  open_reserved(slot, index, filter, emit, gen);
+  return slot;
+}
+
+void HostEngine::reserve(int k, std::vector<int>& out) {
+  std::lock_guard<std::mutex> g(mu_);
+  for (int i = 0; i < k; ++i) {
+    if (!free_.empty()) {
+      out.push_back(free_.back());
+      free_.pop_back();
+    } else {
+      out.push_back((int)meta_.size());
+      meta_.emplace_back();
+      core_.emplace_back();
+    }
+  }
+}
+
+void HostEngine::open_reserved(int slot, int index, bool filter, bool emit, uint32_t* gen) {
   // reset in place: a reused slot keeps its (small) buffers, so a new session costs no
   // allocation under the engine lock
   auto recycle = [](std::string& x) {
@@ -334,7 +353,6 @@ int HostEngine::open(int index, bool filter, bool emit, uint32_t* gen) {
   recycle(c.content);
   recycle(c.tpl_pre);
   recycle(c.tpl_suf);
-  return slot;
 }
 
 void HostEngine::feed(int slot, const std::string& data) {

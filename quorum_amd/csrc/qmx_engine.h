@@ -128,6 +128,11 @@ class HostEngine {
 
   // returns the slot; *gen (optional) receives the slot's open generation (SlotResult::gen)
   int open(int index, bool filter, bool emit, uint32_t* gen = nullptr);
+  // A caller that opens many slots (an io loop) takes k free slots under ONE lock, then
+  // opens them one by one without the lock: a reserved slot is in no list a tick lane reads,
+  // and its first feed / finish / release goes through the lock (apply_ops) as usual.
+  void reserve(int k, std::vector<int>& out);
+  void open_reserved(int slot, int index, bool filter, bool emit, uint32_t* gen = nullptr);
   void feed(int slot, const std::string& data);
   void finish(int slot);
   void release(int slot);

@@ -538,7 +538,7 @@ class Verifier {
 class GpuHub {
  public:
   using Sink = std::function<void(ResultBatch&&)>;
-  GpuHub(const ServerCfg& cfg, int nloops) : cfg_(cfg), sinks_(nloops) {
+  GpuHub(const ServerCfg& cfg, int nloops) : cfg_(cfg), sinks_(nloops), pools_(nloops) {
     lanes_ = std::max(1, std::min(cfg.tick_lanes, 8));
     if (cfg.engine == "hip") {
       HipEngine* he = new HipEngine(cfg.tags, cfg.device, cfg.tile, cfg.max_slots, cfg.content_cap, lanes_);
@@ -563,13 +563,21 @@ class GpuHub {
     for (int i = 0; i < lanes_; ++i) th_.emplace_back([this, i] { run(i); });
   }
   void attach(int loop, Sink s) { sinks_[loop] = std::move(s); }
+  // called by io loop `loop` only: slots come from that loop's reserve, refilled 32 at a
+  // time under one engine lock + one owner-map lock (not two locks per open)
   int open(int loop, int index, bool f, bool e, uint32_t* gen, bool verify = true) {
-    int slot = eng_->open(index, f, e, gen);
-    {
+    std::vector<int>& pool = pools_[loop];
+    if (pool.empty()) {
+      eng_->reserve(32, pool);
       std::lock_guard<std::mutex> g(omu_);
-      if ((int)owner_.size() <= slot) owner_.resize(slot + 1024, -1);
-      owner_[slot] = loop;
+      for (int slot : pool) {
+        if ((int)owner_.size() <= slot) owner_.resize(slot + 1024, -1);
+        owner_[slot] = loop;
+      }
     }
+    const int slot = pool.back();
+    pool.pop_back();
+    eng_->open_reserved(slot, index, f, e, gen);
     if (ver_ && verify) ver_->open(slot, *gen, index, f, e);
     return slot;
   }
@@ -671,6 +679,7 @@ class GpuHub {
   std::unique_ptr<HostEngine> eng_;
   std::unique_ptr<Verifier> ver_;
   std::vector<Sink> sinks_;
+  std::vector<std::vector<int>> pools_;  // per io loop: reserved, not yet opened slots
   std::mutex mu_, omu_, smu_;
   std::condition_variable cv_;
   bool work_ = false;
