@@ -601,7 +601,14 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
         kind = EV_CONTENT;  // same shape as this stream's last parsed content event
         sa = e0 + tp;
         sb = e1 - ts;
-        if (lane == 0) atomicAdd(&s.v[V_NTPL], 1);
+        if (lane == 0) {
+          atomicAdd(&s.v[V_NTPL], 1);
+          // a matched event is as good a template as a parsed one: the tile's NEWEST content
+          // event (parsed or matched) becomes the stream's and the backend's template — not
+          // the newest parsed one, which in a burst is the odd-shaped first event (role +
+          // empty content) and would make the next stream of this backend parse again
+          atomicMax(&s.v[V_TPLK], k);
+        }
       } else {
         for (int q = 0; q < BS / 64 && kind != EV_CONTENT; ++q) {
           const int qi = (hint + q) & (BS / 64 - 1);
@@ -614,7 +621,10 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
             sa = e0 + ttp;
             sb = e1 - tts;
             hint = qi;
-            if (lane == 0) atomicAdd(&s.v[V_NTPL], 1);
+            if (lane == 0) {
+              atomicAdd(&s.v[V_NTPL], 1);
+              atomicMax(&s.v[V_TPLK], k);
+            }
           }
         }
         if (probe) c1 = __builtin_amdgcn_s_memtime();
