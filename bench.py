@@ -371,49 +371,78 @@ def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports
     port = args.port + 50
     out = {"ok": False}
     procs = []
+    ok, err = True, None
+
+    def agree(stage: str) -> bool:
+        """Every rank runs the same collectives whatever failed locally (a rank that skipped
+        one would leave the others in it): min over ranks of this rank's ok flag."""
+        import torch
+
+        nonlocal ok, err
+        t = torch.tensor([1.0 if ok else 0.0], device="cuda" if n_dev >= world else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        if t.item() < 1.0 and ok:
+            ok, err = False, f"another rank failed at {stage}"
+        return ok
+
     try:
         nonce = [str(time.time_ns()) if rank == 0 else None]
         dist.broadcast_object_list(nonce, src=0)
         env = dict(os.environ, **exchange_env(rank, world, port, nonce[0]))
         if n_dev < world or engine != "hip":
             env["QMX_XCHG"] = "tcp"  # ranks sharing a GPU (rehearsal): RCCL needs one GPU per rank
-        cfg = os.path.join(tmp, "config_spread.yaml")
-        write_config(cfg, mock_ports, False, args.tile, sc, "spread")
-        spec = os.path.join(tmp, "expect_spread.txt")
-        expect_spec(spec, sc, False, mock_expected(bin_dir))
-        procs = spawn_workers(cfg, "127.0.0.1", port, 1, engine, device, impl="native", threads=args.threads,
-                              env=env)
-        if not wait_healthy("127.0.0.1", port, 120):
-            raise RuntimeError("spread proxy did not become healthy")
-        _barrier(dist, n_dev >= world)
         want_rccl = env.get("QMX_XCHG", "rccl") == "rccl"
-        t0 = time.time()
-        while True:  # the mesh (and, on GPUs, the RCCL communicator) formed on every rank
-            m = scrape(port)
-            if m.get("qmx_exchange_healthy") == 1.0 and (not want_rccl or m.get("qmx_exchange_rccl_active") == 1.0):
-                break
-            if time.time() - t0 > 90:
-                raise RuntimeError(f"exchange did not form: {({k: v for k, v in m.items() if 'exchange' in k})}")
-            time.sleep(0.2)
-        _barrier(dist, n_dev >= world)
-        m0 = scrape(port)
-        st = loadgen(bin_dir, port, 32, 2048, 2, 120, spec)
-        time.sleep(0.2)
-        m1 = scrape(port)
-        d = {k: m1.get(k, 0.0) - m0.get(k, 0.0) for k in m1 if "exchange" in k or "remote_streams" in k}
-        out = {"ok": st["invalid"] == 0 and st["errors"] == 0 and st["completed"] == 2048,
-               "transport": "rccl" if want_rccl else "tcp", "requests": st["completed"], "invalid": st["invalid"],
-               "p50_ttft_ms": st["ttft_p50_ms"], "p50_latency_ms": st["lat_p50_ms"], "req_s": st["rps"],
-               "remote_streams": d.get("qmx_remote_streams_total", 0.0),
-               "rccl_rounds": d.get("qmx_exchange_rounds_total", 0.0),
-               "rccl_final_bytes": d.get("qmx_exchange_bulk_bytes_total", 0.0),
-               "mesh_finals": d.get("qmx_exchange_mesh_finals_total", 0.0),
-               "mesh_messages": d.get("qmx_exchange_messages_total", 0.0),
-               "epochs": m1.get("qmx_exchange_epochs_total", 0.0)}
+        out["transport"] = "rccl" if want_rccl else "tcp"
+        try:
+            cfg = os.path.join(tmp, "config_spread.yaml")
+            write_config(cfg, mock_ports, False, args.tile, sc, "spread")
+            spec = os.path.join(tmp, "expect_spread.txt")
+            expect_spec(spec, sc, False, mock_expected(bin_dir))
+            if os.environ.get("QMX_BENCH_SPREAD_FAIL_RANK") == str(rank):  # test hook: one rank fails
+                raise RuntimeError("injected spread-check failure")
+            procs = spawn_workers(cfg, "127.0.0.1", port, 1, engine, device, impl="native",
+                                  threads=args.threads, env=env)
+            if not wait_healthy("127.0.0.1", port, 120):
+                raise RuntimeError("spread proxy did not become healthy")
+        except Exception as e:  # noqa: BLE001 - agreed on below, reported in the JSON line
+            ok, err = False, repr(e)[:300]
+        if agree("spawn"):
+            try:
+                t0 = time.time()
+                while True:  # the mesh (and, on GPUs, the RCCL communicator) formed on every rank
+                    m = scrape(port)
+                    if m.get("qmx_exchange_healthy") == 1.0 and (not want_rccl or m.get("qmx_exchange_rccl_active") == 1.0):
+                        break
+                    if time.time() - t0 > 90:
+                        raise RuntimeError(f"exchange did not form: {({k: v for k, v in m.items() if 'exchange' in k})}")
+                    time.sleep(0.2)
+            except Exception as e:  # noqa: BLE001
+                ok, err = False, repr(e)[:300]
+        if agree("exchange formation"):
+            try:
+                m0 = scrape(port)
+                st = loadgen(bin_dir, port, 32, 2048, 2, 120, spec)
+                time.sleep(0.2)
+                m1 = scrape(port)
+                d = {k: m1.get(k, 0.0) - m0.get(k, 0.0) for k in m1 if "exchange" in k or "remote_streams" in k}
+                out.update({"ok": st["invalid"] == 0 and st["errors"] == 0 and st["completed"] == 2048,
+                            "requests": st["completed"], "invalid": st["invalid"],
+                            "p50_ttft_ms": st["ttft_p50_ms"], "p50_latency_ms": st["lat_p50_ms"], "req_s": st["rps"],
+                            "remote_streams": d.get("qmx_remote_streams_total", 0.0),
+                            "rccl_rounds": d.get("qmx_exchange_rounds_total", 0.0),
+                            "rccl_final_bytes": d.get("qmx_exchange_bulk_bytes_total", 0.0),
+                            "mesh_finals": d.get("qmx_exchange_mesh_finals_total", 0.0),
+                            "mesh_messages": d.get("qmx_exchange_messages_total", 0.0),
+                            "epochs": m1.get("qmx_exchange_epochs_total", 0.0)})
+            except Exception as e:  # noqa: BLE001
+                ok, err = False, repr(e)[:300]
     except Exception as e:  # noqa: BLE001 - reported in the JSON line
-        out["error"] = repr(e)[:300]
+        ok, err = False, repr(e)[:300]
     finally:
         _kill(procs)
+    if err:
+        out["ok"] = False
+        out["error"] = err
     return out
 
 

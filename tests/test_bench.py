@@ -84,6 +84,27 @@ def test_bench_two_ranks_torchrun(tmp_path):
     res = _check(lines[0], 2, 2, 1)
     assert res["config"]["global_batch"] == 256
     assert res["config"]["parallelism"].startswith("dp2")
+    assert res["spread_check"]["ok"] is True, res["spread_check"]
+
+
+@pytest.mark.slow
+def test_bench_two_ranks_spread_check_failure_is_agreed(tmp_path):
+    """One rank's spread check fails before its proxy starts: every rank still runs the same
+    collectives (no rank left waiting in a barrier), the headline line is printed and valid,
+    and the failure is reported under spread_check."""
+    port = _free_port()
+    env = dict(_env(), QMX_BENCH_SPREAD_FAIL_RANK="1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), BENCH,
+                        "--gpus", "2", "--steps", "1", "--warmup", "0", "--batch", "64", "--threads", "2",
+                        "--conns", "8", "--port", str(port)],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    res = _check(_json_lines(r.stdout)[0], 2, 1, 0)
+    assert res["valid"] is True
+    sc = res["spread_check"]
+    assert sc["ok"] is False
+    assert "injected" in sc["per_rank"][1]["error"] and "another rank failed" in sc["per_rank"][0]["error"]
 
 
 def test_pin_rank_numa_plan(monkeypatch):
