@@ -354,6 +354,16 @@ def breakdown(m0, m1, elapsed):
                              for k, v in d.items() if k.startswith("qmx_syscalls_total")}
         if d.get("qmx_requests_total") else {},
         "exchange_rounds": int(d.get("qmx_exchange_rounds_total", 0.0)),
+        # where a request's time goes (server-side means over the timed region): upstream
+        # TTFB (request sent -> first response bytes), engine wait (a stream's first bytes fed
+        # -> its final result in the io loop: lane queueing + tick + routing), TTFT and whole
+        # request as the proxy sees them
+        "latency_us_avg": {k: round(1e6 * d[f"{m}_sum"] / d[f"{m}_count"], 1)
+                           for k, m in (("upstream_ttfb", "qmx_upstream_ttfb_seconds"),
+                                        ("engine_wait", "qmx_engine_wait_seconds"),
+                                        ("tick", "qmx_tick_seconds"), ("ttft", "qmx_ttft_seconds"),
+                                        ("request", "qmx_request_latency_seconds"))
+                           if d.get(f"{m}_count")},
     }
 
 

@@ -79,7 +79,9 @@ struct Hist {
   }
 };
 constexpr double Hist::le[Hist::N];
-Hist h_ttft, h_latency, h_tick, h_upstream_ttfb;
+// h_engine: a stream's first upstream body bytes handed to the engine -> its final result
+// applied in the io loop (queueing for a tick lane + tick(s) + routing back)
+Hist h_ttft, h_latency, h_tick, h_upstream_ttfb, h_engine;
 
 using Clock = std::chrono::steady_clock;
 inline double now_s() { return std::chrono::duration<double>(Clock::now().time_since_epoch()).count(); }
@@ -337,6 +339,7 @@ struct BState {
   int state = 0;  // 0 running, 1 done, 2 failed
   int status = 0;
   bool aborted = false;
+  double t_fed = 0;  // first body bytes handed to the engine (h_engine)
   // buffered (non-stream) result, call_backend contract
   bool is_json = false;
   JVal js;
@@ -923,6 +926,7 @@ class Loop {
       if ((r.flags & (RF_DONE | RF_ABORTED)) && s->bs[bi].state == 0) {
         s->bs[bi].state = 1;
         s->bs[bi].aborted = (r.flags & RF_ABORTED) != 0;
+        if (s->bs[bi].t_fed > 0) h_engine.observe(now_s() - s->bs[bi].t_fed);
         s->finished++;
       }
       if (s->stage == 0 && s->finished == (int)s->bs.size()) begin_final(s);
@@ -1699,6 +1703,7 @@ class Loop {
   void on_up_body(Up* u, std::string& body) {
     Session* s = u->sess;
     if (u->rp.status == 200 && u->mode == UP_ENGINE) {
+      if (s->bs[u->bi].t_fed == 0) s->bs[u->bi].t_fed = now_s();
       e_feed_move(s->bs[u->bi].slot, body);  // the engine takes the buffer (no copy)
       kick();
       return;
@@ -2492,6 +2497,7 @@ class Loop {
     h_latency.render(m, "qmx_request_latency_seconds");
     h_tick.render(m, "qmx_tick_seconds");
     h_upstream_ttfb.render(m, "qmx_upstream_ttfb_seconds");
+    h_engine.render(m, "qmx_engine_wait_seconds");
     if (xch_) {
       put("qmx_exchange_rounds_total", (double)xch_->rounds());  // RCCL p2p rounds (final texts)
       put("qmx_exchange_bytes_total", (double)xch_->bytes());    // mesh payload bytes
