@@ -116,17 +116,47 @@ struct LdsWords {
 };
 
 // ------------------------------------------------------------------------------------
-// block-level scans (wave64 shuffles + 4-wave combine)
+// block-level scans: wave64 inclusive scans on DPP (row_shr 1/2/4/8 inside each 16-lane
+// row, then row_bcast15 / row_bcast31 across rows — GFX9-family DPP, a few cycles per step
+// instead of a ds_bpermute round trip per __shfl_up), then a cross-wave combine in LDS
 // ------------------------------------------------------------------------------------
+#define QMX_DPP(old, v, ctrl, rm) __builtin_amdgcn_update_dpp((old), (v), (ctrl), (rm), 0xf, false)
+enum : int { DPP_SHR1 = 0x111, DPP_SHR2 = 0x112, DPP_SHR4 = 0x114, DPP_SHR8 = 0x118, DPP_BC15 = 0x142, DPP_BC31 = 0x143 };
+
+__device__ inline int wave_incl_sum(int x) {
+  x += QMX_DPP(0, x, DPP_SHR1, 0xf);  // lanes whose source is outside the row / a masked row get 0
+  x += QMX_DPP(0, x, DPP_SHR2, 0xf);
+  x += QMX_DPP(0, x, DPP_SHR4, 0xf);
+  x += QMX_DPP(0, x, DPP_SHR8, 0xf);
+  x += QMX_DPP(0, x, DPP_BC15, 0xa);  // rows 1, 3 += lane 15 of the row below
+  x += QMX_DPP(0, x, DPP_BC31, 0xc);  // rows 2, 3 += lane 31
+  return x;
+}
+
+// inclusive scan of a (non-commutative) pair monoid, lane order; a lane combines only when
+// its DPP source is valid (exactly the lanes the shuffle scan combined)
+template <class Op>
+__device__ inline int2 wave_incl_pair(int2 x, Op op) {
+  const int lane = threadIdx.x & 63, r = lane & 15;
+  int2 y;
+#define QMX_PAIR_STEP(ctrl, rm, valid) \
+  y.x = QMX_DPP(x.x, x.x, ctrl, rm);   \
+  y.y = QMX_DPP(x.y, x.y, ctrl, rm);   \
+  if (valid) x = op(y, x);
+  QMX_PAIR_STEP(DPP_SHR1, 0xf, r >= 1)
+  QMX_PAIR_STEP(DPP_SHR2, 0xf, r >= 2)
+  QMX_PAIR_STEP(DPP_SHR4, 0xf, r >= 4)
+  QMX_PAIR_STEP(DPP_SHR8, 0xf, r >= 8)
+  QMX_PAIR_STEP(DPP_BC15, 0xa, (lane >> 4) & 1)
+  QMX_PAIR_STEP(DPP_BC31, 0xc, lane >= 32)
+#undef QMX_PAIR_STEP
+  return x;
+}
+
 __device__ inline int block_excl_sum(int v, int32_t* scr, int* total) {
-  int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) scr[w] = x;
+  int w = threadIdx.x >> 6;
+  const int x = wave_incl_sum(v);
+  if ((threadIdx.x & 63) == 63) scr[w] = x;
   __syncthreads();
   int base = 0, tot = 0;
 #pragma unroll
@@ -144,14 +174,7 @@ __device__ inline int block_excl_sum(int v, int32_t* scr, int* total) {
 template <class Op>
 __device__ inline int2 block_excl_pair(int2 v, int2 ident, Op op, int32_t* scr, int2* total) {
   int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int2 x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    int2 y;
-    y.x = __shfl_up(x.x, o, 64);
-    y.y = __shfl_up(x.y, o, 64);
-    if (lane >= o) x = op(y, x);
-  }
+  const int2 x = wave_incl_pair(v, op);
   if (lane == 63) {
     scr[2 * w] = x.x;
     scr[2 * w + 1] = x.y;
@@ -889,13 +912,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
         const int k = __popcll(m & below);
         DepthOp op;
         int2 x = id > 0 ? make_int2(1, 1) : id < 0 ? make_int2(-1, 0) : make_int2(0, 0);
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          int2 y;
-          y.x = __shfl_up(x.x, o, 64);
-          y.y = __shfl_up(x.y, o, 64);
-          if (lane >= o) x = op(y, x);
-        }
+        x = wave_incl_pair(x, op);
         int2 ex;
         ex.x = __shfl_up(x.x, 1, 64);
         ex.y = __shfl_up(x.y, 1, 64);

@@ -289,12 +289,13 @@ __device__ inline int wave_grammar(const uint16_t* tpos, const uint8_t* ttype, i
   // depth: never negative, root closes exactly at the last token
   if (__ballot(v && (da < 0 || (lane < nt - 1 && da < 1) || (lane == nt - 1 && da != 0))) != 0) return LEX_INVALID;
   // container of each token: last opener below at depth db-1
+  // openers occupy every level 0..maxdepth-1 (a token at depth L+1 sits inside an opener
+  // at depth L): walk levels until one has no opener — one ballot per level, no reduction
   int cont = -1;
-  int maxd = db;
-  for (int o = 32; o; o >>= 1) maxd = max(maxd, __shfl_xor(maxd, o, 64));
-  if (maxd > 64) return LEX_COMPLEX;
-  for (int L = 0; L < maxd; ++L) {
-    const uint64_t OL = __ballot(isO && db == L) & below;
+  for (int L = 0; L < 64; ++L) {
+    const uint64_t OLall = __ballot(isO && db == L);
+    if (OLall == 0) break;
+    const uint64_t OL = OLall & below;
     if (db == L + 1 && OL) cont = 63 - __clzll(OL);
   }
   const int ctype = __shfl(ty, cont < 0 ? 0 : cont, 64);
