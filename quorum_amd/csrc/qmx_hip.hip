@@ -2315,6 +2315,7 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
     if (poll_) {
       // one HIP call per tick: completion and kernel span both come from the result records
       wait_results(L, n, m, seq, [&](int i) {
+        if (n_done == 0) L.first_result_us += std::chrono::duration<double, std::micro>(HC::now() - tp1).count();
         if (i == n_done) process_item(n_done++);
       });
       uint64_t a = ~0ull, b = 0;
@@ -2532,6 +2533,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["s3_cycles_lex"] += (double)L.s3_cyc_lex;
     m["host_prep_us"] += L.host_prep_us;
     m["gpu_wait_us"] += L.gpu_wait_us;
+    m["first_result_us"] += L.first_result_us;
     m["process_us"] += L.process_us;
     m["poll_fallbacks"] += (double)L.poll_fallbacks;
     m["fin_launches"] += (double)L.fin_launches;  // tick launches that also carried finalize work

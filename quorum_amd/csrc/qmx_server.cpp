@@ -42,7 +42,8 @@ std::atomic<bool> g_stop{false};
 std::atomic<bool> g_drain{false};  // SIGTERM: stop accepting, finish in-flight sessions, then exit
 std::atomic<int> g_ready{0};       // io loops with a bound listener
 std::atomic<uint64_t> c_requests{0}, c_stream{0}, c_nonstream{0}, c_errors{0}, c_up_fail{0}, c_ticks{0},
-    c_tick_slots{0}, c_up_conns{0}, c_clients{0}, c_remote_streams{0};
+    c_tick_slots{0}, c_up_conns{0}, c_clients{0}, c_remote_streams{0},
+    c_route_ns{0};  // tick lanes: tick returned -> results handed to the io loops + streams settled
 // failures by class
 std::atomic<uint64_t> c_fail_connect{0}, c_fail_timeout{0}, c_fail_status{0}, c_fail_disconnect{0},
     c_fail_protocol{0}, c_stream_aborts{0};
@@ -641,7 +642,8 @@ class GpuHub {
         const double tt = now_s();
         const int64_t created = (int64_t)time(nullptr);
         if (!eng_->tick(created, rb.r, rb.f, lane, &taken)) break;  // nothing this lane may take
-        h_tick.observe(now_s() - tt);
+        const double t_ticked = now_s();
+        h_tick.observe(t_ticked - tt);
         if (ver_) ver_->check(created, rb.r, rb.f);
         c_ticks++;
         c_tick_slots += rb.r.size();
@@ -664,6 +666,7 @@ class GpuHub {
           per[l] = ResultBatch();
         }
         eng_->settle(taken);  // after routing: a stream's next results cannot overtake these
+        c_route_ns += (uint64_t)((now_s() - t_ticked) * 1e9);
         if (tt - last_snap_.load() > 0.05) {
           last_snap_.store(tt);
           std::unordered_map<std::string, double> m;
@@ -2484,6 +2487,7 @@ class Loop {
     put("qmx_client_connections_total", (double)c_clients.load());
     put("qmx_ticks_total", (double)c_ticks.load());
     put("qmx_tick_slots_total", (double)c_tick_slots.load());
+    put("qmx_tick_route_seconds_total", (double)c_route_ns.load() * 1e-9);
     put("qmx_remote_streams_total", (double)c_remote_streams.load());
     m += "qmx_upstream_failures_by_class_total{class=\"connect\"} " + std::to_string(c_fail_connect.load()) + "\n";
     m += "qmx_upstream_failures_by_class_total{class=\"timeout\"} " + std::to_string(c_fail_timeout.load()) + "\n";
