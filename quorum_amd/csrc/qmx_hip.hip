@@ -2318,10 +2318,17 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
         if (n_done == 0) L.first_result_us += std::chrono::duration<double, std::micro>(HC::now() - tp1).count();
         if (i == n_done) process_item(n_done++);
       });
-      uint64_t a = ~0ull, b = 0;
+      uint64_t a = ~0ull, b = 0, t0max = 0;
+      double item_ticks = 0;
       for (int i = 0; i < n; ++i) {
         a = std::min(a, L.h_res[i].t0);
         b = std::max(b, L.h_res[i].t1);
+        t0max = std::max(t0max, L.h_res[i].t0);
+        item_ticks += (double)(L.h_res[i].t1 - L.h_res[i].t0);
+      }
+      if (n > 0) {  // do a tick's items run side by side? (one item's run vs the spread of starts)
+        L.item_us += item_ticks * 1e-2 / n;
+        L.start_spread_us += (double)(t0max - a) * 1e-2;
       }
       for (int i = 0; i < m; ++i) {
         a = std::min(a, L.h_finres[i].t0);
@@ -2534,6 +2541,8 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["host_prep_us"] += L.host_prep_us;
     m["gpu_wait_us"] += L.gpu_wait_us;
     m["first_result_us"] += L.first_result_us;
+    m["item_us"] += L.item_us;
+    m["start_spread_us"] += L.start_spread_us;
     m["process_us"] += L.process_us;
     m["poll_fallbacks"] += (double)L.poll_fallbacks;
     m["fin_launches"] += (double)L.fin_launches;  // tick launches that also carried finalize work
