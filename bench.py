@@ -344,6 +344,7 @@ def breakdown(m0, m1, elapsed):
         "tick_first_result_us_avg": round(d.get("qmx_kernel_first_result_us", 0.0) / launches, 1) if launches else None,
         "tick_item_us_avg": round(d.get("qmx_kernel_item_us", 0.0) / launches, 1) if launches else None,
         "tick_start_spread_us_avg": round(d.get("qmx_kernel_start_spread_us", 0.0) / launches, 1) if launches else None,
+        "tick_items_host_us_avg": round(d.get("qmx_kernel_items_host_us", 0.0) / launches, 1) if launches else None,
         "tick_route_us_avg": round(1e6 * d.get("qmx_tick_route_seconds_total", 0.0) / ticks, 1) if ticks else None,
         "gpu_busy_frac": round(d.get("qmx_kernel_kernel_ms", 0.0) / 1000 / elapsed, 4) if elapsed else None,
         # finalize (K3 strip + K4 join + K5 encode) rides the tick launches: requests folded into

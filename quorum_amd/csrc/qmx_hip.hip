@@ -2315,8 +2315,10 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
     if (poll_) {
       // one HIP call per tick: completion and kernel span both come from the result records
       wait_results(L, n, m, seq, [&](int i) {
-        if (n_done == 0) L.first_result_us += std::chrono::duration<double, std::micro>(HC::now() - tp1).count();
+        const auto ti = HC::now();
+        if (n_done == 0) L.first_result_us += std::chrono::duration<double, std::micro>(ti - tp1).count();
         if (i == n_done) process_item(n_done++);
+        L.items_host_us += std::chrono::duration<double, std::micro>(HC::now() - ti).count();
       });
       uint64_t a = ~0ull, b = 0, t0max = 0;
       double item_ticks = 0;
@@ -2542,6 +2544,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["gpu_wait_us"] += L.gpu_wait_us;
     m["first_result_us"] += L.first_result_us;
     m["item_us"] += L.item_us;
+    m["items_host_us"] += L.items_host_us;
     m["start_spread_us"] += L.start_spread_us;
     m["process_us"] += L.process_us;
     m["poll_fallbacks"] += (double)L.poll_fallbacks;
