@@ -51,8 +51,8 @@ py::tuple tick_to_py(HostEngine& e, int64_t created, int lane = 0, std::vector<i
   }
   py::list r;
   for (auto& x : results) {
-    if (with_gen) r.append(py::make_tuple(x.slot, py::bytes(x.sse), x.flags, x.gen));
-    else r.append(py::make_tuple(x.slot, py::bytes(x.sse), x.flags));
+    if (with_gen) r.append(py::make_tuple(x.slot, py::bytes(x.data(), x.size()), x.flags, x.gen));
+    else r.append(py::make_tuple(x.slot, py::bytes(x.data(), x.size()), x.flags));
   }
   py::list f;
   for (auto& x : fres) {

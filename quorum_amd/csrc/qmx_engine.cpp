@@ -484,7 +484,7 @@ bool HostEngine::tick(int64_t created, std::vector<SlotResult>& results, std::ve
   if (work.empty() && fin.empty()) return false;
   run_tick(work, fin, created, results, fres, lane);
   size_t out = 0;
-  for (auto& r : results) out += r.sse.size();
+  for (auto& r : results) out += r.size();
   std::vector<int>& tk = taken ? *taken : slots;
   for (auto& w : work) tk.push_back(w.slot);
   {

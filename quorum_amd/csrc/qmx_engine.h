@@ -73,14 +73,47 @@ struct EngineOp {
   std::string data;
 };
 
+// A result's SSE bytes may be a view into a tick lane's output arena instead of a copy
+// (HipEngine: the lane turns a tick's result records into results without touching the
+// bytes; the io loop copies them once, into the client's output).  The arena is reused only
+// when no result viewing it is left: ViewRef counts them.
+struct ViewRef {
+  std::atomic<int>* r = nullptr;
+  ViewRef() = default;
+  explicit ViewRef(std::atomic<int>* p) : r(p) {
+    if (r) r->fetch_add(1, std::memory_order_relaxed);
+  }
+  ViewRef(const ViewRef& o) : ViewRef(o.r) {}
+  ViewRef(ViewRef&& o) noexcept : r(o.r) { o.r = nullptr; }
+  ViewRef& operator=(ViewRef o) noexcept {
+    std::swap(r, o.r);
+    return *this;
+  }
+  ~ViewRef() {
+    if (r) r->fetch_sub(1, std::memory_order_release);
+  }
+};
+
 struct SlotResult {
   int slot;
-  std::string sse;
+  std::string sse;  // the SSE bytes, unless `view` is set
   int flags;
   // open() generation of the slot this result belongs to: a slot released while its tick
   // is in flight can be re-opened by another session before the result is applied; the
   // consumer drops results whose generation is not the one it opened (stamped by tick()).
   uint32_t gen = 0;
+  const char* view = nullptr;  // set: the SSE bytes are view[0, view_len) (held by `hold`)
+  uint32_t view_len = 0;
+  ViewRef hold;
+  const char* data() const { return view ? view : sse.data(); }
+  size_t size() const { return view ? view_len : sse.size(); }
+  bool empty() const { return size() == 0; }
+  void clear_sse() {
+    sse.clear();
+    view = nullptr;
+    view_len = 0;
+    hold = ViewRef();
+  }
 };
 struct FinalizeReq {
   int id;

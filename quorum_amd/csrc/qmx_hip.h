@@ -14,6 +14,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <vector>
 
 #include "qmx_engine.h"
 
@@ -37,14 +38,33 @@ struct DevSlot {
   uint8_t tail[kMaxTail];
 };
 
-// Per-backend event shape template (cross-stream): written by the first workgroup of a
-// launch that parses a content event of that backend index, read by the lane's next launch
+// Per-event "hole" template (cross-stream, any event shape): a fully parsed event's bytes
+// with its string-value bodies and numbers as holes.  An event that equals the literal
+// runs between the holes and has a valid JSON string body / number in each hole lexes to
+// the same token sequence, so it has the same parse: its kind (content / skip) and, for
+// content, the target hole's bytes.  Covers what a prefix/suffix template cannot: a new
+// stream's role, first-content and finish events, whose ids and timestamps differ per
+// stream (qmx_lex.h wave_hole_match).
+constexpr int kHoleMax = 16, kHoleTplBytes = 448, kHoleTpls = 4;
+struct HoleTpl {
+  alignas(16) uint8_t bytes[kHoleTplBytes];  // the source event (x[e0, e1))
+  uint16_t len;                               // 0: none
+  uint8_t nh, kind, target, pad0;             // holes; EV_CONTENT / EV_SKIP; content hole
+  uint16_t num_mask;                          // bit i: hole i is a number (else a string body)
+  uint16_t hs[kHoleMax], he[kHoleMax];        // hole i = bytes[hs[i], he[i])
+  uint32_t claim;                             // launch sequence number of the last writer
+  uint32_t pad1[3];
+};
+
+// Per-backend event shape templates (cross-stream): written by the first workgroup of a
+// launch that parses an event of that backend index, read by the lane's next launch
 constexpr int kBackendTpl = 16;  // backend indices with a table entry
 struct BackendTpl {
   alignas(16) uint8_t tpl[kTplBytes];
   uint16_t pre, suf;  // 0: none yet
   uint32_t claim;     // launch sequence number of the last writer
   uint32_t pad[2];
+  HoleTpl hole[kHoleTpls];  // by shape class (hole count, kind): role / content / finish events
 };
 
 enum WorkFlags : uint32_t { WF_EOF = 1, WF_FILTER = 2, WF_EMIT = 4, WF_STARTED = 8, WF_FRESH = 16 };
@@ -104,7 +124,18 @@ struct TickLane {
   bool params_dirty = true;
   uint8_t* h_in = nullptr;
   size_t in_cap = 0;
-  uint8_t* h_out = nullptr;
+  // output arenas (pinned, mapped): results view their SSE bytes in place (SlotResult::view),
+  // so a tick writes into an arena no earlier result still views — a ring that grows while
+  // every arena is held (OutArena objects are never freed: a late ViewRef may still count)
+  struct OutArena {
+    uint8_t* p = nullptr;
+    size_t cap = 0;
+    std::atomic<int> refs{0};
+  };
+  std::vector<OutArena*> outs;
+  size_t out_i = 0;
+  OutArena* out = nullptr;  // this tick's
+  uint8_t* h_out = nullptr;  // == out->p
   size_t out_cap = 0;
   WorkItem* h_items = nullptr;
   WorkResult* h_res = nullptr;

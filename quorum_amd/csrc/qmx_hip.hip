@@ -1903,7 +1903,8 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
     HIP_CHECK(hipMalloc((void**)&L->d_ctl, sizeof(PCtl)));
     HIP_CHECK(hipMemset(L->d_ctl, 0, sizeof(PCtl)));
     ensure_in(*L, 8u << 20);
-    ensure_out(*L, 32u << 20);
+    for (int a = 0; a < 3; ++a) L->outs.push_back(new TickLane::OutArena());
+    ensure_out(*L, 4u << 20);
     L->items_cap = 4096;
     HIP_CHECK(hipHostMalloc((void**)&L->h_items, sizeof(WorkItem) * L->items_cap, hipHostMallocMapped));
     HIP_CHECK(hipHostMalloc((void**)&L->h_res, sizeof(WorkResult) * L->items_cap, hipHostMallocMapped));
@@ -1923,7 +1924,8 @@ HipEngine::~HipEngine() {
     if (L->h_door) hipHostFree(L->h_door);
     if (L->d_ctl) hipFree(L->d_ctl);
     if (L->h_in) hipHostFree(L->h_in);
-    if (L->h_out) hipHostFree(L->h_out);
+    for (TickLane::OutArena* a : L->outs)
+      if (a->p) hipHostFree(a->p);  // the OutArena objects stay (see TickLane::outs)
     if (L->h_items) hipHostFree(L->h_items);
     if (L->h_res) hipHostFree(L->h_res);
     if (L->h_dbg) hipHostFree(L->h_dbg);
@@ -2009,10 +2011,32 @@ void HipEngine::ensure_in(TickLane& L, size_t bytes) {
   HIP_CHECK(hipHostMalloc((void**)&L.h_in, L.in_cap + 64, hipHostMallocMapped));
 }
 void HipEngine::ensure_out(TickLane& L, size_t bytes) {
-  if (bytes <= L.out_cap) return;
-  if (L.h_out) retire_host(L.h_out);
-  L.out_cap = std::max(bytes, L.out_cap * 2);
-  HIP_CHECK(hipHostMalloc((void**)&L.h_out, L.out_cap + 64, hipHostMallocMapped));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const size_t k = L.outs.size();
+    for (size_t i = 1; i <= k; ++i) {
+      const size_t at = (L.out_i + i) % k;
+      TickLane::OutArena* a = L.outs[at];
+      if (a->refs.load(std::memory_order_acquire) != 0) continue;  // an io loop still reads it
+      L.out_i = at;
+      if (bytes > a->cap) {
+        if (a->p) retire_host(a->p);
+        a->cap = std::max(bytes, a->cap * 2);
+        HIP_CHECK(hipHostMalloc((void**)&a->p, a->cap + 64, hipHostMallocMapped));
+      }
+      L.out = a;
+      L.h_out = a->p;
+      L.out_cap = a->cap;
+      return;
+    }
+    if (k < 16) {  // every arena is still viewed: one more
+      L.outs.push_back(new TickLane::OutArena());
+      continue;
+    }
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+      throw std::runtime_error("tick output arenas still viewed by unconsumed results after 10 s");
+    sched_yield();
+  }
 }
 
 void HipEngine::build_params(TickLane& L, int64_t created) {
@@ -2240,10 +2264,16 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
         requeue.push_back(p.slot);  // unprocessed bytes (or a pending EOF) remain
       }
     }
-    std::string sse;
     L.d2h_bytes += r.out_len;
-    if (r.out_len) sse.assign((const char*)L.h_out + L.h_items[i].out_off, r.out_len);
-    if (!sse.empty() || flags) results.push_back({p.slot, std::move(sse), flags});
+    if (r.out_len) {  // a view into this tick's output arena: the io loop copies the bytes once
+      SlotResult x{p.slot, std::string(), flags};
+      x.view = (const char*)L.h_out + L.h_items[i].out_off;
+      x.view_len = r.out_len;
+      x.hold = ViewRef(&L.out->refs);
+      results.push_back(std::move(x));
+    } else if (flags) {
+      results.push_back({p.slot, std::string(), flags});
+    }
   };
   // finalize requests ride the same launch: workgroups [n, n + m)
   std::vector<const FinalizeReq*> fin_host;

@@ -273,7 +273,7 @@ __device__ inline int wave_str_body(const uint8_t* x, int a, int b) {
 // Returns LEX_OK / LEX_INVALID / LEX_COMPLEX exactly like token_grammar (wave-uniform; res
 // is valid in every lane).
 __device__ inline int wave_grammar(const uint16_t* tpos, const uint8_t* ttype, int t0, int nt, EvResult& res,
-                                   bool* content_esc) {
+                                   bool* content_esc, uint64_t* val_open = nullptr) {
   const int lane = threadIdx.x & 63;
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
   res.kind = EV_SKIP;
@@ -303,6 +303,7 @@ __device__ inline int wave_grammar(const uint16_t* tpos, const uint8_t* ttype, i
   const int p = __shfl_up(ty, 1, 64);  // previous token type (lane 0: none)
   const bool keyopen = v && lane > 0 && ty == TK_SOPEN && inObj && (p == TK_LBRACE || p == TK_COMMA);
   const uint64_t KOm = __ballot(keyopen);
+  if (val_open) *val_open = __ballot(v && ty == TK_SOPEN && !keyopen);  // string values (hole templates)
   const bool keyclose = v && ty == TK_SCLOSE && lane > 0 && ((KOm >> (lane - 1)) & 1);
   const bool valend = v && (ty == TK_SCALAR || isC || (ty == TK_SCLOSE && !keyclose));
   const uint64_t VEm = __ballot(valend), KCm = __ballot(keyclose);
@@ -460,6 +461,71 @@ __device__ inline int token_grammar(const uint16_t* tpos, const uint8_t* ttype, 
   res.str_a = tpos[tca] + 1;
   res.str_b = tpos[tcb];
   return LEX_OK;
+}
+
+// ---- hole templates (qmx_hip.h HoleTpl) --------------------------------------------
+// x[a, a+L) == t[q, q+L) with one 8-byte window per lane (L <= 512; t 8-byte aligned with
+// >= 16 readable bytes past q+L).  Wave-uniform.
+__device__ inline bool wave_lit_eq(const uint8_t* x, int a, const uint8_t* t, int q, int L) {
+  const int o = (threadIdx.x & 63) * 8;
+  const bool bad = o < L && lds_window8(x, a + o, a + L) != lds_window8(t, q + o, q + L);
+  return __ballot(bad) == 0;
+}
+
+// The JSON string body that starts at x[a]: the position of its closing (unescaped) quote
+// before b, or -1 (no closing quote, a control character, a bad escape, invalid UTF-8).
+// *bs: the body holds a backslash.  Wave-uniform; 64 bytes per step.
+__device__ inline int wave_str_end(const uint8_t* x, int a, int b, bool* bs) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  int carry_run = 0;
+  bool any_bs = false;
+  for (int blk = a; blk < b; blk += 64) {
+    const int pos = blk + lane;
+    const bool v = pos < b;
+    const uint32_t c = v ? x[pos] : (uint32_t)'a';
+    const uint64_t BSm = __ballot(v && c == '\\');
+    const uint64_t nb = ~BSm & below;
+    const int run = nb ? (lane - 1 - (63 - __clzll(nb))) : (lane + carry_run);
+    const bool esc = run & 1;
+    const uint64_t Qm = __ballot(v && c == '"' && !esc);
+    const int qe = Qm ? __ffsll((unsigned long long)Qm) - 1 : 64;  // the closing quote, if in this block
+    const int bb = Qm ? blk + qe : b;
+    const bool in = v && lane < qe;  // body bytes of this block
+    bool e = in && c < 0x20;
+    if (in && esc) {
+      if (c == 'u') {
+        for (int k = 1; k <= 4; ++k) e = e || pos + k >= bb || hexv(x[pos + k]) < 0;
+      } else {
+        e = e || !(c == '"' || c == '\\' || c == '/' || c == 'b' || c == 'f' || c == 'n' || c == 'r' || c == 't');
+      }
+    }
+    if (__ballot(in && c >= 0x80)) {
+      if (in && c >= 0x80) e = e || utf8_lane_bad(x, pos, a, bb, c);
+    }
+    if (__ballot(e) != 0) return -1;
+    const uint64_t inm = qe >= 64 ? ~0ull : ((1ull << qe) - 1);
+    any_bs = any_bs || (BSm & inm) != 0;
+    if (Qm) {
+      *bs = any_bs;
+      return blk + qe;
+    }
+    const int nv = min(64, b - blk);  // trailing backslash run of this block's valid bytes
+    const uint64_t vm = nv == 64 ? ~0ull : ((1ull << nv) - 1);
+    const uint64_t nbs = ~(BSm & vm) & vm;
+    carry_run = nbs ? (nv - 1 - (63 - __clzll(nbs))) : carry_run + nv;
+  }
+  return -1;
+}
+
+// A number hole at x[p]: the maximal scalar run (<= 32 bytes) must be a JSON number; its
+// end, or -1.  One lane.
+__device__ inline int num_hole_end(const uint8_t* x, int p, int b) {
+  int e = p;
+  while (e < b && e - p <= 32 && lex_scalar_byte(x[e])) ++e;
+  if (e == p || e - p > 32) return -1;
+  const NumScan ns = scan_number(x, p, e);
+  return ns.ok && ns.end == e ? e : -1;
 }
 
 }  // namespace qmx

@@ -451,7 +451,7 @@ class Verifier {
     for (auto& x : r) {
       auto it = map_.find(x.slot);
       if (it == map_.end() || it->second.gen != x.gen) continue;  // stale: slot re-opened
-      it->second.acc[0] += x.sse;
+      it->second.acc[0].append(x.data(), x.size());
       it->second.term[0] |= x.flags & (RF_DONE | RF_ABORTED);
     }
     for (auto& x : f) pfin_[x.id] = x;
@@ -462,7 +462,7 @@ class Verifier {
       auto rit = rmap_.find(x.slot);
       if (rit == rmap_.end()) continue;
       Track& t = map_[rit->second];
-      t.acc[1] += x.sse;
+      t.acc[1].append(x.data(), x.size());
       t.term[1] |= x.flags & (RF_DONE | RF_ABORTED);
     }
     for (auto& kv : map_) {
@@ -916,15 +916,16 @@ class Loop {
       if (it == slot_owner_.end() || it->second.gen != r.gen) continue;
       Session* s = it->second.s;
       int bi = it->second.bi;
-      if (fault_drop_every_ > 0 && !r.sse.empty() && ++fault_n_ % fault_drop_every_ == 0)
-        r.sse.clear();  // QMX_FAULT_DROP_DELTA: fault injection (the bench's validator must notice)
-      if (!r.sse.empty()) {
+      if (fault_drop_every_ > 0 && !r.empty() && ++fault_n_ % fault_drop_every_ == 0)
+        r.clear_sse();  // QMX_FAULT_DROP_DELTA: fault injection (the bench's validator must notice)
+      if (!r.empty()) {
         if (s->kind == K_REMOTE) {
-          post_owner(s, X_DATA, 0, 0, r.sse);
+          post_owner(s, X_DATA, 0, 0, std::string(r.data(), r.size()));
           s->data_sent++;
         }
-        else if (s->cl) send_content(s, r.sse);
+        else if (s->cl) send_content(s, r.data(), r.size());
       }
+      r.hold = ViewRef();  // the bytes were copied (or dropped): the lane may reuse its arena
       if ((r.flags & RF_ABORTED)) c_stream_aborts++;
       if ((r.flags & (RF_DONE | RF_ABORTED)) && s->bs[bi].state == 0) {
         s->bs[bi].state = 1;
@@ -1093,16 +1094,17 @@ class Loop {
     }
   }
   // HTTP chunk framing appended straight into the corked output (no temporary string)
-  void write_chunk(Client* c, const std::string& data) {
-    if (c->dead || data.empty()) return;
+  void write_chunk(Client* c, const std::string& data) { write_chunk(c, data.data(), data.size()); }
+  void write_chunk(Client* c, const char* data, size_t len) {
+    if (c->dead || len == 0) return;
     if (c->out.size() == c->out_off) {
       c->out.clear();
       c->out_off = 0;
     }
     char h[24];
-    const int n = snprintf(h, sizeof(h), "%zx\r\n", data.size());
+    const int n = snprintf(h, sizeof(h), "%zx\r\n", len);
     c->out.append(h, n);
-    c->out += data;
+    c->out.append(data, len);
     c->out.append("\r\n", 2);
     if (!c->queued && !c->want_out) {
       c->queued = true;
@@ -1834,12 +1836,13 @@ class Loop {
     if (s->cl) write_chunk(s->cl, data);
   }
   // content-bearing events: the first one closes the session's TTFT span
-  void send_content(Session* s, const std::string& data) {
+  void send_content(Session* s, const std::string& data) { send_content(s, data.data(), data.size()); }
+  void send_content(Session* s, const char* data, size_t len) {
     if (!s->first_content) {
       s->first_content = true;
       h_ttft.observe(now_s() - s->t0);
     }
-    send_chunk(s, data);
+    if (s->cl) write_chunk(s->cl, data, len);
   }
   void start_parallel(Session* s, const std::vector<int>& valid) {
     c_stream++;
