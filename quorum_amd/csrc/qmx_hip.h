@@ -49,9 +49,9 @@ constexpr int kHoleMax = 16, kHoleTplBytes = 448, kHoleTpls = 4;
 struct HoleTpl {
   alignas(16) uint8_t bytes[kHoleTplBytes];  // the source event (x[e0, e1))
   uint16_t len;                               // 0: none
-  uint8_t nh, kind, target, pad0;             // holes; EV_CONTENT / EV_SKIP; content hole
-  uint16_t num_mask;                          // bit i: hole i is a number (else a string body)
+  uint8_t nh, kind, target, tgt_bs;           // holes; EV_CONTENT / EV_SKIP; content hole; it has a '\\'
   uint16_t hs[kHoleMax], he[kHoleMax];        // hole i = bytes[hs[i], he[i])
+  uint8_t num[kHoleMax];                      // 1: hole i is a number, 0: a string body
   uint32_t claim;                             // launch sequence number of the last writer
   uint32_t pad1[3];
 };
@@ -145,7 +145,7 @@ struct TickLane {
   // counters (summed over lanes by kernel_stats)
   uint64_t launches = 0, items = 0, h2d_bytes = 0, d2h_bytes = 0;
   uint64_t s3_full = 0, s3_tpl = 0, s3_events = 0, stage_n = 0;  // QMX_STAGE_TIMING: S3 path counters
-  uint64_t s3_cyc_full = 0, s3_cyc_tpl = 0, s3_cyc_lex = 0;  // S3 wave cycles: full parse / templates / lexer
+  uint64_t s3_cyc_full = 0, s3_cyc_tpl = 0, s3_cyc_lex = 0, s3_hole = 0;  // S3 wave cycles: full parse / templates / lexer
   double kernel_ms = 0.0, host_prep_us = 0, gpu_wait_us = 0, process_us = 0;  // host-side tick breakdown
   double first_result_us = 0;  // tick posted -> first result record seen by the host
   double item_us = 0, start_spread_us = 0;
@@ -246,6 +246,7 @@ class HipEngine : public HostEngine {
   bool poll_ = true;  // QMX_WAIT=event: wait on a blocking-sync HIP event instead of polling
   int poll_us_ = 1;   // QMX_POLL_US: poll period once the expected kernel time has passed (MI355X A/Bs: 2 beats 6, 1 beats 2)
   bool persistent_ = true;   // a long-lived grid per lane, ticks posted by doorbell (QMX_PERSISTENT=0: a launch per tick)
+  bool views_ = true;         // QMX_VIEWS=0: results copy their SSE bytes on the lane thread
   int p_grid_ = 64;          // QMX_PERSISTENT_WG: workgroups per lane grid (1 per CU: 256 VGPRs)
   int p_idle_ms_ = 50;       // the grid exits after this long without a tick
 

@@ -95,7 +95,7 @@ static_assert(TPL_BYTES == kTplBytes, "template size");
 enum : int {
   V_START = 0, V_NSEP, V_LASTSEP, V_ABORT, V_NEV, V_CONSUMED, V_STATUS, V_NDELTA, V_YLEN, V_NCAND,
   V_NTOK, V_BAIL, V_DEPTH0, V_TAILLEN, V_NEWTAIL, V_NEWDEPTH, V_WLEN, V_NEMIT, V_ETOT, V_OUTLEN,
-  V_TPLPRE, V_TPLSUF, V_TPLK, V_NEXTEV, V_NFULL, V_NTPL, V_CFULL, V_CTPL, V_CLEX
+  V_TPLPRE, V_TPLSUF, V_TPLK, V_NEXTEV, V_NFULL, V_NTPL, V_CFULL, V_CTPL, V_CLEX, V_NHOLE
 };
 
 // LDS byte reader that fetches one aligned 64-bit word per 8 sequential bytes: a byte-serial
@@ -324,6 +324,102 @@ __device__ inline int hold_cut(const Smem& s, const uint8_t* Z, int ncand, int n
 }
 
 // ------------------------------------------------------------------------------------
+// hole templates (qmx_hip.h HoleTpl): match and publish, one wave per event
+// ------------------------------------------------------------------------------------
+// Does the event x[e0, e1) equal T's literal runs with a valid string body / number in each
+// hole?  Then it has T's parse: kind T.kind and, for content, the target hole (*sa, *sb,
+// *body: 1 when it holds a backslash).  Wave-uniform (T is in LDS).
+__device__ inline bool wave_hole_match(const uint8_t* x, int e0, int e1, const HoleTpl& T, int* sa, int* sb,
+                                       int* body) {
+  const int n = T.len, nh = T.nh;
+  if (e1 - e0 == n && wave_lit_eq(x, e0, T.bytes, 0, n)) {  // the very same bytes (one compare)
+    if (T.kind == EV_CONTENT) {
+      *sa = e0 + T.hs[T.target];
+      *sb = e0 + T.he[T.target];
+      *body = T.tgt_bs;
+    }
+    return true;
+  }
+  int p = e0, q = 0;
+  for (int i = 0; i < nh; ++i) {
+    const int L = (int)T.hs[i] - q;
+    if (p + L > e1 || !wave_lit_eq(x, p, T.bytes, q, L)) return false;
+    p += L;
+    q = T.he[i];
+    int end;
+    bool bs = false;
+    if (T.num[i]) {
+      int r = -1;
+      if ((threadIdx.x & 63) == 0) r = num_hole_end(x, p, e1);
+      end = __builtin_amdgcn_readfirstlane(r);
+    } else {
+      end = wave_str_end(x, p, e1, &bs);
+    }
+    if (end < 0) return false;
+    if (i == T.target && T.kind == EV_CONTENT) {
+      *sa = p;
+      *sb = end;
+      *body = bs ? 1 : 0;
+    }
+    p = end;
+  }
+  const int L = n - q;
+  return p + L == e1 && wave_lit_eq(x, p, T.bytes, q, L);
+}
+
+// After a full parse of x[e0, e1) (tokens tpos/ttype[0, nt), string-value opens `vopen`,
+// result kind / content body start str_a): its hole template into the launch's write table,
+// entry by shape class, if no other workgroup of this launch claimed that entry.
+__device__ inline void wave_hole_publish(const uint8_t* x, int e0, int e1, const uint16_t* tpos,
+                                         const uint8_t* ttype, int nt, uint64_t vopen, int kind, int str_a,
+                                         bool tgt_bs, HoleTpl* table, uint32_t seq) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const bool v = lane < nt;
+  const int pos = v ? (int)tpos[lane] : 0;
+  const int ty = v ? (ttype[lane] & TK_TYPE) : 0;
+  const int nxt = __shfl_down(pos, 1, 64);  // a string value's closing quote (its SCLOSE token)
+  const bool hstr = (vopen >> lane) & 1;
+  int nend = -1;
+  if (v && ty == TK_SCALAR) {
+    const uint32_t c = x[pos];
+    if (c == '-' || c - '0' < 10u) nend = num_hole_end(x, pos, e1);
+  }
+  const bool hnum = nend > 0;
+  const uint64_t H = __ballot(hstr || hnum);
+  const int nh = __popcll(H);
+  if (nh > kHoleMax) return;
+  int target = 0;
+  if (kind == EV_CONTENT) {
+    const uint64_t Tm = __ballot(hstr && pos + 1 == str_a);
+    if (Tm == 0) return;
+    target = __popcll(H & ((1ull << (__ffsll((unsigned long long)Tm) - 1)) - 1));
+  }
+  HoleTpl& D = table[(nh * 2 + (kind == EV_CONTENT ? 1 : 0)) % kHoleTpls];
+  int won = 0;
+  if (lane == 0) {
+    const uint32_t old = __hip_atomic_load(&D.claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    won = old != seq && atomicCAS(&D.claim, old, seq) == old;
+  }
+  if (!__builtin_amdgcn_readfirstlane(won)) return;
+  const int len = e1 - e0;
+  for (int i = lane; i < len; i += 64) D.bytes[i] = x[e0 + i];
+  if ((H >> lane) & 1) {
+    const int k = __popcll(H & below);
+    D.hs[k] = (uint16_t)((hstr ? pos + 1 : pos) - e0);
+    D.he[k] = (uint16_t)((hstr ? nxt : nend) - e0);
+    D.num[k] = hnum ? 1 : 0;
+  }
+  if (lane == 0) {
+    D.nh = (uint8_t)nh;
+    D.kind = (uint8_t)kind;
+    D.target = (uint8_t)target;
+    D.tgt_bs = tgt_bs ? 1 : 0;
+    D.len = (uint16_t)len;
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // the fused tick kernel
 // ------------------------------------------------------------------------------------
 // LDS of a tick workgroup (the fused kernel overlays it with the finalize workgroup's)
@@ -333,6 +429,7 @@ struct TickShared {
   uint16_t TKP[BS / 64][TOK_CAP];              // per-wave token buffers (positions)
   alignas(8) uint8_t TKT[BS / 64][TOK_CAP];    // token bytes (type | key id | flags)
   int wtpl[BS / 64][4];  // S3: per-wave in-tile templates {p0, tp, s0, ts} (p0 < 0: none)
+  HoleTpl htpl[kHoleTpls];  // S3: this item's backend hole templates (previous launch's)
 };
 
 __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, const uint8_t* __restrict__ in,
@@ -377,7 +474,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     s.v[V_STATUS] = 0;
     s.v[V_TPLK] = -1;
     s.v[V_NEXTEV] = 0;
-    s.v[V_NFULL] = s.v[V_NTPL] = s.v[V_CFULL] = s.v[V_CTPL] = s.v[V_CLEX] = 0;
+    s.v[V_NFULL] = s.v[V_NTPL] = s.v[V_CFULL] = s.v[V_CTPL] = s.v[V_CLEX] = s.v[V_NHOLE] = 0;
     for (int q = 0; q < BS / 64; ++q) wtpl[q][0] = -1;
     if (fresh) {
       s.v[V_DEPTH0] = 0;
@@ -403,6 +500,16 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   if (tid < TPL_BYTES / 16) {
     if (own_tpl) ((uint4*)s.tpl)[tid] = ((const uint4*)state[it.slot].tpl)[tid];
     else if (borrow) ((uint4*)s.tpl)[tid] = ((const uint4*)bt->tpl)[tid];
+  }
+  {  // the backend's hole templates (role / content / finish shapes of other streams)
+    constexpr int kHW = (int)(sizeof(HoleTpl) * kHoleTpls / 16);
+    static_assert(sizeof(HoleTpl) % 16 == 0, "HoleTpl copies as uint4");
+    const bool have = btpl_rd != nullptr && it.index < (uint32_t)kBackendTpl;
+    if (have) {
+      for (int i = tid; i < kHW; i += BS) ((uint4*)U.htpl)[i] = ((const uint4*)btpl_rd[it.index].hole)[i];
+    } else if (tid < kHoleTpls) {
+      U.htpl[tid].len = 0;
+    }
   }
   __syncthreads();
   QMX_STAMP(1);
@@ -603,6 +710,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     const int tp = s.v[V_TPLPRE], ts = s.v[V_TPLSUF];
     bool published = false;
     int hint = w;  // template that matched last (tried first)
+    int hhint = 0;  // hole template that matched last
     while (true) {
       int g = 0;
       if (lane == 0) g = atomicAdd(&s.v[V_NEXTEV], 1);
@@ -655,35 +763,73 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
           int a = e0 + 6, b = e1;
           ustrip(s.A, &a, &b);
           if (!(b - a == 6 && lit_at(s.A, a, b, QMX_LIT("[DONE]")))) {
-            const uint64_t cl0 = probe ? __builtin_amdgcn_s_memtime() : 0;
-            nt = wave_lex(s.A, a, b, TKP[w], TKT[w], 0, TOK_CAP);
-            if (probe && lane == 0) atomicAdd(&s.v[V_CLEX], (int)(__builtin_amdgcn_s_memtime() - cl0));
-            if (lane == 0) atomicAdd(&s.v[V_NFULL], 1);
-            if (nt == -LEX_COMPLEX) {
-              slow = true;
-            } else if (nt > 64) {
-              lexed = true;
-            } else if (nt >= 0) {
-              EvResult r;
-              bool esc = true;
-              const int g = wave_grammar(TKP[w], TKT[w], 0, nt, r, &esc);
-              if (g == LEX_COMPLEX) {
-                slow = true;
-              } else if (g == LEX_OK) {
-                kind = r.kind;
-                sa = r.str_a;
-                sb = r.str_b;
-                body = esc ? 1 : 0;
-                if (kind == EV_CONTENT && sa - e0 <= TPL_PRE_MAX && e1 - sb <= TPL_SUF_MAX && lane == 0) {
-                  if (!published) {  // later events (any wave) compare against this one
+            // a hole template of this backend (another stream's event of the same shape)?
+            bool hm = false;
+            for (int q = 0; q < kHoleTpls && !hm; ++q) {
+              const int qi = (hhint + q) & (kHoleTpls - 1);
+              const HoleTpl& T = U.htpl[qi];
+              if (T.len == 0) continue;
+              int ha = 0, hb = 0, hbody = 0;
+              if (!wave_hole_match(s.A, e0, e1, T, &ha, &hb, &hbody)) continue;
+              hm = true;
+              hhint = qi;
+              kind = T.kind;
+              if (kind == EV_CONTENT) {
+                sa = ha;
+                sb = hb;
+                body = hbody;
+              }
+              if (lane == 0) atomicAdd(&s.v[V_NHOLE], 1);
+              if (kind == EV_CONTENT && sa - e0 <= TPL_PRE_MAX && e1 - sb <= TPL_SUF_MAX) {
+                if (lane == 0) {
+                  if (!published) {  // as a parsed event: later events compare against this one
                     wtpl[w][1] = sa - e0;
                     wtpl[w][2] = sb;
                     wtpl[w][3] = e1 - sb;
                     __atomic_store_n(&wtpl[w][0], e0, __ATOMIC_RELEASE);
                   }
-                  atomicMax(&s.v[V_TPLK], k);  // newest parsed content → device template
+                  atomicMax(&s.v[V_TPLK], k);
                 }
-                if (kind == EV_CONTENT && sa - e0 <= TPL_PRE_MAX && e1 - sb <= TPL_SUF_MAX) published = true;
+                published = true;
+              }
+            }
+            if (!hm) {
+              const uint64_t cl0 = probe ? __builtin_amdgcn_s_memtime() : 0;
+              nt = wave_lex(s.A, a, b, TKP[w], TKT[w], 0, TOK_CAP);
+              if (probe && lane == 0) atomicAdd(&s.v[V_CLEX], (int)(__builtin_amdgcn_s_memtime() - cl0));
+              if (lane == 0) atomicAdd(&s.v[V_NFULL], 1);
+              if (nt == -LEX_COMPLEX) {
+                slow = true;
+              } else if (nt > 64) {
+                lexed = true;
+              } else if (nt >= 0) {
+                EvResult r;
+                bool esc = true;
+                uint64_t vopen = 0;
+                const int g = wave_grammar(TKP[w], TKT[w], 0, nt, r, &esc, &vopen);
+                if (g == LEX_COMPLEX) {
+                  slow = true;
+                } else if (g == LEX_OK) {
+                  kind = r.kind;
+                  sa = r.str_a;
+                  sb = r.str_b;
+                  body = esc ? 1 : 0;
+                  if (kind == EV_CONTENT && sa - e0 <= TPL_PRE_MAX && e1 - sb <= TPL_SUF_MAX && lane == 0) {
+                    if (!published) {  // later events (any wave) compare against this one
+                      wtpl[w][1] = sa - e0;
+                      wtpl[w][2] = sb;
+                      wtpl[w][3] = e1 - sb;
+                      __atomic_store_n(&wtpl[w][0], e0, __ATOMIC_RELEASE);
+                    }
+                    atomicMax(&s.v[V_TPLK], k);  // newest parsed content → device template
+                  }
+                  if (kind == EV_CONTENT && sa - e0 <= TPL_PRE_MAX && e1 - sb <= TPL_SUF_MAX) published = true;
+                  // its hole template for the next launch: other streams' events of this shape
+                  // (ids / timestamps / text differ) then skip the full parse
+                  if ((kind == EV_CONTENT || kind == EV_SKIP) && e1 - e0 <= kHoleTplBytes && btpl_wr != nullptr &&
+                      it.index < (uint32_t)kBackendTpl)
+                    wave_hole_publish(s.A, e0, e1, TKP[w], TKT[w], nt, vopen, kind, sa, esc, btpl_wr[it.index].hole, seq);
+                }
               }
             }
           }
@@ -1221,6 +1367,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     P.dbg[bi * kDbg + 16] = (unsigned long long)s.v[V_CFULL];  // S3 cycles: full parses (sum over waves)
     P.dbg[bi * kDbg + 17] = (unsigned long long)s.v[V_CTPL];   // S3 cycles: template checks
     P.dbg[bi * kDbg + 18] = (unsigned long long)s.v[V_CLEX];   // S3 cycles: wave_lex part of full
+    P.dbg[bi * kDbg + 19] = (unsigned long long)s.v[V_NHOLE];  // S3: hole-template hits
   }
   if (tid == 0) {
     WorkResult r{(uint32_t)s.v[V_CONSUMED], (uint32_t)out_len, (uint32_t)s.v[V_STATUS], new_clen};
@@ -1851,6 +1998,7 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
   // device (a rehearsal with more ranks than GPUs) need not all be resident at once
   if (const char* gs = getenv("QMX_GPU_SHARERS")) persistent_ = atoi(gs) <= 1;
   if (const char* pe = getenv("QMX_PERSISTENT")) persistent_ = atoi(pe) != 0;
+  if (const char* va = getenv("QMX_VIEWS")) views_ = atoi(va) != 0;
   if (const char* pw = getenv("QMX_PERSISTENT_WG")) p_grid_ = std::min(std::max(8, atoi(pw)), 1024);
   if (const char* pi = getenv("QMX_PERSISTENT_IDLE_MS")) p_idle_ms_ = std::min(std::max(5, atoi(pi)), 1000);
   HIP_CHECK(hipMalloc(&d_state_, sizeof(DevSlot) * (size_t)max_slots_));
@@ -2014,7 +2162,7 @@ void HipEngine::ensure_out(TickLane& L, size_t bytes) {
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     const size_t k = L.outs.size();
-    for (size_t i = 1; i <= k; ++i) {
+    for (size_t i = 0; i < k; ++i) {  // the last one first: a GPU-warm set of host pages
       const size_t at = (L.out_i + i) % k;
       TickLane::OutArena* a = L.outs[at];
       if (a->refs.load(std::memory_order_acquire) != 0) continue;  // an io loop still reads it
@@ -2265,7 +2413,9 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
       }
     }
     L.d2h_bytes += r.out_len;
-    if (r.out_len) {  // a view into this tick's output arena: the io loop copies the bytes once
+    if (r.out_len && !views_) {
+      results.push_back({p.slot, std::string((const char*)L.h_out + L.h_items[i].out_off, r.out_len), flags});
+    } else if (r.out_len) {  // a view into this tick's output arena: the io loop copies the bytes once
       SlotResult x{p.slot, std::string(), flags};
       x.view = (const char*)L.h_out + L.h_items[i].out_off;
       x.view_len = r.out_len;
@@ -2403,6 +2553,7 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
         L.s3_cyc_full += L.h_dbg[kDbg * i + 16];
         L.s3_cyc_tpl += L.h_dbg[kDbg * i + 17];
         L.s3_cyc_lex += L.h_dbg[kDbg * i + 18];
+        L.s3_hole += L.h_dbg[kDbg * i + 19];
       }
     }
   }
@@ -2570,6 +2721,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["s3_cycles_full"] += (double)L.s3_cyc_full;
     m["s3_cycles_template"] += (double)L.s3_cyc_tpl;
     m["s3_cycles_lex"] += (double)L.s3_cyc_lex;
+    m["s3_hole_hits"] += (double)L.s3_hole;
     m["host_prep_us"] += L.host_prep_us;
     m["gpu_wait_us"] += L.gpu_wait_us;
     m["first_result_us"] += L.first_result_us;

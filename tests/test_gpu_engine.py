@@ -305,3 +305,70 @@ def test_hip_completion_modes(ext, monkeypatch):
     eng.release(slot)
     monkeypatch.setenv("QMX_WAIT", "event")
     _check(7002, 40)
+
+
+def _oai_event(id_, created, model, delta, finish=b"null", compact=False):
+    sep = b"," if compact else b", "
+    col = b":" if compact else b": "
+    obj = (b"{" + b'"id"' + col + b'"' + id_ + b'"' + sep + b'"object"' + col + b'"chat.completion.chunk"' + sep +
+           b'"created"' + col + created + sep + b'"model"' + col + b'"' + model + b'"' + sep + b'"choices"' + col +
+           b'[{"index"' + col + b"0" + sep + b'"delta"' + col + delta + sep + b'"logprobs"' + col + b"null" + sep +
+           b'"finish_reason"' + col + finish + b"}]}")
+    return b"data: " + obj + b"\n\n"
+
+
+# hole contents: valid and invalid string bodies / numbers, type changes
+HOLE_STR = [b"abc", b"", b'q\\"x', b"\\u00e9\\ud83d\\ude00", b"\xc3\xa9 ok", b"bad\xff", b"tail\\\\", b"a\\", b"x\x01y",
+            b"\\uZZZZ", b"<think>", b"</think>", b"e\\nf", b"\\/", b"\xe4\xb8\xad" * 20, b"q" * 120]
+HOLE_NUM = [b"1700000000", b"0", b"-1", b"01", b"1.5e3", b"-", b"1e400", b"123456789012345678901234567890123456",
+            b"2.", b"-0", b"1E+2", b"true", b"null", b'"1700000000"']
+
+
+def test_hip_hole_templates(ext, monkeypatch):
+    """Cross-stream hole templates: fresh streams whose ids / timestamps / models / text all
+    differ match an earlier launch's role, content and finish shapes without a full parse,
+    and every anomaly in a hole (invalid string body, invalid or non-number scalar, a type
+    change, a different spacing) falls back to the full parse — byte-identical to the CPU
+    engine either way."""
+    monkeypatch.setenv("QMX_STAGE_TIMING", "1")  # per-item S3 counters (hole hits)
+    rng = random.Random(11)
+    tags = ["think", "reason"]
+    hip, cpu = _hip(tags), NativeEngine("cpu", tags)
+    got = {"hip": {}, "cpu": {}}
+    for rnd in range(6):
+        bodies = []
+        for k in range(16):
+            bad = rnd >= 2 and rng.random() < 0.5  # anomalies only after templates exist
+            id_ = b"chatcmpl-" + bytes(rng.choice(b"abcdef0123456789") for _ in range(rng.randint(4, 24)))
+            created = rng.choice(HOLE_NUM) if bad and rng.random() < 0.3 else str(rng.randint(1, 2 ** 31)).encode()
+            model = rng.choice(HOLE_STR) if bad and rng.random() < 0.3 else rng.choice([b"m-1", b"gpt-x", b"mock"])
+            compact = bad and rng.random() < 0.1
+            evs = [_oai_event(id_, created, model, b'{"role": "assistant", "content": ""}', compact=compact)]
+            for _ in range(rng.randint(1, 12)):
+                txt = rng.choice(HOLE_STR) if bad else bytes(rng.choice(b"abc <>xyz") for _ in range(rng.randint(0, 9)))
+                delta = b'{"content": "' + txt + b'"}'
+                if bad and rng.random() < 0.15:
+                    delta = rng.choice([b'{"content": null}', b'{"content": 5}', b'{"content": ["x"]}', b"{}"])
+                evs.append(_oai_event(id_, created, model, delta, compact=compact))
+            evs.append(_oai_event(id_, created, model, b"{}", finish=rng.choice([b'"stop"', b'"length"', b"null"])))
+            evs.append(b"data: [DONE]\n\n")
+            bodies.append(b"".join(evs))
+        for name, eng in (("hip", hip), ("cpu", cpu)):
+            slots = [eng.open(k % 3, True, True) for k in range(len(bodies))]
+            for sl, body in zip(slots, bodies):
+                eng.feed(sl, body)
+                eng.finish(sl)
+            acc = {sl: [b"", 0] for sl in slots}
+            for _ in range(50):
+                res, _ = eng.tick(H.CREATED)
+                for sl, data, fl in res:
+                    acc[sl][0] += data
+                    acc[sl][1] |= fl
+                if not eng.has_work():
+                    break
+            for k, sl in enumerate(slots):
+                got[name][(rnd, k)] = tuple(acc[sl])
+                eng.release(sl)
+    assert got["hip"] == got["cpu"]
+    st = hip._e.kernel_stats()
+    assert st.get("s3_hole_hits", 0) > 50, st  # fresh streams' role / finish / first events
