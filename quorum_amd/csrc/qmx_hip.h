@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cstddef>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -52,9 +53,12 @@ struct HoleTpl {
   uint8_t nh, kind, target, tgt_bs;           // holes; EV_CONTENT / EV_SKIP; content hole; it has a '\\'
   uint16_t hs[kHoleMax], he[kHoleMax];        // hole i = bytes[hs[i], he[i])
   uint8_t num[kHoleMax];                      // 1: hole i is a number, 0: a string body
-  uint32_t claim;                             // launch sequence number of the last writer
+  uint8_t pad0[10];
+  uint32_t claim;  // launch sequence number of the last writer (its own 16 B: a copy skips it)
   uint32_t pad1[3];
 };
+
+static_assert(offsetof(HoleTpl, claim) == sizeof(HoleTpl) - 16, "claim in the last 16 bytes");
 
 // Per-backend event shape templates (cross-stream): written by the first workgroup of a
 // launch that parses an event of that backend index, read by the lane's next launch

@@ -419,6 +419,21 @@ __device__ inline void wave_hole_publish(const uint8_t* x, int e0, int e1, const
   }
 }
 
+// A hole template that matched in this launch is carried into the launch's write table
+// (the tables alternate per launch: a shape that only ever matches would otherwise vanish
+// from every other launch).  Everything but the claim word is copied.
+__device__ inline void wave_hole_carry(const HoleTpl& T, HoleTpl* dst, uint32_t seq) {
+  const int lane = threadIdx.x & 63;
+  int won = 0;
+  if (lane == 0) {
+    const uint32_t old = __hip_atomic_load(&dst->claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    won = old != seq && atomicCAS(&dst->claim, old, seq) == old;
+  }
+  if (!__builtin_amdgcn_readfirstlane(won)) return;
+  constexpr int kW = (int)(sizeof(HoleTpl) / 16) - 1;
+  if (lane < kW) ((uint4*)dst)[lane] = ((const uint4*)&T)[lane];
+}
+
 // ------------------------------------------------------------------------------------
 // the fused tick kernel
 // ------------------------------------------------------------------------------------
@@ -774,6 +789,8 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
               hm = true;
               hhint = qi;
               kind = T.kind;
+              if (btpl_wr != nullptr && it.index < (uint32_t)kBackendTpl)
+                wave_hole_carry(T, &btpl_wr[it.index].hole[qi], seq);
               if (kind == EV_CONTENT) {
                 sa = ha;
                 sb = hb;
