@@ -55,7 +55,7 @@ constexpr int MAX_EV = 512;  // events per tile (more → WS_MORE requeue); keep
 constexpr int MAX_CAND = 1024;
 constexpr int PAD = 16;
 constexpr int TOK_CAP = 512;
-constexpr int kDbg = 20;  // QMX_STAGE_TIMING record per work item: stamps 0-12, S3 counters 13-17  // tokens per wave (an event with more → scalar fallback)
+constexpr int kDbg = 21;  // QMX_STAGE_TIMING record per work item: stamps 0-12, S3 counters 13-20
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 
@@ -95,7 +95,7 @@ static_assert(TPL_BYTES == kTplBytes, "template size");
 enum : int {
   V_START = 0, V_NSEP, V_LASTSEP, V_ABORT, V_NEV, V_CONSUMED, V_STATUS, V_NDELTA, V_YLEN, V_NCAND,
   V_NTOK, V_BAIL, V_DEPTH0, V_TAILLEN, V_NEWTAIL, V_NEWDEPTH, V_WLEN, V_NEMIT, V_ETOT, V_OUTLEN,
-  V_TPLPRE, V_TPLSUF, V_TPLK, V_NEXTEV, V_NFULL, V_NTPL, V_CFULL, V_CTPL, V_CLEX, V_NHOLE
+  V_TPLPRE, V_TPLSUF, V_TPLK, V_NEXTEV, V_NFULL, V_NTPL, V_CFULL, V_CTPL, V_CLEX, V_NHOLE, V_CHOLE
 };
 
 // LDS byte reader that fetches one aligned 64-bit word per 8 sequential bytes: a byte-serial
@@ -329,17 +329,41 @@ __device__ inline int hold_cut(const Smem& s, const uint8_t* Z, int ncand, int n
 // Does the event x[e0, e1) equal T's literal runs with a valid string body / number in each
 // hole?  Then it has T's parse: kind T.kind and, for content, the target hole (*sa, *sb,
 // *body: 1 when it holds a backslash).  Wave-uniform (T is in LDS).
+__device__ inline bool wave_hole_exact(const uint8_t* x, int e0, int e1, const HoleTpl& T, int* sa, int* sb,
+                                       int* body) {
+  const int n = T.len;
+  if (n == 0 || e1 - e0 != n || !wave_lit_eq(x, e0, T.bytes, 0, n)) return false;  // the very same bytes
+  if (T.kind == EV_CONTENT) {
+    *sa = e0 + T.hs[T.target];
+    *sb = e0 + T.he[T.target];
+    *body = T.tgt_bs;
+  }
+  return true;
+}
+
+// One step that rejects most other shapes: the event's head / tail against T's first / last
+// literal run (up to 256 bytes each, a half wave each).
+__device__ inline bool wave_hole_quick(const uint8_t* x, int e0, int e1, const HoleTpl& T) {
+  const int n = T.len, nh = T.nh;
+  if (n == 0 || nh == 0) return false;  // no holes: only the exact compare applies
+  const int L0 = T.hs[0], Lm = n - (int)T.he[nh - 1];
+  if (e1 - e0 < L0 + Lm) return false;
+  const int lane = threadIdx.x & 63;
+  bool bad = false;
+  if (lane < 32) {
+    const int o = lane * 8, L = min(L0, 256);
+    if (o < L) bad = lds_window8(x, e0 + o, e0 + L) != lds_window8(T.bytes, o, L);
+  } else {
+    const int o = (lane - 32) * 8, L = min(Lm, 256);
+    if (o < L) bad = lds_window8(x, e1 - Lm + o, e1 - Lm + L) != lds_window8(T.bytes, n - Lm + o, n - Lm + L);
+  }
+  return __ballot(bad) == 0;
+}
+
+// The walk: literal run, hole, literal run, ... — every hole's bytes validated.
 __device__ inline bool wave_hole_match(const uint8_t* x, int e0, int e1, const HoleTpl& T, int* sa, int* sb,
                                        int* body) {
   const int n = T.len, nh = T.nh;
-  if (e1 - e0 == n && wave_lit_eq(x, e0, T.bytes, 0, n)) {  // the very same bytes (one compare)
-    if (T.kind == EV_CONTENT) {
-      *sa = e0 + T.hs[T.target];
-      *sb = e0 + T.he[T.target];
-      *body = T.tgt_bs;
-    }
-    return true;
-  }
   int p = e0, q = 0;
   for (int i = 0; i < nh; ++i) {
     const int L = (int)T.hs[i] - q;
@@ -489,7 +513,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     s.v[V_STATUS] = 0;
     s.v[V_TPLK] = -1;
     s.v[V_NEXTEV] = 0;
-    s.v[V_NFULL] = s.v[V_NTPL] = s.v[V_CFULL] = s.v[V_CTPL] = s.v[V_CLEX] = s.v[V_NHOLE] = 0;
+    s.v[V_NFULL] = s.v[V_NTPL] = s.v[V_CFULL] = s.v[V_CTPL] = s.v[V_CLEX] = s.v[V_NHOLE] = s.v[V_CHOLE] = 0;
     for (int q = 0; q < BS / 64; ++q) wtpl[q][0] = -1;
     if (fresh) {
       s.v[V_DEPTH0] = 0;
@@ -780,12 +804,17 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
           if (!(b - a == 6 && lit_at(s.A, a, b, QMX_LIT("[DONE]")))) {
             // a hole template of this backend (another stream's event of the same shape)?
             bool hm = false;
-            for (int q = 0; q < kHoleTpls && !hm; ++q) {
+            const uint64_t ch0 = probe ? __builtin_amdgcn_s_memtime() : 0;
+            // exact bytes first (one compare per same-length template), then the walks of
+            // templates whose first / last literal runs fit
+            for (int q = 0; q < 2 * kHoleTpls && !hm; ++q) {
               const int qi = (hhint + q) & (kHoleTpls - 1);
               const HoleTpl& T = U.htpl[qi];
               if (T.len == 0) continue;
               int ha = 0, hb = 0, hbody = 0;
-              if (!wave_hole_match(s.A, e0, e1, T, &ha, &hb, &hbody)) continue;
+              if (q < kHoleTpls ? !wave_hole_exact(s.A, e0, e1, T, &ha, &hb, &hbody)
+                                : !(wave_hole_quick(s.A, e0, e1, T) && wave_hole_match(s.A, e0, e1, T, &ha, &hb, &hbody)))
+                continue;
               hm = true;
               hhint = qi;
               kind = T.kind;
@@ -810,6 +839,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
                 published = true;
               }
             }
+            if (probe && lane == 0) atomicAdd(&s.v[V_CHOLE], (int)(__builtin_amdgcn_s_memtime() - ch0));
             if (!hm) {
               const uint64_t cl0 = probe ? __builtin_amdgcn_s_memtime() : 0;
               nt = wave_lex(s.A, a, b, TKP[w], TKT[w], 0, TOK_CAP);
@@ -1385,6 +1415,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     P.dbg[bi * kDbg + 17] = (unsigned long long)s.v[V_CTPL];   // S3 cycles: template checks
     P.dbg[bi * kDbg + 18] = (unsigned long long)s.v[V_CLEX];   // S3 cycles: wave_lex part of full
     P.dbg[bi * kDbg + 19] = (unsigned long long)s.v[V_NHOLE];  // S3: hole-template hits
+    P.dbg[bi * kDbg + 20] = (unsigned long long)s.v[V_CHOLE];  // S3 cycles: hole-template tries
   }
   if (tid == 0) {
     WorkResult r{(uint32_t)s.v[V_CONSUMED], (uint32_t)out_len, (uint32_t)s.v[V_STATUS], new_clen};
@@ -2571,6 +2602,7 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
         L.s3_cyc_tpl += L.h_dbg[kDbg * i + 17];
         L.s3_cyc_lex += L.h_dbg[kDbg * i + 18];
         L.s3_hole += L.h_dbg[kDbg * i + 19];
+        L.s3_cyc_hole += L.h_dbg[kDbg * i + 20];
       }
     }
   }
@@ -2739,6 +2771,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["s3_cycles_template"] += (double)L.s3_cyc_tpl;
     m["s3_cycles_lex"] += (double)L.s3_cyc_lex;
     m["s3_hole_hits"] += (double)L.s3_hole;
+    m["s3_cycles_hole"] += (double)L.s3_cyc_hole;
     m["host_prep_us"] += L.host_prep_us;
     m["gpu_wait_us"] += L.gpu_wait_us;
     m["first_result_us"] += L.first_result_us;

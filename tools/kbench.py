@@ -77,7 +77,7 @@ def main():
                 if st.get("s3_events"):
                     rec["s3_per_item"] = {k: round(st[k] / st["stage_items"], 2)
                                           for k in ("s3_events", "s3_full_parses", "s3_template_hits", "s3_hole_hits",
-                                                    "s3_cycles_full", "s3_cycles_template", "s3_cycles_lex")
+                                                    "s3_cycles_full", "s3_cycles_template", "s3_cycles_lex", "s3_cycles_hole")
                                           if k in st}
                 rec["MB_per_s"] = round(n * len(body) / len(pieces) / (st["kernel_ms"] / max(st["launches"], 1)) / 1e3, 1)
             results.append(rec)
