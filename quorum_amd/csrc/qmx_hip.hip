@@ -2049,6 +2049,15 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
   if (const char* va = getenv("QMX_VIEWS")) views_ = atoi(va) != 0;
   if (const char* pw = getenv("QMX_PERSISTENT_WG")) p_grid_ = std::min(std::max(8, atoi(pw)), 1024);
   if (const char* pi = getenv("QMX_PERSISTENT_IDLE_MS")) p_idle_ms_ = std::min(std::max(5, atoi(pi)), 1000);
+  {
+    // HIP streams share GPU_MAX_HW_QUEUES hardware queues round-robin, and a persistent grid
+    // holds its queue: a second lane's grid on the same queue would wait for the first to
+    // idle out (MI355X, 4 lanes / 4 queues: the first result of a tick came 100 us late).
+    // Persistent lanes need a queue each, with one left for everything else.
+    const char* hq = getenv("GPU_MAX_HW_QUEUES");
+    const int queues = hq ? std::max(1, atoi(hq)) : 4;
+    if (persistent_ && lanes > queues - 1) persistent_ = false;
+  }
   HIP_CHECK(hipMalloc(&d_state_, sizeof(DevSlot) * (size_t)max_slots_));
   HIP_CHECK(hipMemset(d_state_, 0, sizeof(DevSlot) * (size_t)max_slots_));
   HIP_CHECK(hipMalloc(&d_content_, (size_t)content_cap_ * (size_t)max_slots_));
