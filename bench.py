@@ -345,6 +345,9 @@ def breakdown(m0, m1, elapsed):
         "tick_item_us_avg": round(d.get("qmx_kernel_item_us", 0.0) / launches, 1) if launches else None,
         "tick_start_spread_us_avg": round(d.get("qmx_kernel_start_spread_us", 0.0) / launches, 1) if launches else None,
         "tick_items_host_us_avg": round(d.get("qmx_kernel_items_host_us", 0.0) / launches, 1) if launches else None,
+        # persistent grid, its own clock: doorbell seen -> relayed -> first item -> last item done
+        "grid_us_avg": {k: round(d.get(f"qmx_kernel_{k}_us", 0.0) / d["qmx_kernel_grid_ticks"], 1)
+                        for k in ("relay", "pickup", "grid_span")} if d.get("qmx_kernel_grid_ticks") else None,
         "tick_route_us_avg": round(1e6 * d.get("qmx_tick_route_seconds_total", 0.0) / ticks, 1) if ticks else None,
         "gpu_busy_frac": round(d.get("qmx_kernel_kernel_ms", 0.0) / 1000 / elapsed, 4) if elapsed else None,
         # finalize (K3 strip + K4 join + K5 encode) rides the tick launches: requests folded into

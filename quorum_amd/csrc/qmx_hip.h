@@ -153,7 +153,8 @@ struct TickLane {
   double kernel_ms = 0.0, host_prep_us = 0, gpu_wait_us = 0, process_us = 0;  // host-side tick breakdown
   double first_result_us = 0;  // tick posted -> first result record seen by the host
   double item_us = 0, start_spread_us = 0;
-  double items_host_us = 0;  // host: result records -> slot state + SSE strings (process_item)  // per tick: mean item run, last item start - first
+  double items_host_us = 0;
+  double relay_us = 0, pickup_us = 0, grid_span_us = 0, grid_ticks = 0;  // persistent: doorbell seen -> ...  // host: result records -> slot state + SSE strings (process_item)  // per tick: mean item run, last item start - first
   double stage_us[16] = {0};
   double clk_cycles = 0, clk_us = 0;
   // finalize arenas (fused into this lane's tick launches)

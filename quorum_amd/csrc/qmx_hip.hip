@@ -1814,6 +1814,7 @@ struct PDoor {  // host-mapped: written by the host, polled by workgroup 0
   alignas(64) uint32_t relayed;  // last tick relayed
   uint32_t exits;                // last grid exit: reason << 16 | launch generation (1 idle, 2 stop)
   uint32_t idle_limit_hit_us;    // the idle time that triggered the last idle exit, us
+  uint64_t t_seen, t_relayed;    // s_memrealtime: the last tick's doorbell seen / relayed (timing)
 };
 struct PCtl {  // device memory: written by workgroup 0, polled by the others
   TickDesc d;
@@ -1846,6 +1847,8 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* door, PCtl* ctl
           const uint32_t v = __hip_atomic_load(&door->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           if ((int32_t)(v - last) > 0) {  // newer only: a control word left by an earlier launch is older
             c = v;
+            __hip_atomic_store(&door->t_seen, (uint64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
             break;
           }
         } else {
@@ -1903,6 +1906,8 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* door, PCtl* ctl
       __threadfence();
       __syncthreads();
       if (tid == 0) {
+        __hip_atomic_store(&door->t_relayed, (uint64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&door->relayed, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (D.stop) __hip_atomic_store(&door->exits, (2u << 16) | (gen & 0xffffu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&ctl->seq, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -2569,6 +2574,17 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
         L.item_us += item_ticks * 1e-2 / n;
         L.start_spread_us += (double)(t0max - a) * 1e-2;
       }
+      if (persist && n > 0) {  // the grid's side of the tick (its own clock): doorbell seen ->
+        // relayed -> first item started -> last item done
+        const uint64_t ts = __atomic_load_n(&L.h_door->t_seen, __ATOMIC_ACQUIRE);
+        const uint64_t tr = __atomic_load_n(&L.h_door->t_relayed, __ATOMIC_ACQUIRE);
+        if (ts && tr >= ts && a >= tr && b >= a) {
+          L.relay_us += (double)(tr - ts) * 1e-2;
+          L.pickup_us += (double)(a - tr) * 1e-2;
+          L.grid_span_us += (double)(b - ts) * 1e-2;
+          ++L.grid_ticks;
+        }
+      }
       for (int i = 0; i < m; ++i) {
         a = std::min(a, L.h_finres[i].t0);
         b = std::max(b, L.h_finres[i].t1);
@@ -2786,6 +2802,10 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["first_result_us"] += L.first_result_us;
     m["item_us"] += L.item_us;
     m["items_host_us"] += L.items_host_us;
+    m["relay_us"] += L.relay_us;
+    m["pickup_us"] += L.pickup_us;
+    m["grid_span_us"] += L.grid_span_us;
+    m["grid_ticks"] += L.grid_ticks;
     m["start_spread_us"] += L.start_spread_us;
     m["process_us"] += L.process_us;
     m["poll_fallbacks"] += (double)L.poll_fallbacks;
