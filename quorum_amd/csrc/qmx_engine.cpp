@@ -1,6 +1,8 @@
 // qmx_engine.cpp — host engine core + the sequential (oracle-equivalent) CPU algorithms.
 #include "qmx_engine.h"
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -298,7 +300,9 @@ void finalize_texts(const TagSet& ts, const std::vector<std::string>& texts, con
 // --------------------------------------------------------------------------------
 // HostEngine
 // --------------------------------------------------------------------------------
-HostEngine::HostEngine(const std::vector<std::string>& tags) : ts_(make_tagset(tags)) {}
+HostEngine::HostEngine(const std::vector<std::string>& tags) : ts_(make_tagset(tags)) {
+  if (const char* pe = getenv("QMX_PIPELINE")) pipeline_ = atoi(pe) != 0;
+}
 
 int HostEngine::open(int index, bool filter, bool emit, uint32_t* gen) {
   std::lock_guard<std::mutex> g(mu_);
@@ -440,60 +444,64 @@ bool HostEngine::has_work() {
   return false;
 }
 
+bool HostEngine::job_take(Job& j, bool allow_fin) {
+  j.work.clear();
+  j.fin.clear();
+  thread_local std::vector<int> keep;
+  keep.clear();
+  std::lock_guard<std::mutex> g(mu_);
+  for (int s : pending_free_) {
+    if (meta_[s].busy) {  // still in flight on another lane: free it once settled
+      keep.push_back(s);
+      continue;
+    }
+    on_free(s);
+    free_.push_back(s);
+  }
+  pending_free_.swap(keep);
+  keep.clear();
+  j.work.reserve(dirty_.size());
+  for (int s : dirty_) {
+    Meta& m = meta_[s];
+    if (m.busy && m.live) {  // this stream's previous tick is not settled: next time
+      keep.push_back(s);
+      continue;
+    }
+    m.dirty = false;
+    if (!m.live) continue;
+    Work w{s, std::string(), m.eof, m.fresh};
+    w.data.swap(m.incoming);
+    m.fresh = false;
+    m.busy = true;
+    j.work.push_back(std::move(w));
+  }
+  dirty_.swap(keep);
+  if (allow_fin) j.fin.swap(fin_);
+  if (!j.work.empty() || !j.fin.empty()) ++ticks_;
+  return !j.work.empty() || !j.fin.empty();
+}
+
+void HostEngine::job_finish(Job& j, std::vector<SlotResult>& results, std::vector<int>& taken) {
+  size_t out = 0;
+  for (auto& r : results) out += r.size();
+  for (auto& w : j.work) taken.push_back(w.slot);
+  std::lock_guard<std::mutex> g(mu_);
+  bytes_out_ += out;
+  // a taken slot stays busy until settled, so it cannot be re-opened meanwhile: its
+  // generation is the one the results belong to
+  for (auto& r : results) r.gen = meta_[r.slot].gen;
+}
+
 bool HostEngine::tick(int64_t created, std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres, int lane,
                       std::vector<int>* taken) {
   // per-thread scratch reused from tick to tick (a tick thread drives one lane)
-  thread_local std::vector<Work> work;
-  thread_local std::vector<FinalizeReq> fin;
-  thread_local std::vector<int> keep, slots;
-  work.clear();
-  fin.clear();
-  keep.clear();
+  thread_local Job j;
+  thread_local std::vector<int> slots;
   slots.clear();
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    for (int s : pending_free_) {
-      if (meta_[s].busy) {  // still in flight on another lane: free it once settled
-        keep.push_back(s);
-        continue;
-      }
-      on_free(s);
-      free_.push_back(s);
-    }
-    pending_free_.swap(keep);
-    keep.clear();
-    work.reserve(dirty_.size());
-    for (int s : dirty_) {
-      Meta& m = meta_[s];
-      if (m.busy && m.live) {  // this stream's previous tick is not settled: next time
-        keep.push_back(s);
-        continue;
-      }
-      m.dirty = false;
-      if (!m.live) continue;
-      Work w{s, std::string(), m.eof, m.fresh};
-      w.data.swap(m.incoming);
-      m.fresh = false;
-      m.busy = true;
-      work.push_back(std::move(w));
-    }
-    dirty_.swap(keep);
-    fin.swap(fin_);
-    if (!work.empty() || !fin.empty()) ++ticks_;
-  }
-  if (work.empty() && fin.empty()) return false;
-  run_tick(work, fin, created, results, fres, lane);
-  size_t out = 0;
-  for (auto& r : results) out += r.size();
+  if (!job_take(j, true)) return false;
+  run_tick(j.work, j.fin, created, results, fres, lane);
   std::vector<int>& tk = taken ? *taken : slots;
-  for (auto& w : work) tk.push_back(w.slot);
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    bytes_out_ += out;
-    // a taken slot stays busy until settled, so it cannot be re-opened meanwhile: its
-    // generation is the one the results belong to
-    for (auto& r : results) r.gen = meta_[r.slot].gen;
-  }
+  job_finish(j, results, tk);
   if (!taken) settle(slots);
   return true;
 }

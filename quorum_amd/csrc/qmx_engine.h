@@ -183,6 +183,34 @@ class HostEngine {
   bool tick(int64_t created, std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres, int lane = 0,
             std::vector<int>* taken = nullptr);
   void settle(const std::vector<int>& taken);
+
+  struct Work {
+    int slot;
+    std::string data;
+    bool eof;
+    bool fresh;
+  };
+  // Pipelined ticks (GpuHub lanes, engines with pipelined()): a job takes the lane's work
+  // (job_take: the dirty streams no other tick holds, optionally the queued finalize
+  // requests), is prepared while the lane's previous job still runs on the device, posted
+  // the moment that one completes, and completed (results) while the next one runs.
+  // job_finish stamps the results' generations and lists the taken slots for settle().
+  struct Job {
+    std::vector<Work> work;
+    std::vector<FinalizeReq> fin;
+    int64_t created = 0;
+    int lane = 0;
+    bool live = false;
+    std::shared_ptr<void> impl;  // the engine's state between the phases
+  };
+  virtual bool pipelined() const { return false; }
+  bool pipeline_ = true;  // QMX_PIPELINE=0: lanes tick one job at a time (A/B)
+  bool job_take(Job& j, bool allow_fin);
+  virtual void job_prepare(Job&) {}
+  virtual void job_post(Job&) {}
+  virtual void job_wait_near(Job&) {}
+  virtual void job_complete(Job&, std::vector<SlotResult>&, std::vector<FinalizeRes>&) {}
+  void job_finish(Job& j, std::vector<SlotResult>& results, std::vector<int>& taken);
   virtual std::string text(int slot);
   virtual std::unordered_map<std::string, double> stats();
   // Spread placement (qmx_exchange.h): a stream whose final text another rank produced.
@@ -199,12 +227,6 @@ class HostEngine {
   const TagSet& tagset() const { return ts_; }
 
  protected:
-  struct Work {
-    int slot;
-    std::string data;
-    bool eof;
-    bool fresh;
-  };
   // engine-specific batch processing: the tick's stream work AND its finalize requests
   // (HipEngine: one fused launch for both; CpuEngine: sequentially)
   virtual void run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin, int64_t created,
@@ -243,6 +265,12 @@ class HostEngine {
 class CpuEngine : public HostEngine {
  public:
   explicit CpuEngine(const std::vector<std::string>& tags) : HostEngine(tags) {}
+  // pipelined lanes on the CPU: the whole tick runs in job_complete (exercises GpuHub's
+  // pipelined loop without a GPU)
+  bool pipelined() const override { return pipeline_; }
+  void job_complete(Job& j, std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres) override {
+    run_tick(j.work, j.fin, j.created, results, fres, j.lane);
+  }
 
  protected:
   void run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin, int64_t created,

@@ -126,8 +126,19 @@ struct TickLane {
   KParams* h_params = nullptr;  // pinned staging for its upload
   int64_t params_created = -1;
   bool params_dirty = true;
-  uint8_t* h_in = nullptr;
-  size_t in_cap = 0;
+  // two buffer sets (tiles, work items, result records, stage stamps), alternated per tick:
+  // the next tick is prepared while this one runs (GpuHub's pipelined lanes)
+  struct Buf {
+    uint8_t* h_in = nullptr;
+    size_t in_cap = 0;
+    WorkItem* h_items = nullptr;
+    WorkResult* h_res = nullptr;
+    size_t items_cap = 0;
+    unsigned long long* h_dbg = nullptr;
+    size_t dbg_cap = 0;
+  };
+  Buf bufs[2];
+  int next_buf = 0;
   // output arenas (pinned, mapped): results view their SSE bytes in place (SlotResult::view),
   // so a tick writes into an arena no earlier result still views — a ring that grows while
   // every arena is held (OutArena objects are never freed: a late ViewRef may still count)
@@ -141,11 +152,6 @@ struct TickLane {
   OutArena* out = nullptr;  // this tick's
   uint8_t* h_out = nullptr;  // == out->p
   size_t out_cap = 0;
-  WorkItem* h_items = nullptr;
-  WorkResult* h_res = nullptr;
-  size_t items_cap = 0;
-  unsigned long long* h_dbg = nullptr;
-  size_t dbg_cap = 0;
   // counters (summed over lanes by kernel_stats)
   uint64_t launches = 0, items = 0, h2d_bytes = 0, d2h_bytes = 0;
   uint64_t s3_full = 0, s3_tpl = 0, s3_events = 0, stage_n = 0;  // QMX_STAGE_TIMING: S3 path counters
@@ -208,7 +214,21 @@ class HipEngine : public HostEngine {
                 std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres, int lane) override;
   void on_free(int slot) override;
 
+ public:
+  // pipelined lanes (polled completion): the next tick is prepared while this one runs
+  bool pipelined() const override { return poll_ && pipeline_; }
+  void job_prepare(Job& j) override;
+  void job_post(Job& j) override;
+  void job_wait_near(Job& j) override;
+  void job_complete(Job& j, std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres) override;
+
  private:
+  struct HipJob;
+  HipJob& hjob(Job& j);
+  void prepare(HipJob& J);
+  void post(HipJob& J);
+  void wait_near(HipJob& J);
+  void complete(HipJob& J, std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres);
   void escalate(int slot, bool fresh);
   void finalize_host(const FinalizeReq& r, std::vector<FinalizeRes>& out);
   // finalize items of this tick → the lane's arenas; returns the GPU ones (others: host path)
@@ -217,9 +237,10 @@ class HipEngine : public HostEngine {
   void collect_finalize(TickLane& L, const std::vector<const FinalizeReq*>& gpu, std::vector<FinalizeRes>& out);
   void wait_stream(TickLane& L);
   // polls the tick's result records; on_item(i) as stream result i is seen published (in order)
-  void wait_results(TickLane& L, int n, int m, uint32_t seq, const std::function<void(int)>& on_item);
+  void wait_results(TickLane& L, int n, int m, uint32_t seq, const WorkResult* res,
+                    const std::function<void(int)>& on_item);
   void collect_timing(TickLane& L);
-  void ensure_in(TickLane& L, size_t bytes);
+  void ensure_in(TickLane::Buf& B, size_t bytes);
   void ensure_out(TickLane& L, size_t bytes);
   void build_params(TickLane& L, int64_t created);
   std::string device_content(int slot, uint32_t len);

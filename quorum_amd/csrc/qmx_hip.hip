@@ -1980,7 +1980,8 @@ void HipEngine::wait_stream(TickLane& L) {
 // most of the expected kernel time (EMA), then poll every poll_us_ with a 1 us timer slack.
 // A launch that has not published after 4x the EMA + 2 ms synchronises its stream (surfaces a
 // fault; correct even if host-mapped visibility misbehaved: counted in poll_fallbacks).
-void HipEngine::wait_results(TickLane& L, int n, int m, uint32_t seq, const std::function<void(int)>& on_item) {
+void HipEngine::wait_results(TickLane& L, int n, int m, uint32_t seq, const WorkResult* res,
+                             const std::function<void(int)>& on_item) {
   using HC = std::chrono::steady_clock;
   static thread_local bool slack = (prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0), true);
   (void)slack;
@@ -1991,7 +1992,7 @@ void HipEngine::wait_results(TickLane& L, int n, int m, uint32_t seq, const std:
     nanosleep(&ts, nullptr);
   };
   auto done = [&](int& i) {
-    while (i < n && __atomic_load_n(&L.h_res[i].seq, __ATOMIC_ACQUIRE) == seq) on_item(i++);
+    while (i < n && __atomic_load_n(&res[i].seq, __ATOMIC_ACQUIRE) == seq) on_item(i++);
     while (i >= n && i < n + m && __atomic_load_n(&L.h_finres[i - n].seq, __ATOMIC_ACQUIRE) == seq) ++i;
     return i == n + m;
   };
@@ -2112,12 +2113,14 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
     std::memset((void*)L->h_door, 0, sizeof(PDoor));
     HIP_CHECK(hipMalloc((void**)&L->d_ctl, sizeof(PCtl)));
     HIP_CHECK(hipMemset(L->d_ctl, 0, sizeof(PCtl)));
-    ensure_in(*L, 8u << 20);
+    for (TickLane::Buf& B : L->bufs) {
+      ensure_in(B, 4u << 20);
+      B.items_cap = 1024;
+      HIP_CHECK(hipHostMalloc((void**)&B.h_items, sizeof(WorkItem) * B.items_cap, hipHostMallocMapped));
+      HIP_CHECK(hipHostMalloc((void**)&B.h_res, sizeof(WorkResult) * B.items_cap, hipHostMallocMapped));
+    }
     for (int a = 0; a < 3; ++a) L->outs.push_back(new TickLane::OutArena());
     ensure_out(*L, 4u << 20);
-    L->items_cap = 4096;
-    HIP_CHECK(hipHostMalloc((void**)&L->h_items, sizeof(WorkItem) * L->items_cap, hipHostMallocMapped));
-    HIP_CHECK(hipHostMalloc((void**)&L->h_res, sizeof(WorkResult) * L->items_cap, hipHostMallocMapped));
     lanes_.push_back(std::move(L));
   }
   host_mode_.assign(max_slots_, 0);
@@ -2133,12 +2136,14 @@ HipEngine::~HipEngine() {
     if (L->stream) hipStreamSynchronize(L->stream);
     if (L->h_door) hipHostFree(L->h_door);
     if (L->d_ctl) hipFree(L->d_ctl);
-    if (L->h_in) hipHostFree(L->h_in);
+    for (TickLane::Buf& B : L->bufs) {
+      if (B.h_in) hipHostFree(B.h_in);
+      if (B.h_items) hipHostFree(B.h_items);
+      if (B.h_res) hipHostFree(B.h_res);
+      if (B.h_dbg) hipHostFree(B.h_dbg);
+    }
     for (TickLane::OutArena* a : L->outs)
       if (a->p) hipHostFree(a->p);  // the OutArena objects stay (see TickLane::outs)
-    if (L->h_items) hipHostFree(L->h_items);
-    if (L->h_res) hipHostFree(L->h_res);
-    if (L->h_dbg) hipHostFree(L->h_dbg);
     if (L->d_params) hipFree(L->d_params);
     if (L->d_btpl) hipFree(L->d_btpl);
     if (L->h_params) hipHostFree(L->h_params);
@@ -2214,11 +2219,11 @@ void HipEngine::stop_persistent(TickLane& L) {
   HIP_CHECK(hipStreamSynchronize(L.stream));
 }
 
-void HipEngine::ensure_in(TickLane& L, size_t bytes) {
-  if (bytes <= L.in_cap) return;
-  if (L.h_in) retire_host(L.h_in);
-  L.in_cap = std::max(bytes, L.in_cap * 2);
-  HIP_CHECK(hipHostMalloc((void**)&L.h_in, L.in_cap + 64, hipHostMallocMapped));
+void HipEngine::ensure_in(TickLane::Buf& B, size_t bytes) {
+  if (bytes <= B.in_cap) return;
+  if (B.h_in) retire_host(B.h_in);
+  B.in_cap = std::max(bytes, B.in_cap * 2);
+  HIP_CHECK(hipHostMalloc((void**)&B.h_in, B.in_cap + 64, hipHostMallocMapped));
 }
 void HipEngine::ensure_out(TickLane& L, size_t bytes) {
   const auto t0 = std::chrono::steady_clock::now();
@@ -2330,12 +2335,11 @@ std::string HipEngine::text(int slot) {
   return device_content(slot, content_len_[slot]);
 }
 
-void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin, int64_t created,
-                         std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres, int lane) {
-  TickLane& L = *lanes_[(size_t)lane % lanes_.size()];
-  std::lock_guard<std::mutex> lg(L.mu);  // a lane is driven by one thread; kernel_stats() reads under it
-  using HC = std::chrono::steady_clock;
-  const auto tp0 = HC::now();
+// One tick of a lane, in phases (HipJob): prepare (arenas filled; may run while the lane's
+// previous tick is still on the device), post (doorbell / launch), complete (results).  A
+// lane alternates two buffer sets (tiles, items, result records), so the next tick is
+// prepared while this one runs and posted the moment it completes (GpuHub, pipelined).
+struct HipEngine::HipJob {
   struct Pending {
     int slot;
     size_t carry_len;  // carry bytes that preceded w.data in the tile
@@ -2343,14 +2347,40 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
     bool eof_sent;
     Work* w;
   };
-  // per-thread scratch reused from tick to tick (a lane is driven by one thread at a time)
-  thread_local std::vector<Pending> pend;
-  thread_local std::vector<int> requeue;
-  thread_local std::vector<Work*> order;
-  thread_local std::vector<Work*> b[8];
-  pend.clear();
-  requeue.clear();
-  order.clear();
+  std::vector<Work>* work = nullptr;
+  std::vector<FinalizeReq>* fin = nullptr;
+  int64_t created = 0;
+  int lane = 0, n = 0, m = 0;
+  uint32_t seq = 0;
+  bool persist = false, new_params = false, posted = false;
+  std::vector<Pending> pend;
+  std::vector<int> requeue;
+  std::vector<Work*> order;
+  std::vector<Work*> b[8];
+  std::vector<const FinalizeReq*> fin_gpu, fin_host;
+  std::vector<SlotResult> host_results;  // escalated streams, processed on the host in prepare
+  TickLane::Buf* B = nullptr;
+  TickLane::OutArena* arena = nullptr;
+  size_t in_off = 0;
+  std::chrono::steady_clock::time_point tp0, tp1;
+};
+
+void HipEngine::prepare(HipJob& J) {
+  TickLane& L = *lanes_[(size_t)J.lane % lanes_.size()];
+  std::lock_guard<std::mutex> lg(L.mu);  // kernel_stats() reads the counters under it
+  using HC = std::chrono::steady_clock;
+  J.tp0 = HC::now();
+  J.pend.clear();
+  J.requeue.clear();
+  J.order.clear();
+  J.host_results.clear();
+  J.fin_gpu.clear();
+  J.fin_host.clear();
+  J.posted = false;
+  std::vector<Work>& work = *J.work;
+  TickLane::Buf& B = L.bufs[L.next_buf];
+  L.next_buf ^= 1;
+  J.B = &B;
   size_t in_need = 0, out_need = 0;
   for (auto& w : work) {
     size_t tot = core_[w.slot].carry.size() + w.data.size();
@@ -2358,14 +2388,15 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
     in_need += (sub + 15) & ~(size_t)15;
     out_need += ((12 * sub + 1024) + 15) & ~(size_t)15;
   }
-  ensure_in(L, in_need + 64);
+  ensure_in(B, in_need + 64);
   ensure_out(L, out_need + 64);
-  if (work.size() > L.items_cap) {
-    retire_host(L.h_items);
-    retire_host(L.h_res);
-    L.items_cap = work.size() * 2;
-    HIP_CHECK(hipHostMalloc((void**)&L.h_items, sizeof(WorkItem) * L.items_cap, hipHostMallocMapped));
-    HIP_CHECK(hipHostMalloc((void**)&L.h_res, sizeof(WorkResult) * L.items_cap, hipHostMallocMapped));
+  J.arena = L.out;
+  if (work.size() > B.items_cap) {
+    retire_host(B.h_items);
+    retire_host(B.h_res);
+    B.items_cap = work.size() * 2;
+    HIP_CHECK(hipHostMalloc((void**)&B.h_items, sizeof(WorkItem) * B.items_cap, hipHostMallocMapped));
+    HIP_CHECK(hipHostMalloc((void**)&B.h_res, sizeof(WorkResult) * B.items_cap, hipHostMallocMapped));
   }
   size_t in_off = 0, out_off = 0;
   int n = 0;
@@ -2373,33 +2404,34 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
   // stream with slot % 8 == i % 8 where possible — a stream's DevSlot state, template and
   // content-arena tail stay in one XCD's L2 from tick to tick.  Host-path streams first.
   {
-    for (auto& q : b) q.clear();
+    for (auto& q : J.b) q.clear();
     for (auto& w : work) {
-      if (w.slot >= max_slots_ || host_mode_[w.slot]) order.push_back(&w);
-      else b[w.slot & 7].push_back(&w);
+      if (w.slot >= max_slots_ || host_mode_[w.slot]) J.order.push_back(&w);
+      else J.b[w.slot & 7].push_back(&w);
     }
     size_t left = 0;
-    for (auto& q : b) left += q.size();
+    for (auto& q : J.b) left += q.size();
     for (int i = 0; left; ++i) {
       int bi = i & 7;
-      if (b[bi].empty())
+      if (J.b[bi].empty())
         for (int j = 0; j < 8; ++j)
-          if (b[j].size() > b[bi].size()) bi = j;  // affinity bucket empty: the fullest one
-      order.push_back(b[bi].back());
-      b[bi].pop_back();
+          if (J.b[j].size() > J.b[bi].size()) bi = j;  // affinity bucket empty: the fullest one
+      J.order.push_back(J.b[bi].back());
+      J.b[bi].pop_back();
       --left;
     }
   }
-  for (Work* wp : order) {
+  for (Work* wp : J.order) {
     Work& w = *wp;
     int slot = w.slot;
     SlotCore& c = core_[slot];
     if (slot >= max_slots_ || host_mode_[slot]) {
       bool was_closed = c.done || c.aborted;
       std::string o;
-      process_slot(ts_, c, (const uint8_t*)w.data.data(), w.data.size(), w.eof, created, o);
+      process_slot(ts_, c, (const uint8_t*)w.data.data(), w.data.size(), w.eof, J.created, o);
       int flags = (c.done ? RF_DONE : 0) | (c.aborted ? RF_ABORTED : 0) | RF_ESCALATED;
-      if (!o.empty() || ((flags & (RF_DONE | RF_ABORTED)) && !was_closed)) results.push_back({slot, std::move(o), flags});
+      if (!o.empty() || ((flags & (RF_DONE | RF_ABORTED)) && !was_closed))
+        J.host_results.push_back({slot, std::move(o), flags});
       continue;
     }
     if (c.done || c.aborted) continue;
@@ -2408,9 +2440,9 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
     bool eof_sent = w.eof && sub == tot;
     // copy carry + data prefix into the arena
     size_t a = std::min(cl, sub);
-    std::memcpy(L.h_in + in_off, c.carry.data(), a);
-    if (sub > a) std::memcpy(L.h_in + in_off + a, w.data.data(), sub - a);
-    WorkItem& it = L.h_items[n];
+    std::memcpy(B.h_in + in_off, c.carry.data(), a);
+    if (sub > a) std::memcpy(B.h_in + in_off + a, w.data.data(), sub - a);
+    WorkItem& it = B.h_items[n];
     it.slot = (uint32_t)slot;
     it.in_off = (uint32_t)in_off;
     it.in_len = (uint32_t)sub;
@@ -2422,16 +2454,116 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
     it.content_len = content_len_[slot];
     in_off += (sub + 15) & ~(size_t)15;
     out_off += ((size_t)it.out_cap + 15) & ~(size_t)15;
-    pend.push_back({slot, cl, sub, eof_sent, &w});
+    J.pend.push_back({slot, cl, sub, eof_sent, &w});
     ++n;
   }
+  J.n = n;
+  J.in_off = in_off;
+  // finalize requests ride the same launch: workgroups [n, n + m)
+  J.fin_gpu = prep_finalize(L, *J.fin, J.fin_host);
+  J.m = (int)J.fin_gpu.size();
+  if (n + J.m > 0) {
+    if (J.created != L.params_created) {  // envelopes carry the second: rebuilt + uploaded once a second
+      build_params(L, J.created);
+      L.params_created = J.created;
+      L.params_dirty = true;
+    }
+    unsigned long long* const dbg0 = L.params.dbg;
+    L.params.dbg = nullptr;
+    if (getenv("QMX_STAGE_TIMING")) {
+      if (B.dbg_cap < (size_t)n) {
+        if (B.h_dbg) retire_host(B.h_dbg);
+        B.dbg_cap = std::max((size_t)n, B.items_cap);
+        HIP_CHECK(hipHostMalloc((void**)&B.h_dbg, sizeof(unsigned long long) * kDbg * B.dbg_cap, hipHostMallocMapped));
+      }
+      std::memset(B.h_dbg, 0, sizeof(unsigned long long) * kDbg * n);
+      L.params.dbg = B.h_dbg;
+    }
+    if (L.params.dbg != dbg0) L.params_dirty = true;
+  }
+  J.tp1 = HC::now();
+  L.host_prep_us += std::chrono::duration<double, std::micro>(J.tp1 - J.tp0).count();
+}
+
+void HipEngine::post(HipJob& J) {
+  if (J.n + J.m == 0) return;
+  TickLane& L = *lanes_[(size_t)J.lane % lanes_.size()];
+  std::lock_guard<std::mutex> lg(L.mu);
+  TickLane::Buf& B = *J.B;
+  // persistent grid (needs polled completion) or a one-shot launch for this tick
+  J.persist = persistent_ && poll_;
+  if (!J.persist && L.p_running) stop_persistent(L);  // mode switched: the grid must not hold the stream
+  J.new_params = L.params_dirty;
+  if (L.params_dirty) {  // the pinned copy is not touched again until this tick completed
+    std::memcpy(L.h_params, &L.params, sizeof(KParams));
+    // one-shot launches: a stream-ordered upload; persistent: the grid copies it itself
+    if (!J.persist) HIP_CHECK(hipMemcpyAsync(L.d_params, L.h_params, sizeof(KParams), hipMemcpyHostToDevice, L.stream));
+    L.params_dirty = false;
+  }
+  J.tp1 = std::chrono::steady_clock::now();
+  roctxRangePushA("qmx_tick");  // rocprofv3 --marker-trace: one range per tick launch + wait
+  L.h2d_bytes += J.in_off;
+  if (J.persist) ensure_persistent(L);  // before the tick's sequence number: a relaunch starts from L.seq
+  J.seq = next_seq(L);
+  const uint32_t par = L.launches & 1;  // backend template table: read last tick's half, write the other
+  if (!poll_) HIP_CHECK(hipEventRecord(L.ev0, L.stream));
+  FinArgs fa{L.h_fin, L.h_fint, L.h_fin_in, L.d_join, L.d_fout, L.h_fout, L.h_finres, L.h_tl, (int2*)L.d_segs};
+  if (J.persist) {
+    TickDesc& d = L.h_door->d;  // host-mapped: plain stores, then the release store of `posted`
+    d.items = B.h_items;
+    d.in = B.h_in;
+    d.out = J.arena->p;
+    d.res = B.h_res;
+    d.params = L.d_params;
+    d.params_src = J.new_params ? L.h_params : nullptr;
+    d.btpl_rd = L.d_btpl + (size_t)(par ^ 1) * kBackendTpl;
+    d.btpl_wr = L.d_btpl + (size_t)par * kBackendTpl;
+    d.fa = fa;
+    d.seq = J.seq;
+    d.n_tick = (uint32_t)J.n;
+    d.n_fin = (uint32_t)J.m;
+    d.stop = 0;
+    __atomic_store_n(&L.h_door->posted, J.seq, __ATOMIC_RELEASE);
+    L.p_last_post = steady_s();
+    ++L.p_ticks;
+  } else {
+    hipLaunchKernelGGL(qmx_tick_kernel, dim3(J.n + J.m), dim3(BS), 0, L.stream, B.h_items, B.h_in, J.arena->p,
+                       B.h_res, d_state_, d_content_, L.d_params, J.seq, (uint32_t)J.n, fa,
+                       L.d_btpl + (size_t)(par ^ 1) * kBackendTpl, L.d_btpl + (size_t)par * kBackendTpl);
+    HIP_CHECK(hipGetLastError());
+  }
+  J.posted = true;
+}
+
+// Until the posted tick is about to complete (the expected time less the next tick's
+// preparation): the lane then prepares the next tick, so it can post it at once.
+void HipEngine::wait_near(HipJob& J) {
+  if (!J.posted) return;
+  TickLane& L = *lanes_[(size_t)J.lane % lanes_.size()];
+  const double el = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - J.tp1).count();
+  const double prep = L.launches ? L.host_prep_us / (double)L.launches : 5.0;
+  const double target = L.ema_us - prep - 4.0;
+  if (target - el >= 2.0) {
+    timespec ts{0, (long)((target - el) * 1000)};
+    nanosleep(&ts, nullptr);
+  }
+}
+
+void HipEngine::complete(HipJob& J, std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres) {
+  TickLane& L = *lanes_[(size_t)J.lane % lanes_.size()];
+  std::lock_guard<std::mutex> lg(L.mu);
+  using HC = std::chrono::steady_clock;
+  for (auto& r : J.host_results) results.push_back(std::move(r));
+  J.host_results.clear();
+  const int n = J.n, m = J.m;
+  TickLane::Buf& B = *J.B;
   // one stream's result → slot state + SSE; run as each result record is published (the
   // host's share of a tick overlaps the kernel's stragglers), the rest after the wait
   int n_done = 0;
   auto process_item = [&](int i) {
-    Pending& p = pend[i];
+    HipJob::Pending& p = J.pend[i];
     SlotCore& c = core_[p.slot];
-    const WorkResult r = L.h_res[i];
+    const WorkResult r = B.h_res[i];
     Work& w = *p.w;
     // the unconsumed remainder (carry + data)[consumed:] becomes the carry, in place
     auto keep_remainder = [&](size_t consumed) {
@@ -2452,7 +2584,7 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
       all.swap(c.carry);
       bool was_closed = c.done || c.aborted;
       std::string o;
-      process_slot(ts_, c, (const uint8_t*)all.data(), all.size(), w.eof, created, o);
+      process_slot(ts_, c, (const uint8_t*)all.data(), all.size(), w.eof, J.created, o);
       int flags = (c.done ? RF_DONE : 0) | (c.aborted ? RF_ABORTED : 0) | RF_ESCALATED;
       if (!o.empty() || ((flags & (RF_DONE | RF_ABORTED)) && !was_closed)) results.push_back({p.slot, std::move(o), flags});
       return;
@@ -2471,110 +2603,47 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
         c.carry.clear();
         flags |= RF_DONE;
       } else if ((r.status & WS_MORE) || p.submitted < p.carry_len + w.data.size()) {
-        requeue.push_back(p.slot);  // unprocessed bytes (or a pending EOF) remain
+        J.requeue.push_back(p.slot);  // unprocessed bytes (or a pending EOF) remain
       }
     }
     L.d2h_bytes += r.out_len;
+    const char* bytes = (const char*)J.arena->p + B.h_items[i].out_off;
     if (r.out_len && !views_) {
-      results.push_back({p.slot, std::string((const char*)L.h_out + L.h_items[i].out_off, r.out_len), flags});
+      results.push_back({p.slot, std::string(bytes, r.out_len), flags});
     } else if (r.out_len) {  // a view into this tick's output arena: the io loop copies the bytes once
       SlotResult x{p.slot, std::string(), flags};
-      x.view = (const char*)L.h_out + L.h_items[i].out_off;
+      x.view = bytes;
       x.view_len = r.out_len;
-      x.hold = ViewRef(&L.out->refs);
+      x.hold = ViewRef(&J.arena->refs);
       results.push_back(std::move(x));
     } else if (flags) {
       results.push_back({p.slot, std::string(), flags});
     }
   };
-  // finalize requests ride the same launch: workgroups [n, n + m)
-  std::vector<const FinalizeReq*> fin_host;
-  const std::vector<const FinalizeReq*> fin_gpu = prep_finalize(L, fin, fin_host);
-  const int m = (int)fin_gpu.size();
-  if (n + m > 0) {
-    if (created != L.params_created) {  // envelopes carry the second: rebuilt + uploaded once a second
-      build_params(L, created);
-      L.params_created = created;
-      L.params_dirty = true;
-    }
-    unsigned long long* const dbg0 = L.params.dbg;
-    L.params.dbg = nullptr;
-    if (getenv("QMX_STAGE_TIMING")) {
-      if (L.dbg_cap < (size_t)n) {
-        if (L.h_dbg) retire_host(L.h_dbg);
-        L.dbg_cap = std::max((size_t)n, L.items_cap);
-        HIP_CHECK(hipHostMalloc((void**)&L.h_dbg, sizeof(unsigned long long) * kDbg * L.dbg_cap, hipHostMallocMapped));
-      }
-      std::memset(L.h_dbg, 0, sizeof(unsigned long long) * kDbg * n);
-      L.params.dbg = L.h_dbg;
-    }
-    if (L.params.dbg != dbg0) L.params_dirty = true;
-    // persistent grid (needs polled completion) or a one-shot launch for this tick
-    const bool persist = persistent_ && poll_;
-    if (!persist && L.p_running) stop_persistent(L);  // mode switched: the grid must not hold the stream
-    const bool new_params = L.params_dirty;
-    if (L.params_dirty) {  // the pinned copy is not touched again until this tick completed
-      std::memcpy(L.h_params, &L.params, sizeof(KParams));
-      // one-shot launches: a stream-ordered upload; persistent: the grid copies it itself
-      if (!persist) HIP_CHECK(hipMemcpyAsync(L.d_params, L.h_params, sizeof(KParams), hipMemcpyHostToDevice, L.stream));
-      L.params_dirty = false;
-    }
-    const auto tp1 = HC::now();
-    L.host_prep_us += std::chrono::duration<double, std::micro>(tp1 - tp0).count();
-    roctxRangePushA("qmx_tick");  // rocprofv3 --marker-trace: one range per tick launch + wait
-    L.h2d_bytes += in_off;
-    if (persist) ensure_persistent(L);  // before the tick's sequence number: a relaunch starts from L.seq
-    const uint32_t seq = next_seq(L);
-    const uint32_t par = L.launches & 1;  // backend template table: read last tick's half, write the other
-    if (!poll_) HIP_CHECK(hipEventRecord(L.ev0, L.stream));
-    FinArgs fa{L.h_fin, L.h_fint, L.h_fin_in, L.d_join, L.d_fout, L.h_fout, L.h_finres, L.h_tl, (int2*)L.d_segs};
-    if (persist) {
-      TickDesc& d = L.h_door->d;  // host-mapped: plain stores, then the release store of `posted`
-      d.items = L.h_items;
-      d.in = L.h_in;
-      d.out = L.h_out;
-      d.res = L.h_res;
-      d.params = L.d_params;
-      d.params_src = new_params ? L.h_params : nullptr;
-      d.btpl_rd = L.d_btpl + (size_t)(par ^ 1) * kBackendTpl;
-      d.btpl_wr = L.d_btpl + (size_t)par * kBackendTpl;
-      d.fa = fa;
-      d.seq = seq;
-      d.n_tick = (uint32_t)n;
-      d.n_fin = (uint32_t)m;
-      d.stop = 0;
-      __atomic_store_n(&L.h_door->posted, seq, __ATOMIC_RELEASE);
-      L.p_last_post = steady_s();
-      ++L.p_ticks;
-    } else {
-      hipLaunchKernelGGL(qmx_tick_kernel, dim3(n + m), dim3(BS), 0, L.stream, L.h_items, L.h_in, L.h_out, L.h_res,
-                         d_state_, d_content_, L.d_params, seq, (uint32_t)n, fa,
-                         L.d_btpl + (size_t)(par ^ 1) * kBackendTpl, L.d_btpl + (size_t)par * kBackendTpl);
-      HIP_CHECK(hipGetLastError());
-    }
+  if (J.posted) {
     // sessions the GPU does not finalize (escalated streams) are finalized here meanwhile
-    for (const FinalizeReq* r : fin_host) finalize_host(*r, fres);
+    for (const FinalizeReq* r : J.fin_host) finalize_host(*r, fres);
     if (poll_) {
-      // one HIP call per tick: completion and kernel span both come from the result records
-      wait_results(L, n, m, seq, [&](int i) {
+      // one HIP call per tick, or none: completion and kernel span come from the result records
+      wait_results(L, n, m, J.seq, B.h_res, [&](int i) {
         const auto ti = HC::now();
-        if (n_done == 0) L.first_result_us += std::chrono::duration<double, std::micro>(ti - tp1).count();
+        if (n_done == 0) L.first_result_us += std::chrono::duration<double, std::micro>(ti - J.tp1).count();
         if (i == n_done) process_item(n_done++);
         L.items_host_us += std::chrono::duration<double, std::micro>(HC::now() - ti).count();
       });
       uint64_t a = ~0ull, b = 0, t0max = 0;
       double item_ticks = 0;
       for (int i = 0; i < n; ++i) {
-        a = std::min(a, L.h_res[i].t0);
-        b = std::max(b, L.h_res[i].t1);
-        t0max = std::max(t0max, L.h_res[i].t0);
-        item_ticks += (double)(L.h_res[i].t1 - L.h_res[i].t0);
+        a = std::min(a, B.h_res[i].t0);
+        b = std::max(b, B.h_res[i].t1);
+        t0max = std::max(t0max, B.h_res[i].t0);
+        item_ticks += (double)(B.h_res[i].t1 - B.h_res[i].t0);
       }
       if (n > 0) {  // do a tick's items run side by side? (one item's run vs the spread of starts)
         L.item_us += item_ticks * 1e-2 / n;
         L.start_spread_us += (double)(t0max - a) * 1e-2;
       }
-      if (persist && n > 0) {  // the grid's side of the tick (its own clock): doorbell seen ->
+      if (J.persist && n > 0) {  // the grid's side of the tick (its own clock): doorbell seen ->
         // relayed -> first item started -> last item done
         const uint64_t ts = __atomic_load_n(&L.h_door->t_seen, __ATOMIC_ACQUIRE);
         const uint64_t tr = __atomic_load_n(&L.h_door->t_relayed, __ATOMIC_ACQUIRE);
@@ -2597,16 +2666,16 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
       collect_timing(L);
     }
     roctxRangePop();
-    L.gpu_wait_us += std::chrono::duration<double, std::micro>(HC::now() - tp1).count();
+    L.gpu_wait_us += std::chrono::duration<double, std::micro>(HC::now() - J.tp1).count();
     ++L.launches;
     L.items += n;
     if (m > 0) {
       ++L.fin_launches;
       L.fin_items += m;
     }
-    if (L.params.dbg) {
+    if (L.params.dbg && L.params.dbg == B.h_dbg) {
       for (int i = 0; i < n; ++i) {
-        const unsigned long long* d = L.h_dbg + kDbg * i;
+        const unsigned long long* d = B.h_dbg + kDbg * i;
         if (d[12] > d[11] && d[10] > d[0]) {
           L.clk_cycles += (double)(d[12] - d[11]);
           L.clk_us += (double)(d[10] - d[0]) * 0.01;
@@ -2620,31 +2689,60 @@ void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
       }
       L.stage_n += n;
       for (int i = 0; i < n; ++i) {
-        L.s3_full += L.h_dbg[kDbg * i + 13];
-        L.s3_tpl += L.h_dbg[kDbg * i + 14];
-        L.s3_events += L.h_dbg[kDbg * i + 15];
-        L.s3_cyc_full += L.h_dbg[kDbg * i + 16];
-        L.s3_cyc_tpl += L.h_dbg[kDbg * i + 17];
-        L.s3_cyc_lex += L.h_dbg[kDbg * i + 18];
-        L.s3_hole += L.h_dbg[kDbg * i + 19];
-        L.s3_cyc_hole += L.h_dbg[kDbg * i + 20];
+        L.s3_full += B.h_dbg[kDbg * i + 13];
+        L.s3_tpl += B.h_dbg[kDbg * i + 14];
+        L.s3_events += B.h_dbg[kDbg * i + 15];
+        L.s3_cyc_full += B.h_dbg[kDbg * i + 16];
+        L.s3_cyc_tpl += B.h_dbg[kDbg * i + 17];
+        L.s3_cyc_lex += B.h_dbg[kDbg * i + 18];
+        L.s3_hole += B.h_dbg[kDbg * i + 19];
+        L.s3_cyc_hole += B.h_dbg[kDbg * i + 20];
       }
     }
   }
   for (; n_done < n; ++n_done) process_item(n_done);  // the rest (event wait, stage timing)
-  if (m > 0) collect_finalize(L, fin_gpu, fres);
-  if (n + m == 0)
-    for (const FinalizeReq* r : fin_host) finalize_host(*r, fres);
-  if (!requeue.empty()) {
+  if (m > 0) collect_finalize(L, J.fin_gpu, fres);
+  if (!J.posted)
+    for (const FinalizeReq* r : J.fin_host) finalize_host(*r, fres);
+  if (!J.requeue.empty()) {
     std::lock_guard<std::mutex> g(mu_);
-    for (int s : requeue) {
-      Meta& m = meta_[s];
-      if (!m.live || m.dirty) continue;
-      m.dirty = true;
+    for (int s : J.requeue) {
+      Meta& mt = meta_[s];
+      if (!mt.live || mt.dirty) continue;
+      mt.dirty = true;
       dirty_.push_back(s);
     }
   }
-  L.process_us += std::chrono::duration<double, std::micro>(HC::now() - tp0).count();
+  L.process_us += std::chrono::duration<double, std::micro>(HC::now() - J.tp0).count();
+}
+
+void HipEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin, int64_t created,
+                         std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres, int lane) {
+  thread_local HipJob J;
+  J.work = &work;
+  J.fin = &fin;
+  J.created = created;
+  J.lane = lane;
+  prepare(J);
+  post(J);
+  complete(J, results, fres);
+}
+
+// ---- pipelined ticks (GpuHub lanes) ---------------------------------------------------
+HipEngine::HipJob& HipEngine::hjob(Job& j) {
+  if (!j.impl) j.impl = std::make_shared<HipJob>();
+  HipJob& J = *std::static_pointer_cast<HipJob>(j.impl);
+  J.work = &j.work;
+  J.fin = &j.fin;
+  J.created = j.created;
+  J.lane = j.lane;
+  return J;
+}
+void HipEngine::job_prepare(Job& j) { prepare(hjob(j)); }
+void HipEngine::job_post(Job& j) { post(hjob(j)); }
+void HipEngine::job_wait_near(Job& j) { wait_near(hjob(j)); }
+void HipEngine::job_complete(Job& j, std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres) {
+  complete(hjob(j), results, fres);
 }
 
 void HipEngine::finalize_host(const FinalizeReq& r, std::vector<FinalizeRes>& out) {

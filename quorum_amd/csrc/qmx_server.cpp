@@ -628,6 +628,7 @@ class GpuHub {
     crash_thread();
     if (cfg_.engine == "hip") hipSetDevice(cfg_.device);
     std::vector<ResultBatch> per(sinks_.size());
+    if (eng_->pipelined()) return run_pipelined(lane, per);
     std::vector<int> taken;
     while (true) {
       {
@@ -645,39 +646,103 @@ class GpuHub {
         const double t_ticked = now_s();
         h_tick.observe(t_ticked - tt);
         if (ver_) ver_->check(created, rb.r, rb.f);
-        c_ticks++;
-        c_tick_slots += rb.r.size();
-        {
-          std::lock_guard<std::mutex> g(omu_);
-          for (auto& r : rb.r) {
-            const int l = r.slot < (int)owner_.size() ? owner_[r.slot] : -1;
-            if (l >= 0) per[l].r.push_back(std::move(r));
-          }
-          for (auto& f : rb.f) {
-            auto it = fin_owner_.find(f.id);
-            if (it == fin_owner_.end()) continue;
-            per[it->second].f.push_back(std::move(f));
-            fin_owner_.erase(it);
-          }
-        }
-        for (size_t l = 0; l < per.size(); ++l) {
-          if (per[l].r.empty() && per[l].f.empty()) continue;
-          if (sinks_[l]) sinks_[l](std::move(per[l]));
-          per[l] = ResultBatch();
-        }
-        eng_->settle(taken);  // after routing: a stream's next results cannot overtake these
-        c_route_ns += (uint64_t)((now_s() - t_ticked) * 1e9);
-        if (tt - last_snap_.load() > 0.05) {
-          last_snap_.store(tt);
-          std::unordered_map<std::string, double> m;
-          for (auto& kv : eng_->stats()) m["qmx_engine_" + kv.first] = kv.second;
-          if (auto* h = dynamic_cast<HipEngine*>(eng_.get()))
-            for (auto& kv : h->kernel_stats()) m["qmx_kernel_" + kv.first] = kv.second;
-          std::lock_guard<std::mutex> g(smu_);
-          snap_.swap(m);
-        }
+        deliver(rb, per, taken, t_ticked);
         if (stop_) break;
       }
+    }
+  }
+  // A pipelined lane (HipEngine with polled completion): while its tick runs on the device,
+  // the lane takes and prepares the next one, posts it the moment the running one completes,
+  // and only then turns the completed tick into results and routes them — the lane's host
+  // work (preparation, routing, settling) overlaps its device time instead of adding to it.
+  void run_pipelined(int lane, std::vector<ResultBatch>& per) {
+    HostEngine::Job jobs[2];
+    double t_post[2] = {0.0, 0.0};
+    std::vector<int> taken;
+    int c = 0;
+    while (!stop_) {
+      HostEngine::Job& cur = jobs[c];
+      if (!cur.live) {
+        {
+          std::unique_lock<std::mutex> lk(mu_);
+          cv_.wait_for(lk, std::chrono::milliseconds(2), [this] { return work_ || stop_; });
+          if (stop_) break;
+          work_ = false;
+        }
+        cur.created = (int64_t)time(nullptr);
+        cur.lane = lane;
+        if (!eng_->job_take(cur, true)) continue;
+        t_post[c] = now_s();
+        eng_->job_prepare(cur);
+        eng_->job_post(cur);
+        cur.live = true;
+      }
+      HostEngine::Job& nxt = jobs[c ^ 1];
+      eng_->job_wait_near(cur);
+      nxt.created = (int64_t)time(nullptr);
+      nxt.lane = lane;
+      // finalize requests use the lane's single finalize arenas: one tick in flight with them
+      const bool have = !stop_ && eng_->job_take(nxt, cur.fin.empty());
+      if (have) eng_->job_prepare(nxt);
+      ResultBatch rb;
+      taken.clear();
+      eng_->job_complete(cur, rb.r, rb.f);
+      eng_->job_finish(cur, rb.r, taken);
+      cur.live = false;
+      if (have) {
+        t_post[c ^ 1] = now_s();
+        eng_->job_post(nxt);
+        nxt.live = true;
+      }
+      const double t_ticked = now_s();
+      h_tick.observe(t_ticked - t_post[c]);
+      if (ver_) ver_->check(cur.created, rb.r, rb.f);
+      deliver(rb, per, taken, t_ticked);
+      c ^= 1;
+    }
+    for (HostEngine::Job& j : jobs) {  // stopping: a posted tick still completes (its slots are busy)
+      if (!j.live) continue;
+      ResultBatch rb;
+      taken.clear();
+      eng_->job_complete(j, rb.r, rb.f);
+      eng_->job_finish(j, rb.r, taken);
+      j.live = false;
+      deliver(rb, per, taken, now_s());
+    }
+  }
+  // a tick's results → the owning io loops, then its streams settle (in that order: a
+  // stream's next results cannot overtake these)
+  void deliver(ResultBatch& rb, std::vector<ResultBatch>& per, const std::vector<int>& taken, double t_ticked) {
+    c_ticks++;
+    c_tick_slots += rb.r.size();
+    {
+      std::lock_guard<std::mutex> g(omu_);
+      for (auto& r : rb.r) {
+        const int l = r.slot < (int)owner_.size() ? owner_[r.slot] : -1;
+        if (l >= 0) per[l].r.push_back(std::move(r));
+      }
+      for (auto& f : rb.f) {
+        auto it = fin_owner_.find(f.id);
+        if (it == fin_owner_.end()) continue;
+        per[it->second].f.push_back(std::move(f));
+        fin_owner_.erase(it);
+      }
+    }
+    for (size_t l = 0; l < per.size(); ++l) {
+      if (per[l].r.empty() && per[l].f.empty()) continue;
+      if (sinks_[l]) sinks_[l](std::move(per[l]));
+      per[l] = ResultBatch();
+    }
+    eng_->settle(taken);
+    c_route_ns += (uint64_t)((now_s() - t_ticked) * 1e9);
+    if (t_ticked - last_snap_.load() > 0.05) {
+      last_snap_.store(t_ticked);
+      std::unordered_map<std::string, double> m;
+      for (auto& kv : eng_->stats()) m["qmx_engine_" + kv.first] = kv.second;
+      if (auto* h = dynamic_cast<HipEngine*>(eng_.get()))
+        for (auto& kv : h->kernel_stats()) m["qmx_kernel_" + kv.first] = kv.second;
+      std::lock_guard<std::mutex> g(smu_);
+      snap_.swap(m);
     }
   }
   const ServerCfg& cfg_;
