@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <chrono>
 #include <cstddef>
 #include <functional>
 #include <memory>
@@ -238,7 +239,7 @@ class HipEngine : public HostEngine {
   void wait_stream(TickLane& L);
   // polls the tick's result records; on_item(i) as stream result i is seen published (in order)
   void wait_results(TickLane& L, int n, int m, uint32_t seq, const WorkResult* res,
-                    const std::function<void(int)>& on_item);
+                    std::chrono::steady_clock::time_point t0, const std::function<void(int)>& on_item);
   void collect_timing(TickLane& L);
   void ensure_in(TickLane::Buf& B, size_t bytes);
   void ensure_out(TickLane& L, size_t bytes);

@@ -1981,11 +1981,11 @@ void HipEngine::wait_stream(TickLane& L) {
 // A launch that has not published after 4x the EMA + 2 ms synchronises its stream (surfaces a
 // fault; correct even if host-mapped visibility misbehaved: counted in poll_fallbacks).
 void HipEngine::wait_results(TickLane& L, int n, int m, uint32_t seq, const WorkResult* res,
-                             const std::function<void(int)>& on_item) {
+                             std::chrono::steady_clock::time_point t0, const std::function<void(int)>& on_item) {
   using HC = std::chrono::steady_clock;
   static thread_local bool slack = (prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0), true);
   (void)slack;
-  const auto t0 = HC::now();
+  // t0: when the tick was posted (a pipelined lane prepares its next tick before waiting)
   auto nap = [](double us) {
     if (us < 1) return;
     timespec ts{0, (long)(us * 1000)};
@@ -1997,7 +1997,7 @@ void HipEngine::wait_results(TickLane& L, int n, int m, uint32_t seq, const Work
     return i == n + m;
   };
   int i = 0;
-  nap(0.6 * L.ema_us - 6.0);
+  nap(0.6 * L.ema_us - 6.0 - std::chrono::duration<double, std::micro>(HC::now() - t0).count());
   while (!done(i)) {
     const double el = std::chrono::duration<double, std::micro>(HC::now() - t0).count();
     // a persistent grid is only stopped to surface a fault: a tick it has not reached yet
@@ -2391,6 +2391,9 @@ void HipEngine::prepare(HipJob& J) {
   ensure_in(B, in_need + 64);
   ensure_out(L, out_need + 64);
   J.arena = L.out;
+  // the job holds its arena until complete(): a tick prepared meanwhile (pipelined lanes)
+  // must not pick it while this kernel writes it and before any result views it
+  J.arena->refs.fetch_add(1, std::memory_order_relaxed);
   if (work.size() > B.items_cap) {
     retire_host(B.h_items);
     retire_host(B.h_res);
@@ -2625,7 +2628,7 @@ void HipEngine::complete(HipJob& J, std::vector<SlotResult>& results, std::vecto
     for (const FinalizeReq* r : J.fin_host) finalize_host(*r, fres);
     if (poll_) {
       // one HIP call per tick, or none: completion and kernel span come from the result records
-      wait_results(L, n, m, J.seq, B.h_res, [&](int i) {
+      wait_results(L, n, m, J.seq, B.h_res, J.tp1, [&](int i) {
         const auto ti = HC::now();
         if (n_done == 0) L.first_result_us += std::chrono::duration<double, std::micro>(ti - J.tp1).count();
         if (i == n_done) process_item(n_done++);
@@ -2713,6 +2716,7 @@ void HipEngine::complete(HipJob& J, std::vector<SlotResult>& results, std::vecto
       dirty_.push_back(s);
     }
   }
+  J.arena->refs.fetch_sub(1, std::memory_order_release);  // results hold their own references
   L.process_us += std::chrono::duration<double, std::micro>(HC::now() - J.tp0).count();
 }
 

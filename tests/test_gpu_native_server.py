@@ -44,3 +44,25 @@ def test_native_hip_random_sessions(seed, monkeypatch):
     monkeypatch.setattr(T, "VERIFY", True)
     R.test_random_session_native_matches_python(seed)
     assert ext.server_counters()["verify_mismatches"] == before
+
+
+def test_gpu_bench_headline_valid(tmp_path):
+    """The headline bench on the HIP engine (shared engine, pipelined tick lanes, persistent
+    grids, result views) under full closed-loop load: every response is validated byte for
+    byte by the load generator, so a lane that reuses an output arena too early, or any other
+    cross-tick corruption, fails here."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, QMX_BENCH_ENGINE="hip")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "4", "--warmup", "1",
+                        "--batch", "8192", "--port", "23400"],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=180)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert lines, r.stderr[-3000:]
+    res = json.loads(lines[-1])
+    assert r.returncode == 0 and res["valid"] and res["invalid"] == 0, (res.get("invalid"), r.stderr[-2000:])
+    assert res["validated"] == 4 * 8192 and res["breakdown_one_rank"]["kernel_launches"] > 0
