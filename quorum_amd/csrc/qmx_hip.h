@@ -187,6 +187,7 @@ struct TickLane {
   // completion by polling the kernel-published sequence numbers (HipEngine::wait_results)
   uint32_t seq = 0;
   double ema_us = 40.0;  // launch-to-results time, smoothed
+  double span_ema_us = 30.0;  // kernel span per tick (device clock), smoothed: pipelined lanes
   bool timing_pending = false;
   uint64_t poll_fallbacks = 0;
   // persistent mode (QMX_PERSISTENT=1): the lane's long-lived grid and its doorbell

@@ -2544,8 +2544,10 @@ void HipEngine::wait_near(HipJob& J) {
   if (!J.posted) return;
   TickLane& L = *lanes_[(size_t)J.lane % lanes_.size()];
   const double el = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - J.tp1).count();
+  // the device's own clock (kernel span per tick) sets the target: an estimate from host
+  // wake-ups would include this very nap and drift upward tick after tick
   const double prep = L.launches ? L.host_prep_us / (double)L.launches : 5.0;
-  const double target = L.ema_us - prep - 4.0;
+  const double target = L.span_ema_us + 6.0 - prep;
   if (target - el >= 2.0) {
     timespec ts{0, (long)((target - el) * 1000)};
     nanosleep(&ts, nullptr);
@@ -2661,7 +2663,10 @@ void HipEngine::complete(HipJob& J, std::vector<SlotResult>& results, std::vecto
         a = std::min(a, L.h_finres[i].t0);
         b = std::max(b, L.h_finres[i].t1);
       }
-      if (b > a) L.kernel_ms += (double)(b - a) * 1e-5;  // 100 MHz ticks -> ms
+      if (b > a) {
+        L.kernel_ms += (double)(b - a) * 1e-5;  // 100 MHz ticks -> ms
+        L.span_ema_us = 0.85 * L.span_ema_us + 0.15 * std::min((double)(b - a) * 1e-2, 2000.0);
+      }
     } else {
       HIP_CHECK(hipEventRecord(L.ev1, L.stream));
       wait_stream(L);
