@@ -204,7 +204,9 @@ class HostEngine {
     std::shared_ptr<void> impl;  // the engine's state between the phases
   };
   virtual bool pipelined() const { return false; }
-  bool pipeline_ = true;  // QMX_PIPELINE=0: lanes tick one job at a time (A/B)
+  // QMX_PIPELINE=1: pipelined lanes.  Off by default: on MI355X they raise the tick rate
+  // ~40% but not the closed-loop req/s (latency-bound), and cost ~3 us of proxy CPU per request
+  bool pipeline_ = false;
   bool job_take(Job& j, bool allow_fin);
   virtual void job_prepare(Job&) {}
   virtual void job_post(Job&) {}

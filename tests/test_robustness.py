@@ -64,12 +64,15 @@ def _spec(path, exp, n):
 
 
 @native_only
-@pytest.mark.parametrize("threads,lanes", [(1, 2), (3, 3)])
-def test_abort_churn_shared_engine(tmp_path, threads, lanes):
+@pytest.mark.parametrize("threads,lanes,pipe", [(1, 2, "0"), (3, 3, "0"), (3, 2, "1")])
+def test_abort_churn_shared_engine(tmp_path, monkeypatch, threads, lanes, pipe):
     """30% of clients hang up mid-stream while new requests keep landing on the same io
     loops (slot reuse under in-flight ticks): every completed response must still be
-    exactly its own two backends' streams."""
+    exactly its own two backends' streams — also with pipelined lanes (QMX_PIPELINE=1: the
+    next tick taken and prepared while the current one runs)."""
     import yaml  # noqa: F401
+
+    monkeypatch.setenv("QMX_PIPELINE", pipe)
 
     sys.path.insert(0, ROOT)
     import bench
