@@ -373,6 +373,14 @@ def breakdown(m0, m1, elapsed):
                                         ("tick", "qmx_tick_seconds"), ("ttft", "qmx_ttft_seconds"),
                                         ("request", "qmx_request_latency_seconds"))
                            if d.get(f"{m}_count")},
+        # the io-loop / lane hand-offs around a tick (means): the oldest upstream bytes of an
+        # io-loop iteration until they reach the engine, a dirty stream until a lane takes
+        # it, a tick's results from routing until the io loop applies them
+        "handoff_us_avg": {k: round(f * d[a] / d[b], 1)
+                           for k, a, b, f in (("feed_to_engine", "qmx_flush_wait_seconds_total", "qmx_flushes_total", 1e6),
+                                              ("dirty_to_taken", "qmx_engine_take_wait_us", "qmx_engine_takes", 1.0),
+                                              ("routed_to_applied", "qmx_apply_wait_seconds_total", "qmx_applies_total", 1e6))
+                           if d.get(b)},
     }
 
 

@@ -2,6 +2,7 @@
 #include "qmx_engine.h"
 
 #include <cstdlib>
+#include <ctime>
 
 #include <algorithm>
 #include <cstdio>
@@ -300,6 +301,12 @@ void finalize_texts(const TagSet& ts, const std::vector<std::string>& texts, con
 // --------------------------------------------------------------------------------
 // HostEngine
 // --------------------------------------------------------------------------------
+static double mono_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
 HostEngine::HostEngine(const std::vector<std::string>& tags) : ts_(make_tagset(tags)) {
   if (const char* pe = getenv("QMX_PIPELINE")) pipeline_ = atoi(pe) != 0;
 }
@@ -393,6 +400,7 @@ void HostEngine::feed_locked(int slot, const std::string& data) {
   bytes_in_ += data.size();
   if (!m.dirty) {
     m.dirty = true;
+    m.t_dirty = mono_s();
     dirty_.push_back(slot);
   }
 }
@@ -407,6 +415,7 @@ void HostEngine::feed_locked_move(int slot, std::string& data) {
   Meta& m = meta_[slot];
   if (!m.dirty) {
     m.dirty = true;
+    m.t_dirty = mono_s();
     dirty_.push_back(slot);
   }
 }
@@ -417,6 +426,7 @@ void HostEngine::finish_locked(int slot) {
   m.eof = true;
   if (!m.dirty) {
     m.dirty = true;
+    m.t_dirty = mono_s();
     dirty_.push_back(slot);
   }
 }
@@ -461,6 +471,7 @@ bool HostEngine::job_take(Job& j, bool allow_fin) {
   pending_free_.swap(keep);
   keep.clear();
   j.work.reserve(dirty_.size());
+  double now = 0;
   for (int s : dirty_) {
     Meta& m = meta_[s];
     if (m.busy && m.live) {  // this stream's previous tick is not settled: next time
@@ -469,6 +480,11 @@ bool HostEngine::job_take(Job& j, bool allow_fin) {
     }
     m.dirty = false;
     if (!m.live) continue;
+    if (m.t_dirty > 0) {
+      if (now == 0) now = mono_s();
+      take_wait_s_ += now - m.t_dirty;
+      ++takes_;
+    }
     Work w{s, std::string(), m.eof, m.fresh};
     w.data.swap(m.incoming);
     m.fresh = false;
@@ -530,6 +546,7 @@ void HostEngine::set_remote_content(int slot, const std::string* bytes, size_t l
 std::unordered_map<std::string, double> HostEngine::stats() {
   std::lock_guard<std::mutex> g(mu_);
   return {{"ticks", (double)ticks_}, {"bytes_in", (double)bytes_in_}, {"bytes_out", (double)bytes_out_},
+          {"takes", (double)takes_}, {"take_wait_us", take_wait_s_ * 1e6},
           {"slots", (double)meta_.size()}, {"free", (double)free_.size()}};
 }
 

@@ -248,6 +248,7 @@ class HostEngine {
     bool closed = false;  // DONE/ABORTED reported
     bool busy = false;    // taken by an unsettled tick (in flight on some lane)
     uint32_t gen = 0;     // bumped by every open()
+    double t_dirty = 0;   // steady clock (s) when it last became dirty: take-wait timing
     std::string incoming;
   };
 
@@ -261,7 +262,8 @@ class HostEngine {
   std::vector<int> dirty_;
   std::vector<FinalizeReq> fin_;
   int next_fid_ = 0;
-  uint64_t ticks_ = 0, bytes_in_ = 0, bytes_out_ = 0;
+  uint64_t ticks_ = 0, bytes_in_ = 0, bytes_out_ = 0, takes_ = 0;
+  double take_wait_s_ = 0;  // dirty -> taken by a tick, summed over takes
 };
 
 class CpuEngine : public HostEngine {

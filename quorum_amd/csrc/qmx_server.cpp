@@ -43,7 +43,9 @@ std::atomic<bool> g_drain{false};  // SIGTERM: stop accepting, finish in-flight 
 std::atomic<int> g_ready{0};       // io loops with a bound listener
 std::atomic<uint64_t> c_requests{0}, c_stream{0}, c_nonstream{0}, c_errors{0}, c_up_fail{0}, c_ticks{0},
     c_tick_slots{0}, c_up_conns{0}, c_clients{0}, c_remote_streams{0},
-    c_route_ns{0};  // tick lanes: tick returned -> results handed to the io loops + streams settled
+    c_route_ns{0},  // tick lanes: tick returned -> results handed to the io loops + streams settled
+    c_flush_ns{0}, c_flushes{0},  // io loop: oldest upstream bytes of a batch -> handed to the engine
+    c_apply_ns{0}, c_applies{0};  // io loop: a tick's results routed -> applied (sent to clients)
 // failures by class
 std::atomic<uint64_t> c_fail_connect{0}, c_fail_timeout{0}, c_fail_status{0}, c_fail_disconnect{0},
     c_fail_protocol{0}, c_stream_aborts{0};
@@ -387,6 +389,7 @@ struct Session {
 struct ResultBatch {
   std::vector<SlotResult> r;
   std::vector<FinalizeRes> f;
+  double t_routed = 0;
 };
 
 // --------------------------------------------------------------------------------------
@@ -730,6 +733,7 @@ class GpuHub {
     }
     for (size_t l = 0; l < per.size(); ++l) {
       if (per[l].r.empty() && per[l].f.empty()) continue;
+      per[l].t_routed = now_s();
       if (sinks_[l]) sinks_[l](std::move(per[l]));
       per[l] = ResultBatch();
     }
@@ -971,7 +975,14 @@ class Loop {
       std::lock_guard<std::mutex> g(rmu_);
       q.swap(rq_);
     }
-    for (auto& rb : q) apply(rb);
+    const double t = now_s();
+    for (auto& rb : q) {
+      if (rb.t_routed > 0) {
+        c_apply_ns += (uint64_t)((t - rb.t_routed) * 1e9);
+        c_applies++;
+      }
+      apply(rb);
+    }
   }
   void apply(ResultBatch& rb) {
     for (auto& r : rb.r) {
@@ -1030,11 +1041,19 @@ class Loop {
   // feed / finish / release are queued in order and handed to the engine once per loop
   // iteration (flush_ops: one engine lock instead of one per upstream read — with the
   // shared engine, 8+ loops and the tick lanes otherwise contend on it per call)
-  void e_feed_move(int slot, std::string& d) { ops_.push_back(EngineOp{EngineOp::FEED, slot, std::move(d)}); }
+  void e_feed_move(int slot, std::string& d) {
+    if (ops_t0_ == 0) ops_t0_ = now_s();
+    ops_.push_back(EngineOp{EngineOp::FEED, slot, std::move(d)});
+  }
   void e_finish(int slot) { ops_.push_back(EngineOp{EngineOp::FINISH, slot, std::string()}); }
   void e_release(int slot) { ops_.push_back(EngineOp{EngineOp::RELEASE, slot, std::string()}); }
   void flush_ops() {
     if (ops_.empty()) return;
+    if (ops_t0_ > 0) {
+      c_flush_ns += (uint64_t)((now_s() - ops_t0_) * 1e9);
+      c_flushes++;
+      ops_t0_ = 0;
+    }
     if (hub_) {
       hub_->apply_ops(ops_);
     } else {
@@ -2556,6 +2575,10 @@ class Loop {
     put("qmx_ticks_total", (double)c_ticks.load());
     put("qmx_tick_slots_total", (double)c_tick_slots.load());
     put("qmx_tick_route_seconds_total", (double)c_route_ns.load() * 1e-9);
+    put("qmx_flush_wait_seconds_total", (double)c_flush_ns.load() * 1e-9);
+    put("qmx_flushes_total", (double)c_flushes.load());
+    put("qmx_apply_wait_seconds_total", (double)c_apply_ns.load() * 1e-9);
+    put("qmx_applies_total", (double)c_applies.load());
     put("qmx_remote_streams_total", (double)c_remote_streams.load());
     m += "qmx_upstream_failures_by_class_total{class=\"connect\"} " + std::to_string(c_fail_connect.load()) + "\n";
     m += "qmx_upstream_failures_by_class_total{class=\"timeout\"} " + std::to_string(c_fail_timeout.load()) + "\n";
@@ -2660,6 +2683,7 @@ class Loop {
     return (e ? atof(e) : 1000.0) * 1e-6;
   }();
   std::vector<EngineOp> ops_;  // engine feed / finish / release of this iteration (flush_ops)
+  double ops_t0_ = 0;  // the oldest unflushed FEED op (flush-wait timing)
   int64_t role_sec_ = -1;      // second of the cached SSE head + role event
   std::string role_head_;
   // fault injection (tests): drop every Nth stream result's SSE bytes before it is sent
