@@ -838,6 +838,16 @@ class Loop {
       cnt(SC_EPOLL_WAIT);
       for (int i = 0; i < n; ++i) dispatch(evs[i]);
       if (g_drain.load() && drain_step()) break;
+      if (hub_ && early_flush_) {
+        // upstream bytes to the tick lanes and finished responses to their clients before
+        // this iteration's new requests (whose parsing and upstream sends are the slow part)
+        flush_ops();
+        if (kick_) {
+          kick_ = false;
+          hub_->kick();
+        }
+        if (!flushq_.empty()) flush_queued();
+      }
       if (!pending_requests_.empty()) {
         std::vector<int>& fds = scratch_fds_;  // swapped each iteration: both buffers keep their capacity
         fds.clear();
@@ -2683,6 +2693,7 @@ class Loop {
     return (e ? atof(e) : 1000.0) * 1e-6;
   }();
   std::vector<EngineOp> ops_;  // engine feed / finish / release of this iteration (flush_ops)
+  bool early_flush_ = !getenv("QMX_EARLY_FLUSH") || atoi(getenv("QMX_EARLY_FLUSH")) != 0;  // A/B knob
   double ops_t0_ = 0;  // the oldest unflushed FEED op (flush-wait timing)
   int64_t role_sec_ = -1;      // second of the cached SSE head + role event
   std::string role_head_;
