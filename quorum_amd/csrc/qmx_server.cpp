@@ -781,6 +781,7 @@ class Loop {
           std::lock_guard<std::mutex> g(rmu_);
           rq_.push_back(std::move(rb));
         }
+        rq_pending_.store(true, std::memory_order_release);
         uint64_t one = 1;
         ssize_t w = write(evfd_, &one, 8);
         (void)w;
@@ -836,7 +837,11 @@ class Loop {
       const int to = (!hub_ && kick_) ? 0 : deferq_.empty() ? 50 : 1;
       int n = epoll_wait(ep_, evs.data(), (int)evs.size(), to);
       cnt(SC_EPOLL_WAIT);
-      for (int i = 0; i < n; ++i) dispatch(evs[i]);
+      for (int i = 0; i < n; ++i) {
+        dispatch(evs[i]);
+        // a long batch: tick results that arrived meanwhile are applied now, not after it
+        if ((i & 7) == 7 && early_flush_ && rq_pending_.load(std::memory_order_acquire)) on_results(false);
+      }
       if (g_drain.load() && drain_step()) break;
       if (hub_ && early_flush_) {
         // upstream bytes to the tick lanes and finished responses to their clients before
@@ -974,16 +979,21 @@ class Loop {
     c_tick_slots += rb.r.size();
     apply(rb);
   }
-  void on_results() {
-    uint64_t v;
-    ssize_t r = read(evfd_, &v, 8);
-    cnt(SC_WAKE_READ);
-    (void)r;
+  // read_fd = false: results picked up between the events of a busy iteration (the eventfd
+  // stays readable and is drained when epoll reports it)
+  void on_results(bool read_fd = true) {
+    if (read_fd) {
+      uint64_t v;
+      ssize_t r = read(evfd_, &v, 8);
+      cnt(SC_WAKE_READ);
+      (void)r;
+    }
     std::vector<ResultBatch>& q = scratch_rq_;
     q.clear();
     {
       std::lock_guard<std::mutex> g(rmu_);
       q.swap(rq_);
+      rq_pending_.store(false, std::memory_order_relaxed);
     }
     const double t = now_s();
     for (auto& rb : q) {
@@ -2646,6 +2656,7 @@ class Loop {
   bool kick_ = false;
   std::mutex rmu_;
   std::vector<ResultBatch> rq_;
+  std::atomic<bool> rq_pending_{false};  // set by the tick lanes with each batch pushed
   std::unordered_map<int, std::unique_ptr<Client>> clients_;
   std::unordered_map<int, std::unique_ptr<Up>> ups_;
   std::unordered_map<Session*, std::unique_ptr<Session>> sessions_;
