@@ -488,9 +488,6 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   // the work item is wave-uniform: keep its fields in scalar registers (a one-shot launch
   // reads it through the scalar cache anyway; a persistent grid loads it per tick with
   // vector loads, and every address derived from VGPR copies would cost vector registers)
-  // the host lays tile k out at k * TILE_MAX (HipEngine::prepare): its first BS * 16 bytes
-  // are loaded now, in the same round trip over PCIe as the work item, not after it
-  const uint4 spec = *(const uint4*)&in[(size_t)bi * TILE_MAX + tid * 16];
   WorkItem it = items[bi];
   it.slot = __builtin_amdgcn_readfirstlane(it.slot);
   it.in_off = __builtin_amdgcn_readfirstlane(it.in_off);
@@ -507,9 +504,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   const bool fresh = it.flags & WF_FRESH;
 
   // ---- S0: load tile (16-B vector loads from host-mapped memory) -----------------
-  const bool spec_ok = it.in_off == (uint32_t)bi * TILE_MAX;  // uniform: the fixed layout
-  if (spec_ok && tid * 16 < in_len) *(uint4*)&s.A[tid * 16] = spec;
-  for (int i = tid * 16 + (spec_ok ? BS * 16 : 0); i < in_len; i += BS * 16)
+  for (int i = tid * 16; i < in_len; i += BS * 16)
     *(uint4*)&s.A[i] = *(const uint4*)&in[it.in_off + i];
   if (tid == 0) {
     s.v[V_ABORT] = MAX_EV;
@@ -2366,7 +2361,7 @@ struct HipEngine::HipJob {
   std::vector<SlotResult> host_results;  // escalated streams, processed on the host in prepare
   TickLane::Buf* B = nullptr;
   TickLane::OutArena* arena = nullptr;
-  size_t in_off = 0, in_bytes = 0;
+  size_t in_off = 0;
   std::chrono::steady_clock::time_point tp0, tp1;
 };
 
@@ -2382,7 +2377,6 @@ void HipEngine::prepare(HipJob& J) {
   J.fin_gpu.clear();
   J.fin_host.clear();
   J.posted = false;
-  J.in_bytes = 0;
   std::vector<Work>& work = *J.work;
   TickLane::Buf& B = L.bufs[L.next_buf];
   L.next_buf ^= 1;
@@ -2391,7 +2385,7 @@ void HipEngine::prepare(HipJob& J) {
   for (auto& w : work) {
     size_t tot = core_[w.slot].carry.size() + w.data.size();
     size_t sub = std::min(tot, (size_t)tile_);
-    in_need += TILE_MAX;  // tile k at k * TILE_MAX: the kernel prefetches it with the work item
+    in_need += (sub + 15) & ~(size_t)15;
     out_need += ((12 * sub + 1024) + 15) & ~(size_t)15;
   }
   ensure_in(B, in_need + 64);
@@ -2461,8 +2455,7 @@ void HipEngine::prepare(HipJob& J) {
                (c.started ? WF_STARTED : 0) | (w.fresh ? WF_FRESH : 0);
     it.index = (uint32_t)c.index;
     it.content_len = content_len_[slot];
-    in_off += TILE_MAX;
-    J.in_bytes += sub;
+    in_off += (sub + 15) & ~(size_t)15;
     out_off += ((size_t)it.out_cap + 15) & ~(size_t)15;
     J.pend.push_back({slot, cl, sub, eof_sent, &w});
     ++n;
@@ -2512,7 +2505,7 @@ void HipEngine::post(HipJob& J) {
   }
   J.tp1 = std::chrono::steady_clock::now();
   roctxRangePushA("qmx_tick");  // rocprofv3 --marker-trace: one range per tick launch + wait
-  L.h2d_bytes += J.in_bytes;
+  L.h2d_bytes += J.in_off;
   if (J.persist) ensure_persistent(L);  // before the tick's sequence number: a relaunch starts from L.seq
   J.seq = next_seq(L);
   const uint32_t par = L.launches & 1;  // backend template table: read last tick's half, write the other
