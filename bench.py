@@ -429,7 +429,7 @@ def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports
                 raise RuntimeError("injected spread-check failure")
             procs = spawn_workers(cfg, "127.0.0.1", port, 1, engine, device, impl="native",
                                   threads=args.threads, env=env)
-            if not wait_healthy("127.0.0.1", port, 120):
+            if not wait_healthy("127.0.0.1", port, 60):
                 raise RuntimeError("spread proxy did not become healthy")
         except Exception as e:  # noqa: BLE001 - agreed on below, reported in the JSON line
             ok, err = False, repr(e)[:300]
@@ -440,7 +440,7 @@ def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports
                     m = scrape(port)
                     if m.get("qmx_exchange_healthy") == 1.0 and (not want_rccl or m.get("qmx_exchange_rccl_active") == 1.0):
                         break
-                    if time.time() - t0 > 90:
+                    if time.time() - t0 > 60:
                         raise RuntimeError(f"exchange did not form: {({k: v for k, v in m.items() if 'exchange' in k})}")
                     time.sleep(0.2)
             except Exception as e:  # noqa: BLE001
@@ -448,7 +448,7 @@ def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports
         if agree("exchange formation"):
             try:
                 m0 = scrape(port)
-                st = loadgen(bin_dir, port, 32, 2048, 2, 120, spec)
+                st = loadgen(bin_dir, port, 32, 2048, 2, 60, spec)
                 time.sleep(0.2)
                 m1 = scrape(port)
                 d = {k: m1.get(k, 0.0) - m0.get(k, 0.0) for k in m1 if "exchange" in k or "remote_streams" in k}
