@@ -48,6 +48,9 @@ def native_cluster(cfg, world: int, placement: str = "spread"):
     ports = [free_port() for _ in range(world)]
     xport = free_port_block(world)  # the mesh: rank r listens on xport + r
     threads = []
+    # every rank's config first, then the servers: the environment is only changed while no
+    # server thread runs (a running server reads it — getenv racing setenv can crash)
+    cfgs = []
     for r in range(world):
         env = {"QMX_RANK": str(r), "QMX_WORLD": str(world), "QMX_XCHG": "tcp", "QMX_XCHG_PORT": str(xport),
                "QMX_XCHG_ROUND_US": "100"}
@@ -62,6 +65,8 @@ def native_cluster(cfg, world: int, placement: str = "spread"):
                 else:
                     os.environ[k] = v
         d["install_signals"] = False
+        cfgs.append(d)
+    for d in cfgs:
         th = threading.Thread(target=ext.run_server, args=(d,), daemon=True)
         th.start()
         threads.append(th)
