@@ -88,6 +88,12 @@ Hist h_ttft, h_latency, h_tick, h_upstream_ttfb, h_engine;
 
 using Clock = std::chrono::steady_clock;
 inline double now_s() { return std::chrono::duration<double>(Clock::now().time_since_epoch()).count(); }
+// QMX_* on/off knobs, read once where a loop or engine is built ("0" / "false": off)
+inline bool env_flag(const char* name, bool dflt) {
+  const char* v = getenv(name);
+  if (!v || !*v) return dflt;
+  return !(std::strcmp(v, "0") == 0 || std::strcmp(v, "false") == 0);
+}
 
 // Header block [p, p+n) ("k: v\r\n" lines, no start line): calls f(lower(trim(k)), trim(v)) per line that
 // has a colon, building each key and value string once (no per-line/per-field temporaries).
@@ -2704,7 +2710,7 @@ class Loop {
     return (e ? atof(e) : 1000.0) * 1e-6;
   }();
   std::vector<EngineOp> ops_;  // engine feed / finish / release of this iteration (flush_ops)
-  bool early_flush_ = !getenv("QMX_EARLY_FLUSH") || atoi(getenv("QMX_EARLY_FLUSH")) != 0;  // A/B knob
+  const bool early_flush_ = env_flag("QMX_EARLY_FLUSH", true);  // A/B knob
   double ops_t0_ = 0;  // the oldest unflushed FEED op (flush-wait timing)
   int64_t role_sec_ = -1;      // second of the cached SSE head + role event
   std::string role_head_;
