@@ -275,6 +275,7 @@ class HipEngine : public HostEngine {
   int poll_us_ = 1;   // QMX_POLL_US: poll period once the expected kernel time has passed (MI355X A/Bs: 2 beats 6, 1 beats 2)
   bool persistent_ = true;   // a long-lived grid per lane, ticks posted by doorbell (QMX_PERSISTENT=0: a launch per tick)
   bool views_ = true;         // QMX_VIEWS=0: results copy their SSE bytes on the lane thread
+  bool stage_timing_ = false;  // QMX_STAGE_TIMING: per-item stage stamps (tools/kbench.py)
   int p_grid_ = 64;          // QMX_PERSISTENT_WG: workgroups per lane grid (1 per CU: 256 VGPRs)
   int p_idle_ms_ = 50;       // the grid exits after this long without a tick
 

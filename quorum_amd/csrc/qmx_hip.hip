@@ -2053,6 +2053,7 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
   if (const char* gs = getenv("QMX_GPU_SHARERS")) persistent_ = atoi(gs) <= 1;
   if (const char* pe = getenv("QMX_PERSISTENT")) persistent_ = atoi(pe) != 0;
   if (const char* va = getenv("QMX_VIEWS")) views_ = atoi(va) != 0;
+  stage_timing_ = getenv("QMX_STAGE_TIMING") != nullptr;  // read once: getenv scans the environment
   if (const char* pw = getenv("QMX_PERSISTENT_WG")) p_grid_ = std::min(std::max(8, atoi(pw)), 1024);
   if (const char* pi = getenv("QMX_PERSISTENT_IDLE_MS")) p_idle_ms_ = std::min(std::max(5, atoi(pi)), 1000);
   {
@@ -2473,7 +2474,7 @@ void HipEngine::prepare(HipJob& J) {
     }
     unsigned long long* const dbg0 = L.params.dbg;
     L.params.dbg = nullptr;
-    if (getenv("QMX_STAGE_TIMING")) {
+    if (stage_timing_) {
       if (B.dbg_cap < (size_t)n) {
         if (B.h_dbg) retire_host(B.h_dbg);
         B.dbg_cap = std::max((size_t)n, B.items_cap);
