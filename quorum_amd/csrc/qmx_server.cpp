@@ -787,7 +787,11 @@ class Loop {
           std::lock_guard<std::mutex> g(rmu_);
           rq_.push_back(std::move(rb));
         }
-        rq_pending_.store(true, std::memory_order_release);
+        rq_pending_.store(true, std::memory_order_seq_cst);
+        // QMX_LAZY_WAKE: a loop that is not parked in epoll_wait picks the batch up itself
+        // (between events, or before it waits: the Dekker pair in_wait_ / rq_pending_), so
+        // only a parked loop costs the lane an eventfd write
+        if (lazy_wake_ && !in_wait_.load(std::memory_order_seq_cst)) return;
         uint64_t one = 1;
         ssize_t w = write(evfd_, &one, 8);
         (void)w;
@@ -840,8 +844,16 @@ class Loop {
     while (!g_stop.load()) {
       // inline engine with work queued by the last iteration (e.g. a finalize submitted
       // while applying tick results): poll instead of sleeping
-      const int to = (!hub_ && kick_) ? 0 : deferq_.empty() ? 50 : 1;
+      int to = (!hub_ && kick_) ? 0 : deferq_.empty() ? 50 : 1;
+      if (lazy_wake_ && hub_) {
+        in_wait_.store(true, std::memory_order_seq_cst);
+        if (rq_pending_.load(std::memory_order_seq_cst)) to = 0;  // a batch came in: do not sleep
+      }
       int n = epoll_wait(ep_, evs.data(), (int)evs.size(), to);
+      if (lazy_wake_ && hub_) {
+        in_wait_.store(false, std::memory_order_seq_cst);
+        if (rq_pending_.load(std::memory_order_acquire)) on_results(false);
+      }
       cnt(SC_EPOLL_WAIT);
       for (int i = 0; i < n; ++i) {
         dispatch(evs[i]);
@@ -2711,6 +2723,8 @@ class Loop {
   }();
   std::vector<EngineOp> ops_;  // engine feed / finish / release of this iteration (flush_ops)
   const bool early_flush_ = env_flag("QMX_EARLY_FLUSH", true);  // A/B knob
+  const bool lazy_wake_ = env_flag("QMX_LAZY_WAKE", false);   // A/B knob (see attach_hub)
+  std::atomic<bool> in_wait_{false};                          // in epoll_wait (lazy wake)
   double ops_t0_ = 0;  // the oldest unflushed FEED op (flush-wait timing)
   int64_t role_sec_ = -1;      // second of the cached SSE head + role event
   std::string role_head_;

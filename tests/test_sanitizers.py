@@ -178,9 +178,10 @@ def test_server_tsan_shared_engine_lanes(tmp_path):
     d.update(env_api_key="", api_key_from_env=False, shared_engine=1, tick_lanes=3, verify=True)
     path = tmp_path / "tsan.json"
     path.write_text(json.dumps(d))
-    # pipelined lanes on (QMX_PIPELINE=1): the next tick is taken while the current one runs
+    # pipelined lanes on (QMX_PIPELINE=1): the next tick is taken while the current one runs;
+    # lazy wakes (QMX_LAZY_WAKE=1): lanes skip the eventfd of an io loop that is not waiting
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=0:second_deadlock_stack=1:report_signal_unsafe=0",
-               QMX_PIPELINE="1")
+               QMX_PIPELINE="1", QMX_LAZY_WAKE="1")
     srv = subprocess.Popen([str(tsan), str(path)], stderr=subprocess.PIPE, env=env)
     try:
         t0 = time.time()
