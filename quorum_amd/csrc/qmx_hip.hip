@@ -1022,26 +1022,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   // ---- S4: think filter ----------------------------------------------------------------
   const uint8_t* W = Z;  // identity when not filtering
   int ncand = 0, ntok = 0;
-  bool any_lt = false;  // a '<' anywhere in Z (old holdback tail + new deltas)?
   if (filt && ndelta > 0) {
-    int found = 0;
-    for (int p = tid; p < Zn; p += BS) found |= Z[p] == '<';
-    any_lt = __syncthreads_or(found) != 0;
-  }
-  if (filt && ndelta > 0 && !any_lt) {
-    // no tag can start in these bytes (and no holdback is pending: a held tail starts with
-    // '<'): outside a think block every byte is kept, inside one every byte is dropped
-    const bool keep = depth0 == 0;
-    for (int j = tid; j < ndelta; j += BS) {
-      s.cut[j] = s.dl_end[j];
-      s.wpos[j] = keep ? s.dl_end[j] : 0;
-    }
-    if (tid == 0) {
-      s.v[V_WLEN] = keep ? Zn : 0;
-      s.v[V_NEWTAIL] = -1;
-      s.v[V_NEWDEPTH] = depth0;
-    }
-  } else if (filt && ndelta > 0) {
     // candidates: per-thread 8-byte-multiple chunks of Z (16-B aligned) as ds_read_b64
     // words, a 32-bit '<' mask per thread (SWAR compare), popcount + ordered compaction
     {
@@ -1076,6 +1057,21 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       }
       ncand = tot;
     }
+  }
+  if (filt && ndelta > 0 && ncand == 0) {  // no '<' anywhere in Z (old holdback tail + new deltas)
+    // no tag can start in these bytes (and no holdback is pending: a held tail starts with
+    // '<'): outside a think block every byte is kept, inside one every byte is dropped
+    const bool keep = depth0 == 0;
+    for (int j = tid; j < ndelta; j += BS) {
+      s.cut[j] = s.dl_end[j];
+      s.wpos[j] = keep ? s.dl_end[j] : 0;
+    }
+    if (tid == 0) {
+      s.v[V_WLEN] = keep ? Zn : 0;
+      s.v[V_NEWTAIL] = -1;
+      s.v[V_NEWDEPTH] = depth0;
+    }
+  } else if (filt && ndelta > 0) {
     if (ncand > MAX_CAND) {
       if (tid == 0) {
         WorkResult r{0u, 0u, (uint32_t)WS_ESCALATE, it.content_len};
