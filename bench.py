@@ -39,14 +39,19 @@ sys.path.insert(0, ROOT)
 BASELINE_SOURCE_SAME = "reference proxy, same box + same harness (bench.py --impl reference)"
 BASELINE_SOURCE_SURVEY = "reference proxy, survey container (8 vCPU, Python harness; SURVEY §6)"
 
+# port layout above --port: +7.. exchange mesh, +50 the spread check's proxies (+57.. its mesh),
+# +100 + 10 rank + i mock backends, +200 + rank / +230 + rank each rank's own admin port
+# (headline / spread check)
+ADMIN_OFF, SPREAD_ADMIN_OFF = 200, 230
+
 # BASELINE.json configs.  "headline" is the driver's metric; the others are measured with
 # --scenario; every one with a reference number has it from the same harness.
 SCENARIOS = {
-    # headline: 16384 requests per step so the timed window (one load-generator run) is ~2 s
-    # and its start/connect/drain is amortised (MI355X A/B, profiles/r1n_batch_ab.txt: 4/4
-    # pairs higher, mean 180k vs 153k req/s against 4096 per step)
+    # headline: 131072 requests per step per rank, so the driver's 20 timed steps are one
+    # load-generator run of >= 10 s on one GPU (~230k req/s): box noise, connection set-up and
+    # drain are amortised (r2's 16384 gave a 1.4 s window that moved +-15% run to run)
     "headline": dict(n=2, strategy="concatenate", hide_final=False, skip=True, faults={}, timeout=30,
-                     batch=16384, baseline=21.071, baseline_ttft_ms=619.6, baseline_source=BASELINE_SOURCE_SAME,
+                     batch=131072, baseline=21.071, baseline_ttft_ms=619.6, baseline_source=BASELINE_SOURCE_SAME,
                      desc="2 mock backends, streaming concatenate, hide_intermediate_think"),
     "aggregate4": dict(n=4, strategy="aggregate", hide_final=False, skip=False, faults={}, timeout=30,
                        baseline=10.09, baseline_ttft_ms=1191.9, baseline_source=BASELINE_SOURCE_SAME,
@@ -349,7 +354,9 @@ def breakdown(m0, m1, elapsed):
         "grid_us_avg": {k: round(d.get(f"qmx_kernel_{k}_us", 0.0) / d["qmx_kernel_grid_ticks"], 1)
                         for k in ("relay", "pickup", "grid_span")} if d.get("qmx_kernel_grid_ticks") else None,
         "tick_route_us_avg": round(1e6 * d.get("qmx_tick_route_seconds_total", 0.0) / ticks, 1) if ticks else None,
-        "gpu_busy_frac": round(d.get("qmx_kernel_kernel_ms", 0.0) / 1000 / elapsed, 4) if elapsed else None,
+        # kernel seconds per wall second, SUMMED over the tick lanes (two lanes with kernels in
+        # flight at once count twice): a lane-occupancy figure, not the GPU's busy fraction
+        "kernel_s_per_s_lane_sum": round(d.get("qmx_kernel_kernel_ms", 0.0) / 1000 / elapsed, 4) if elapsed else None,
         # finalize (K3 strip + K4 join + K5 encode) rides the tick launches: requests folded into
         # them, and launches of its own (always 0 since r2)
         "finalize_items_fused": int(d.get("qmx_kernel_fin_items", 0.0)),
@@ -384,6 +391,30 @@ def breakdown(m0, m1, elapsed):
     }
 
 
+def compact_breakdown(rank: int, bd: dict, row) -> dict:
+    """One rank's row of the JSON line: which process answered, its load and its key timings."""
+    lat = bd.get("latency_us_avg", {})
+    return {"rank": rank, "pid": bd.get("pid"), "requests": int(row[1]), "req_s": round(row[1] / row[0], 1) if row[0] else None,
+            "p50_ttft_ms": round(row[2], 3), "ticks": bd.get("ticks"), "streams_per_tick": bd.get("streams_per_tick"),
+            "tick_kernel_us_avg": bd.get("tick_kernel_us_avg"), "tick_wall_us_avg": bd.get("tick_wall_us_avg"),
+            "engine_wait_us": lat.get("engine_wait"), "proxy_cpu_ms_per_1k_req": bd.get("proxy_cpu_ms_per_1k_req")}
+
+
+def spread_summary(rows) -> dict:
+    """The spread check of every rank, compact: totals plus each rank's own counters."""
+    keys = ("requests", "invalid", "remote_streams", "rccl_rounds", "rccl_final_bytes", "mesh_finals", "delta_mismatch")
+    out = {"ok": all(r.get("ok") for r in rows), "transport": rows[0].get("transport"),
+           "rccl_formed": all(r.get("rccl_formed") for r in rows)}
+    for k in keys:
+        out[k] = int(sum(r.get(k) or 0 for r in rows))
+    lat = [r["p50_latency_ms"] for r in rows if r.get("p50_latency_ms") is not None]
+    out["p50_latency_ms"] = round(statistics.median(lat), 3) if lat else None
+    out["per_rank"] = [{k: r.get(k) for k in ("ok", "pid", "requests", "invalid", "remote_streams", "rccl_rounds",
+                                             "mesh_finals", "delta_mismatch", "p50_latency_ms", "error") if r.get(k) is not None}
+                       for r in rows]
+    return out
+
+
 def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports, dist, n_dev):
     """Outside the timed region, N > 1: expert-parallel placement end to end.  A second proxy
     set on port + 50 runs the headline backends with ``placement: spread`` and the final
@@ -396,6 +427,7 @@ def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports
     from quorum_amd.serve import spawn_workers, wait_healthy
 
     port = args.port + 50
+    admin = args.port + SPREAD_ADMIN_OFF + rank  # this rank's spread proxy alone
     out = {"ok": False}
     procs = []
     ok, err = True, None
@@ -427,42 +459,64 @@ def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports
             expect_spec(spec, sc, False, mock_expected(bin_dir))
             if os.environ.get("QMX_BENCH_SPREAD_FAIL_RANK") == str(rank):  # test hook: one rank fails
                 raise RuntimeError("injected spread-check failure")
+            env["QMX_READY_FILE"] = os.path.join(tmp, "ready_spread")
+            env["QMX_ADMIN_PORT"] = str(admin)
             procs = spawn_workers(cfg, "127.0.0.1", port, 1, engine, device, impl="native",
                                   threads=args.threads, env=env)
-            if not wait_healthy("127.0.0.1", port, 60):
-                raise RuntimeError("spread proxy did not become healthy")
+            for p in procs:
+                p.ready_file = f"{env['QMX_READY_FILE']}.{p.pid}"
+            if not (wait_ready(procs, 60) and wait_healthy("127.0.0.1", admin, 30)):
+                raise RuntimeError(f"spread proxy did not become ready: {[exit_status(p) for p in procs]}")
         except Exception as e:  # noqa: BLE001 - agreed on below, reported in the JSON line
             ok, err = False, repr(e)[:300]
         if agree("spawn"):
             try:
                 t0 = time.time()
-                while True:  # the mesh (and, on GPUs, the RCCL communicator) formed on every rank
-                    m = scrape(port)
-                    if m.get("qmx_exchange_healthy") == 1.0 and (not want_rccl or m.get("qmx_exchange_rccl_active") == 1.0):
+                while True:  # the mesh formed on every rank (and, on GPUs, the RCCL communicator)
+                    m = scrape(admin)
+                    healthy = m.get("qmx_exchange_healthy") == 1.0
+                    rccl = m.get("qmx_exchange_rccl_active") == 1.0
+                    if healthy and (not want_rccl or rccl):
                         break
-                    if time.time() - t0 > 60:
+                    if not healthy and time.time() - t0 > 60:
                         raise RuntimeError(f"exchange did not form: {({k: v for k, v in m.items() if 'exchange' in k})}")
+                    if healthy and time.time() - t0 > 60:
+                        # no communicator: the finals fall back to the mesh (still validated);
+                        # reported, so a node where RCCL never formed is visible in the line
+                        break
                     time.sleep(0.2)
+                out["rccl_formed"] = bool(want_rccl and rccl)
             except Exception as e:  # noqa: BLE001
                 ok, err = False, repr(e)[:300]
         if agree("exchange formation"):
+            st = None
             try:
-                m0 = scrape(port)
+                m0 = scrape(admin)
                 st = loadgen(bin_dir, port, 32, 2048, 2, 60, spec)
-                time.sleep(0.2)
-                m1 = scrape(port)
-                d = {k: m1.get(k, 0.0) - m0.get(k, 0.0) for k in m1 if "exchange" in k or "remote_streams" in k}
-                out.update({"ok": st["invalid"] == 0 and st["errors"] == 0 and st["completed"] == 2048,
-                            "requests": st["completed"], "invalid": st["invalid"],
-                            "p50_ttft_ms": st["ttft_p50_ms"], "p50_latency_ms": st["lat_p50_ms"], "req_s": st["rps"],
-                            "remote_streams": d.get("qmx_remote_streams_total", 0.0),
-                            "rccl_rounds": d.get("qmx_exchange_rounds_total", 0.0),
-                            "rccl_final_bytes": d.get("qmx_exchange_bulk_bytes_total", 0.0),
-                            "mesh_finals": d.get("qmx_exchange_mesh_finals_total", 0.0),
-                            "mesh_messages": d.get("qmx_exchange_messages_total", 0.0),
-                            "epochs": m1.get("qmx_exchange_epochs_total", 0.0)})
             except Exception as e:  # noqa: BLE001
                 ok, err = False, repr(e)[:300]
+            # every rank's load is done before any rank reads its counters: a worker rank
+            # still serves other owners' remote streams after its own load ends
+            agree("load")
+            if st is not None:
+                try:
+                    time.sleep(0.2)
+                    m1 = scrape(admin)
+                    d = {k: m1.get(k, 0.0) - m0.get(k, 0.0) for k in m1
+                         if "exchange" in k or "remote" in k or "spread" in k}
+                    out.update({"ok": st["invalid"] == 0 and st["errors"] == 0 and st["completed"] == 2048,
+                                "requests": st["completed"], "invalid": st["invalid"],
+                                "p50_ttft_ms": st["ttft_p50_ms"], "p50_latency_ms": st["lat_p50_ms"],
+                                "req_s": st["rps"], "pid": procs[0].pid if procs else None,
+                                "remote_streams": d.get("qmx_remote_streams_total", 0.0),
+                                "rccl_rounds": d.get("qmx_exchange_rounds_total", 0.0),
+                                "rccl_final_bytes": d.get("qmx_exchange_bulk_bytes_total", 0.0),
+                                "mesh_finals": d.get("qmx_exchange_mesh_finals_total", 0.0),
+                                "mesh_messages": d.get("qmx_exchange_messages_total", 0.0),
+                                "delta_mismatch": d.get("qmx_spread_delta_mismatch_total", 0.0),
+                                "epochs": m1.get("qmx_exchange_epochs_total", 0.0)})
+                except Exception as e:  # noqa: BLE001
+                    ok, err = False, repr(e)[:300]
     except Exception as e:  # noqa: BLE001 - reported in the JSON line
         ok, err = False, repr(e)[:300]
     finally:
@@ -473,13 +527,56 @@ def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports
     return out
 
 
+def self_launch(n: int) -> int:
+    """``python bench.py --gpus N`` without a launcher: start ``torch.distributed.run
+    --nproc-per-node N`` on this same command line as a CHILD process (never an exec: nothing
+    here has touched the GPU, and the ranks must own their devices), relay its output and
+    exit with its code.  The driver's own torchrun invocation sets WORLD_SIZE and skips this."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        mport = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", os.environ.get("MASTER_PORT", str(mport)),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"bench: --gpus {n}: launching {n} ranks: {' '.join(cmd[1:7])} ...", file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd)
+
+    def fwd(signum, _frame):
+        try:
+            p.send_signal(signum)
+        except OSError:
+            pass
+
+    old = {sg: signal.signal(sg, fwd) for sg in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        return p.wait()
+    finally:
+        for sg, h in old.items():
+            signal.signal(sg, h)
+
+
+def wait_ready(procs, timeout: float) -> bool:
+    """Every proxy process of THIS rank has written its ready file (``QMX_READY_FILE`` +
+    ``.pid``, written once all its io loops listen): readiness of this rank's own workers,
+    not of whichever rank's proxy answers on the shared SO_REUSEPORT port."""
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        if any(p.poll() is not None for p in procs):
+            return False
+        if all(os.path.exists(p.ready_file) for p in procs):
+            return True
+        time.sleep(0.05)
+    return False
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); > 1 without WORLD_SIZE: launches them (torch.distributed.run)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=0,
-                    help="requests per step per rank (0: the scenario's default, 16384 headline / 4096 others)")
+                    help="requests per step per rank (0: the scenario's default, 131072 headline / 4096 others)")
     ap.add_argument("--conns", type=int, default=64, help="concurrent client connections per rank")
     ap.add_argument("--impl", default=os.environ.get("QMX_BENCH_IMPL", "native"),
                     choices=["native", "python", "reference"],
@@ -502,13 +599,20 @@ def main() -> int:
     ap.add_argument("--skip-final", type=int, default=1)
     ap.add_argument("--tile", type=int, default=16384)
     ap.add_argument("--port", type=int, default=int(os.environ.get("QMX_BENCH_PORT", "18000")))
-    ap.add_argument("--timeout", type=float, default=300)
+    ap.add_argument("--timeout", type=float, default=900)
     ap.add_argument("--scenario", default="headline", choices=sorted(SCENARIOS))
     ap.add_argument("--spread-check", type=int, default=1,
                     help="N > 1: after the timed steps, validate spread placement (RCCL finals) end to end")
     ap.add_argument("--placement", default="local", choices=["local", "spread"],
                     help="spread: a session's backend streams run on consecutive ranks (RCCL exchange)")
     args = ap.parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus is not None and args.gpus > 1 and env_world is None:
+        return self_launch(args.gpus)
+    if args.gpus is not None and env_world is not None and int(env_world) != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={env_world}: refusing to measure a different "
+              f"world than the one requested", file=sys.stderr, flush=True)
+        return 2
     sc = SCENARIOS[args.scenario]
     if "conns" in sc and args.conns == 64:  # scenario default unless set explicitly
         args.conns = sc["conns"]
@@ -587,16 +691,31 @@ def main() -> int:
             env.update(exchange_env(rank, world, args.port, nonce[0]))
         mock_procs = list(procs)
         proxy_port = args.port
+        # this rank's own proxy process answers on admin_port (no SO_REUSEPORT): its ready
+        # file says when it listens, and /metrics is scraped there — never through the shared
+        # port, where any rank's proxy may answer
+        admin_port = args.port + ADMIN_OFF + rank
         if args.impl == "reference":
             proxy_port = args.port + rank  # uvicorn binds without SO_REUSEPORT: a port per rank
             proxy_procs = [spawn_reference(args.ref_root, tmp, cfg_path, proxy_port)]
+            admin_port = proxy_port
         else:
+            env["QMX_READY_FILE"] = os.path.join(tmp, "ready")
+            env["QMX_ADMIN_PORT"] = str(admin_port)
             proxy_procs = spawn_workers(cfg_path, "127.0.0.1", args.port, args.workers, engine,
                                         device, impl=args.impl, threads=args.threads, env=env)
+            for p in proxy_procs:
+                p.ready_file = f"{env['QMX_READY_FILE']}.{p.pid}"
         procs += proxy_procs
         _trace("workers spawned")
-        if not wait_healthy("127.0.0.1", proxy_port, 180):
-            raise RuntimeError(f"proxy did not become healthy: {[exit_status(p) for p in proxy_procs]}")
+        if args.impl == "reference":
+            up = wait_healthy("127.0.0.1", proxy_port, 180)
+        else:
+            up = wait_ready(proxy_procs, 180)
+            if up and args.impl == "native":
+                up = wait_healthy("127.0.0.1", admin_port, 30)
+        if not up:
+            raise RuntimeError(f"proxy did not become ready: {[exit_status(p) for p in proxy_procs]}")
         xchg_kind = os.environ.get("QMX_XCHG", "rccl" if engine == "hip" else "tcp")
         _trace("healthy")
         if dist is not None:
@@ -620,7 +739,7 @@ def main() -> int:
             _barrier(dist, coll_cuda)
         if use_cuda:
             torch.cuda.synchronize()
-        m0 = scrape(proxy_port) if args.impl == "native" else {}
+        m0 = scrape(admin_port) if args.impl == "native" else {}
         c0 = cpu_snapshot(mock_procs, proxy_procs)
         t0 = time.perf_counter()
         stats = loadgen(bin_dir, proxy_port, args.conns, args.steps * args.batch, args.lg_threads, args.timeout,
@@ -631,7 +750,8 @@ def main() -> int:
             _barrier(dist, coll_cuda)
         elapsed = time.perf_counter() - t0
         c1 = cpu_snapshot(mock_procs, proxy_procs)
-        bd = breakdown(m0, scrape(proxy_port), elapsed) if args.impl == "native" else {}
+        bd = breakdown(m0, scrape(admin_port), elapsed) if args.impl == "native" else {}
+        bd["pid"] = proxy_procs[0].pid
         bd.update(cpu_breakdown(c0, c1, stats["completed"], elapsed))
         dead = casualties()
         if dead and not dead_warm:
@@ -661,6 +781,14 @@ def main() -> int:
         else:
             rows = [local]
         ok = all(r[11] == 0 for r in rows)
+        headline_ok = ok
+        if spread is not None:  # a failed spread check fails the run (its responses are validated too)
+            ok = ok and all(r.get("ok") for r in spread)
+        # per-rank breakdowns, each scraped from that rank's own proxy (admin port)
+        bd_rows = [bd]
+        if dist is not None:
+            bd_rows = [None] * world
+            dist.all_gather_object(bd_rows, bd)
         if rank == 0:
             max_el = max(r[0] for r in rows)
             total = sum(r[1] for r in rows)
@@ -694,7 +822,8 @@ def main() -> int:
                            "impl": args.impl, "engine": engine if args.impl != "reference" else "reference",
                            "conns_per_rank": args.conns,
                            "io_threads_per_rank": args.threads, "cpu_pinning": pinning,
-                           "gpu_links": {k: v for k, v in link_summary().items() if k != "links_per_gpu"}},
+                           "gpu_links": ({k: v for k, v in link_summary().items() if k != "links_per_gpu"}
+                                         if world > 1 else None)},
                 "p50_ttft_ms": round(p50, 3),
                 "p99_ttft_ms": round(max(r[3] for r in rows), 3),
                 "p50_ttfb_ms": round(statistics.median(r[5] for r in rows), 3),
@@ -706,15 +835,18 @@ def main() -> int:
                 "no_content": int(sum(r[9] for r in rows)),
                 "processes_exited": int(sum(r[7] for r in rows)),
                 "valid": ok,
+                "headline_valid": headline_ok,
                 "baseline_p50_ttft_ms": sc.get("baseline_ttft_ms"),
-                # one rank proxy process counters over the timed region (SURVEY §5.1 time breakdown;
-                # with N>1 the shared port answers from any rank)
+                # rank 0's proxy counters over the timed region (SURVEY §5.1 time breakdown),
+                # scraped from its own admin port
                 "breakdown_one_rank": bd,
             }
+            if world > 1:  # every rank's own proxy: distinct pids, its own counters
+                res["breakdown_per_rank"] = [compact_breakdown(r, b, row) for r, (b, row) in enumerate(zip(bd_rows, rows))]
             if dead or dead_warm:
                 res["exited"] = dead or dead_warm
-            if spread is not None:  # outside the timed region; per rank
-                res["spread_check"] = {"ok": all(r.get("ok") for r in spread), "per_rank": spread}
+            if spread is not None:  # outside the timed region; per rank, each from its own proxy
+                res["spread_check"] = spread_summary(spread)
             print(json.dumps(res), flush=True)
     finally:
         _kill(procs)

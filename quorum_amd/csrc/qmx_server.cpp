@@ -823,6 +823,8 @@ class Loop {
     (void)w;
   }
   ~Loop() {
+    for (int fd : {lfd_, afd_})
+      if (fd >= 0) close(fd);
     for (auto& kv : idle_ssl_) SSL_free(kv.second);  // before the run's SSL_CTX goes away
     for (auto& kv : ups_)
       if (kv.second->ssl) SSL_free(kv.second->ssl);
@@ -836,6 +838,7 @@ class Loop {
       FILE* f = fopen(cfg_.ready_file.c_str(), "w");  // supervisor: this generation is serving
       if (f) {
         fprintf(f, "%d\n", (int)getpid());
+        if (cfg_.admin_port > 0) fprintf(f, "admin_port %d\n", cfg_.admin_port);
         fclose(f);
       }
     }
@@ -937,6 +940,16 @@ class Loop {
     if (bind(lfd_, (sockaddr*)&a, sizeof(a)) != 0) throw std::runtime_error("bind failed: " + std::string(strerror(errno)));
     listen(lfd_, 4096);
     add(lfd_, EPOLLIN, tag_listen());
+    if (idx_ == 0 && cfg_.admin_port > 0) {  // this process alone (per-rank /metrics, /health)
+      afd_ = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK, 0);
+      setsockopt(afd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+      sockaddr_in b = a;
+      b.sin_port = htons(cfg_.admin_port);
+      if (bind(afd_, (sockaddr*)&b, sizeof(b)) != 0)
+        throw std::runtime_error("admin port bind failed: " + std::string(strerror(errno)));
+      listen(afd_, 256);
+      add(afd_, EPOLLIN, tag(6, 0));
+    }
     evfd_ = eventfd(0, EFD_NONBLOCK);
     add(evfd_, EPOLLIN, tag_event());
     add(xfd_, EPOLLIN, tag(5, 0));
@@ -969,7 +982,8 @@ class Loop {
   void dispatch(const epoll_event& e) {
     int kind = (int)(e.data.u64 >> 32);
     int fd = (int)(uint32_t)e.data.u64;
-    if (kind == 1) return on_accept();
+    if (kind == 1) return on_accept(lfd_);
+    if (kind == 6) return on_accept(afd_);
     if (kind == 2) return on_results();
     if (kind == 5) return on_xmsgs();
     if (kind == 3) {
@@ -1116,12 +1130,13 @@ class Loop {
     if (!draining_) {
       draining_ = true;
       drain_deadline_ = t + cfg_.drain_s;
-      if (lfd_ >= 0) {
-        on_accept();  // connections already queued on this listener are served, not reset
-        epoll_ctl(ep_, EPOLL_CTL_DEL, lfd_, nullptr);
+      for (int* l : {&lfd_, &afd_}) {
+        if (*l < 0) continue;
+        on_accept(*l);  // connections already queued on this listener are served, not reset
+        epoll_ctl(ep_, EPOLL_CTL_DEL, *l, nullptr);
         cnt(SC_EPOLL_CTL);
-        close(lfd_);
-        lfd_ = -1;
+        close(*l);
+        *l = -1;
       }
     }
     for (auto& kv : clients_) {
@@ -1137,9 +1152,9 @@ class Loop {
   }
 
   // ---------------------------------------------------------------- clients
-  void on_accept() {
+  void on_accept(int lfd) {
     while (true) {
-      int fd = accept4(lfd_, nullptr, nullptr, SOCK_NONBLOCK);
+      int fd = accept4(lfd, nullptr, nullptr, SOCK_NONBLOCK);
       if (fd < 0) break;
       int one = 1;
       setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
@@ -2666,7 +2681,7 @@ class Loop {
 
   const ServerCfg& cfg_;
   int idx_;
-  int ep_ = -1, lfd_ = -1, evfd_ = -1;
+  int ep_ = -1, lfd_ = -1, afd_ = -1, evfd_ = -1;
   std::unique_ptr<HostEngine> eng_;  // CPU engine (no GPU hub)
   std::unique_ptr<Verifier> ver_;
   GpuHub* hub_ = nullptr;            // shared HIP engine

@@ -71,6 +71,9 @@ struct ServerCfg {
   // every io loop is listening (supervisor rolling reloads)
   double drain_s = 10.0;
   std::string ready_file;
+  // admin_port > 0: io loop 0 also listens here, without SO_REUSEPORT — a port that reaches
+  // exactly this process (/metrics and /health of ONE rank; bench.py scrapes it per rank)
+  int admin_port = 0;
   bool verify = false;  // shadow CPU oracle engine compares every stream + finalize result
   // https upstreams: CA bundle (httpx default: certifi) and peer verification
   std::string ca_file;

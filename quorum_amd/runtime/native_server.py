@@ -67,7 +67,10 @@ def native_config(cfg: Dict[str, Any], host: str, port: int, engine: str, device
         "drain_s": float(rt.drain_timeout), "verify": bool(rt.verify),
         "shared_engine": -1 if rt.shared_engine in ("auto", None) else int(bool(rt.shared_engine)),
         "tick_lanes": int(rt.tick_lanes),
-        "ca_file": _ca_bundle(), "tls_verify": os.environ.get("QMX_TLS_VERIFY", "1") not in ("0", "false"), "ready_file": (os.environ["QMX_READY_FILE"] + f".{os.getpid()}") if os.environ.get("QMX_READY_FILE") else "",
+        "ca_file": _ca_bundle(), "tls_verify": os.environ.get("QMX_TLS_VERIFY", "1") not in ("0", "false"),
+        "ready_file": (os.environ["QMX_READY_FILE"] + f".{os.getpid()}") if os.environ.get("QMX_READY_FILE") else "",
+        # QMX_ADMIN_PORT: this process's own /metrics + /health port (not SO_REUSEPORT-shared)
+        "admin_port": int(os.environ.get("QMX_ADMIN_PORT", "0")),
         **cluster_config(rt, port, engine),
         **doc_routes(cfg),
     }

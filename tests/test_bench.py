@@ -99,12 +99,52 @@ def test_bench_two_ranks_spread_check_failure_is_agreed(tmp_path):
                         "--gpus", "2", "--steps", "1", "--warmup", "0", "--batch", "64", "--threads", "2",
                         "--conns", "8", "--port", str(port)],
                        cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    # the headline responses were fine, but a failed spread check fails the run
+    assert r.returncode == 1, (r.stdout[-2000:], r.stderr[-3000:])
     res = _check(_json_lines(r.stdout)[0], 2, 1, 0)
-    assert res["valid"] is True
+    assert res["headline_valid"] is True and res["valid"] is False
     sc = res["spread_check"]
     assert sc["ok"] is False
     assert "injected" in sc["per_rank"][1]["error"] and "another rank failed" in sc["per_rank"][0]["error"]
+
+
+@pytest.mark.slow
+def test_bench_gpus_flag_self_launches_ranks(tmp_path):
+    """``python bench.py --gpus 4`` with no launcher starts its own 4 ranks (a child
+    torch.distributed.run): one JSON line, n_gpus 4, one breakdown row per rank scraped from
+    that rank's own proxy (4 distinct pids), and a spread check whose rows carry each rank's
+    own counters."""
+    port = _free_port()
+    env = dict(_env(), QMX_BENCH_NDEV="1")  # rehearsal: the ranks share (at most) one GPU
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "4", "--steps", "2", "--warmup", "1", "--batch", "128",
+                        "--threads", "2", "--conns", "8", "--port", str(port)],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    res = _check(lines[0], 4, 2, 1)
+    assert res["valid"] is True and res["config"]["global_batch"] == 512
+    rows = res["breakdown_per_rank"]
+    assert [x["rank"] for x in rows] == [0, 1, 2, 3]
+    assert len({x["pid"] for x in rows}) == 4 and all(x["requests"] == 256 for x in rows)
+    assert rows[0]["pid"] == res["breakdown_one_rank"]["pid"]
+    sc = res["spread_check"]
+    assert sc["ok"] is True and sc["requests"] == 4 * 2048 and sc["delta_mismatch"] == 0
+    assert len({x["pid"] for x in sc["per_rank"]}) == 4
+    # every session has one remote stream, run by the next rank: each rank's own counter
+    # is its own share, and the shares add up to every session once
+    assert sum(x["remote_streams"] for x in sc["per_rank"]) == 4 * 2048
+    assert all(0 < x["remote_streams"] < 4 * 2048 for x in sc["per_rank"])
+
+
+def test_bench_refuses_world_mismatch(tmp_path):
+    """Under a launcher, --gpus must name the launcher's world: a mismatch is refused
+    before anything starts (exit 2), never measured as some other world."""
+    env = dict(_env(), WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "4", "--steps", "1"], cwd=str(tmp_path), env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
 
 
 def test_pin_rank_numa_plan(monkeypatch):
