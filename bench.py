@@ -282,6 +282,10 @@ def spawn_reference(ref_root: str, tmp: str, cfg_path: str, port: int) -> subpro
                             start_new_session=True)
 
 
+# labelled series bench.py reads (histogram buckets are skipped)
+LABELED = ("qmx_syscalls_total", "qmx_spread_remote_ends_total", "qmx_upstream_failures_by_class_total")
+
+
 def scrape(port):
     """Sum the proxy's /metrics counters (engine / kernel / tick / exchange) — one process
     per rank, io loops already aggregated inside it."""
@@ -293,7 +297,7 @@ def scrape(port):
     except Exception:  # noqa: BLE001
         return out
     for ln in txt.splitlines():
-        if not ln or ln[0] == "#" or ("{" in ln and not ln.startswith("qmx_syscalls_total")):
+        if not ln or ln[0] == "#" or ("{" in ln and not ln.startswith(LABELED)):
             continue
         k, _, v = ln.rpartition(" ")
         try:
@@ -402,15 +406,22 @@ def compact_breakdown(rank: int, bd: dict, row) -> dict:
 
 def spread_summary(rows) -> dict:
     """The spread check of every rank, compact: totals plus each rank's own counters."""
-    keys = ("requests", "invalid", "remote_streams", "rccl_rounds", "rccl_final_bytes", "mesh_finals", "delta_mismatch")
+    keys = ("requests", "invalid", "remote_streams", "rccl_rounds", "rccl_final_bytes", "mesh_finals", "delta_mismatch",
+            "worker_nodata", "peer_downs")
     out = {"ok": all(r.get("ok") for r in rows), "transport": rows[0].get("transport"),
            "rccl_formed": all(r.get("rccl_formed") for r in rows)}
     for k in keys:
         out[k] = int(sum(r.get(k) or 0 for r in rows))
     lat = [r["p50_latency_ms"] for r in rows if r.get("p50_latency_ms") is not None]
     out["p50_latency_ms"] = round(statistics.median(lat), 3) if lat else None
+    ends = {}
+    for r in rows:
+        for k, v in (r.get("remote_ends") or {}).items():
+            ends[k] = ends.get(k, 0) + int(v)
+    out["remote_ends"] = ends
     out["per_rank"] = [{k: r.get(k) for k in ("ok", "pid", "requests", "invalid", "remote_streams", "rccl_rounds",
-                                             "mesh_finals", "delta_mismatch", "p50_latency_ms", "error") if r.get(k) is not None}
+                                             "mesh_finals", "delta_mismatch", "worker_nodata", "remote_ends",
+                                             "up_failures", "p50_latency_ms", "error") if r.get(k)}
                        for r in rows]
     return out
 
@@ -503,7 +514,7 @@ def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports
                     time.sleep(0.2)
                     m1 = scrape(admin)
                     d = {k: m1.get(k, 0.0) - m0.get(k, 0.0) for k in m1
-                         if "exchange" in k or "remote" in k or "spread" in k}
+                         if "exchange" in k or "remote" in k or "spread" in k or "failures" in k}
                     out.update({"ok": st["invalid"] == 0 and st["errors"] == 0 and st["completed"] == 2048,
                                 "requests": st["completed"], "invalid": st["invalid"],
                                 "p50_ttft_ms": st["ttft_p50_ms"], "p50_latency_ms": st["lat_p50_ms"],
@@ -514,6 +525,14 @@ def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports
                                 "mesh_finals": d.get("qmx_exchange_mesh_finals_total", 0.0),
                                 "mesh_messages": d.get("qmx_exchange_messages_total", 0.0),
                                 "delta_mismatch": d.get("qmx_spread_delta_mismatch_total", 0.0),
+                                "worker_nodata": d.get("qmx_spread_worker_nodata_total", 0.0),
+                                "peer_downs": d.get("qmx_exchange_peer_downs_total", 0.0),
+                                # how this rank's remote streams ended (owner side), and its
+                                # upstream failures by class (worker side included)
+                                "remote_ends": {k.split('"')[1]: v for k, v in d.items()
+                                                if k.startswith("qmx_spread_remote_ends_total") and v},
+                                "up_failures": {k.split('"')[1]: v for k, v in d.items()
+                                                if k.startswith("qmx_upstream_failures_by_class_total") and v},
                                 "epochs": m1.get("qmx_exchange_epochs_total", 0.0)})
                 except Exception as e:  # noqa: BLE001
                     ok, err = False, repr(e)[:300]

@@ -178,8 +178,12 @@ struct Exchange::Impl {
     int one = 1;
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
   }
-  void mark_down(int r) {
+  void mark_down(int r, const char* why) {
     Peer& p = peers[r];
+    if (p.up) {
+      X->downs_++;
+      fprintf(stderr, "qmx exchange (rank %d): peer %d down (%s, errno %d)\n", X->o_.rank, r, why, errno);
+    }
     if (p.fd >= 0) {
       epoll_ctl(ep, EPOLL_CTL_DEL, p.fd, nullptr);
       close(p.fd);
@@ -269,7 +273,7 @@ struct Exchange::Impl {
         }
         return;
       }
-      return mark_down(r);
+      return mark_down(r, "send failed");
     }
     if (p.fd >= 0) {
       p.out.clear();
@@ -647,7 +651,7 @@ void Exchange::mesh_loop() {
             dead = true;
           } else {
             Impl::Peer& p = I.peers[pr];
-            if (p.fd >= 0) I.mark_down(pr);  // a re-joined peer replaces its dead connection
+            if (p.fd >= 0) I.mark_down(pr, "replaced by a new connection");  // a re-joined peer replaces its dead connection
             p.fd = fd;
             p.in = in.substr(sizeof(WireHdr) + h.len);
             epoll_event e{};
@@ -678,7 +682,7 @@ void Exchange::mesh_loop() {
         socklen_t el = sizeof(err);
         getsockopt(p.fd, SOL_SOCKET, SO_ERROR, &err, &el);
         if (err != 0) {
-          I.mark_down(r);
+          I.mark_down(r, "connect failed");
           continue;
         }
         p.dialing = false;
@@ -698,7 +702,7 @@ void Exchange::mesh_loop() {
           break;
         }
         if (!p.in.empty()) I.on_frames(r, p.in);
-        if (dead) I.mark_down(r);
+        if (dead) I.mark_down(r, "connection closed");
       }
     }
     I.take_posted();

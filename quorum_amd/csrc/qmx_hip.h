@@ -196,6 +196,7 @@ struct TickLane {
   bool p_running = false;
   uint32_t p_gen = 0;
   double p_last_post = 0;  // steady clock, seconds
+  uint64_t p_revivals = 0;  // grids relaunched for a tick posted after they idled out
   uint64_t p_launches = 0, p_ticks = 0;
 };
 

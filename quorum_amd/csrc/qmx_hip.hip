@@ -1956,6 +1956,10 @@ static void put(char* dst, int cap, int* len, const std::string& s) {
   *len = (int)s.size();
 }
 
+static double steady_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 // Wait for a lane's stream without pinning a core: the io loops share the CPU with the tick
 // threads.  A blocking-sync event sleeps on the completion interrupt: measured on MI355X
 // (tools/probes/launch_bench.hip) launch+wait = 11 us, vs 18 us spinning
@@ -1993,9 +1997,31 @@ void HipEngine::wait_results(TickLane& L, int n, int m, uint32_t seq, const Work
     return i == n + m;
   };
   int i = 0;
+  bool revived = false;
   nap(0.6 * L.ema_us - 6.0 - std::chrono::duration<double, std::micro>(HC::now() - t0).count());
   while (!done(i)) {
     const double el = std::chrono::duration<double, std::micro>(HC::now() - t0).count();
+    // the persistent grid idled out between ensure_persistent() and this tick's doorbell (the
+    // lane thread was descheduled for longer than the margin): it reported an idle exit for
+    // its generation and never relayed the tick.  Relaunch it from just before this tick's
+    // sequence number — the doorbell still holds the descriptor — instead of losing the tick.
+    if (L.p_running && !revived && el > 2.0 * L.ema_us + 500.0) {
+      const uint32_t ex = __atomic_load_n(&L.h_door->exits, __ATOMIC_ACQUIRE);
+      const uint32_t rl = __atomic_load_n(&L.h_door->relayed, __ATOMIC_ACQUIRE);
+      if ((ex >> 16) == 1 && (ex & 0xffffu) == (L.p_gen & 0xffffu) && rl != seq) {
+        uint32_t seq0 = seq - 1;
+        if (seq0 == 0) seq0 = (uint32_t)-1;  // (0 never names a tick)
+        HIP_CHECK(hipStreamSynchronize(L.stream));  // the idle grid has left
+        hipLaunchKernelGGL(qmx_tick_persistent, dim3(p_grid_), dim3(BS), 0, L.stream, L.h_door, L.d_ctl, d_state_,
+                           d_content_, seq0, ++L.p_gen, (uint32_t)p_idle_ms_ * 100000u);
+        HIP_CHECK(hipGetLastError());
+        L.p_last_post = steady_s();
+        ++L.p_launches;
+        ++L.p_revivals;
+        revived = true;
+        continue;
+      }
+    }
     // a persistent grid is only stopped to surface a fault: a tick it has not reached yet
     // (first launch loading the code object, a long finalize) would be lost to the stop
     if (el > (L.p_running ? 1e6 : 4.0 * L.ema_us + 2000.0)) {
@@ -2185,10 +2211,6 @@ void HipEngine::set_persistent(bool on) {
 uint32_t HipEngine::next_seq(TickLane& L) {
   if (++L.seq == 0) ++L.seq;  // 0 never names a tick (fresh result records hold it)
   return L.seq;
-}
-
-static double steady_s() {
-  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 // The lane's grid is running and will see the next post: launch it when it is not running,
@@ -2886,6 +2908,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     TickLane& L = *Lp;
     std::lock_guard<std::mutex> lg(L.mu);
     m["launches"] += (double)L.launches;
+    m["persistent_revivals"] += (double)L.p_revivals;
     m["persistent_grids"] += (double)L.p_launches;  // persistent mode: grid launches (ticks ride doorbells)
     m["persistent_ticks"] += (double)L.p_ticks;
     m["items"] += (double)L.items;

@@ -48,7 +48,14 @@ std::atomic<uint64_t> c_requests{0}, c_stream{0}, c_nonstream{0}, c_errors{0}, c
     c_apply_ns{0}, c_applies{0};  // io loop: a tick's results routed -> applied (sent to clients)
 // failures by class
 std::atomic<uint64_t> c_fail_connect{0}, c_fail_timeout{0}, c_fail_status{0}, c_fail_disconnect{0},
-    c_fail_protocol{0}, c_stream_aborts{0};
+    c_fail_protocol{0}, c_stream_aborts{0},
+    c_host_path_opens{0};  // HIP engine: streams opened past max_slots (host path)
+// spread placement accounting (owner side unless noted): how every remote stream ended, and
+// the delta invariant — the owner must have received exactly the deltas the worker sent
+// before it applies the stream's final (X_BULK / X_FINAL carry the worker's count in b)
+std::atomic<uint64_t> c_sp_failed{0}, c_sp_aborted{0}, c_sp_empty{0}, c_sp_text{0}, c_sp_down{0},
+    c_sp_delta_mismatch{0}, c_sp_nodata{0} /* worker: content but no delta sent */;
+std::atomic<int> g_sp_logs{0};  // rate limit: the first 20 anomalies are logged with their state
 
 // Prometheus histogram with lock-free buckets (seconds)
 struct Hist {
@@ -576,12 +583,15 @@ class GpuHub {
     for (int i = 0; i < lanes_; ++i) th_.emplace_back([this, i] { run(i); });
   }
   void attach(int loop, Sink s) { sinks_[loop] = std::move(s); }
-  // called by io loop `loop` only: slots come from that loop's reserve, refilled 32 at a
-  // time under one engine lock + one owner-map lock (not two locks per open)
+  // called by io loop `loop` only: slots come from that loop's reserve, refilled a chunk at
+  // a time under one engine lock + one owner-map lock (not two locks per open).  The chunk is
+  // at most max_slots / (4 x loops): reserves parked in idle loops can never push the other
+  // loops' opens past max_slots (the device state table) onto the slow host path.
   int open(int loop, int index, bool f, bool e, uint32_t* gen, bool verify = true) {
     std::vector<int>& pool = pools_[loop];
     if (pool.empty()) {
-      eng_->reserve(32, pool);
+      const int chunk = std::max(1, std::min(32, cfg_.max_slots / (4 * (int)pools_.size())));
+      eng_->reserve(chunk, pool);
       std::lock_guard<std::mutex> g(omu_);
       for (int slot : pool) {
         if ((int)owner_.size() <= slot) owner_.resize(slot + 1024, -1);
@@ -590,6 +600,7 @@ class GpuHub {
     }
     const int slot = pool.back();
     pool.pop_back();
+    if (cfg_.engine == "hip" && slot >= cfg_.max_slots) c_host_path_opens++;  // beyond HBM slot state
     eng_->open_reserved(slot, index, f, e, gen);
     if (ver_ && verify) ver_->open(slot, *gen, index, f, e);
     return slot;
@@ -632,7 +643,20 @@ class GpuHub {
   }
 
  private:
+  // A tick lane that throws (a device fault surfaced by a synchronise, output arenas never
+  // released, a lost tick) cannot know which of its streams' bytes were consumed: the process
+  // exits with a message and a distinct code (the supervisor restarts it; clients see their
+  // connections close) instead of dying in std::terminate.
   void run(int lane) {
+    try {
+      run_lane(lane);
+    } catch (const std::exception& e) {
+      fprintf(stderr, "qmx: tick lane %d failed: %s — exiting\n", lane, e.what());
+      fflush(stderr);
+      _exit(70);
+    }
+  }
+  void run_lane(int lane) {
     prof_thread();
     crash_thread();
     if (cfg_.engine == "hip") hipSetDevice(cfg_.device);
@@ -1035,13 +1059,17 @@ class Loop {
       }
       apply(rb);
     }
+    q.clear();  // now, not at the next call: an idle loop must not hold the batches (or their views)
   }
   void apply(ResultBatch& rb) {
     for (auto& r : rb.r) {
       auto it = slot_owner_.find(r.slot);
       // a result of an earlier session on this slot (ended while its tick was in flight; the
       // slot was freed and re-opened before this batch was applied) is dropped
-      if (it == slot_owner_.end() || it->second.gen != r.gen) continue;
+      if (it == slot_owner_.end() || it->second.gen != r.gen) {
+        r.hold = ViewRef();  // dropped: its bytes must not keep the lane's output arena pinned
+        continue;
+      }
       Session* s = it->second.s;
       int bi = it->second.bi;
       if (fault_drop_every_ > 0 && !r.empty() && ++fault_n_ % fault_drop_every_ == 0)
@@ -1934,7 +1962,7 @@ class Loop {
     if (b.state != 0) return;
     if (s->kind == K_REMOTE) {
       b.state = 2;
-      post_owner(s, X_FINAL, XF_FAILED, status, have_result ? error_message(b) : msg);
+      post_owner(s, X_FINAL, XF_FAILED, status, have_result ? error_message(b) : msg, s->data_sent);
       return end_session(s);
     }
     if (!have_result) {
@@ -2066,8 +2094,17 @@ class Loop {
     if (s->kind == K_REMOTE) {  // worker: ship the stream's final text to the owner
       const BState& b = s->bs[0];
       const size_t len = b.aborted || cfg_.skip_final ? 0 : eng().content_size(b.slot);
+      if (s->emit && !b.aborted && s->data_sent == 0 && eng().content_size(b.slot) > 0) {
+        // content reached the engine but not one delta left for the owner: an emitting
+        // stream's every non-empty filtered delta is an event (oai_proxy.py:629-652)
+        c_sp_nodata++;
+        if (g_sp_logs.fetch_add(1) < 20)
+          fprintf(stderr, "qmx spread (rank %d loop %d): worker stream slot %d has %zu content bytes but sent no delta "
+                  "(skey %llx bi %d filter %d)\n", cfg_.rank, idx_, b.slot, eng().content_size(b.slot),
+                  (unsigned long long)s->owner_skey, s->shadow_bi, (int)s->filter);
+      }
       if (len == 0) {
-        post_owner(s, X_FINAL, b.aborted ? XF_ABORTED : 0, 0, std::string());
+        post_owner(s, X_FINAL, b.aborted ? XF_ABORTED : 0, 0, std::string(), s->data_sent);
         return end_session(s);
       }
       // HBM content slot → the owner's shadow slot (RCCL p2p round), or its bytes over the
@@ -2098,7 +2135,7 @@ class Loop {
     fin_owner_[s->fin_id] = {s, -1};
     kick();
   }
-  void post_owner(Session* s, uint8_t type, uint8_t flags, int a, const std::string& payload) {
+  void post_owner(Session* s, uint8_t type, uint8_t flags, int a, const std::string& payload, int b = 0) {
     if (!xch_) return;
     XMsg m;
     m.type = type;
@@ -2110,8 +2147,20 @@ class Loop {
     m.bi = s->shadow_bi;
     m.skey = s->owner_skey;
     m.a = a;
+    m.b = b;
     m.payload = payload;
     xch_->post(std::move(m));
+  }
+  // owner: a remote stream ends with `sent` deltas announced by its worker; anything else
+  // than the count received means deltas were lost or are still missing
+  bool delta_check(Session* s, int bi, int sent, const char* how) {
+    const BState& b = s->bs[bi];
+    if (b.rx_data == sent) return true;
+    c_sp_delta_mismatch++;
+    if (g_sp_logs.fetch_add(1) < 20)
+      fprintf(stderr, "qmx spread (rank %d loop %d): remote stream %d of session %llx (rank %d) ended by %s after %d "
+              "of its %d deltas\n", cfg_.rank, idx_, bi, (unsigned long long)s->skey, b.remote, how, b.rx_data, sent);
+    return false;
   }
   void on_xmsgs() {
     uint64_t v;
@@ -2136,8 +2185,10 @@ class Loop {
           if (sessions_.count(s) && (m.a < 0 || s->owner_rank == m.a) && !s->bulk_pending) end_session(s);
         for (Session* s : owners) {
           for (int i = 0; i < (int)s->bs.size() && sessions_.count(s); ++i)
-            if (s->bs[i].remote >= 0 && (m.a < 0 || s->bs[i].remote == m.a) && s->bs[i].state == 0)
+            if (s->bs[i].remote >= 0 && (m.a < 0 || s->bs[i].remote == m.a) && s->bs[i].state == 0) {
+              c_sp_down++;
               fail_backend(s, i, 500, "rank exchange failed", "proxy_error");
+            }
         }
         continue;
       }
@@ -2198,10 +2249,17 @@ class Loop {
       }
       if (m.type == X_FINAL) {
         if (b.state != 0) continue;
+        delta_check(s, m.bi, m.b, (m.flags & XF_FAILED) ? "failure" : (m.flags & XF_ABORTED) ? "abort" : "empty final");
         if (m.flags & XF_FAILED) {
+          c_sp_failed++;
+          if (g_sp_logs.fetch_add(1) < 20)
+            fprintf(stderr, "qmx spread (rank %d loop %d): remote stream %d of session %llx failed on rank %d: %d %s\n",
+                    cfg_.rank, idx_, m.bi, (unsigned long long)s->skey, m.src_rank, m.a, m.payload.substr(0, 200).c_str());
           fail_backend(s, m.bi, m.a, m.payload, "proxy_error");
           continue;
         }
+        if (m.flags & XF_ABORTED) c_sp_aborted++;
+        else c_sp_empty++;
         b.state = 1;
         b.aborted = (m.flags & XF_ABORTED) != 0;
         s->finished++;
@@ -2213,6 +2271,8 @@ class Loop {
   void remote_final(Session* s, int bi, XMsg& m) {
     BState& b = s->bs[bi];
     if (b.state != 0) return;
+    delta_check(s, bi, m.b, "final text");
+    c_sp_text++;
     // over the mesh the bytes are in the payload; an RCCL round already wrote them to HBM
     // (a final text is never empty: an empty one travels as X_FINAL)
     const bool bytes = !m.payload.empty();
@@ -2633,12 +2693,19 @@ class Loop {
     put("qmx_apply_wait_seconds_total", (double)c_apply_ns.load() * 1e-9);
     put("qmx_applies_total", (double)c_applies.load());
     put("qmx_remote_streams_total", (double)c_remote_streams.load());
+    for (auto& kv : {std::make_pair("failed", &c_sp_failed), std::make_pair("aborted", &c_sp_aborted),
+                     std::make_pair("empty", &c_sp_empty), std::make_pair("text", &c_sp_text),
+                     std::make_pair("peer_down", &c_sp_down)})
+      m += std::string("qmx_spread_remote_ends_total{how=\"") + kv.first + "\"} " + std::to_string(kv.second->load()) + "\n";
+    put("qmx_spread_delta_mismatch_total", (double)c_sp_delta_mismatch.load());
+    put("qmx_spread_worker_nodata_total", (double)c_sp_nodata.load());
     m += "qmx_upstream_failures_by_class_total{class=\"connect\"} " + std::to_string(c_fail_connect.load()) + "\n";
     m += "qmx_upstream_failures_by_class_total{class=\"timeout\"} " + std::to_string(c_fail_timeout.load()) + "\n";
     m += "qmx_upstream_failures_by_class_total{class=\"http_status\"} " + std::to_string(c_fail_status.load()) + "\n";
     m += "qmx_upstream_failures_by_class_total{class=\"disconnect\"} " + std::to_string(c_fail_disconnect.load()) + "\n";
     m += "qmx_upstream_failures_by_class_total{class=\"protocol\"} " + std::to_string(c_fail_protocol.load()) + "\n";
     put("qmx_stream_aborts_total", (double)c_stream_aborts.load());
+    put("qmx_host_path_opens_total", (double)c_host_path_opens.load());
     put("qmx_verify_checked_total", (double)c_verify_checked.load());
     put("qmx_verify_mismatches_total", (double)c_verify_mismatch.load());
     h_ttft.render(m, "qmx_ttft_seconds");
@@ -2654,6 +2721,7 @@ class Loop {
       put("qmx_exchange_mesh_finals_total", (double)xch_->mesh_bulk());  // final texts over the mesh
       put("qmx_exchange_epochs_total", (double)xch_->epochs());
       put("qmx_exchange_rejoins_total", (double)xch_->rejoins());
+      put("qmx_exchange_peer_downs_total", (double)xch_->downs());
       put("qmx_exchange_busy_us_total", xch_->busy_us());
       put("qmx_exchange_healthy", xch_->healthy() ? 1.0 : 0.0);
       put("qmx_exchange_rccl_active", xch_->rccl_active() ? 1.0 : 0.0);

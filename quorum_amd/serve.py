@@ -113,7 +113,11 @@ class Supervisor:
     * SIGTERM / SIGINT — drain and stop every worker, then exit.
     * A worker of the current generation that dies unexpectedly is restarted (the
       surviving workers / ranks keep serving meanwhile) with exponential backoff.
-    Reference counterpart: none (uvicorn --reload restarts the process, Makefile:4).
+    * ``runtime.watch_config`` / ``--watch-config``: the config file is polled (mtime, size,
+      then content hash) and a change triggers the same rolling reload as SIGHUP.  A file
+      that fails validation is reported once and not retried until it changes again.
+    Reference counterpart: ``uvicorn --reload --reload-include "*.yaml"`` (Makefile:4), which
+    restarts the single process and drops its in-flight requests.
     """
 
     def __init__(self, args, config: str):
@@ -130,6 +134,53 @@ class Supervisor:
         self.restarts = 0
         self.backoff = 0.5
         self.active = config  # config the current generation runs (restarts reuse it)
+        self.watch_interval = 1.0
+        self.watch = self._runtime_watch() or bool(getattr(args, "watch_config", False))
+        self.reloads = 0
+        self._stamp = self._file_stamp()
+        self._next_watch = 0.0
+
+    def _runtime_watch(self) -> bool:
+        try:
+            import yaml
+
+            from .utils.config import RuntimeConfig
+
+            with open(self.config) as f:
+                rt = RuntimeConfig.from_config(yaml.safe_load(f) or {})
+            self.watch_interval = max(0.05, float(rt.watch_interval))
+            return bool(rt.watch_config)
+        except Exception:  # noqa: BLE001 - an unreadable config is reported by validate()
+            return False
+
+    def _file_stamp(self):
+        """(mtime_ns, size, sha256) of the config file, None when it cannot be read."""
+        import hashlib
+
+        try:
+            st = os.stat(self.config)
+            with open(self.config, "rb") as f:
+                return (st.st_mtime_ns, st.st_size, hashlib.sha256(f.read()).hexdigest())
+        except OSError:
+            return None
+
+    def poll_config(self) -> bool:
+        """Watch mode: True when the config's content changed since the last look (an mtime
+        touch with identical bytes is not a change)."""
+        now = time.time()
+        if not self.watch or now < self._next_watch:
+            return False
+        self._next_watch = now + self.watch_interval
+        try:
+            st = os.stat(self.config)
+        except OSError:
+            return False
+        old = self._stamp
+        if old is not None and (st.st_mtime_ns, st.st_size) == old[:2]:
+            return False
+        new = self._file_stamp()
+        self._stamp = new
+        return new is not None and (old is None or new[2] != old[2])
 
     def validate(self) -> Optional[str]:
         import yaml
@@ -186,6 +237,7 @@ class Supervisor:
         snap = self.validate()
         if snap is None:
             return
+        self.reloads += 1
         new = self.spawn(config=snap)
         if not self.wait_ready(new):
             logging.getLogger("qmx.serve").error("new generation failed to start; keeping the old one")
@@ -216,6 +268,9 @@ class Supervisor:
                 while any(p.poll() is None for p in self.current + self.retiring) and time.time() - t0 < 60:
                     time.sleep(0.05)
                 return 0
+            if self.poll_config():
+                logging.getLogger("qmx.serve").warning("config %s changed: rolling reload", self.config)
+                self.reload_requested = True
             if self.reload_requested:
                 self.reload_requested = False
                 self.reload()
@@ -245,6 +300,8 @@ def main(argv=None) -> int:
     ap.add_argument("--device", type=int, default=None)
     ap.add_argument("--impl", default="python", choices=["python", "native"])
     ap.add_argument("--gpus", type=int, default=1, help="rank processes on this node (one per GPU)")
+    ap.add_argument("--watch-config", action="store_true",
+                    help="roll a new worker generation in whenever the config file's content changes")
     ap.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--native-worker", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args(argv)

@@ -220,6 +220,10 @@ class RuntimeConfig:
                arenas, disjoint stream sets) — QMX_TICK_LANES
     log_content: allow prompts / per-backend answers in the ``aggregation`` log (off: user
                data; see utils/logging_setup.py) — QMX_LOG_CONTENT
+    watch_config: the supervisor polls the config file and rolls a new worker generation in
+               when its content changes (the reference's ``uvicorn --reload --reload-include
+               "*.yaml"``, Makefile:4; here without dropping a request) — QMX_WATCH_CONFIG
+    watch_interval: seconds between those polls
     """
 
     engine: str = "auto"
@@ -237,6 +241,8 @@ class RuntimeConfig:
     shared_engine: Any = "auto"
     tick_lanes: int = 2
     log_content: bool = False
+    watch_config: bool = False
+    watch_interval: float = 1.0
 
     @classmethod
     def from_config(cls, cfg: Dict[str, Any]) -> "RuntimeConfig":
@@ -250,6 +256,8 @@ class RuntimeConfig:
             rt["verify"] = os.environ["QMX_VERIFY"] not in ("0", "", "false")
         if os.environ.get("QMX_SHARED_ENGINE"):
             rt["shared_engine"] = os.environ["QMX_SHARED_ENGINE"] not in ("0", "false")
+        if os.environ.get("QMX_WATCH_CONFIG"):
+            rt["watch_config"] = os.environ["QMX_WATCH_CONFIG"] not in ("0", "", "false")
         if os.environ.get("QMX_TICK_LANES"):
             rt["tick_lanes"] = int(os.environ["QMX_TICK_LANES"])
         known = {k: v for k, v in rt.items() if k in cls.__dataclass_fields__}

@@ -125,6 +125,93 @@ def test_reload_drain_restart(tmp_path, impl):
     assert rc == 0
 
 
+def test_config_watch_rolls_new_generation(tmp_path):
+    """``runtime.watch_config``: editing the YAML (no signal) rolls a new worker generation in
+    while a client hammers the port — no request fails, the new backend answers, an edit that
+    does not validate is ignored (the current generation keeps serving), and rewriting the
+    same bytes is not a change (reference: uvicorn --reload --reload-include "*.yaml",
+    Makefile:4, which restarts and drops in-flight requests)."""
+    if not native.available():
+        pytest.skip("native extension not built")
+    live = LiveUpstream()
+    pa = live.serve("a", ("stream", 200, sse_stream(["AAA"])))
+    pb = live.serve("b", ("stream", 200, sse_stream(["BBB"])))
+    cfg = str(tmp_path / "config.yaml")
+
+    def write(url):
+        _write(cfg, [url, url])
+        with open(cfg) as f:
+            c = yaml.safe_load(f)
+        c["runtime"].update(watch_config=True, watch_interval=0.1)
+        with open(cfg, "w") as f:
+            yaml.safe_dump(c, f)
+
+    write(f"http://127.0.0.1:{pa}/v1")
+    port = free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT, QMX_ENGINE="cpu")
+    sup = subprocess.Popen([sys.executable, "-m", "quorum_amd.serve", "--impl", "native", "--engine", "cpu",
+                            "--config", cfg, "--port", str(port), "--threads", "2"], cwd=ROOT, env=env,
+                           start_new_session=True)
+    errors, stop = [], threading.Event()
+
+    def hammer():
+        while not stop.is_set():
+            try:
+                r = _post(port)
+                if r.status_code != 200 or _final(r.text) is None:
+                    errors.append(r.status_code)
+            except httpx.HTTPError as e:
+                errors.append(repr(e))
+
+    th = threading.Thread(target=hammer)
+    try:
+        assert _final(_wait(port, lambda r: r.status_code == 200).text) == "AAA\n\n--\nAAA"
+        th.start()
+        write(f"http://127.0.0.1:{pb}/v1")  # an edit, no SIGHUP
+        _wait(port, lambda r: _final(r.text) == "BBB\n\n--\nBBB", timeout=30)
+        time.sleep(0.5)
+        with open(cfg, "w") as f:  # an edit that does not validate: ignored
+            f.write("primary_backends: [unclosed\n")
+        time.sleep(1.0)
+        assert _final(_post(port).text) == "BBB\n\n--\nBBB"
+        stop.set()
+        th.join()
+        assert errors == [], errors[:5]
+    finally:
+        stop.set()
+        if th.is_alive():
+            th.join()
+        os.kill(sup.pid, signal.SIGTERM)
+        try:
+            sup.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            os.killpg(sup.pid, signal.SIGKILL)
+        live.close()
+
+
+def test_watch_poll_ignores_identical_rewrite(tmp_path):
+    """Supervisor.poll_config: a touch or an identical rewrite is not a change; new bytes are."""
+    from types import SimpleNamespace
+
+    from quorum_amd.serve import Supervisor
+
+    cfg = tmp_path / "c.yaml"
+    cfg.write_text("settings: {timeout: 5}\nruntime: {watch_config: true, watch_interval: 0.05}\n")
+    sup = Supervisor(SimpleNamespace(watch_config=False), str(cfg))
+    assert sup.watch and sup.watch_interval == 0.05
+    time.sleep(0.06)
+    assert not sup.poll_config()
+    os.utime(cfg, None)
+    cfg.write_text(cfg.read_text())  # same bytes, new mtime
+    time.sleep(0.06)
+    assert not sup.poll_config()
+    cfg.write_text("settings: {timeout: 6}\nruntime: {watch_config: true, watch_interval: 0.05}\n")
+    time.sleep(0.06)
+    assert sup.poll_config()
+    time.sleep(0.06)
+    assert not sup.poll_config()
+
+
 def test_native_drain_finishes_inflight(tmp_path):
     """SIGTERM to a native worker: the listener closes at once, an in-flight slow stream
     still completes, then the process exits 0."""

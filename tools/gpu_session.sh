@@ -138,6 +138,19 @@ for l in open('$OUT/kbench.jsonl'):
       [ $rc -eq 0 ] || exit 1 ;;
     multirank=*)
       n=${step#multirank=}; torchrun_bench multirank_$n $n --steps 5 --warmup 1 --threads 2 --batch 4096 || exit 1 ;;
+    selfrank=*)  # bench.py --gpus N launching its own N ranks (no torchrun), sharing GPU 0
+      n=${step#selfrank=}
+      QMX_BENCH_NDEV=${QMX_BENCH_NDEV:-1} timeout -k 10 400 python bench.py --gpus $n --steps 5 --warmup 1 --threads 2 \
+        --batch 4096 > $OUT/selfrank_$n.json 2> $OUT/selfrank_$n.err
+      rc=$?; summ selfrank_$n $OUT/selfrank_$n.json
+      python3 -c "
+import json
+d=json.loads([l for l in open('$OUT/selfrank_$n.json') if l.startswith('{')][-1]); s=d.get('spread_check',{})
+print('per-rank pids', [r['pid'] for r in d.get('breakdown_per_rank',[])], 'spread', {k: s.get(k) for k in ('ok','requests','invalid','remote_streams','mesh_finals','delta_mismatch','worker_nodata','peer_downs','remote_ends','p50_latency_ms')})
+for r in s.get('per_rank',[]): print('  ', r)
+" || true
+      grep "qmx spread\|qmx exchange" $OUT/selfrank_$n.err | head -20
+      [ $rc -eq 0 ] || { echo "step selfrank_$n failed rc=$rc"; tail -30 $OUT/selfrank_$n.err; exit 1; } ;;
     spread=*)
       n=${step#spread=}; QMX_XCHG=tcp torchrun_bench spread_$n $n --steps 5 --warmup 1 --threads 2 --batch 4096 --placement spread || exit 1 ;;
     cpuprof)
