@@ -406,10 +406,10 @@ def compact_breakdown(rank: int, bd: dict, row) -> dict:
 
 def spread_summary(rows) -> dict:
     """The spread check of every rank, compact: totals plus each rank's own counters."""
-    keys = ("requests", "invalid", "remote_streams", "rccl_rounds", "rccl_final_bytes", "mesh_finals", "delta_mismatch",
+    keys = ("requests", "invalid", "remote_streams", "bulk_rounds", "bulk_final_bytes", "mesh_finals", "delta_mismatch",
             "worker_nodata", "peer_downs")
     out = {"ok": all(r.get("ok") for r in rows), "transport": rows[0].get("transport"),
-           "rccl_formed": all(r.get("rccl_formed") for r in rows)}
+           "bulk_formed": all(r.get("bulk_formed") for r in rows)}
     for k in keys:
         out[k] = int(sum(r.get(k) or 0 for r in rows))
     lat = [r["p50_latency_ms"] for r in rows if r.get("p50_latency_ms") is not None]
@@ -419,7 +419,7 @@ def spread_summary(rows) -> dict:
         for k, v in (r.get("remote_ends") or {}).items():
             ends[k] = ends.get(k, 0) + int(v)
     out["remote_ends"] = ends
-    out["per_rank"] = [{k: r.get(k) for k in ("ok", "pid", "requests", "invalid", "remote_streams", "rccl_rounds",
+    out["per_rank"] = [{k: r.get(k) for k in ("ok", "pid", "requests", "invalid", "remote_streams", "bulk_rounds",
                                              "mesh_finals", "delta_mismatch", "worker_nodata", "remote_ends",
                                              "up_failures", "p50_latency_ms", "error") if r.get(k)}
                        for r in rows]
@@ -460,9 +460,14 @@ def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports
         dist.broadcast_object_list(nonce, src=0)
         env = dict(os.environ, **exchange_env(rank, world, port, nonce[0]))
         if n_dev < world or engine != "hip":
-            env["QMX_XCHG"] = "tcp"  # ranks sharing a GPU (rehearsal): RCCL needs one GPU per rank
-        want_rccl = env.get("QMX_XCHG", "rccl") == "rccl"
-        out["transport"] = "rccl" if want_rccl else "tcp"
+            # ranks sharing a GPU (rehearsal) or no GPU: RCCL needs one GPU per rank, so the
+            # same bulk rounds run with the socket executor (tcpbulk)
+            env.setdefault("QMX_XCHG", "tcpbulk")
+            if env["QMX_XCHG"] == "rccl":
+                env["QMX_XCHG"] = "tcpbulk"
+        xchg = env.get("QMX_XCHG", "rccl")
+        want_bulk = xchg in ("rccl", "tcpbulk")
+        out["transport"] = xchg
         try:
             cfg = os.path.join(tmp, "config_spread.yaml")
             write_config(cfg, mock_ports, False, args.tile, sc, "spread")
@@ -486,8 +491,8 @@ def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports
                 while True:  # the mesh formed on every rank (and, on GPUs, the RCCL communicator)
                     m = scrape(admin)
                     healthy = m.get("qmx_exchange_healthy") == 1.0
-                    rccl = m.get("qmx_exchange_rccl_active") == 1.0
-                    if healthy and (not want_rccl or rccl):
+                    bulk = m.get("qmx_exchange_rccl_active") == 1.0
+                    if healthy and (not want_bulk or bulk):
                         break
                     if not healthy and time.time() - t0 > 60:
                         raise RuntimeError(f"exchange did not form: {({k: v for k, v in m.items() if 'exchange' in k})}")
@@ -496,7 +501,7 @@ def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports
                         # reported, so a node where RCCL never formed is visible in the line
                         break
                     time.sleep(0.2)
-                out["rccl_formed"] = bool(want_rccl and rccl)
+                out["bulk_formed"] = bool(want_bulk and bulk)
             except Exception as e:  # noqa: BLE001
                 ok, err = False, repr(e)[:300]
         if agree("exchange formation"):
@@ -520,8 +525,8 @@ def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports
                                 "p50_ttft_ms": st["ttft_p50_ms"], "p50_latency_ms": st["lat_p50_ms"],
                                 "req_s": st["rps"], "pid": procs[0].pid if procs else None,
                                 "remote_streams": d.get("qmx_remote_streams_total", 0.0),
-                                "rccl_rounds": d.get("qmx_exchange_rounds_total", 0.0),
-                                "rccl_final_bytes": d.get("qmx_exchange_bulk_bytes_total", 0.0),
+                                "bulk_rounds": d.get("qmx_exchange_rounds_total", 0.0),
+                                "bulk_final_bytes": d.get("qmx_exchange_bulk_bytes_total", 0.0),
                                 "mesh_finals": d.get("qmx_exchange_mesh_finals_total", 0.0),
                                 "mesh_messages": d.get("qmx_exchange_messages_total", 0.0),
                                 "delta_mismatch": d.get("qmx_spread_delta_mismatch_total", 0.0),

@@ -131,7 +131,7 @@ ServerCfg server_cfg_from(const py::dict& d) {
   gs("redoc_html", c.redoc_html); gs("oauth2_redirect_html", c.oauth2_redirect_html);
   gb("install_signals", c.install_signals);
   gi("rank", c.rank); gi("world", c.world); gs("placement", c.placement); gs("xchg", c.xchg);
-  gs("xchg_addr", c.xchg_addr); gi("xchg_port", c.xchg_port); gs("xchg_id_file", c.xchg_id_file);
+  gs("xchg_addr", c.xchg_addr); gi("xchg_port", c.xchg_port); gi("xchg_bulk_port", c.xchg_bulk_port); gs("xchg_id_file", c.xchg_id_file);
   gi("xchg_round_us", c.xchg_round_us); gd("xchg_timeout", c.xchg_timeout);
   gd("drain_s", c.drain_s); gs("ready_file", c.ready_file); gb("verify", c.verify); gi("admin_port", c.admin_port);
   gi("shared_engine", c.shared_engine); gi("tick_lanes", c.tick_lanes);
@@ -186,8 +186,11 @@ PYBIND11_MODULE(_qmx, m) {
     auto gs = [&](const char* k, std::string& v) { if (d.contains(k)) v = py::cast<std::string>(d[k]); };
     auto gi = [&](const char* k, int& v) { if (d.contains(k)) v = py::cast<int>(d[k]); };
     gi("rank", o.rank); gi("world", o.world); gs("transport", o.transport); gs("addr", o.addr);
-    gi("port", o.port); gi("device", o.device);
+    gi("port", o.port); gi("device", o.device); gi("bulk_port", o.bulk_port);
     if (d.contains("timeout")) o.timeout_s = py::cast<double>(d["timeout"]);
+    const double wait_s = o.timeout_s;  // the whole test; round_timeout: the exchange's own round limit
+    if (d.contains("round_timeout")) o.timeout_s = py::cast<double>(d["round_timeout"]);
+    const uint64_t min_epochs = d.contains("min_epochs") ? py::cast<uint64_t>(d["min_epochs"]) : 0;
     const bool dev = o.transport == "rccl";
     auto payload = [](int r, int src, int dst, int kind) {
       uint64_t x = 1234567 ^ ((uint64_t)r * 1000003ull) ^ ((uint64_t)src * 7919ull) ^ ((uint64_t)dst * 104729ull) ^
@@ -229,13 +232,14 @@ PYBIND11_MODULE(_qmx, m) {
           if (src == o.rank && !loop1) continue;
           const size_t n = payload(r, src, o.rank, 1).size();
           void* p = dev ? dalloc(n) : nullptr;
+          // (skey, bi) names ONE stream: bi = src x world + dst, as a session key names one owner
           sinks[{r, src}] = p;
-          x.expect_bulk((uint64_t)(r + 1), src, p, n);
+          x.expect_bulk((uint64_t)(r + 1), src * o.world + o.rank, p, n);
         }
       const auto t0 = std::chrono::steady_clock::now();
       auto secs = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
-      while (!x.healthy() || (dev && !x.rccl_active())) {
-        if (secs() > o.timeout_s) {
+      while (!x.healthy() || (x.bulk_transport() && !x.rccl_active())) {
+        if (secs() > wait_s) {
           ok = false;
           break;
         }
@@ -263,7 +267,7 @@ PYBIND11_MODULE(_qmx, m) {
           h.dst_rank = p;
           h.src_rank = o.rank;
           h.skey = (uint64_t)(r + 1);
-          h.bi = o.rank;
+          h.bi = o.rank * o.world + p;
           h.flags = XF_TEXT;
           x.send_bulk(std::move(h), src, b.size(), [b] { return b; });
         }
@@ -278,11 +282,12 @@ PYBIND11_MODULE(_qmx, m) {
               if (n_data == want) data_us = 1e6 * std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
             } else if (m.type == X_BULK) {
               ++n_bulk;
-              const std::string exp = payload((int)m.skey - 1, m.bi, o.rank, 1);
+              const int src = m.bi / o.world;
+              const std::string exp = payload((int)m.skey - 1, src, o.rank, 1);
               std::string have = m.payload;
               if (have.empty() && m.a > 0) {  // RCCL: in the HBM sink
                 have.assign((size_t)m.a, '\0');
-                void* sp = sinks[{(int)m.skey - 1, m.bi}];
+                void* sp = sinks[{(int)m.skey - 1, src}];
                 if (!sp || hipMemcpy(&have[0], sp, have.size(), hipMemcpyDeviceToHost) != hipSuccess) have.clear();
               }
               if (have != exp) ++bad;
@@ -291,8 +296,8 @@ PYBIND11_MODULE(_qmx, m) {
             }
           }
           got.clear();
-          if (n_data >= want && n_bulk >= want && n_sent >= want) break;
-          if (secs() > o.timeout_s) {
+          if (n_data >= want && n_bulk >= want && n_sent >= want && x.epochs() >= min_epochs) break;
+          if (secs() > wait_s) {
             ok = false;
             break;
           }

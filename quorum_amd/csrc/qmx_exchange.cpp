@@ -13,6 +13,7 @@
 #include <sched.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -21,6 +22,7 @@
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <stdexcept>
 
 namespace qmx {
@@ -180,7 +182,7 @@ struct Exchange::Impl {
   }
   void mark_down(int r, const char* why) {
     Peer& p = peers[r];
-    if (p.up) {
+    if (p.up && !X->stop_.load()) {
       X->downs_++;
       fprintf(stderr, "qmx exchange (rank %d): peer %d down (%s, errno %d)\n", X->o_.rank, r, why, errno);
     }
@@ -204,7 +206,7 @@ struct Exchange::Impl {
         X->deliver_(l, std::move(v));
       }
       bcv.notify_all();  // a bulk round waiting on this peer gives up at once
-      if (X->o_.rank == 0 && X->o_.transport == "rccl") rccl_down_everywhere();
+      if (X->o_.rank == 0 && X->bulk_transport()) rccl_down_everywhere();
     }
   }
   void mark_up(int r) {
@@ -416,10 +418,11 @@ struct Exchange::Impl {
     }
   }
   void maybe_new_epoch() {
-    if (X->o_.rank != 0 || X->o_.transport != "rccl" || epoch_live || !all_up() || now_s() < next_epoch_at) return;
+    if (X->o_.rank != 0 || !X->bulk_transport() || epoch_live || !all_up() || now_s() < next_epoch_at) return;
     std::string id;
-    try {
-      id = rccl_unique_id_hex();
+    try {  // names the epoch (RCCL: its unique id; tcpbulk: hashed into every hello)
+      if (X->o_.transport == "rccl") id = rccl_unique_id_hex();
+      else id = std::to_string(now_s()) + "/" + std::to_string(epoch_no + 1);
     } catch (const std::exception& ex) {
       fprintf(stderr, "qmx exchange: %s\n", ex.what());
       return;
@@ -493,7 +496,7 @@ Exchange::Exchange(const XOptions& o, int nloops, Deliver deliver)
     epoll_ctl(im_->ep, EPOLL_CTL_ADD, im_->lfd, &e);
   }
   mesh_th_ = std::thread([this] { mesh_loop(); });
-  if (o_.transport == "rccl") bulk_th_ = std::thread([this] { bulk_loop(); });
+  if (bulk_transport()) bulk_th_ = std::thread([this] { bulk_loop(); });
 }
 
 Exchange::~Exchange() {
@@ -519,7 +522,8 @@ bool Exchange::peer_up(int r) const {
 
 void Exchange::send_bulk(XMsg&& hdr, const void* dev, size_t len, std::function<std::string()> host) {
   const int dst = hdr.dst_rank;
-  if (rccl_active() && dev != nullptr && len > 0) {
+  // rounds move the bytes (an RCCL round needs them in HBM; tcpbulk reads them on the host)
+  if (rccl_active() && len > 0 && (dev != nullptr || o_.transport == "tcpbulk")) {
     WireEntry e{};
     e.src = o_.rank;
     e.dst = dst;
@@ -720,26 +724,354 @@ void Exchange::mesh_loop() {
   }
 }
 
-// ------------------------------------------------------------------ the bulk (RCCL) thread
+// ------------------------------------------------------------------ bulk executors
+// The round protocol — announcements, manifests rank 0 numbers, epochs, a failed round →
+// communicator dropped everywhere → mesh fallback → a new epoch once every rank is up — is
+// the same whatever moves a round's bytes.  An executor only (re)forms its communicator and
+// runs one round's sends and receives, in manifest order per peer pair:
+//  * RcclExec — ncclSend / ncclRecv in one group, HBM to HBM over xGMI (the MI355X path);
+//  * TcpExec  — a socket per rank pair (transport tcpbulk): the same rounds on CPU-only
+//    hosts and rank rehearsals sharing one GPU, where RCCL cannot form (one GPU per rank).
+//    Every transfer carries (round, skey, bi, len), so a desynchronised round fails loudly.
+namespace {
+
+struct BulkOp {
+  const WireEntry* e;
+  bool send;
+  const void* src;  // send: HBM (device executors) or host bytes; nullptr: a vanished send
+  std::string host;  // send (host executors): the bytes; receive: filled on completion
+  size_t off = 0;    // receive (device executors): staging offset
+};
+
+struct BulkExec {
+  virtual ~BulkExec() = default;
+  virtual bool device() const = 0;
+  virtual bool form(const std::string& id, int epoch, double timeout_s, const std::atomic<bool>& stop) = 0;
+  virtual void drop() = 0;
+  virtual bool formed() const = 0;
+  virtual bool start(int round, std::vector<BulkOp>& ops) = 0;
+  virtual int progress() = 0;  // 1 complete, 0 in flight, -1 failed
+  // device executors: copy a completed receive from staging into the owner's sink
+  virtual bool to_sink(const BulkOp&, void*) { return false; }
+};
+
+class RcclExec : public BulkExec {
+ public:
+  RcclExec(int device, int world, int rank) : device_(device), world_(world), rank_(rank) {
+    XHIP(hipSetDevice(device_));
+    XHIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+  }
+  ~RcclExec() override {
+    drop();
+    if (scratch_) hipFree(scratch_);
+    if (st_) hipStreamDestroy(st_);
+  }
+  bool device() const override { return true; }
+  bool formed() const override { return comm_ != nullptr; }
+  bool form(const std::string& id, int, double timeout_s, const std::atomic<bool>& stop) override {
+    drop();
+    ncclUniqueId uid;
+    if (!from_hex(id, &uid)) return false;
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t r = ncclCommInitRankConfig(&comm_, world_, uid, rank_, &cfg);
+    if ((r == ncclSuccess || r == ncclInProgress) && ready(now_s() + timeout_s, stop)) return true;
+    drop();
+    return false;
+  }
+  void drop() override {
+    if (comm_) ncclCommAbort(comm_);
+    comm_ = nullptr;
+    if (st_) hipStreamSynchronize(st_);  // the aborted communicator's kernels have been flushed
+  }
+  bool start(int, std::vector<BulkOp>& ops) override {
+    size_t need = 256;
+    for (auto& o : ops)
+      if (!o.send) need += (o.e->len + 255) & ~(size_t)255;
+    if (need > cap_) {
+      if (scratch_) hipFree(scratch_);
+      cap_ = std::max(need, cap_ * 2);
+      if (hipMalloc(&scratch_, cap_) != hipSuccess) {
+        scratch_ = nullptr;
+        cap_ = 0;
+        return false;
+      }
+    }
+    if (ncclGroupStart() != ncclSuccess) return false;
+    bool ok = true;
+    size_t off = 0;
+    for (auto& o : ops) {
+      ncclResult_t r;
+      if (o.send) {
+        // a vanished send (its session ended) still posts len bytes, or the pair desyncs
+        const void* src = o.src ? o.src : scratch_ + cap_ - 256;
+        r = ncclSend(src, o.e->len, ncclUint8, o.e->dst, comm_, st_);
+      } else {
+        o.off = off;
+        r = ncclRecv(scratch_ + off, o.e->len, ncclUint8, o.e->src, comm_, st_);
+        off += (o.e->len + 255) & ~(size_t)255;
+      }
+      if (r != ncclSuccess && r != ncclInProgress) ok = false;
+    }
+    ncclResult_t r = ncclGroupEnd();
+    std::atomic<bool> never{false};
+    return ok && (r == ncclSuccess || r == ncclInProgress) && ready(now_s() + 30.0, never);
+  }
+  int progress() override {
+    hipError_t e = hipStreamQuery(st_);
+    if (e == hipSuccess) return 1;
+    return e == hipErrorNotReady ? 0 : -1;
+  }
+  bool to_sink(const BulkOp& o, void* dst) override {
+    if (!o.e->len) return true;
+    return hipMemcpyAsync(dst, scratch_ + o.off, o.e->len, hipMemcpyDeviceToDevice, st_) == hipSuccess &&
+           hipStreamSynchronize(st_) == hipSuccess;
+  }
+
+ private:
+  bool ready(double deadline, const std::atomic<bool>& stop) {  // non-blocking communicator settled
+    while (true) {
+      ncclResult_t ae = ncclSuccess;
+      if (ncclCommGetAsyncError(comm_, &ae) != ncclSuccess) return false;
+      if (ae == ncclSuccess) return true;
+      if (ae != ncclInProgress || now_s() > deadline || stop.load()) return false;
+      std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+  }
+  int device_, world_, rank_;
+  ncclComm_t comm_ = nullptr;
+  hipStream_t st_ = nullptr;
+  uint8_t* scratch_ = nullptr;
+  size_t cap_ = 0;
+};
+
+#pragma pack(push, 1)
+struct TcpHello {
+  uint32_t magic;
+  int32_t epoch, rank;
+  uint64_t id;  // hash of the epoch's id string (rank 0 names each epoch)
+};
+struct TcpXfer {  // precedes every transfer's bytes
+  uint32_t magic, round;
+  uint64_t skey;
+  int32_t bi;
+  uint32_t len;
+};
+#pragma pack(pop)
+constexpr uint32_t kHelloMagic = 0x514d5842, kXferMagic = 0x514d5858;
+
+class TcpExec : public BulkExec {
+ public:
+  TcpExec(const std::string& addr, int base_port, int world, int rank)
+      : addr_(addr), base_(base_port), world_(world), rank_(rank), fds_(world, -1), inbuf_(world) {
+    lfd_ = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK, 0);
+    int one = 1;
+    setsockopt(lfd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    sockaddr_in a = sa(rank_);
+    if (bind(lfd_, (sockaddr*)&a, sizeof(a)) != 0 || listen(lfd_, 64) != 0)
+      throw std::runtime_error("tcpbulk listen on " + std::to_string(base_ + rank_) + " failed: " + strerror(errno));
+  }
+  ~TcpExec() override {
+    drop();
+    if (lfd_ >= 0) close(lfd_);
+  }
+  bool device() const override { return false; }
+  bool formed() const override { return formed_; }
+  bool form(const std::string& id, int epoch, double timeout_s, const std::atomic<bool>& stop) override {
+    drop();
+    const uint64_t h = std::hash<std::string>()(id);
+    const double deadline = now_s() + timeout_s;
+    // lower ranks are dialled (retrying while their listener is not up yet), higher ranks dial us
+    for (int p = 0; p < rank_; ++p) {
+      while (fds_[p] < 0) {
+        if (now_s() > deadline || stop.load()) return fail();
+        int fd = socket(AF_INET, SOCK_STREAM, 0);
+        sockaddr_in a = sa(p);
+        if (connect(fd, (sockaddr*)&a, sizeof(a)) != 0) {
+          close(fd);
+          std::this_thread::sleep_for(std::chrono::milliseconds(20));
+          continue;
+        }
+        TcpHello hl{kHelloMagic, epoch, rank_, h};
+        if (send(fd, &hl, sizeof(hl), MSG_NOSIGNAL) != (ssize_t)sizeof(hl)) {
+          close(fd);
+          continue;
+        }
+        setup(fd);
+        fds_[p] = fd;
+      }
+    }
+    int need = world_ - 1 - rank_;
+    while (need > 0) {
+      if (now_s() > deadline || stop.load()) return fail();
+      pollfd pf{lfd_, POLLIN, 0};
+      if (poll(&pf, 1, 20) <= 0) continue;
+      int fd = accept(lfd_, nullptr, nullptr);
+      if (fd < 0) continue;
+      TcpHello hl{};
+      timeval tv{1, 0};
+      setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+      // a hello from another epoch (a stale dial) or another deployment is refused
+      if (recv(fd, &hl, sizeof(hl), MSG_WAITALL) != (ssize_t)sizeof(hl) || hl.magic != kHelloMagic ||
+          hl.epoch != epoch || hl.id != h || hl.rank <= rank_ || hl.rank >= world_ || fds_[hl.rank] >= 0) {
+        close(fd);
+        continue;
+      }
+      setup(fd);
+      fds_[hl.rank] = fd;
+      --need;
+    }
+    formed_ = true;
+    return true;
+  }
+  void drop() override {
+    for (int& fd : fds_)
+      if (fd >= 0) {
+        close(fd);  // the peers' rounds see EOF and fail: everyone drops to the mesh
+        fd = -1;
+      }
+    formed_ = false;
+    peers_.clear();
+    inbuf_.assign(world_, std::string());
+  }
+  bool start(int round, std::vector<BulkOp>& ops) override {
+    peers_.assign(world_, Pipe());
+    for (auto& o : ops) {
+      const WireEntry& e = *o.e;
+      const int p = o.send ? e.dst : e.src;
+      if (p < 0 || p >= world_) return false;
+      Pipe& q = peers_[p];
+      if (o.send) {
+        TcpXfer x{kXferMagic, (uint32_t)round, e.skey, e.bi, e.len};
+        q.out.append((const char*)&x, sizeof(x));
+        if (o.host.size() == e.len) q.out += o.host;
+        else q.out.append(e.len, '\0');  // a vanished send keeps the pair in step
+      } else {
+        q.want.push_back(&o);
+      }
+    }
+    {  // loopback (a one-rank self-test): straight through
+      Pipe& q = peers_[rank_];
+      inbuf_[rank_] += q.out;
+      q.out.clear();
+    }
+    round_ = (uint32_t)round;
+    return true;
+  }
+  int progress() override {
+    std::vector<pollfd> pf;
+    std::vector<int> who;
+    for (int p = 0; p < world_; ++p) {
+      Pipe& q = peers_[p];
+      // bytes already buffered (loopback, or a peer that ran ahead into this round while we
+      // finished the last one) complete receives without any new readiness
+      if (q.got < q.want.size() && parse(p) < 0) return -1;
+      if (p == rank_) continue;
+      const bool out = q.off < q.out.size(), in = q.got < q.want.size();
+      if (!out && !in) continue;
+      if (fds_[p] < 0) return -1;
+      pf.push_back(pollfd{fds_[p], (short)((out ? POLLOUT : 0) | POLLIN), 0});
+      who.push_back(p);
+    }
+    if (pf.empty()) return 1;
+    if (poll(pf.data(), pf.size(), 1) < 0 && errno != EINTR) return -1;
+    char buf[65536];
+    for (size_t k = 0; k < pf.size(); ++k) {
+      Pipe& q = peers_[who[k]];
+      if (pf[k].revents & (POLLERR | POLLNVAL)) return -1;
+      if ((pf[k].revents & POLLOUT) && q.off < q.out.size()) {
+        ssize_t w = send(pf[k].fd, q.out.data() + q.off, q.out.size() - q.off, MSG_NOSIGNAL | MSG_DONTWAIT);
+        if (w < 0 && errno != EAGAIN && errno != EWOULDBLOCK) return -1;
+        if (w > 0) q.off += (size_t)w;
+      }
+      if (pf[k].revents & (POLLIN | POLLHUP)) {
+        ssize_t r = recv(pf[k].fd, buf, sizeof(buf), MSG_DONTWAIT);
+        if (r == 0 || (r < 0 && errno != EAGAIN && errno != EWOULDBLOCK)) return -1;  // peer gone
+        // (bytes of the peer's next round may already be here: they stay in inbuf_)
+        if (r > 0) inbuf_[who[k]].append(buf, (size_t)r);
+        if (parse(who[k]) < 0) return -1;
+      }
+    }
+    for (int p = 0; p < world_; ++p) {
+      const Pipe& q = peers_[p];
+      if (q.off < q.out.size() && p != rank_) return 0;
+      if (q.got < q.want.size()) return 0;
+    }
+    return 1;
+  }
+
+ private:
+  struct Pipe {
+    std::string out;
+    size_t off = 0, got = 0;
+    std::vector<BulkOp*> want;  // receives from this peer, manifest order
+  };
+  int parse(int peer) {  // complete transfers from `peer` → its next expected receives
+    Pipe& q = peers_[peer];
+    std::string& in = inbuf_[peer];
+    size_t p = 0;
+    while (q.got < q.want.size() && in.size() - p >= sizeof(TcpXfer)) {
+      TcpXfer x;
+      std::memcpy(&x, in.data() + p, sizeof(x));
+      const WireEntry& e = *q.want[q.got]->e;
+      if (x.magic != kXferMagic || x.round != round_ || x.skey != e.skey || x.bi != e.bi || x.len != e.len) {
+        fprintf(stderr, "qmx exchange (rank %d): tcpbulk round %u desynchronised (got skey %llx bi %d len %u, "
+                "manifest skey %llx bi %d len %u)\n", rank_, round_, (unsigned long long)x.skey, x.bi, x.len,
+                (unsigned long long)e.skey, e.bi, e.len);
+        return -1;
+      }
+      if (in.size() - p - sizeof(x) < x.len) break;
+      q.want[q.got]->host.assign(in.data() + p + sizeof(x), x.len);
+      p += sizeof(x) + x.len;
+      ++q.got;
+    }
+    in.erase(0, p);
+    return 0;
+  }
+  bool fail() {
+    drop();
+    return false;
+  }
+  sockaddr_in sa(int r) const {
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons((uint16_t)(base_ + r));
+    inet_pton(AF_INET, addr_.c_str(), &a.sin_addr);
+    return a;
+  }
+  static void setup(int fd) {
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    fcntl(fd, F_SETFL, fcntl(fd, F_GETFL) | O_NONBLOCK);
+  }
+  std::string addr_;
+  int base_, world_, rank_, lfd_ = -1;
+  std::vector<int> fds_;
+  bool formed_ = false;
+  uint32_t round_ = 0;
+  std::vector<Pipe> peers_;
+  std::vector<std::string> inbuf_;  // per peer, across rounds (a peer may run ahead by one)
+};
+
+}  // namespace
+
+// ------------------------------------------------------------------ the bulk thread
 void Exchange::bulk_loop() {
   prof_thread();
   crash_thread();
   Impl& I = *im_;
-  ncclComm_t comm = nullptr;
-  int epoch = 0;
-  hipStream_t st = nullptr;
-  uint8_t* scratch = nullptr;
-  size_t scratch_cap = 0;
+  std::unique_ptr<BulkExec> ex;
   try {
-    XHIP(hipSetDevice(o_.device));
-    XHIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    if (o_.transport == "rccl") ex.reset(new RcclExec(o_.device, o_.world, o_.rank));
+    else ex.reset(new TcpExec(o_.addr, o_.bulk_port > 0 ? o_.bulk_port : o_.port + o_.world, o_.world, o_.rank));
   } catch (const std::exception& e) {
     fprintf(stderr, "qmx exchange (rank %d): %s — bulk transfers use the mesh\n", o_.rank, e.what());
     return;
   }
+  int epoch = 0, my_rounds = 0;
+  const int stall_round = getenv("QMX_XCHG_FAULT_STALL_ROUND") ? atoi(getenv("QMX_XCHG_FAULT_STALL_ROUND")) : 0;
   auto drop = [&](bool report) {
-    if (comm) ncclCommAbort(comm);
-    comm = nullptr;
+    ex->drop();
     rccl_ok_.store(false);
     if (report && epoch > 0) {
       XMsg m;
@@ -747,16 +1079,6 @@ void Exchange::bulk_loop() {
       m.a = epoch;
       m.dst_rank = 0;
       I.enqueue(0, frame(m));
-    }
-  };
-  // wait for the communicator's pending operation (non-blocking communicator)
-  auto comm_ready = [&](double deadline) {
-    while (true) {
-      ncclResult_t ae = ncclSuccess;
-      if (ncclCommGetAsyncError(comm, &ae) != ncclSuccess) return false;
-      if (ae == ncclSuccess) return true;
-      if (ae != ncclInProgress || now_s() > deadline || stop_.load()) return false;
-      std::this_thread::sleep_for(std::chrono::microseconds(100));
     }
   };
   auto mesh_fallback = [&](const WireEntry& e) {
@@ -808,53 +1130,29 @@ void Exchange::bulk_loop() {
     }
     if (want_epoch) {  // (re)form the world communicator
       drop(false);
-      ncclUniqueId uid;
-      if (from_hex(id, &uid)) {
-        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-        cfg.blocking = 0;
-        ncclResult_t r = ncclCommInitRankConfig(&comm, o_.world, uid, o_.rank, &cfg);
-        if ((r == ncclSuccess || r == ncclInProgress) && comm_ready(now_s() + o_.timeout_s)) {
-          epoch = want_epoch;
-          rccl_epoch_.store((uint64_t)epoch);
-          rccl_ok_.store(true);
-        } else {
-          fprintf(stderr, "qmx exchange (rank %d): RCCL epoch %d did not form — bulk uses the mesh\n", o_.rank,
-                  want_epoch);
-          epoch = want_epoch;
-          drop(true);
-        }
+      epoch = want_epoch;
+      if (ex->form(id, want_epoch, o_.timeout_s, stop_)) {
+        rccl_epoch_.store((uint64_t)epoch);
+        rccl_ok_.store(true);
+      } else {
+        fprintf(stderr, "qmx exchange (rank %d): %s epoch %d did not form — bulk uses the mesh\n", o_.rank,
+                o_.transport.c_str(), want_epoch);
+        drop(true);
       }
     }
     if (mf.es.empty() && !mf.fallback) continue;
-    if (mf.fallback || !comm || mf.epoch != epoch) {
+    if (mf.fallback || !ex->formed() || mf.epoch != epoch) {
       for (const WireEntry& e : mf.es)
         if (e.src == o_.rank) mesh_fallback(e);
       // a receive whose sender falls back arrives over the mesh (F_BULK_MESH)
       continue;
     }
-    // one group: this rank's sends and receives of the round, in manifest order
+    // this rank's sends and receives of the round, in manifest order
     const double t0 = now_s();
-    std::vector<std::pair<const WireEntry*, Impl::Send>> my_sends;
-    std::vector<std::pair<const WireEntry*, size_t>> my_recvs;  // (entry, staging offset)
-    bool ok = true;
-    size_t recv_off = 0;
-    {
-      size_t scratch_need = 256;
-      for (const WireEntry& e : mf.es)
-        if (e.dst == o_.rank) scratch_need += (e.len + 255) & ~(size_t)255;
-      if (scratch_need > scratch_cap) {
-        if (scratch) hipFree(scratch);
-        scratch_cap = std::max(scratch_need, scratch_cap * 2);
-        if (hipMalloc(&scratch, scratch_cap) != hipSuccess) {
-          scratch = nullptr;
-          scratch_cap = 0;
-          ok = false;
-        }
-      }
-    }
-    if (ok && ncclGroupStart() != ncclSuccess) ok = false;
+    std::vector<BulkOp> ops;
+    std::vector<Impl::Send> held;  // the sends' state (host producers for a fallback resend)
+    ops.reserve(mf.es.size() * 2);
     for (const WireEntry& e : mf.es) {
-      if (!ok) break;
       if (e.src == o_.rank) {
         Impl::Send s;
         {
@@ -865,30 +1163,30 @@ void Exchange::bulk_loop() {
             I.sends.erase(it);
           }
         }
-        const void* src = s.dev ? s.dev : scratch + scratch_cap - 256;  // (a vanished send still matches)
-        ncclResult_t r = ncclSend(src, e.len, ncclUint8, e.dst, comm, st);
-        ok = r == ncclSuccess || r == ncclInProgress;
-        my_sends.emplace_back(&e, std::move(s));
+        BulkOp o{&e, true, s.dev, std::string()};
+        if (!ex->device()) {
+          if (s.host) o.host = s.host();  // host executor: the engine's bytes (HBM → host for HIP)
+          o.src = s.host ? o.host.data() : nullptr;
+        }
+        ops.push_back(std::move(o));
+        held.push_back(std::move(s));
       }
-      if (ok && e.dst == o_.rank) {  // (a loopback entry — self-test — has both halves here)
-        // into this rank's staging area (one slot per receive of the round): the owner may
-        // release the destination slot while the round is in flight; the copy into its HBM
-        // content slot happens under the sink lock once the data is here
-        ncclResult_t r = ncclRecv(scratch + recv_off, e.len, ncclUint8, e.src, comm, st);
-        ok = r == ncclSuccess || r == ncclInProgress;
-        my_recvs.emplace_back(&e, recv_off);
-        recv_off += (e.len + 255) & ~(size_t)255;
-      }
+      if (e.dst == o_.rank) ops.push_back(BulkOp{&e, false, nullptr, std::string()});
     }
-    if (ok) {
-      ncclResult_t r = ncclGroupEnd();
-      ok = (r == ncclSuccess || r == ncclInProgress) && comm_ready(now_s() + o_.timeout_s);
+    bool ok;
+    if (stall_round > 0 && ++my_rounds == stall_round) {
+      // fault injection: this rank hangs in its round (posts nothing) until the round times out
+      fprintf(stderr, "qmx exchange (rank %d): injected stall in round %d\n", o_.rank, mf.round);
+      while (now_s() - t0 <= o_.timeout_s && !stop_.load()) std::this_thread::sleep_for(std::chrono::milliseconds(5));
+      ok = false;
+    } else {
+      ok = ex->start(mf.round, ops);
     }
-    // completion: poll the stream; give up at the timeout or as soon as a peer of the round
-    // leaves the mesh (its socket closed)
+    // completion: poll; give up at the timeout or as soon as a peer of the round leaves the
+    // mesh (its socket closed) or rank 0 declared the communicator down (another round failed)
     while (ok) {
-      hipError_t e = hipStreamQuery(st);
-      if (e == hipSuccess) break;
+      const int pr = ex->progress();
+      if (pr == 1) break;
       bool peer_gone = false;
       for (const WireEntry& w : mf.es) {
         const int p = w.src == o_.rank ? w.dst : w.src;
@@ -897,68 +1195,74 @@ void Exchange::bulk_loop() {
       bool dropped;
       {
         std::lock_guard<std::mutex> g(I.bmu);
-        dropped = I.drop_comm;  // rank 0 declared RCCL down (another rank's round failed)
+        dropped = I.drop_comm;
       }
-      if (e != hipErrorNotReady || peer_gone || dropped || now_s() - t0 > o_.timeout_s || stop_.load()) {
+      if (pr < 0 || peer_gone || dropped || now_s() - t0 > o_.timeout_s || stop_.load()) {
+        fprintf(stderr, "qmx exchange (rank %d): round %d ends early: %s\n", o_.rank, mf.round,
+                pr < 0 ? "transfer failed" : peer_gone ? "a peer left the mesh" : dropped ? "communicator dropped"
+                : stop_.load() ? "stopping" : "timeout");
         ok = false;
         break;
       }
-      if (now_s() - t0 < 5e-4) sched_yield();
-      else std::this_thread::sleep_for(std::chrono::microseconds(50));
+      if (ex->device()) {
+        if (now_s() - t0 < 5e-4) sched_yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(50));
+      }
     }
     busy_us_.store(busy_us_.load() + 1e6 * (now_s() - t0));
     if (!ok) {
-      fprintf(stderr, "qmx exchange (rank %d): RCCL round %d failed — communicator dropped, bulk uses the mesh\n",
-              o_.rank, mf.round);
+      fprintf(stderr, "qmx exchange (rank %d): %s round %d failed — communicator dropped, bulk uses the mesh\n",
+              o_.rank, o_.transport.c_str(), mf.round);
       drop(true);
-      hipStreamSynchronize(st);  // the aborted communicator's kernels have been flushed
-      for (auto& s : my_sends) {  // resend over the mesh (a receiver may see it twice: it dedups)
-        if (!s.second.host) continue;
+      {  // resend over the mesh (a receiver may see it twice: it dedups)
         std::lock_guard<std::mutex> g(I.bmu);
-        I.sends[{s.first->skey, s.first->bi}] = std::move(s.second);
+        size_t k = 0;
+        for (auto& o : ops) {
+          if (!o.send) continue;
+          Impl::Send& s = held[k++];
+          if (s.host) I.sends[{o.e->skey, o.e->bi}] = std::move(s);
+        }
       }
-      for (auto& s : my_sends) mesh_fallback(*s.first);
+      for (auto& o : ops)
+        if (o.send) mesh_fallback(*o.e);
       continue;
     }
     rounds_++;
-    for (auto& s : my_sends) {
-      bulk_bytes_ += s.first->len;
-      std::vector<XMsg> v(1);
-      v[0].type = X_SENT;
-      v[0].skey = s.first->skey;
-      v[0].bi = s.first->bi;
-      v[0].dst_loop = s.first->src_loop;
-      deliver_(s.first->src_loop % nloops_, std::move(v));
-    }
-    for (auto& rcv : my_recvs) {
-      const WireEntry& e = *rcv.first;
+    for (auto& o : ops) {
+      const WireEntry& e = *o.e;
       bulk_bytes_ += e.len;
-      {
+      if (o.send) {
+        std::vector<XMsg> v(1);
+        v[0].type = X_SENT;
+        v[0].skey = e.skey;
+        v[0].bi = e.bi;
+        v[0].dst_loop = e.src_loop;
+        deliver_(e.src_loop % nloops_, std::move(v));
+        continue;
+      }
+      std::vector<XMsg> v(1);
+      if (ex->device()) {
         std::lock_guard<std::mutex> g(I.bmu);
         auto it = I.sinks.find({e.skey, e.bi});
         if (it == I.sinks.end() || !it->second.dev || it->second.cap < e.len) continue;  // session gone
         // HBM → HBM into the owner's shadow slot; complete before the lock drops, so a
         // forget_bulk() that returns guarantees no later write into a released slot
-        if (e.len && (hipMemcpyAsync(it->second.dev, scratch + rcv.second, e.len, hipMemcpyDeviceToDevice, st) !=
-                          hipSuccess ||
-                      hipStreamSynchronize(st) != hipSuccess))
-          continue;
+        if (!ex->to_sink(o, it->second.dev)) continue;
+      } else {
+        v[0].payload = std::move(o.host);  // host executor: the bytes ride the delivery
       }
-      std::vector<XMsg> v(1);
       v[0].type = X_BULK;
       v[0].flags = e.flags;
       v[0].skey = e.skey;
       v[0].bi = e.bi;
-      v[0].a = (int32_t)e.len;  // already in the owner's HBM content arena
+      v[0].a = (int32_t)e.len;  // device executors: already in the owner's HBM content arena
       v[0].b = e.b;
       v[0].src_rank = e.src;
       v[0].dst_loop = e.dst_loop;
       deliver_(e.dst_loop % nloops_, std::move(v));
     }
   }
-  if (comm) ncclCommAbort(comm);
-  if (scratch) hipFree(scratch);
-  if (st) hipStreamDestroy(st);
+  ex.reset();
 }
 
 }  // namespace qmx

@@ -62,9 +62,12 @@ struct XMsg {
 
 struct XOptions {
   int rank = 0, world = 1;
-  std::string transport = "tcp";  // tcp | rccl
+  // tcp: bulk bytes ride the mesh; rccl: RCCL rounds (HBM → HBM); tcpbulk: the same rounds
+  // over a socket per rank pair (CPU / one-GPU rehearsals of the round protocol)
+  std::string transport = "tcp";
   std::string addr = "127.0.0.1";
   int port = 0;                   // mesh: rank r listens on port + r
+  int bulk_port = 0;              // tcpbulk: rank r listens on bulk_port + r (0: port + world)
   int device = 0;
   int batch_us = 50;              // rank 0: announcements arriving within this window share a round
   double timeout_s = 30.0;        // bulk round / epoch formation slower than this = peer failure
@@ -96,7 +99,9 @@ class Exchange {
   bool peer_up(int r) const;
   int rank() const { return o_.rank; }
   int world() const { return o_.world; }
+  // the bulk communicator (RCCL or tcpbulk) of the current epoch is formed
   bool rccl_active() const { return rccl_epoch_.load() > 0 && rccl_ok_.load(); }
+  bool bulk_transport() const { return o_.transport == "rccl" || o_.transport == "tcpbulk"; }
   // counters (/metrics)
   uint64_t rounds() const { return rounds_.load(); }        // RCCL bulk rounds executed here
   uint64_t bytes() const { return bytes_.load(); }          // mesh payload bytes sent + received

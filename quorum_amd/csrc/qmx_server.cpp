@@ -2884,6 +2884,7 @@ int run_server(const ServerCfg& cfg0) {
     o.transport = cfg.xchg;
     o.addr = cfg.xchg_addr;
     o.port = cfg.xchg_port;
+    o.bulk_port = cfg.xchg_bulk_port;
     o.device = cfg.device;
     o.batch_us = cfg.xchg_round_us;
     o.timeout_s = cfg.xchg_timeout;

@@ -63,6 +63,7 @@ struct ServerCfg {
   std::string xchg = "tcp";  // tcp | rccl
   std::string xchg_addr = "127.0.0.1";
   int xchg_port = 0;
+  int xchg_bulk_port = 0;  // tcpbulk: rank r listens on xchg_bulk_port + r (0: xchg_port + world)
   std::string xchg_id_file;
   int xchg_round_us = 200;
   double xchg_timeout = 30.0;

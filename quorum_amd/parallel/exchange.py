@@ -11,8 +11,10 @@ event-driven (an idle node exchanges nothing):
 * bulk (``rccl``): each stream's final text moves from the worker's HBM content arena into
   the owner's HBM shadow slot with ``ncclSend``/``ncclRecv`` over xGMI, in rounds rank 0
   orders (so both ends of every pair post matching operations), and the owner's fused
-  finalize kernel merges remote and local texts.  ``tcp`` (CPU tests) moves the bytes over
-  the mesh instead, as does ``rccl`` while its communicator is (re)forming.
+  finalize kernel merges remote and local texts.  ``tcpbulk`` runs the very same rounds,
+  epochs and fallbacks with a socket per rank pair as the executor (CPU hosts, and rank
+  rehearsals sharing one GPU, where RCCL cannot form).  ``tcp`` moves the bytes over the
+  mesh, as do the others while their communicator is (re)forming.
 
 Every rank must agree on the transport and the mesh base port: :func:`exchange_env` builds
 them once (launcher / bench) and :func:`cluster_config` turns them into the native
@@ -44,8 +46,8 @@ def cluster_config(placement: str, exchange: str, round_us: int, timeout: float,
     xchg = e.get("QMX_XCHG", exchange)
     if xchg == "auto":
         xchg = "rccl" if engine == "hip" else "tcp"
-    if xchg not in ("rccl", "tcp"):
-        raise ValueError(f"runtime.exchange {xchg!r}: expected 'auto', 'rccl' or 'tcp'")
+    if xchg not in ("rccl", "tcp", "tcpbulk"):
+        raise ValueError(f"runtime.exchange {xchg!r}: expected 'auto', 'rccl', 'tcpbulk' or 'tcp'")
     if placement not in ("local", "spread"):
         raise ValueError(f"runtime.placement {placement!r}: expected 'local' or 'spread'")
     nonce = e.get("QMX_XCHG_NONCE", "0")
@@ -53,6 +55,8 @@ def cluster_config(placement: str, exchange: str, round_us: int, timeout: float,
         "rank": r.rank, "world": r.world, "placement": placement, "xchg": xchg,
         "xchg_addr": e.get("QMX_XCHG_ADDR", "127.0.0.1"),
         "xchg_port": int(e.get("QMX_XCHG_PORT", str(port + 7))),
+        # tcpbulk: the round executor's sockets (rank r listens on this + r; 0 = mesh port + world)
+        "xchg_bulk_port": int(e.get("QMX_XCHG_BULK_PORT", "0")),
         "xchg_id_file": "",  # the RCCL unique id travels over the mesh (rank 0 → all)
         # rank 0 batches bulk announcements arriving within this window into one round
         "xchg_round_us": int(e.get("QMX_XCHG_ROUND_US", str(round_us))),

@@ -131,6 +131,10 @@ def test_bench_gpus_flag_self_launches_ranks(tmp_path):
     assert rows[0]["pid"] == res["breakdown_one_rank"]["pid"]
     sc = res["spread_check"]
     assert sc["ok"] is True and sc["requests"] == 4 * 2048 and sc["delta_mismatch"] == 0
+    # the ranks share (no) GPU: the final texts move in tcpbulk rounds — the RCCL round
+    # protocol (announce, rank-0 manifests, epochs) with the socket executor
+    assert sc["transport"] == "tcpbulk" and sc["bulk_formed"] is True
+    assert sc["bulk_rounds"] > 0 and sc["mesh_finals"] == 0 and sc["remote_ends"] == {"text": 4 * 2048}
     assert len({x["pid"] for x in sc["per_rank"]}) == 4
     # every session has one remote stream, run by the next rank: each rank's own counter
     # is its own share, and the shares add up to every session once

@@ -38,21 +38,23 @@ THINK = [sse_chunk({"role": "assistant"}), sse_chunk({"content": "<think>"}), ss
 
 
 @contextlib.contextmanager
-def native_cluster(cfg, world: int, placement: str = "spread"):
-    """`world` native ranks in-process (threads), TCP exchange hub on a free port."""
+def native_cluster(cfg, world: int, placement: str = "spread", xchg: str = "tcp"):
+    """`world` native ranks in-process (threads), TCP exchange on a free port block.
+    ``xchg="tcpbulk"``: final texts move in rank-0-numbered bulk rounds (the RCCL round
+    protocol with a socket executor) instead of riding the mesh."""
     from quorum_amd.runtime.native_server import native_config
 
     ext = native.require()
     cfg = copy.deepcopy(cfg)
     cfg.setdefault("runtime", {})["placement"] = placement
     ports = [free_port() for _ in range(world)]
-    xport = free_port_block(world)  # the mesh: rank r listens on xport + r
+    xport = free_port_block(2 * world)  # the mesh: rank r listens on xport + r (tcpbulk: + world + r)
     threads = []
     # every rank's config first, then the servers: the environment is only changed while no
     # server thread runs (a running server reads it — getenv racing setenv can crash)
     cfgs = []
     for r in range(world):
-        env = {"QMX_RANK": str(r), "QMX_WORLD": str(world), "QMX_XCHG": "tcp", "QMX_XCHG_PORT": str(xport),
+        env = {"QMX_RANK": str(r), "QMX_WORLD": str(world), "QMX_XCHG": xchg, "QMX_XCHG_PORT": str(xport),
                "QMX_XCHG_ROUND_US": "100"}
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
@@ -83,7 +85,8 @@ def native_cluster(cfg, world: int, placement: str = "spread"):
             t0 = time.time()
             while time.time() - t0 < 20:
                 m = httpx.get(f"http://127.0.0.1:{p}/metrics").text
-                if f"qmx_exchange_peers_up {float(world):f}" in m and "qmx_exchange_healthy 1.000000" in m:
+                if (f"qmx_exchange_peers_up {float(world):f}" in m and "qmx_exchange_healthy 1.000000" in m
+                        and (xchg == "tcp" or "qmx_exchange_rccl_active 1.000000" in m)):
                     break
                 time.sleep(0.02)
     try:
@@ -92,6 +95,10 @@ def native_cluster(cfg, world: int, placement: str = "spread"):
         ext.stop_server()
         for th in threads:
             th.join(timeout=15)
+
+
+def _metric(text, name):
+    return float([ln for ln in text.splitlines() if ln.startswith(name + " ")][0].split()[1])
 
 
 def _events(text):
@@ -153,9 +160,9 @@ SPREAD_CASES = {
 }
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world,xchg", [(2, "tcp"), (3, "tcp"), (2, "tcpbulk"), (4, "tcpbulk")])
 @pytest.mark.parametrize("name", sorted(SPREAD_CASES))
-def test_spread_matches_local(name, world):
+def test_spread_matches_local(name, world, xchg):
     n, block, strategy, behs = SPREAD_CASES[name]
     live, ports = _live({f"b{i + 1}": b for i, b in enumerate(behs)})
     try:
@@ -165,7 +172,7 @@ def test_spread_matches_local(name, world):
             ref = httpx.post(f"http://127.0.0.1:{p}/chat/completions", json=req, headers=AUTH, timeout=30)
         ref_calls = sorted(json.dumps(c["body"], sort_keys=True) for c in live.calls)
         live.calls.clear()
-        with native_cluster(cfg, world) as cports:
+        with native_cluster(cfg, world, xchg=xchg) as cports:
             for owner in range(world):  # every rank as session owner
                 r = httpx.post(f"http://127.0.0.1:{cports[owner]}/chat/completions", json=req, headers=AUTH,
                                timeout=30)
@@ -178,6 +185,10 @@ def test_spread_matches_local(name, world):
         assert "qmx_exchange_rounds_total" in m
         remote = float([ln for ln in m.splitlines() if ln.startswith("qmx_remote_streams_total")][0].split()[1])
         assert remote >= 1, m
+        assert _metric(m, "qmx_spread_delta_mismatch_total") == 0
+        if xchg == "tcpbulk" and not block.get("skip_final_aggregation"):
+            # final texts moved by bulk rounds, none over the mesh
+            assert _metric(m, "qmx_exchange_mesh_finals_total") == 0, m
     finally:
         live.close()
 
@@ -208,21 +219,63 @@ def test_spread_many_concurrent_sessions():
         live.close()
 
 
-def test_exchange_transport_selftest_tcp():
-    """Raw transport: 3 ranks, 60 all-gather rounds with payloads below and above the fixed
-    first-phase slot; every rank must receive every rank's exact bytes and flags."""
+def _selftest(world, transport, rounds, env=None, **opts):
     ext = native.require()
-    port = free_port_block(3)
+    port = free_port_block(2 * world)
     res = {}
+    old = {k: os.environ.get(k) for k in (env or {})}
+    os.environ.update(env or {})
 
     def run(r):
-        res[r] = ext.exchange_selftest({"rank": r, "world": 3, "transport": "tcp", "port": port}, 60)
-    ts = [threading.Thread(target=run, args=(r,)) for r in range(3)]
-    for t in ts:
-        t.start()
-    for t in ts:
-        t.join(timeout=60)
-    assert len(res) == 3 and all(v["ok"] for v in res.values()), res
+        res[r] = ext.exchange_selftest(dict({"rank": r, "world": world, "transport": transport, "port": port,
+                                             "timeout": 20.0}, **opts), rounds)
+    try:
+        ts = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=90)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert len(res) == world, res
+    return res
+
+
+def test_exchange_transport_selftest_tcp():
+    """Raw transport: 3 ranks, 60 rounds of deltas and final texts over the mesh; every rank
+    must receive every rank's exact bytes and flags."""
+    res = _selftest(3, "tcp", 60)
+    assert all(v["ok"] for v in res.values()), res
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_exchange_bulk_rounds_tcpbulk(world):
+    """The RCCL round protocol with the socket executor: every rank sends every other rank
+    40 final texts (1 B .. 20 KB) in rank-0-numbered rounds; each pair's transfers run in
+    manifest order (each carries its round/skey/bi/len, so a desynchronised round would
+    fail loudly), every byte is checked, and no text falls back to the mesh."""
+    res = _selftest(world, "tcpbulk", 40)
+    assert all(v["ok"] for v in res.values()), res
+    for v in res.values():
+        assert v["bad"] == 0 and v["bulk"] == 40 * (world - 1)
+        assert v["rccl_rounds"] > 0 and v["mesh_finals"] == 0 and v["epochs"] >= 1
+
+
+def test_exchange_bulk_round_stall_falls_back_and_reforms():
+    """Fault injection: every rank hangs in its 3rd round (QMX_XCHG_FAULT_STALL_ROUND): the
+    round times out, the communicator is dropped everywhere, that round's texts are resent
+    over the mesh — every byte still arrives exactly once-checked — and rank 0 re-forms a
+    new epoch over which the later rounds run again."""
+    res = _selftest(3, "tcpbulk", 40, env={"QMX_XCHG_FAULT_STALL_ROUND": "3"}, round_timeout=0.5, min_epochs=2)
+    assert all(v["ok"] for v in res.values()), res
+    for v in res.values():
+        assert v["bad"] == 0
+        assert v["mesh_finals"] > 0          # the stalled round's texts took the mesh
+        assert v["epochs"] >= 2              # a new communicator formed after the failure
 
 
 def test_idle_cluster_exchanges_nothing():
