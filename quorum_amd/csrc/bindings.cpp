@@ -3,6 +3,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "qmx_env.h"
 #include "qmx_engine.h"
 #include "qmx_hip.h"
 #include "qmx_json.h"
@@ -171,8 +172,13 @@ PYBIND11_MODULE(_qmx, m) {
     json_unescape((const uint8_t*)s.data(), r.str_a, r.str_b, (uint8_t*)&out[0]);
     return py::make_tuple(r.kind, py::bytes(out));
   });
+  // the native side never calls getenv on its threads (qmx_env.h): it reads a snapshot
+  // taken here, on the calling thread, before any server thread starts
+  m.def("env_refresh", &env_refresh,
+        "re-snapshot the process environment for the native side (e.g. a rotated OPENAI_API_KEY)");
   m.def("run_server", [](const py::dict& d) {
     ServerCfg c = server_cfg_from(d);
+    env_refresh();
     py::gil_scoped_release nogil;
     return run_server(c);
   });
@@ -182,6 +188,7 @@ PYBIND11_MODULE(_qmx, m) {
   // mesh and `rounds` final texts through the bulk plane (RCCL p2p rounds from HBM into HBM
   // sinks with transport=rccl, the mesh with tcp); receivers verify every byte.
   m.def("exchange_selftest", [](const py::dict& d, int rounds) {
+    env_refresh();  // fault-injection knobs set by the caller
     XOptions o;
     auto gs = [&](const char* k, std::string& v) { if (d.contains(k)) v = py::cast<std::string>(d[k]); };
     auto gi = [&](const char* k, int& v) { if (d.contains(k)) v = py::cast<int>(d[k]); };
@@ -340,13 +347,21 @@ PYBIND11_MODULE(_qmx, m) {
   py::class_<PyStripper>(m, "Stripper")
       .def(py::init<const std::vector<std::string>&>())
       .def("strip", &PyStripper::strip);
+  env_refresh();
   py::class_<CpuEngine> ce(m, "CpuEngine");
-  ce.def(py::init<const std::vector<std::string>&>());
+  ce.def(py::init([](const std::vector<std::string>& tags) {
+    env_refresh();
+    return new CpuEngine(tags);
+  }));
   bind_engine(ce);
   py::class_<HipEngine> he(m, "HipEngine");
-  he.def(py::init<const std::vector<std::string>&, int, int, int, int, int>(), py::arg("tags"), py::arg("device"),
-         py::arg("tile_bytes") = 16384, py::arg("max_slots") = 8192, py::arg("content_cap") = 1 << 20,
-         py::arg("lanes") = 1);
+  he.def(py::init([](const std::vector<std::string>& tags, int device, int tile, int max_slots, int content_cap,
+                      int lanes) {
+           env_refresh();
+           return new HipEngine(tags, device, tile, max_slots, content_cap, lanes);
+         }),
+         py::arg("tags"), py::arg("device"), py::arg("tile_bytes") = 16384, py::arg("max_slots") = 8192,
+         py::arg("content_cap") = 1 << 20, py::arg("lanes") = 1);
   bind_engine(he);
   he.def("kernel_stats", &HipEngine::kernel_stats);
 }

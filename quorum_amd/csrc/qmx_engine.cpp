@@ -1,4 +1,5 @@
 // qmx_engine.cpp — host engine core + the sequential (oracle-equivalent) CPU algorithms.
+#include "qmx_env.h"
 #include "qmx_engine.h"
 
 #include <cstdlib>
@@ -308,7 +309,7 @@ static double mono_s() {
 }
 
 HostEngine::HostEngine(const std::vector<std::string>& tags) : ts_(make_tagset(tags)) {
-  if (const char* pe = getenv("QMX_PIPELINE")) pipeline_ = atoi(pe) != 0;
+  if (const char* pe = env_get("QMX_PIPELINE")) pipeline_ = atoi(pe) != 0;
 }
 
 int HostEngine::open(int index, bool filter, bool emit, uint32_t* gen) {

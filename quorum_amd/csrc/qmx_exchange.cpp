@@ -1,5 +1,6 @@
 // qmx_exchange.cpp — TCP mesh (control + deltas) and RCCL point-to-point rounds (final
 // texts, HBM to HBM) for spread placement; see qmx_exchange.h.
+#include "qmx_env.h"
 #include "qmx_exchange.h"
 #include "qmx_prof.h"
 
@@ -1069,7 +1070,7 @@ void Exchange::bulk_loop() {
     return;
   }
   int epoch = 0, my_rounds = 0;
-  const int stall_round = getenv("QMX_XCHG_FAULT_STALL_ROUND") ? atoi(getenv("QMX_XCHG_FAULT_STALL_ROUND")) : 0;
+  const int stall_round = env_get("QMX_XCHG_FAULT_STALL_ROUND") ? atoi(env_get("QMX_XCHG_FAULT_STALL_ROUND")) : 0;
   auto drop = [&](bool report) {
     ex->drop();
     rccl_ok_.store(false);

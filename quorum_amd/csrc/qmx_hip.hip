@@ -19,6 +19,7 @@
 //                coalesced 16-B stores to host-mapped output
 //
 // Semantics: SURVEY §2.7 (reference src/quorum/oai_proxy.py:262-371, 578-673).
+#include "qmx_env.h"
 #include "qmx_hip.h"
 
 #include <rocprofiler-sdk-roctx/roctx.h>
@@ -2067,23 +2068,23 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
       max_slots_(max_slots),
       content_cap_((uint32_t)content_cap) {
   HIP_CHECK(hipSetDevice(device_));
-  if (const char* sp = getenv("QMX_WAIT_SPIN_US")) spin_us_ = atoi(sp);
-  if (const char* w = getenv("QMX_WAIT")) poll_ = std::string(w) != "event";
-  if (const char* pu = getenv("QMX_POLL_US")) poll_us_ = std::max(1, atoi(pu));
+  if (const char* sp = env_get("QMX_WAIT_SPIN_US")) spin_us_ = atoi(sp);
+  if (const char* w = env_get("QMX_WAIT")) poll_ = std::string(w) != "event";
+  if (const char* pu = env_get("QMX_POLL_US")) poll_us_ = std::max(1, atoi(pu));
   // a persistent grid assumes its process owns the GPU: grids of several processes on one
   // device (a rehearsal with more ranks than GPUs) need not all be resident at once
-  if (const char* gs = getenv("QMX_GPU_SHARERS")) persistent_ = atoi(gs) <= 1;
-  if (const char* pe = getenv("QMX_PERSISTENT")) persistent_ = atoi(pe) != 0;
-  if (const char* va = getenv("QMX_VIEWS")) views_ = atoi(va) != 0;
-  stage_timing_ = getenv("QMX_STAGE_TIMING") != nullptr;  // read once: getenv scans the environment
-  if (const char* pw = getenv("QMX_PERSISTENT_WG")) p_grid_ = std::min(std::max(8, atoi(pw)), 1024);
-  if (const char* pi = getenv("QMX_PERSISTENT_IDLE_MS")) p_idle_ms_ = std::min(std::max(5, atoi(pi)), 1000);
+  if (const char* gs = env_get("QMX_GPU_SHARERS")) persistent_ = atoi(gs) <= 1;
+  if (const char* pe = env_get("QMX_PERSISTENT")) persistent_ = atoi(pe) != 0;
+  if (const char* va = env_get("QMX_VIEWS")) views_ = atoi(va) != 0;
+  stage_timing_ = env_get("QMX_STAGE_TIMING") != nullptr;  // read once: getenv scans the environment
+  if (const char* pw = env_get("QMX_PERSISTENT_WG")) p_grid_ = std::min(std::max(8, atoi(pw)), 1024);
+  if (const char* pi = env_get("QMX_PERSISTENT_IDLE_MS")) p_idle_ms_ = std::min(std::max(5, atoi(pi)), 1000);
   {
     // HIP streams share GPU_MAX_HW_QUEUES hardware queues round-robin, and a persistent grid
     // holds its queue: a second lane's grid on the same queue would wait for the first to
     // idle out (MI355X, 4 lanes / 4 queues: the first result of a tick came 100 us late).
     // Persistent lanes need a queue each, with one left for everything else.
-    const char* hq = getenv("GPU_MAX_HW_QUEUES");
+    const char* hq = env_get("GPU_MAX_HW_QUEUES");
     const int queues = hq ? std::max(1, atoi(hq)) : 4;
     if (persistent_ && lanes > queues - 1) persistent_ = false;
   }

@@ -1,4 +1,5 @@
 // qmx_prof.cpp — see qmx_prof.h.
+#include "qmx_env.h"
 #include "qmx_prof.h"
 
 #include <dlfcn.h>
@@ -194,7 +195,7 @@ void crash_handler_install() {
 }
 
 void prof_start() {
-  const char* p = getenv("QMX_PROF");
+  const char* p = env_get("QMX_PROF");
   if (!p || !*p || g_ring) return;
   g_path = p;
   const size_t at = g_path.find("%p");  // per-process file: %p -> pid
@@ -208,7 +209,7 @@ void prof_start() {
   sa.sa_flags = SA_SIGINFO | SA_RESTART;
   sigemptyset(&sa.sa_mask);
   sigaction(SIGPROF, &sa, nullptr);
-  if (const char* e = getenv("QMX_PROF_US")) g_us = std::max(50, atoi(e));
+  if (const char* e = env_get("QMX_PROF_US")) g_us = std::max(50, atoi(e));
   // Only per-thread CPU-time timers (prof_thread, armed by every hot thread): a process-wide
   // ITIMER_PROF signal may be delivered to any thread, including one blocked in a join, and
   // would charge its stack with CPU it never used.  The kernel checks thread CPU timers at

@@ -1,4 +1,5 @@
 // qmx_server.cpp — native epoll data plane (see qmx_server.h).
+#include "qmx_env.h"
 #include "qmx_server.h"
 
 #include <arpa/inet.h>
@@ -97,7 +98,7 @@ using Clock = std::chrono::steady_clock;
 inline double now_s() { return std::chrono::duration<double>(Clock::now().time_since_epoch()).count(); }
 // QMX_* on/off knobs, read once where a loop or engine is built ("0" / "false": off)
 inline bool env_flag(const char* name, bool dflt) {
-  const char* v = getenv(name);
+  const char* v = env_get(name);
   if (!v || !*v) return dflt;
   return !(std::strcmp(v, "0") == 0 || std::strcmp(v, "false") == 0);
 }
@@ -1466,8 +1467,11 @@ class Loop {
     }
     if (!has_auth) {
       std::string env_key = cfg_.env_api_key;
-      if (cfg_.api_key_from_env) {  // per request, like os.environ.get (a rotated key applies at once)
-        const char* e = getenv("OPENAI_API_KEY");
+      if (cfg_.api_key_from_env) {
+        // per request, like os.environ.get (oai_proxy.py:981), from the environment snapshot
+        // (qmx_env.h: getenv on an io thread can race a library's setenv and fault); a key
+        // rotated inside this process applies once env_refresh() re-snapshots it
+        const char* e = env_get("OPENAI_API_KEY");
         env_key = e ? e : "";
       }
       if (env_key.empty()) {
@@ -2801,7 +2805,7 @@ class Loop {
   std::vector<Deferred> deferq_;
   uint64_t next_serial_ = 0;
   const double role_defer_s_ = [] {
-    const char* e = getenv("QMX_ROLE_DEFER_US");
+    const char* e = env_get("QMX_ROLE_DEFER_US");
     return (e ? atof(e) : 1000.0) * 1e-6;
   }();
   std::vector<EngineOp> ops_;  // engine feed / finish / release of this iteration (flush_ops)
@@ -2813,7 +2817,7 @@ class Loop {
   std::string role_head_;
   // fault injection (tests): drop every Nth stream result's SSE bytes before it is sent
   const long fault_drop_every_ = [] {
-    const char* e = getenv("QMX_FAULT_DROP_DELTA");
+    const char* e = env_get("QMX_FAULT_DROP_DELTA");
     return e ? atol(e) : 0L;
   }();
   long fault_n_ = 0;
@@ -2827,6 +2831,7 @@ void on_signal(int sig) {
 }  // namespace
 
 int run_server(const ServerCfg& cfg0) {
+  env_refresh();  // before any thread: the io loops, lanes and exchange read this snapshot
   ServerCfg cfg = cfg0;
   crash_handler_install();  // a native fault leaves a backtrace on stderr, not a silent exit
   prof_start();  // QMX_PROF=<path>: CPU sampling profile of this process (qmx_prof.h)

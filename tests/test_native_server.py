@@ -457,10 +457,12 @@ def test_native_api_key_read_per_request(monkeypatch):
             url = f"http://127.0.0.1:{port}/chat/completions"
             assert httpx.post(url, json=req, timeout=30).status_code == 401
             monkeypatch.setenv("OPENAI_API_KEY", "rotated-key")
+            native.require().env_refresh()  # the native threads read a snapshot, never environ
             r = httpx.post(url, json=req, timeout=30)
             assert r.status_code == 200
             assert live.calls[-1]["headers"]["authorization"] == "Bearer rotated-key"
             monkeypatch.delenv("OPENAI_API_KEY")
+            native.require().env_refresh()
             r = httpx.post(url, json=req, timeout=30)
             assert r.status_code == 401 and r.json()["error"]["type"] == "auth_error"
     finally:
