@@ -23,11 +23,16 @@ TagSet make_tagset(const std::vector<std::string>& tags) {
     std::string t;
     for (char c : t0) t.push_back((char)lower_ascii((uint8_t)c));
     if (std::find(seen.begin(), seen.end(), t) != seen.end()) continue;
-    if (t.empty() || (int)t.size() > kMaxTagLen) throw std::invalid_argument("unsupported tag length: " + t0);
-    for (char c : t) {
-      bool ok = (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9') || c == '_' || c == '-' || c == ':';
+    // regex metacharacters change what quorum's alternation matches (oai_proxy.py:137,
+    // 271-274); '<', '>' and '/' in a tag let one tag's pattern start inside another's, so
+    // the token model (at most one pattern per '<') would not hold; non-ASCII would need
+    // Unicode case folding.  Everything else is literal, exactly as in the regex.
+    for (char ch : t) {
+      const uint8_t c = (uint8_t)ch;
+      const bool ok = c >= 0x20 && c < 0x7f && !std::strchr(".^$*+?{}[]\\|()<>/", (int)c);
       if (!ok) throw std::invalid_argument("tag needs regex semantics: " + t0);
     }
+    if (t.empty() || (int)t.size() > kMaxTagLen) throw std::invalid_argument("unsupported tag length: " + t0);
     if (ts.n >= kMaxTags) throw std::invalid_argument("too many thinking tags");
     seen.push_back(t);
     ts.len[ts.n] = (int)t.size();

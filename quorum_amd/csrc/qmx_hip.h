@@ -78,10 +78,14 @@ enum WorkStatus : uint32_t { WS_DONE = 1, WS_ABORTED = 2, WS_STARTED = 4, WS_ESC
 struct KParams {
   TagSet ts;
   int npat;
-  int32_t pat_E[2 * kMaxTags];  // Σ_j m(q0²+q1²) per pattern (match iff dot == -E)
-  // MFMA B operand (patterns × window features) per lane, built once on the host:
-  // lane l = pattern (l & 15), feature group (l >> 4): 0: -2·q0, 1: -2·q1, 2/3: mask
-  alignas(16) int8_t bfrag[64 * 16];
+  int32_t pat_E[2 * kMaxTags];  // Σ_j m(q0²+q1²) over the window part of each pattern (match iff dot == -E)
+  // byte → matcher code: 1..94 for the bytes that occur in patterns (letters folded), 95 for
+  // every other byte (never equal to a pattern byte), 0 past the end of the text
+  alignas(16) uint8_t code[256];
+  // MFMA B operand (patterns × window features) per lane, built once on the host, one
+  // 16-pattern column block per MFMA: lane l = pattern 16·blk + (l & 15), feature group
+  // (l >> 4): 0: -2·q0, 1: -2·q1, 2/3: mask (q = code, q0 = q & 7, q1 = q >> 3)
+  alignas(16) int8_t bfrag[2][64 * 16];
   uint32_t content_cap;
   int pre1_len, pre2_len, suf_len;
   char pre1[48];

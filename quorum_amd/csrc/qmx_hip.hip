@@ -71,7 +71,7 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 
 struct Smem {
   alignas(16) uint8_t A[TILE_MAX + 64];  // X (input) → W (kept bytes) / output window
-  alignas(16) uint8_t B[TILE_MAX + 64];  // Z = tail ++ decoded deltas (at B+PAD) → output window
+  alignas(16) uint8_t B[TILE_MAX + 128];  // Z = tail (<= 63) ++ decoded deltas (at B+PAD) → output window
   uint16_t ev_a[MAX_EV], ev_b[MAX_EV], ev_sa[MAX_EV], ev_sb[MAX_EV], ev_dl[MAX_EV];
   uint8_t ev_kind[MAX_EV];
   uint16_t dl_end[MAX_EV];
@@ -209,32 +209,29 @@ struct DepthOp {
 // ------------------------------------------------------------------------------------
 // MFMA tag matcher
 // ------------------------------------------------------------------------------------
-__device__ inline int code_of(uint8_t b) {
-  if (b >= 'a' && b <= 'z') return b - 'a' + 1;
-  if (b >= 'A' && b <= 'Z') return b - 'A' + 1;
-  if (b >= '0' && b <= '9') return 27 + b - '0';
-  switch (b) {
-    case '<': return 37;
-    case '/': return 38;
-    case '>': return 39;
-    case '_': return 40;
-    case '-': return 41;
-    case ':': return 42;
-    default: return 63;
-  }
-}
-
-// B operand (patterns × window features): host-built per lane (KParams::bfrag), one
-// 16-byte LDS read per lane instead of per-byte pattern decoding.
-__device__ inline v4i build_pattern_frag(const KParams& P) {
+// B operand (patterns × window features) of column block `blk`: host-built per lane
+// (KParams::bfrag), one 16-byte LDS read per lane instead of per-byte pattern decoding.
+__device__ inline v4i build_pattern_frag(const KParams& P, int blk) {
   v4i b;
-  __builtin_memcpy(&b, &P.bfrag[(threadIdx.x & 63) * 16], 16);
+  __builtin_memcpy(&b, &P.bfrag[blk][(threadIdx.x & 63) * 16], 16);
   return b;
 }
 
-// 16 candidate windows per MFMA; result[row][pat] == -E[pat]  <=>  window == pattern.
+// pattern t's bytes past the 16-byte window at Z[p ...) (patterns longer than the window)
+__device__ inline bool pattern_tail_ok(const uint8_t* Z, int Zn, int p, int t, const KParams& P) {
+  const int L = pattern_len(P.ts, t);
+  if (p + L > Zn) return false;
+  for (int j = kWindow; j < L; ++j)
+    if (lower_ascii(Z[p + j]) != pattern_byte(P.ts, t, j)) return false;
+  return true;
+}
+
+// 16 candidate windows per MFMA and 16 patterns per column block; result[row][pat] ==
+// -E[pat]  <=>  the window equals the pattern's first 16 bytes (all of it for tags up to
+// 13 bytes; longer patterns then compare their tail).  Distinct tags never both match at
+// one '<' (make_tagset), so at most one column of a row survives.
 __device__ inline void mfma_match_group(const uint8_t* Z, int Zn, const uint16_t* cand, int ncand, int g,
-                                        const KParams& P, v4i bfrag, int8_t* cand_tok) {
+                                        const KParams& P, v4i bf0, v4i bf1, int8_t* cand_tok) {
   int l = threadIdx.x & 63, r = l & 15, kg = l >> 4;
   int c = g * 16 + r;
   int p = c < ncand ? (int)cand[c] : -1;
@@ -250,21 +247,25 @@ __device__ inline void mfma_match_group(const uint8_t* Z, int Zn, const uint16_t
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const uint8_t zb = (uint8_t)((j < 8 ? w0 : w1) >> ((j & 7) * 8));
-    int code = j < nv ? code_of(zb) : 0;
-    int d0 = code & 7, d1 = code >> 3;
+    int code = j < nv ? (int)P.code[zb] : 0;
+    int d0 = code & 7, d1 = code >> 3;  // d1 <= 11: d1² fits an int8
     bytes[j] = (int8_t)(kg == 0 ? d0 : kg == 1 ? d1 : kg == 2 ? d0 * d0 : d1 * d1);
   }
   v4i a;
   __builtin_memcpy(&a, bytes, 16);
-  v4i acc = {0, 0, 0, 0};
-  acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bfrag, acc, 0, 0, 0);
-  int t = l & 15;
+  const int nblk = P.npat > 16 ? 2 : 1;
+  for (int blk = 0; blk < nblk; ++blk) {
+    v4i acc = {0, 0, 0, 0};
+    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, blk ? bf1 : bf0, acc, 0, 0, 0);
+    const int t = 16 * blk + (l & 15);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int row = 4 * (l >> 4) + i;
-    int cc = g * 16 + row;
-    if (t < P.npat && cc < ncand && acc[i] == -P.pat_E[t])
-      cand_tok[cc] = (int8_t)(t < P.ts.n ? t + 1 : -(t - P.ts.n + 1));
+    for (int i = 0; i < 4; ++i) {
+      int row = 4 * (l >> 4) + i;
+      int cc = g * 16 + row;
+      if (t < P.npat && cc < ncand && acc[i] == -P.pat_E[t] &&
+          (pattern_len(P.ts, t) <= kWindow || pattern_tail_ok(Z, Zn, (int)cand[cc], t, P)))
+        cand_tok[cc] = (int8_t)(t < P.ts.n ? t + 1 : -(t - P.ts.n + 1));
+    }
   }
 }
 
@@ -1083,9 +1084,9 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     for (int c = tid; c < ncand; c += BS) s.cand_tok[c] = 0;
     __syncthreads();
     {
-      v4i bfrag = build_pattern_frag(P);
+      const v4i bf0 = build_pattern_frag(P, 0), bf1 = build_pattern_frag(P, P.npat > 16 ? 1 : 0);
       int w = tid >> 6;
-      for (int g = w; g * 16 < ncand; g += BS / 64) mfma_match_group(Z, Zn, s.cand, ncand, g, P, bfrag, s.cand_tok);
+      for (int g = w; g * 16 < ncand; g += BS / 64) mfma_match_group(Z, Zn, s.cand, ncand, g, P, bf0, bf1, s.cand_tok);
     }
     __syncthreads();
     QMX_STAMP(6);
@@ -2095,33 +2096,42 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
   std::memset(&base_params_, 0, sizeof(base_params_));
   base_params_.ts = ts_;
   base_params_.npat = 2 * ts_.n;
+  // matcher codes: every byte that occurs in a pattern gets its own code (letters: one code
+  // for both cases, the tags' IGNORECASE), everything else shares code 95
+  {
+    int next = 1;
+    for (int b = 0; b < 256; ++b) base_params_.code[b] = 95;
+    for (int p = 0; p < base_params_.npat; ++p)
+      for (int j = 0; j < pattern_len(ts_, p); ++j) {
+        const uint8_t b = pattern_byte(ts_, p, j);
+        if (base_params_.code[b] != 95) continue;
+        if (next > 94) throw std::invalid_argument("thinking tags use more than 94 distinct characters");
+        base_params_.code[b] = (uint8_t)next;
+        if (b >= 'a' && b <= 'z') base_params_.code[b - 32] = (uint8_t)next;
+        ++next;
+      }
+  }
   for (int p = 0; p < base_params_.npat; ++p) {
     int E = 0;
-    for (int j = 0; j < pattern_len(ts_, p); ++j) {
-      uint8_t b = pattern_byte(ts_, p, j);
-      int q = (b >= 'a' && b <= 'z') ? b - 'a' + 1 : (b >= '0' && b <= '9') ? 27 + b - '0'
-              : b == '<' ? 37 : b == '/' ? 38 : b == '>' ? 39 : b == '_' ? 40 : b == '-' ? 41 : b == ':' ? 42 : 63;
+    for (int j = 0; j < std::min(kWindow, pattern_len(ts_, p)); ++j) {
+      const int q = base_params_.code[pattern_byte(ts_, p, j)];
       E += (q & 7) * (q & 7) + (q >> 3) * (q >> 3);
     }
     base_params_.pat_E[p] = E;
   }
   base_params_.content_cap = content_cap_;
-  auto code_host = [](uint8_t b) {
-    return (b >= 'a' && b <= 'z') ? b - 'a' + 1 : (b >= 'A' && b <= 'Z') ? b - 'A' + 1
-           : (b >= '0' && b <= '9') ? 27 + b - '0' : b == '<' ? 37 : b == '/' ? 38 : b == '>' ? 39
-           : b == '_' ? 40 : b == '-' ? 41 : b == ':' ? 42 : 63;
-  };
-  for (int l = 0; l < 64; ++l) {
-    const int t = l & 15, kg = l >> 4;
-    for (int j = 0; j < 16; ++j) {
-      int v = 0;
-      if (t < base_params_.npat && j < pattern_len(ts_, t)) {
-        const int q = code_host(pattern_byte(ts_, t, j));
-        v = kg == 0 ? -2 * (q & 7) : kg == 1 ? -2 * (q >> 3) : 1;
+  for (int blk = 0; blk < 2; ++blk)
+    for (int l = 0; l < 64; ++l) {
+      const int t = 16 * blk + (l & 15), kg = l >> 4;
+      for (int j = 0; j < 16; ++j) {
+        int v = 0;
+        if (t < base_params_.npat && j < pattern_len(ts_, t)) {
+          const int q = base_params_.code[pattern_byte(ts_, t, j)];
+          v = kg == 0 ? -2 * (q & 7) : kg == 1 ? -2 * (q >> 3) : 1;
+        }
+        base_params_.bfrag[blk][l * 16 + j] = (int8_t)v;
       }
-      base_params_.bfrag[l * 16 + j] = (int8_t)v;
     }
-  }
   for (int i = 0; i < std::max(1, lanes); ++i) {
     std::unique_ptr<TickLane> L(new TickLane());
     HIP_CHECK(hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking));

@@ -16,10 +16,16 @@
 
 namespace qmx {
 
-constexpr int kMaxTags = 8;
-constexpr int kMaxTagLen = 13;   // "</" + 13 + ">" = 16-byte MFMA window
+// Tag sets the native engines run exactly ("<= ~16 tags"): up to 16 distinct
+// (lowercased) tags of up to 61 printable-ASCII bytes with no regex metacharacter and no
+// '<', '>' or '/'.  The MFMA matcher compares a 16-byte window per candidate '<' (a pattern
+// longer than that — "</" + tag + ">" beyond 16 bytes — is a window prefix match plus a
+// compare of its tail bytes), 16 patterns per MFMA column block (open + close of 16 tags:
+// two blocks).  The holdback of a partial tag is at most the longest pattern - 1 bytes.
+constexpr int kMaxTags = 16;
+constexpr int kMaxTagLen = 61;   // "</" + 61 + ">" = 64 bytes
 constexpr int kWindow = 16;
-constexpr int kMaxTail = 16;
+constexpr int kMaxTail = 64;
 constexpr int kJsonMaxDepth = 256;  // deeper == RecursionError (stream abort)
 
 // ---------------------------------------------------------------------------

@@ -53,15 +53,21 @@ class FinalizeRequest:
     created: int = 0
 
 
-_PLAIN_TAG = re.compile(r"^[A-Za-z0-9_:\-]+$")
+# printable ASCII with no regex metacharacter (quorum alternates the tags unescaped into
+# its patterns, oai_proxy.py:137, 271-274) and no '<', '>' or '/' (one tag's pattern could
+# then start inside another's, which the token model of the native matchers excludes)
+_PLAIN_TAG = re.compile(r"^[ -~]+$")
+_NOT_PLAIN = set(".^$*+?{}[]\\|()<>/")
 
 
-def native_tag_ok(tags: Sequence[str], max_tags: int = 8, max_len: int = 13) -> bool:
-    """Tags the native/GPU matchers support exactly: plain ASCII (no regex metachar),
-    ≤ 8 distinct (lowercased) tags, each ≤ 13 chars (``</tag>`` fits a 16-byte window).
+def native_tag_ok(tags: Sequence[str], max_tags: int = 16, max_len: int = 61) -> bool:
+    """Tags the native/GPU matchers run exactly (qmx_text.h): literal printable ASCII, at
+    most 16 distinct (lowercased) tags of at most 61 bytes — the MFMA matcher compares a
+    16-byte window per '<' and the tail of longer patterns, two 16-pattern column blocks.
     Anything else runs on the python engine with real regex semantics."""
     low = {t.lower() for t in tags}
-    return (0 < len(low) <= max_tags and all(_PLAIN_TAG.match(t) and len(t) <= max_len for t in low))
+    return (0 < len(low) <= max_tags
+            and all(_PLAIN_TAG.match(t) and not (set(t) & _NOT_PLAIN) and len(t) <= max_len for t in low))
 
 
 class PyEngine:

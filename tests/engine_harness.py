@@ -24,6 +24,35 @@ def rand_text(rng: random.Random, n: int) -> str:
     return "".join(rng.choice(ALPHABET) for _ in range(n))
 
 
+# the widest tag set the native engines take (qmx_text.h): 16 distinct tags, long ones
+# (18-33 bytes: patterns past the 16-byte MFMA window, including two that share their first
+# 28 bytes), spaces and ASCII symbols that are literal in quorum's regex
+WIDE_TAGS = ["think", "reason", "reasoning", "thought", "internal_monologue", "scratch pad", "a=b", "x#1",
+             "chain_of_thought_reasoning_v2", "chain_of_thought_reasoning_v3", "plan!", "t", "reflection",
+             "self-critique:draft", "q&a", "analysis_of_the_problem_statement"]
+
+
+def wide_alphabet(tags: Sequence[str]) -> List[str]:
+    """Pieces that build whole, case-varied, split and near-miss tags of `tags` (a near miss
+    differs in its last name byte: it passes a 16-byte window test and fails the tail)."""
+    out = ["<", "</", ">", " ", "\n", "é", "😀", "a", "Z", "0", '"', "\\"]
+    for t in tags:
+        h = len(t) // 2
+        out += [f"<{t}>", f"</{t}>", f"<{t.upper()}>", f"</{t.title()}>", "<" + t[:h], t[h:] + ">", "</" + t[:h],
+                f"<{t[:-1]}~>", f"</{t[:-1]}~>", t]
+    return out
+
+
+def rand_wide_text(rng: random.Random, n: int, alphabet: Sequence[str]) -> str:
+    return "".join(rng.choice(alphabet) for _ in range(n))
+
+
+def rand_wide_stream(rng: random.Random, alphabet: Sequence[str]) -> bytes:
+    parts = [event_bytes(rng, rand_wide_text(rng, rng.randint(0, 10), alphabet)) for _ in range(rng.randint(1, 12))]
+    parts.append(b"data: [DONE]\n\n")
+    return b"".join(parts)
+
+
 def event_bytes(rng: random.Random, content) -> bytes:
     """One upstream SSE event with a random (valid) JSON shape around `content`."""
     delta = {"content": content}

@@ -46,6 +46,24 @@ def _check(seed, n_streams, hip_kw=None, max_piece=None):
     assert ct == gt
 
 
+@pytest.mark.parametrize("seed", range(24))
+def test_hip_matches_cpu_wide_tags(ext, seed):
+    """16 tags (two MFMA column blocks), 18-33-byte tags (window prefix match + tail compare,
+    near misses that differ only past the window), spaces and symbols, long holdbacks across
+    tile boundaries: HIP == C++ CPU engine (== the python oracle, test_native_differential)."""
+    rng = random.Random(seed)
+    tags = rng.sample(H.WIDE_TAGS, rng.randint(9, 16))
+    alpha = H.wide_alphabet(tags)
+    raw = [H.rand_wide_stream(rng, alpha) for _ in range(rng.choice([4, 24]))]
+    streams = [H.split_random(rng, r, rng.choice([3, 17, 64, 400])) for r in raw]
+    filt = [rng.random() < 0.9 for _ in raw]
+    emit = [rng.random() < 0.9 for _ in raw]
+    tseed = rng.randint(0, 10**9)
+    cpu = H.run_engine(NativeEngine("cpu", tags), streams, filt, emit, random.Random(tseed))
+    hip = H.run_engine(_hip(tags), streams, filt, emit, random.Random(tseed))
+    assert hip == cpu, (tags, raw)
+
+
 @pytest.mark.parametrize("seed", range(60))
 def test_hip_matches_cpu_random(ext, seed):
     _check(seed, 6)

@@ -96,6 +96,71 @@ def test_strip_random(pieces, tags):
     assert got == exp, text
 
 
+# ---------------------------------------------------------------- wide tag sets
+WIDE_ALPHA = H.wide_alphabet(H.WIDE_TAGS)
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.lists(st.sampled_from(WIDE_ALPHA), max_size=40), st.integers(0, 2**32 - 1),
+       st.integers(1, len(H.WIDE_TAGS)))
+def test_filter_wide_tags_random_chunks(pieces, seed, ntags):
+    """16 tags, 18-33-byte tags, spaces and symbols: the native streaming filter equals the
+    oracle at every chunk boundary (and the holdback of a partial long tag is exact)."""
+    rng = random.Random(seed)
+    tags = rng.sample(H.WIDE_TAGS, ntags)
+    text = "".join(pieces)
+    py = ref.ThinkingTagFilter(tags)
+    nat = _ext().StreamFilter([t.lower() for t in tags])
+    i = 0
+    while i <= len(text):
+        k = rng.randint(0, 9)
+        chunk = text[i:i + k]
+        assert nat.feed(chunk.encode()).decode() == py.feed(chunk), (tags, text, i, k)
+        i += max(k, 1)
+    assert nat.flush().decode() == py.flush()
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.lists(st.sampled_from(WIDE_ALPHA), max_size=50), st.integers(0, 2**32 - 1))
+def test_strip_wide_tags(pieces, seed):
+    tags = random.Random(seed).sample(H.WIDE_TAGS, random.Random(seed).randint(1, 16))
+    text = "".join(pieces)
+    assert native.strip_fn(tags)(text, True) == ref.strip_thinking_tags(text, tags), (tags, text)
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_cpu_engine_matches_python_wide_tags(seed):
+    rng = random.Random(seed)
+    tags = rng.sample(H.WIDE_TAGS, rng.randint(8, 16))
+    alpha = H.wide_alphabet(tags)
+    raw = [H.rand_wide_stream(rng, alpha) for _ in range(4)]
+    streams = [H.split_random(rng, r, rng.choice([3, 17, 64, 400])) for r in raw]
+    filt, emit = [True] * 4, [True] * 4
+    ts = rng.randint(0, 10**9)
+    py = H.run_engine(H.python_engine(tags), streams, filt, emit, random.Random(ts))
+    nat = H.run_engine(NativeEngine("cpu", tags), streams, filt, emit, random.Random(ts))
+    assert py == nat, (tags, raw)
+
+
+def test_native_tag_rules():
+    """What the native engines take (16 literal tags <= 61 bytes) and what stays on the
+    python engine: regex metacharacters (quorum alternates tags unescaped), '<', '>', '/',
+    non-ASCII, more than 16 distinct tags, longer tags."""
+    from quorum_amd.ops.engine import native_tag_ok
+
+    assert native_tag_ok(H.WIDE_TAGS)
+    assert native_tag_ok(["x" * 61]) and not native_tag_ok(["x" * 62])
+    assert native_tag_ok(H.WIDE_TAGS + ["THINK"])  # 16 distinct after lowercasing
+    assert not native_tag_ok(H.WIDE_TAGS + ["extra"])
+    for bad in ["a.b", "a|b", "th(ink)", "x*", "a+", "q?", "[x]", "{2}", "^a", "a$", "a\\d", "<a", "a>", "a/b",
+                "é", ""]:
+        assert not native_tag_ok(["think", bad]), bad
+    ext = _ext()
+    for bad in ["a.b", "a/b", "é"]:
+        with pytest.raises(ValueError, match="regex semantics"):
+            ext.StreamFilter(["think", bad])
+
+
 # ---------------------------------------------------------------- whole engine
 def _compare(seed, n_streams=4):
     rng = random.Random(seed)

@@ -38,7 +38,19 @@ def split7(chunks):
     return [raw[i:i + 7] for i in range(0, len(raw), 7)]
 
 
+WIDE_TAGS = ["think", "reason", "reasoning", "thought", "internal_monologue", "scratch pad", "a=b", "x#1",
+             "chain_of_thought_reasoning_v2", "chain_of_thought_reasoning_v3", "plan!", "t", "reflection",
+             "self-critique:draft", "q&a", "analysis_of_the_problem_statement"]
+WIDE = [sse_chunk({"role": "assistant"}), sse_chunk({"content": "Hi <internal_mono"}),
+        sse_chunk({"content": "logue>secret</INTERNAL_MONOLOGUE> and <chain_of_thought_reasoning_v"}),
+        sse_chunk({"content": "2>x</chain_of_thought_reasoning_v3>y</chain_of_thought_reasoning_v2>!"}),
+        sse_chunk({"content": " <scratch pad>s</scratch pad><q&a>z</q&a> <chain_of_thought_reasoning_vX>kept"}),
+        sse_chunk({}, finish="stop"), b"data: [DONE]\n\n"]
+
 SCENARIOS = {
+    "par_stream_wide_tags": (cfg_parallel(2, block=dict(CONCAT, hide_final_think=True, thinking_tags=WIDE_TAGS)),
+                             {"b1.test": ("stream", 200, split7(WIDE)), "b2.test": ("stream", 200, WIDE)},
+                             {"messages": MSG, "stream": True}, AUTH),
     "par_stream_concat": (cfg_parallel(2, block=CONCAT),
                           {"b1.test": ("stream", 200, sse_stream(["Hel", "lo"])),
                            "b2.test": ("stream", 200, sse_stream(["Wor", "ld"]))},
@@ -467,6 +479,17 @@ def test_native_api_key_read_per_request(monkeypatch):
             assert r.status_code == 401 and r.json()["error"]["type"] == "auth_error"
     finally:
         live.close()
+
+
+def test_native_config_tag_rules():
+    """The native server starts with 16 tags and 30+-byte tags; a tag with a regex
+    metacharacter is still refused with the same message (it needs --impl python)."""
+    from quorum_amd.runtime.native_server import NativeUnsupported, native_config
+
+    cfg = cfg_parallel(2, block=dict(CONCAT, thinking_tags=WIDE_TAGS))
+    assert native_config(cfg, "127.0.0.1", 1, "cpu", 0, 1)["tags"] == WIDE_TAGS
+    with pytest.raises(NativeUnsupported, match="need regex semantics: run with --impl python"):
+        native_config(cfg_parallel(2, block=dict(CONCAT, thinking_tags=["think", "th.nk"])), "127.0.0.1", 1, "cpu", 0, 1)
 
 
 def test_native_serves_fastapi_doc_routes():
