@@ -63,11 +63,16 @@ enum : uint8_t {
   F_RCCL_DOWN = 105, // any rank → rank 0: my communicator failed (a = epoch)
 };
 
-std::string frame(const XMsg& m) {
+void put_frame(std::string& out, const XMsg& m, const char* payload, size_t n) {
   WireHdr h{m.type, m.flags, m.dst_loop, m.src_loop, 0, m.dst_rank, m.src_rank, m.bi, m.skey, m.a, m.b,
-            (uint32_t)m.payload.size()};
-  std::string s((const char*)&h, sizeof(h));
-  s += m.payload;
+            (uint32_t)n};
+  out.append((const char*)&h, sizeof(h));
+  out.append(payload, n);
+}
+std::string frame(const XMsg& m) {
+  std::string s;
+  s.reserve(sizeof(WireHdr) + m.payload.size());
+  put_frame(s, m, m.payload.data(), m.payload.size());
   return s;
 }
 
@@ -514,6 +519,30 @@ void Exchange::post(XMsg&& m) {
   if (stop_.load() || m.dst_rank < 0 || m.dst_rank >= o_.world) return;
   const int r = m.dst_rank;
   im_->enqueue(r, frame(m));
+}
+
+void Exchange::append_frame(std::string& out, const XMsg& hdr, const char* payload, size_t n) {
+  put_frame(out, hdr, payload, n);
+}
+
+void Exchange::post_frames(int dst, std::string& frames) {
+  if (frames.empty()) return;
+  if (stop_.load() || dst < 0 || dst >= o_.world) {
+    frames.clear();
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> g(im_->omu);
+    if (dst == o_.rank) {
+      im_->local_frames.emplace_back(dst, std::move(frames));
+    } else if (im_->posted[dst].empty()) {
+      im_->posted[dst].swap(frames);  // the common case: no copy at all
+    } else {
+      im_->posted[dst] += frames;
+    }
+  }
+  frames.clear();
+  im_->wake();
 }
 
 bool Exchange::peer_up(int r) const {

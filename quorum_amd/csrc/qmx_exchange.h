@@ -85,6 +85,11 @@ class Exchange {
   Exchange(const XOptions& o, int nloops, Deliver deliver);
   ~Exchange();
   void post(XMsg&& m);  // thread-safe: control / delta message to m.dst_rank over the mesh
+  // Batched posting (an io loop's messages of one event-loop pass): frames are encoded by the
+  // caller straight into a per-destination buffer (append_frame: one copy of each payload),
+  // then handed over with one lock and one mesh-thread wake (post_frames clears `frames`).
+  static void append_frame(std::string& out, const XMsg& hdr, const char* payload, size_t n);
+  void post_frames(int dst_rank, std::string& frames);
   // Worker: ship stream (hdr.skey, hdr.bi)'s final text to hdr.dst_rank.  `dev` points at
   // `len` bytes in HBM that stay valid until X_SENT comes back to hdr.src_loop; `host`
   // produces the bytes for the mesh fallback.  hdr.flags / hdr.b travel with it.

@@ -928,6 +928,7 @@ class Loop {
       if (!deferq_.empty()) release_deferred(now_s());
       if (!flushq_.empty()) flush_queued();
       if (!pending_close_.empty()) reap_clients();
+      flush_x();
     }
   }
   // deferred heads whose deadline passed are queued for this iteration's flush; entries whose
@@ -1077,7 +1078,7 @@ class Loop {
         r.clear_sse();  // QMX_FAULT_DROP_DELTA: fault injection (the bench's validator must notice)
       if (!r.empty()) {
         if (s->kind == K_REMOTE) {
-          post_owner(s, X_DATA, 0, 0, std::string(r.data(), r.size()));
+          post_owner(s, X_DATA, 0, 0, r.data(), r.size());  // framed from the view: one copy
           s->data_sent++;
         }
         else if (s->cl) send_content(s, r.data(), r.size());
@@ -2079,7 +2080,7 @@ class Loop {
         m.a = valid[i];
         m.b = (int)(cfg_.timeout * 1000.0);
         m.payload = build_req(cfg_.backends[valid[i]], s->fwd, body);
-        xch_->post(std::move(m));
+        xq(m);
         continue;
       }
       Up* u = open_up(s, (int)i, valid[i], UP_ENGINE, build_req(cfg_.backends[valid[i]], s->fwd, body), cfg_.timeout);
@@ -2127,6 +2128,7 @@ class Loop {
       HostEngine* e = &eng();
       const int slot = b.slot;
       s->bulk_pending = true;
+      flush_x();  // the stream's deltas go out ahead of its final text
       xch_->send_bulk(std::move(h), dev, len, [e, slot] { return e->text(slot); });
       return;
     }
@@ -2140,6 +2142,23 @@ class Loop {
     kick();
   }
   void post_owner(Session* s, uint8_t type, uint8_t flags, int a, const std::string& payload, int b = 0) {
+    post_owner(s, type, flags, a, payload.data(), payload.size(), b);
+  }
+  // mesh messages of this loop pass, framed per destination rank and handed to the exchange
+  // once per pass (flush_x: one lock + one wake), not one locked post + wake per message
+  void xq(const XMsg& hdr, const char* payload, size_t n) {
+    if (!xch_) return;
+    if (xout_.size() < (size_t)xch_->world()) xout_.resize(xch_->world());
+    Exchange::append_frame(xout_[hdr.dst_rank], hdr, payload, n);
+    xpending_ = true;
+  }
+  void xq(const XMsg& m) { xq(m, m.payload.data(), m.payload.size()); }
+  void flush_x() {
+    if (!xpending_) return;
+    xpending_ = false;
+    for (int r = 0; r < (int)xout_.size(); ++r) xch_->post_frames(r, xout_[r]);
+  }
+  void post_owner(Session* s, uint8_t type, uint8_t flags, int a, const char* payload, size_t n, int b = 0) {
     if (!xch_) return;
     XMsg m;
     m.type = type;
@@ -2152,8 +2171,7 @@ class Loop {
     m.skey = s->owner_skey;
     m.a = a;
     m.b = b;
-    m.payload = payload;
-    xch_->post(std::move(m));
+    xq(m, payload, n);
   }
   // owner: a remote stream ends with `sent` deltas announced by its worker; anything else
   // than the count received means deltas were lost or are still missing
@@ -2646,7 +2664,7 @@ class Loop {
         m.dst_loop = m.src_loop = (uint16_t)idx_;
         m.bi = i;
         m.skey = s->skey;
-        xch_->post(std::move(m));
+        xq(m);
       }
     }
     for (int i = 0; i < (int)s->bs.size(); ++i) {
@@ -2785,6 +2803,8 @@ class Loop {
   bool valid_init_ = false;
   std::mutex xmu_;
   std::vector<XMsg> xin_;
+  std::vector<std::string> xout_;  // per destination rank: frames of this loop pass
+  bool xpending_ = false;
   uint64_t next_skey_ = 1;
   std::unordered_map<uint64_t, Session*> rsess_;            // owner sessions with remote streams
   std::map<std::pair<uint64_t, int>, Session*> shadow_;     // worker streams by (owner key, bi)
