@@ -72,7 +72,9 @@ struct BackendTpl {
   HoleTpl hole[kHoleTpls];  // by shape class (hole count, kind): role / content / finish events
 };
 
-enum WorkFlags : uint32_t { WF_EOF = 1, WF_FILTER = 2, WF_EMIT = 4, WF_STARTED = 8, WF_FRESH = 16 };
+// WF_PUBLISH: the tick's first item of its backend index — the one workgroup that writes that
+// backend's event-shape / hole templates for the lane's next launch
+enum WorkFlags : uint32_t { WF_EOF = 1, WF_FILTER = 2, WF_EMIT = 4, WF_STARTED = 8, WF_FRESH = 16, WF_PUBLISH = 32 };
 enum WorkStatus : uint32_t { WS_DONE = 1, WS_ABORTED = 2, WS_STARTED = 4, WS_ESCALATE = 8, WS_MORE = 16 };
 
 struct KParams {
@@ -87,6 +89,9 @@ struct KParams {
   // (l >> 4): 0: -2·q0, 1: -2·q1, 2/3: mask (q = code, q0 = q & 7, q1 = q >> 3)
   alignas(16) int8_t bfrag[2][64 * 16];
   uint32_t content_cap;
+  // single-wave fast paths of the common small tile (QMX_KFAST bit mask, default all):
+  // 1 S2 framing, 2 S3a template prepass, 4 S4 filter, 8 S6 sizing
+  uint32_t fast;
   int pre1_len, pre2_len, suf_len;
   char pre1[48];
   char pre2[176];

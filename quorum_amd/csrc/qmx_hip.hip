@@ -55,8 +55,11 @@ constexpr int TILE_MAX = 16384;
 constexpr int MAX_EV = 512;  // events per tile (more → WS_MORE requeue); keeps LDS < 80 KiB (2 WG/CU)
 constexpr int MAX_CAND = 1024;
 constexpr int PAD = 16;
+constexpr int kSpecTile = 4096;  // tile bytes loaded before the work item is known (256 threads x 16 B)
 constexpr int TOK_CAP = 512;
-constexpr int kDbg = 21;  // QMX_STAGE_TIMING record per work item: stamps 0-12, S3 counters 13-20
+// QMX_STAGE_TIMING record per work item: stamps 0-12, S3 counters 13-20, sub-stage stamps
+// 21 (S3a done), 22 (S3 loop done), 23 (s4_wave: matched), 24 (s4_wave: cuts)
+constexpr int kDbg = 25;
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 
@@ -88,7 +91,7 @@ struct Smem {
   int16_t tok_dep[MAX_CAND + 1];
   int32_t chunk_base[BS + 1];
   int32_t scr[2 * (BS / 64)];  // block scans: one (pair) partial per wave
-  int32_t v[32];
+  int32_t v[40];
   alignas(16) uint8_t tpl[TPL_BYTES];  // this stream's event shape template
 };
 static_assert(TPL_BYTES == kTplBytes, "template size");
@@ -96,7 +99,8 @@ static_assert(TPL_BYTES == kTplBytes, "template size");
 enum : int {
   V_START = 0, V_NSEP, V_LASTSEP, V_ABORT, V_NEV, V_CONSUMED, V_STATUS, V_NDELTA, V_YLEN, V_NCAND,
   V_NTOK, V_BAIL, V_DEPTH0, V_TAILLEN, V_NEWTAIL, V_NEWDEPTH, V_WLEN, V_NEMIT, V_ETOT, V_OUTLEN,
-  V_TPLPRE, V_TPLSUF, V_TPLK, V_NEXTEV, V_NFULL, V_NTPL, V_CFULL, V_CTPL, V_CLEX, V_NHOLE, V_CHOLE
+  V_TPLPRE, V_TPLSUF, V_TPLK, V_NEXTEV, V_NFULL, V_NTPL, V_CFULL, V_CTPL, V_CLEX, V_NHOLE, V_CHOLE, V_S4W,
+  V_HCLAIM  // hole-template slots this workgroup wrote (bit per slot): one writer per slot
 };
 
 // LDS byte reader that fetches one aligned 64-bit word per 8 sequential bytes: a byte-serial
@@ -398,7 +402,7 @@ __device__ inline bool wave_hole_match(const uint8_t* x, int e0, int e1, const H
 // entry by shape class, if no other workgroup of this launch claimed that entry.
 __device__ inline void wave_hole_publish(const uint8_t* x, int e0, int e1, const uint16_t* tpos,
                                          const uint8_t* ttype, int nt, uint64_t vopen, int kind, int str_a,
-                                         bool tgt_bs, HoleTpl* table, uint32_t seq) {
+                                         bool tgt_bs, HoleTpl* table, int* claims) {
   const int lane = threadIdx.x & 63;
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
   const bool v = lane < nt;
@@ -421,12 +425,12 @@ __device__ inline void wave_hole_publish(const uint8_t* x, int e0, int e1, const
     if (Tm == 0) return;
     target = __popcll(H & ((1ull << (__ffsll((unsigned long long)Tm) - 1)) - 1));
   }
-  HoleTpl& D = table[(nh * 2 + (kind == EV_CONTENT ? 1 : 0)) % kHoleTpls];
+  const int slot = (nh * 2 + (kind == EV_CONTENT ? 1 : 0)) % kHoleTpls;
+  HoleTpl& D = table[slot];
+  // the launch's only writer of this backend's table is its publishing workgroup (WF_PUBLISH);
+  // within it one wave per slot (an LDS claim — no global atomic round trip on the path)
   int won = 0;
-  if (lane == 0) {
-    const uint32_t old = __hip_atomic_load(&D.claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    won = old != seq && atomicCAS(&D.claim, old, seq) == old;
-  }
+  if (lane == 0) won = (atomicOr(claims, 1 << slot) & (1 << slot)) == 0;
   if (!__builtin_amdgcn_readfirstlane(won)) return;
   const int len = e1 - e0;
   for (int i = lane; i < len; i += 64) D.bytes[i] = x[e0 + i];
@@ -448,13 +452,10 @@ __device__ inline void wave_hole_publish(const uint8_t* x, int e0, int e1, const
 // A hole template that matched in this launch is carried into the launch's write table
 // (the tables alternate per launch: a shape that only ever matches would otherwise vanish
 // from every other launch).  Everything but the claim word is copied.
-__device__ inline void wave_hole_carry(const HoleTpl& T, HoleTpl* dst, uint32_t seq) {
+__device__ inline void wave_hole_carry(const HoleTpl& T, HoleTpl* dst, int slot, int* claims) {
   const int lane = threadIdx.x & 63;
   int won = 0;
-  if (lane == 0) {
-    const uint32_t old = __hip_atomic_load(&dst->claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    won = old != seq && atomicCAS(&dst->claim, old, seq) == old;
-  }
+  if (lane == 0) won = (atomicOr(claims, 1 << slot) & (1 << slot)) == 0;
   if (!__builtin_amdgcn_readfirstlane(won)) return;
   constexpr int kW = (int)(sizeof(HoleTpl) / 16) - 1;
   if (lane < kW) ((uint4*)dst)[lane] = ((const uint4*)&T)[lane];
@@ -464,6 +465,246 @@ __device__ inline void wave_hole_carry(const HoleTpl& T, HoleTpl* dst, uint32_t 
 // the fused tick kernel
 // ------------------------------------------------------------------------------------
 // LDS of a tick workgroup (the fused kernel overlays it with the finalize workgroup's)
+// ------------------------------------------------------------------------------------
+// S4 on one wave (the common tile: Z <= 2048 bytes, <= 64 deltas, <= 63 '<' candidates)
+// ------------------------------------------------------------------------------------
+// The block-wide S4 spends ten block barriers and four block scans on what is, in a
+// streaming tile, a few hundred bytes with a handful of '<': wave 0 alone runs the same
+// stages wave-synchronously — ballot candidate scan in 64-byte strides, the MFMA matcher,
+// the (a,b) depth scan on DPP, a hold_cut per delta lane, ballot compaction of the kept
+// bytes with each delta's kept-prefix count — and the other waves wait at one barrier.
+// Returns false (nothing written that the block path does not rewrite) when the tile has
+// more than 63 candidates.
+__device__ inline void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
+
+__device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth0, const KParams& P,
+                        unsigned long long* dbg) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  // candidates: every '<' of Z, in position order
+  int nc = 0;
+  for (int base = 0; base < Zn; base += 64) {
+    const int x = base + lane;
+    const bool isc = x < Zn && Z[x] == '<';
+    const uint64_t m = __ballot(isc);
+    if (isc && nc + __popcll(m & below) < 64) s.cand[nc + __popcll(m & below)] = (uint16_t)x;
+    nc += __popcll(m);
+    if (nc > 63) return false;  // (lane k owns token k AND the gap after it: ntok <= 63)
+  }
+  if (lane < nc) s.cand_tok[lane] = 0;
+  wave_fence();
+  {
+    const v4i bf0 = build_pattern_frag(P, 0), bf1 = build_pattern_frag(P, P.npat > 16 ? 1 : 0);
+    for (int g = 0; g * 16 < nc; ++g) mfma_match_group(Z, Zn, s.cand, nc, g, P, bf0, bf1, s.cand_tok);
+  }
+  wave_fence();
+  if (dbg != nullptr && lane == 0) dbg[23] = __builtin_amdgcn_s_memrealtime();
+  // tokens and the depth before each (candidates in order, non-tokens the scan identity)
+  {
+    const int id = lane < nc ? (int)s.cand_tok[lane] : 0;
+    const uint64_t m = __ballot(id != 0);
+    const int k = __popcll(m & below);
+    DepthOp op;
+    int2 x = id > 0 ? make_int2(1, 1) : id < 0 ? make_int2(-1, 0) : make_int2(0, 0);
+    x = wave_incl_pair(x, op);
+    int2 ex;
+    ex.x = __shfl_up(x.x, 1, 64);
+    ex.y = __shfl_up(x.y, 1, 64);
+    if (lane == 0) ex = make_int2(0, 0);
+    if (id != 0) {
+      s.tok_pos[k] = s.cand[lane];
+      s.tok_id[k] = (int8_t)id;
+      s.tok_len[k] = (uint8_t)tok_plen(P, id);
+      s.tok_dep[k] = (int16_t)max(depth0 + ex.x, ex.y);
+    }
+    if (lane == 63) {
+      const int nt = __popcll(m);
+      s.v[V_NTOK] = nt;
+      s.tok_dep[nt] = (int16_t)max(depth0 + x.x, x.y);
+    }
+  }
+  wave_fence();
+  const int ntok = __builtin_amdgcn_readfirstlane(s.v[V_NTOK]);
+  // a cut per delta (lane j), the new holdback tail (lane 0)
+  int cut = 0;
+  if (lane < ndelta) {
+    int q;
+    cut = hold_cut(s, Z, nc, ntok, s.dl_end[lane], P, false, &q);
+    s.cut[lane] = (uint16_t)cut;
+  }
+  if (lane == 0) {
+    int q;
+    hold_cut(s, Z, nc, ntok, Zn, P, true, &q);
+    s.v[V_NEWTAIL] = q;
+    s.v[V_NEWDEPTH] = s.tok_dep[ntok];
+  }
+  const int cutN = __shfl(cut, ndelta - 1, 64);
+  if (dbg != nullptr && lane == 0) dbg[24] = __builtin_amdgcn_s_memrealtime();
+  // compaction of the kept bytes of [0, cutN) into A, by segments (kept_at's cases): lane k
+  // owns the gap before token k (kept at depth 0) and token k itself (kept when it is a
+  // close tag at depth 0: literal text); a DPP scan gives each segment its output offset,
+  // the kept segments are copied 64 bytes per step, and each delta's kept prefix is one
+  // segment lookup — no per-byte token search
+  const bool seg = lane <= ntok;
+  int gs = 0, ge = 0, ts0 = 0, te = 0;
+  bool gk = false, tk = false;
+  if (seg) {
+    gs = lane == 0 ? 0 : min((int)s.tok_pos[lane - 1] + (int)s.tok_len[lane - 1], cutN);
+    ge = lane < ntok ? min((int)s.tok_pos[lane], cutN) : cutN;
+    ge = max(ge, gs);
+    const int dep = s.tok_dep[lane];
+    gk = dep == 0;
+    if (lane < ntok) {
+      ts0 = min((int)s.tok_pos[lane], cutN);
+      te = min((int)s.tok_pos[lane] + (int)s.tok_len[lane], cutN);
+      tk = s.tok_id[lane] < 0 && dep == 0;
+    }
+  }
+  const int gl = gk ? ge - gs : 0, tl = tk ? te - ts0 : 0;
+  const int incl = wave_incl_sum(gl + tl);
+  const int ob = incl - gl - tl;  // output offset of this lane's gap (its token follows it)
+  const int out = __shfl(incl, 63, 64);
+  for (uint64_t m = __ballot(gl > 0); m; m &= m - 1) {
+    const int k = __ffsll((unsigned long long)m) - 1;
+    const int a = __shfl(gs, k, 64), n = __shfl(gl, k, 64), o = __shfl(ob, k, 64);
+    for (int x = lane; x < n; x += 64) s.A[o + x] = Z[a + x];
+  }
+  for (uint64_t m = __ballot(tl > 0); m; m &= m - 1) {
+    const int k = __ffsll((unsigned long long)m) - 1;
+    const int a = __shfl(ts0, k, 64), n = __shfl(tl, k, 64), o = __shfl(ob, k, 64) + __shfl(gl, k, 64);
+    for (int x = lane; x < n; x += 64) s.A[o + x] = Z[a + x];
+  }
+  // kept bytes before each delta's cut: the segment that holds cut - 1
+  const int c = lane < ndelta ? cut : 0;
+  const int kk = c > 0 && c < cutN ? tok_upper(s, ntok, c - 1) : 0;  // tokens starting before c
+  const int pk = kk > 0 ? kk - 1 : 0;
+  const int p_gs = __shfl(gs, kk, 64), p_ob = __shfl(ob, kk, 64), p_gk = __shfl((int)gk, kk, 64);
+  const int q_ts = __shfl(ts0, pk, 64), q_te = __shfl(te, pk, 64), q_ob = __shfl(ob, pk, 64),
+            q_gl = __shfl(gl, pk, 64), q_tk = __shfl((int)tk, pk, 64);
+  if (lane < ndelta) {
+    int wp;
+    if (c >= cutN) wp = out;
+    else if (c == 0) wp = 0;
+    else if (kk > 0 && c < q_te) wp = q_ob + q_gl + (q_tk ? c - q_ts : 0);  // inside token kk-1
+    else wp = p_ob + (p_gk ? c - p_gs : 0);                                   // in gap kk
+    s.wpos[lane] = (uint16_t)wp;
+  }
+  if (lane == 0) s.v[V_WLEN] = out;
+  return true;
+}
+
+// S2's last step (one thread): events of the tile from the separators, what it consumed,
+// and whether the stream is done / has more events than one tile holds
+__device__ inline void s2_finalize(Smem& s, int start, int in_len, bool eof) {
+  int nsep = s.v[V_NSEP];
+  int nev, consumed;
+  bool done = false, more = false;
+  if (nsep > MAX_EV) {
+    nev = MAX_EV;
+    consumed = s.ev_b[MAX_EV - 1] + 2;
+    more = true;
+  } else {
+    nev = nsep;
+    int rem = nsep > 0 ? s.v[V_LASTSEP] + 2 : start;
+    consumed = rem;
+    if (eof) {
+      if (rem < in_len) {
+        if (nev < MAX_EV) {
+          s.ev_a[nev] = (uint16_t)rem;
+          s.ev_b[nev] = (uint16_t)in_len;
+          ++nev;
+          consumed = in_len;
+          done = true;
+        } else {
+          more = true;
+        }
+      } else {
+        consumed = in_len;
+        done = true;
+      }
+    }
+  }
+  s.v[V_NEV] = nev;
+  s.v[V_CONSUMED] = consumed;
+  if (done) s.v[V_STATUS] |= WS_DONE;
+  if (more) s.v[V_STATUS] |= WS_MORE;
+}
+
+// newline mask of x[lo, lo + len) (len <= 64, 8-byte aligned lo, 64 B readable past it):
+// SWAR byte compares on ds_read_b64 words
+__device__ inline uint64_t nl_mask64(const uint8_t* x, int lo, int len) {
+  uint64_t nm = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    if (q * 8 < len) {
+      const uint64_t w = *(const uint64_t*)&x[lo + 8 * q];
+      const uint64_t v = w ^ 0x0a0a0a0a0a0a0a0aull;
+      const uint64_t y = (((v & 0x7f7f7f7f7f7f7f7full) + 0x7f7f7f7f7f7f7f7full) | v) & 0x8080808080808080ull;
+      const uint64_t zb = ~y & 0x8080808080808080ull;  // high bit of every '\n' byte
+      nm |= (uint64_t)(((zb >> 7) * 0x0102040810204080ull) >> 56) << (8 * q);
+    }
+  }
+  return nm & (len >= 64 ? ~0ull : ((1ull << len) - 1ull));
+}
+
+// S2 on wave 0 (tiles up to 4 KiB past the leading whitespace: a streaming tick, or a whole
+// short response): the block path's newline-run framing with DPP wave scans instead of block
+// scans and the finalize on lane 0 — one block barrier instead of five
+__device__ inline void s2_wave(Smem& s, int start, int in_len, bool eof) {
+  const int lane = threadIdx.x & 63;
+  const int flen = in_len - start;
+  const int C8 = (((flen + 63) / 64) + 7) & ~7;  // <= 64
+  const int lo = min(start + lane * C8, in_len), hi = min(lo + C8, in_len), len = hi - lo;
+  const uint64_t nm = nl_mask64(s.A, lo, len);
+  const uint64_t valid = len >= 64 ? ~0ull : ((1ull << len) - 1ull);
+  const uint64_t inv = ~nm & valid;
+  const bool all_nl = inv == 0;
+  const int trail = all_nl ? len : len - 64 + __clzll(inv);
+  const bool next_nl = hi < in_len && s.A[hi] == '\n';
+  const int2 run = all_nl ? make_int2(1, len) : make_int2(0, trail);
+  const int2 incl = wave_incl_pair(run, RunOp());
+  int2 ex;
+  ex.x = __shfl_up(incl.x, 1, 64);
+  ex.y = __shfl_up(incl.y, 1, 64);
+  if (lane == 0) ex = make_int2(1, 0);
+  // separators: "\n" at an even position of its newline run, followed by a "\n"
+  auto each_sep = [&](auto&& f) {
+    uint64_t m = nm;
+    while (m) {
+      const int r0 = __ffsll((unsigned long long)m) - 1;
+      const uint64_t rest = ~(m >> r0);
+      const int L = rest == 0 ? 64 - r0 : __ffsll((unsigned long long)rest) - 1;
+      const int c = r0 == 0 ? ex.y : 0;
+      const bool ext = r0 + L == len && next_nl;
+      for (int i = 0; i < L; ++i)
+        if (!((c + i) & 1) && (i + 1 < L || ext)) f(lo + r0 + i);
+      m &= ~(L >= 64 ? ~0ull : (((1ull << L) - 1ull) << r0));
+    }
+  };
+  int cnt = 0, last = -1;
+  each_sep([&](int p) {
+    ++cnt;
+    last = p;
+  });
+  const int ci = wave_incl_sum(cnt);
+  int k = ci - cnt;
+  const int nsep = __shfl(ci, 63, 64);
+  each_sep([&](int p) {
+    if (k < MAX_EV) s.ev_b[k] = (uint16_t)p;
+    if (k + 1 < MAX_EV) s.ev_a[k + 1] = (uint16_t)(p + 2);
+    ++k;
+  });
+  int lastsep = last;  // the tile's last separator: a wave max
+  for (int o = 32; o > 0; o >>= 1) lastsep = max(lastsep, __shfl_xor(lastsep, o, 64));
+  if (lane == 0) {
+    s.ev_a[0] = (uint16_t)start;
+    s.v[V_NSEP] = nsep;
+    s.v[V_LASTSEP] = lastsep;
+  }
+  wave_fence();
+  if (lane == 0) s2_finalize(s, start, in_len, eof);
+}
+
 struct TickShared {
   Smem s;
   KParams P;                                   // kernel args staged in LDS: lane-divergent reads
@@ -484,13 +725,20 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   auto& TKT = U.TKT;
   auto& wtpl = U.wtpl;
   const int tid = threadIdx.x;
+  // Tiles sit at a fixed stride (item bi at bi x TILE_MAX, HipEngine::prepare), so the first
+  // 4 KiB of this item's tile — all of it for a streaming tick or a short response — is
+  // requested from host memory together with the work item itself: one PCIe round trip
+  // before the tile is in registers, not item → offset → tile (two)
+  const uint8_t* tile = in + (size_t)bi * TILE_MAX;
+  uint4 spec = make_uint4(0, 0, 0, 0);
+  if (tid * 16 < kSpecTile) spec = *(const uint4*)&tile[tid * 16];
+  WorkItem it = items[bi];
   for (int i = tid; i < (int)(sizeof(KParams) / 4); i += BS) ((uint32_t*)&P)[i] = ((const uint32_t*)&Pk)[i];
   if (Pk.dbg != nullptr && threadIdx.x == 0) Pk.dbg[bi * kDbg + 0] = __builtin_amdgcn_s_memrealtime();
   if (Pk.dbg != nullptr && threadIdx.x == 0) Pk.dbg[bi * kDbg + 11] = __builtin_amdgcn_s_memtime();
   // the work item is wave-uniform: keep its fields in scalar registers (a one-shot launch
   // reads it through the scalar cache anyway; a persistent grid loads it per tick with
   // vector loads, and every address derived from VGPR copies would cost vector registers)
-  WorkItem it = items[bi];
   it.slot = __builtin_amdgcn_readfirstlane(it.slot);
   it.in_off = __builtin_amdgcn_readfirstlane(it.in_off);
   it.in_len = __builtin_amdgcn_readfirstlane(it.in_len);
@@ -504,10 +752,12 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   const bool filt = it.flags & WF_FILTER;
   const bool emit = it.flags & WF_EMIT;
   const bool fresh = it.flags & WF_FRESH;
+  // this workgroup writes the launch's backend templates of its index (first item of it)
+  const bool pub = (it.flags & WF_PUBLISH) && btpl_wr != nullptr && it.index < (uint32_t)kBackendTpl;
 
   // ---- S0: load tile (16-B vector loads from host-mapped memory) -----------------
-  for (int i = tid * 16; i < in_len; i += BS * 16)
-    *(uint4*)&s.A[i] = *(const uint4*)&in[it.in_off + i];
+  if (tid * 16 < kSpecTile && tid * 16 < in_len) *(uint4*)&s.A[tid * 16] = spec;
+  for (int i = kSpecTile + tid * 16; i < in_len; i += BS * 16) *(uint4*)&s.A[i] = *(const uint4*)&tile[i];
   if (tid == 0) {
     s.v[V_ABORT] = MAX_EV;
     s.v[V_LASTSEP] = -1;
@@ -516,6 +766,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     s.v[V_TPLK] = -1;
     s.v[V_NEXTEV] = 0;
     s.v[V_NFULL] = s.v[V_NTPL] = s.v[V_CFULL] = s.v[V_CTPL] = s.v[V_CLEX] = s.v[V_NHOLE] = s.v[V_CHOLE] = 0;
+    s.v[V_HCLAIM] = 0;
     for (int q = 0; q < BS / 64; ++q) wtpl[q][0] = -1;
     if (fresh) {
       s.v[V_DEPTH0] = 0;
@@ -602,7 +853,10 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   // over stride-C chunks were bank-conflicted LDS reads, three passes over every byte.
   const int flen0 = in_len - start;
   const int C8 = (((flen0 + BS - 1) / BS) + 7) & ~7;
-  if ((start & 7) == 0 && C8 <= 32) {
+  const bool s2_wave_ok = (P.fast & 1) && (start & 7) == 0 && flen0 <= 4096;
+  if (s2_wave_ok) {
+    if (tid < 64) s2_wave(s, start, in_len, eof);
+  } else if ((start & 7) == 0 && C8 <= 32) {
     const int lo = min(start + tid * C8, in_len), hi = min(lo + C8, in_len);
     const int len = hi - lo;
     uint32_t nm = 0;
@@ -699,40 +953,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     }
   }
   __syncthreads();
-  if (tid == 0) {
-    int nsep = s.v[V_NSEP];
-    int nev, consumed;
-    bool done = false, more = false;
-    if (nsep > MAX_EV) {
-      nev = MAX_EV;
-      consumed = s.ev_b[MAX_EV - 1] + 2;
-      more = true;
-    } else {
-      nev = nsep;
-      int rem = nsep > 0 ? s.v[V_LASTSEP] + 2 : start;
-      consumed = rem;
-      if (eof) {
-        if (rem < in_len) {
-          if (nev < MAX_EV) {
-            s.ev_a[nev] = (uint16_t)rem;
-            s.ev_b[nev] = (uint16_t)in_len;
-            ++nev;
-            consumed = in_len;
-            done = true;
-          } else {
-            more = true;
-          }
-        } else {
-          consumed = in_len;
-          done = true;
-        }
-      }
-    }
-    s.v[V_NEV] = nev;
-    s.v[V_CONSUMED] = consumed;
-    if (done) s.v[V_STATUS] |= WS_DONE;
-    if (more) s.v[V_STATUS] |= WS_MORE;
-  }
+  if (tid == 0 && !s2_wave_ok) s2_finalize(s, start, in_len, eof);
   __syncthreads();
   QMX_STAMP(3);
   const int nev = s.v[V_NEV];
@@ -745,6 +966,68 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   // Lane 0 writes the result.  > 64 tokens → per-token walk; exotic → validating scalar
   // scanner (both by lane 0, rare) — exact either way.
   int packed_local[4];
+  // S3a: content events of the stream's known shape (its own or its backend's template),
+  // one wave per event by static assignment, one 8-byte word per lane: the prefix and suffix
+  // words compared with the template, the body bytes tested with SWAR for anything that would
+  // need a real string scan ('"', '\\', control bytes, non-ASCII).  An event that passes has
+  // the template's parse with an escape-free body — exactly wave_tpl_match + wave_str_body's
+  // answer for it — at ~4 dependent LDS round trips instead of an atomic claim, two ballot
+  // passes and LDS atomics per event.  Everything else (0xFF) goes through the loop below.
+  {
+    const int w = tid >> 6, lane = tid & 63;
+    const int tp = s.v[V_TPLPRE], ts = s.v[V_TPLSUF];
+    int newest = -1, nm = 0;
+    for (int k = w; k < nev; k += BS / 64) {
+      const int e0 = s.ev_a[k], e1 = s.ev_b[k], L = e1 - e0;
+      bool ok = (P.fast & 2) && tp > 0 && L >= tp + ts && L <= 512;
+      if (ok) {
+        bool bad = false;
+        const int o = lane * 8;
+        if (o < L) {
+          const int nb = min(8, L - o);
+          const uint64_t valid = nb == 8 ? ~0ull : ((1ull << (8 * nb)) - 1);
+          const uint64_t ev = lds_window8(s.A, e0 + o, e1);
+          const int pe = min(max(tp - o, 0), 8);  // prefix bytes of this word
+          const uint64_t pmask = pe == 8 ? ~0ull : ((1ull << (8 * pe)) - 1);
+          const int ss = (L - ts) - o;  // the suffix starts at byte ss of this word
+          uint64_t smask = 0, sw = 0;
+          if (ts > 0 && ss < 8) {
+            const int s0 = max(ss, 0);
+            smask = valid & ~(s0 == 0 ? 0ull : ((1ull << (8 * s0)) - 1));
+            sw = ss >= 0 ? lds_window8(s.tpl + TPL_PRE_MAX, 0, ts) << (8 * ss)
+                         : lds_window8(s.tpl + TPL_PRE_MAX, -ss, ts);
+          }
+          const uint64_t tw = pe > 0 ? ((const uint64_t*)s.tpl)[lane] : 0ull;
+          const uint64_t bmask = valid & ~pmask & ~smask;
+          const uint64_t hi = 0x8080808080808080ull, one = 0x0101010101010101ull;
+          const uint64_t q = ev ^ 0x2222222222222222ull, b = ev ^ 0x5c5c5c5c5c5c5c5cull;
+          // any '"', '\\', byte < 0x20 or >= 0x80 (the zero / less-than tricks only ever err
+          // towards "bad", which just sends the event down the exact path)
+          const uint64_t odd = (((q - one) & ~q) | ((b - one) & ~b) | ((ev - 0x20 * one) & ~ev) | ev) & hi;
+          bad = ((ev ^ tw) & pmask) != 0 || ((ev ^ sw) & smask) != 0 || (odd & bmask) != 0;
+        }
+        ok = __ballot(bad) == 0;
+      }
+      if (lane == 0) {
+        s.ev_kind[k] = ok ? (uint8_t)EV_CONTENT : (uint8_t)0xFF;
+        if (ok) {
+          s.ev_sa[k] = (uint16_t)(e0 + tp);
+          s.ev_sb[k] = (uint16_t)(e1 - ts);
+          s.ev_dl[k] = (uint16_t)(L - tp - ts);
+        }
+      }
+      if (ok) {
+        newest = k;
+        ++nm;
+      }
+    }
+    if (lane == 0 && nm > 0) {
+      atomicAdd(&s.v[V_NTPL], nm);
+      atomicMax(&s.v[V_TPLK], newest);  // the tile's newest content event becomes the template
+    }
+  }
+  __syncthreads();
+  QMX_STAMP(21);
   {
     const int w = tid >> 6, lane = tid & 63;
     const LdsWords rd(s.A);
@@ -761,6 +1044,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       // reason, usage, [DONE] — usually have their own shape and need a full parse), then the
       // middle, which by then matches a published template: the few full parses overlap
       const int k = nev <= 8 ? g : g < 4 ? g : g < 8 ? nev - 1 - (g - 4) : g - 4;
+      if (s.ev_kind[k] != 0xFF) continue;  // resolved by S3a
       const int e0 = s.ev_a[k], e1 = s.ev_b[k];
       int kind = EV_SKIP, sa = 0, sb = 0, body = -1;
       bool slow = false, lexed = false;
@@ -820,8 +1104,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
               hm = true;
               hhint = qi;
               kind = T.kind;
-              if (btpl_wr != nullptr && it.index < (uint32_t)kBackendTpl)
-                wave_hole_carry(T, &btpl_wr[it.index].hole[qi], seq);
+              if (pub) wave_hole_carry(T, &btpl_wr[it.index].hole[qi], qi, &s.v[V_HCLAIM]);
               if (kind == EV_CONTENT) {
                 sa = ha;
                 sb = hb;
@@ -875,9 +1158,9 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
                   if (kind == EV_CONTENT && sa - e0 <= TPL_PRE_MAX && e1 - sb <= TPL_SUF_MAX) published = true;
                   // its hole template for the next launch: other streams' events of this shape
                   // (ids / timestamps / text differ) then skip the full parse
-                  if ((kind == EV_CONTENT || kind == EV_SKIP) && e1 - e0 <= kHoleTplBytes && btpl_wr != nullptr &&
-                      it.index < (uint32_t)kBackendTpl)
-                    wave_hole_publish(s.A, e0, e1, TKP[w], TKT[w], nt, vopen, kind, sa, esc, btpl_wr[it.index].hole, seq);
+                  if ((kind == EV_CONTENT || kind == EV_SKIP) && e1 - e0 <= kHoleTplBytes && pub)
+                    wave_hole_publish(s.A, e0, e1, TKP[w], TKT[w], nt, vopen, kind, sa, esc, btpl_wr[it.index].hole,
+                                      &s.v[V_HCLAIM]);
                 }
               }
             }
@@ -924,6 +1207,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     }
   }
   __syncthreads();
+  QMX_STAMP(22);
   {  // persist the newest template now: S4 reuses the input tile
     const int tk = s.v[V_TPLK];
     if (tk >= 0) {
@@ -935,16 +1219,10 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
         ds.tpl_pre = (uint16_t)pre;
         ds.tpl_suf = (uint16_t)suf;
       }
-      // publish it for this backend index: the first workgroup of the launch to claim the
-      // entry writes it; the lane's next launch reads it (a kernel boundary in between)
-      int won = 0;
-      if (tid == 0 && btpl_wr != nullptr && it.index < (uint32_t)kBackendTpl) {
-        uint32_t* claim = &btpl_wr[it.index].claim;
-        uint32_t old = __hip_atomic_load(claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        won = old != seq && atomicCAS(claim, old, seq) == old;
-      }
-      won = __syncthreads_or(won);
-      if (won) {
+      // publish it for this backend index: the launch's publishing workgroup of that index
+      // (WF_PUBLISH, picked by the host) writes it; the lane's next launch reads it (a kernel
+      // boundary in between).  No claim: a global atomic here cost every item a round trip.
+      if (pub) {
         BackendTpl& bw = btpl_wr[it.index];
         if (tid < pre) bw.tpl[tid] = s.A[e0 + tid];
         if (tid < suf) bw.tpl[TPL_PRE_MAX + tid] = s.A[e1 - suf + tid];
@@ -1024,7 +1302,19 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   // ---- S4: think filter ----------------------------------------------------------------
   const uint8_t* W = Z;  // identity when not filtering
   int ncand = 0, ntok = 0;
-  if (filt && ndelta > 0) {
+  bool s4_done = false;
+  if ((P.fast & 4) && filt && ndelta > 0 && Zn <= 2048 && ndelta <= 64) {  // the common tile: one wave (s4_wave)
+    if (tid < 64) {
+      const bool ok = s4_wave(s, Z, Zn, ndelta, depth0, P, P.dbg != nullptr ? P.dbg + bi * kDbg : nullptr);
+      if (tid == 0) s.v[V_S4W] = ok ? 1 : 0;
+    }
+    __syncthreads();
+    if (s.v[V_S4W]) {
+      s4_done = true;
+      W = s.A;
+    }
+  }
+  if (filt && ndelta > 0 && !s4_done) {
     // candidates: per-thread 8-byte-multiple chunks of Z (16-B aligned) as ds_read_b64
     // words, a 32-bit '<' mask per thread (SWAR compare), popcount + ordered compaction
     {
@@ -1060,7 +1350,9 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       ncand = tot;
     }
   }
-  if (filt && ndelta > 0 && ncand == 0) {  // no '<' anywhere in Z (old holdback tail + new deltas)
+  if (s4_done) {
+    // s4_wave wrote cut / wpos / V_WLEN / V_NEWTAIL / V_NEWDEPTH
+  } else if (filt && ndelta > 0 && ncand == 0) {  // no '<' anywhere in Z (old holdback tail + new deltas)
     // no tag can start in these bytes (and no holdback is pending: a held tail starts with
     // '<'): outside a think block every byte is kept, inside one every byte is dropped
     const bool keep = depth0 == 0;
@@ -1245,9 +1537,61 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
 
   // ---- S6 (sizing): emitted deltas, escaped lengths -------------------------------------
   int n_emit = 0, etot = 0;
+  bool s6_wave = false;  // sizing ran on wave 0: 64 escaped-content chunks instead of BS
   const int ndig = it.index >= 100 ? 3 : it.index >= 10 ? 2 : 1;
   const int PRE = P.pre1_len + ndig + P.pre2_len, SUF = P.suf_len, EVL = PRE + SUF;
-  if (emit && ndelta > 0) {
+  if ((P.fast & 8) && emit && ndelta > 0 && ndelta <= 64 && Wlen <= 2048) {
+    // the common tile on wave 0 alone (as s4_wave): emitted-delta ballot, per-lane chunks of
+    // escaped lengths with a DPP scan, each delta's escaped prefix; one barrier for the block
+    if (tid < 64) {
+      const int lane = tid;
+      const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+      const int wp = lane < ndelta ? (int)s.wpos[lane] : 0;
+      const int prev = __shfl_up(wp, 1, 64);
+      const bool f = lane < ndelta && wp > (lane ? prev : 0);
+      const uint64_t m = __ballot(f);
+      if (lane < ndelta) s.eidx[lane] = (uint16_t)__popcll(m & below);
+      if (f) s.ejx[__popcll(m & below)] = (uint16_t)lane;
+      const int C = (Wlen + 63) / 64;
+      const int lo = min(lane * C, Wlen), hi = min(lo + C, Wlen);
+      int x = lo, e = 0;
+      while (x < hi && is_cont(W[x])) ++x;
+      while (x < hi) {
+        uint32_t cp;
+        x += wtf8_decode(W, x, Wlen, &cp);
+        e += escaped_len_cp(cp);
+      }
+      const int incl = wave_incl_sum(e);
+      const int excl = incl - e;
+      const int tot = __shfl(incl, 63, 64);
+      s.chunk_base[lane] = excl;  // the write phase's escaped-content chunks (64 of them here)
+      // (shuffles with every lane active: a lane's chunk base for its delta's escaped prefix)
+      const int t = (lane < ndelta && wp < Wlen && C > 0) ? wp / C : 0;
+      const int tbase = __shfl(excl, t, 64);
+      if (lane < ndelta) {
+        uint32_t ep = (uint32_t)tot;
+        if (wp < Wlen) {
+          int xx = min(t * C, Wlen), ee = tbase;
+          while (xx < wp && is_cont(W[xx])) ++xx;
+          while (xx < wp) {
+            uint32_t cp;
+            xx += wtf8_decode(W, xx, Wlen, &cp);
+            ee += escaped_len_cp(cp);
+          }
+          ep = (uint32_t)ee;
+        }
+        s.epos[lane] = ep;
+      }
+      if (lane == 0) {
+        s.v[V_NEMIT] = __popcll(m);
+        s.v[V_ETOT] = tot;
+      }
+    }
+    __syncthreads();
+    n_emit = s.v[V_NEMIT];
+    etot = s.v[V_ETOT];
+    s6_wave = true;
+  } else if (emit && ndelta > 0) {
     {
       int loc = 0, pre[4];
 #pragma unroll
@@ -1339,7 +1683,9 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     // output window: whichever tile buffer does not hold W (Z's tail is already committed)
     uint8_t* O = (W == s.A) ? s.B : s.A;
     const int WIN = TILE_MAX;
-    const int C = (Wlen + BS - 1) / BS;
+    // the sizing's chunking (chunk_base): per thread, or per lane of wave 0 (s6_wave; the
+    // other threads' chunks then start at Wlen and are empty)
+    const int C = s6_wave ? (Wlen + 63) / 64 : (Wlen + BS - 1) / BS;
     for (int w0 = 0; w0 < out_len; w0 += WIN) {
       const int w1 = min(w0 + WIN, out_len);
       // envelopes: fully parallel over (emitted event, envelope byte)
@@ -2120,6 +2466,8 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
     base_params_.pat_E[p] = E;
   }
   base_params_.content_cap = content_cap_;
+  base_params_.fast = 15;
+  if (const char* kf = env_get("QMX_KFAST")) base_params_.fast = (uint32_t)strtoul(kf, nullptr, 0);
   for (int blk = 0; blk < 2; ++blk)
     for (int l = 0; l < 64; ++l) {
       const int t = 16 * blk + (l & 15), kg = l >> 4;
@@ -2411,14 +2759,15 @@ void HipEngine::prepare(HipJob& J) {
   TickLane::Buf& B = L.bufs[L.next_buf];
   L.next_buf ^= 1;
   J.B = &B;
-  size_t in_need = 0, out_need = 0;
+  size_t out_need = 0;
   for (auto& w : work) {
     size_t tot = core_[w.slot].carry.size() + w.data.size();
     size_t sub = std::min(tot, (size_t)tile_);
-    in_need += (sub + 15) & ~(size_t)15;
     out_need += ((12 * sub + 1024) + 15) & ~(size_t)15;
   }
-  ensure_in(B, in_need + 64);
+  // tiles at a fixed stride: item n's tile at n x TILE_MAX (the kernel requests its first
+  // kSpecTile bytes before it has read the work item)
+  ensure_in(B, work.size() * (size_t)TILE_MAX + kSpecTile + 64);
   ensure_out(L, out_need + 64);
   J.arena = L.out;
   // the job holds its arena until complete(): a tick prepared meanwhile (pipelined lanes)
@@ -2431,7 +2780,8 @@ void HipEngine::prepare(HipJob& J) {
     HIP_CHECK(hipHostMalloc((void**)&B.h_items, sizeof(WorkItem) * B.items_cap, hipHostMallocMapped));
     HIP_CHECK(hipHostMalloc((void**)&B.h_res, sizeof(WorkResult) * B.items_cap, hipHostMallocMapped));
   }
-  size_t in_off = 0, out_off = 0;
+  size_t in_off = 0, in_bytes = 0, out_off = 0;
+  uint32_t pub_mask = 0;  // backend indices with a publishing item in this tick
   int n = 0;
   // XCD-aware item order: the dispatcher hands workgroup i to XCD i % 8, so item i gets a
   // stream with slot % 8 == i % 8 where possible — a stream's DevSlot state, template and
@@ -2472,6 +2822,7 @@ void HipEngine::prepare(HipJob& J) {
     size_t sub = std::min(tot, (size_t)tile_);
     bool eof_sent = w.eof && sub == tot;
     // copy carry + data prefix into the arena
+    in_off = (size_t)n * TILE_MAX;
     size_t a = std::min(cl, sub);
     std::memcpy(B.h_in + in_off, c.carry.data(), a);
     if (sub > a) std::memcpy(B.h_in + in_off + a, w.data.data(), sub - a);
@@ -2484,14 +2835,18 @@ void HipEngine::prepare(HipJob& J) {
     it.flags = (eof_sent ? WF_EOF : 0) | (c.filter ? WF_FILTER : 0) | (c.emit ? WF_EMIT : 0) |
                (c.started ? WF_STARTED : 0) | (w.fresh ? WF_FRESH : 0);
     it.index = (uint32_t)c.index;
+    if (c.index >= 0 && c.index < kBackendTpl && !(pub_mask & (1u << c.index))) {
+      pub_mask |= 1u << c.index;  // this launch's publisher of its backend's templates
+      it.flags |= WF_PUBLISH;
+    }
     it.content_len = content_len_[slot];
-    in_off += (sub + 15) & ~(size_t)15;
+    in_bytes += sub;
     out_off += ((size_t)it.out_cap + 15) & ~(size_t)15;
     J.pend.push_back({slot, cl, sub, eof_sent, &w});
     ++n;
   }
   J.n = n;
-  J.in_off = in_off;
+  J.in_off = in_bytes;  // (bytes staged: h2d accounting)
   // finalize requests ride the same launch: workgroups [n, n + m)
   J.fin_gpu = prep_finalize(L, *J.fin, J.fin_host);
   J.m = (int)J.fin_gpu.size();
@@ -2724,6 +3079,15 @@ void HipEngine::complete(HipJob& J, std::vector<SlotResult>& results, std::vecto
           L.stage_us[k] += (double)(d[k] - d[prev]) * 0.01;  // 100 MHz ticks -> us
           prev = k;
         }
+        // sub-stages: S3a prepass / S3 event loop / template persist; s4_wave match / cuts / compaction
+        auto sub = [&](int slot, int a, int b) {
+          if (d[a] && d[b] && d[b] >= d[a]) L.stage_us[slot] += (double)(d[b] - d[a]) * 0.01;
+        };
+        sub(11, 3, 21);
+        sub(12, 21, 22);
+        sub(13, 22, 4);
+        sub(14, 5, 23);
+        sub(15, 23, 24);
       }
       L.stage_n += n;
       for (int i = 0; i < n; ++i) {
@@ -2949,11 +3313,16 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["poll_fallbacks"] += (double)L.poll_fallbacks;
     m["fin_launches"] += (double)L.fin_launches;  // tick launches that also carried finalize work
     m["fin_items"] += (double)L.fin_items;
-    for (int k = 1; k < 11; ++k) stage[k] += L.stage_us[k];
+    for (int k = 1; k < 16; ++k) stage[k] += L.stage_us[k];
     cyc += L.clk_cycles;
     cus += L.clk_us;
   }
   for (int k = 1; k < 11; ++k) m["stage" + std::to_string(k) + "_us"] = stage[k];
+  m["stage_s3a_us"] = stage[11];
+  m["stage_s3loop_us"] = stage[12];
+  m["stage_s3persist_us"] = stage[13];
+  m["stage_s4match_us"] = stage[14];
+  m["stage_s4cuts_us"] = stage[15];
   m["shader_mhz"] = cus > 0 ? cyc / cus : 0.0;
   m["escalations"] = (double)escalations_.load();
   m["fin_host"] = (double)fin_host_.load();

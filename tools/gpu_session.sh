@@ -125,7 +125,8 @@ import json
 for l in open('$OUT/kbench.jsonl'):
     if not l.startswith('{'): continue
     d=json.loads(l); st=d.get('stage_us_per_item',{})
-    print(d.get('filter'),d.get('emit'),d['slots'],d['wall_us_p50'],d['kernel_us_avg'],[st.get('stage%d_us'%k) for k in range(1,11)])
+    print(d.get('filter'),d.get('emit'),d['slots'],d['wall_us_p50'],d['kernel_us_avg'],[st.get('stage%d_us'%k) for k in range(1,11)],
+          {k[6:-3]: v for k, v in st.items() if k.startswith('stage_s')}, d.get('s3_per_item', {}))
 " ;;
     gpuprocs=*)  # which processes hold the GPU during an N-rank rehearsal (N <= 4 keeps it under the limit)
       n=${step#gpuprocs=}
