@@ -1161,7 +1161,9 @@ void Exchange::bulk_loop() {
     if (want_epoch) {  // (re)form the world communicator
       drop(false);
       epoch = want_epoch;
-      if (ex->form(id, want_epoch, o_.timeout_s, stop_)) {
+      // forming a communicator (RCCL bootstrap over 8 ranks) may take longer than a round
+      // is allowed to: at least 20 s
+      if (ex->form(id, want_epoch, std::max(o_.timeout_s, 20.0), stop_)) {
         rccl_epoch_.store((uint64_t)epoch);
         rccl_ok_.store(true);
       } else {

@@ -88,6 +88,9 @@ struct KParams {
   // 16-pattern column block per MFMA: lane l = pattern 16·blk + (l & 15), feature group
   // (l >> 4): 0: -2·q0, 1: -2·q1, 2/3: mask (q = code, q0 = q & 7, q1 = q >> 3)
   alignas(16) int8_t bfrag[2][64 * 16];
+  // each pattern's bytes as little-endian words (zero past its end): the holdback's prefix
+  // test compares 8 bytes at a time (pattern_prefix_w) instead of byte by byte
+  uint64_t pw[2 * kMaxTags][kMaxTail / 8];
   uint32_t content_cap;
   // single-wave fast paths of the common small tile (QMX_KFAST bit mask, default all):
   // 1 S2 framing, 2 S3a template prepass, 4 S4 filter, 8 S6 sizing

@@ -303,6 +303,37 @@ __device__ inline bool kept_at(const Smem& s, int k, int x) {
   return s.tok_dep[k] == 0;
 }
 
+// ASCII upper → lower case on 8 bytes at once (other bytes unchanged)
+__device__ inline uint64_t lower8(uint64_t x) {
+  constexpr uint64_t ones = 0x0101010101010101ull, hi = 0x8080808080808080ull;
+  const uint64_t lo7 = x & ~hi;
+  const uint64_t ge_a = lo7 + (0x80 - 'A') * ones;      // bit 7 set: byte >= 'A'
+  const uint64_t gt_z = lo7 + (0x80 - 'Z' - 1) * ones;  // bit 7 set: byte > 'Z'
+  return x | (((ge_a & ~gt_z & ~x) & hi) >> 2);
+}
+
+// Is Z[q, e) (lowercased) a prefix of some pattern (opens only: open patterns)?  The device
+// form of qmx_text.h pattern_prefix: 8-byte words against KParams::pw.
+__device__ inline bool pattern_prefix_w(const uint8_t* Z, int q, int e, const KParams& P, bool opens_only) {
+  const int m = e - q;
+  if (m <= 0 || m > kMaxTail) return m <= 0;
+  const int npat = opens_only ? P.ts.n : 2 * P.ts.n;
+  // the first 16 bytes stay in registers (every default tag's pattern fits); longer partial
+  // tags read their further words per pattern
+  const uint64_t z0 = lower8(lds_window8(Z, q, e)), z1 = m > 8 ? lower8(lds_window8(Z, q + 8, e)) : 0ull;
+  auto word_mask = [m](int w) {
+    const int nb = min(8, m - 8 * w);
+    return nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1);
+  };
+  for (int t = 0; t < npat; ++t) {
+    if (m > pattern_len(P.ts, t)) continue;
+    bool ok = z0 == (P.pw[t][0] & word_mask(0)) && (m <= 8 || z1 == (P.pw[t][1] & word_mask(1)));
+    for (int w = 2; ok && 8 * w < m; ++w) ok = lower8(lds_window8(Z, q + 8 * w, e)) == (P.pw[t][w] & word_mask(w));
+    if (ok) return true;
+  }
+  return false;
+}
+
 // holdback test at stream position e (Z coords): returns cut (q when held, else e).
 // opens_only=false also reports any-pattern prefixes at depth > 0 (tail carry).
 __device__ inline int hold_cut(const Smem& s, const uint8_t* Z, int ncand, int ntok, int e, const KParams& P,
@@ -320,7 +351,7 @@ __device__ inline int hold_cut(const Smem& s, const uint8_t* Z, int ncand, int n
   int tk = s.cand_tok[idx];
   if (tk != 0 && q + tok_plen(P, tk) <= e) return e;  // completed token
   int dq = s.tok_dep[tok_lower(s, ntok, q)];
-  bool pre = pattern_prefix(Z, q, e, P.ts, dq == 0);
+  bool pre = pattern_prefix_w(Z, q, e, P, dq == 0);
   if (!pre) return e;
   if (dq == 0 || for_tail) {
     *q_out = q;
@@ -481,14 +512,26 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
                         unsigned long long* dbg) {
   const int lane = threadIdx.x & 63;
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-  // candidates: every '<' of Z, in position order
+  // candidates: every '<' of Z, in position order — 8 bytes per lane (SWAR compare on one
+  // ds_read_b64; Z is 8-byte aligned with readable bytes past Zn), 512 bytes per step
   int nc = 0;
-  for (int base = 0; base < Zn; base += 64) {
-    const int x = base + lane;
-    const bool isc = x < Zn && Z[x] == '<';
-    const uint64_t m = __ballot(isc);
-    if (isc && nc + __popcll(m & below) < 64) s.cand[nc + __popcll(m & below)] = (uint16_t)x;
-    nc += __popcll(m);
+  for (int base = 0; base < Zn; base += 512) {
+    const int x0 = base + lane * 8;
+    uint32_t lm = 0;
+    if (x0 < Zn) {
+      const uint64_t w = *(const uint64_t*)&Z[x0];
+      const uint64_t v = w ^ 0x3c3c3c3c3c3c3c3cull;
+      const uint64_t y = (((v & 0x7f7f7f7f7f7f7f7full) + 0x7f7f7f7f7f7f7f7full) | v) & 0x8080808080808080ull;
+      lm = (uint32_t)((((~y & 0x8080808080808080ull) >> 7) * 0x0102040810204080ull) >> 56);
+      const int nb = Zn - x0;
+      if (nb < 8) lm &= (1u << nb) - 1u;
+    }
+    const int cnt = __popc(lm);
+    const int incl = wave_incl_sum(cnt);
+    int k = nc + incl - cnt;
+    for (uint32_t m = lm; m; m &= m - 1, ++k)
+      if (k < 64) s.cand[k] = (uint16_t)(x0 + __ffs(m) - 1);
+    nc += __shfl(incl, 63, 64);
     if (nc > 63) return false;  // (lane k owns token k AND the gap after it: ntok <= 63)
   }
   if (lane < nc) s.cand_tok[lane] = 0;
@@ -2466,6 +2509,9 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
     base_params_.pat_E[p] = E;
   }
   base_params_.content_cap = content_cap_;
+  for (int p = 0; p < base_params_.npat; ++p)
+    for (int j = 0; j < pattern_len(ts_, p); ++j)
+      base_params_.pw[p][j >> 3] |= (uint64_t)pattern_byte(ts_, p, j) << (8 * (j & 7));
   base_params_.fast = 15;
   if (const char* kf = env_get("QMX_KFAST")) base_params_.fast = (uint32_t)strtoul(kf, nullptr, 0);
   for (int blk = 0; blk < 2; ++blk)

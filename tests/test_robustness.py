@@ -171,3 +171,55 @@ def test_native_fatal_signal_leaves_backtrace(tmp_path):
     err = err.decode(errors="replace")
     assert proc.returncode == -signal.SIGSEGV, (proc.returncode, err[-2000:])
     assert "qmx fatal: signal 11" in err and "#0 " in err, err[-2000:]
+
+
+def test_native_threads_never_read_environ_while_it_changes():
+    """Regression (the round-2 'spread delta loss'): a native thread called getenv while a
+    library thread wrote the environment, and the process died in getenv.  Native code now
+    reads a snapshot (qmx_env.h).  Here the environment is rewritten in a tight loop (a
+    putenv/unsetenv pair reallocates ``environ``) while a native server answers requests
+    whose auth comes from OPENAI_API_KEY (read per request) — the server must survive and
+    answer every one."""
+    import threading
+
+    import httpx
+
+    from quorum_amd.ops import native as _native
+    from conftest import cfg_parallel, sse_stream
+    from live_upstream import LiveUpstream, native_server
+
+    if not _native.available():
+        pytest.skip("native extension not built")
+    live = LiveUpstream()
+    p1 = live.serve("a", ("stream", 200, sse_stream(["x"])))
+    cfg = cfg_parallel(2, block={"separator": "\n", "hide_intermediate_think": True, "hide_final_think": False,
+                                 "thinking_tags": ["think"], "skip_final_aggregation": False})
+    for b in cfg["primary_backends"]:
+        b["url"] = f"http://127.0.0.1:{p1}/v1"
+    stop = threading.Event()
+
+    def churn():
+        i = 0
+        while not stop.is_set():
+            os.environ[f"QMX_CHURN_{i % 64}"] = "x" * (i % 200)
+            os.environ.pop(f"QMX_CHURN_{(i + 32) % 64}", None)
+            i += 1
+
+    os.environ["OPENAI_API_KEY"] = "churn-key"
+    th = threading.Thread(target=churn, daemon=True)
+    try:
+        with native_server(cfg, key_from_env=True) as port:
+            th.start()
+            with httpx.Client() as c:
+                for _ in range(80):
+                    r = c.post(f"http://127.0.0.1:{port}/chat/completions",
+                               json={"messages": [{"role": "user", "content": "q"}], "stream": True}, timeout=20)
+                    assert r.status_code == 200 and "[DONE]" in r.text
+    finally:
+        stop.set()
+        if th.is_alive():
+            th.join()
+        for i in range(64):
+            os.environ.pop(f"QMX_CHURN_{i}", None)
+        os.environ.pop("OPENAI_API_KEY", None)
+        live.close()
