@@ -1010,23 +1010,26 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   // scanner (both by lane 0, rare) — exact either way.
   int packed_local[4];
   // S3a: content events of the stream's known shape (its own or its backend's template),
-  // one wave per event by static assignment, one 8-byte word per lane: the prefix and suffix
+  // half a wave per event by static assignment, one 8-byte word per lane: the prefix and suffix
   // words compared with the template, the body bytes tested with SWAR for anything that would
   // need a real string scan ('"', '\\', control bytes, non-ASCII).  An event that passes has
   // the template's parse with an escape-free body — exactly wave_tpl_match + wave_str_body's
   // answer for it — at ~4 dependent LDS round trips instead of an atomic claim, two ballot
   // passes and LDS atomics per event.  Everything else (0xFF) goes through the loop below.
   {
-    const int w = tid >> 6, lane = tid & 63;
+    // half a wave per event (32 lanes x 8 bytes: events up to 256 bytes), two per wave
+    const int hw = tid >> 5, lane = tid & 31;
     const int tp = s.v[V_TPLPRE], ts = s.v[V_TPLSUF];
     int newest = -1, nm = 0;
-    for (int k = w; k < nev; k += BS / 64) {
-      const int e0 = s.ev_a[k], e1 = s.ev_b[k], L = e1 - e0;
-      bool ok = (P.fast & 2) && tp > 0 && L >= tp + ts && L <= 512;
-      if (ok) {
+    for (int kb = 0; kb < nev; kb += BS / 32) {
+      const int k = kb + hw;
+      const bool have = k < nev;
+      const int e0 = have ? s.ev_a[k] : 0, e1 = have ? s.ev_b[k] : 0, L = e1 - e0;
+      bool ok = have && (P.fast & 2) && tp > 0 && L >= tp + ts && L <= 256;
+      {
         bool bad = false;
         const int o = lane * 8;
-        if (o < L) {
+        if (ok && o < L) {
           const int nb = min(8, L - o);
           const uint64_t valid = nb == 8 ? ~0ull : ((1ull << (8 * nb)) - 1);
           const uint64_t ev = lds_window8(s.A, e0 + o, e1);
@@ -1040,7 +1043,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
             sw = ss >= 0 ? lds_window8(s.tpl + TPL_PRE_MAX, 0, ts) << (8 * ss)
                          : lds_window8(s.tpl + TPL_PRE_MAX, -ss, ts);
           }
-          const uint64_t tw = pe > 0 ? ((const uint64_t*)s.tpl)[lane] : 0ull;
+          const uint64_t tw = pe > 0 ? ((const uint64_t*)s.tpl)[lane] : 0ull;  // (lane < 32: o < 256)
           const uint64_t bmask = valid & ~pmask & ~smask;
           const uint64_t hi = 0x8080808080808080ull, one = 0x0101010101010101ull;
           const uint64_t q = ev ^ 0x2222222222222222ull, b = ev ^ 0x5c5c5c5c5c5c5c5cull;
@@ -1049,9 +1052,10 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
           const uint64_t odd = (((q - one) & ~q) | ((b - one) & ~b) | ((ev - 0x20 * one) & ~ev) | ev) & hi;
           bad = ((ev ^ tw) & pmask) != 0 || ((ev ^ sw) & smask) != 0 || (odd & bmask) != 0;
         }
-        ok = __ballot(bad) == 0;
+        const uint64_t bm = __ballot(bad);
+        ok = ok && ((tid >> 5) & 1 ? (bm >> 32) : (bm & 0xffffffffull)) == 0;  // this half's lanes
       }
-      if (lane == 0) {
+      if (lane == 0 && have) {
         s.ev_kind[k] = ok ? (uint8_t)EV_CONTENT : (uint8_t)0xFF;
         if (ok) {
           s.ev_sa[k] = (uint16_t)(e0 + tp);
@@ -1064,7 +1068,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
         ++nm;
       }
     }
-    if (lane == 0 && nm > 0) {
+    if (lane == 0 && nm > 0) {  // (both half-waves)
       atomicAdd(&s.v[V_NTPL], nm);
       atomicMax(&s.v[V_TPLK], newest);  // the tile's newest content event becomes the template
     }
