@@ -1026,8 +1026,9 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       const bool have = k < nev;
       const int e0 = have ? s.ev_a[k] : 0, e1 = have ? s.ev_b[k] : 0, L = e1 - e0;
       bool ok = have && (P.fast & 2) && tp > 0 && L >= tp + ts && L <= 256;
+      bool shape_bad = false;  // the prefix / suffix words differ (not just an odd body byte)
       {
-        bool bad = false;
+        bool bad = false, sbad = false;
         const int o = lane * 8;
         if (ok && o < L) {
           const int nb = min(8, L - o);
@@ -1050,13 +1051,20 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
           // any '"', '\\', byte < 0x20 or >= 0x80 (the zero / less-than tricks only ever err
           // towards "bad", which just sends the event down the exact path)
           const uint64_t odd = (((q - one) & ~q) | ((b - one) & ~b) | ((ev - 0x20 * one) & ~ev) | ev) & hi;
-          bad = ((ev ^ tw) & pmask) != 0 || ((ev ^ sw) & smask) != 0 || (odd & bmask) != 0;
+          sbad = ((ev ^ tw) & pmask) != 0 || ((ev ^ sw) & smask) != 0;
+          bad = sbad || (odd & bmask) != 0;
         }
-        const uint64_t bm = __ballot(bad);
-        ok = ok && ((tid >> 5) & 1 ? (bm >> 32) : (bm & 0xffffffffull)) == 0;  // this half's lanes
+        const uint64_t bm = __ballot(bad), sm = __ballot(sbad);
+        const bool upper = (tid >> 5) & 1;
+        ok = ok && (upper ? (bm >> 32) : (bm & 0xffffffffull)) == 0;  // this half's lanes
+        shape_bad = (upper ? (sm >> 32) : (sm & 0xffffffffull)) != 0 || L < tp + ts;
       }
+      // unresolved: 0xFE when the stream template cannot match (its prefix / suffix differ:
+      // the loop skips its own template compare), 0xFF otherwise (an escaped or non-ASCII
+      // body the loop's exact string check may still accept, or no check ran)
+      const bool examined = (P.fast & 2) && tp > 0 && L <= 256 && shape_bad;
       if (lane == 0 && have) {
-        s.ev_kind[k] = ok ? (uint8_t)EV_CONTENT : (uint8_t)0xFF;
+        s.ev_kind[k] = ok ? (uint8_t)EV_CONTENT : examined ? (uint8_t)0xFE : (uint8_t)0xFF;
         if (ok) {
           s.ev_sa[k] = (uint16_t)(e0 + tp);
           s.ev_sb[k] = (uint16_t)(e1 - ts);
@@ -1091,7 +1099,8 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       // reason, usage, [DONE] — usually have their own shape and need a full parse), then the
       // middle, which by then matches a published template: the few full parses overlap
       const int k = nev <= 8 ? g : g < 4 ? g : g < 8 ? nev - 1 - (g - 4) : g - 4;
-      if (s.ev_kind[k] != 0xFF) continue;  // resolved by S3a
+      const int k0 = s.ev_kind[k];
+      if (k0 < 0xFE) continue;  // resolved by S3a
       const int e0 = s.ev_a[k], e1 = s.ev_b[k];
       int kind = EV_SKIP, sa = 0, sb = 0, body = -1;
       bool slow = false, lexed = false;
@@ -1099,7 +1108,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       const bool probe = P.dbg != nullptr;
       const uint64_t c0 = probe ? __builtin_amdgcn_s_memtime() : 0;
       uint64_t c1 = 0;
-      if (tp > 0 && e1 - e0 >= tp + ts && wave_tpl_match(s.A, e0, e1, s.tpl, tp, ts) &&
+      if (k0 == 0xFF && tp > 0 && e1 - e0 >= tp + ts && wave_tpl_match(s.A, e0, e1, s.tpl, tp, ts) &&
           (body = wave_str_body(s.A, e0 + tp, e1 - ts)) >= 0) {
         kind = EV_CONTENT;  // same shape as this stream's last parsed content event
         sa = e0 + tp;
@@ -1744,21 +1753,30 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
                                  : ndig == 2 ? (uint32_t)('0' + ix / 10) | ((uint32_t)('0' + ix % 10) << 8)
                                              : (uint32_t)('0' + ix / 100) | ((uint32_t)('0' + (ix / 10) % 10) << 8) |
                                                    ((uint32_t)('0' + ix % 10) << 16);
-        for (int idx = tid; idx < n_emit * EVL; idx += BS) {
-          int k = idx / EVL, bpos = idx - k * EVL;
-          int j = s.ejx[k];
-          int o;
-          uint8_t ch;
-          if (bpos < PRE) {
-            o = k * EVL + (j ? (int)s.epos[j - 1] : 0) + bpos;
-            ch = bpos < P.pre1_len ? (uint8_t)P.pre1[bpos]
-                 : bpos < P.pre1_len + ndig ? (uint8_t)(dg_packed >> (8 * (bpos - P.pre1_len)))
-                                            : (uint8_t)P.pre2[bpos - P.pre1_len - ndig];
-          } else {
-            o = k * EVL + PRE + (int)s.epos[j] + (bpos - PRE);
-            ch = (uint8_t)P.suf[bpos - PRE];
+        // 8 envelope bytes per thread: one division, one ejx / epos lookup per 8 bytes
+        const int CPE = (EVL + 7) >> 3;  // chunks per event
+        for (int idx = tid; idx < n_emit * CPE; idx += BS) {
+          const int k = idx / CPE, b0 = (idx - k * CPE) * 8;
+          const int j = s.ejx[k];
+          const int opre = k * EVL + (j ? (int)s.epos[j - 1] : 0);  // the event's start
+          const int osuf = k * EVL + PRE + (int)s.epos[j] - PRE;    // + bpos for suffix bytes
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int bpos = b0 + q;
+            if (bpos >= EVL) break;
+            int o;
+            uint8_t ch;
+            if (bpos < PRE) {
+              o = opre + bpos;
+              ch = bpos < P.pre1_len ? (uint8_t)P.pre1[bpos]
+                   : bpos < P.pre1_len + ndig ? (uint8_t)(dg_packed >> (8 * (bpos - P.pre1_len)))
+                                              : (uint8_t)P.pre2[bpos - P.pre1_len - ndig];
+            } else {
+              o = osuf + bpos;
+              ch = (uint8_t)P.suf[bpos - PRE];
+            }
+            if (o >= w0 && o < w1) O[o - w0] = ch;
           }
-          if (o >= w0 && o < w1) O[o - w0] = ch;
         }
       }
       // escaped content
