@@ -42,7 +42,8 @@ BASELINE_SOURCE_SURVEY = "reference proxy, survey container (8 vCPU, Python harn
 # port layout above --port: +7.. exchange mesh, +50 the spread check's proxies (+57.. its mesh),
 # +100 + 10 rank + i mock backends, +200 + rank / +230 + rank each rank's own admin port
 # (headline / spread check)
-ADMIN_OFF, SPREAD_ADMIN_OFF = 200, 230
+ADMIN_OFF, SPREAD_ADMIN_OFF, LOCAL_ADMIN_OFF, EAGER_ADMIN_OFF = 200, 230, 240, 250
+PROBE_REQUESTS = 256  # spread check: requests of the one-connection latency probes
 
 # BASELINE.json configs.  "headline" is the driver's metric; the others are measured with
 # --scenario; every one with a reference number has it from the same harness.
@@ -419,9 +420,27 @@ def spread_summary(rows) -> dict:
         for k, v in (r.get("remote_ends") or {}).items():
             ends[k] = ends.get(k, 0) + int(v)
     out["remote_ends"] = ends
+
+    def med(vals):
+        vals = [v for v in vals if v is not None]
+        return round(statistics.median(vals), 3) if vals else None
+
+    # one session at a time per rank: spread vs the same config with local placement
+    # (probe: the eager default; probe_rendezvous: every final text through a round)
+    for name in ("probe", "probe_rendezvous", "local_probe"):
+        out[f"{name}_p50_latency_ms"] = med([(r.get(name) or {}).get("p50_latency_ms") for r in rows])
+        out[f"{name}_ok"] = all((r.get(name) or {}).get("ok") for r in rows)
+        out["ok"] = out["ok"] and out[f"{name}_ok"]  # every probe response is validated too
+    out["probe_eager_finals"] = int(sum((r.get("probe") or {}).get("eager_finals") or 0 for r in rows))
+    hop_src = (("hops_us_loaded", lambda r: r.get("hops_us")), ("hops_us_probe", lambda r: (r.get("probe") or {}).get("hops_us")),
+               ("hops_us_probe_rendezvous", lambda r: (r.get("probe_rendezvous") or {}).get("hops_us")))
+    for key, get in hop_src:
+        hops = [get(r) or {} for r in rows]
+        out[key] = {k: med([h.get(k) for h in hops]) for k in ("open_to_first_delta", "last_delta_to_final")}
     out["per_rank"] = [{k: r.get(k) for k in ("ok", "pid", "requests", "invalid", "remote_streams", "bulk_rounds",
                                              "mesh_finals", "delta_mismatch", "worker_nodata", "remote_ends",
-                                             "up_failures", "p50_latency_ms", "error") if r.get(k)}
+                                             "up_failures", "p50_latency_ms", "hops_us", "probe", "probe_rendezvous", "local_probe",
+                                             "error") if r.get(k)}
                        for r in rows]
     return out
 
@@ -440,7 +459,7 @@ def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports
     port = args.port + 50
     admin = args.port + SPREAD_ADMIN_OFF + rank  # this rank's spread proxy alone
     out = {"ok": False}
-    procs = []
+    procs, env = [], {}
     ok, err = True, None
 
     def agree(stage: str) -> bool:
@@ -472,6 +491,9 @@ def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports
         # bytes) gives up after 3 s, not the production 30 s: its texts fall back to the mesh
         # and the check still validates every response inside the load generator's window
         env.setdefault("QMX_XCHG_TIMEOUT", "3")
+        # every final text takes a bulk round here (rendezvous), however short: the check
+        # exercises the round protocol under load; the eager default is probed separately
+        env.setdefault("QMX_XCHG_EAGER_BYTES", "0")
         try:
             cfg = os.path.join(tmp, "config_spread.yaml")
             write_config(cfg, mock_ports, False, args.tile, sc, "spread")
@@ -542,17 +564,108 @@ def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports
                                                 if k.startswith("qmx_spread_remote_ends_total") and v},
                                 "up_failures": {k.split('"')[1]: v for k, v in d.items()
                                                 if k.startswith("qmx_upstream_failures_by_class_total") and v},
-                                "epochs": m1.get("qmx_exchange_epochs_total", 0.0)})
+                                "epochs": m1.get("qmx_exchange_epochs_total", 0.0),
+                                # owner side, means: X_OPEN -> first delta back; last delta -> final applied
+                                "hops_us": hop_means(d)})
                 except Exception as e:  # noqa: BLE001
                     ok, err = False, repr(e)[:300]
+            # the latency of one session at a time (1 connection per rank): the closed-loop
+            # check above runs the box at its CPU limit, where latency is queueing
+            if agree("probe"):
+                try:
+                    m0 = scrape(admin)
+                    pr = loadgen(bin_dir, port, 1, PROBE_REQUESTS, 1, 120, spec)
+                    m1 = scrape(admin)
+                    d = {k: m1.get(k, 0.0) - m0.get(k, 0.0) for k in m1}
+                    out["probe_rendezvous"] = {"ok": pr["invalid"] == 0 and pr["errors"] == 0 and pr["completed"] == PROBE_REQUESTS,
+                                    "p50_latency_ms": pr["lat_p50_ms"], "p50_ttft_ms": pr["ttft_p50_ms"],
+                                    "hops_us": hop_means(d)}
+                except Exception as e:  # noqa: BLE001
+                    ok, err = False, repr(e)[:300]
+                agree("probe done")  # a rank's proxy serves its peers' remote streams to the end
     except Exception as e:  # noqa: BLE001 - reported in the JSON line
         ok, err = False, repr(e)[:300]
     finally:
         _kill(procs)
+    # one session at a time per rank on two more proxy sets of the same config: spread with
+    # the production default (short final texts eager over the mesh) and local placement (the
+    # control).  Their failures are reported, not fatal; every rank joins the same collectives.
+    if agree("probes"):
+        nonce = [str(time.time_ns()) if rank == 0 else None]
+        dist.broadcast_object_list(nonce, src=0)
+        xenv = exchange_env(rank, world, args.port + 20, nonce[0])
+        xenv.update({k: env[k] for k in ("QMX_XCHG", "QMX_XCHG_TIMEOUT") if k in env})
+        out["probe"] = probe_set(args, "spread_eager", "spread", args.port + 20, args.port + EAGER_ADMIN_OFF + rank,
+                                 xenv, sc, engine, device, bin_dir, tmp, mock_ports, dist, n_dev >= world)
+        out["local_probe"] = probe_set(args, "spread_local", "local", args.port + 80, args.port + LOCAL_ADMIN_OFF + rank,
+                                       {}, sc, engine, device, bin_dir, tmp, mock_ports, dist, n_dev >= world)
     if err:
         out["ok"] = False
         out["error"] = err
     return out
+
+
+def probe_set(args, label, placement, port, admin, xenv, sc, engine, device, bin_dir, tmp, mock_ports, dist,
+              on_gpu) -> dict:
+    """Spawn one proxy per rank on ``port`` (``placement``; ``xenv``: its exchange settings),
+    wait until every rank's is up (spread: its mesh formed), run PROBE_REQUESTS validated
+    requests over one connection, and stop the set once every rank's probe is done (a spread
+    rank serves its peers' remote streams to the end).  The result, or the failure, as a dict."""
+    from quorum_amd.serve import spawn_workers, wait_healthy
+
+    procs, err, res = [], None, {"ok": False}
+    try:
+        cfg = os.path.join(tmp, f"config_{label}.yaml")
+        write_config(cfg, mock_ports, False, args.tile, sc, placement)
+        env = dict(os.environ, **xenv, QMX_READY_FILE=os.path.join(tmp, f"ready_{label}"), QMX_ADMIN_PORT=str(admin))
+        procs = spawn_workers(cfg, "127.0.0.1", port, 1, engine, device, impl="native", threads=args.threads, env=env)
+        for p in procs:
+            p.ready_file = f"{env['QMX_READY_FILE']}.{p.pid}"
+        if not (wait_ready(procs, 60) and wait_healthy("127.0.0.1", admin, 30)):
+            raise RuntimeError(f"{label} proxy did not become ready: {[exit_status(p) for p in procs]}")
+        if placement == "spread":
+            t0 = time.time()
+            while scrape(admin).get("qmx_exchange_healthy") != 1.0:
+                if time.time() - t0 > 60:
+                    raise RuntimeError(f"{label}: the mesh did not form")
+                time.sleep(0.2)
+    except Exception as e:  # noqa: BLE001
+        err = repr(e)[:300]
+    try:
+        if torch_min_flag(dist, err is None, on_gpu):
+            m0 = scrape(admin)
+            pr = loadgen(bin_dir, port, 1, PROBE_REQUESTS, 1, 120, os.path.join(tmp, "expect_spread.txt"))
+            time.sleep(0.1)
+            d = {k: v - m0.get(k, 0.0) for k, v in scrape(admin).items()}
+            res = {"ok": pr["invalid"] == 0 and pr["errors"] == 0 and pr["completed"] == PROBE_REQUESTS,
+                   "p50_latency_ms": pr["lat_p50_ms"], "p50_ttft_ms": pr["ttft_p50_ms"]}
+            if placement == "spread":
+                res.update({"hops_us": hop_means(d), "eager_finals": d.get("qmx_spread_eager_finals_total", 0.0),
+                            "bulk_rounds": d.get("qmx_exchange_rounds_total", 0.0)})
+        else:
+            res = {"ok": False, "error": err or f"another rank's {label} set failed"}
+    except Exception as e:  # noqa: BLE001
+        res = {"ok": False, "error": repr(e)[:300]}
+    torch_min_flag(dist, True, on_gpu)  # every rank's probe is done
+    _kill(procs)
+    return res
+
+
+def torch_min_flag(dist, flag: bool, on_gpu: bool) -> bool:
+    """min over ranks of a bool (an all-reduce every rank joins)."""
+    import torch
+
+    t = torch.tensor([1.0 if flag else 0.0], device="cuda" if on_gpu else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return t.item() >= 1.0
+
+
+def hop_means(d) -> dict:
+    """Spread hop means (µs) from a /metrics delta: X_OPEN -> first delta, last delta -> final."""
+    return {k: round(1e6 * d[f"{m}_sum"] / d[f"{m}_count"], 1)
+            for k, m in (("open_to_first_delta", "qmx_spread_first_delta_seconds"),
+                         ("last_delta_to_final", "qmx_spread_final_seconds"))
+            if d.get(f"{m}_count")}
 
 
 def self_launch(n: int) -> int:

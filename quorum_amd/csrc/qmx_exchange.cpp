@@ -154,6 +154,7 @@ struct Exchange::Impl {
   // coordinator (rank 0, mesh thread only)
   std::vector<WireEntry> ann;
   double ann_deadline = 0;
+  double last_round_t = -1e9;  // coordinator: when the last round was issued
   int round_no = 0, epoch_no = 0;
   bool epoch_live = false;  // an epoch is formed (or forming) and not reported down
   bool ever_all_up = false;
@@ -364,7 +365,10 @@ struct Exchange::Impl {
         if (X->o_.rank != 0 || m.payload.size() != sizeof(WireEntry)) return;
         WireEntry e;
         std::memcpy(&e, m.payload.data(), sizeof(e));
-        if (ann.empty()) ann_deadline = now_s() + X->o_.batch_us * 1e-6;
+        // leading edge: with no round issued within the batch window the announcement goes
+        // out at once (one session at a time waits for nothing); otherwise it waits for the
+        // window's end together with whatever else arrives (under load: one round per window)
+        if (ann.empty()) ann_deadline = std::max(now_s(), last_round_t + X->o_.batch_us * 1e-6);
         ann.push_back(e);
         return;
       }
@@ -460,6 +464,7 @@ struct Exchange::Impl {
       if (e.dst != e.src) part[e.dst].push_back(e);  // (loopback: one entry, both halves)
     }
     ann.clear();
+    last_round_t = now_s();
     for (auto& kv : part) {
       XMsg m;
       m.type = F_MANIFEST;

@@ -55,7 +55,8 @@ std::atomic<uint64_t> c_fail_connect{0}, c_fail_timeout{0}, c_fail_status{0}, c_
 // the delta invariant — the owner must have received exactly the deltas the worker sent
 // before it applies the stream's final (X_BULK / X_FINAL carry the worker's count in b)
 std::atomic<uint64_t> c_sp_failed{0}, c_sp_aborted{0}, c_sp_empty{0}, c_sp_text{0}, c_sp_down{0},
-    c_sp_delta_mismatch{0}, c_sp_nodata{0} /* worker: content but no delta sent */;
+    c_sp_delta_mismatch{0}, c_sp_nodata{0} /* worker: content but no delta sent */,
+    c_sp_eager{0} /* worker: final texts sent eagerly over the mesh (no round) */;
 std::atomic<int> g_sp_logs{0};  // rate limit: the first 20 anomalies are logged with their state
 
 // Prometheus histogram with lock-free buckets (seconds)
@@ -93,6 +94,10 @@ constexpr double Hist::le[Hist::N];
 // h_engine: a stream's first upstream body bytes handed to the engine -> its final result
 // applied in the io loop (queueing for a tick lane + tick(s) + routing back)
 Hist h_ttft, h_latency, h_tick, h_upstream_ttfb, h_engine;
+// spread placement, owner side: a remote stream's X_OPEN queued -> its first delta applied
+// (the mesh hop both ways + the worker's upstream and engine), and its last delta (or open)
+// -> its final text applied (the bulk round or mesh transfer of the final)
+Hist h_sp_first, h_sp_final;
 
 using Clock = std::chrono::steady_clock;
 inline double now_s() { return std::chrono::duration<double>(Clock::now().time_since_epoch()).count(); }
@@ -350,6 +355,7 @@ struct BState {
   int slot = -1;          // engine slot (spread: the owner's shadow slot of a remote stream)
   int remote = -1;        // spread placement: rank running this stream (-1 = local)
   int rx_data = 0;        // spread: delta messages received from the worker
+  double t_sp_open = 0, t_sp_last = 0;  // spread: X_OPEN queued / last delta applied (h_sp_*)
   bool bulk_waiting = false;  // spread: the final text arrived before some of its deltas
   XMsg bulk_msg;
   Up* up = nullptr;
@@ -2081,6 +2087,7 @@ class Loop {
         m.b = (int)(cfg_.timeout * 1000.0);
         m.payload = build_req(cfg_.backends[valid[i]], s->fwd, body);
         xq(m);
+        s->bs[i].t_sp_open = now_s();
         continue;
       }
       Up* u = open_up(s, (int)i, valid[i], UP_ENGINE, build_req(cfg_.backends[valid[i]], s->fwd, body), cfg_.timeout);
@@ -2110,6 +2117,14 @@ class Loop {
       }
       if (len == 0) {
         post_owner(s, X_FINAL, b.aborted ? XF_ABORTED : 0, 0, std::string(), s->data_sent);
+        return end_session(s);
+      }
+      if ((long long)len <= (long long)cfg_.xchg_eager_bytes) {
+        // eager: a short text rides this loop's mesh frames right behind the stream's deltas
+        // (one hop, no rank-0 manifest); the owner applies it as it would a round's delivery
+        const std::string t = eng().text(b.slot);
+        post_owner(s, X_BULK, XF_TEXT, (int)t.size(), t.data(), t.size(), s->data_sent);
+        c_sp_eager++;
         return end_session(s);
       }
       // HBM content slot → the owner's shadow slot (RCCL p2p round), or its bytes over the
@@ -2250,6 +2265,9 @@ class Loop {
       if (m.bi < 0 || m.bi >= (int)s->bs.size()) continue;
       BState& b = s->bs[m.bi];
       if (m.type == X_DATA) {
+        const double t = now_s();
+        if (b.rx_data == 0 && b.t_sp_open > 0) h_sp_first.observe(t - b.t_sp_open);
+        b.t_sp_last = t;
         b.rx_data++;
         if (s->cl) send_content(s, m.payload);
         if (b.bulk_waiting && b.rx_data >= b.bulk_msg.b) {
@@ -2282,6 +2300,7 @@ class Loop {
         }
         if (m.flags & XF_ABORTED) c_sp_aborted++;
         else c_sp_empty++;
+        sp_final_time(b);
         b.state = 1;
         b.aborted = (m.flags & XF_ABORTED) != 0;
         s->finished++;
@@ -2289,12 +2308,17 @@ class Loop {
       }
     }
   }
+  static void sp_final_time(const BState& b) {
+    const double t0 = b.t_sp_last > 0 ? b.t_sp_last : b.t_sp_open;
+    if (t0 > 0) h_sp_final.observe(now_s() - t0);
+  }
   // owner: a remote stream's final text is in (HBM already, or the mesh payload)
   void remote_final(Session* s, int bi, XMsg& m) {
     BState& b = s->bs[bi];
     if (b.state != 0) return;
     delta_check(s, bi, m.b, "final text");
     c_sp_text++;
+    sp_final_time(b);
     // over the mesh the bytes are in the payload; an RCCL round already wrote them to HBM
     // (a final text is never empty: an empty one travels as X_FINAL)
     const bool bytes = !m.payload.empty();
@@ -2721,6 +2745,7 @@ class Loop {
       m += std::string("qmx_spread_remote_ends_total{how=\"") + kv.first + "\"} " + std::to_string(kv.second->load()) + "\n";
     put("qmx_spread_delta_mismatch_total", (double)c_sp_delta_mismatch.load());
     put("qmx_spread_worker_nodata_total", (double)c_sp_nodata.load());
+    put("qmx_spread_eager_finals_total", (double)c_sp_eager.load());
     m += "qmx_upstream_failures_by_class_total{class=\"connect\"} " + std::to_string(c_fail_connect.load()) + "\n";
     m += "qmx_upstream_failures_by_class_total{class=\"timeout\"} " + std::to_string(c_fail_timeout.load()) + "\n";
     m += "qmx_upstream_failures_by_class_total{class=\"http_status\"} " + std::to_string(c_fail_status.load()) + "\n";
@@ -2735,6 +2760,8 @@ class Loop {
     h_tick.render(m, "qmx_tick_seconds");
     h_upstream_ttfb.render(m, "qmx_upstream_ttfb_seconds");
     h_engine.render(m, "qmx_engine_wait_seconds");
+    h_sp_first.render(m, "qmx_spread_first_delta_seconds");
+    h_sp_final.render(m, "qmx_spread_final_seconds");
     if (xch_) {
       put("qmx_exchange_rounds_total", (double)xch_->rounds());  // RCCL p2p rounds (final texts)
       put("qmx_exchange_bytes_total", (double)xch_->bytes());    // mesh payload bytes

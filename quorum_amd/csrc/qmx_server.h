@@ -66,6 +66,10 @@ struct ServerCfg {
   int xchg_bulk_port = 0;  // tcpbulk: rank r listens on xchg_bulk_port + r (0: xchg_port + world)
   std::string xchg_id_file;
   int xchg_round_us = 200;
+  // spread: a final text up to this size rides the mesh right behind its deltas (eager: no
+  // round, no rank-0 manifest — the MPI eager protocol); a larger one takes a bulk round
+  // (rendezvous: manifest + RCCL / socket transfer).  0: every final text takes a round
+  int xchg_eager_bytes = 4096;
   double xchg_timeout = 30.0;
   // lifecycle: SIGTERM drains (no new connections; in-flight sessions finish, at most
   // drain_s seconds), SIGINT / stop_server() stop at once; ready_file is written once

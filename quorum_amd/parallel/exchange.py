@@ -38,7 +38,7 @@ def exchange_env(rank: int, world: int, port: int, nonce: Optional[str] = None) 
 
 
 def cluster_config(placement: str, exchange: str, round_us: int, timeout: float, port: int, engine: str,
-                   env: Optional[Mapping[str, str]] = None) -> Dict[str, Any]:
+                   env: Optional[Mapping[str, str]] = None, eager_bytes: int = 4096) -> Dict[str, Any]:
     """Rank / placement / exchange settings of the native server (env wins: QMX_RANK,
     QMX_WORLD, QMX_XCHG_*).  ``exchange: auto`` = RCCL with the HIP engine, else TCP."""
     e = os.environ if env is None else env
@@ -61,4 +61,6 @@ def cluster_config(placement: str, exchange: str, round_us: int, timeout: float,
         # rank 0 batches bulk announcements arriving within this window into one round
         "xchg_round_us": int(e.get("QMX_XCHG_ROUND_US", str(round_us))),
         "xchg_timeout": float(e.get("QMX_XCHG_TIMEOUT", str(timeout))),
+        # final texts up to this size ride the mesh behind their deltas (eager, no round)
+        "xchg_eager_bytes": int(e.get("QMX_XCHG_EAGER_BYTES", str(eager_bytes))),
     }

@@ -117,7 +117,8 @@ def cluster_config(rt: RuntimeConfig, port: int, engine: str) -> Dict[str, Any]:
     from ..parallel.exchange import cluster_config as _cc
 
     try:
-        return _cc(rt.placement, rt.exchange, rt.exchange_round_us, rt.exchange_timeout, port, engine)
+        return _cc(rt.placement, rt.exchange, rt.exchange_round_us, rt.exchange_timeout, port, engine,
+                   eager_bytes=rt.exchange_eager_bytes)
     except ValueError as exc:
         raise NativeUnsupported(str(exc)) from exc
 

@@ -89,6 +89,7 @@ int main(int argc, char** argv) {
   c.xchg_port = gi(d, "xchg_port", 0);
   c.xchg_id_file = gs(d, "xchg_id_file", "");
   c.xchg_round_us = gi(d, "xchg_round_us", c.xchg_round_us);
+  c.xchg_eager_bytes = gi(d, "xchg_eager_bytes", c.xchg_eager_bytes);
   c.xchg_timeout = gd(d, "xchg_timeout", c.xchg_timeout);
   c.drain_s = gd(d, "drain_s", c.drain_s);
   c.ready_file = gs(d, "ready_file", "");

@@ -211,6 +211,9 @@ class RuntimeConfig:
     exchange:  spread transport: "auto" (rccl with a GPU engine, else tcp) | "rccl" | "tcp"
     exchange_round_us: pacing of the lock-step all-gather rounds while traffic flows
     exchange_timeout: a round slower than this = peer failure (fall back to local placement)
+    exchange_eager_bytes: spread final texts up to this size ride the mesh right behind their
+               deltas (eager); larger ones take a bulk round — rank-0 manifest, RCCL / socket
+               transfer (rendezvous); 0 = every text takes a round — QMX_XCHG_EAGER_BYTES
     total_timeout: optional per-backend total deadline in seconds (None = quorum semantics)
     drain_timeout: SIGTERM grace period for in-flight sessions (rolling reload / shutdown)
     verify:    debug mode: a shadow CPU oracle engine checks every stream and final (QMX_VERIFY=1)
@@ -235,6 +238,7 @@ class RuntimeConfig:
     exchange: str = "auto"
     exchange_round_us: int = 200
     exchange_timeout: float = 30.0
+    exchange_eager_bytes: int = 4096
     total_timeout: Optional[float] = None
     drain_timeout: float = 10.0
     verify: bool = False

@@ -136,6 +136,12 @@ def test_bench_gpus_flag_self_launches_ranks(tmp_path):
     assert sc["transport"] == "tcpbulk" and sc["bulk_formed"] is True
     assert sc["bulk_rounds"] > 0 and sc["mesh_finals"] == 0 and sc["remote_ends"] == {"text": 4 * 2048}
     assert len({x["pid"] for x in sc["per_rank"]}) == 4
+    # one-session latency probes, every response validated: rendezvous (every text through
+    # a round), the eager default (short texts behind their deltas, no round) and local
+    assert sc["probe_rendezvous_ok"] and sc["probe_ok"] and sc["local_probe_ok"]
+    assert sc["probe_eager_finals"] == 4 * 256
+    assert all(r["probe"]["bulk_rounds"] == 0 for r in sc["per_rank"])
+    assert sc["hops_us_probe"]["last_delta_to_final"] is not None
     # every session has one remote stream, run by the next rank: each rank's own counter
     # is its own share, and the shares add up to every session once
     assert sum(x["remote_streams"] for x in sc["per_rank"]) == 4 * 2048

@@ -38,10 +38,11 @@ THINK = [sse_chunk({"role": "assistant"}), sse_chunk({"content": "<think>"}), ss
 
 
 @contextlib.contextmanager
-def native_cluster(cfg, world: int, placement: str = "spread", xchg: str = "tcp"):
+def native_cluster(cfg, world: int, placement: str = "spread", xchg: str = "tcp", eager=None):
     """`world` native ranks in-process (threads), TCP exchange on a free port block.
     ``xchg="tcpbulk"``: final texts move in rank-0-numbered bulk rounds (the RCCL round
-    protocol with a socket executor) instead of riding the mesh."""
+    protocol with a socket executor) instead of riding the mesh.  ``eager``: the largest final
+    text that rides the mesh behind its deltas instead (None: the default; 0: none)."""
     from quorum_amd.runtime.native_server import native_config
 
     ext = native.require()
@@ -56,6 +57,8 @@ def native_cluster(cfg, world: int, placement: str = "spread", xchg: str = "tcp"
     for r in range(world):
         env = {"QMX_RANK": str(r), "QMX_WORLD": str(world), "QMX_XCHG": xchg, "QMX_XCHG_PORT": str(xport),
                "QMX_XCHG_ROUND_US": "100"}
+        if eager is not None:
+            env["QMX_XCHG_EAGER_BYTES"] = str(eager)
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
         try:
@@ -160,9 +163,13 @@ SPREAD_CASES = {
 }
 
 
-@pytest.mark.parametrize("world,xchg", [(2, "tcp"), (3, "tcp"), (2, "tcpbulk"), (4, "tcpbulk")])
+@pytest.mark.parametrize("world,xchg,eager", [(2, "tcp", None), (3, "tcp", 0), (2, "tcpbulk", 0), (4, "tcpbulk", 0),
+                                               (3, "tcpbulk", None)])
 @pytest.mark.parametrize("name", sorted(SPREAD_CASES))
-def test_spread_matches_local(name, world, xchg):
+def test_spread_matches_local(name, world, xchg, eager):
+    """Spread responses equal single-rank ones, with every final-text path: eager (short texts
+    ride the mesh behind their deltas: the default), mesh bulk (tcp, eager off) and bulk
+    rounds (tcpbulk, eager off)."""
     n, block, strategy, behs = SPREAD_CASES[name]
     live, ports = _live({f"b{i + 1}": b for i, b in enumerate(behs)})
     try:
@@ -172,13 +179,16 @@ def test_spread_matches_local(name, world, xchg):
             ref = httpx.post(f"http://127.0.0.1:{p}/chat/completions", json=req, headers=AUTH, timeout=30)
         ref_calls = sorted(json.dumps(c["body"], sort_keys=True) for c in live.calls)
         live.calls.clear()
-        with native_cluster(cfg, world, xchg=xchg) as cports:
+        with native_cluster(cfg, world, xchg=xchg, eager=eager) as cports:
+            # (in-process ranks share one process's counters, across tests too: deltas)
+            m0 = [httpx.get(f"http://127.0.0.1:{p}/metrics").text for p in cports]
             for owner in range(world):  # every rank as session owner
                 r = httpx.post(f"http://127.0.0.1:{cports[owner]}/chat/completions", json=req, headers=AUTH,
                                timeout=30)
                 assert r.status_code == ref.status_code
                 assert _split(_events(r.text)) == _split(_events(ref.text)), (name, owner)
-            m = httpx.get(f"http://127.0.0.1:{cports[0]}/metrics").text
+            ms = [httpx.get(f"http://127.0.0.1:{p}/metrics").text for p in cports]
+            m = ms[0]
         # each owner's run sent exactly the single-rank upstream requests
         calls = sorted(json.dumps(c["body"], sort_keys=True) for c in live.calls)
         assert calls == sorted(ref_calls * world)
@@ -186,9 +196,22 @@ def test_spread_matches_local(name, world, xchg):
         remote = float([ln for ln in m.splitlines() if ln.startswith("qmx_remote_streams_total")][0].split()[1])
         assert remote >= 1, m
         assert _metric(m, "qmx_spread_delta_mismatch_total") == 0
-        if xchg == "tcpbulk" and not block.get("skip_final_aggregation"):
-            # final texts moved by bulk rounds, none over the mesh
-            assert _metric(m, "qmx_exchange_mesh_finals_total") == 0, m
+        def total(k):
+            # exchange counters are per rank (summed); server counters are per process, which
+            # the in-process ranks share (rank 0's delta)
+            ranks = range(world) if k.startswith("qmx_exchange_") else [0]
+            return sum(_metric(ms[r], k) - _metric(m0[r], k) for r in ranks)
+        texts = total("qmx_spread_remote_ends_total{how=\"text\"}")
+        if eager is None:  # short texts: every one eager, nothing through a round or mesh bulk
+            assert total("qmx_spread_eager_finals_total") == texts
+            assert total("qmx_exchange_mesh_finals_total") == 0 and total("qmx_exchange_rounds_total") == 0
+        else:
+            assert total("qmx_spread_eager_finals_total") == 0
+            if xchg == "tcpbulk":  # final texts moved by bulk rounds, none over the mesh
+                assert total("qmx_exchange_mesh_finals_total") == 0, m
+                assert (total("qmx_exchange_rounds_total") > 0) == (texts > 0)
+            else:
+                assert total("qmx_exchange_mesh_finals_total") == texts
     finally:
         live.close()
 
