@@ -42,7 +42,7 @@ BASELINE_SOURCE_SURVEY = "reference proxy, survey container (8 vCPU, Python harn
 # port layout above --port: +7.. exchange mesh, +50 the spread check's proxies (+57.. its mesh),
 # +100 + 10 rank + i mock backends, +200 + rank / +230 + rank each rank's own admin port
 # (headline / spread check)
-ADMIN_OFF, SPREAD_ADMIN_OFF, LOCAL_ADMIN_OFF, EAGER_ADMIN_OFF = 200, 230, 240, 250
+ADMIN_OFF, SPREAD_ADMIN_OFF, LOCAL_ADMIN_OFF, RDV_ADMIN_OFF = 200, 230, 240, 250
 PROBE_REQUESTS = 256  # spread check: requests of the one-connection latency probes
 
 # BASELINE.json configs.  "headline" is the driver's metric; the others are measured with
@@ -406,248 +406,227 @@ def compact_breakdown(rank: int, bd: dict, row) -> dict:
 
 
 def spread_summary(rows) -> dict:
-    """The spread check of every rank, compact: totals plus each rank's own counters."""
-    keys = ("requests", "invalid", "remote_streams", "bulk_rounds", "bulk_final_bytes", "mesh_finals", "delta_mismatch",
-            "worker_nodata", "peer_downs")
-    out = {"ok": all(r.get("ok") for r in rows), "transport": rows[0].get("transport"),
-           "bulk_formed": all(r.get("bulk_formed") for r in rows)}
-    for k in keys:
-        out[k] = int(sum(r.get(k) or 0 for r in rows))
-    lat = [r["p50_latency_ms"] for r in rows if r.get("p50_latency_ms") is not None]
-    out["p50_latency_ms"] = round(statistics.median(lat), 3) if lat else None
-    ends = {}
-    for r in rows:
-        for k, v in (r.get("remote_ends") or {}).items():
-            ends[k] = ends.get(k, 0) + int(v)
-    out["remote_ends"] = ends
-
+    """The spread check of every rank, compact: totals plus each rank's own counters.  ``main``:
+    the production defaults under load (short final texts eager); ``rendezvous``: every final
+    text through a bulk round (RCCL on GPUs, tcpbulk in rehearsals); ``local``: the control."""
     def med(vals):
         vals = [v for v in vals if v is not None]
         return round(statistics.median(vals), 3) if vals else None
 
-    # one session at a time per rank: spread vs the same config with local placement
-    # (probe: the eager default; probe_rendezvous: every final text through a round)
-    for name in ("probe", "probe_rendezvous", "local_probe"):
-        out[f"{name}_p50_latency_ms"] = med([(r.get(name) or {}).get("p50_latency_ms") for r in rows])
-        out[f"{name}_ok"] = all((r.get(name) or {}).get("ok") for r in rows)
-        out["ok"] = out["ok"] and out[f"{name}_ok"]  # every probe response is validated too
-    out["probe_eager_finals"] = int(sum((r.get("probe") or {}).get("eager_finals") or 0 for r in rows))
-    hop_src = (("hops_us_loaded", lambda r: r.get("hops_us")), ("hops_us_probe", lambda r: (r.get("probe") or {}).get("hops_us")),
-               ("hops_us_probe_rendezvous", lambda r: (r.get("probe_rendezvous") or {}).get("hops_us")))
-    for key, get in hop_src:
-        hops = [get(r) or {} for r in rows]
-        out[key] = {k: med([h.get(k) for h in hops]) for k in ("open_to_first_delta", "last_delta_to_final")}
-    out["per_rank"] = [{k: r.get(k) for k in ("ok", "pid", "requests", "invalid", "remote_streams", "bulk_rounds",
-                                             "mesh_finals", "delta_mismatch", "worker_nodata", "remote_ends",
-                                             "up_failures", "p50_latency_ms", "hops_us", "probe", "probe_rendezvous", "local_probe",
-                                             "error") if r.get(k)}
-                       for r in rows]
+    def get(r, *path):
+        for k in path:
+            r = (r or {}).get(k)
+        return r
+
+    def tot(*path):
+        return int(sum(get(r, *path) or 0 for r in rows))
+
+    def ends(*path):
+        e = {}
+        for r in rows:
+            for k, v in (get(r, *path) or {}).items():
+                e[k] = e.get(k, 0) + int(v)
+        return e
+
+    def hops(*path):
+        hs = [get(r, *path) or {} for r in rows]
+        return {k: med([h.get(k) for h in hs]) for k in ("open_to_first_delta", "last_delta_to_final")}
+
+    passes = [("main", "load"), ("main", "probe"), ("rendezvous", "load"), ("rendezvous", "probe"), ("local", "probe")]
+    out = {"ok": all(r.get("ok") for r in rows), "transport": rows[0].get("transport"),
+           # main set under load (32 connections per rank, 2048 requests each)
+           "requests": tot("main", "load", "requests"),
+           "invalid": sum(tot(a, b, "invalid") for a, b in passes),
+           "remote_streams": tot("main", "load", "remote_streams"),
+           "eager_finals": tot("main", "load", "eager_finals"),
+           "mesh_finals": tot("main", "load", "mesh_finals") + tot("rendezvous", "load", "mesh_finals"),
+           "delta_mismatch": sum(tot(a, b, "delta_mismatch") for a, b in passes[:4]),
+           "worker_nodata": sum(tot(a, b, "worker_nodata") for a, b in passes[:4]),
+           "peer_downs": sum(tot(a, b, "peer_downs") for a, b in passes[:4]),
+           "remote_ends": ends("main", "load", "remote_ends"),
+           "p50_latency_ms": med([get(r, "main", "load", "p50_latency_ms") for r in rows]),
+           "hops_us_loaded": hops("main", "load", "hops_us"),
+           # one session at a time per rank: spread (defaults) vs the same config placed locally
+           "probe_p50_latency_ms": med([get(r, "main", "probe", "p50_latency_ms") for r in rows]),
+           "local_probe_p50_latency_ms": med([get(r, "local", "probe", "p50_latency_ms") for r in rows]),
+           "hops_us_probe": hops("main", "probe", "hops_us"),
+           # every final text through a round: the RCCL / tcpbulk round protocol exercised
+           "bulk_formed": all(get(r, "rendezvous", "bulk_formed") for r in rows),
+           "bulk_rounds": tot("rendezvous", "load", "bulk_rounds") + tot("rendezvous", "probe", "bulk_rounds"),
+           "rendezvous": {"requests": tot("rendezvous", "load", "requests") + tot("rendezvous", "probe", "requests"),
+                          "bulk_final_bytes": tot("rendezvous", "load", "bulk_final_bytes")
+                          + tot("rendezvous", "probe", "bulk_final_bytes"),
+                          "remote_ends": ends("rendezvous", "load", "remote_ends"),
+                          "p50_latency_ms": med([get(r, "rendezvous", "load", "p50_latency_ms") for r in rows]),
+                          "probe_p50_latency_ms": med([get(r, "rendezvous", "probe", "p50_latency_ms") for r in rows]),
+                          "hops_us_probe": hops("rendezvous", "probe", "hops_us")}}
+    errs = [f"rank {i} {k}: {get(r, k, 'error')}" for i, r in enumerate(rows) for k in ("main", "rendezvous", "local")
+            if get(r, k, "error")]
+    if errs or any(r.get("error") for r in rows):
+        out["errors"] = (errs + [f"rank {i}: {r['error']}" for i, r in enumerate(rows) if r.get("error")])[:8]
+
+    def compact(d):
+        keep = ("requests", "invalid", "p50_latency_ms", "remote_streams", "eager_finals", "bulk_rounds", "mesh_finals",
+                "delta_mismatch", "worker_nodata", "remote_ends", "up_failures", "hops_us", "error")
+        return {k: v for k, v in (d or {}).items() if k in keep and v}
+
+    def rank_error(r):
+        e = [f"{k}: {get(r, k, 'error')}" for k in ("main", "rendezvous", "local") if get(r, k, "error")]
+        return "; ".join(e + ([r["error"]] if r.get("error") else [])) or None
+
+    out["per_rank"] = [{"ok": r.get("ok"), "pid": get(r, "main", "pid"), "error": rank_error(r),
+                        **{f"{a}_{b}": compact(get(r, a, b)) for a, b in passes}} for r in rows]
     return out
 
 
 def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports, dist, n_dev):
-    """Outside the timed region, N > 1: expert-parallel placement end to end.  A second proxy
-    set on port + 50 runs the headline backends with ``placement: spread`` and the final
-    event on (skip_final_aggregation: false), so backend 1 of every session runs on the next
-    rank: its deltas cross the TCP mesh, its final text moves HBM → HBM by an RCCL
-    ncclSend/ncclRecv round (rank 0 orders the rounds), and the owner's fused finalize kernel
-    merges it.  Every response is validated; the exchange counters say which path moved
-    the finals.  Failures are reported, never hidden, and do not touch the headline numbers."""
+    """Outside the timed region, N > 1: expert-parallel placement end to end, on three proxy
+    sets of the headline backends with the final event on (skip_final_aggregation: false), so
+    backend 1 of every session runs on the next rank and its deltas cross the TCP mesh:
+
+    * ``main`` (port + 50): the production defaults under load — a final text up to
+      ``exchange_eager_bytes`` rides the mesh behind its deltas (eager), a longer one takes a
+      bulk round — then a one-connection latency probe;
+    * ``rendezvous`` (port + 20): every final text through a bulk round (rank 0 numbers the
+      rounds; RCCL ncclSend/ncclRecv HBM → HBM on GPUs, the socket executor in rehearsals),
+      a lighter load and the probe;
+    * ``local`` (port + 80): the same config placed locally — the probe's control.
+
+    Every response is validated; the exchange counters say which path moved the finals.
+    Failures are reported, never hidden (the run is then invalid), and do not touch the
+    headline numbers."""
     from quorum_amd.parallel.exchange import exchange_env
-    from quorum_amd.serve import spawn_workers, wait_healthy
 
-    port = args.port + 50
-    admin = args.port + SPREAD_ADMIN_OFF + rank  # this rank's spread proxy alone
-    out = {"ok": False}
-    procs, env = [], {}
-    ok, err = True, None
-
-    def agree(stage: str) -> bool:
-        """Every rank runs the same collectives whatever failed locally (a rank that skipped
-        one would leave the others in it): min over ranks of this rank's ok flag."""
-        import torch
-
-        nonlocal ok, err
-        t = torch.tensor([1.0 if ok else 0.0], device="cuda" if n_dev >= world else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MIN)
-        if t.item() < 1.0 and ok:
-            ok, err = False, f"another rank failed at {stage}"
-        return ok
-
+    on_gpu = n_dev >= world
+    spec = os.path.join(tmp, "expect_spread.txt")
+    prep_err = None
     try:
+        expect_spec(spec, sc, False, mock_expected(bin_dir))
+    except Exception as e:  # noqa: BLE001
+        prep_err = repr(e)[:300]
+    if not torch_min_flag(dist, prep_err is None, on_gpu):
+        return {"ok": False, "error": prep_err or "another rank failed to prepare the spread check"}
+    # ranks sharing a GPU (rehearsal) or no GPU: RCCL needs one GPU per rank, so the same
+    # bulk rounds run with the socket executor (tcpbulk)
+    xchg = os.environ.get("QMX_XCHG") or ("rccl" if on_gpu and engine == "hip" else "tcpbulk")
+    if xchg == "rccl" and not (on_gpu and engine == "hip"):
+        xchg = "tcpbulk"
+
+    def xenv(off, **extra):
         nonce = [str(time.time_ns()) if rank == 0 else None]
         dist.broadcast_object_list(nonce, src=0)
-        env = dict(os.environ, **exchange_env(rank, world, port, nonce[0]))
-        if n_dev < world or engine != "hip":
-            # ranks sharing a GPU (rehearsal) or no GPU: RCCL needs one GPU per rank, so the
-            # same bulk rounds run with the socket executor (tcpbulk)
-            env.setdefault("QMX_XCHG", "tcpbulk")
-            if env["QMX_XCHG"] == "rccl":
-                env["QMX_XCHG"] = "tcpbulk"
-        xchg = env.get("QMX_XCHG", "rccl")
-        want_bulk = xchg in ("rccl", "tcpbulk")
-        out["transport"] = xchg
         # a bulk round that cannot complete (a communicator that formed but does not move
         # bytes) gives up after 3 s, not the production 30 s: its texts fall back to the mesh
         # and the check still validates every response inside the load generator's window
-        env.setdefault("QMX_XCHG_TIMEOUT", "3")
-        # every final text takes a bulk round here (rendezvous), however short: the check
-        # exercises the round protocol under load; the eager default is probed separately
-        env.setdefault("QMX_XCHG_EAGER_BYTES", "0")
-        try:
-            cfg = os.path.join(tmp, "config_spread.yaml")
-            write_config(cfg, mock_ports, False, args.tile, sc, "spread")
-            spec = os.path.join(tmp, "expect_spread.txt")
-            expect_spec(spec, sc, False, mock_expected(bin_dir))
-            if os.environ.get("QMX_BENCH_SPREAD_FAIL_RANK") == str(rank):  # test hook: one rank fails
-                raise RuntimeError("injected spread-check failure")
-            env["QMX_READY_FILE"] = os.path.join(tmp, "ready_spread")
-            env["QMX_ADMIN_PORT"] = str(admin)
-            procs = spawn_workers(cfg, "127.0.0.1", port, 1, engine, device, impl="native",
-                                  threads=args.threads, env=env)
-            for p in procs:
-                p.ready_file = f"{env['QMX_READY_FILE']}.{p.pid}"
-            if not (wait_ready(procs, 60) and wait_healthy("127.0.0.1", admin, 30)):
-                raise RuntimeError(f"spread proxy did not become ready: {[exit_status(p) for p in procs]}")
-        except Exception as e:  # noqa: BLE001 - agreed on below, reported in the JSON line
-            ok, err = False, repr(e)[:300]
-        if agree("spawn"):
-            try:
-                t0 = time.time()
-                while True:  # the mesh formed on every rank (and, on GPUs, the RCCL communicator)
-                    m = scrape(admin)
-                    healthy = m.get("qmx_exchange_healthy") == 1.0
-                    bulk = m.get("qmx_exchange_rccl_active") == 1.0
-                    if healthy and (not want_bulk or bulk):
-                        break
-                    if not healthy and time.time() - t0 > 60:
-                        raise RuntimeError(f"exchange did not form: {({k: v for k, v in m.items() if 'exchange' in k})}")
-                    if healthy and time.time() - t0 > 60:
-                        # no communicator: the finals fall back to the mesh (still validated);
-                        # reported, so a node where RCCL never formed is visible in the line
-                        break
-                    time.sleep(0.2)
-                out["bulk_formed"] = bool(want_bulk and bulk)
-            except Exception as e:  # noqa: BLE001
-                ok, err = False, repr(e)[:300]
-        if agree("exchange formation"):
-            st = None
-            try:
-                m0 = scrape(admin)
-                st = loadgen(bin_dir, port, 32, 2048, 2, 120, spec)
-            except Exception as e:  # noqa: BLE001
-                ok, err = False, repr(e)[:300]
-            # every rank's load is done before any rank reads its counters: a worker rank
-            # still serves other owners' remote streams after its own load ends
-            agree("load")
-            if st is not None:
-                try:
-                    time.sleep(0.2)
-                    m1 = scrape(admin)
-                    d = {k: m1.get(k, 0.0) - m0.get(k, 0.0) for k in m1
-                         if "exchange" in k or "remote" in k or "spread" in k or "failures" in k}
-                    out.update({"ok": st["invalid"] == 0 and st["errors"] == 0 and st["completed"] == 2048,
-                                "requests": st["completed"], "invalid": st["invalid"],
-                                "p50_ttft_ms": st["ttft_p50_ms"], "p50_latency_ms": st["lat_p50_ms"],
-                                "req_s": st["rps"], "pid": procs[0].pid if procs else None,
-                                "remote_streams": d.get("qmx_remote_streams_total", 0.0),
-                                "bulk_rounds": d.get("qmx_exchange_rounds_total", 0.0),
-                                "bulk_final_bytes": d.get("qmx_exchange_bulk_bytes_total", 0.0),
-                                "mesh_finals": d.get("qmx_exchange_mesh_finals_total", 0.0),
-                                "mesh_messages": d.get("qmx_exchange_messages_total", 0.0),
-                                "delta_mismatch": d.get("qmx_spread_delta_mismatch_total", 0.0),
-                                "worker_nodata": d.get("qmx_spread_worker_nodata_total", 0.0),
-                                "peer_downs": d.get("qmx_exchange_peer_downs_total", 0.0),
-                                # how this rank's remote streams ended (owner side), and its
-                                # upstream failures by class (worker side included)
-                                "remote_ends": {k.split('"')[1]: v for k, v in d.items()
-                                                if k.startswith("qmx_spread_remote_ends_total") and v},
-                                "up_failures": {k.split('"')[1]: v for k, v in d.items()
-                                                if k.startswith("qmx_upstream_failures_by_class_total") and v},
-                                "epochs": m1.get("qmx_exchange_epochs_total", 0.0),
-                                # owner side, means: X_OPEN -> first delta back; last delta -> final applied
-                                "hops_us": hop_means(d)})
-                except Exception as e:  # noqa: BLE001
-                    ok, err = False, repr(e)[:300]
-            # the latency of one session at a time (1 connection per rank): the closed-loop
-            # check above runs the box at its CPU limit, where latency is queueing
-            if agree("probe"):
-                try:
-                    m0 = scrape(admin)
-                    pr = loadgen(bin_dir, port, 1, PROBE_REQUESTS, 1, 120, spec)
-                    m1 = scrape(admin)
-                    d = {k: m1.get(k, 0.0) - m0.get(k, 0.0) for k in m1}
-                    out["probe_rendezvous"] = {"ok": pr["invalid"] == 0 and pr["errors"] == 0 and pr["completed"] == PROBE_REQUESTS,
-                                    "p50_latency_ms": pr["lat_p50_ms"], "p50_ttft_ms": pr["ttft_p50_ms"],
-                                    "hops_us": hop_means(d)}
-                except Exception as e:  # noqa: BLE001
-                    ok, err = False, repr(e)[:300]
-                agree("probe done")  # a rank's proxy serves its peers' remote streams to the end
-    except Exception as e:  # noqa: BLE001 - reported in the JSON line
-        ok, err = False, repr(e)[:300]
-    finally:
-        _kill(procs)
-    # one session at a time per rank on two more proxy sets of the same config: spread with
-    # the production default (short final texts eager over the mesh) and local placement (the
-    # control).  Their failures are reported, not fatal; every rank joins the same collectives.
-    if agree("probes"):
-        nonce = [str(time.time_ns()) if rank == 0 else None]
-        dist.broadcast_object_list(nonce, src=0)
-        xenv = exchange_env(rank, world, args.port + 20, nonce[0])
-        xenv.update({k: env[k] for k in ("QMX_XCHG", "QMX_XCHG_TIMEOUT") if k in env})
-        out["probe"] = probe_set(args, "spread_eager", "spread", args.port + 20, args.port + EAGER_ADMIN_OFF + rank,
-                                 xenv, sc, engine, device, bin_dir, tmp, mock_ports, dist, n_dev >= world)
-        out["local_probe"] = probe_set(args, "spread_local", "local", args.port + 80, args.port + LOCAL_ADMIN_OFF + rank,
-                                       {}, sc, engine, device, bin_dir, tmp, mock_ports, dist, n_dev >= world)
-    if err:
-        out["ok"] = False
-        out["error"] = err
-    return out
+        e = dict(exchange_env(rank, world, args.port + off, nonce[0]), QMX_XCHG=xchg,
+                 QMX_XCHG_TIMEOUT=os.environ.get("QMX_XCHG_TIMEOUT", "3"))
+        e.update(extra)
+        return e
+
+    ctx = {"args": args, "rank": rank, "dist": dist, "on_gpu": on_gpu, "tmp": tmp, "mock_ports": mock_ports, "sc": sc,
+           "engine": engine, "device": device, "bin_dir": bin_dir, "spec": spec}
+    main = run_set(ctx, "spread", "spread", args.port + 50, args.port + SPREAD_ADMIN_OFF + rank, xenv(50),
+                   [("load", 32, 2048), ("probe", 1, PROBE_REQUESTS)])
+    rdv = run_set(ctx, "spread_rendezvous", "spread", args.port + 20, args.port + RDV_ADMIN_OFF + rank,
+                  xenv(20, QMX_XCHG_EAGER_BYTES="0"), [("load", 8, 512), ("probe", 1, PROBE_REQUESTS)], want_bulk=True)
+    local = run_set(ctx, "spread_local", "local", args.port + 80, args.port + LOCAL_ADMIN_OFF + rank, {},
+                    [("probe", 1, PROBE_REQUESTS)])
+    return {"ok": main["ok"] and rdv["ok"] and local["ok"], "transport": xchg, "main": main, "rendezvous": rdv,
+            "local": local}
 
 
-def probe_set(args, label, placement, port, admin, xenv, sc, engine, device, bin_dir, tmp, mock_ports, dist,
-              on_gpu) -> dict:
-    """Spawn one proxy per rank on ``port`` (``placement``; ``xenv``: its exchange settings),
-    wait until every rank's is up (spread: its mesh formed), run PROBE_REQUESTS validated
-    requests over one connection, and stop the set once every rank's probe is done (a spread
-    rank serves its peers' remote streams to the end).  The result, or the failure, as a dict."""
+def spread_counters(d) -> dict:
+    """A spread proxy's /metrics delta over one pass: how its remote streams moved and ended."""
+    return {"remote_streams": d.get("qmx_remote_streams_total", 0.0),
+            "eager_finals": d.get("qmx_spread_eager_finals_total", 0.0),
+            "bulk_rounds": d.get("qmx_exchange_rounds_total", 0.0),
+            "bulk_final_bytes": d.get("qmx_exchange_bulk_bytes_total", 0.0),
+            "mesh_finals": d.get("qmx_exchange_mesh_finals_total", 0.0),
+            "mesh_messages": d.get("qmx_exchange_messages_total", 0.0),
+            "delta_mismatch": d.get("qmx_spread_delta_mismatch_total", 0.0),
+            "worker_nodata": d.get("qmx_spread_worker_nodata_total", 0.0),
+            "peer_downs": d.get("qmx_exchange_peer_downs_total", 0.0),
+            # how this rank's remote streams ended (owner side), and its upstream failures by
+            # class (worker side included)
+            "remote_ends": {k.split('"')[1]: v for k, v in d.items() if k.startswith("qmx_spread_remote_ends_total") and v},
+            "up_failures": {k.split('"')[1]: v for k, v in d.items()
+                            if k.startswith("qmx_upstream_failures_by_class_total") and v},
+            # owner side, means: X_OPEN -> first delta back; last delta -> final applied
+            "hops_us": hop_means(d)}
+
+
+def run_set(ctx, label, placement, port, admin, xenv, passes, want_bulk=False) -> dict:
+    """One proxy per rank on ``port`` (``placement``; ``xenv``: its exchange settings): wait
+    until every rank's is up (spread: its mesh formed; ``want_bulk``: its bulk executor too, at
+    most 60 s), run each pass ``(name, connections, requests)`` of validated requests, and stop
+    the set.  Every rank joins the same collectives whatever fails locally: a rank's counters
+    are read only after every rank's pass is done (a spread rank serves its peers' remote
+    streams to the end).  The result, or the failure, as a dict."""
     from quorum_amd.serve import spawn_workers, wait_healthy
 
-    procs, err, res = [], None, {"ok": False}
+    args, rank, dist, on_gpu = ctx["args"], ctx["rank"], ctx["dist"], ctx["on_gpu"]
+    res, procs, err = {}, [], None
     try:
-        cfg = os.path.join(tmp, f"config_{label}.yaml")
-        write_config(cfg, mock_ports, False, args.tile, sc, placement)
-        env = dict(os.environ, **xenv, QMX_READY_FILE=os.path.join(tmp, f"ready_{label}"), QMX_ADMIN_PORT=str(admin))
-        procs = spawn_workers(cfg, "127.0.0.1", port, 1, engine, device, impl="native", threads=args.threads, env=env)
+        if label == "spread" and os.environ.get("QMX_BENCH_SPREAD_FAIL_RANK") == str(rank):  # test hook
+            raise RuntimeError("injected spread-check failure")
+        cfg = os.path.join(ctx["tmp"], f"config_{label}.yaml")
+        write_config(cfg, ctx["mock_ports"], False, args.tile, ctx["sc"], placement)
+        env = dict(os.environ, **xenv, QMX_READY_FILE=os.path.join(ctx["tmp"], f"ready_{label}"),
+                   QMX_ADMIN_PORT=str(admin))
+        procs = spawn_workers(cfg, "127.0.0.1", port, 1, ctx["engine"], ctx["device"], impl="native",
+                              threads=args.threads, env=env)
         for p in procs:
             p.ready_file = f"{env['QMX_READY_FILE']}.{p.pid}"
+        res["pid"] = procs[0].pid if procs else None
         if not (wait_ready(procs, 60) and wait_healthy("127.0.0.1", admin, 30)):
             raise RuntimeError(f"{label} proxy did not become ready: {[exit_status(p) for p in procs]}")
-        if placement == "spread":
-            t0 = time.time()
-            while scrape(admin).get("qmx_exchange_healthy") != 1.0:
-                if time.time() - t0 > 60:
-                    raise RuntimeError(f"{label}: the mesh did not form")
-                time.sleep(0.2)
     except Exception as e:  # noqa: BLE001
         err = repr(e)[:300]
-    try:
-        if torch_min_flag(dist, err is None, on_gpu):
-            m0 = scrape(admin)
-            pr = loadgen(bin_dir, port, 1, PROBE_REQUESTS, 1, 120, os.path.join(tmp, "expect_spread.txt"))
+    up = torch_min_flag(dist, err is None, on_gpu)
+    if up and placement == "spread":
+        try:
+            t0, bulk = time.time(), False
+            while True:  # the mesh formed on every rank (and the bulk executor: RCCL communicator)
+                m = scrape(admin)
+                healthy = m.get("qmx_exchange_healthy") == 1.0
+                bulk = m.get("qmx_exchange_rccl_active") == 1.0
+                if healthy and (not want_bulk or bulk):
+                    break
+                if time.time() - t0 > 60:
+                    if not healthy:
+                        raise RuntimeError(f"{label}: exchange did not form: "
+                                           f"{({k: v for k, v in m.items() if 'exchange' in k})}")
+                    # no communicator: the finals fall back to the mesh (still validated);
+                    # reported, so a node where RCCL never formed is visible in the line
+                    break
+                time.sleep(0.2)
+            res["bulk_formed"] = bulk
+        except Exception as e:  # noqa: BLE001
+            err = repr(e)[:300]
+        up = torch_min_flag(dist, err is None, on_gpu)
+    for name, conns, n in passes:
+        if not up:
+            break
+        st, m0 = None, scrape(admin)
+        try:
+            st = loadgen(ctx["bin_dir"], port, conns, n, min(2, conns), 120, ctx["spec"])
+        except Exception as e:  # noqa: BLE001
+            err = repr(e)[:300]
+        up = torch_min_flag(dist, err is None, on_gpu)  # every rank's pass is done
+        if st is not None:
             time.sleep(0.1)
             d = {k: v - m0.get(k, 0.0) for k, v in scrape(admin).items()}
-            res = {"ok": pr["invalid"] == 0 and pr["errors"] == 0 and pr["completed"] == PROBE_REQUESTS,
-                   "p50_latency_ms": pr["lat_p50_ms"], "p50_ttft_ms": pr["ttft_p50_ms"]}
+            res[name] = {"ok": st["invalid"] == 0 and st["errors"] == 0 and st["completed"] == n,
+                         "requests": st["completed"], "invalid": st["invalid"], "errors": st["errors"],
+                         "p50_latency_ms": st["lat_p50_ms"], "p50_ttft_ms": st["ttft_p50_ms"], "req_s": st["rps"]}
             if placement == "spread":
-                res.update({"hops_us": hop_means(d), "eager_finals": d.get("qmx_spread_eager_finals_total", 0.0),
-                            "bulk_rounds": d.get("qmx_exchange_rounds_total", 0.0)})
-        else:
-            res = {"ok": False, "error": err or f"another rank's {label} set failed"}
-    except Exception as e:  # noqa: BLE001
-        res = {"ok": False, "error": repr(e)[:300]}
-    torch_min_flag(dist, True, on_gpu)  # every rank's probe is done
+                res[name].update(spread_counters(d))
     _kill(procs)
+    if err is None and not up:
+        err = f"another rank's {label} set failed"
+    res["ok"] = err is None and all((res.get(p[0]) or {}).get("ok") for p in passes)
+    if err:
+        res["error"] = err
     return res
 
 

@@ -147,7 +147,7 @@ for l in open('$OUT/kbench.jsonl'):
       python3 -c "
 import json
 d=json.loads([l for l in open('$OUT/selfrank_$n.json') if l.startswith('{')][-1]); s=d.get('spread_check',{})
-print('per-rank pids', [r['pid'] for r in d.get('breakdown_per_rank',[])], 'spread', {k: s.get(k) for k in ('ok','requests','invalid','remote_streams','mesh_finals','delta_mismatch','worker_nodata','peer_downs','remote_ends','p50_latency_ms')})
+print('per-rank pids', [r['pid'] for r in d.get('breakdown_per_rank',[])], 'spread', {k: s.get(k) for k in ('ok','requests','invalid','remote_streams','bulk_rounds','mesh_finals','delta_mismatch','worker_nodata','peer_downs','remote_ends','p50_latency_ms','eager_finals','probe_p50_latency_ms','local_probe_p50_latency_ms','hops_us_loaded','hops_us_probe','bulk_formed','rendezvous','errors')})
 for r in s.get('per_rank',[]): print('  ', r)
 " || true
       grep "qmx spread\|qmx exchange" $OUT/selfrank_$n.err | head -20
