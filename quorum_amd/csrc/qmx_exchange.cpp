@@ -61,6 +61,7 @@ enum : uint8_t {
   F_EPOCH = 103,     // rank 0 → all: a = epoch (0: RCCL down everywhere), payload = unique id hex
   F_BULK_MESH = 104, // worker → owner: the final text's bytes over the mesh
   F_RCCL_DOWN = 105, // any rank → rank 0: my communicator failed (a = epoch)
+  F_ROUND_DONE = 106,  // involved rank → rank 0: round a is over on this rank (either way)
 };
 
 void put_frame(std::string& out, const XMsg& m, const char* payload, size_t n) {
@@ -156,6 +157,16 @@ struct Exchange::Impl {
   double ann_deadline = 0;
   double last_round_t = -1e9;  // coordinator: when the last round was issued
   int round_no = 0, epoch_no = 0;
+  // coordinator: rounds issued and not yet reported over by every rank in them.  At most
+  // kMaxInflight run at once; meanwhile announcements collect into the next round, which so
+  // grows with the load — a queue of small rounds would instead grow the latency of each
+  struct Inflight {
+    int round;
+    uint64_t pending;  // ranks of the round that have not reported it over
+    double t;
+  };
+  static constexpr int kMaxInflight = 2;
+  std::deque<Inflight> inflight;
   bool epoch_live = false;  // an epoch is formed (or forming) and not reported down
   bool ever_all_up = false;
   double next_epoch_at = 0;  // retry backoff after an epoch / communicator failure
@@ -405,6 +416,11 @@ struct Exchange::Impl {
       case F_RCCL_DOWN:
         if (X->o_.rank == 0 && m.a == epoch_no) rccl_down_everywhere();
         return;
+      case F_ROUND_DONE:
+        if (X->o_.rank == 0 && r >= 0 && r < 64)
+          for (Inflight& f : inflight)
+            if (f.round == m.a) f.pending &= ~(1ull << r);
+        return;
       default:
         (void)r;
         return;
@@ -413,6 +429,7 @@ struct Exchange::Impl {
   // coordinator: RCCL is unusable (a round failed, a peer left): every rank drops its
   // communicator; a new epoch forms once every rank is up again
   void rccl_down_everywhere() {
+    inflight.clear();  // (their ranks drop the communicator: nothing more to wait for)
     if (!epoch_live) return;
     epoch_live = false;
     // back off before the next epoch: 0.5 s, 1 s, 2 s, ... 60 s (a communicator that cannot
@@ -448,6 +465,15 @@ struct Exchange::Impl {
       enqueue(r, frame(e));
     }
   }
+  // coordinator: may a new round go out?  Rounds every rank reported over, and rounds older
+  // than the round timeout (their ranks fail them and fall back), no longer count
+  bool round_credit() {
+    const double t = now_s();
+    inflight.erase(std::remove_if(inflight.begin(), inflight.end(),
+                                  [&](const Inflight& f) { return f.pending == 0 || t - f.t > X->o_.timeout_s + 1.0; }),
+                   inflight.end());
+    return (int)inflight.size() < kMaxInflight;
+  }
   // coordinator: turn the batched announcements into a round; each involved rank gets its
   // own entries in round order (per-pair order identical on both ends)
   void form_round() {
@@ -465,6 +491,11 @@ struct Exchange::Impl {
     }
     ann.clear();
     last_round_t = now_s();
+    if (!fallback) {
+      uint64_t mask = 0;
+      for (auto& kv : part) mask |= 1ull << kv.first;
+      inflight.push_back(Inflight{round_no, mask, last_round_t});
+    }
     for (auto& kv : part) {
       XMsg m;
       m.type = F_MANIFEST;
@@ -645,9 +676,14 @@ void Exchange::mesh_loop() {
       Impl::Peer& p = I.peers[r];
       if (p.fd < 0 && t >= p.next_dial) I.dial(r);
     }
-    int to = 20;
-    if (o_.rank == 0 && !I.ann.empty()) to = std::max(0, (int)((I.ann_deadline - t) * 1000));
-    int n = epoll_wait(I.ep, evs.data(), (int)evs.size(), to);
+    // rank 0 with announcements waiting for the batch window to end: a sub-millisecond wait
+    // (a round blocked on credits waits for a report, which wakes the loop)
+    double wait_s = 0.02;
+    if (o_.rank == 0 && !I.ann.empty() && (int)I.inflight.size() < Impl::kMaxInflight)
+      wait_s = std::max(0.0, std::min(wait_s, I.ann_deadline - t));
+    timespec ts{(time_t)wait_s, (long)((wait_s - (double)(time_t)wait_s) * 1e9)};
+    int n = epoll_pwait2(I.ep, evs.data(), (int)evs.size(), &ts, nullptr);
+    if (n < 0 && errno == ENOSYS) n = epoll_wait(I.ep, evs.data(), (int)evs.size(), (int)(wait_s * 1000) + 1);
     for (int i = 0; i < n; ++i) {
       const uint64_t tag = evs[i].data.u64;
       if (tag == (1ull << 40)) {
@@ -751,7 +787,7 @@ void Exchange::mesh_loop() {
     }
     if (o_.rank == 0) {
       I.maybe_new_epoch();
-      if (!I.ann.empty() && now_s() >= I.ann_deadline) {
+      if (!I.ann.empty() && now_s() >= I.ann_deadline && I.round_credit()) {
         I.form_round();
         I.take_posted();
       }
@@ -1247,6 +1283,14 @@ void Exchange::bulk_loop() {
       }
     }
     busy_us_.store(busy_us_.load() + 1e6 * (now_s() - t0));
+    {  // this rank is done with the round: rank 0 may issue another
+      XMsg d;
+      d.type = F_ROUND_DONE;
+      d.a = mf.round;
+      d.dst_rank = 0;
+      d.src_rank = o_.rank;
+      I.enqueue(0, frame(d));
+    }
     if (!ok) {
       fprintf(stderr, "qmx exchange (rank %d): %s round %d failed — communicator dropped, bulk uses the mesh\n",
               o_.rank, o_.transport.c_str(), mf.round);
