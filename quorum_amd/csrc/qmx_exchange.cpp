@@ -835,6 +835,7 @@ class RcclExec : public BulkExec {
   ~RcclExec() override {
     drop();
     if (scratch_) hipFree(scratch_);
+    if (zeros_) hipFree(zeros_);
     if (st_) hipStreamDestroy(st_);
   }
   bool device() const override { return true; }
@@ -856,9 +857,11 @@ class RcclExec : public BulkExec {
     if (st_) hipStreamSynchronize(st_);  // the aborted communicator's kernels have been flushed
   }
   bool start(int, std::vector<BulkOp>& ops) override {
-    size_t need = 256;
-    for (auto& o : ops)
+    size_t need = 256, zero = 0;
+    for (auto& o : ops) {
       if (!o.send) need += (o.e->len + 255) & ~(size_t)255;
+      else if (!o.src) zero = std::max(zero, (size_t)o.e->len);
+    }
     if (need > cap_) {
       if (scratch_) hipFree(scratch_);
       cap_ = std::max(need, cap_ * 2);
@@ -868,14 +871,25 @@ class RcclExec : public BulkExec {
         return false;
       }
     }
+    // a vanished send (its text already left over the mesh) still posts its len bytes, or
+    // the pair desyncs: zeros from a buffer of its own, as long as the longest such send
+    if (zero > zcap_) {
+      if (zeros_) hipFree(zeros_);
+      zcap_ = std::max(zero, 2 * zcap_);
+      if (hipMalloc(&zeros_, zcap_) != hipSuccess || hipMemsetAsync(zeros_, 0, zcap_, st_) != hipSuccess) {
+        if (zeros_) hipFree(zeros_);
+        zeros_ = nullptr;
+        zcap_ = 0;
+        return false;
+      }
+    }
     if (ncclGroupStart() != ncclSuccess) return false;
     bool ok = true;
     size_t off = 0;
     for (auto& o : ops) {
       ncclResult_t r;
       if (o.send) {
-        // a vanished send (its session ended) still posts len bytes, or the pair desyncs
-        const void* src = o.src ? o.src : scratch_ + cap_ - 256;
+        const void* src = o.src ? o.src : (const void*)zeros_;
         r = ncclSend(src, o.e->len, ncclUint8, o.e->dst, comm_, st_);
       } else {
         o.off = off;
@@ -914,6 +928,8 @@ class RcclExec : public BulkExec {
   hipStream_t st_ = nullptr;
   uint8_t* scratch_ = nullptr;
   size_t cap_ = 0;
+  uint8_t* zeros_ = nullptr;  // vanished sends' bytes
+  size_t zcap_ = 0;
 };
 
 #pragma pack(push, 1)
