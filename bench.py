@@ -941,6 +941,9 @@ def main() -> int:
                                              if args.placement == "spread" and world > 1 else ""),
                            "impl": args.impl, "engine": engine if args.impl != "reference" else "reference",
                            "conns_per_rank": args.conns,
+                           # hip: io loops post their own ticks into one multi-door grid ("loops",
+                           # the default) or hand streams to tick-lane threads ("lanes")
+                           "tick_mode": os.environ.get("QMX_TICK_MODE", "auto") if engine == "hip" else None,
                            "io_threads_per_rank": args.threads, "cpu_pinning": pinning,
                            "gpu_links": ({k: v for k, v in link_summary().items() if k != "links_per_gpu"}
                                          if world > 1 else None)},

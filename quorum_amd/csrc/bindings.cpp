@@ -135,7 +135,7 @@ ServerCfg server_cfg_from(const py::dict& d) {
   gs("xchg_addr", c.xchg_addr); gi("xchg_port", c.xchg_port); gi("xchg_bulk_port", c.xchg_bulk_port); gs("xchg_id_file", c.xchg_id_file);
   gi("xchg_round_us", c.xchg_round_us); gi("xchg_eager_bytes", c.xchg_eager_bytes); gd("xchg_timeout", c.xchg_timeout);
   gd("drain_s", c.drain_s); gs("ready_file", c.ready_file); gb("verify", c.verify); gi("admin_port", c.admin_port);
-  gi("shared_engine", c.shared_engine); gi("tick_lanes", c.tick_lanes);
+  gi("shared_engine", c.shared_engine); gi("tick_lanes", c.tick_lanes); gs("tick_mode", c.tick_mode);
   gs("ca_file", c.ca_file); gb("tls_verify", c.tls_verify);
   if (d.contains("backends")) {
     for (auto item : py::cast<py::list>(d["backends"])) {
@@ -354,14 +354,25 @@ PYBIND11_MODULE(_qmx, m) {
     return new CpuEngine(tags);
   }));
   bind_engine(ce);
+  // the multi-door grid of loop ticks (tests drive several door engines from Python threads)
+  py::class_<HipGrid>(m, "HipGrid")
+      .def(py::init([](int device, int doors, int wg_per_door, int idle_ms) {
+             env_refresh();
+             return new HipGrid(device, doors, wg_per_door, idle_ms);
+           }),
+           py::arg("device"), py::arg("doors"), py::arg("wg_per_door") = 8, py::arg("idle_ms") = 50)
+      .def("housekeep", &HipGrid::housekeep)
+      .def("stop", &HipGrid::stop, py::call_guard<py::gil_scoped_release>())
+      .def("stats", &HipGrid::stats);
   py::class_<HipEngine> he(m, "HipEngine");
   he.def(py::init([](const std::vector<std::string>& tags, int device, int tile, int max_slots, int content_cap,
-                      int lanes) {
+                      int lanes, HipGrid* grid, int door) {
            env_refresh();
-           return new HipEngine(tags, device, tile, max_slots, content_cap, lanes);
+           return new HipEngine(tags, device, tile, max_slots, content_cap, lanes, grid, door);
          }),
          py::arg("tags"), py::arg("device"), py::arg("tile_bytes") = 16384, py::arg("max_slots") = 8192,
-         py::arg("content_cap") = 1 << 20, py::arg("lanes") = 1);
+         py::arg("content_cap") = 1 << 20, py::arg("lanes") = 1, py::arg("grid") = nullptr, py::arg("door") = -1,
+         py::keep_alive<1, 8>());
   bind_engine(he);
   he.def("kernel_stats", &HipEngine::kernel_stats);
 }

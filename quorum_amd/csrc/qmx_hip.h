@@ -16,6 +16,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <vector>
 
 #include "qmx_engine.h"
@@ -126,6 +127,49 @@ struct FinResult {
 struct PDoor;  // persistent mode: host-mapped doorbell (qmx_hip.hip)
 struct PCtl;   // persistent mode: device control block
 
+// One persistent grid serving several doorbells ("loop ticks"): every io loop owns an engine
+// (its own slots, arenas and templates) and posts its own ticks into door `d` of this grid —
+// no tick-lane thread between an io loop and the GPU, no hand-off of results back.  The
+// grid is `doors` sub-grids of `wg_per_door` workgroups; each sub-grid's first workgroup
+// polls its door and relays the tick to its workers, exactly as a lane's grid does.
+//
+// Lifetime: a door's owner posts under post_guard() (a shared lock that launches the grid
+// when it is not running).  housekeep(), from any io loop's periodic sweep, keeps the grid
+// alive with a heartbeat every door sees, and stops it (stop ticks on every door, under the
+// exclusive lock) once no door has posted for idle_ms.  The kernel's own exit — every relay
+// idle, heartbeat included, for 2 s — only fires when the host stopped beating (a hung
+// process), so every wave reaches an exit even if the host never stops the grid.
+class HipGrid {
+ public:
+  HipGrid(int device, int doors, int wg_per_door, int idle_ms);
+  ~HipGrid();
+  int doors() const { return n_; }
+  PDoor* door(int d) const;
+  // held by a door's owner while it writes and posts a tick
+  std::shared_lock<std::shared_mutex> post_guard();
+  void note_post();
+  void housekeep();
+  // a tick that never completed: relaunch a grid that left on its own (its exit word names
+  // the current generation); true when it did
+  bool revive_if_exited();
+  void stop();
+  std::unordered_map<std::string, double> stats();
+
+ private:
+  void launch_locked();
+  void stop_locked();
+  int device_, n_, wpd_, idle_ms_;
+  std::shared_mutex mu_;
+  std::atomic<bool> running_{false};
+  uint32_t gen_ = 0;
+  std::atomic<double> last_post_{0.0};
+  std::atomic<uint32_t> beat_{0};
+  hipStream_t stream_ = nullptr;
+  PDoor* h_doors_ = nullptr;  // host-mapped, n_ of them
+  PCtl* d_ctls_ = nullptr;    // device, n_ of them
+  std::atomic<uint64_t> launches_{0}, stops_{0}, revivals_{0};
+};
+
 // Launch resources of one tick lane: a tick thread owns a lane (HIP stream, events,
 // host-mapped in/out arenas, work/result descriptors, counters), so several lanes can have
 // tick kernels in flight at once over disjoint slot sets (HostEngine busy flags).
@@ -214,9 +258,13 @@ struct TickLane {
 
 class HipEngine : public HostEngine {
  public:
+  // grid: loop-tick mode — one lane whose ticks go to door `door` of a shared multi-door grid
   HipEngine(const std::vector<std::string>& tags, int device, int tile_bytes, int max_slots, int content_cap,
-            int lanes = 1);
+            int lanes = 1, HipGrid* grid = nullptr, int door = -1);
   ~HipEngine() override;
+  // loop-tick mode (the io loop drives its own ticks): has the posted job's every result been
+  // published?  Never blocks.  expect_us: the job's expected remaining time (poll timing).
+  bool job_ready(Job& j, double* expect_us = nullptr);
   std::string text(int slot) override;
   void* content_device_ptr(int slot, size_t* cap) override;
   size_t content_size(int slot) override;
@@ -291,6 +339,8 @@ class HipEngine : public HostEngine {
   bool stage_timing_ = false;  // QMX_STAGE_TIMING: per-item stage stamps (tools/kbench.py)
   int p_grid_ = 64;          // QMX_PERSISTENT_WG: workgroups per lane grid (1 per CU: 256 VGPRs)
   int p_idle_ms_ = 50;       // the grid exits after this long without a tick
+  HipGrid* grid_ = nullptr;  // loop-tick mode: the shared grid and this engine's door
+  int door_ = -1;
 
  public:
   bool persistent() const { return persistent_; }

@@ -2214,51 +2214,71 @@ struct TickDesc {
   const BackendTpl* btpl_rd;
   BackendTpl* btpl_wr;
   FinArgs fa;
+  DevSlot* state;  // the posting engine's slot state and content arena
+  uint8_t* content;
   uint32_t seq, n_tick, n_fin, stop;
 };
-struct PDoor {  // host-mapped: written by the host, polled by workgroup 0
+struct PDoor {  // host-mapped: written by the host, polled by the door's relay workgroup
   TickDesc d;
   alignas(64) uint32_t posted;
-  // written by workgroup 0 (diagnostics: the host reports them when a tick goes missing)
+  uint32_t beat;  // host keep-alive (multi-door grid): a change resets the relay's idle clock
+  uint32_t base;  // the last tick relayed before this launch (the launch's starting point)
+  // written by the relay (diagnostics: the host reports them when a tick goes missing)
   alignas(64) uint32_t relayed;  // last tick relayed
   uint32_t exits;                // last grid exit: reason << 16 | launch generation (1 idle, 2 stop)
   uint32_t idle_limit_hit_us;    // the idle time that triggered the last idle exit, us
   uint64_t t_seen, t_relayed;    // s_memrealtime: the last tick's doorbell seen / relayed (timing)
 };
-struct PCtl {  // device memory: written by workgroup 0, polled by the others
+struct PCtl {  // device memory: written by the relay, polled by the door's other workgroups
   TickDesc d;
   alignas(64) uint32_t seq;
   uint32_t exit_gen;
+  uint32_t beat;                 // the door's heartbeat, mirrored by the relay (workers' idle clock)
   alignas(64) uint32_t next[4];  // item counters, tick seq & 3 (reset by the relay before publishing)
 };
+static_assert(offsetof(PDoor, beat) == offsetof(PDoor, posted) + 4, "posted + beat: one 8-byte load");
 
 // `door` / `ctl` are neither const nor __restrict__ and their words are read with atomic
 // loads: a readonly noalias kernel argument may be read through the scalar cache, which no
 // acquire fence invalidates — the next tick's descriptor would come back stale.
-__global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* door, PCtl* ctl,
-                                                          DevSlot* __restrict__ state, uint8_t* __restrict__ content,
-                                                          uint32_t seq0, uint32_t gen, uint32_t idle_ticks) {
+__global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* doors, PCtl* ctls, int wpd, uint32_t gen,
+                                                          uint32_t idle_ticks) {
   __shared__ TickLds U;
   __shared__ TickDesc D;
   __shared__ uint32_t cmd;  // new tick's sequence number, 0: exit
-  uint32_t last = seq0;     // the value the host posted last before this launch
-  const bool relay = blockIdx.x == 0;
+  // sub-grid blockIdx.x / wpd serves door blockIdx.x / wpd; its first workgroup is the relay
+  PDoor* const door = doors + blockIdx.x / wpd;
+  PCtl* const ctl = ctls + blockIdx.x / wpd;
+  const bool relay = blockIdx.x % wpd == 0;
   constexpr int kWords = (int)(sizeof(TickDesc) / 4);
   static_assert(kWords <= 64, "the descriptor is copied by one wave, a word per lane");
   const int tid = threadIdx.x;
+  // the last tick relayed before this launch (written by the host before it launched)
+  if (tid == 0) cmd = __hip_atomic_load(&door->base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __syncthreads();
+  uint32_t last = cmd;
+  uint32_t beat = 0;  // thread 0's view of the door's heartbeat
+  __syncthreads();
   for (;;) {
     if (tid == 0) {
-      const uint64_t t_idle = __builtin_amdgcn_s_memrealtime();
+      uint64_t t_idle = __builtin_amdgcn_s_memrealtime();
       const uint64_t limit = relay ? (uint64_t)idle_ticks : 2ull * idle_ticks;
       uint32_t c = 0;
       for (;;) {
         if (relay) {
-          const uint32_t v = __hip_atomic_load(&door->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          // posted and beat in one 8-byte load: one PCIe read in flight per poll
+          const uint64_t pb = __hip_atomic_load((uint64_t*)&door->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          const uint32_t v = (uint32_t)pb;
           if ((int32_t)(v - last) > 0) {  // newer only: a control word left by an earlier launch is older
             c = v;
             __hip_atomic_store(&door->t_seen, (uint64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
             break;
+          }
+          if ((uint32_t)(pb >> 32) != beat) {  // the host is alive: idle time starts over
+            beat = (uint32_t)(pb >> 32);
+            t_idle = __builtin_amdgcn_s_memrealtime();
+            __hip_atomic_store(&ctl->beat, beat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
         } else {
           const uint32_t v = __hip_atomic_load(&ctl->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2267,6 +2287,11 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* door, PCtl* ctl
             break;
           }
           if (__hip_atomic_load(&ctl->exit_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) break;
+          const uint32_t b = __hip_atomic_load(&ctl->beat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (b != beat) {
+            beat = b;
+            t_idle = __builtin_amdgcn_s_memrealtime();
+          }
         }
         const uint64_t idle = __builtin_amdgcn_s_memrealtime() - t_idle;
         if (idle > limit) {
@@ -2352,8 +2377,8 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* door, PCtl* ctl
       // launch-invariant data (which the compiler does for uniform addresses it proves
       // unclobbered within the kernel)
       asm volatile("" ::: "memory");
-      run_item(k, uni(D.items), uni(D.in), uni(D.out), uni(D.res), state, content, *uni(D.params), seq, n_tick, fa,
-               uni(D.btpl_rd), uni(D.btpl_wr), U);
+      run_item(k, uni(D.items), uni(D.in), uni(D.out), uni(D.res), uni(D.state), uni(D.content), *uni(D.params), seq,
+               n_tick, fa, uni(D.btpl_rd), uni(D.btpl_wr), U);
       __syncthreads();  // LDS is reused by the next item
     }
     __syncthreads();  // D / cmd are rewritten by thread 0 for the next tick
@@ -2411,9 +2436,24 @@ void HipEngine::wait_results(TickLane& L, int n, int m, uint32_t seq, const Work
   };
   int i = 0;
   bool revived = false;
+  double revive_at = 2e5;  // loop-tick mode: us after the post
   nap(0.6 * L.ema_us - 6.0 - std::chrono::duration<double, std::micro>(HC::now() - t0).count());
   while (!done(i)) {
     const double el = std::chrono::duration<double, std::micro>(HC::now() - t0).count();
+    if (grid_) {
+      // loop-tick mode: a grid that left on its own (the host's heartbeat stopped for 2 s) is
+      // relaunched from the last tick it relayed; a grid that runs but never answers is fatal
+      if (el > revive_at) {
+        revive_at = el + 1e5;
+        grid_->revive_if_exited();
+      }
+      if (el > 1e7)
+        throw std::runtime_error("tick results missing after 10 s (door " + std::to_string(door_) + ", seq " +
+                                 std::to_string(seq) + ", relayed " +
+                                 std::to_string(__atomic_load_n(&L.h_door->relayed, __ATOMIC_ACQUIRE)) + ")");
+      nap(el < 2e3 ? poll_us_ : 50.0);
+      continue;
+    }
     // the persistent grid idled out between ensure_persistent() and this tick's doorbell (the
     // lane thread was descheduled for longer than the margin): it reported an idle exit for
     // its generation and never relayed the tick.  Relaunch it from just before this tick's
@@ -2425,8 +2465,9 @@ void HipEngine::wait_results(TickLane& L, int n, int m, uint32_t seq, const Work
         uint32_t seq0 = seq - 1;
         if (seq0 == 0) seq0 = (uint32_t)-1;  // (0 never names a tick)
         HIP_CHECK(hipStreamSynchronize(L.stream));  // the idle grid has left
-        hipLaunchKernelGGL(qmx_tick_persistent, dim3(p_grid_), dim3(BS), 0, L.stream, L.h_door, L.d_ctl, d_state_,
-                           d_content_, seq0, ++L.p_gen, (uint32_t)p_idle_ms_ * 100000u);
+        L.h_door->base = seq0;
+        hipLaunchKernelGGL(qmx_tick_persistent, dim3(p_grid_), dim3(BS), 0, L.stream, L.h_door, L.d_ctl, p_grid_,
+                           ++L.p_gen, (uint32_t)p_idle_ms_ * 100000u);
         HIP_CHECK(hipGetLastError());
         L.p_last_post = steady_s();
         ++L.p_launches;
@@ -2473,13 +2514,17 @@ void HipEngine::collect_timing(TickLane& L) {
 }
 
 HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_bytes, int max_slots,
-                     int content_cap, int lanes)
+                     int content_cap, int lanes, HipGrid* grid, int door)
     : HostEngine(tags),
       device_(device),
       tile_(std::min(std::max(tile_bytes, 1024), TILE_MAX) & ~15),
       max_slots_(max_slots),
-      content_cap_((uint32_t)content_cap) {
+      content_cap_((uint32_t)content_cap),
+      grid_(grid),
+      door_(door) {
   HIP_CHECK(hipSetDevice(device_));
+  if (grid_ && (door_ < 0 || door_ >= grid_->doors())) throw std::invalid_argument("HipEngine: door out of range");
+  if (grid_) lanes = 1;
   if (const char* sp = env_get("QMX_WAIT_SPIN_US")) spin_us_ = atoi(sp);
   if (const char* w = env_get("QMX_WAIT")) poll_ = std::string(w) != "event";
   if (const char* pu = env_get("QMX_POLL_US")) poll_us_ = std::max(1, atoi(pu));
@@ -2499,6 +2544,10 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
     const char* hq = env_get("GPU_MAX_HW_QUEUES");
     const int queues = hq ? std::max(1, atoi(hq)) : 4;
     if (persistent_ && lanes > queues - 1) persistent_ = false;
+  }
+  if (grid_) {  // the shared grid is the only way this engine's ticks run
+    persistent_ = false;
+    poll_ = true;
   }
   HIP_CHECK(hipMalloc(&d_state_, sizeof(DevSlot) * (size_t)max_slots_));
   HIP_CHECK(hipMemset(d_state_, 0, sizeof(DevSlot) * (size_t)max_slots_));
@@ -2559,18 +2608,24 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
     HIP_CHECK(hipMalloc((void**)&L->d_btpl, sizeof(BackendTpl) * 2 * kBackendTpl));
     HIP_CHECK(hipMemset(L->d_btpl, 0, sizeof(BackendTpl) * 2 * kBackendTpl));
     HIP_CHECK(hipHostMalloc((void**)&L->h_params, sizeof(KParams), hipHostMallocMapped));
-    HIP_CHECK(hipHostMalloc((void**)&L->h_door, sizeof(PDoor), hipHostMallocMapped));
-    std::memset((void*)L->h_door, 0, sizeof(PDoor));
-    HIP_CHECK(hipMalloc((void**)&L->d_ctl, sizeof(PCtl)));
-    HIP_CHECK(hipMemset(L->d_ctl, 0, sizeof(PCtl)));
+    if (grid_) {
+      L->h_door = grid_->door(door_);  // the grid's (not freed here)
+    } else {
+      HIP_CHECK(hipHostMalloc((void**)&L->h_door, sizeof(PDoor), hipHostMallocMapped));
+      std::memset((void*)L->h_door, 0, sizeof(PDoor));
+      HIP_CHECK(hipMalloc((void**)&L->d_ctl, sizeof(PCtl)));
+      HIP_CHECK(hipMemset(L->d_ctl, 0, sizeof(PCtl)));
+    }
+    // an io loop's engine (loop ticks) carries a few streams per tick: arenas start small
+    const size_t arena0 = grid_ ? (1u << 20) : (4u << 20);
     for (TickLane::Buf& B : L->bufs) {
-      ensure_in(B, 4u << 20);
+      ensure_in(B, arena0);
       B.items_cap = 1024;
       HIP_CHECK(hipHostMalloc((void**)&B.h_items, sizeof(WorkItem) * B.items_cap, hipHostMallocMapped));
       HIP_CHECK(hipHostMalloc((void**)&B.h_res, sizeof(WorkResult) * B.items_cap, hipHostMallocMapped));
     }
     for (int a = 0; a < 3; ++a) L->outs.push_back(new TickLane::OutArena());
-    ensure_out(*L, 4u << 20);
+    ensure_out(*L, arena0);
     lanes_.push_back(std::move(L));
   }
   host_mode_.assign(max_slots_, 0);
@@ -2578,13 +2633,19 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
 }
 
 HipEngine::~HipEngine() {
+  if (grid_) {  // frees below wait for the device: the shared grid must have left
+    try {
+      grid_->stop();
+    } catch (const std::exception&) {
+    }
+  }
   for (auto& L : lanes_) {
     try {
       stop_persistent(*L);
     } catch (const std::exception&) {
     }
     if (L->stream) hipStreamSynchronize(L->stream);
-    if (L->h_door) hipHostFree(L->h_door);
+    if (L->h_door && !grid_) hipHostFree(L->h_door);
     if (L->d_ctl) hipFree(L->d_ctl);
     for (TickLane::Buf& B : L->bufs) {
       if (B.h_in) hipHostFree(B.h_in);
@@ -2646,8 +2707,9 @@ uint32_t HipEngine::next_seq(TickLane& L) {
 void HipEngine::ensure_persistent(TickLane& L) {
   if (L.p_running && steady_s() - L.p_last_post > 0.4e-3 * p_idle_ms_) stop_persistent(L);
   if (L.p_running) return;
-  hipLaunchKernelGGL(qmx_tick_persistent, dim3(p_grid_), dim3(BS), 0, L.stream, L.h_door, L.d_ctl,
-                     d_state_, d_content_, L.seq, ++L.p_gen, (uint32_t)p_idle_ms_ * 100000u);
+  L.h_door->base = L.seq;  // the value posted last before this launch
+  hipLaunchKernelGGL(qmx_tick_persistent, dim3(p_grid_), dim3(BS), 0, L.stream, L.h_door, L.d_ctl, p_grid_,
+                     ++L.p_gen, (uint32_t)p_idle_ms_ * 100000u);
   HIP_CHECK(hipGetLastError());
   L.p_running = true;
   L.p_last_post = steady_s();
@@ -2947,7 +3009,7 @@ void HipEngine::post(HipJob& J) {
   std::lock_guard<std::mutex> lg(L.mu);
   TickLane::Buf& B = *J.B;
   // persistent grid (needs polled completion) or a one-shot launch for this tick
-  J.persist = persistent_ && poll_;
+  J.persist = grid_ || (persistent_ && poll_);
   if (!J.persist && L.p_running) stop_persistent(L);  // mode switched: the grid must not hold the stream
   J.new_params = L.params_dirty;
   if (L.params_dirty) {  // the pinned copy is not touched again until this tick completed
@@ -2959,11 +3021,42 @@ void HipEngine::post(HipJob& J) {
   J.tp1 = std::chrono::steady_clock::now();
   roctxRangePushA("qmx_tick");  // rocprofv3 --marker-trace: one range per tick launch + wait
   L.h2d_bytes += J.in_off;
+  const uint32_t par = L.launches & 1;  // backend template table: read last tick's half, write the other
+  FinArgs fa{L.h_fin, L.h_fint, L.h_fin_in, L.d_join, L.d_fout, L.h_fout, L.h_finres, L.h_tl, (int2*)L.d_segs};
+  if (grid_) {
+    // loop-tick mode: this engine's door of the shared grid.  The door's sequence numbers
+    // continue from its last post (a grid stop posts stop ticks on every door, under the
+    // exclusive side of the guard this post holds the shared side of).
+    auto guard = grid_->post_guard();
+    PDoor* door = L.h_door;
+    uint32_t s = door->posted + 1;
+    if (s == 0) s = 1;  // (0 never names a tick)
+    J.seq = s;
+    TickDesc& d = door->d;
+    d.items = B.h_items;
+    d.in = B.h_in;
+    d.out = J.arena->p;
+    d.res = B.h_res;
+    d.params = L.d_params;
+    d.params_src = J.new_params ? L.h_params : nullptr;
+    d.btpl_rd = L.d_btpl + (size_t)(par ^ 1) * kBackendTpl;
+    d.btpl_wr = L.d_btpl + (size_t)par * kBackendTpl;
+    d.fa = fa;
+    d.state = d_state_;
+    d.content = d_content_;
+    d.seq = s;
+    d.n_tick = (uint32_t)J.n;
+    d.n_fin = (uint32_t)J.m;
+    d.stop = 0;
+    __atomic_store_n(&door->posted, s, __ATOMIC_RELEASE);
+    grid_->note_post();
+    ++L.p_ticks;
+    J.posted = true;
+    return;
+  }
   if (J.persist) ensure_persistent(L);  // before the tick's sequence number: a relaunch starts from L.seq
   J.seq = next_seq(L);
-  const uint32_t par = L.launches & 1;  // backend template table: read last tick's half, write the other
   if (!poll_) HIP_CHECK(hipEventRecord(L.ev0, L.stream));
-  FinArgs fa{L.h_fin, L.h_fint, L.h_fin_in, L.d_join, L.d_fout, L.h_fout, L.h_finres, L.h_tl, (int2*)L.d_segs};
   if (J.persist) {
     TickDesc& d = L.h_door->d;  // host-mapped: plain stores, then the release store of `posted`
     d.items = B.h_items;
@@ -2975,6 +3068,8 @@ void HipEngine::post(HipJob& J) {
     d.btpl_rd = L.d_btpl + (size_t)(par ^ 1) * kBackendTpl;
     d.btpl_wr = L.d_btpl + (size_t)par * kBackendTpl;
     d.fa = fa;
+    d.state = d_state_;
+    d.content = d_content_;
     d.seq = J.seq;
     d.n_tick = (uint32_t)J.n;
     d.n_fin = (uint32_t)J.m;
@@ -3209,6 +3304,23 @@ HipEngine::HipJob& HipEngine::hjob(Job& j) {
   J.lane = j.lane;
   return J;
 }
+bool HipEngine::job_ready(Job& j, double* expect_us) {
+  HipJob& J = hjob(j);
+  if (expect_us) *expect_us = 0;
+  if (!J.posted) return true;
+  TickLane& L = *lanes_[(size_t)J.lane % lanes_.size()];
+  const WorkResult* res = J.B->h_res;
+  for (int i = 0; i < J.n; ++i)
+    if (__atomic_load_n(&res[i].seq, __ATOMIC_ACQUIRE) != J.seq) goto pending;
+  for (int i = 0; i < J.m; ++i)
+    if (__atomic_load_n(&L.h_finres[i].seq, __ATOMIC_ACQUIRE) != J.seq) goto pending;
+  return true;
+pending:
+  if (expect_us)
+    *expect_us = L.ema_us - std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - J.tp1).count();
+  return false;
+}
+
 void HipEngine::job_prepare(Job& j) { prepare(hjob(j)); }
 void HipEngine::job_post(Job& j) { post(hjob(j)); }
 void HipEngine::job_wait_near(Job& j) { wait_near(hjob(j)); }
@@ -3396,7 +3508,129 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   m["fin_host"] = (double)fin_host_.load();
   m["lanes"] = (double)lanes_.size();
   m["fin_separate_launches"] = 0.0;  // finalize no longer has a launch (or a wait) of its own
+  if (grid_ && door_ == 0)  // the shared grid's counters, once per process
+    for (auto& kv : grid_->stats()) m[kv.first] += kv.second;
   return m;
+}
+
+// ---- the multi-door grid (loop ticks) ----------------------------------------------------
+HipGrid::HipGrid(int device, int doors, int wg_per_door, int idle_ms)
+    : device_(device), n_(std::max(1, doors)), wpd_(std::max(1, wg_per_door)), idle_ms_(std::max(5, idle_ms)) {
+  HIP_CHECK(hipSetDevice(device_));
+  HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  HIP_CHECK(hipHostMalloc((void**)&h_doors_, sizeof(PDoor) * (size_t)n_, hipHostMallocMapped));
+  std::memset((void*)h_doors_, 0, sizeof(PDoor) * (size_t)n_);
+  HIP_CHECK(hipMalloc((void**)&d_ctls_, sizeof(PCtl) * (size_t)n_));
+  HIP_CHECK(hipMemset(d_ctls_, 0, sizeof(PCtl) * (size_t)n_));
+  HIP_CHECK(hipDeviceSynchronize());  // the zeroed control blocks before any launch reads them
+}
+
+HipGrid::~HipGrid() {
+  try {
+    stop();
+  } catch (const std::exception& e) {
+    fprintf(stderr, "qmx: grid stop failed: %s\n", e.what());
+  }
+  if (stream_) hipStreamSynchronize(stream_);
+  if (h_doors_) hipHostFree(h_doors_);
+  if (d_ctls_) hipFree(d_ctls_);
+  if (stream_) hipStreamDestroy(stream_);
+}
+
+PDoor* HipGrid::door(int d) const { return h_doors_ + d; }
+
+std::shared_lock<std::shared_mutex> HipGrid::post_guard() {
+  for (;;) {
+    std::shared_lock<std::shared_mutex> lk(mu_);
+    if (running_.load(std::memory_order_acquire)) return lk;
+    lk.unlock();
+    std::unique_lock<std::shared_mutex> ex(mu_);
+    if (!running_.load(std::memory_order_relaxed)) launch_locked();
+  }
+}
+
+void HipGrid::note_post() { last_post_.store(steady_s(), std::memory_order_relaxed); }
+
+// Each sub-grid starts from the last tick its door's relay saw: a tick posted to a grid that
+// left without relaying it (the host's heartbeat stopped) is picked up by the new launch.
+void HipGrid::launch_locked() {
+  HIP_CHECK(hipSetDevice(device_));
+  for (int d = 0; d < n_; ++d) h_doors_[d].base = __atomic_load_n(&h_doors_[d].relayed, __ATOMIC_ACQUIRE);
+  const uint32_t idle_ticks = 2000u * 100000u;  // 2 s at 100 MHz: only a host that stopped beating
+  hipLaunchKernelGGL(qmx_tick_persistent, dim3(n_ * wpd_), dim3(BS), 0, stream_, h_doors_, d_ctls_, wpd_, ++gen_,
+                     idle_ticks);
+  HIP_CHECK(hipGetLastError());
+  last_post_.store(steady_s(), std::memory_order_relaxed);
+  running_.store(true, std::memory_order_release);
+  ++launches_;
+}
+
+// Under the exclusive lock (no door is posting): every posted tick relayed, then a stop tick
+// on every door; the grid finishes the ticks it holds and leaves.
+void HipGrid::stop_locked() {
+  if (!running_.load(std::memory_order_relaxed)) return;
+  const double t0 = steady_s();
+  const uint32_t left = (1u << 16) | (gen_ & 0xffffu);
+  auto exited = [&](int d) { return __atomic_load_n(&h_doors_[d].exits, __ATOMIC_ACQUIRE) == left; };
+  for (int d = 0; d < n_; ++d)
+    while (__atomic_load_n(&h_doors_[d].relayed, __ATOMIC_ACQUIRE) != h_doors_[d].posted && !exited(d)) {
+      if (steady_s() - t0 > 5.0) throw std::runtime_error("grid: door " + std::to_string(d) + " never relayed its tick");
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+  for (int d = 0; d < n_; ++d) {
+    if (exited(d)) continue;
+    PDoor& D = h_doors_[d];
+    uint32_t s = D.posted + 1;
+    if (s == 0) s = 1;
+    D.d.stop = 1;
+    D.d.seq = s;
+    __atomic_store_n(&D.posted, s, __ATOMIC_RELEASE);
+  }
+  for (;;) {
+    const hipError_t e = hipStreamQuery(stream_);
+    if (e == hipSuccess) break;
+    if (e != hipErrorNotReady) HIP_CHECK(e);
+    if (steady_s() - t0 > 10.0) throw std::runtime_error("grid: did not leave after its stop ticks");
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+  running_.store(false, std::memory_order_release);
+  ++stops_;
+}
+
+void HipGrid::stop() {
+  std::unique_lock<std::shared_mutex> ex(mu_);
+  stop_locked();
+}
+
+void HipGrid::housekeep() {
+  if (!running_.load(std::memory_order_acquire)) return;
+  if (steady_s() - last_post_.load(std::memory_order_relaxed) > 1e-3 * idle_ms_) {
+    std::unique_lock<std::shared_mutex> ex(mu_, std::try_to_lock);
+    if (ex.owns_lock() && steady_s() - last_post_.load(std::memory_order_relaxed) > 1e-3 * idle_ms_) {
+      stop_locked();
+      return;
+    }
+  }
+  const uint32_t b = beat_.fetch_add(1, std::memory_order_relaxed) + 1;
+  for (int d = 0; d < n_; ++d) __atomic_store_n(&h_doors_[d].beat, b, __ATOMIC_RELAXED);
+}
+
+bool HipGrid::revive_if_exited() {
+  std::unique_lock<std::shared_mutex> ex(mu_);
+  if (!running_.load(std::memory_order_relaxed)) return false;
+  const uint32_t left = (1u << 16) | (gen_ & 0xffffu);
+  bool any = false;
+  for (int d = 0; d < n_; ++d) any = any || __atomic_load_n(&h_doors_[d].exits, __ATOMIC_ACQUIRE) == left;
+  if (!any) return false;
+  stop_locked();  // the sub-grids still running take their stop ticks
+  launch_locked();
+  ++revivals_;
+  return true;
+}
+
+std::unordered_map<std::string, double> HipGrid::stats() {
+  return {{"grid_launches", (double)launches_.load()}, {"grid_stops", (double)stops_.load()},
+          {"grid_revivals", (double)revivals_.load()}, {"grid_doors", (double)n_}};
 }
 
 }  // namespace qmx

@@ -10,6 +10,7 @@
 #include <signal.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
+#include <sys/prctl.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -829,6 +830,8 @@ class Loop {
       });
   }
   void attach_tls(SSL_CTX* t) { tls_ = t; }
+  // loop ticks: this loop's HIP engine posts into door idx_ of the shared grid
+  void attach_grid(HipGrid* g) { grid_ = g; }
   void attach_loops(const std::vector<Loop*>* ls) { loops_ = ls; }
   std::mutex smu_;
   std::unordered_map<std::string, double> snap_;  // engine stats snapshot (read by /metrics on any loop)
@@ -840,6 +843,8 @@ class Loop {
     if (!eng_) return;
     std::unordered_map<std::string, double> m;
     for (auto& kv : eng_->stats()) m["qmx_engine_" + kv.first] = kv.second;
+    if (heng_)
+      for (auto& kv : heng_->kernel_stats()) m["qmx_kernel_" + kv.first] = kv.second;
     std::lock_guard<std::mutex> g(smu_);
     snap_.swap(m);
   }
@@ -878,12 +883,30 @@ class Loop {
     while (!g_stop.load()) {
       // inline engine with work queued by the last iteration (e.g. a finalize submitted
       // while applying tick results): poll instead of sleeping
-      int to = (!hub_ && kick_) ? 0 : deferq_.empty() ? 50 : 1;
+      int to = (!hub_ && !heng_ && kick_) ? 0 : deferq_.empty() ? 50 : 1;
       if (lazy_wake_ && hub_) {
         in_wait_.store(true, std::memory_order_seq_cst);
         if (rq_pending_.load(std::memory_order_seq_cst)) to = 0;  // a batch came in: do not sleep
       }
-      int n = epoll_wait(ep_, evs.data(), (int)evs.size(), to);
+      int n;
+      if (job_live_) {
+        // a tick of this loop is on the GPU: wake when it is expected done, then poll finely
+        // (results are published to host memory; nothing signals them)
+        double exp_us = 0;
+        if (heng_->job_ready(job_, &exp_us)) {
+          n = epoll_wait(ep_, evs.data(), (int)evs.size(), 0);
+        } else {
+          const double us = std::min(std::max(exp_us, (double)poll_us_), 1000.0 * std::max(to, 1));
+          timespec ts{0, (long)(us * 1000.0)};
+          n = epoll_pwait2(ep_, evs.data(), (int)evs.size(), &ts, nullptr);
+          if (n < 0 && errno == ENOSYS) {  // a kernel before 5.11: sleep, then look
+            nanosleep(&ts, nullptr);
+            n = epoll_wait(ep_, evs.data(), (int)evs.size(), 0);
+          }
+        }
+      } else {
+        n = epoll_wait(ep_, evs.data(), (int)evs.size(), to);
+      }
       if (lazy_wake_ && hub_) {
         in_wait_.store(false, std::memory_order_seq_cst);
         if (rq_pending_.load(std::memory_order_acquire)) on_results(false);
@@ -893,13 +916,16 @@ class Loop {
         dispatch(evs[i]);
         // a long batch: tick results that arrived meanwhile are applied now, not after it
         if ((i & 7) == 7 && early_flush_ && rq_pending_.load(std::memory_order_acquire)) on_results(false);
+        if ((i & 7) == 7 && job_live_ && heng_->job_ready(job_)) loop_tick();
       }
       if (g_drain.load() && drain_step()) break;
-      if (hub_ && early_flush_) {
+      if ((hub_ || heng_) && early_flush_) {
         // upstream bytes to the tick lanes and finished responses to their clients before
         // this iteration's new requests (whose parsing and upstream sends are the slow part)
         flush_ops();
-        if (kick_) {
+        if (heng_) {
+          loop_tick();
+        } else if (kick_) {
           kick_ = false;
           hub_->kick();
         }
@@ -919,9 +945,12 @@ class Loop {
         sweep_timeouts(t);
         last_sweep = t;
         snapshot();  // own CPU engine (the GPU hub snapshots the shared HIP engine)
+        if (grid_) grid_->housekeep();  // the shared grid's heartbeat / idle stop
       }
       flush_ops();
-      if (!hub_) {
+      if (heng_) {
+        loop_tick();
+      } else if (!hub_) {
         if (kick_ || eng_->has_work()) {
           kick_ = false;
           tick_inline();
@@ -935,6 +964,14 @@ class Loop {
       if (!flushq_.empty()) flush_queued();
       if (!pending_close_.empty()) reap_clients();
       flush_x();
+    }
+    // a tick still on the GPU completes before the engine (and its arenas) can go
+    for (int k = 0; job_live_ && k < 200000; ++k) {
+      if (heng_->job_ready(job_)) {
+        finish_job();
+        break;
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
   }
   // deferred heads whose deadline passed are queued for this iteration's flush; entries whose
@@ -986,8 +1023,16 @@ class Loop {
     add(evfd_, EPOLLIN, tag_event());
     add(xfd_, EPOLLIN, tag(5, 0));
     idle_.resize(cfg_.backends.size());
-    if (!hub_) {  // CPU engine: ticked inline by this io loop
-      eng_.reset(new CpuEngine(cfg_.tags));
+    if (!hub_) {  // own engine: the CPU engine ticked inline, or a HIP engine on the shared grid
+      if (grid_) {
+        prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // 1 us: the tick polls sleep a few us
+        const int per = std::max(128, cfg_.max_slots / std::max(1, cfg_.threads));
+        heng_ = new HipEngine(cfg_.tags, cfg_.device, cfg_.tile, per, cfg_.content_cap, 1, grid_, idx_);
+        eng_.reset(heng_);
+        loop_slots_ = per;
+      } else {
+        eng_.reset(new CpuEngine(cfg_.tags));
+      }
       if (cfg_.verify) ver_.reset(new Verifier(cfg_.tags));
     }
   }
@@ -1032,6 +1077,39 @@ class Loop {
   }
 
   // ---------------------------------------------------------------- engine plumbing
+  // Loop ticks: this loop's ticks go straight from here to its door of the shared grid, and
+  // their results are applied here — no tick thread, no queue, no eventfd in between.  One
+  // tick in flight per loop: while it runs, this loop's newly dirty streams collect for the
+  // next one (a stream in flight is busy in the engine until its results are applied).
+  void loop_tick() {
+    if (job_live_) {
+      if (!heng_->job_ready(job_)) return;
+      finish_job();
+      flush_ops();  // releases queued while applying the results
+    }
+    kick_ = false;
+    job_.created = (int64_t)time(nullptr);
+    job_.lane = 0;
+    if (!eng_->job_take(job_, true)) return;
+    job_t_post_ = now_s();
+    eng_->job_prepare(job_);
+    eng_->job_post(job_);
+    job_live_ = true;
+    if (heng_->job_ready(job_)) finish_job();  // nothing went to the GPU (host-path streams only)
+  }
+  void finish_job() {
+    ResultBatch rb;
+    taken_.clear();
+    eng_->job_complete(job_, rb.r, rb.f);
+    eng_->job_finish(job_, rb.r, taken_);
+    job_live_ = false;
+    eng_->settle(taken_);
+    h_tick.observe(now_s() - job_t_post_);
+    if (ver_) ver_->check(job_.created, rb.r, rb.f);
+    c_ticks++;
+    c_tick_slots += rb.r.size();
+    apply(rb);
+  }
   void tick_inline() {
     ResultBatch rb;
     const double tt = now_s();
@@ -1121,6 +1199,7 @@ class Loop {
       slot = hub_->open(idx_, index, f, e, &gen, verify);
     } else {
       slot = eng_->open(index, f, e, &gen);
+      if (heng_ && slot >= loop_slots_) c_host_path_opens++;  // beyond this loop's HBM slot state
       if (ver_ && verify) ver_->open(slot, gen, index, f, e);
     }
     slot_owner_[slot] = SlotOwner{s, bi, gen};
@@ -2802,6 +2881,17 @@ class Loop {
   std::unique_ptr<HostEngine> eng_;  // CPU engine (no GPU hub)
   std::unique_ptr<Verifier> ver_;
   GpuHub* hub_ = nullptr;            // shared HIP engine
+  HipGrid* grid_ = nullptr;          // loop ticks: the shared multi-door grid
+  HipEngine* heng_ = nullptr;        // loop ticks: eng_ as this loop's HIP engine
+  int loop_slots_ = 0;
+  HostEngine::Job job_;              // loop ticks: the tick this loop has on the GPU
+  bool job_live_ = false;
+  double job_t_post_ = 0;
+  std::vector<int> taken_;
+  const int poll_us_ = [] {
+    const char* e = env_get("QMX_LOOP_POLL_US");
+    return e ? std::max(1, atoi(e)) : 3;
+  }();
   TagSet ts_ = make_tagset(cfg_.tags);
   bool kick_ = false;
   std::mutex rmu_;
@@ -2920,12 +3010,24 @@ int run_server(const ServerCfg& cfg0) {
   std::vector<Loop*> loop_ptrs;
   for (auto& l : loops) loop_ptrs.push_back(l.get());
   std::unique_ptr<GpuHub> hub;
-  const bool shared = cfg.shared_engine < 0 ? cfg.engine == "hip" : cfg.shared_engine > 0;
+  std::unique_ptr<HipGrid> grid;  // destroyed after the loops (their engines stop it first)
+  const bool hip = cfg.engine == "hip";
+  const bool spread = cfg.world > 1 && cfg.placement == "spread";
+  // hip: loop ticks unless asked for lanes (tick_mode / an explicit shared engine) or sessions
+  // spread across ranks (remote texts land in the content arena outside the grid's protocol)
+  const bool loop_ticks = hip && !spread && cfg.tick_mode != "lanes" && cfg.shared_engine != 1;
+  const bool shared = !loop_ticks && (cfg.shared_engine < 0 ? hip : cfg.shared_engine > 0);
   if (shared) hub.reset(new GpuHub(cfg, (int)loops.size()));
+  if (loop_ticks) {
+    const char* w = env_get("QMX_GRID_WPD");
+    const char* im = env_get("QMX_PERSISTENT_IDLE_MS");
+    grid.reset(new HipGrid(cfg.device, (int)loops.size(), w ? std::max(1, atoi(w)) : 8, im ? atoi(im) : 50));
+  }
   for (auto& l : loops) {
     l->attach_loops(&loop_ptrs);
     l->attach_tls(tls);
     l->attach_hub(hub.get());
+    l->attach_grid(grid.get());
   }
   if (hub) hub->start();
   std::unique_ptr<Exchange> xch;
@@ -2964,7 +3066,9 @@ int run_server(const ServerCfg& cfg0) {
     xch.reset();
   }
   hub.reset();  // tick thread joined before the loops (its result sinks) go away
+  if (grid) grid->stop();  // before the loops' engines free what the grid may touch
   loops.clear();
+  grid.reset();
   if (tls) SSL_CTX_free(tls);
   return 0;
 }

@@ -36,6 +36,10 @@ struct ServerCfg {
   std::string engine = "cpu";
   int shared_engine = -1;  // one engine per process shared by all io loops (-1: auto = hip only)
   int tick_lanes = 2;      // shared engine: tick threads, each with its own HIP stream + arenas
+  // hip: "loops" = every io loop owns an engine and posts its own ticks into one multi-door
+  // persistent grid (HipGrid), "lanes" = the shared engine + tick-lane threads (GpuHub),
+  // "auto" = loops unless sessions spread across ranks
+  std::string tick_mode = "auto";
   int device = 0;
   int tile = 16384, max_slots = 4096, content_cap = 1 << 20;
   // config

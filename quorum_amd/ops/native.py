@@ -69,7 +69,8 @@ class NativeEngine:
     """Python face of the C++ engines (``cpu`` = host library, ``hip`` = GPU tick kernels)."""
 
     def __init__(self, kind: str, tags: Sequence[str], device: Optional[int] = None,
-                 tile_bytes: int = 16384, max_slots: int = 8192, content_cap: int = 1 << 20, lanes: int = 1):
+                 tile_bytes: int = 16384, max_slots: int = 8192, content_cap: int = 1 << 20, lanes: int = 1,
+                 grid=None, door: int = -1):
         ext = require()
         self.kind = kind
         self.name = kind
@@ -84,7 +85,8 @@ class NativeEngine:
                 raise RuntimeError("engine 'hip' requested but no GPU is visible")
             if device is None:
                 device = int(os.environ.get("LOCAL_RANK", "0")) % max(ext.device_count(), 1)
-            self._e = ext.HipEngine(low, device, tile_bytes, max_slots, content_cap, lanes)
+            # grid: a HipGrid (loop ticks) — this engine posts its ticks into door `door` of it
+            self._e = ext.HipEngine(low, device, tile_bytes, max_slots, content_cap, lanes, grid, door)
             self.offload = True
         else:
             self._e = ext.CpuEngine(low)

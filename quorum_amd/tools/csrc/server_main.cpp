@@ -96,6 +96,7 @@ int main(int argc, char** argv) {
   c.verify = gb(d, "verify", false);
   c.shared_engine = gi(d, "shared_engine", -1);
   c.tick_lanes = gi(d, "tick_lanes", c.tick_lanes);
+  c.tick_mode = gs(d, "tick_mode", c.tick_mode);
   c.ca_file = gs(d, "ca_file", "");
   c.tls_verify = gb(d, "tls_verify", true);
   if (const JVal* bs = d.get("backends")) {

@@ -221,6 +221,10 @@ class RuntimeConfig:
                engines for cpu) | true | false (QMX_SHARED_ENGINE=0/1)
     tick_lanes: shared engine: tick threads with a kernel in flight each (own HIP stream and
                arenas, disjoint stream sets) — QMX_TICK_LANES
+    tick_mode: hip engine: "loops" (every io loop owns an engine and posts its own ticks into
+               one shared multi-door persistent grid, applying the results itself — no tick
+               thread in between) | "lanes" (one shared engine ticked by `tick_lanes` threads)
+               | "auto" (loops, except spread placement across ranks: lanes) — QMX_TICK_MODE
     log_content: allow prompts / per-backend answers in the ``aggregation`` log (off: user
                data; see utils/logging_setup.py) — QMX_LOG_CONTENT
     watch_config: the supervisor polls the config file and rolls a new worker generation in
@@ -244,6 +248,7 @@ class RuntimeConfig:
     verify: bool = False
     shared_engine: Any = "auto"
     tick_lanes: int = 2
+    tick_mode: str = "auto"
     log_content: bool = False
     watch_config: bool = False
     watch_interval: float = 1.0
@@ -264,5 +269,7 @@ class RuntimeConfig:
             rt["watch_config"] = os.environ["QMX_WATCH_CONFIG"] not in ("0", "", "false")
         if os.environ.get("QMX_TICK_LANES"):
             rt["tick_lanes"] = int(os.environ["QMX_TICK_LANES"])
+        if os.environ.get("QMX_TICK_MODE"):
+            rt["tick_mode"] = os.environ["QMX_TICK_MODE"]
         known = {k: v for k, v in rt.items() if k in cls.__dataclass_fields__}
         return cls(**known)
