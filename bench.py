@@ -393,6 +393,14 @@ def breakdown(m0, m1, elapsed):
                                               ("dirty_to_taken", "qmx_engine_take_wait_us", "qmx_engine_takes", 1.0),
                                               ("routed_to_applied", "qmx_apply_wait_seconds_total", "qmx_applies_total", 1e6))
                            if d.get(b)},
+        # QMX_STAGE_TIMING=1 runs only: in-kernel stage split per item (s_memrealtime stamps;
+        # stages as tools/kbench.py) and the shader clock the items ran at
+        "stage_us_per_item": ({k[11:]: round(v / d["qmx_kernel_stage_items"], 2)
+                               for k, v in sorted(d.items())
+                               if k.startswith("qmx_kernel_stage") and k.endswith("_us")}
+                              if d.get("qmx_kernel_stage_items") else None),
+        "shader_mhz": (round(d["qmx_kernel_clk_cycles"] / d["qmx_kernel_clk_us"], 1)
+                       if d.get("qmx_kernel_clk_us") else None),
     }
 
 

@@ -364,15 +364,16 @@ PYBIND11_MODULE(_qmx, m) {
       .def("housekeep", &HipGrid::housekeep)
       .def("stop", &HipGrid::stop, py::call_guard<py::gil_scoped_release>())
       .def("stats", &HipGrid::stats);
+  m.def("_free_doors", [](HipEngine& e) { return e.free_doors(); });
   py::class_<HipEngine> he(m, "HipEngine");
   he.def(py::init([](const std::vector<std::string>& tags, int device, int tile, int max_slots, int content_cap,
-                      int lanes, HipGrid* grid, int door) {
+                      int lanes, HipGrid* grid, int door, int ndoors) {
            env_refresh();
-           return new HipEngine(tags, device, tile, max_slots, content_cap, lanes, grid, door);
+           return new HipEngine(tags, device, tile, max_slots, content_cap, lanes, grid, door, ndoors);
          }),
          py::arg("tags"), py::arg("device"), py::arg("tile_bytes") = 16384, py::arg("max_slots") = 8192,
          py::arg("content_cap") = 1 << 20, py::arg("lanes") = 1, py::arg("grid") = nullptr, py::arg("door") = -1,
-         py::keep_alive<1, 8>());
+         py::arg("ndoors") = 1, py::keep_alive<1, 8>());
   bind_engine(he);
   he.def("kernel_stats", &HipEngine::kernel_stats);
 }

@@ -178,13 +178,14 @@ struct TickLane {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evb = nullptr;
   KParams params;
-  KParams* d_params = nullptr;  // device copy read by the kernel
-  BackendTpl* d_btpl = nullptr;  // [2][kBackendTpl]: launch parity double buffer
-  KParams* h_params = nullptr;  // pinned staging for its upload
+  uint64_t params_ver = 1;  // bumped whenever `params` changes (each Buf uploads its own copy)
+  // [door sets][2][kBackendTpl]: per door set (loop ticks: a door of the engine's own; lanes:
+  // one) a launch-parity double buffer — a tick reads its door set's last tick's half
+  BackendTpl* d_btpl = nullptr;
+  uint32_t tpl_launches[2] = {0, 0};  // completed ticks per door set (the parity)
   int64_t params_created = -1;
-  bool params_dirty = true;
-  // two buffer sets (tiles, work items, result records, stage stamps), alternated per tick:
-  // the next tick is prepared while this one runs (GpuHub's pipelined lanes)
+  // two buffer sets (tiles, work items, result records, stage stamps, kernel parameters), one
+  // per tick in flight or in preparation (GpuHub's pipelined lanes; two doors of a loop)
   struct Buf {
     uint8_t* h_in = nullptr;
     size_t in_cap = 0;
@@ -193,9 +194,12 @@ struct TickLane {
     size_t items_cap = 0;
     unsigned long long* h_dbg = nullptr;
     size_t dbg_cap = 0;
+    KParams* h_params = nullptr;  // pinned staging of this buffer's parameter upload
+    KParams* d_params = nullptr;  // device copy read by this buffer's ticks
+    uint64_t params_ver = 0;      // the TickLane::params version in d_params
+    bool busy = false;            // a prepared tick holds it until complete()
   };
   Buf bufs[2];
-  int next_buf = 0;
   // output arenas (pinned, mapped): results view their SSE bytes in place (SlotResult::view),
   // so a tick writes into an arena no earlier result still views — a ring that grows while
   // every arena is held (OutArena objects are never freed: a late ViewRef may still count)
@@ -244,6 +248,7 @@ struct TickLane {
   uint32_t seq = 0;
   double ema_us = 40.0;  // launch-to-results time, smoothed
   double span_ema_us = 30.0;  // kernel span per tick (device clock), smoothed: pipelined lanes
+  double lead_ema_us = 8.0;   // persistent: doorbell seen -> first item started (device clock), smoothed
   bool timing_pending = false;
   uint64_t poll_fallbacks = 0;
   // persistent mode (QMX_PERSISTENT=1): the lane's long-lived grid and its doorbell
@@ -260,11 +265,13 @@ class HipEngine : public HostEngine {
  public:
   // grid: loop-tick mode — one lane whose ticks go to door `door` of a shared multi-door grid
   HipEngine(const std::vector<std::string>& tags, int device, int tile_bytes, int max_slots, int content_cap,
-            int lanes = 1, HipGrid* grid = nullptr, int door = -1);
+            int lanes = 1, HipGrid* grid = nullptr, int door = -1, int ndoors = 1);
   ~HipEngine() override;
   // loop-tick mode (the io loop drives its own ticks): has the posted job's every result been
   // published?  Never blocks.  expect_us: the job's expected remaining time (poll timing).
   bool job_ready(Job& j, double* expect_us = nullptr);
+  // loop-tick mode: doors of this engine with no tick on them (a job may be prepared + posted)
+  int free_doors() const;
   std::string text(int slot) override;
   void* content_device_ptr(int slot, size_t* cap) override;
   size_t content_size(int slot) override;
@@ -339,8 +346,10 @@ class HipEngine : public HostEngine {
   bool stage_timing_ = false;  // QMX_STAGE_TIMING: per-item stage stamps (tools/kbench.py)
   int p_grid_ = 64;          // QMX_PERSISTENT_WG: workgroups per lane grid (1 per CU: 256 VGPRs)
   int p_idle_ms_ = 50;       // the grid exits after this long without a tick
-  HipGrid* grid_ = nullptr;  // loop-tick mode: the shared grid and this engine's door
-  int door_ = -1;
+  HipGrid* grid_ = nullptr;  // loop-tick mode: the shared grid and this engine's doors
+  int door_ = -1;            // the first of them
+  int ndoors_ = 1;           // doors [door_, door_ + ndoors_): ticks in flight at once (<= 2)
+  std::vector<char> door_busy_;
 
  public:
   bool persistent() const { return persistent_; }

@@ -2195,6 +2195,13 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
 // this launch generation; or (safety net) any workgroup idle for 2 x idle_ticks.  The host
 // never posts to a grid that may be idling out (HipEngine::ensure_persistent), and stops it
 // before anything that would wait for the device.
+// Multi-door grids (HipGrid, loop ticks): the grid is doors x wpd workgroups, sub-grid
+// blockIdx.x / wpd serving door blockIdx.x / wpd with its own control block — one launch,
+// one hardware queue, every io loop's ticks.  The host bumps each door's heartbeat word
+// (read with `posted` in one 8-byte load) while it wants the grid; a change resets the idle
+// clock of the relay and, through the control block, of its workers, so a door with no
+// traffic keeps its sub-grid while the others are busy.  Idle time counts from the last
+// post or heartbeat, so the 2 s limit HipGrid passes fires only for a host that stopped.
 // ------------------------------------------------------------------------------------
 template <class T>
 __device__ __forceinline__ T* uni(T* p) {  // a wave-uniform pointer held in SGPRs
@@ -2514,17 +2521,19 @@ void HipEngine::collect_timing(TickLane& L) {
 }
 
 HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_bytes, int max_slots,
-                     int content_cap, int lanes, HipGrid* grid, int door)
+                     int content_cap, int lanes, HipGrid* grid, int door, int ndoors)
     : HostEngine(tags),
       device_(device),
       tile_(std::min(std::max(tile_bytes, 1024), TILE_MAX) & ~15),
       max_slots_(max_slots),
       content_cap_((uint32_t)content_cap),
       grid_(grid),
-      door_(door) {
+      door_(door),
+      ndoors_(grid ? std::min(std::max(ndoors, 1), 2) : 1) {
   HIP_CHECK(hipSetDevice(device_));
-  if (grid_ && (door_ < 0 || door_ >= grid_->doors())) throw std::invalid_argument("HipEngine: door out of range");
+  if (grid_ && (door_ < 0 || door_ + ndoors_ > grid_->doors())) throw std::invalid_argument("HipEngine: door out of range");
   if (grid_) lanes = 1;
+  door_busy_.assign(ndoors_, 0);
   if (const char* sp = env_get("QMX_WAIT_SPIN_US")) spin_us_ = atoi(sp);
   if (const char* w = env_get("QMX_WAIT")) poll_ = std::string(w) != "event";
   if (const char* pu = env_get("QMX_POLL_US")) poll_us_ = std::max(1, atoi(pu));
@@ -2604,10 +2613,8 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
     HIP_CHECK(hipEventCreate(&L->ev1));
     HIP_CHECK(hipEventCreateWithFlags(&L->evb, hipEventBlockingSync | hipEventDisableTiming));
     L->params = base_params_;
-    HIP_CHECK(hipMalloc((void**)&L->d_params, sizeof(KParams)));
-    HIP_CHECK(hipMalloc((void**)&L->d_btpl, sizeof(BackendTpl) * 2 * kBackendTpl));
-    HIP_CHECK(hipMemset(L->d_btpl, 0, sizeof(BackendTpl) * 2 * kBackendTpl));
-    HIP_CHECK(hipHostMalloc((void**)&L->h_params, sizeof(KParams), hipHostMallocMapped));
+    HIP_CHECK(hipMalloc((void**)&L->d_btpl, sizeof(BackendTpl) * 2 * kBackendTpl * ndoors_));
+    HIP_CHECK(hipMemset(L->d_btpl, 0, sizeof(BackendTpl) * 2 * kBackendTpl * ndoors_));
     if (grid_) {
       L->h_door = grid_->door(door_);  // the grid's (not freed here)
     } else {
@@ -2619,6 +2626,8 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
     // an io loop's engine (loop ticks) carries a few streams per tick: arenas start small
     const size_t arena0 = grid_ ? (1u << 20) : (4u << 20);
     for (TickLane::Buf& B : L->bufs) {
+      HIP_CHECK(hipMalloc((void**)&B.d_params, sizeof(KParams)));
+      HIP_CHECK(hipHostMalloc((void**)&B.h_params, sizeof(KParams), hipHostMallocMapped));
       ensure_in(B, arena0);
       B.items_cap = 1024;
       HIP_CHECK(hipHostMalloc((void**)&B.h_items, sizeof(WorkItem) * B.items_cap, hipHostMallocMapped));
@@ -2652,12 +2661,12 @@ HipEngine::~HipEngine() {
       if (B.h_items) hipHostFree(B.h_items);
       if (B.h_res) hipHostFree(B.h_res);
       if (B.h_dbg) hipHostFree(B.h_dbg);
+      if (B.h_params) hipHostFree(B.h_params);
+      if (B.d_params) hipFree(B.d_params);
     }
     for (TickLane::OutArena* a : L->outs)
       if (a->p) hipHostFree(a->p);  // the OutArena objects stay (see TickLane::outs)
-    if (L->d_params) hipFree(L->d_params);
     if (L->d_btpl) hipFree(L->d_btpl);
-    if (L->h_params) hipHostFree(L->h_params);
     if (L->h_fin) hipHostFree(L->h_fin);
     if (L->h_finres) hipHostFree(L->h_finres);
     if (L->h_fint) hipHostFree(L->h_fint);
@@ -2859,6 +2868,7 @@ struct HipEngine::HipJob {
   std::vector<FinalizeReq>* fin = nullptr;
   int64_t created = 0;
   int lane = 0, n = 0, m = 0;
+  int dk = 0;  // loop ticks: the engine's door the tick went to (its template tables)
   uint32_t seq = 0;
   bool persist = false, new_params = false, posted = false;
   std::vector<Pending> pend;
@@ -2886,8 +2896,16 @@ void HipEngine::prepare(HipJob& J) {
   J.fin_host.clear();
   J.posted = false;
   std::vector<Work>& work = *J.work;
-  TickLane::Buf& B = L.bufs[L.next_buf];
-  L.next_buf ^= 1;
+  // a buffer set no prepared / in-flight tick holds (two: pipelined lanes, two doors)
+  TickLane::Buf* bp = nullptr;
+  for (TickLane::Buf& b : L.bufs)
+    if (!b.busy) {
+      bp = &b;
+      break;
+    }
+  if (!bp) throw std::logic_error("tick prepared with both buffer sets in use");
+  TickLane::Buf& B = *bp;
+  B.busy = true;
   J.B = &B;
   size_t out_need = 0;
   for (auto& w : work) {
@@ -2984,7 +3002,7 @@ void HipEngine::prepare(HipJob& J) {
     if (J.created != L.params_created) {  // envelopes carry the second: rebuilt + uploaded once a second
       build_params(L, J.created);
       L.params_created = J.created;
-      L.params_dirty = true;
+      ++L.params_ver;
     }
     unsigned long long* const dbg0 = L.params.dbg;
     L.params.dbg = nullptr;
@@ -2997,7 +3015,7 @@ void HipEngine::prepare(HipJob& J) {
       std::memset(B.h_dbg, 0, sizeof(unsigned long long) * kDbg * n);
       L.params.dbg = B.h_dbg;
     }
-    if (L.params.dbg != dbg0) L.params_dirty = true;
+    if (L.params.dbg != dbg0) ++L.params_ver;
   }
   J.tp1 = HC::now();
   L.host_prep_us += std::chrono::duration<double, std::micro>(J.tp1 - J.tp0).count();
@@ -3011,24 +3029,32 @@ void HipEngine::post(HipJob& J) {
   // persistent grid (needs polled completion) or a one-shot launch for this tick
   J.persist = grid_ || (persistent_ && poll_);
   if (!J.persist && L.p_running) stop_persistent(L);  // mode switched: the grid must not hold the stream
-  J.new_params = L.params_dirty;
-  if (L.params_dirty) {  // the pinned copy is not touched again until this tick completed
-    std::memcpy(L.h_params, &L.params, sizeof(KParams));
+  J.new_params = B.params_ver != L.params_ver;
+  if (J.new_params) {  // the buffer's pinned copy is not touched again until its tick completed
+    std::memcpy(B.h_params, &L.params, sizeof(KParams));
     // one-shot launches: a stream-ordered upload; persistent: the grid copies it itself
-    if (!J.persist) HIP_CHECK(hipMemcpyAsync(L.d_params, L.h_params, sizeof(KParams), hipMemcpyHostToDevice, L.stream));
-    L.params_dirty = false;
+    if (!J.persist) HIP_CHECK(hipMemcpyAsync(B.d_params, B.h_params, sizeof(KParams), hipMemcpyHostToDevice, L.stream));
+    B.params_ver = L.params_ver;
   }
   J.tp1 = std::chrono::steady_clock::now();
   roctxRangePushA("qmx_tick");  // rocprofv3 --marker-trace: one range per tick launch + wait
   L.h2d_bytes += J.in_off;
-  const uint32_t par = L.launches & 1;  // backend template table: read last tick's half, write the other
+  // backend template tables of the tick's door set: read its last tick's half, write the other
+  J.dk = 0;
+  if (grid_) {
+    while (J.dk < ndoors_ && door_busy_[J.dk]) ++J.dk;
+    if (J.dk == ndoors_) throw std::logic_error("tick posted with every door of the engine busy");
+  }
+  const uint32_t par = L.tpl_launches[J.dk] & 1;
+  BackendTpl* const tpl = L.d_btpl + (size_t)J.dk * 2 * kBackendTpl;
   FinArgs fa{L.h_fin, L.h_fint, L.h_fin_in, L.d_join, L.d_fout, L.h_fout, L.h_finres, L.h_tl, (int2*)L.d_segs};
   if (grid_) {
     // loop-tick mode: this engine's door of the shared grid.  The door's sequence numbers
     // continue from its last post (a grid stop posts stop ticks on every door, under the
     // exclusive side of the guard this post holds the shared side of).
     auto guard = grid_->post_guard();
-    PDoor* door = L.h_door;
+    PDoor* door = grid_->door(door_ + J.dk);
+    door_busy_[J.dk] = 1;
     uint32_t s = door->posted + 1;
     if (s == 0) s = 1;  // (0 never names a tick)
     J.seq = s;
@@ -3037,10 +3063,10 @@ void HipEngine::post(HipJob& J) {
     d.in = B.h_in;
     d.out = J.arena->p;
     d.res = B.h_res;
-    d.params = L.d_params;
-    d.params_src = J.new_params ? L.h_params : nullptr;
-    d.btpl_rd = L.d_btpl + (size_t)(par ^ 1) * kBackendTpl;
-    d.btpl_wr = L.d_btpl + (size_t)par * kBackendTpl;
+    d.params = B.d_params;
+    d.params_src = J.new_params ? B.h_params : nullptr;
+    d.btpl_rd = tpl + (size_t)(par ^ 1) * kBackendTpl;
+    d.btpl_wr = tpl + (size_t)par * kBackendTpl;
     d.fa = fa;
     d.state = d_state_;
     d.content = d_content_;
@@ -3063,10 +3089,10 @@ void HipEngine::post(HipJob& J) {
     d.in = B.h_in;
     d.out = J.arena->p;
     d.res = B.h_res;
-    d.params = L.d_params;
-    d.params_src = J.new_params ? L.h_params : nullptr;
-    d.btpl_rd = L.d_btpl + (size_t)(par ^ 1) * kBackendTpl;
-    d.btpl_wr = L.d_btpl + (size_t)par * kBackendTpl;
+    d.params = B.d_params;
+    d.params_src = J.new_params ? B.h_params : nullptr;
+    d.btpl_rd = tpl + (size_t)(par ^ 1) * kBackendTpl;
+    d.btpl_wr = tpl + (size_t)par * kBackendTpl;
     d.fa = fa;
     d.state = d_state_;
     d.content = d_content_;
@@ -3079,8 +3105,8 @@ void HipEngine::post(HipJob& J) {
     ++L.p_ticks;
   } else {
     hipLaunchKernelGGL(qmx_tick_kernel, dim3(J.n + J.m), dim3(BS), 0, L.stream, B.h_items, B.h_in, J.arena->p,
-                       B.h_res, d_state_, d_content_, L.d_params, J.seq, (uint32_t)J.n, fa,
-                       L.d_btpl + (size_t)(par ^ 1) * kBackendTpl, L.d_btpl + (size_t)par * kBackendTpl);
+                       B.h_res, d_state_, d_content_, B.d_params, J.seq, (uint32_t)J.n, fa,
+                       tpl + (size_t)(par ^ 1) * kBackendTpl, tpl + (size_t)par * kBackendTpl);
     HIP_CHECK(hipGetLastError());
   }
   J.posted = true;
@@ -3198,9 +3224,11 @@ void HipEngine::complete(HipJob& J, std::vector<SlotResult>& results, std::vecto
       }
       if (J.persist && n > 0) {  // the grid's side of the tick (its own clock): doorbell seen ->
         // relayed -> first item started -> last item done
-        const uint64_t ts = __atomic_load_n(&L.h_door->t_seen, __ATOMIC_ACQUIRE);
-        const uint64_t tr = __atomic_load_n(&L.h_door->t_relayed, __ATOMIC_ACQUIRE);
+        const PDoor* dr = grid_ ? grid_->door(door_ + J.dk) : L.h_door;
+        const uint64_t ts = __atomic_load_n(&dr->t_seen, __ATOMIC_ACQUIRE);
+        const uint64_t tr = __atomic_load_n(&dr->t_relayed, __ATOMIC_ACQUIRE);
         if (ts && tr >= ts && a >= tr && b >= a) {
+          L.lead_ema_us = 0.85 * L.lead_ema_us + 0.15 * std::min((double)(a - ts) * 1e-2, 500.0);
           L.relay_us += (double)(tr - ts) * 1e-2;
           L.pickup_us += (double)(a - tr) * 1e-2;
           L.grid_span_us += (double)(b - ts) * 1e-2;
@@ -3224,6 +3252,8 @@ void HipEngine::complete(HipJob& J, std::vector<SlotResult>& results, std::vecto
     roctxRangePop();
     L.gpu_wait_us += std::chrono::duration<double, std::micro>(HC::now() - J.tp1).count();
     ++L.launches;
+    ++L.tpl_launches[J.dk];
+    if (grid_) door_busy_[J.dk] = 0;
     L.items += n;
     if (m > 0) {
       ++L.fin_launches;
@@ -3279,6 +3309,7 @@ void HipEngine::complete(HipJob& J, std::vector<SlotResult>& results, std::vecto
     }
   }
   J.arena->refs.fetch_sub(1, std::memory_order_release);  // results hold their own references
+  J.B->busy = false;
   L.process_us += std::chrono::duration<double, std::micro>(HC::now() - J.tp0).count();
 }
 
@@ -3304,6 +3335,12 @@ HipEngine::HipJob& HipEngine::hjob(Job& j) {
   J.lane = j.lane;
   return J;
 }
+int HipEngine::free_doors() const {
+  int k = 0;
+  for (char b : door_busy_) k += !b;
+  return k;
+}
+
 bool HipEngine::job_ready(Job& j, double* expect_us) {
   HipJob& J = hjob(j);
   if (expect_us) *expect_us = 0;
@@ -3316,8 +3353,12 @@ bool HipEngine::job_ready(Job& j, double* expect_us) {
     if (__atomic_load_n(&L.h_finres[i].seq, __ATOMIC_ACQUIRE) != J.seq) goto pending;
   return true;
 pending:
+  // from the device's own clocks (doorbell seen -> first item, kernel span), not from host
+  // wake-ups: a poller that sleeps until an estimate built from its own wake-ups never
+  // wakes earlier than that estimate, and the estimate only drifts up
   if (expect_us)
-    *expect_us = L.ema_us - std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - J.tp1).count();
+    *expect_us = L.lead_ema_us + L.span_ema_us + 3.0 -
+                 std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - J.tp1).count();
   return false;
 }
 
@@ -3504,6 +3545,8 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   m["stage_s4match_us"] = stage[14];
   m["stage_s4cuts_us"] = stage[15];
   m["shader_mhz"] = cus > 0 ? cyc / cus : 0.0;
+  m["clk_cycles"] = cyc;  // summable across engines (/metrics sums the io loops' engines)
+  m["clk_us"] = cus;
   m["escalations"] = (double)escalations_.load();
   m["fin_host"] = (double)fin_host_.load();
   m["lanes"] = (double)lanes_.size();

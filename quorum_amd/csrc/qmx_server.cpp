@@ -889,11 +889,18 @@ class Loop {
         if (rq_pending_.load(std::memory_order_seq_cst)) to = 0;  // a batch came in: do not sleep
       }
       int n;
-      if (job_live_) {
-        // a tick of this loop is on the GPU: wake when it is expected done, then poll finely
-        // (results are published to host memory; nothing signals them)
-        double exp_us = 0;
-        if (heng_->job_ready(job_, &exp_us)) {
+      if (jobs_live_) {
+        // ticks of this loop are on the GPU: wake when the first is expected done, then poll
+        // finely (results are published to host memory; nothing signals them)
+        double exp_us = 1e9;
+        bool ready = false;
+        for (int k = 0; k < 2 && !ready; ++k) {
+          double e = 0;
+          if (!job_live_[k]) continue;
+          ready = heng_->job_ready(job_[k], &e);
+          exp_us = std::min(exp_us, e);
+        }
+        if (ready) {
           n = epoll_wait(ep_, evs.data(), (int)evs.size(), 0);
         } else {
           const double us = std::min(std::max(exp_us, (double)poll_us_), 1000.0 * std::max(to, 1));
@@ -916,7 +923,7 @@ class Loop {
         dispatch(evs[i]);
         // a long batch: tick results that arrived meanwhile are applied now, not after it
         if ((i & 7) == 7 && early_flush_ && rq_pending_.load(std::memory_order_acquire)) on_results(false);
-        if ((i & 7) == 7 && job_live_ && heng_->job_ready(job_)) loop_tick();
+        if ((i & 7) == 7 && jobs_live_ && any_ready()) loop_tick();
       }
       if (g_drain.load() && drain_step()) break;
       if ((hub_ || heng_) && early_flush_) {
@@ -965,13 +972,11 @@ class Loop {
       if (!pending_close_.empty()) reap_clients();
       flush_x();
     }
-    // a tick still on the GPU completes before the engine (and its arenas) can go
-    for (int k = 0; job_live_ && k < 200000; ++k) {
-      if (heng_->job_ready(job_)) {
-        finish_job();
-        break;
-      }
-      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    // ticks still on the GPU complete before the engine (and its arenas) can go
+    for (int w = 0; jobs_live_ && w < 200000; ++w) {
+      for (int k = 0; k < 2; ++k)
+        if (job_live_[k] && heng_->job_ready(job_[k])) finish_job(k);
+      if (jobs_live_) std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
   }
   // deferred heads whose deadline passed are queued for this iteration's flush; entries whose
@@ -1027,7 +1032,8 @@ class Loop {
       if (grid_) {
         prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // 1 us: the tick polls sleep a few us
         const int per = std::max(128, cfg_.max_slots / std::max(1, cfg_.threads));
-        heng_ = new HipEngine(cfg_.tags, cfg_.device, cfg_.tile, per, cfg_.content_cap, 1, grid_, idx_);
+        heng_ = new HipEngine(cfg_.tags, cfg_.device, cfg_.tile, per, cfg_.content_cap, 1, grid_,
+                              idx_ * loop_doors_, loop_doors_);
         eng_.reset(heng_);
         loop_slots_ = per;
       } else {
@@ -1077,35 +1083,51 @@ class Loop {
   }
 
   // ---------------------------------------------------------------- engine plumbing
-  // Loop ticks: this loop's ticks go straight from here to its door of the shared grid, and
-  // their results are applied here — no tick thread, no queue, no eventfd in between.  One
-  // tick in flight per loop: while it runs, this loop's newly dirty streams collect for the
-  // next one (a stream in flight is busy in the engine until its results are applied).
-  void loop_tick() {
-    if (job_live_) {
-      if (!heng_->job_ready(job_)) return;
-      finish_job();
-      flush_ops();  // releases queued while applying the results
-    }
-    kick_ = false;
-    job_.created = (int64_t)time(nullptr);
-    job_.lane = 0;
-    if (!eng_->job_take(job_, true)) return;
-    job_t_post_ = now_s();
-    eng_->job_prepare(job_);
-    eng_->job_post(job_);
-    job_live_ = true;
-    if (heng_->job_ready(job_)) finish_job();  // nothing went to the GPU (host-path streams only)
+  // Loop ticks: this loop's ticks go straight from here to its doors of the shared grid, and
+  // their results are applied here — no tick thread, no queue, no eventfd in between.  Up to
+  // `loop_doors_` ticks in flight per loop (a door each): a stream that becomes dirty while
+  // one runs goes out on the other at once (a stream in flight is busy in the engine until
+  // its results are applied, so its own ticks stay in order).
+  bool any_ready() {
+    for (int k = 0; k < 2; ++k)
+      if (job_live_[k] && heng_->job_ready(job_[k])) return true;
+    return false;
   }
-  void finish_job() {
+  void loop_tick() {
+    bool applied = false;
+    for (int k = 0; k < 2; ++k)
+      if (job_live_[k] && heng_->job_ready(job_[k])) {
+        finish_job(k);
+        applied = true;
+      }
+    if (applied) flush_ops();  // releases queued while applying the results
+    kick_ = false;
+    if (heng_->free_doors() == 0) return;
+    const int k = job_live_[0] ? 1 : 0;
+    // the finalize arenas are one set per engine: one tick with finalize work at a time
+    const bool fin_ok = !(job_live_[k ^ 1] && !job_[k ^ 1].fin.empty());
+    HostEngine::Job& j = job_[k];
+    j.created = (int64_t)time(nullptr);
+    j.lane = 0;
+    if (!eng_->job_take(j, fin_ok)) return;
+    job_t_post_[k] = now_s();
+    eng_->job_prepare(j);
+    eng_->job_post(j);
+    job_live_[k] = true;
+    ++jobs_live_;
+    if (heng_->job_ready(j)) finish_job(k);  // nothing went to the GPU (host-path streams only)
+  }
+  void finish_job(int k) {
     ResultBatch rb;
     taken_.clear();
-    eng_->job_complete(job_, rb.r, rb.f);
-    eng_->job_finish(job_, rb.r, taken_);
-    job_live_ = false;
+    HostEngine::Job& j = job_[k];
+    eng_->job_complete(j, rb.r, rb.f);
+    eng_->job_finish(j, rb.r, taken_);
+    job_live_[k] = false;
+    --jobs_live_;
     eng_->settle(taken_);
-    h_tick.observe(now_s() - job_t_post_);
-    if (ver_) ver_->check(job_.created, rb.r, rb.f);
+    h_tick.observe(now_s() - job_t_post_[k]);
+    if (ver_) ver_->check(j.created, rb.r, rb.f);
     c_ticks++;
     c_tick_slots += rb.r.size();
     apply(rb);
@@ -2884,9 +2906,14 @@ class Loop {
   HipGrid* grid_ = nullptr;          // loop ticks: the shared multi-door grid
   HipEngine* heng_ = nullptr;        // loop ticks: eng_ as this loop's HIP engine
   int loop_slots_ = 0;
-  HostEngine::Job job_;              // loop ticks: the tick this loop has on the GPU
-  bool job_live_ = false;
-  double job_t_post_ = 0;
+  HostEngine::Job job_[2];           // loop ticks: the ticks this loop has on the GPU
+  bool job_live_[2] = {false, false};
+  int jobs_live_ = 0;
+  double job_t_post_[2] = {0, 0};
+  const int loop_doors_ = [] {  // QMX_LOOP_INFLIGHT: ticks in flight per loop (1 or 2)
+    const char* e = env_get("QMX_LOOP_INFLIGHT");
+    return e ? std::min(std::max(atoi(e), 1), 2) : 2;
+  }();
   std::vector<int> taken_;
   const int poll_us_ = [] {
     const char* e = env_get("QMX_LOOP_POLL_US");
@@ -3015,13 +3042,20 @@ int run_server(const ServerCfg& cfg0) {
   const bool spread = cfg.world > 1 && cfg.placement == "spread";
   // hip: loop ticks unless asked for lanes (tick_mode / an explicit shared engine) or sessions
   // spread across ranks (remote texts land in the content arena outside the grid's protocol)
-  const bool loop_ticks = hip && !spread && cfg.tick_mode != "lanes" && cfg.shared_engine != 1;
+  // ... or ranks sharing one GPU (rehearsals): a grid that never idles out needs all of its
+  // workgroups resident, which several processes' grids on one device cannot all be
+  const char* sharers = env_get("QMX_GPU_SHARERS");
+  const bool shared_gpu = sharers && atoi(sharers) > 1;
+  const bool loop_ticks = hip && !spread && !shared_gpu && cfg.tick_mode != "lanes" && cfg.shared_engine != 1;
   const bool shared = !loop_ticks && (cfg.shared_engine < 0 ? hip : cfg.shared_engine > 0);
   if (shared) hub.reset(new GpuHub(cfg, (int)loops.size()));
   if (loop_ticks) {
     const char* w = env_get("QMX_GRID_WPD");
     const char* im = env_get("QMX_PERSISTENT_IDLE_MS");
-    grid.reset(new HipGrid(cfg.device, (int)loops.size(), w ? std::max(1, atoi(w)) : 8, im ? atoi(im) : 50));
+    const char* fl = env_get("QMX_LOOP_INFLIGHT");
+    const int per_loop = fl ? std::min(std::max(atoi(fl), 1), 2) : 2;  // doors per loop (as Loop::loop_doors_)
+    grid.reset(new HipGrid(cfg.device, (int)loops.size() * per_loop, w ? std::max(1, atoi(w)) : 8,
+                           im ? atoi(im) : 50));
   }
   for (auto& l : loops) {
     l->attach_loops(&loop_ptrs);

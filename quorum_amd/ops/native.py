@@ -70,7 +70,7 @@ class NativeEngine:
 
     def __init__(self, kind: str, tags: Sequence[str], device: Optional[int] = None,
                  tile_bytes: int = 16384, max_slots: int = 8192, content_cap: int = 1 << 20, lanes: int = 1,
-                 grid=None, door: int = -1):
+                 grid=None, door: int = -1, ndoors: int = 1):
         ext = require()
         self.kind = kind
         self.name = kind
@@ -86,7 +86,7 @@ class NativeEngine:
             if device is None:
                 device = int(os.environ.get("LOCAL_RANK", "0")) % max(ext.device_count(), 1)
             # grid: a HipGrid (loop ticks) — this engine posts its ticks into door `door` of it
-            self._e = ext.HipEngine(low, device, tile_bytes, max_slots, content_cap, lanes, grid, door)
+            self._e = ext.HipEngine(low, device, tile_bytes, max_slots, content_cap, lanes, grid, door, ndoors)
             self.offload = True
         else:
             self._e = ext.CpuEngine(low)

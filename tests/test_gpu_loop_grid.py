@@ -78,6 +78,20 @@ def test_grid_doors_concurrent_threads(ext):
     grid.stop()
 
 
+def test_grid_two_doors_per_engine(ext):
+    """An engine with two doors (two ticks in flight: buffer sets, kernel parameters and
+    template tables per door) matches the CPU engine; both doors are used."""
+    grid = ext.HipGrid(0, 4, 4)
+    tags = ["think", "reason", "reasoning", "thought"]
+    for seed in range(8):
+        tags_, streams, filt, emit, tseed = _case(900 + seed, 10)
+        cpu = H.run_engine(NativeEngine("cpu", tags_), streams, filt, emit, random.Random(tseed))
+        eng = NativeEngine("hip", tags, device=0, max_slots=256, grid=grid, door=2 * (seed % 2), ndoors=2)
+        got = H.run_engine(eng, streams, filt, emit, random.Random(tseed))
+        assert got == cpu, seed
+    grid.stop()
+
+
 def test_grid_idle_stop_and_relaunch(ext):
     """The host stops an idle grid (stop ticks on every door) and the next post relaunches it
     from where each door's relay left off."""

@@ -492,6 +492,19 @@ def test_native_config_tag_rules():
         native_config(cfg_parallel(2, block=dict(CONCAT, thinking_tags=["think", "th.nk"])), "127.0.0.1", 1, "cpu", 0, 1)
 
 
+def test_native_config_tick_mode(monkeypatch):
+    """runtime.tick_mode reaches the native server (YAML, then QMX_TICK_MODE over it); a
+    server with the cpu engine ignores it and still serves."""
+    from quorum_amd.runtime.native_server import native_config
+
+    cfg = cfg_parallel(2, block=dict(CONCAT))
+    assert native_config(cfg, "127.0.0.1", 1, "cpu", 0, 1)["tick_mode"] == "auto"
+    cfg["runtime"] = {"tick_mode": "lanes"}
+    assert native_config(cfg, "127.0.0.1", 1, "cpu", 0, 1)["tick_mode"] == "lanes"
+    monkeypatch.setenv("QMX_TICK_MODE", "loops")
+    assert native_config(cfg, "127.0.0.1", 1, "cpu", 0, 1)["tick_mode"] == "loops"
+
+
 def test_native_serves_fastapi_doc_routes():
     """FastAPI's default documentation routes of the reference app (oai_proxy.py:70)."""
     from quorum_amd.server.app import create_app

@@ -104,8 +104,9 @@ for step in "$@"; do
         bench ref_$SC 600 QMX_NOP=1 -- --impl reference --scenario $SC --steps 5 --warmup 1 --batch 32 || exit 1
       done ;;
     prof)
-      # one-shot launches: a persistent grid is one long dispatch per lane, no per-tick kernel stats
-      QMX_PERSISTENT=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o native --output-format csv -- \
+      # one-shot launches (tick lanes, QMX_PERSISTENT=0): a persistent grid — the loop-tick grid
+      # or a lane's — is one long dispatch, with no per-tick kernel stats
+      QMX_TICK_MODE=lanes QMX_PERSISTENT=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o native --output-format csv -- \
         python3 bench.py --steps 5 --warmup 1 > $OUT/bench_prof.json 2> $OUT/bench_prof.err \
         || { echo "prof failed"; tail -10 $OUT/bench_prof.err; exit 1; }
       summ prof $OUT/bench_prof.json
