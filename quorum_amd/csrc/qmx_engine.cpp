@@ -579,3 +579,68 @@ void CpuEngine::run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin,
 }
 
 }  // namespace qmx
+
+namespace qmx {
+
+struct AsyncCpuEngine::Done {
+  std::vector<SlotResult> results;
+  std::vector<FinalizeRes> fres;
+  std::atomic<bool> ready{false};
+};
+
+AsyncCpuEngine::AsyncCpuEngine(const std::vector<std::string>& tags) : CpuEngine(tags) {
+  th_ = std::thread([this] { run(); });
+}
+
+AsyncCpuEngine::~AsyncCpuEngine() {
+  {
+    std::lock_guard<std::mutex> g(qmu_);
+    stop_ = true;
+  }
+  qcv_.notify_all();
+  if (th_.joinable()) th_.join();
+}
+
+void AsyncCpuEngine::job_post(Job& j) {
+  auto d = std::make_shared<Done>();
+  j.impl = d;
+  inflight_.fetch_add(1, std::memory_order_acq_rel);
+  {
+    std::lock_guard<std::mutex> g(qmu_);
+    q_.push_back(&j);
+  }
+  qcv_.notify_one();
+}
+
+void AsyncCpuEngine::run() {
+  for (;;) {
+    Job* j = nullptr;
+    {
+      std::unique_lock<std::mutex> lk(qmu_);
+      qcv_.wait(lk, [this] { return stop_ || !q_.empty(); });
+      if (q_.empty()) return;  // stopping with nothing queued
+      j = q_.front();
+      q_.erase(q_.begin());
+    }
+    auto d = std::static_pointer_cast<Done>(j->impl);
+    run_tick(j->work, j->fin, j->created, d->results, d->fres, 0);
+    d->ready.store(true, std::memory_order_release);
+  }
+}
+
+bool AsyncCpuEngine::job_ready(Job& j, double* expect_us) {
+  if (expect_us) *expect_us = 5.0;
+  auto d = std::static_pointer_cast<Done>(j.impl);
+  return !d || d->ready.load(std::memory_order_acquire);
+}
+
+void AsyncCpuEngine::job_complete(Job& j, std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres) {
+  auto d = std::static_pointer_cast<Done>(j.impl);
+  if (!d) return;  // never posted
+  for (auto& r : d->results) results.push_back(std::move(r));
+  for (auto& f : d->fres) fres.push_back(std::move(f));
+  j.impl.reset();
+  inflight_.fetch_sub(1, std::memory_order_acq_rel);
+}
+
+}  // namespace qmx

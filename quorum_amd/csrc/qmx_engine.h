@@ -12,7 +12,9 @@
 #include <stdint.h>
 
 #include <atomic>
+#include <condition_variable>
 #include <memory>
+#include <thread>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -213,6 +215,15 @@ class HostEngine {
   virtual void job_wait_near(Job&) {}
   virtual void job_complete(Job&, std::vector<SlotResult>&, std::vector<FinalizeRes>&) {}
   void job_finish(Job& j, std::vector<SlotResult>& results, std::vector<int>& taken);
+  // Loop ticks (an io loop drives its own jobs, at most free_doors() posted at once): has a
+  // posted job completed?  Never blocks; expect_us: its expected remaining time.  Engines
+  // that run jobs synchronously (in job_complete) are always ready.
+  virtual bool async_jobs() const { return false; }
+  virtual bool job_ready(Job&, double* expect_us = nullptr) {
+    if (expect_us) *expect_us = 0;
+    return true;
+  }
+  virtual int free_doors() const { return 1; }
   virtual std::string text(int slot);
   virtual std::unordered_map<std::string, double> stats();
   // Spread placement (qmx_exchange.h): a stream whose final text another rank produced.
@@ -279,6 +290,32 @@ class CpuEngine : public HostEngine {
  protected:
   void run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin, int64_t created,
                 std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres, int lane) override;
+};
+
+// The loop-tick protocol on the CPU (tick_mode "loops" with the cpu engine): a posted job
+// runs on the engine's worker thread while the io loop keeps serving, which polls
+// job_ready() exactly as with HipEngine's grid doors.  Exercises the io loops' asynchronous
+// tick path (two jobs in flight, completion in any order, finalize on one of them) in the
+// CPU and TSan suites, where no GPU is.
+class AsyncCpuEngine : public CpuEngine {
+ public:
+  explicit AsyncCpuEngine(const std::vector<std::string>& tags);
+  ~AsyncCpuEngine() override;
+  bool async_jobs() const override { return true; }
+  void job_post(Job& j) override;
+  bool job_ready(Job& j, double* expect_us = nullptr) override;
+  void job_complete(Job& j, std::vector<SlotResult>& results, std::vector<FinalizeRes>& fres) override;
+  int free_doors() const override { return 2 - inflight_.load(std::memory_order_acquire); }
+
+ private:
+  struct Done;
+  void run();
+  std::mutex qmu_;
+  std::condition_variable qcv_;
+  std::vector<Job*> q_;
+  bool stop_ = false;
+  std::atomic<int> inflight_{0};
+  std::thread th_;
 };
 
 // Shared by both engines' host-side finalisation.

@@ -269,9 +269,10 @@ class HipEngine : public HostEngine {
   ~HipEngine() override;
   // loop-tick mode (the io loop drives its own ticks): has the posted job's every result been
   // published?  Never blocks.  expect_us: the job's expected remaining time (poll timing).
-  bool job_ready(Job& j, double* expect_us = nullptr);
+  bool job_ready(Job& j, double* expect_us = nullptr) override;
+  bool async_jobs() const override { return grid_ != nullptr; }
   // loop-tick mode: doors of this engine with no tick on them (a job may be prepared + posted)
-  int free_doors() const;
+  int free_doors() const override;
   std::string text(int slot) override;
   void* content_device_ptr(int slot, size_t* cap) override;
   size_t content_size(int slot) override;

@@ -883,7 +883,7 @@ class Loop {
     while (!g_stop.load()) {
       // inline engine with work queued by the last iteration (e.g. a finalize submitted
       // while applying tick results): poll instead of sleeping
-      int to = (!hub_ && !heng_ && kick_) ? 0 : deferq_.empty() ? 50 : 1;
+      int to = (!hub_ && !aeng_ && kick_) ? 0 : deferq_.empty() ? 50 : 1;
       if (lazy_wake_ && hub_) {
         in_wait_.store(true, std::memory_order_seq_cst);
         if (rq_pending_.load(std::memory_order_seq_cst)) to = 0;  // a batch came in: do not sleep
@@ -897,7 +897,7 @@ class Loop {
         for (int k = 0; k < 2 && !ready; ++k) {
           double e = 0;
           if (!job_live_[k]) continue;
-          ready = heng_->job_ready(job_[k], &e);
+          ready = aeng_->job_ready(job_[k], &e);
           exp_us = std::min(exp_us, e);
         }
         if (ready) {
@@ -926,11 +926,11 @@ class Loop {
         if ((i & 7) == 7 && jobs_live_ && any_ready()) loop_tick();
       }
       if (g_drain.load() && drain_step()) break;
-      if ((hub_ || heng_) && early_flush_) {
+      if ((hub_ || aeng_) && early_flush_) {
         // upstream bytes to the tick lanes and finished responses to their clients before
         // this iteration's new requests (whose parsing and upstream sends are the slow part)
         flush_ops();
-        if (heng_) {
+        if (aeng_) {
           loop_tick();
         } else if (kick_) {
           kick_ = false;
@@ -953,9 +953,21 @@ class Loop {
         last_sweep = t;
         snapshot();  // own CPU engine (the GPU hub snapshots the shared HIP engine)
         if (grid_) grid_->housekeep();  // the shared grid's heartbeat / idle stop
+        // a tick that never completes: relaunch a grid that left on its own; after 10 s the
+        // streams' bytes are in an unknown state — exit (the supervisor restarts the worker)
+        for (int k = 0; k < 2 && jobs_live_; ++k) {
+          if (!job_live_[k] || t - job_t_post_[k] < 0.2) continue;
+          if (grid_) grid_->revive_if_exited();
+          if (t - job_t_post_[k] > 10.0) {
+            fprintf(stderr, "qmx: io loop %d: a tick posted %.1f s ago never completed — exiting\n", idx_,
+                    t - job_t_post_[k]);
+            fflush(stderr);
+            _exit(70);
+          }
+        }
       }
       flush_ops();
-      if (heng_) {
+      if (aeng_) {
         loop_tick();
       } else if (!hub_) {
         if (kick_ || eng_->has_work()) {
@@ -975,7 +987,7 @@ class Loop {
     // ticks still on the GPU complete before the engine (and its arenas) can go
     for (int w = 0; jobs_live_ && w < 200000; ++w) {
       for (int k = 0; k < 2; ++k)
-        if (job_live_[k] && heng_->job_ready(job_[k])) finish_job(k);
+        if (job_live_[k] && aeng_->job_ready(job_[k])) finish_job(k);
       if (jobs_live_) std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
   }
@@ -1035,7 +1047,13 @@ class Loop {
         heng_ = new HipEngine(cfg_.tags, cfg_.device, cfg_.tile, per, cfg_.content_cap, 1, grid_,
                               idx_ * loop_doors_, loop_doors_);
         eng_.reset(heng_);
+        aeng_ = heng_;
         loop_slots_ = per;
+      } else if (cfg_.tick_mode == "loops") {
+        // the loop-tick protocol on the CPU: jobs run on the engine's worker thread while the
+        // loop polls for them (tests / TSan of the io loops' asynchronous tick path)
+        aeng_ = new AsyncCpuEngine(cfg_.tags);
+        eng_.reset(aeng_);
       } else {
         eng_.reset(new CpuEngine(cfg_.tags));
       }
@@ -1090,19 +1108,19 @@ class Loop {
   // its results are applied, so its own ticks stay in order).
   bool any_ready() {
     for (int k = 0; k < 2; ++k)
-      if (job_live_[k] && heng_->job_ready(job_[k])) return true;
+      if (job_live_[k] && aeng_->job_ready(job_[k])) return true;
     return false;
   }
   void loop_tick() {
     bool applied = false;
     for (int k = 0; k < 2; ++k)
-      if (job_live_[k] && heng_->job_ready(job_[k])) {
+      if (job_live_[k] && aeng_->job_ready(job_[k])) {
         finish_job(k);
         applied = true;
       }
     if (applied) flush_ops();  // releases queued while applying the results
     kick_ = false;
-    if (heng_->free_doors() == 0) return;
+    if (aeng_->free_doors() == 0) return;
     const int k = job_live_[0] ? 1 : 0;
     // the finalize arenas are one set per engine: one tick with finalize work at a time
     const bool fin_ok = !(job_live_[k ^ 1] && !job_[k ^ 1].fin.empty());
@@ -1115,7 +1133,7 @@ class Loop {
     eng_->job_post(j);
     job_live_[k] = true;
     ++jobs_live_;
-    if (heng_->job_ready(j)) finish_job(k);  // nothing went to the GPU (host-path streams only)
+    if (aeng_->job_ready(j)) finish_job(k);  // nothing went to the GPU (host-path streams only)
   }
   void finish_job(int k) {
     ResultBatch rb;
@@ -2905,6 +2923,7 @@ class Loop {
   GpuHub* hub_ = nullptr;            // shared HIP engine
   HipGrid* grid_ = nullptr;          // loop ticks: the shared multi-door grid
   HipEngine* heng_ = nullptr;        // loop ticks: eng_ as this loop's HIP engine
+  HostEngine* aeng_ = nullptr;       // loop ticks: eng_, driven asynchronously (HIP grid / AsyncCpuEngine)
   int loop_slots_ = 0;
   HostEngine::Job job_[2];           // loop ticks: the ticks this loop has on the GPU
   bool job_live_[2] = {false, false};

@@ -136,12 +136,14 @@ class LiveUpstream:
 @contextlib.contextmanager
 def native_server(cfg: Dict[str, Any], engine: str = "cpu", threads: int = 1, env_key: str = "",
                   verify: bool = False, shared: Optional[bool] = None, lanes: Optional[int] = None,
-                  key_from_env: bool = False):
+                  key_from_env: bool = False, tick_mode: Optional[str] = None):
     """Run the C++ data plane in-process (background thread) for one config.
 
     verify: run the shadow CPU-oracle engine (server_counters()['verify_mismatches']).
     shared: one engine per process shared by all io loops (None = the config's default).
-    lanes: tick lanes of the shared engine (None = the config's default)."""
+    lanes: tick lanes of the shared engine (None = the config's default).
+    tick_mode: "loops" runs the io loops' asynchronous tick path (with the cpu engine: each
+    loop's jobs on an engine worker thread, polled by the loop as a GPU grid's doors are)."""
     import http.client
     import os
 
@@ -159,6 +161,8 @@ def native_server(cfg: Dict[str, Any], engine: str = "cpu", threads: int = 1, en
         d["shared_engine"] = int(shared)
     if lanes is not None:
         d["tick_lanes"] = int(lanes)
+    if tick_mode is not None:
+        d["tick_mode"] = tick_mode
     th = threading.Thread(target=ext.run_server, args=(d,), daemon=True)
     th.start()
     t0 = time.time()

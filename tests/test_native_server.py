@@ -207,7 +207,7 @@ def _python_side(cfg, ups, req, hdrs):
     return _normalize(r.status_code, r.headers.get("content-type"), r.content), fu.calls
 
 
-def _native_side(cfg, ups, req, hdrs):
+def _native_side(cfg, ups, req, hdrs, tick_mode=None):
     live = LiveUpstream()
     cfg = copy.deepcopy(cfg)
     try:
@@ -216,18 +216,20 @@ def _native_side(cfg, ups, req, hdrs):
             if host and host in ups:
                 port = live.serve(host, ups[host])
                 b["url"] = f"http://127.0.0.1:{port}/v1"
-        with native_server(cfg, engine=ENGINE, verify=VERIFY) as port:
+        with native_server(cfg, engine=ENGINE, verify=VERIFY, tick_mode=tick_mode) as port:
             r = httpx.post(f"http://127.0.0.1:{port}/chat/completions", json=req, headers=hdrs, timeout=30)
             return _normalize(r.status_code, r.headers.get("content-type"), r.content), live.calls
     finally:
         live.close()
 
 
+@pytest.mark.parametrize("tick_mode", [None, "loops"])
 @pytest.mark.parametrize("name", sorted(SCENARIOS))
-def test_native_matches_python(name):
+def test_native_matches_python(name, tick_mode):
+    """tick_mode "loops": the io loops' asynchronous tick path (jobs polled, two in flight)."""
     cfg, ups, req, hdrs = SCENARIOS[name]
     py, py_calls = _python_side(cfg, ups, req, hdrs)
-    nat, nat_calls = _native_side(cfg, ups, req, hdrs)
+    nat, nat_calls = _native_side(cfg, ups, req, hdrs, tick_mode)
     if py[1] == "text/event-stream" and py[0] == 200:
         # backends interleave differently; compare per-backend streams + the tail
         def per(evs):
@@ -378,6 +380,47 @@ def test_native_shared_engine_many_loops(threads, lanes):
         live.close()
     after = ext.server_counters()
     assert after["verify_checked"] - before["verify_checked"] >= 48 * 3
+    assert after["verify_mismatches"] == before["verify_mismatches"]
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_native_loop_ticks_many_loops(threads):
+    """Loop ticks on the CPU (tick_mode "loops" with the cpu engine: every io loop posts its
+    jobs to its engine's worker and polls them, two in flight): concurrent sessions, streaming
+    concatenate and the aggregate strategy (finalize rides one of the two jobs), every result
+    checked by the shadow oracle and equal to the inline engine's."""
+    import concurrent.futures as cf
+
+    ext = native.require()
+    before = ext.server_counters()
+    live = LiveUpstream()
+    p1 = live.serve("b1", ("stream", 200, THINK))
+    p2 = live.serve("b2", ("stream", 200, sse_stream(["Wor", "ld <think>x</think>", " é😀"])))
+    try:
+        for strategy in ("concatenate", "aggregate"):
+            cfg = cfg_parallel(2, block=dict(CONCAT, hide_final_think=True))
+            cfg["primary_backends"][0]["url"] = f"http://127.0.0.1:{p1}/v1"
+            cfg["primary_backends"][1]["url"] = f"http://127.0.0.1:{p2}/v1"
+            if strategy == "aggregate":
+                cfg["iterations"] = {"aggregation": {"strategy": "aggregate"}}
+                cfg["strategy"]["aggregate"] = dict(CONCAT, aggregator_backend="LLM2", skip_final_aggregation=False)
+            req = {"messages": MSG, "stream": True}
+            with native_server(cfg) as port:
+                ref = _norm_sse(httpx.post(f"http://127.0.0.1:{port}/chat/completions", json=req, headers=AUTH,
+                                           timeout=30).text)
+            with native_server(cfg, threads=threads, verify=True, tick_mode="loops") as port:
+                def one(_):
+                    with httpx.Client(base_url=f"http://127.0.0.1:{port}") as cl:
+                        return [_norm_sse(cl.post("/chat/completions", json=req, headers=AUTH, timeout=30).text)
+                                for _ in range(6)]
+                with cf.ThreadPoolExecutor(8) as ex:
+                    for res in ex.map(one, range(8)):
+                        for r in res:
+                            assert _per_stream(r) == _per_stream(ref), strategy
+    finally:
+        live.close()
+    after = ext.server_counters()
+    assert after["verify_checked"] - before["verify_checked"] >= 2 * 48 * 2
     assert after["verify_mismatches"] == before["verify_mismatches"]
 
 

@@ -152,10 +152,13 @@ def test_server_asan_traffic(san_bins, tmp_path):
     assert not errs, errs
 
 
-def test_server_tsan_shared_engine_lanes(tmp_path):
-    """ThreadSanitizer build of the data plane: 4 io loops share one engine with 3 tick lanes
-    (the GPU-hub topology, CPU engine) plus the verify shadow, under concurrent clients with
-    aborting and failing backends.  Any data race report fails the test."""
+@pytest.mark.parametrize("mode", ["lanes", "loops"])
+def test_server_tsan_shared_engine_lanes(tmp_path, mode):
+    """ThreadSanitizer build of the data plane under concurrent clients with aborting and
+    failing backends, plus the verify shadow.  lanes: 4 io loops share one engine with 3 tick
+    lanes (the GPU-hub topology, CPU engine).  loops: the loop-tick protocol — every io loop
+    posts its jobs to its own engine's worker thread and polls them, two in flight (the grid
+    doors' pattern, AsyncCpuEngine).  Any data race report fails the test."""
     import concurrent.futures as cf
 
     from quorum_amd.ops import build
@@ -175,7 +178,11 @@ def test_server_tsan_shared_engine_lanes(tmp_path):
         b["url"] = u
     port = free_port()
     d = native_config(cfg, "127.0.0.1", port, "cpu", 0, 4)
-    d.update(env_api_key="", api_key_from_env=False, shared_engine=1, tick_lanes=3, verify=True)
+    d.update(env_api_key="", api_key_from_env=False, verify=True)
+    if mode == "lanes":
+        d.update(shared_engine=1, tick_lanes=3)
+    else:
+        d.update(tick_mode="loops")
     path = tmp_path / "tsan.json"
     path.write_text(json.dumps(d))
     # pipelined lanes on (QMX_PIPELINE=1): the next tick is taken while the current one runs;

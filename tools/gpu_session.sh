@@ -95,7 +95,7 @@ for step in "$@"; do
       bench ab_$name 300 ${envs//,/ } -- ${a//,/ } || exit 1 ;;
     scenarios)
       for SC in aggregate4 highqps8 failure paced; do
-        bench sc_$SC 300 QMX_NOP=1 -- --scenario $SC --steps 10 --warmup 2 || exit 1
+        bench sc_$SC 300 QMX_NOP=1 -- --scenario $SC --steps 10 --warmup 2 $( [ $SC = paced ] || echo --batch 16384 ) || exit 1
       done ;;
     reference)
       bench reference 600 QMX_NOP=1 -- --impl reference --steps 10 --warmup 1 --batch 64 || exit 1 ;;
