@@ -154,10 +154,17 @@ class HipGrid {
   bool revive_if_exited();
   void stop();
   std::unordered_map<std::string, double> stats();
+  // host steady clock (us) minus the device's s_memrealtime clock (us), from the quickest of
+  // a few doorbell round trips; NaN before the first calibration
+  double clock_offset_us() const { return clk_off_us_.load(std::memory_order_relaxed); }
 
  private:
   void launch_locked();
   void stop_locked();
+  void calibrate_locked();
+  std::atomic<double> clk_off_us_{__builtin_nan("")};
+  bool interleave_ = true;  // doors' sub-grids XCD-local (blocks d, d + doors, ...)
+  double clk_rtt_us_ = 0, last_cal_ = 0;
   int device_, n_, wpd_, idle_ms_;
   std::shared_mutex mu_;
   std::atomic<bool> running_{false};
@@ -249,6 +256,7 @@ struct TickLane {
   double ema_us = 40.0;  // launch-to-results time, smoothed
   double span_ema_us = 30.0;  // kernel span per tick (device clock), smoothed: pipelined lanes
   double lead_ema_us = 8.0;   // persistent: doorbell seen -> first item started (device clock), smoothed
+  double post_seen_us = 0, done_host_us = 0, hop_ticks = 0;  // loop ticks: host <-> device hops (calibrated)
   bool timing_pending = false;
   uint64_t poll_fallbacks = 0;
   // persistent mode (QMX_PERSISTENT=1): the lane's long-lived grid and its doorbell

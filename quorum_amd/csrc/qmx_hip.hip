@@ -2249,14 +2249,19 @@ static_assert(offsetof(PDoor, beat) == offsetof(PDoor, posted) + 4, "posted + be
 // loads: a readonly noalias kernel argument may be read through the scalar cache, which no
 // acquire fence invalidates — the next tick's descriptor would come back stale.
 __global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* doors, PCtl* ctls, int wpd, uint32_t gen,
-                                                          uint32_t idle_ticks) {
+                                                          uint32_t idle_ticks, int interleave) {
   __shared__ TickLds U;
   __shared__ TickDesc D;
   __shared__ uint32_t cmd;  // new tick's sequence number, 0: exit
-  // sub-grid blockIdx.x / wpd serves door blockIdx.x / wpd; its first workgroup is the relay
-  PDoor* const door = doors + blockIdx.x / wpd;
-  PCtl* const ctl = ctls + blockIdx.x / wpd;
-  const bool relay = blockIdx.x % wpd == 0;
+  // door of this workgroup: blocks [d·wpd, (d+1)·wpd) — or, interleaved, blocks d, d + ndoors,
+  // d + 2·ndoors, ...: the dispatcher deals block b to XCD b % 8, so with a multiple of 8
+  // doors every door's sub-grid (and, tick after tick, its io loop's slot state, templates and
+  // content tails) stays in ONE XCD's L2.  The door's first workgroup is its relay.
+  const int ndoors = (int)gridDim.x / wpd;
+  const int di = interleave ? (int)blockIdx.x % ndoors : (int)blockIdx.x / wpd;
+  PDoor* const door = doors + di;
+  PCtl* const ctl = ctls + di;
+  const bool relay = interleave ? (int)blockIdx.x < ndoors : blockIdx.x % wpd == 0;
   constexpr int kWords = (int)(sizeof(TickDesc) / 4);
   static_assert(kWords <= 64, "the descriptor is copied by one wave, a word per lane");
   const int tid = threadIdx.x;
@@ -2474,7 +2479,7 @@ void HipEngine::wait_results(TickLane& L, int n, int m, uint32_t seq, const Work
         HIP_CHECK(hipStreamSynchronize(L.stream));  // the idle grid has left
         L.h_door->base = seq0;
         hipLaunchKernelGGL(qmx_tick_persistent, dim3(p_grid_), dim3(BS), 0, L.stream, L.h_door, L.d_ctl, p_grid_,
-                           ++L.p_gen, (uint32_t)p_idle_ms_ * 100000u);
+                           ++L.p_gen, (uint32_t)p_idle_ms_ * 100000u, 0);
         HIP_CHECK(hipGetLastError());
         L.p_last_post = steady_s();
         ++L.p_launches;
@@ -2718,7 +2723,7 @@ void HipEngine::ensure_persistent(TickLane& L) {
   if (L.p_running) return;
   L.h_door->base = L.seq;  // the value posted last before this launch
   hipLaunchKernelGGL(qmx_tick_persistent, dim3(p_grid_), dim3(BS), 0, L.stream, L.h_door, L.d_ctl, p_grid_,
-                     ++L.p_gen, (uint32_t)p_idle_ms_ * 100000u);
+                     ++L.p_gen, (uint32_t)p_idle_ms_ * 100000u, 0);
   HIP_CHECK(hipGetLastError());
   L.p_running = true;
   L.p_last_post = steady_s();
@@ -3229,6 +3234,17 @@ void HipEngine::complete(HipJob& J, std::vector<SlotResult>& results, std::vecto
         const uint64_t tr = __atomic_load_n(&dr->t_relayed, __ATOMIC_ACQUIRE);
         if (ts && tr >= ts && a >= tr && b >= a) {
           L.lead_ema_us = 0.85 * L.lead_ema_us + 0.15 * std::min((double)(a - ts) * 1e-2, 500.0);
+          const double off = grid_ ? grid_->clock_offset_us() : __builtin_nan("");
+          if (off == off) {  // calibrated: the hops between the two clocks
+            const double post_h = std::chrono::duration<double, std::micro>(J.tp1.time_since_epoch()).count();
+            const double seen_h = (double)ts * 1e-2 + off, done_h = (double)b * 1e-2 + off;
+            const double now_h = std::chrono::duration<double, std::micro>(HC::now().time_since_epoch()).count();
+            if (seen_h >= post_h - 5.0 && now_h >= done_h - 5.0) {
+              L.post_seen_us += seen_h - post_h;
+              L.done_host_us += now_h - done_h;
+              ++L.hop_ticks;
+            }
+          }
           L.relay_us += (double)(tr - ts) * 1e-2;
           L.pickup_us += (double)(a - tr) * 1e-2;
           L.grid_span_us += (double)(b - ts) * 1e-2;
@@ -3529,6 +3545,9 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["pickup_us"] += L.pickup_us;
     m["grid_span_us"] += L.grid_span_us;
     m["grid_ticks"] += L.grid_ticks;
+    m["post_seen_us"] += L.post_seen_us;  // loop ticks: host post -> relay saw it (calibrated clocks)
+    m["done_host_us"] += L.done_host_us;  // last item done -> the io loop took the results
+    m["hop_ticks"] += L.hop_ticks;
     m["start_spread_us"] += L.start_spread_us;
     m["process_us"] += L.process_us;
     m["poll_fallbacks"] += (double)L.poll_fallbacks;
@@ -3559,6 +3578,9 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
 // ---- the multi-door grid (loop ticks) ----------------------------------------------------
 HipGrid::HipGrid(int device, int doors, int wg_per_door, int idle_ms)
     : device_(device), n_(std::max(1, doors)), wpd_(std::max(1, wg_per_door)), idle_ms_(std::max(5, idle_ms)) {
+  // XCD-local sub-grids (QMX_GRID_XCD=0: contiguous blocks per door, every door on all XCDs)
+  const char* x = env_get("QMX_GRID_XCD");
+  interleave_ = (x ? atoi(x) != 0 : true) && n_ % 8 == 0;
   HIP_CHECK(hipSetDevice(device_));
   HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   HIP_CHECK(hipHostMalloc((void**)&h_doors_, sizeof(PDoor) * (size_t)n_, hipHostMallocMapped));
@@ -3601,11 +3623,43 @@ void HipGrid::launch_locked() {
   for (int d = 0; d < n_; ++d) h_doors_[d].base = __atomic_load_n(&h_doors_[d].relayed, __ATOMIC_ACQUIRE);
   const uint32_t idle_ticks = 2000u * 100000u;  // 2 s at 100 MHz: only a host that stopped beating
   hipLaunchKernelGGL(qmx_tick_persistent, dim3(n_ * wpd_), dim3(BS), 0, stream_, h_doors_, d_ctls_, wpd_, ++gen_,
-                     idle_ticks);
+                     idle_ticks, interleave_ ? 1 : 0);
   HIP_CHECK(hipGetLastError());
   last_post_.store(steady_s(), std::memory_order_relaxed);
   running_.store(true, std::memory_order_release);
   ++launches_;
+  calibrate_locked();
+}
+
+// Clock calibration (timing only): empty ticks on door 0, each timed on the host from the
+// post to the relay's `relayed` store; the relay stamped s_memrealtime when it saw the post.
+// The quickest round trip bounds the offset best (error <= its half).  Under the exclusive
+// lock: no door is posting.
+void HipGrid::calibrate_locked() {
+  PDoor& D = h_doors_[0];
+  double best = 1e9, off = 0;
+  for (int i = 0; i < 12; ++i) {
+    uint32_t s = D.posted + 1;
+    if (s == 0) s = 1;
+    D.d.n_tick = 0;
+    D.d.n_fin = 0;
+    D.d.stop = 0;
+    D.d.params_src = nullptr;
+    D.d.seq = s;
+    const double h0 = steady_s();
+    __atomic_store_n(&D.posted, s, __ATOMIC_RELEASE);
+    while (__atomic_load_n(&D.relayed, __ATOMIC_ACQUIRE) != s)
+      if (steady_s() - h0 > 0.05) return;  // the grid is not answering: no calibration now
+    const double h1 = steady_s();
+    const double g = (double)__atomic_load_n(&D.t_seen, __ATOMIC_ACQUIRE) * 1e-2;  // 100 MHz -> us
+    if ((h1 - h0) * 1e6 < best) {
+      best = (h1 - h0) * 1e6;
+      off = 0.5 * (h0 + h1) * 1e6 - g;
+    }
+  }
+  clk_off_us_.store(off, std::memory_order_relaxed);
+  clk_rtt_us_ = best;
+  last_cal_ = steady_s();
 }
 
 // Under the exclusive lock (no door is posting): every posted tick relayed, then a stop tick
@@ -3656,6 +3710,13 @@ void HipGrid::housekeep() {
   }
   const uint32_t b = beat_.fetch_add(1, std::memory_order_relaxed) + 1;
   for (int d = 0; d < n_; ++d) __atomic_store_n(&h_doors_[d].beat, b, __ATOMIC_RELAXED);
+  if (steady_s() - last_cal_ > 1.0) {  // the two clocks drift apart by ~us per second
+    std::unique_lock<std::shared_mutex> ex(mu_, std::try_to_lock);
+    if (ex.owns_lock() && running_.load(std::memory_order_relaxed)) {
+      // door 0's tick in flight (if any) must have been relayed: calibration reuses the door
+      if (__atomic_load_n(&h_doors_[0].relayed, __ATOMIC_ACQUIRE) == h_doors_[0].posted) calibrate_locked();
+    }
+  }
 }
 
 bool HipGrid::revive_if_exited() {
@@ -3673,7 +3734,8 @@ bool HipGrid::revive_if_exited() {
 
 std::unordered_map<std::string, double> HipGrid::stats() {
   return {{"grid_launches", (double)launches_.load()}, {"grid_stops", (double)stops_.load()},
-          {"grid_revivals", (double)revivals_.load()}, {"grid_doors", (double)n_}};
+          {"grid_revivals", (double)revivals_.load()}, {"grid_doors", (double)n_},
+          {"grid_clock_rtt_us", clk_rtt_us_}, {"grid_xcd_local", interleave_ ? 1.0 : 0.0}};
 }
 
 }  // namespace qmx

@@ -90,6 +90,7 @@ def test_random_session_native_matches_python(seed):
     cfg, ups, req, hdrs = _scenario(seed)
     T.SCENARIOS[f"_random_{seed}"] = (cfg, ups, req, hdrs)
     try:
-        T.test_native_matches_python(f"_random_{seed}")
+        # odd seeds through the io loops' asynchronous tick path (tick_mode "loops")
+        T.test_native_matches_python(f"_random_{seed}", "loops" if seed % 2 else None)
     finally:
         del T.SCENARIOS[f"_random_{seed}"]
