@@ -757,6 +757,16 @@ struct TickShared {
   HoleTpl htpl[kHoleTpls];  // S3: this item's backend hole templates (previous launch's)
 };
 
+// threadIdx.x as an opaque value: in the persistent grid the tick body sits inside a loop,
+// and the compiler hoists every `tid < k` mask it derives out of that loop — dozens of 64-bit
+// masks live across the whole body, more than the SGPR file holds, spilled into VGPR lanes
+// (v_writelane / v_readlane) and scratch.  Re-deriving a mask costs one v_cmp.
+__device__ __forceinline__ int opaque_tid() {
+  int t;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
+  return t;
+}
+
 __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, const uint8_t* __restrict__ in,
                                           uint8_t* __restrict__ out, WorkResult* __restrict__ res,
                                           DevSlot* __restrict__ state, uint8_t* __restrict__ content,
@@ -767,7 +777,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   auto& TKP = U.TKP;
   auto& TKT = U.TKT;
   auto& wtpl = U.wtpl;
-  const int tid = threadIdx.x;
+  const int tid = opaque_tid();
   // Tiles sit at a fixed stride (item bi at bi x TILE_MAX, HipEngine::prepare), so the first
   // 4 KiB of this item's tile — all of it for a streaming tick or a short response — is
   // requested from host memory together with the work item itself: one PCIe round trip
@@ -1977,7 +1987,7 @@ struct FinArgs {
 
 __device__ __forceinline__ void fin_body(const FinArgs& fa, int j, const uint8_t* __restrict__ content, uint32_t content_cap,
                          const TagSet& ts_mem, FinShared& F) {
-  const int tid = threadIdx.x;
+  const int tid = opaque_tid();
   for (int i = tid; i < (int)(sizeof(TagSet) / 4); i += BS) ((uint32_t*)&F.ts)[i] = ((const uint32_t*)&ts_mem)[i];
   __syncthreads();
   const TagSet& ts = F.ts;
