@@ -777,13 +777,13 @@ def main() -> int:
     device = local_rank % n_dev if n_dev else None
     coll_cuda = use_cuda
     dist = None
+    if use_cuda:  # before the process group: RCCL's barrier picks the current device
+        torch.cuda.set_device(device)
     if world > 1:
         import torch.distributed as dist  # noqa: F811
 
         dist.init_process_group("nccl" if coll_cuda else "gloo")
     _trace("init_process_group")
-    if use_cuda:
-        torch.cuda.set_device(device)
     try:
         pinning = pin_rank(torch, world, local_rank, n_dev)
     except (OSError, RuntimeError, ValueError, AttributeError) as e:  # placement is an optimisation only
