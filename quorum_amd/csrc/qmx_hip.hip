@@ -3588,6 +3588,18 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
 // ---- the multi-door grid (loop ticks) ----------------------------------------------------
 HipGrid::HipGrid(int device, int doors, int wg_per_door, int idle_ms)
     : device_(device), n_(std::max(1, doors)), wpd_(std::max(1, wg_per_door)), idle_ms_(std::max(5, idle_ms)) {
+  // every workgroup of a persistent grid must be resident at once (a relay that is not never
+  // relays its door's ticks), and the tick kernels run one workgroup per CU (LDS, VGPRs):
+  // keep the grid within half the device's CUs — room for a second process's grid during a
+  // rolling reload, and for a partitioned GPU (CPX: 32 CUs per logical device)
+  {
+    hipDeviceProp_t pr{};
+    HIP_CHECK(hipGetDeviceProperties(&pr, device_));
+    const int cus = std::max(1, pr.multiProcessorCount);
+    if (n_ * wpd_ > cus / 2) wpd_ = std::max(1, (cus / 2) / n_);
+    if (n_ * wpd_ > cus) throw std::runtime_error("grid: " + std::to_string(n_) + " doors do not fit " +
+                                                  std::to_string(cus) + " CUs");
+  }
   // XCD-local sub-grids (QMX_GRID_XCD=0: contiguous blocks per door, every door on all XCDs)
   const char* x = env_get("QMX_GRID_XCD");
   interleave_ = (x ? atoi(x) != 0 : true) && n_ % 8 == 0;
@@ -3745,7 +3757,8 @@ bool HipGrid::revive_if_exited() {
 std::unordered_map<std::string, double> HipGrid::stats() {
   return {{"grid_launches", (double)launches_.load()}, {"grid_stops", (double)stops_.load()},
           {"grid_revivals", (double)revivals_.load()}, {"grid_doors", (double)n_},
-          {"grid_clock_rtt_us", clk_rtt_us_}, {"grid_xcd_local", interleave_ ? 1.0 : 0.0}};
+          {"grid_clock_rtt_us", clk_rtt_us_}, {"grid_xcd_local", interleave_ ? 1.0 : 0.0},
+          {"grid_wg_per_door", (double)wpd_}};
 }
 
 }  // namespace qmx

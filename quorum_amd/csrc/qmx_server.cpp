@@ -3073,8 +3073,13 @@ int run_server(const ServerCfg& cfg0) {
     const char* im = env_get("QMX_PERSISTENT_IDLE_MS");
     const char* fl = env_get("QMX_LOOP_INFLIGHT");
     const int per_loop = fl ? std::min(std::max(atoi(fl), 1), 2) : 2;  // doors per loop (as Loop::loop_doors_)
-    grid.reset(new HipGrid(cfg.device, (int)loops.size() * per_loop, w ? std::max(1, atoi(w)) : 8,
-                           im ? atoi(im) : 50));
+    try {
+      grid.reset(new HipGrid(cfg.device, (int)loops.size() * per_loop, w ? std::max(1, atoi(w)) : 8,
+                             im ? atoi(im) : 50));
+    } catch (const std::exception& e) {  // e.g. more io loops than a partitioned GPU has CUs
+      fprintf(stderr, "qmx: loop ticks unavailable (%s) — tick lanes instead\n", e.what());
+      hub.reset(new GpuHub(cfg, (int)loops.size()));
+    }
   }
   for (auto& l : loops) {
     l->attach_loops(&loop_ptrs);

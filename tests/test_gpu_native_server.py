@@ -6,17 +6,19 @@ import test_native_server as T
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("tick_mode", ["loops", "lanes"])
 @pytest.mark.parametrize("name", sorted(T.SCENARIOS))
-def test_native_hip_matches_python(name, monkeypatch):
+def test_native_hip_matches_python(name, tick_mode, monkeypatch):
     """HIP engine + verify mode: every stream and final is also checked against the
-    shadow C++ CPU oracle inside the server (byte-identical or counted as mismatch)."""
+    shadow C++ CPU oracle inside the server (byte-identical or counted as mismatch).
+    loops: io loops post into the multi-door grid (the default); lanes: the shared engine."""
     from quorum_amd.ops import native
 
     ext = native.require()
     before = ext.server_counters()["verify_mismatches"]
     monkeypatch.setattr(T, "ENGINE", "hip")
     monkeypatch.setattr(T, "VERIFY", True)
-    T.test_native_matches_python(name)
+    T.test_native_matches_python(name, tick_mode)
     assert ext.server_counters()["verify_mismatches"] == before
 
 
@@ -42,7 +44,7 @@ def test_native_hip_random_sessions(seed, monkeypatch):
     before = ext.server_counters()["verify_mismatches"]
     monkeypatch.setattr(T, "ENGINE", "hip")
     monkeypatch.setattr(T, "VERIFY", True)
-    R.test_random_session_native_matches_python(seed)
+    R.run_random_session(seed, "loops" if seed % 2 else "lanes")
     assert ext.server_counters()["verify_mismatches"] == before
 
 

@@ -85,12 +85,16 @@ def _scenario(seed):
     return cfg, ups, req, {"Authorization": "Bearer k"}
 
 
-@pytest.mark.parametrize("seed", range(int(os.environ.get("QMX_RANDOM_SEEDS", "40"))))
-def test_random_session_native_matches_python(seed):
+def run_random_session(seed, tick_mode):
     cfg, ups, req, hdrs = _scenario(seed)
     T.SCENARIOS[f"_random_{seed}"] = (cfg, ups, req, hdrs)
     try:
-        # odd seeds through the io loops' asynchronous tick path (tick_mode "loops")
-        T.test_native_matches_python(f"_random_{seed}", "loops" if seed % 2 else None)
+        T.test_native_matches_python(f"_random_{seed}", tick_mode)
     finally:
         del T.SCENARIOS[f"_random_{seed}"]
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("QMX_RANDOM_SEEDS", "40"))))
+def test_random_session_native_matches_python(seed):
+    # odd seeds through the io loops' asynchronous tick path (tick_mode "loops")
+    run_random_session(seed, "loops" if seed % 2 else None)

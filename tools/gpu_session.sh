@@ -22,6 +22,7 @@
 #   multirank=N           bench.py under torch.distributed.run with N ranks sharing GPU 0
 #   spread=N              same, --placement spread over the TCP exchange
 #   cpuprof               headline bench with the in-process CPU profiler on the proxy
+#   probe:NAME            tools/probes/NAME (built beforehand), e.g. probe:doorbell_probe
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -78,6 +79,10 @@ for step in "$@"; do
       timeout -k 10 600 python -u -m pytest ${f//,/ } -x -v --timeout 120 --timeout-method thread \
         > $OUT/pytest_$slug.log 2>&1 || { echo "pytest $f failed"; tail -40 $OUT/pytest_$slug.log; exit 1; }
       tail -3 $OUT/pytest_$slug.log ;;
+    probe:*)  # a probe binary built on the CPU side (tools/probes/<name>), its JSON lines kept
+      pb=${step#probe:}
+      timeout -k 10 120 tools/probes/$pb > $OUT/probe_$pb.jsonl 2>&1 || { echo "probe $pb failed"; tail -5 $OUT/probe_$pb.jsonl; exit 1; }
+      cat $OUT/probe_$pb.jsonl ;;
     fdprobe)  # which bench-rank step opens a GPU device file
       timeout -k 10 120 python tools/probes/fd_probe.py > $OUT/fdprobe.log 2>&1; cat $OUT/fdprobe.log ;;
     smoke)
