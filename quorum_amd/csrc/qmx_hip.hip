@@ -3595,10 +3595,14 @@ HipGrid::HipGrid(int device, int doors, int wg_per_door, int idle_ms)
   {
     hipDeviceProp_t pr{};
     HIP_CHECK(hipGetDeviceProperties(&pr, device_));
-    const int cus = std::max(1, pr.multiProcessorCount);
-    if (n_ * wpd_ > cus / 2) wpd_ = std::max(1, (cus / 2) / n_);
-    if (n_ * wpd_ > cus) throw std::runtime_error("grid: " + std::to_string(n_) + " doors do not fit " +
-                                                  std::to_string(cus) + " CUs");
+    // processes sharing the GPU (rank rehearsals) split that half between their grids
+    const char* sh = env_get("QMX_GPU_SHARERS");
+    const int sharers = sh ? std::max(1, atoi(sh)) : 1;
+    const int cus = std::max(1, pr.multiProcessorCount), budget = cus / 2 / sharers;
+    if (n_ * wpd_ > budget) wpd_ = std::max(1, budget / n_);
+    if (n_ * wpd_ > budget) throw std::runtime_error("grid: " + std::to_string(n_) + " doors do not fit " +
+                                                     std::to_string(cus) + " CUs shared by " +
+                                                     std::to_string(sharers) + " processes");
   }
   // XCD-local sub-grids (QMX_GRID_XCD=0: contiguous blocks per door, every door on all XCDs)
   const char* x = env_get("QMX_GRID_XCD");

@@ -3061,11 +3061,9 @@ int run_server(const ServerCfg& cfg0) {
   const bool spread = cfg.world > 1 && cfg.placement == "spread";
   // hip: loop ticks unless asked for lanes (tick_mode / an explicit shared engine) or sessions
   // spread across ranks (remote texts land in the content arena outside the grid's protocol)
-  // ... or ranks sharing one GPU (rehearsals): a grid that never idles out needs all of its
-  // workgroups resident, which several processes' grids on one device cannot all be
-  const char* sharers = env_get("QMX_GPU_SHARERS");
-  const bool shared_gpu = sharers && atoi(sharers) > 1;
-  const bool loop_ticks = hip && !spread && !shared_gpu && cfg.tick_mode != "lanes" && cfg.shared_engine != 1;
+  // (ranks sharing one GPU — rehearsals — split the grid budget: HipGrid sizes itself from
+  // QMX_GPU_SHARERS, and a grid that does not fit falls back to lanes below)
+  const bool loop_ticks = hip && !spread && cfg.tick_mode != "lanes" && cfg.shared_engine != 1;
   const bool shared = !loop_ticks && (cfg.shared_engine < 0 ? hip : cfg.shared_engine > 0);
   if (shared) hub.reset(new GpuHub(cfg, (int)loops.size()));
   if (loop_ticks) {
