@@ -919,11 +919,16 @@ class Loop {
         if (rq_pending_.load(std::memory_order_acquire)) on_results(false);
       }
       cnt(SC_EPOLL_WAIT);
+      // loop ticks: results published while this loop slept or worked are applied first, and
+      // between every two events of the batch (a look at a few host-memory words): an io loop
+      // is busy most of the time, and a tick's results waiting out a whole event batch were
+      // most of its done -> taken time (tick_hops_us_avg)
+      if (jobs_live_ && any_ready()) loop_tick();
       for (int i = 0; i < n; ++i) {
         dispatch(evs[i]);
         // a long batch: tick results that arrived meanwhile are applied now, not after it
         if ((i & 7) == 7 && early_flush_ && rq_pending_.load(std::memory_order_acquire)) on_results(false);
-        if ((i & 7) == 7 && jobs_live_ && any_ready()) loop_tick();
+        if ((i & 1) == 1 && jobs_live_ && any_ready()) loop_tick();
       }
       if (g_drain.load() && drain_step()) break;
       if ((hub_ || aeng_) && early_flush_) {
