@@ -900,7 +900,8 @@ class Loop {
           ready = aeng_->job_ready(job_[k], &e);
           exp_us = std::min(exp_us, e);
         }
-        if (ready) {
+        if (ready || exp_us <= spin_us_) {
+          // ready, or due within QMX_LOOP_SPIN_US: look again at once (no timer wake-up)
           n = epoll_wait(ep_, evs.data(), (int)evs.size(), 0);
         } else {
           const double us = std::min(std::max(exp_us, (double)poll_us_), 1000.0 * std::max(to, 1));
@@ -2942,6 +2943,12 @@ class Loop {
   const int poll_us_ = [] {
     const char* e = env_get("QMX_LOOP_POLL_US");
     return e ? std::max(1, atoi(e)) : 3;
+  }();
+  // a tick due within this many us is waited for by looking again at once, not by a timer
+  // (a timed wake-up of a sleeping thread costs several us more)
+  const double spin_us_ = [] {
+    const char* e = env_get("QMX_LOOP_SPIN_US");
+    return e ? atof(e) : 0.0;
   }();
   TagSet ts_ = make_tagset(cfg_.tags);
   bool kick_ = false;
