@@ -68,3 +68,48 @@ def test_gpu_bench_headline_valid(tmp_path):
     res = json.loads(lines[-1])
     assert r.returncode == 0 and res["valid"] and res["invalid"] == 0, (res.get("invalid"), r.stderr[-2000:])
     assert res["validated"] == 4 * 8192 and res["breakdown_one_rank"]["kernel_launches"] > 0
+
+
+def _metric(text, name):
+    for ln in text.splitlines():
+        if ln.startswith(name + " "):
+            return float(ln.split()[1])
+    return None
+
+
+@pytest.mark.parametrize("sharers,want_grid", [("1", True), ("16", True), ("64", False)])
+def test_native_hip_grid_sizing(sharers, want_grid, monkeypatch):
+    """The loop-tick grid fits within half the CUs split between the processes sharing the
+    GPU (QMX_GPU_SHARERS, set by rank rehearsals): 16 sharers shrink it to 2 workgroups per
+    door; 64 leave no room and the server falls back to tick lanes — it serves either way."""
+    import time
+
+    import httpx
+
+    from quorum_amd.ops import native
+
+    ext = native.require()
+    monkeypatch.setenv("QMX_GPU_SHARERS", sharers)
+    live = T.LiveUpstream()
+    p1 = live.serve("b1", ("stream", 200, T.THINK))
+    p2 = live.serve("b2", ("stream", 200, T.sse_stream(["Wor", "ld <think>x</think>", " é😀"])))
+    cfg = T.cfg_parallel(2, block=dict(T.CONCAT))
+    cfg["primary_backends"][0]["url"] = f"http://127.0.0.1:{p1}/v1"
+    cfg["primary_backends"][1]["url"] = f"http://127.0.0.1:{p2}/v1"
+    before = ext.server_counters()["verify_mismatches"]
+    try:
+        with T.native_server(cfg, engine="hip", threads=2, verify=True) as port:
+            for _ in range(20):
+                r = httpx.post(f"http://127.0.0.1:{port}/chat/completions", json={"messages": T.MSG, "stream": True},
+                               headers=T.AUTH, timeout=30)
+                assert r.status_code == 200 and r.text.rstrip().endswith("data: [DONE]")
+            time.sleep(0.3)  # an io-loop sweep snapshots the engines' counters
+            m = httpx.get(f"http://127.0.0.1:{port}/metrics").text
+    finally:
+        live.close()
+    assert ext.server_counters()["verify_mismatches"] == before
+    doors, wpd = _metric(m, "qmx_kernel_grid_doors"), _metric(m, "qmx_kernel_grid_wg_per_door")
+    if want_grid:
+        assert doors == 4 and wpd == (2 if sharers == "16" else 8), (doors, wpd)
+    else:
+        assert doors is None and (_metric(m, "qmx_kernel_launches") or 0) > 0
