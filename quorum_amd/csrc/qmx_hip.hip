@@ -378,6 +378,49 @@ __device__ inline bool wave_hole_exact(const uint8_t* x, int e0, int e1, const H
   return true;
 }
 
+// Same-length fast path: an event as long as T whose holes are as long as T's (ids,
+// timestamps and counters of one backend usually are) has every literal run at T's offsets,
+// so one wave-parallel pass decides it — literal bytes equal, string-hole bytes printable
+// ASCII other than '"' and '\\', number-hole bytes digits without a leading zero.  What passes
+// is exactly what wave_hole_match accepts with the same holes (each string body ends at T's
+// closing quote, each number at T's next literal); anything else (escapes, UTF-8, DEL, signs,
+// fractions, other lengths) is left to the walk.  T in LDS; the hole bounds sit one per lane.
+__device__ inline bool wave_hole_samelen(const uint8_t* x, int e0, int e1, const HoleTpl& T, int* sa, int* sb,
+                                         int* body) {
+  const int n = T.len, nh = T.nh;
+  if (n == 0 || nh == 0 || e1 - e0 != n) return false;
+  const int lane = threadIdx.x & 63;
+  const int hs_l = lane < nh ? (int)T.hs[lane] : 0, he_l = lane < nh ? (int)T.he[lane] : 0;
+  const int num_l = lane < nh ? (int)T.num[lane] : 0;
+  bool bad = false;
+  for (int c0 = 0; c0 < n; c0 += 64) {
+    const int i = c0 + lane;
+    const bool v = i < n;
+    const uint32_t c = v ? x[e0 + i] : 0u;
+    int h = -1, hs = 0, he = 0, num = 0;
+    for (int k = 0; k < nh; ++k) {  // (uniform: the bounds come from lane k)
+      const int a = __builtin_amdgcn_readlane(hs_l, k), b = __builtin_amdgcn_readlane(he_l, k);
+      if (i >= a && i < b) {
+        h = k;
+        hs = a;
+        he = b;
+        num = __builtin_amdgcn_readlane(num_l, k);
+      }
+    }
+    if (!v) continue;
+    if (h < 0) bad = bad || c != T.bytes[i];
+    else if (num) bad = bad || c - '0' > 9u || (i == hs && c == '0' && he - hs > 1);
+    else bad = bad || c < 0x20u || c > 0x7eu || c == '"' || c == '\\';
+  }
+  if (__ballot(bad) != 0) return false;
+  if (T.kind == EV_CONTENT) {
+    *sa = e0 + T.hs[T.target];
+    *sb = e0 + T.he[T.target];
+    *body = 0;
+  }
+  return true;
+}
+
 // One step that rejects most other shapes: the event's head / tail against T's first / last
 // literal run (up to 256 bytes each, a half wave each).
 __device__ inline bool wave_hole_quick(const uint8_t* x, int e0, int e1, const HoleTpl& T) {
@@ -1132,7 +1175,10 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
           atomicMax(&s.v[V_TPLK], k);
         }
       } else {
-        for (int q = 0; q < BS / 64 && kind != EV_CONTENT; ++q) {
+        // in-tile templates (this tile's parsed content shapes) — not for an event S3a already
+        // found to differ from the stream's content shape (0xFE: a role / finish / usage
+        // event, which the hole templates below resolve); skipping a try never changes a result
+        for (int q = 0; q < BS / 64 && kind != EV_CONTENT && k0 == 0xFF; ++q) {
           const int qi = (hint + q) & (BS / 64 - 1);
           const int p0 = __atomic_load_n(&wtpl[qi][0], __ATOMIC_ACQUIRE);  // published last
           if (p0 < 0) continue;
@@ -1164,7 +1210,8 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
               const HoleTpl& T = U.htpl[qi];
               if (T.len == 0) continue;
               int ha = 0, hb = 0, hbody = 0;
-              if (q < kHoleTpls ? !wave_hole_exact(s.A, e0, e1, T, &ha, &hb, &hbody)
+              if (q < kHoleTpls ? !(wave_hole_exact(s.A, e0, e1, T, &ha, &hb, &hbody) ||
+                                    wave_hole_samelen(s.A, e0, e1, T, &ha, &hb, &hbody))
                                 : !(wave_hole_quick(s.A, e0, e1, T) && wave_hole_match(s.A, e0, e1, T, &ha, &hb, &hbody)))
                 continue;
               hm = true;

@@ -390,3 +390,51 @@ def test_hip_hole_templates(ext, monkeypatch):
     assert got["hip"] == got["cpu"]
     st = hip._e.kernel_stats()
     assert st.get("s3_hole_hits", 0) > 50, st  # fresh streams' role / finish / first events
+
+
+def test_hip_hole_samelen(ext, monkeypatch):
+    """The same-length hole fast path (ids / timestamps of one backend keep their lengths):
+    fixed-length fields, and anomalies of exactly the template's lengths — escapes, a quote,
+    control bytes, DEL, UTF-8, a leading zero, a sign, a fraction, an exponent, a string where
+    a number was — must come out byte-identical to the CPU engine (the fast path refuses
+    every one of them and the walk / full parse decides)."""
+    monkeypatch.setenv("QMX_STAGE_TIMING", "1")
+    rng = random.Random(21)
+    tags = ["think"]
+    hip, cpu = _hip(tags), NativeEngine("cpu", tags)
+    id_anom = [b"abcd\\n12345678", b"abcd\\\\12345678", b'abcd\\"12345678', b"abcd\x0112345678",
+               b"abcd\x7f123456789", b"abcd\xc3\xa912345678", b"abcd1234567890"]
+    num_anom = [b"0123456789", b"-123456789", b"1.23456789", b"1234567e10", b'"12345678"', b"1234567890"]
+    got = {"hip": {}, "cpu": {}}
+    for rnd in range(5):
+        bodies = []
+        for k in range(24):
+            bad = rnd >= 2 and rng.random() < 0.5
+            id_ = b"chatcmpl-" + (rng.choice(id_anom) if bad and rng.random() < 0.5 else
+                                  bytes(rng.choice(b"abcdef0123456789") for _ in range(14)))
+            created = rng.choice(num_anom) if bad and rng.random() < 0.5 else str(rng.randint(10 ** 9, 2 * 10 ** 9 - 1)).encode()
+            evs = [_oai_event(id_, created, b"mock", b'{"role": "assistant", "content": ""}')]
+            for _ in range(rng.randint(1, 6)):
+                evs.append(_oai_event(id_, created, b"mock", b'{"content": "' + bytes(rng.choice(b"abc <>xyz")
+                                                                                       for _ in range(rng.randint(0, 9))) + b'"}'))
+            evs.append(_oai_event(id_, created, b"mock", b"{}", finish=b'"stop"'))
+            evs.append(b"data: [DONE]\n\n")
+            bodies.append(b"".join(evs))
+        for name, eng in (("hip", hip), ("cpu", cpu)):
+            slots = [eng.open(k % 2, True, True) for k in range(len(bodies))]
+            for sl, body in zip(slots, bodies):
+                eng.feed(sl, body)
+                eng.finish(sl)
+            acc = {sl: [b"", 0] for sl in slots}
+            for _ in range(50):
+                res, _ = eng.tick(H.CREATED)
+                for sl, data, fl in res:
+                    acc[sl][0] += data
+                    acc[sl][1] |= fl
+                if not eng.has_work():
+                    break
+            for k, sl in enumerate(slots):
+                got[name][(rnd, k)] = tuple(acc[sl])
+                eng.release(sl)
+    assert got["hip"] == got["cpu"]
+    assert hip._e.kernel_stats().get("s3_hole_hits", 0) > 50
