@@ -403,6 +403,11 @@ def breakdown(m0, m1, elapsed):
                                for k, v in sorted(d.items())
                                if k.startswith("qmx_kernel_stage") and k.endswith("_us")}
                               if d.get("qmx_kernel_stage_items") else None),
+        # ... and S3's event paths per item: full parses, stream-template and hole-template hits
+        "s3_per_item": ({k[len("qmx_kernel_s3_"):]: round(d.get(k, 0.0) / d["qmx_kernel_stage_items"], 2)
+                         for k in ("qmx_kernel_s3_events", "qmx_kernel_s3_full_parses", "qmx_kernel_s3_template_hits",
+                                   "qmx_kernel_s3_hole_hits")}
+                        if d.get("qmx_kernel_stage_items") else None),
         "shader_mhz": (round(d["qmx_kernel_clk_cycles"] / d["qmx_kernel_clk_us"], 1)
                        if d.get("qmx_kernel_clk_us") else None),
     }

@@ -213,6 +213,15 @@ struct DepthOp {
 // ------------------------------------------------------------------------------------
 // MFMA tag matcher
 // ------------------------------------------------------------------------------------
+// ASCII upper → lower case on 8 bytes at once (other bytes unchanged)
+__device__ inline uint64_t lower8(uint64_t x) {
+  constexpr uint64_t ones = 0x0101010101010101ull, hi = 0x8080808080808080ull;
+  const uint64_t lo7 = x & ~hi;
+  const uint64_t ge_a = lo7 + (0x80 - 'A') * ones;      // bit 7 set: byte >= 'A'
+  const uint64_t gt_z = lo7 + (0x80 - 'Z' - 1) * ones;  // bit 7 set: byte > 'Z'
+  return x | (((ge_a & ~gt_z & ~x) & hi) >> 2);
+}
+
 // B operand (patterns × window features) of column block `blk`: host-built per lane
 // (KParams::bfrag), one 16-byte LDS read per lane instead of per-byte pattern decoding.
 __device__ inline v4i build_pattern_frag(const KParams& P, int blk) {
@@ -231,8 +240,9 @@ __device__ inline bool pattern_tail_ok(const uint8_t* Z, int Zn, int p, int t, c
 }
 
 // 16 candidate windows per MFMA and 16 patterns per column block; result[row][pat] ==
-// -E[pat]  <=>  the window equals the pattern's first 16 bytes (all of it for tags up to
-// 13 bytes; longer patterns then compare their tail).  Distinct tags never both match at
+// Σ_j mask·(w_j²) − 2·w_j·p_j (per base-8 digit) == −E[pat]  <=>  Σ_j (w_j − p_j)² == 0 over
+// the pattern's first 16 bytes  <=>  the window equals them (all of a tag up to 13 bytes;
+// longer patterns then compare their tail).  Distinct tags never both match at
 // one '<' (make_tagset), so at most one column of a row survives.
 __device__ inline void mfma_match_group(const uint8_t* Z, int Zn, const uint16_t* cand, int ncand, int g,
                                         const KParams& P, v4i bf0, v4i bf1, int8_t* cand_tok) {
@@ -243,17 +253,19 @@ __device__ inline void mfma_match_group(const uint8_t* Z, int Zn, const uint16_t
   // readable bytes past Zn), bytes past Zn get code 0
   uint64_t w0 = 0, w1 = 0;
   const int nv = p >= 0 ? min(16, Zn - p) : 0;
-  if (nv > 0) {
-    w0 = lds_window8(Z, p, Zn);
-    w1 = lds_window8(Z, p + 8, Zn);
+  if (nv > 0) {  // (zero past Zn: 0 is no pattern byte)
+    w0 = lower8(lds_window8(Z, p, Zn));
+    w1 = lower8(lds_window8(Z, p + 8, Zn));
   }
+  // the window's bytes themselves (ASCII-lowercased, the tags' IGNORECASE) as base-8 digits
+  // d0, d1 (0..7) and d2 (0..3), and d0² + d1² + d2² (<= 107: int8) — feature group kg of the
+  // A operand; no per-byte table lookup
   int8_t bytes[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    const uint8_t zb = (uint8_t)((j < 8 ? w0 : w1) >> ((j & 7) * 8));
-    int code = j < nv ? (int)P.code[zb] : 0;
-    int d0 = code & 7, d1 = code >> 3;  // d1 <= 11: d1² fits an int8
-    bytes[j] = (int8_t)(kg == 0 ? d0 : kg == 1 ? d1 : kg == 2 ? d0 * d0 : d1 * d1);
+    const uint32_t zb = (uint32_t)((j < 8 ? w0 : w1) >> ((j & 7) * 8)) & 0xffu;
+    const int d0 = zb & 7, d1 = (zb >> 3) & 7, d2 = zb >> 6;
+    bytes[j] = (int8_t)(kg == 0 ? d0 : kg == 1 ? d1 : kg == 2 ? d2 : d0 * d0 + d1 * d1 + d2 * d2);
   }
   v4i a;
   __builtin_memcpy(&a, bytes, 16);
@@ -301,15 +313,6 @@ __device__ inline bool kept_at(const Smem& s, int k, int x) {
   if (k > 0 && x < (int)s.tok_pos[k - 1] + (int)s.tok_len[k - 1])
     return s.tok_id[k - 1] < 0 && s.tok_dep[k - 1] == 0;
   return s.tok_dep[k] == 0;
-}
-
-// ASCII upper → lower case on 8 bytes at once (other bytes unchanged)
-__device__ inline uint64_t lower8(uint64_t x) {
-  constexpr uint64_t ones = 0x0101010101010101ull, hi = 0x8080808080808080ull;
-  const uint64_t lo7 = x & ~hi;
-  const uint64_t ge_a = lo7 + (0x80 - 'A') * ones;      // bit 7 set: byte >= 'A'
-  const uint64_t gt_z = lo7 + (0x80 - 'Z' - 1) * ones;  // bit 7 set: byte > 'Z'
-  return x | (((ge_a & ~gt_z & ~x) & hi) >> 2);
 }
 
 // Is Z[q, e) (lowercased) a prefix of some pattern (opens only: open patterns)?  The device
@@ -1150,7 +1153,9 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       if (g >= nev) break;
       // pull order: the first 4 events, then the last 4 (a stream's closing events — finish
       // reason, usage, [DONE] — usually have their own shape and need a full parse), then the
-      // middle, which by then matches a published template: the few full parses overlap
+      // middle, which by then matches a published template: the few full parses overlap.
+      // (A compacted list of the events S3a left unresolved measured no faster: the claims
+      // are not what this loop waits on.)
       const int k = nev <= 8 ? g : g < 4 ? g : g < 8 ? nev - 1 - (g - 4) : g - 4;
       const int k0 = s.ev_kind[k];
       if (k0 < 0xFE) continue;  // resolved by S3a
@@ -2642,11 +2647,14 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
         ++next;
       }
   }
+  // the matcher works on the bytes themselves as base-8 digits (mfma_match_group): E is the
+  // squared digit sum of the pattern's window part
+  auto digits = [](int b, int k) { return k == 0 ? (b & 7) : k == 1 ? ((b >> 3) & 7) : (b >> 6); };
   for (int p = 0; p < base_params_.npat; ++p) {
     int E = 0;
     for (int j = 0; j < std::min(kWindow, pattern_len(ts_, p)); ++j) {
-      const int q = base_params_.code[pattern_byte(ts_, p, j)];
-      E += (q & 7) * (q & 7) + (q >> 3) * (q >> 3);
+      const int b = pattern_byte(ts_, p, j);
+      for (int k = 0; k < 3; ++k) E += digits(b, k) * digits(b, k);
     }
     base_params_.pat_E[p] = E;
   }
@@ -2662,8 +2670,8 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
       for (int j = 0; j < 16; ++j) {
         int v = 0;
         if (t < base_params_.npat && j < pattern_len(ts_, t)) {
-          const int q = base_params_.code[pattern_byte(ts_, t, j)];
-          v = kg == 0 ? -2 * (q & 7) : kg == 1 ? -2 * (q >> 3) : 1;
+          const int b = pattern_byte(ts_, t, j);
+          v = kg < 3 ? -2 * digits(b, kg) : 1;  // -2·p digit, or the mask of the squares
         }
         base_params_.bfrag[blk][l * 16 + j] = (int8_t)v;
       }
