@@ -219,3 +219,28 @@ def test_bench_reference_same_harness(tmp_path):
     res = json.loads(_json_lines(r.stdout)[0])
     assert res["config"]["impl"] == "reference" and res["validated"] == 16 and res["invalid"] == 0
     assert res["vs_baseline"] is None
+
+
+def test_breakdown_loop_tick_fields():
+    """bench.breakdown on two synthetic /metrics scrapes: the loop-tick hops (calibrated
+    clocks), S3's event paths per item and the shader clock come from summable counters (the
+    io loops' engines add up in /metrics), means over the window between the scrapes."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("qmx_bench_mod2", BENCH)
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    m0 = {"qmx_kernel_launches": 10.0, "qmx_kernel_hop_ticks": 10.0, "qmx_kernel_post_seen_us": 15.0,
+          "qmx_kernel_done_host_us": 100.0, "qmx_kernel_stage_items": 0.0, "qmx_kernel_clk_cycles": 0.0,
+          "qmx_kernel_clk_us": 0.0, "qmx_tick_seconds_count": 10.0, "qmx_tick_seconds_sum": 5e-4}
+    m1 = dict(m0, qmx_kernel_launches=110.0, qmx_kernel_hop_ticks=110.0, qmx_kernel_post_seen_us=165.0,
+              qmx_kernel_done_host_us=1400.0, qmx_kernel_stage_items=40.0, qmx_kernel_s3_events=1080.0,
+              qmx_kernel_s3_full_parses=0.0, qmx_kernel_s3_template_hits=960.0, qmx_kernel_s3_hole_hits=80.0,
+              qmx_kernel_stage4_us=240.0, qmx_kernel_clk_cycles=2.4e6, qmx_kernel_clk_us=1000.0,
+              qmx_tick_seconds_count=110.0, qmx_tick_seconds_sum=5.5e-3)
+    bd = bench.breakdown(m0, m1, 1.0)
+    assert bd["tick_hops_us_avg"] == {"post_seen": 1.5, "done_host": 13.0}
+    assert bd["s3_per_item"] == {"events": 27.0, "full_parses": 0.0, "template_hits": 24.0, "hole_hits": 2.0}
+    assert bd["stage_us_per_item"]["stage4_us"] == 6.0
+    assert bd["shader_mhz"] == 2400.0
+    assert bd["tick_wall_us_avg"] == 50.0
