@@ -2885,6 +2885,15 @@ size_t HipEngine::content_size(int slot) {
 // any local stream.
 void HipEngine::set_remote_content(int slot, const std::string* bytes, size_t len) {
   if (slot < 0 || slot >= (int)nslots()) return;
+  if (grid_) {
+    // loop ticks: the grid runs on while a remote text lands in HBM by RCCL (or would by a
+    // DMA copy), outside the release / acquire protocol its items use — so the text is kept
+    // on the host, and the session's finalize takes the host path (prep_finalize), reading
+    // nothing of it from the content arena
+    core_[slot].content = bytes ? *bytes : device_content(slot, (uint32_t)len);
+    if (slot < max_slots_) host_mode_[slot] = 1;
+    return;
+  }
   if (slot >= max_slots_ || (bytes && len > content_cap_)) {
     if (slot < max_slots_) host_mode_[slot] = 1;
     core_[slot].content = bytes ? *bytes : std::string();

@@ -3071,11 +3071,14 @@ int run_server(const ServerCfg& cfg0) {
   std::unique_ptr<HipGrid> grid;  // destroyed after the loops (their engines stop it first)
   const bool hip = cfg.engine == "hip";
   const bool spread = cfg.world > 1 && cfg.placement == "spread";
-  // hip: loop ticks unless asked for lanes (tick_mode / an explicit shared engine) or sessions
-  // spread across ranks (remote texts land in the content arena outside the grid's protocol)
-  // (ranks sharing one GPU — rehearsals — split the grid budget: HipGrid sizes itself from
-  // QMX_GPU_SHARERS, and a grid that does not fit falls back to lanes below)
-  const bool loop_ticks = hip && !spread && cfg.tick_mode != "lanes" && cfg.shared_engine != 1;
+  // hip: loop ticks unless asked for lanes (tick_mode / an explicit shared engine).  Spread
+  // placement included: a remote stream's final text is kept on the owner's host and its
+  // session finalized there (HipEngine::set_remote_content) — lanes instead use one-shot
+  // launches, whose kernel boundaries order the RCCL / DMA writes.  Ranks sharing one GPU
+  // (rehearsals) split the grid budget: HipGrid sizes itself from QMX_GPU_SHARERS, and a grid
+  // that does not fit falls back to lanes below.
+  (void)spread;
+  const bool loop_ticks = hip && cfg.tick_mode != "lanes" && cfg.shared_engine != 1;
   const bool shared = !loop_ticks && (cfg.shared_engine < 0 ? hip : cfg.shared_engine > 0);
   if (shared) hub.reset(new GpuHub(cfg, (int)loops.size()));
   if (loop_ticks) {

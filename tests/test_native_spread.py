@@ -38,11 +38,13 @@ THINK = [sse_chunk({"role": "assistant"}), sse_chunk({"content": "<think>"}), ss
 
 
 @contextlib.contextmanager
-def native_cluster(cfg, world: int, placement: str = "spread", xchg: str = "tcp", eager=None):
+def native_cluster(cfg, world: int, placement: str = "spread", xchg: str = "tcp", eager=None, tick_mode=None):
     """`world` native ranks in-process (threads), TCP exchange on a free port block.
     ``xchg="tcpbulk"``: final texts move in rank-0-numbered bulk rounds (the RCCL round
     protocol with a socket executor) instead of riding the mesh.  ``eager``: the largest final
-    text that rides the mesh behind its deltas instead (None: the default; 0: none)."""
+    text that rides the mesh behind its deltas instead (None: the default; 0: none).
+    ``tick_mode="loops"``: every rank's io loops drive their own engine asynchronously (the
+    loop-tick protocol, AsyncCpuEngine on the CPU) while remote streams come and go."""
     from quorum_amd.runtime.native_server import native_config
 
     ext = native.require()
@@ -70,6 +72,8 @@ def native_cluster(cfg, world: int, placement: str = "spread", xchg: str = "tcp"
                 else:
                     os.environ[k] = v
         d["install_signals"] = False
+        if tick_mode is not None:
+            d["tick_mode"] = tick_mode
         cfgs.append(d)
     for d in cfgs:
         th = threading.Thread(target=ext.run_server, args=(d,), daemon=True)
@@ -216,8 +220,10 @@ def test_spread_matches_local(name, world, xchg, eager):
         live.close()
 
 
-def test_spread_many_concurrent_sessions():
-    """Concurrent sessions on both ranks; every response complete and correct."""
+@pytest.mark.parametrize("tick_mode", [None, "loops"])
+def test_spread_many_concurrent_sessions(tick_mode):
+    """Concurrent sessions on both ranks; every response complete and correct (also with
+    every rank's io loops on the loop-tick protocol)."""
     behs = [("stream", 200, THINK), ("stream", 200, sse_stream(["x", "y", "z"]))]
     live, ports = _live({"b1": behs[0], "b2": behs[1]})
     try:
@@ -227,7 +233,7 @@ def test_spread_many_concurrent_sessions():
         with native_server(cfg) as p:
             ref = _split(_events(httpx.post(f"http://127.0.0.1:{p}/chat/completions", json=req, headers=AUTH,
                                             timeout=30).text))
-        with native_cluster(cfg, 2) as cports:
+        with native_cluster(cfg, 2, tick_mode=tick_mode) as cports:
             import concurrent.futures as cf
 
             def one(i):
