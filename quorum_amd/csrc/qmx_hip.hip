@@ -58,8 +58,9 @@ constexpr int PAD = 16;
 constexpr int kSpecTile = 4096;  // tile bytes loaded before the work item is known (256 threads x 16 B)
 constexpr int TOK_CAP = 512;
 // QMX_STAGE_TIMING record per work item: stamps 0-12, S3 counters 13-20, sub-stage stamps
-// 21 (S3a done), 22 (S3 loop done), 23 (s4_wave: matched), 24 (s4_wave: cuts)
-constexpr int kDbg = 25;
+// 21 (S3a done), 22 (S3 loop done), 23 (s4_wave: matched), 24 (s4_wave: cuts), 25 (s4_wave:
+// token list + depth scan done), 26 (S6 write: output window filled, host stores next)
+constexpr int kDbg = 27;
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 
@@ -614,6 +615,7 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
   }
   wave_fence();
   const int ntok = __builtin_amdgcn_readfirstlane(s.v[V_NTOK]);
+  if (dbg != nullptr && lane == 0) dbg[25] = __builtin_amdgcn_s_memrealtime();
   // a cut per delta (lane j), the new holdback tail (lane 0)
   int cut = 0;
   if (lane < ndelta) {
@@ -1871,6 +1873,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
         }
       }
       __syncthreads();
+      if (w0 == 0) QMX_STAMP(26);
       const int wl = w1 - w0;
       for (int i = tid * 16; i < wl; i += BS * 16) *(uint4*)&out[it.out_off + w0 + i] = *(const uint4*)&O[i];
       __syncthreads();
@@ -3371,6 +3374,10 @@ void HipEngine::complete(HipJob& J, std::vector<SlotResult>& results, std::vecto
         sub(13, 22, 4);
         sub(14, 5, 23);
         sub(15, 23, 24);
+        sub(16, 23, 25);  // s4_wave cuts: token list + depth scan / the holdback cuts
+        sub(17, 25, 24);
+        sub(18, 9, 26);   // S6 write: output window fill / host-memory stores
+        sub(19, 26, 10);
       }
       L.stage_n += n;
       for (int i = 0; i < n; ++i) {
@@ -3589,7 +3596,7 @@ void HipEngine::collect_finalize(TickLane& L, const std::vector<const FinalizeRe
 
 std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   std::unordered_map<std::string, double> m;
-  double stage[16] = {0}, cyc = 0, cus = 0;
+  double stage[20] = {0}, cyc = 0, cus = 0;
   for (auto& Lp : lanes_) {
     TickLane& L = *Lp;
     std::lock_guard<std::mutex> lg(L.mu);
@@ -3627,7 +3634,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["poll_fallbacks"] += (double)L.poll_fallbacks;
     m["fin_launches"] += (double)L.fin_launches;  // tick launches that also carried finalize work
     m["fin_items"] += (double)L.fin_items;
-    for (int k = 1; k < 16; ++k) stage[k] += L.stage_us[k];
+    for (int k = 1; k < 20; ++k) stage[k] += L.stage_us[k];
     cyc += L.clk_cycles;
     cus += L.clk_us;
   }
@@ -3637,6 +3644,10 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   m["stage_s3persist_us"] = stage[13];
   m["stage_s4match_us"] = stage[14];
   m["stage_s4cuts_us"] = stage[15];
+  m["stage_s4tok_us"] = stage[16];
+  m["stage_s4hold_us"] = stage[17];
+  m["stage_s6fill_us"] = stage[18];
+  m["stage_s6store_us"] = stage[19];
   m["shader_mhz"] = cus > 0 ? cyc / cus : 0.0;
   m["clk_cycles"] = cyc;  // summable across engines (/metrics sums the io loops' engines)
   m["clk_us"] = cus;
