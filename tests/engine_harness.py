@@ -119,9 +119,10 @@ def split_random(rng: random.Random, data: bytes, max_piece: int = 40) -> List[b
 
 
 def run_engine(engine, streams: Sequence[List[bytes]], filt: Sequence[bool], emit: Sequence[bool],
-               rng: random.Random, strip_final: bool = True, joiner: str = "\n---\n"):
-    """Feed chunk lists round-robin with ticks at random points; return per-stream results."""
-    slots = [engine.open(i % 7, filt[i], emit[i]) for i in range(len(streams))]
+               rng: random.Random, strip_final: bool = True, joiner: str = "\n---\n", indices=None):
+    """Feed chunk lists round-robin with ticks at random points; return per-stream results.
+    ``indices``: each stream's backend index (default i % 7)."""
+    slots = [engine.open(indices[i] if indices else i % 7, filt[i], emit[i]) for i in range(len(streams))]
     out: Dict[int, List[bytes]] = {s: [] for s in slots}
     flags: Dict[int, int] = {s: 0 for s in slots}
     cursors = [0] * len(streams)

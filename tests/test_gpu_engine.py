@@ -75,6 +75,29 @@ def test_hip_matches_cpu_wide_batch(ext, seed):
     _check(1000 + seed, 300)
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_hip_clean_content_envelopes(ext, seed):
+    """Printable-ASCII content without quotes or backslashes (the S6 clean path: escaped
+    offsets are raw offsets, one wave per event): 1-3 digit backend indices, up to 60 events
+    per tile, mixed with tiles that need escapes (the general path) in the same launch."""
+    rng = random.Random(seed)
+    clean = "abcdefghijklmnopqrstuvwxyz ABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789.,!?-:;()<>/"
+    raw, idx = [], []
+    for i in range(24):
+        texts = ["".join(rng.choice(clean) for _ in range(rng.randint(0, 40))) for _ in range(rng.randint(1, 60))]
+        if i % 5 == 4:
+            texts[rng.randrange(len(texts))] += rng.choice(['"', "\\", "\n", "\u00e9"])
+        raw.append(b"".join(H.event_bytes(rng, t) for t in texts) + b"data: [DONE]\n\n")
+        idx.append(rng.choice([0, 3, 9, 10, 42, 99, 100, 123, 255]))
+    streams = [H.split_random(rng, r, rng.choice([64, 400, 5000])) for r in raw]
+    filt = [rng.random() < 0.5 for _ in raw]
+    emit = [True] * len(raw)
+    tseed = rng.randint(0, 10**9)
+    cpu = H.run_engine(NativeEngine("cpu", ["think"]), streams, filt, emit, random.Random(tseed), indices=idx)
+    hip = H.run_engine(_hip(["think"]), streams, filt, emit, random.Random(tseed), indices=idx)
+    assert hip == cpu
+
+
 def test_hip_small_tiles_and_escalation(ext):
     """Tiny tiles force MORE/requeue and oversize-event escalation to the host path."""
     for seed in range(20):
