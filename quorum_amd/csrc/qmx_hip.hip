@@ -67,10 +67,16 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 // optional per-stage wall-clock stamps (s_memrealtime, 100 MHz) written by thread 0
 // (reads the LDS copy P of the kernel parameters: a persistent grid's parameters are not
 // launch-invariant, so reading them from memory at every use would cost vector registers)
+// Stamps are stored through the global address space: a flat store also counts against
+// lgkmcnt, so the stage's next LDS wait would wait for the host-memory write too and the
+// stamp would bill its own PCIe store to the stage after it.
+__device__ __forceinline__ void dbg_put(unsigned long long* p, unsigned long long v) {
+  *(__attribute__((address_space(1))) unsigned long long*)p = v;
+}
 #define QMX_STAMP(k)                                               \
   do {                                                             \
     if (P.dbg != nullptr && threadIdx.x == 0)                      \
-      P.dbg[bi * kDbg + (k)] = __builtin_amdgcn_s_memrealtime();       \
+      dbg_put(&P.dbg[bi * kDbg + (k)], __builtin_amdgcn_s_memrealtime()); \
   } while (0)
 
 struct Smem {
@@ -588,7 +594,7 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
     for (int g = 0; g * 16 < nc; ++g) mfma_match_group(Z, Zn, s.cand, nc, g, P, bf0, bf1, s.cand_tok);
   }
   wave_fence();
-  if (dbg != nullptr && lane == 0) dbg[23] = __builtin_amdgcn_s_memrealtime();
+  if (dbg != nullptr && lane == 0) dbg_put(&dbg[23], __builtin_amdgcn_s_memrealtime());
   // tokens and the depth before each (candidates in order, non-tokens the scan identity)
   {
     const int id = lane < nc ? (int)s.cand_tok[lane] : 0;
@@ -615,7 +621,7 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
   }
   wave_fence();
   const int ntok = __builtin_amdgcn_readfirstlane(s.v[V_NTOK]);
-  if (dbg != nullptr && lane == 0) dbg[25] = __builtin_amdgcn_s_memrealtime();
+  if (dbg != nullptr && lane == 0) dbg_put(&dbg[25], __builtin_amdgcn_s_memrealtime());
   // a cut per delta (lane j), the new holdback tail (lane 0)
   int cut = 0;
   if (lane < ndelta) {
@@ -630,7 +636,7 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
     s.v[V_NEWDEPTH] = s.tok_dep[ntok];
   }
   const int cutN = __shfl(cut, ndelta - 1, 64);
-  if (dbg != nullptr && lane == 0) dbg[24] = __builtin_amdgcn_s_memrealtime();
+  if (dbg != nullptr && lane == 0) dbg_put(&dbg[24], __builtin_amdgcn_s_memrealtime());
   // compaction of the kept bytes of [0, cutN) into A, by segments (kept_at's cases): lane k
   // owns the gap before token k (kept at depth 0) and token k itself (kept when it is a
   // close tag at depth 0: literal text); a DPP scan gives each segment its output offset,
@@ -835,8 +841,8 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   if (tid * 16 < kSpecTile) spec = *(const uint4*)&tile[tid * 16];
   WorkItem it = items[bi];
   for (int i = tid; i < (int)(sizeof(KParams) / 4); i += BS) ((uint32_t*)&P)[i] = ((const uint32_t*)&Pk)[i];
-  if (Pk.dbg != nullptr && threadIdx.x == 0) Pk.dbg[bi * kDbg + 0] = __builtin_amdgcn_s_memrealtime();
-  if (Pk.dbg != nullptr && threadIdx.x == 0) Pk.dbg[bi * kDbg + 11] = __builtin_amdgcn_s_memtime();
+  if (Pk.dbg != nullptr && threadIdx.x == 0) dbg_put(&Pk.dbg[bi * kDbg + 0], __builtin_amdgcn_s_memrealtime());
+  if (Pk.dbg != nullptr && threadIdx.x == 0) dbg_put(&Pk.dbg[bi * kDbg + 11], __builtin_amdgcn_s_memtime());
   // the work item is wave-uniform: keep its fields in scalar registers (a one-shot launch
   // reads it through the scalar cache anyway; a persistent grid loads it per tick with
   // vector loads, and every address derived from VGPR copies would cost vector registers)
@@ -2292,12 +2298,17 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
 // traffic keeps its sub-grid while the others are busy.  Idle time counts from the last
 // post or heartbeat, so the 2 s limit HipGrid passes fires only for a host that stopped.
 // ------------------------------------------------------------------------------------
+// A wave-uniform pointer held in SGPRs, into the global address space (device or host-mapped
+// memory, never LDS).  Saying so lets the compiler emit global_* instead of flat_* accesses
+// through the descriptor's pointers, as it does for kernel arguments: a flat access also
+// counts against lgkmcnt, so every LDS wait after it would wait for the memory access too.
 template <class T>
-__device__ __forceinline__ T* uni(T* p) {  // a wave-uniform pointer held in SGPRs
+__device__ __forceinline__ T* uni(T* p) {
+  typedef __attribute__((address_space(1))) T GT;
   const uint64_t v = (uint64_t)p;
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return (T*)(((uint64_t)hi << 32) | lo);
+  return (T*)(GT*)(((uint64_t)hi << 32) | lo);
 }
 
 struct TickDesc {
