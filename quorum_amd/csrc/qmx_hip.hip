@@ -622,14 +622,23 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
   wave_fence();
   const int ntok = __builtin_amdgcn_readfirstlane(s.v[V_NTOK]);
   if (dbg != nullptr && lane == 0) dbg_put(&dbg[25], __builtin_amdgcn_s_memrealtime());
-  // a cut per delta (lane j), the new holdback tail (lane 0)
+  // a cut per delta (lane j) and the new holdback tail (lane ndelta, in the same pass: the
+  // searches are chains of dependent LDS reads, so a second pass would double their latency)
   int cut = 0;
-  if (lane < ndelta) {
+  const bool tail_here = ndelta < 64;  // a free lane for the tail: lane ndelta
+  if (lane < ndelta || (tail_here && lane == ndelta)) {
+    const bool is_tail = lane == ndelta;
     int q;
-    cut = hold_cut(s, Z, nc, ntok, s.dl_end[lane], P, false, &q);
-    s.cut[lane] = (uint16_t)cut;
+    const int c = hold_cut(s, Z, nc, ntok, is_tail ? Zn : (int)s.dl_end[lane], P, is_tail, &q);
+    if (is_tail) {
+      s.v[V_NEWTAIL] = q;
+      s.v[V_NEWDEPTH] = s.tok_dep[ntok];
+    } else {
+      cut = c;
+      s.cut[lane] = (uint16_t)cut;
+    }
   }
-  if (lane == 0) {
+  if (!tail_here && lane == 0) {  // 64 deltas: the tail after them, on lane 0
     int q;
     hold_cut(s, Z, nc, ntok, Zn, P, true, &q);
     s.v[V_NEWTAIL] = q;
