@@ -111,6 +111,8 @@ inline bool env_flag(const char* name, bool dflt) {
 
 // Header block [p, p+n) ("k: v\r\n" lines, no start line): calls f(lower(trim(k)), trim(v)) per line that
 // has a colon, building each key and value string once (no per-line/per-field temporaries).
+// ASCII lower case (what tolower does in the C locale, inline: no locale lookup per byte)
+inline char alow(unsigned char c) { return (char)(c - 'A' < 26u ? c | 0x20 : c); }
 template <class F>
 void for_each_header(const char* p, size_t n, F&& f) {
   auto ws = [](char ch) { return ch == ' ' || ch == '\t'; };
@@ -127,7 +129,7 @@ void for_each_header(const char* p, size_t n, F&& f) {
       while (va < vb && ws(p[va])) ++va;
       while (vb > va && (ws(p[vb - 1]) || p[vb - 1] == '\r')) --vb;
       std::string k(p + ka, kb - ka);
-      for (auto& ch : k) ch = (char)tolower((unsigned char)ch);
+      for (auto& ch : k) ch = alow((unsigned char)ch);
       f(std::move(k), std::string(p + va, vb - va));
     }
     pos = e + 2;
@@ -138,14 +140,14 @@ bool ieq(const std::string& s, const char* lw) {
   size_t n = strlen(lw);
   if (s.size() != n) return false;
   for (size_t i = 0; i < n; ++i)
-    if ((char)tolower((unsigned char)s[i]) != lw[i]) return false;
+    if (alow((unsigned char)s[i]) != lw[i]) return false;
   return true;
 }
 bool icontains(const std::string& s, const char* lw) {
   size_t n = strlen(lw);
   for (size_t i = 0; i + n <= s.size(); ++i) {
     size_t j = 0;
-    while (j < n && (char)tolower((unsigned char)s[i + j]) == lw[j]) ++j;
+    while (j < n && alow((unsigned char)s[i + j]) == lw[j]) ++j;
     if (j == n) return true;
   }
   return false;
