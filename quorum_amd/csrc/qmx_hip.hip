@@ -561,6 +561,9 @@ __device__ inline void wave_hole_carry(const HoleTpl& T, HoleTpl* dst, int slot,
 // more than 63 candidates.
 __device__ inline void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); }
 
+// (a call, not inlined: inlined, the persistent kernel spills 16 B per lane and its span
+// grows 28.0 -> 29.7 us, r3/loops/s3tune/; the call's entry wait for the wave's outstanding
+// stores is the cheaper cost)
 __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth0, const KParams& P,
                         unsigned long long* dbg) {
   const int lane = threadIdx.x & 63;
