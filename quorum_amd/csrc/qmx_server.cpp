@@ -953,6 +953,7 @@ class Loop {
         for (int fd : fds) {
           auto it = clients_.find(fd);
           if (it != clients_.end() && !it->second->sess && !it->second->dead) process_requests(it->second.get());
+          if (req_check_ && jobs_live_ && any_ready()) loop_tick();
         }
       }
       double t = now_s();
@@ -2951,6 +2952,13 @@ class Loop {
   const double spin_us_ = [] {
     const char* e = env_get("QMX_LOOP_SPIN_US");
     return e ? atof(e) : 0.0;
+  }();
+  // loop ticks: also look for results between the new requests an iteration parses (parsing
+  // and the upstream sends are an iteration's longest stretch without a look);
+  // QMX_LOOP_REQ_CHECK=0 turns it off (A/B)
+  const bool req_check_ = [] {
+    const char* e = env_get("QMX_LOOP_REQ_CHECK");
+    return !e || atoi(e) != 0;
   }();
   TagSet ts_ = make_tagset(cfg_.tags);
   bool kick_ = false;
