@@ -59,8 +59,9 @@ constexpr int kSpecTile = 4096;  // tile bytes loaded before the work item is kn
 constexpr int TOK_CAP = 512;
 // QMX_STAGE_TIMING record per work item: stamps 0-12, S3 counters 13-20, sub-stage stamps
 // 21 (S3a done), 22 (S3 loop done), 23 (s4_wave: matched), 24 (s4_wave: cuts), 25 (s4_wave:
-// token list + depth scan done), 26 (S6 write: output window filled, host stores next)
-constexpr int kDbg = 27;
+// token list + depth scan done), 26 (S6 write: output window filled, host stores next),
+// 27 (the item's system-scope release fence done: its cost is 27 minus the result's t1)
+constexpr int kDbg = 28;
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 
@@ -73,6 +74,9 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void dbg_put(unsigned long long* p, unsigned long long v) {
   *(__attribute__((address_space(1))) unsigned long long*)p = v;
 }
+// s_waitcnt vmcnt(0) (expcnt and lgkmcnt left alone): this wave's vector memory accesses,
+// stores included, have completed
+__device__ __forceinline__ void wave_stores_done() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 #define QMX_STAMP(k)                                               \
   do {                                                             \
     if (P.dbg != nullptr && threadIdx.x == 0)                      \
@@ -2260,6 +2264,7 @@ __device__ __forceinline__ void run_item(int k, const WorkItem* __restrict__ ite
     }
     __threadfence_system();
     __syncthreads();
+    if (Pk.dbg != nullptr && threadIdx.x == 0) dbg_put(&Pk.dbg[k * kDbg + 27], __builtin_amdgcn_s_memrealtime());
     if (threadIdx.x == 0) __hip_atomic_store(&res[k].seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   } else {
     const int j = (int)(k - n_tick);
@@ -3425,6 +3430,7 @@ void HipEngine::complete(HipJob& J, std::vector<SlotResult>& results, std::vecto
         sub(17, 25, 24);
         sub(18, 9, 26);   // S6 write: output window fill / host-memory stores
         sub(19, 26, 10);
+        if (d[27] && d[27] >= B.h_res[i].t1 && B.h_res[i].t1) L.stage_us[20] += (double)(d[27] - B.h_res[i].t1) * 0.01;
       }
       L.stage_n += n;
       for (int i = 0; i < n; ++i) {
@@ -3643,7 +3649,7 @@ void HipEngine::collect_finalize(TickLane& L, const std::vector<const FinalizeRe
 
 std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   std::unordered_map<std::string, double> m;
-  double stage[20] = {0}, cyc = 0, cus = 0;
+  double stage[21] = {0}, cyc = 0, cus = 0;
   for (auto& Lp : lanes_) {
     TickLane& L = *Lp;
     std::lock_guard<std::mutex> lg(L.mu);
@@ -3681,7 +3687,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["poll_fallbacks"] += (double)L.poll_fallbacks;
     m["fin_launches"] += (double)L.fin_launches;  // tick launches that also carried finalize work
     m["fin_items"] += (double)L.fin_items;
-    for (int k = 1; k < 20; ++k) stage[k] += L.stage_us[k];
+    for (int k = 1; k < 21; ++k) stage[k] += L.stage_us[k];
     cyc += L.clk_cycles;
     cus += L.clk_us;
   }
@@ -3695,6 +3701,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   m["stage_s4hold_us"] = stage[17];
   m["stage_s6fill_us"] = stage[18];
   m["stage_s6store_us"] = stage[19];
+  m["stage_fence_us"] = stage[20];  // the item's system-scope release fence (L2 write-back)
   m["shader_mhz"] = cus > 0 ? cyc / cus : 0.0;
   m["clk_cycles"] = cyc;  // summable across engines (/metrics sums the io loops' engines)
   m["clk_us"] = cus;
