@@ -10,6 +10,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <map>
+#include <set>
 #include <mutex>
 #include <thread>
 
@@ -186,7 +187,10 @@ PYBIND11_MODULE(_qmx, m) {
   m.def("rccl_unique_id", &rccl_unique_id_hex);
   // Exchange self-test: every rank sends every other rank `rounds` delta messages over the
   // mesh and `rounds` final texts through the bulk plane (RCCL p2p rounds from HBM into HBM
-  // sinks with transport=rccl, the mesh with tcp); receivers verify every byte.
+  // sinks with transport=rccl, the mesh with tcp); receivers verify every byte and that each
+  // text arrives exactly once.  Options: pace_ms spaces the sends so they form many rounds;
+  // min_epochs waits for re-formed communicators; wave2 then sends that many more rounds
+  // and reports how many bulk rounds / mesh finals carried them (the re-formed epoch's work).
   m.def("exchange_selftest", [](const py::dict& d, int rounds) {
     env_refresh();  // fault-injection knobs set by the caller
     XOptions o;
@@ -198,6 +202,9 @@ PYBIND11_MODULE(_qmx, m) {
     const double wait_s = o.timeout_s;  // the whole test; round_timeout: the exchange's own round limit
     if (d.contains("round_timeout")) o.timeout_s = py::cast<double>(d["round_timeout"]);
     const uint64_t min_epochs = d.contains("min_epochs") ? py::cast<uint64_t>(d["min_epochs"]) : 0;
+    const double pace_ms = d.contains("pace_ms") ? py::cast<double>(d["pace_ms"]) : 0.0;
+    int wave2 = 0;
+    gi("wave2", wave2);
     const bool dev = o.transport == "rccl";
     auto payload = [](int r, int src, int dst, int kind) {
       uint64_t x = 1234567 ^ ((uint64_t)r * 1000003ull) ^ ((uint64_t)src * 7919ull) ^ ((uint64_t)dst * 104729ull) ^
@@ -214,9 +221,10 @@ PYBIND11_MODULE(_qmx, m) {
     std::condition_variable cv;
     std::vector<XMsg> got;
     bool ok = true;
-    int bad = 0, n_data = 0, n_bulk = 0, n_sent = 0;
+    int bad = 0, dups = 0, n_data = 0, n_bulk = 0, n_sent = 0;
     double data_us = 0, wall = 0;
-    uint64_t rounds_done = 0, mesh_finals = 0, epochs = 0;
+    uint64_t rounds_done = 0, mesh_finals = 0, epochs = 0, w2_rounds = 0, w2_mesh = 0, rescued = 0;
+    std::string why;
     {
       py::gil_scoped_release nogil;
       std::vector<void*> bufs;
@@ -231,10 +239,11 @@ PYBIND11_MODULE(_qmx, m) {
         for (auto& m : v) got.push_back(std::move(m));
         cv.notify_all();
       });
+      const bool loop1 = o.world == 1;  // one rank: everything goes to itself (RCCL send/recv to self)
+      const int total = rounds + wave2;  // message round r: skey r + 1 (wave 2: r >= rounds)
       // sinks first: a bulk that finds no sink is dropped
       std::map<std::pair<int, int>, void*> sinks;
-      const bool loop1 = o.world == 1;  // one rank: everything goes to itself (RCCL send/recv to self)
-      for (int r = 0; r < rounds; ++r)
+      for (int r = 0; r < total; ++r)
         for (int src = 0; src < o.world; ++src) {
           if (src == o.rank && !loop1) continue;
           const size_t n = payload(r, src, o.rank, 1).size();
@@ -245,41 +254,50 @@ PYBIND11_MODULE(_qmx, m) {
         }
       const auto t0 = std::chrono::steady_clock::now();
       auto secs = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
-      while (!x.healthy() || (x.bulk_transport() && !x.rccl_active())) {
-        if (secs() > wait_s) {
-          ok = false;
-          break;
-        }
-        std::this_thread::sleep_for(std::chrono::milliseconds(5));
-      }
-      const auto t1 = std::chrono::steady_clock::now();
-      for (int r = 0; r < rounds && ok; ++r)
-        for (int p = 0; p < o.world; ++p) {
-          if (p == o.rank && !loop1) continue;
-          XMsg m;
-          m.type = X_DATA;
-          m.dst_rank = p;
-          m.src_rank = o.rank;
-          m.skey = (uint64_t)(r + 1);
-          m.bi = o.rank;
-          m.payload = payload(r, o.rank, p, 0);
-          x.post(std::move(m));
-          std::string b = payload(r, o.rank, p, 1);
-          void* src = nullptr;
-          if (dev) {
-            src = dalloc(b.size());
-            if (!src || hipMemcpy(src, b.data(), b.size(), hipMemcpyHostToDevice) != hipSuccess) ok = false;
+      auto wait_bulk_ready = [&] {
+        while (!x.healthy() || (x.bulk_transport() && !x.rccl_active())) {
+          if (secs() > wait_s) {
+            why = "bulk plane not ready";
+            return false;
           }
-          XMsg h;
-          h.dst_rank = p;
-          h.src_rank = o.rank;
-          h.skey = (uint64_t)(r + 1);
-          h.bi = o.rank * o.world + p;
-          h.flags = XF_TEXT;
-          x.send_bulk(std::move(h), src, b.size(), [b] { return b; });
+          std::this_thread::sleep_for(std::chrono::milliseconds(5));
         }
-      const int want = rounds * (loop1 ? 1 : o.world - 1);
-      {
+        return true;
+      };
+      ok = wait_bulk_ready();
+      const auto t1 = std::chrono::steady_clock::now();
+      std::set<std::pair<uint64_t, int>> seen_bulk, seen_sent;
+      auto send_rounds = [&](int r0, int r1) {
+        for (int r = r0; r < r1 && ok; ++r) {
+          for (int p = 0; p < o.world; ++p) {
+            if (p == o.rank && !loop1) continue;
+            XMsg m;
+            m.type = X_DATA;
+            m.dst_rank = p;
+            m.src_rank = o.rank;
+            m.skey = (uint64_t)(r + 1);
+            m.bi = o.rank;
+            m.payload = payload(r, o.rank, p, 0);
+            x.post(std::move(m));
+            std::string b = payload(r, o.rank, p, 1);
+            void* src = nullptr;
+            if (dev) {
+              src = dalloc(b.size());
+              if (!src || hipMemcpy(src, b.data(), b.size(), hipMemcpyHostToDevice) != hipSuccess) ok = false;
+            }
+            XMsg h;
+            h.dst_rank = p;
+            h.src_rank = o.rank;
+            h.skey = (uint64_t)(r + 1);
+            h.bi = o.rank * o.world + p;
+            h.flags = XF_TEXT;
+            x.send_bulk(std::move(h), src, b.size(), [b] { return b; });
+          }
+          if (pace_ms > 0) std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(pace_ms * 1000)));
+        }
+      };
+      // drain deliveries until `want` of each kind (and the epochs) are in
+      auto collect = [&](int want, uint64_t epochs_needed) {
         std::unique_lock<std::mutex> lk(mu);
         while (ok) {
           for (auto& m : got) {
@@ -290,6 +308,7 @@ PYBIND11_MODULE(_qmx, m) {
             } else if (m.type == X_BULK) {
               ++n_bulk;
               const int src = m.bi / o.world;
+              if (!seen_bulk.insert({m.skey, m.bi}).second) ++dups;
               const std::string exp = payload((int)m.skey - 1, src, o.rank, 1);
               std::string have = m.payload;
               if (have.empty() && m.a > 0) {  // RCCL: in the HBM sink
@@ -300,32 +319,59 @@ PYBIND11_MODULE(_qmx, m) {
               if (have != exp) ++bad;
             } else if (m.type == X_SENT) {
               ++n_sent;
+              if (!seen_sent.insert({m.skey, m.bi}).second) ++dups;
             }
           }
           got.clear();
-          if (n_data >= want && n_bulk >= want && n_sent >= want && x.epochs() >= min_epochs) break;
+          if (n_data >= want && n_bulk >= want && n_sent >= want && x.epochs() >= epochs_needed) break;
           if (secs() > wait_s) {
             ok = false;
+            why = "deadline: data " + std::to_string(n_data) + " bulk " + std::to_string(n_bulk) + " sent " +
+                  std::to_string(n_sent) + " of " + std::to_string(want) + ", epochs " + std::to_string(x.epochs());
             break;
           }
           cv.wait_for(lk, std::chrono::milliseconds(20));
         }
+      };
+      const int per = loop1 ? 1 : o.world - 1;
+      send_rounds(0, rounds);
+      collect(rounds * per, min_epochs);
+      if (ok && wave2 > 0) {
+        // the communicator re-formed: the next texts must travel in its rounds again
+        ok = wait_bulk_ready();
+        const uint64_t r0 = x.rounds(), m0 = x.mesh_bulk();
+        send_rounds(rounds, total);
+        collect(total * per, min_epochs);
+        // let the peers finish the rounds that carry our receives' counterparts
+        w2_rounds = x.rounds() - r0;
+        w2_mesh = x.mesh_bulk() - m0;
       }
       wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
       rounds_done = x.rounds();
       mesh_finals = x.mesh_bulk();
       epochs = x.epochs();
-      // linger so peers still waiting for our bytes get them, then stop
+      rescued = x.rescued();
+      // linger so peers still waiting for our bytes (or reports) get them, then stop
       std::this_thread::sleep_for(std::chrono::milliseconds(300));
+      {  // nothing may arrive twice, not even late
+        std::lock_guard<std::mutex> lk(mu);
+        for (auto& m : got) {
+          if (m.type == X_BULK && !seen_bulk.insert({m.skey, m.bi}).second) ++dups;
+          if (m.type == X_SENT && !seen_sent.insert({m.skey, m.bi}).second) ++dups;
+        }
+        got.clear();
+      }
       x.request_stop();
       x.join();
       for (void* p : bufs) hipFree(p);
     }
-    return py::dict(py::arg("ok") = ok && bad == 0, py::arg("bad") = bad, py::arg("rounds") = rounds,
-                    py::arg("data") = n_data, py::arg("bulk") = n_bulk, py::arg("sent") = n_sent,
-                    py::arg("data_wall_us") = data_us, py::arg("wall_s") = wall,
+    return py::dict(py::arg("ok") = ok && bad == 0 && dups == 0, py::arg("bad") = bad, py::arg("dups") = dups,
+                    py::arg("rounds") = rounds, py::arg("data") = n_data, py::arg("bulk") = n_bulk,
+                    py::arg("sent") = n_sent, py::arg("data_wall_us") = data_us, py::arg("wall_s") = wall,
                     py::arg("rccl_rounds") = rounds_done, py::arg("mesh_finals") = mesh_finals,
-                    py::arg("epochs") = epochs);
+                    py::arg("epochs") = epochs, py::arg("wave2_rounds") = w2_rounds,
+                    py::arg("wave2_mesh_finals") = w2_mesh, py::arg("rescued") = rescued,
+                    py::arg("why") = why);
   });
   m.def("stop_server", &stop_server);
   m.def("json_roundtrip", [](const py::bytes& b) -> py::object {

@@ -51,6 +51,12 @@ struct WireEntry {
   uint16_t src_loop, dst_loop;
   uint8_t flags, pad[3];
 };
+// one receive of a round, as its receiver reports it back to the sender
+struct WireAck {
+  uint64_t skey;
+  int32_t bi;
+  uint8_t got, pad[3];
+};
 #pragma pack(pop)
 
 // mesh-internal frame types (never delivered to the io loops)
@@ -62,6 +68,7 @@ enum : uint8_t {
   F_BULK_MESH = 104, // worker → owner: the final text's bytes over the mesh
   F_RCCL_DOWN = 105, // any rank → rank 0: my communicator failed (a = epoch)
   F_ROUND_DONE = 106,  // involved rank → rank 0: round a is over on this rank (either way)
+  F_RECV_REPORT = 107, // receiver → sender: a = round, payload = WireAck per receive (got or missed)
 };
 
 void put_frame(std::string& out, const XMsg& m, const char* payload, size_t n) {
@@ -148,6 +155,22 @@ struct Exchange::Impl {
   std::condition_variable bcv;
   std::map<Key, Send> sends;
   std::map<Key, Sink> sinks;
+  // Sends a round carried, held until the RECEIVER reports the bytes in or missed.  The
+  // sender's own view of a round proves nothing about delivery: its side can complete (bytes
+  // handed to the socket / RCCL FIFO) while the receiver's round fails on a third rank and
+  // throws the bytes away — and the sender could fail while the receiver got everything.
+  // So a send is released (X_SENT) only on the receiver's "got", and resent over the mesh on
+  // its "missed": every final text arrives exactly once whichever side fails.
+  struct Await {
+    Send s;
+    int dst = 0;
+    bool round_over = false;  // the sender's round ended (its executor no longer reads s.dev)
+    bool sender_ok = false;   // ... and succeeded on the sender's side
+    int8_t verdict = -1;      // the receiver's report: -1 not yet, 0 missed, 1 got
+  };
+  std::map<Key, Await> await;
+  std::vector<Send> resend;  // missed by their receiver: over the mesh (bulk thread)
+  std::vector<int> downs_q;  // peers that left the mesh since the bulk thread last looked
   std::deque<Manifest> manifests;
   int pending_epoch = 0;  // bulk thread: (re)form the communicator for this epoch
   std::string pending_id;
@@ -222,6 +245,10 @@ struct Exchange::Impl {
         v[0].type = X_DOWN;
         v[0].a = r;
         X->deliver_(l, std::move(v));
+      }
+      {  // the bulk thread releases the sends that can no longer reach (or be reported by) r
+        std::lock_guard<std::mutex> g(bmu);
+        downs_q.push_back(r);
       }
       bcv.notify_all();  // a bulk round waiting on this peer gives up at once
       if (X->o_.rank == 0 && X->bulk_transport()) rccl_down_everywhere();
@@ -421,10 +448,48 @@ struct Exchange::Impl {
           for (Inflight& f : inflight)
             if (f.round == m.a) f.pending &= ~(1ull << r);
         return;
+      case F_RECV_REPORT: {  // sender: the receiver's verdict on our sends of round a
+        const size_t n = m.payload.size() / sizeof(WireAck);
+        bool wake_bulk = false;
+        {
+          std::lock_guard<std::mutex> g(bmu);
+          for (size_t k = 0; k < n; ++k) {
+            WireAck a;
+            std::memcpy(&a, m.payload.data() + k * sizeof(WireAck), sizeof(a));
+            auto it = await.find({a.skey, a.bi});
+            if (it == await.end()) continue;  // (sent over the mesh already: a fallback manifest)
+            it->second.verdict = a.got ? 1 : 0;
+            if (it->second.round_over) wake_bulk |= settle(it, per);
+          }
+        }
+        if (wake_bulk) bcv.notify_all();
+        return;
+      }
       default:
         (void)r;
         return;
     }
+  }
+  // (bmu held) a carried send whose round is over and whose receiver reported: release it
+  // (X_SENT into `out`, per loop) or queue its mesh resend.  True when a resend was queued.
+  template <class It>
+  bool settle(It it, std::vector<std::vector<XMsg>>& out) {
+    Await& w = it->second;
+    bool rs = false;
+    if (w.verdict == 0) {
+      if (w.sender_ok) X->rescued_++;  // the old sender-side release would have lost it
+      resend.push_back(std::move(w.s));
+      rs = true;
+    } else {
+      XMsg v;
+      v.type = X_SENT;
+      v.skey = it->first.first;
+      v.bi = it->first.second;
+      v.dst_loop = w.s.hdr.src_loop;
+      out[v.dst_loop % X->nloops_].push_back(std::move(v));
+    }
+    await.erase(it);
+    return rs;
   }
   // coordinator: RCCL is unusable (a round failed, a peer left): every rank drops its
   // communicator; a new epoch forms once every rank is up again
@@ -589,7 +654,7 @@ bool Exchange::peer_up(int r) const {
 void Exchange::send_bulk(XMsg&& hdr, const void* dev, size_t len, std::function<std::string()> host) {
   const int dst = hdr.dst_rank;
   // rounds move the bytes (an RCCL round needs them in HBM; tcpbulk reads them on the host)
-  if (rccl_active() && len > 0 && (dev != nullptr || o_.transport == "tcpbulk")) {
+  if (rccl_active() && len > 0 && peer_up(0) && (dev != nullptr || o_.transport == "tcpbulk")) {
     WireEntry e{};
     e.src = o_.rank;
     e.dst = dst;
@@ -615,7 +680,19 @@ void Exchange::send_bulk(XMsg&& hdr, const void* dev, size_t len, std::function<
     a.src_rank = o_.rank;
     a.payload.assign((const char*)&e, sizeof(e));
     im_->enqueue(0, frame(a));
-    return;
+    if (peer_up(0)) return;
+    // rank 0 left between the check and the announcement: the bulk thread's sweep of the
+    // departure may have run before our insert — whoever erases the send ships it
+    Impl::Send s;
+    {
+      std::lock_guard<std::mutex> g(im_->bmu);
+      auto it = im_->sends.find({e.skey, e.bi});
+      if (it == im_->sends.end()) return;
+      s = std::move(it->second);
+      im_->sends.erase(it);
+    }
+    hdr = std::move(s.hdr);
+    host = std::move(s.host);
   }
   // mesh: the bytes ride the owner's connection right behind the stream's deltas
   XMsg m = std::move(hdr);
@@ -812,6 +889,7 @@ struct BulkOp {
   const void* src;  // send: HBM (device executors) or host bytes; nullptr: a vanished send
   std::string host;  // send (host executors): the bytes; receive: filled on completion
   size_t off = 0;    // receive (device executors): staging offset
+  bool done = false; // receive (host executors): its bytes are all in, whatever the round does
 };
 
 struct BulkExec {
@@ -1109,6 +1187,7 @@ class TcpExec : public BulkExec {
       }
       if (in.size() - p - sizeof(x) < x.len) break;
       q.want[q.got]->host.assign(in.data() + p + sizeof(x), x.len);
+      q.want[q.got]->done = true;
       p += sizeof(x) + x.len;
       ++q.got;
     }
@@ -1155,8 +1234,19 @@ void Exchange::bulk_loop() {
     fprintf(stderr, "qmx exchange (rank %d): %s — bulk transfers use the mesh\n", o_.rank, e.what());
     return;
   }
-  int epoch = 0, my_rounds = 0;
+  int epoch = 0;
+  bool stalled = false;
+  // fault injection: every rank of global round N hangs in it (posts nothing) until the
+  // round times out — once per process
   const int stall_round = env_get("QMX_XCHG_FAULT_STALL_ROUND") ? atoi(env_get("QMX_XCHG_FAULT_STALL_ROUND")) : 0;
+  std::vector<std::vector<XMsg>> out(nloops_);
+  auto deliver_all = [&] {
+    for (int l = 0; l < nloops_; ++l)
+      if (!out[l].empty()) {
+        deliver_(l, std::move(out[l]));
+        out[l].clear();
+      }
+  };
   auto drop = [&](bool report) {
     ex->drop();
     rccl_ok_.store(false);
@@ -1168,7 +1258,22 @@ void Exchange::bulk_loop() {
       I.enqueue(0, frame(m));
     }
   };
-  auto mesh_fallback = [&](const WireEntry& e) {
+  // a final text over the mesh, then released to its loop (X_SENT)
+  auto mesh_send = [&](Impl::Send& s) {
+    XMsg m = s.hdr;
+    const uint16_t src_loop = m.src_loop;
+    m.type = F_BULK_MESH;
+    m.payload = s.len ? s.host() : std::string();
+    post(std::move(m));  // (to a peer that left: dropped — X_DOWN failed its sessions)
+    mesh_bulk_++;
+    std::vector<XMsg> v(1);
+    v[0].type = X_SENT;
+    v[0].skey = s.hdr.skey;
+    v[0].bi = s.hdr.bi;
+    v[0].dst_loop = src_loop;
+    deliver_(src_loop % nloops_, std::move(v));
+  };
+  auto mesh_fallback = [&](const WireEntry& e) {  // a send no round carries
     Impl::Send s;
     {
       std::lock_guard<std::mutex> g(I.bmu);
@@ -1177,27 +1282,45 @@ void Exchange::bulk_loop() {
       s = std::move(it->second);
       I.sends.erase(it);
     }
-    XMsg m = s.hdr;
-    m.type = F_BULK_MESH;
-    m.payload = s.len ? s.host() : std::string();
-    post(std::move(m));
-    mesh_bulk_++;
-    std::vector<XMsg> v(1);
-    v[0].type = X_SENT;
-    v[0].skey = e.skey;
-    v[0].bi = e.bi;
-    v[0].dst_loop = e.src_loop;
-    deliver_(e.src_loop % nloops_, std::move(v));
+    mesh_send(s);
+  };
+  // receiver: every receive of a round is reported to its sender, got or missed
+  std::map<int, std::string> rep;
+  auto ack = [&](const WireEntry& e, bool got) {
+    WireAck a{e.skey, e.bi, (uint8_t)(got ? 1 : 0), {0, 0, 0}};
+    rep[e.src].append((const char*)&a, sizeof(a));
+  };
+  auto send_reports = [&](int round) {
+    for (auto& kv : rep) {
+      XMsg m;
+      m.type = F_RECV_REPORT;
+      m.a = round;
+      m.dst_rank = kv.first;
+      m.src_rank = o_.rank;
+      m.payload = std::move(kv.second);
+      I.enqueue(kv.first, frame(m));
+    }
+    rep.clear();
+  };
+  auto round_done = [&](int round) {  // this rank is done with the round: rank 0 may issue another
+    XMsg d;
+    d.type = F_ROUND_DONE;
+    d.a = round;
+    d.dst_rank = 0;
+    d.src_rank = o_.rank;
+    I.enqueue(0, frame(d));
   };
   while (!stop_.load()) {
     Impl::Manifest mf;
     int want_epoch = 0;
     std::string id;
-    bool dropc = false;
+    bool dropc = false, lost_coord = false;
+    std::vector<Impl::Send> rs;
     {
       std::unique_lock<std::mutex> lk(I.bmu);
       I.bcv.wait_for(lk, std::chrono::milliseconds(50), [&] {
-        return stop_.load() || !I.manifests.empty() || I.drop_comm || (I.pending_epoch && I.pending_epoch != epoch);
+        return stop_.load() || !I.manifests.empty() || I.drop_comm || (I.pending_epoch && I.pending_epoch != epoch) ||
+               !I.resend.empty() || !I.downs_q.empty();
       });
       if (stop_.load()) break;
       dropc = I.drop_comm;
@@ -1210,8 +1333,28 @@ void Exchange::bulk_loop() {
         mf = std::move(I.manifests.front());
         I.manifests.pop_front();
       }
+      rs.swap(I.resend);
+      for (int r : I.downs_q) {
+        // a receiver that left can neither take nor report a carried send: release them
+        for (auto it = I.await.begin(); it != I.await.end();) {
+          auto nx = std::next(it);
+          if (it->second.dst == r) {
+            it->second.verdict = 1;
+            if (it->second.round_over) I.settle(it, out);
+          }
+          it = nx;
+        }
+        if (r == 0 && o_.rank != 0) {  // no manifest will come: announced sends take the mesh
+          lost_coord = true;
+          for (auto& kv : I.sends) rs.push_back(std::move(kv.second));
+          I.sends.clear();
+        }
+      }
+      I.downs_q.clear();
     }
-    if (dropc) {
+    deliver_all();
+    for (auto& s : rs) mesh_send(s);
+    if (dropc || lost_coord) {
       drop(false);
       epoch = 0;
     }
@@ -1231,40 +1374,51 @@ void Exchange::bulk_loop() {
     }
     if (mf.es.empty() && !mf.fallback) continue;
     if (mf.fallback || !ex->formed() || mf.epoch != epoch) {
-      for (const WireEntry& e : mf.es)
+      for (const WireEntry& e : mf.es) {
         if (e.src == o_.rank) mesh_fallback(e);
-      // a receive whose sender falls back arrives over the mesh (F_BULK_MESH)
+        // (a fallback manifest goes to senders only; otherwise the sender may be executing
+        // the round: it resends over the mesh on this report)
+        else if (e.dst == o_.rank) ack(e, false);
+      }
+      send_reports(mf.round);
+      if (!mf.fallback) round_done(mf.round);
       continue;
     }
-    // this rank's sends and receives of the round, in manifest order
+    // this rank's sends and receives of the round, in manifest order; the sends move to
+    // `await` until their receivers report
     const double t0 = now_s();
     std::vector<BulkOp> ops;
-    std::vector<Impl::Send> held;  // the sends' state (host producers for a fallback resend)
+    std::vector<Impl::Key> carried;
     ops.reserve(mf.es.size() * 2);
     for (const WireEntry& e : mf.es) {
       if (e.src == o_.rank) {
-        Impl::Send s;
+        const void* dev = nullptr;
+        std::function<std::string()> host;
         {
           std::lock_guard<std::mutex> g(I.bmu);
           auto it = I.sends.find({e.skey, e.bi});
           if (it != I.sends.end()) {
-            s = std::move(it->second);
+            dev = it->second.dev;
+            host = it->second.host;
+            Impl::Await& w = I.await[it->first];
+            w.s = std::move(it->second);
+            w.dst = e.dst;
+            carried.push_back(it->first);
             I.sends.erase(it);
           }
         }
-        BulkOp o{&e, true, s.dev, std::string()};
+        BulkOp o{&e, true, dev, std::string()};
         if (!ex->device()) {
-          if (s.host) o.host = s.host();  // host executor: the engine's bytes (HBM → host for HIP)
-          o.src = s.host ? o.host.data() : nullptr;
+          if (host) o.host = host();  // host executor: the engine's bytes (HBM → host for HIP)
+          o.src = host ? o.host.data() : nullptr;
         }
         ops.push_back(std::move(o));
-        held.push_back(std::move(s));
       }
       if (e.dst == o_.rank) ops.push_back(BulkOp{&e, false, nullptr, std::string()});
     }
     bool ok;
-    if (stall_round > 0 && ++my_rounds == stall_round) {
-      // fault injection: this rank hangs in its round (posts nothing) until the round times out
+    if (stall_round > 0 && mf.round == stall_round && !stalled) {
+      stalled = true;
       fprintf(stderr, "qmx exchange (rank %d): injected stall in round %d\n", o_.rank, mf.round);
       while (now_s() - t0 <= o_.timeout_s && !stop_.load()) std::this_thread::sleep_for(std::chrono::milliseconds(5));
       ok = false;
@@ -1299,65 +1453,68 @@ void Exchange::bulk_loop() {
       }
     }
     busy_us_.store(busy_us_.load() + 1e6 * (now_s() - t0));
-    {  // this rank is done with the round: rank 0 may issue another
-      XMsg d;
-      d.type = F_ROUND_DONE;
-      d.a = mf.round;
-      d.dst_rank = 0;
-      d.src_rank = o_.rank;
-      I.enqueue(0, frame(d));
-    }
+    round_done(mf.round);
     if (!ok) {
       fprintf(stderr, "qmx exchange (rank %d): %s round %d failed — communicator dropped, bulk uses the mesh\n",
               o_.rank, o_.transport.c_str(), mf.round);
       drop(true);
-      {  // resend over the mesh (a receiver may see it twice: it dedups)
-        std::lock_guard<std::mutex> g(I.bmu);
-        size_t k = 0;
-        for (auto& o : ops) {
-          if (!o.send) continue;
-          Impl::Send& s = held[k++];
-          if (s.host) I.sends[{o.e->skey, o.e->bi}] = std::move(s);
+    } else {
+      rounds_++;
+    }
+    // receives: deliver what arrived (all of them, or — a failed round — the transfers a
+    // host executor completed), and tell every sender which of its texts got here
+    for (auto& o : ops) {
+      if (o.send) continue;
+      const WireEntry& e = *o.e;
+      bool got = ok || o.done;
+      if (got) {
+        bulk_bytes_ += e.len;
+        XMsg v;
+        bool deliver = true;
+        if (ex->device()) {
+          std::lock_guard<std::mutex> g(I.bmu);
+          auto it = I.sinks.find({e.skey, e.bi});
+          if (it == I.sinks.end() || !it->second.dev || it->second.cap < e.len) {
+            deliver = false;  // session gone: nobody needs the text (reported got)
+          } else if (!ex->to_sink(o, it->second.dev)) {
+            // HBM → HBM into the owner's shadow slot; complete before the lock drops, so a
+            // forget_bulk() that returns guarantees no later write into a released slot
+            deliver = got = false;  // (the sender resends over the mesh)
+          }
+        } else {
+          v.payload = std::move(o.host);  // host executor: the bytes ride the delivery
+        }
+        if (deliver) {
+          v.type = X_BULK;
+          v.flags = e.flags;
+          v.skey = e.skey;
+          v.bi = e.bi;
+          v.a = (int32_t)e.len;  // device executors: already in the owner's HBM content arena
+          v.b = e.b;
+          v.src_rank = e.src;
+          v.dst_loop = e.dst_loop;
+          out[e.dst_loop % nloops_].push_back(std::move(v));
         }
       }
-      for (auto& o : ops)
-        if (o.send) mesh_fallback(*o.e);
-      continue;
+      ack(e, got);
     }
-    rounds_++;
-    for (auto& o : ops) {
-      const WireEntry& e = *o.e;
-      bulk_bytes_ += e.len;
-      if (o.send) {
-        std::vector<XMsg> v(1);
-        v[0].type = X_SENT;
-        v[0].skey = e.skey;
-        v[0].bi = e.bi;
-        v[0].dst_loop = e.src_loop;
-        deliver_(e.src_loop % nloops_, std::move(v));
-        continue;
+    deliver_all();
+    send_reports(mf.round);
+    // our sends: the round is over; each is settled by its receiver's report
+    bool wake = false;
+    {
+      std::lock_guard<std::mutex> g(I.bmu);
+      for (const Impl::Key& k : carried) {
+        auto it = I.await.find(k);
+        if (it == I.await.end()) continue;
+        if (ok) bulk_bytes_ += it->second.s.len;
+        it->second.round_over = true;
+        it->second.sender_ok = ok;
+        if (it->second.verdict >= 0) wake |= I.settle(it, out);
       }
-      std::vector<XMsg> v(1);
-      if (ex->device()) {
-        std::lock_guard<std::mutex> g(I.bmu);
-        auto it = I.sinks.find({e.skey, e.bi});
-        if (it == I.sinks.end() || !it->second.dev || it->second.cap < e.len) continue;  // session gone
-        // HBM → HBM into the owner's shadow slot; complete before the lock drops, so a
-        // forget_bulk() that returns guarantees no later write into a released slot
-        if (!ex->to_sink(o, it->second.dev)) continue;
-      } else {
-        v[0].payload = std::move(o.host);  // host executor: the bytes ride the delivery
-      }
-      v[0].type = X_BULK;
-      v[0].flags = e.flags;
-      v[0].skey = e.skey;
-      v[0].bi = e.bi;
-      v[0].a = (int32_t)e.len;  // device executors: already in the owner's HBM content arena
-      v[0].b = e.b;
-      v[0].src_rank = e.src;
-      v[0].dst_loop = e.dst_loop;
-      deliver_(e.dst_loop % nloops_, std::move(v));
     }
+    deliver_all();
+    (void)wake;  // (queued resends are taken at the top of the loop)
   }
   ex.reset();
 }

@@ -117,6 +117,9 @@ class Exchange {
   uint64_t rejoins() const { return rejoins_.load(); }      // peer (re)connections after the first
   uint64_t downs() const { return downs_.load(); }          // live peer connections lost
   double busy_us() const { return busy_us_.load(); }        // time inside RCCL rounds
+  // texts a round carried whose sender finished the round but whose receiver missed them
+  // (it failed the round on another peer): resent over the mesh on the receiver's report
+  uint64_t rescued() const { return rescued_.load(); }
 
   struct Impl;
 
@@ -127,7 +130,7 @@ class Exchange {
   std::unique_ptr<Impl> im_;
   std::atomic<bool> stop_{false}, healthy_{false}, rccl_ok_{false};
   std::atomic<uint64_t> rounds_{0}, bytes_{0}, bulk_bytes_{0}, mesh_bulk_{0}, msgs_{0}, rccl_epoch_{0}, rejoins_{0},
-      downs_{0};
+      downs_{0}, rescued_{0};
   std::atomic<double> busy_us_{0};
   std::thread mesh_th_, bulk_th_;
   void mesh_loop();

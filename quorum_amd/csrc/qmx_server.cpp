@@ -2897,6 +2897,7 @@ class Loop {
       put("qmx_exchange_bulk_bytes_total", (double)xch_->bulk_bytes());  // final texts, HBM to HBM
       put("qmx_exchange_mesh_finals_total", (double)xch_->mesh_bulk());  // final texts over the mesh
       put("qmx_exchange_epochs_total", (double)xch_->epochs());
+      put("qmx_exchange_rescued_total", (double)xch_->rescued());  // resent on the receiver's report
       put("qmx_exchange_rejoins_total", (double)xch_->rejoins());
       put("qmx_exchange_peer_downs_total", (double)xch_->downs());
       put("qmx_exchange_busy_us_total", xch_->busy_us());

@@ -294,17 +294,25 @@ def test_exchange_bulk_rounds_tcpbulk(world):
         assert v["rccl_rounds"] > 0 and v["mesh_finals"] == 0 and v["epochs"] >= 1
 
 
-def test_exchange_bulk_round_stall_falls_back_and_reforms():
-    """Fault injection: every rank hangs in its 3rd round (QMX_XCHG_FAULT_STALL_ROUND): the
-    round times out, the communicator is dropped everywhere, that round's texts are resent
-    over the mesh — every byte still arrives exactly once-checked — and rank 0 re-forms a
-    new epoch over which the later rounds run again."""
-    res = _selftest(3, "tcpbulk", 40, env={"QMX_XCHG_FAULT_STALL_ROUND": "3"}, round_timeout=0.5, min_epochs=2)
+@pytest.mark.parametrize("world", [3, 4])
+def test_exchange_bulk_round_stall_falls_back_and_reforms(world):
+    """Fault injection: every rank of global round 3 hangs in it (QMX_XCHG_FAULT_STALL_ROUND;
+    the sends are paced 3 ms apart so there are many rounds): the round times out, the
+    communicator is dropped everywhere, the texts its receivers missed are resent over the
+    mesh on their receivers' reports, and rank 0 re-forms a new epoch.  Every text must
+    arrive exactly once and byte-exact — including texts whose SENDER finished the round
+    while their receiver failed it on a third rank (the round-3 loss: before receiver reports
+    the sender released those as sent and they vanished).  A second wave sent after the
+    re-formed epoch must travel in its rounds again, with no mesh fallback."""
+    res = _selftest(world, "tcpbulk", 24, env={"QMX_XCHG_FAULT_STALL_ROUND": "3"}, round_timeout=0.5,
+                    min_epochs=2, pace_ms=3.0, wave2=12)
     assert all(v["ok"] for v in res.values()), res
     for v in res.values():
-        assert v["bad"] == 0
+        assert v["bad"] == 0 and v["dups"] == 0
+        assert v["bulk"] == v["sent"] == 36 * (world - 1)
         assert v["mesh_finals"] > 0          # the stalled round's texts took the mesh
         assert v["epochs"] >= 2              # a new communicator formed after the failure
+        assert v["wave2_rounds"] > 0 and v["wave2_mesh_finals"] == 0, v  # ... and carries traffic
 
 
 def test_idle_cluster_exchanges_nothing():
