@@ -379,6 +379,25 @@ def breakdown(m0, m1, elapsed):
                              for k, v in d.items() if k.startswith("qmx_syscalls_total")}
         if d.get("qmx_requests_total") else {},
         "exchange_rounds": int(d.get("qmx_exchange_rounds_total", 0.0)),
+        # spread placement (EP): how the remote streams' finals moved — bulk rounds (RCCL
+        # ncclSend/ncclRecv HBM -> HBM, or tcpbulk in rehearsals) vs the mesh — what the rounds
+        # cost, and whether the owner finalized them on the GPU (HBM-resident / staged texts)
+        "exchange": ({"remote_streams": int(d.get("qmx_remote_streams_total", 0.0)),
+                      "bulk_rounds": int(d.get("qmx_exchange_rounds_total", 0.0)),
+                      "round_us_avg": (round(d.get("qmx_exchange_busy_us_total", 0.0)
+                                             / d["qmx_exchange_rounds_total"], 1)
+                                       if d.get("qmx_exchange_rounds_total") else None),
+                      "bulk_final_MB": round(d.get("qmx_exchange_bulk_bytes_total", 0.0) / 1e6, 3),
+                      "eager_finals": int(d.get("qmx_spread_eager_finals_total", 0.0)),
+                      "mesh_finals": int(d.get("qmx_exchange_mesh_finals_total", 0.0)),
+                      "rescued": int(d.get("qmx_exchange_rescued_total", 0.0)),
+                      "epochs": int(d.get("qmx_exchange_epochs_total", 0.0)),
+                      "delta_mismatch": int(d.get("qmx_spread_delta_mismatch_total", 0.0)),
+                      "worker_nodata": int(d.get("qmx_spread_worker_nodata_total", 0.0)),
+                      "remote_texts_hbm": int(d.get("qmx_kernel_remote_texts_hbm", 0.0)),
+                      "remote_texts_staged": int(d.get("qmx_kernel_remote_texts_staged", 0.0)),
+                      "hops_us": hop_means(d)}
+                     if d.get("qmx_remote_streams_total") else None),
         # where a request's time goes (server-side means over the timed region): upstream
         # TTFB (request sent -> first response bytes), engine wait (a stream's first bytes fed
         # -> its final result in the io loop: lane queueing + tick + routing), TTFT and whole
@@ -419,7 +438,8 @@ def compact_breakdown(rank: int, bd: dict, row) -> dict:
     return {"rank": rank, "pid": bd.get("pid"), "requests": int(row[1]), "req_s": round(row[1] / row[0], 1) if row[0] else None,
             "p50_ttft_ms": round(row[2], 3), "ticks": bd.get("ticks"), "streams_per_tick": bd.get("streams_per_tick"),
             "tick_kernel_us_avg": bd.get("tick_kernel_us_avg"), "tick_wall_us_avg": bd.get("tick_wall_us_avg"),
-            "engine_wait_us": lat.get("engine_wait"), "proxy_cpu_ms_per_1k_req": bd.get("proxy_cpu_ms_per_1k_req")}
+            "engine_wait_us": lat.get("engine_wait"), "proxy_cpu_ms_per_1k_req": bd.get("proxy_cpu_ms_per_1k_req"),
+            "finalize_host": bd.get("finalize_host"), "exchange": bd.get("exchange")}
 
 
 def spread_summary(rows) -> dict:
@@ -624,23 +644,40 @@ def run_set(ctx, label, placement, port, admin, xenv, passes, want_bulk=False) -
     for name, conns, n in passes:
         if not up:
             break
+        # a pass's counters are this rank's deltas, but its sessions shard over every rank's
+        # proxy (SO_REUSEPORT) and their streams spread over the ranks: every rank takes its
+        # baseline before any rank's load starts, and its final scrape before any rank's
+        # next pass does (a fast rank's probe would otherwise land in a slow rank's load)
         st, m0 = None, scrape(admin)
+        torch_min_flag(dist, True, on_gpu)
         try:
             st = loadgen(ctx["bin_dir"], port, conns, n, min(2, conns), 120, ctx["spec"])
         except Exception as e:  # noqa: BLE001
             err = repr(e)[:300]
         up = torch_min_flag(dist, err is None, on_gpu)  # every rank's pass is done
+        time.sleep(0.1)
+        m1 = scrape(admin)
+        torch_min_flag(dist, True, on_gpu)
         if st is not None:
-            time.sleep(0.1)
-            d = {k: v - m0.get(k, 0.0) for k, v in scrape(admin).items()}
+            d = {k: v - m0.get(k, 0.0) for k, v in m1.items()}
             res[name] = {"ok": st["invalid"] == 0 and st["errors"] == 0 and st["completed"] == n,
                          "requests": st["completed"], "invalid": st["invalid"], "errors": st["errors"],
                          "p50_latency_ms": st["lat_p50_ms"], "p50_ttft_ms": st["ttft_p50_ms"], "req_s": st["rps"]}
             if placement == "spread":
                 res[name].update(spread_counters(d))
+                # validated bytes are not enough: a delta-count mismatch or a worker stream that
+                # sent nothing for its content breaks the spread invariants
+                if res[name]["delta_mismatch"] or res[name]["worker_nodata"]:
+                    res[name]["ok"] = False
     _kill(procs)
     if err is None and not up:
         err = f"another rank's {label} set failed"
+    if err is None and want_bulk:
+        # the rendezvous set exists to run the round protocol: no communicator or no round
+        # on this rank is a failure, not a silent mesh fallback
+        rounds = sum((res.get(p[0]) or {}).get("bulk_rounds", 0) for p in passes)
+        if not res.get("bulk_formed") or rounds <= 0:
+            err = f"{label}: bulk rounds did not run (formed {res.get('bulk_formed')}, rounds {rounds})"
     res["ok"] = err is None and all((res.get(p[0]) or {}).get("ok") for p in passes)
     if err:
         res["error"] = err
@@ -742,6 +779,10 @@ def main() -> int:
                     help="N > 1: after the timed steps, validate spread placement (RCCL finals) end to end")
     ap.add_argument("--placement", default="local", choices=["local", "spread"],
                     help="spread: a session's backend streams run on consecutive ranks (RCCL exchange)")
+    ap.add_argument("--eager-bytes", type=int, default=-1,
+                    help="spread: final texts up to this size ride the mesh behind their deltas (-1: the "
+                         "production default, 4 KiB); 0 sends every remote final text through a bulk round "
+                         "(RCCL ncclSend/ncclRecv HBM -> HBM on GPUs; tcpbulk when ranks share a GPU)")
     args = ap.parse_args()
     env_world = os.environ.get("WORLD_SIZE")
     if args.gpus is not None and args.gpus > 1 and env_world is None:
@@ -822,10 +863,19 @@ def main() -> int:
         env = dict(os.environ)
         if n_dev:  # processes sharing this rank's GPU (persistent tick grids need it alone)
             env["QMX_GPU_SHARERS"] = str(max(1, -(-int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) // n_dev)))
+        xchg_kind = None
         if args.placement == "spread" and world > 1:
             nonce = [str(time.time_ns()) if rank == 0 else None]
             dist.broadcast_object_list(nonce, src=0)
             env.update(exchange_env(rank, world, args.port, nonce[0]))
+            # RCCL needs one GPU per rank: ranks sharing a GPU (a rehearsal) run the same bulk
+            # rounds with the socket executor
+            xchg_kind = os.environ.get("QMX_XCHG") or ("rccl" if n_dev >= world and engine == "hip" else "tcpbulk")
+            if xchg_kind == "rccl" and not (n_dev >= world and engine == "hip"):
+                xchg_kind = "tcpbulk"
+            env["QMX_XCHG"] = xchg_kind
+            if args.eager_bytes >= 0:
+                env["QMX_XCHG_EAGER_BYTES"] = str(args.eager_bytes)
         mock_procs = list(procs)
         proxy_port = args.port
         # this rank's own proxy process answers on admin_port (no SO_REUSEPORT): its ready
@@ -853,8 +903,15 @@ def main() -> int:
                 up = wait_healthy("127.0.0.1", admin_port, 30)
         if not up:
             raise RuntimeError(f"proxy did not become ready: {[exit_status(p) for p in proxy_procs]}")
-        xchg_kind = os.environ.get("QMX_XCHG", "rccl" if engine == "hip" else "tcp")
         _trace("healthy")
+        if xchg_kind in ("rccl", "tcpbulk"):
+            # the bulk executor (RCCL communicator / tcpbulk sockets) formed on this rank before
+            # anything is timed: a round-carried final must not fall back to the mesh for want of it
+            t_b = time.time()
+            while scrape(admin_port).get("qmx_exchange_rccl_active") != 1.0:
+                if time.time() - t_b > 90:
+                    raise RuntimeError(f"spread: the {xchg_kind} bulk executor did not form in 90 s")
+                time.sleep(0.2)
         if dist is not None:
             _barrier(dist, coll_cuda)
         # the reference has no /v1 prefix (oai_proxy.py:959); qmx serves both
@@ -897,6 +954,10 @@ def main() -> int:
         bad = (stats["invalid"] + stats["no_content"] + stats["errors"] + stats["non200"]
                + warm.get("invalid", 0) + warm.get("errors", 0) + warm.get("non200", 0) + len(dead)
                + (args.steps * args.batch - stats["completed"]))
+        if args.placement == "spread" and bd.get("exchange"):
+            # a remote stream whose delta count disagrees with its worker's, or a worker stream
+            # that sent no delta for content it had, is a broken run even if the bytes validated
+            bad += int(bd["exchange"]["delta_mismatch"] + bd["exchange"]["worker_nodata"])
         spread = None
         if (dist is not None and world > 1 and args.spread_check and args.impl == "native"
                 and args.placement == "local"):

@@ -106,6 +106,18 @@ void bind_engine(py::class_<E>& c) {
         e.settle(taken);
       })
       .def("text", [](E& e, int slot) { return py::bytes(e.text(slot)); })
+      // spread owner's shadow slot: its HBM content area (0: none) and a remote final text —
+      // `data` None: already written into that area (an RCCL round), bytes: over the mesh
+      .def("content_device_ptr", [](E& e, int slot) {
+        size_t cap = 0;
+        void* p = e.content_device_ptr(slot, &cap);
+        return py::make_tuple((uintptr_t)p, cap);
+      })
+      .def("set_remote_content", [](E& e, int slot, const py::object& data, size_t len) {
+        if (data.is_none()) return e.set_remote_content(slot, nullptr, len);
+        std::string b = py::cast<std::string>(py::bytes(data));
+        e.set_remote_content(slot, &b, b.size());
+      })
       .def("stats", &E::stats);
 }
 
@@ -372,6 +384,74 @@ PYBIND11_MODULE(_qmx, m) {
                     py::arg("epochs") = epochs, py::arg("wave2_rounds") = w2_rounds,
                     py::arg("wave2_mesh_finals") = w2_mesh, py::arg("rescued") = rescued,
                     py::arg("why") = why);
+  });
+  // One-rank RCCL rounds into given HBM sinks (GPU tests of the owner's remote-final path):
+  // each payload is copied to a fresh device buffer and sent with send_bulk into its sink
+  // through the exchange's own manifests / epoch / ncclSend+ncclRecv rounds.
+  m.def("rccl_deliver", [](const py::dict& d, const py::list& items) {
+    XOptions o;
+    o.transport = "rccl";
+    if (d.contains("port")) o.port = py::cast<int>(d["port"]);
+    if (d.contains("device")) o.device = py::cast<int>(d["device"]);
+    const double wait_s = d.contains("timeout") ? py::cast<double>(d["timeout"]) : 60.0;
+    std::vector<std::pair<uintptr_t, std::string>> v;
+    for (auto it : items) {
+      py::tuple t = py::cast<py::tuple>(it);
+      v.emplace_back(py::cast<uintptr_t>(t[0]), py::cast<std::string>(t[1]));
+    }
+    int got = 0, sent = 0;
+    uint64_t rounds = 0, mesh = 0;
+    bool ok = true;
+    {
+      py::gil_scoped_release nogil;
+      std::mutex mu;
+      std::condition_variable cv;
+      Exchange x(o, 1, [&](int, std::vector<XMsg>&& ms) {
+        std::lock_guard<std::mutex> g(mu);
+        for (auto& m : ms) {
+          if (m.type == X_BULK) ++got;
+          if (m.type == X_SENT) ++sent;
+        }
+        cv.notify_all();
+      });
+      const auto t0 = std::chrono::steady_clock::now();
+      auto secs = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
+      while (ok && (!x.healthy() || !x.rccl_active())) {
+        if (secs() > wait_s) ok = false;
+        std::this_thread::sleep_for(std::chrono::milliseconds(5));
+      }
+      std::vector<void*> bufs;
+      for (size_t i = 0; i < v.size() && ok; ++i) {
+        x.expect_bulk(1000 + i, 0, (void*)v[i].first, v[i].second.size());
+        void* src = nullptr;
+        if (hipSetDevice(o.device) != hipSuccess || hipMalloc(&src, std::max<size_t>(v[i].second.size(), 16)) != hipSuccess ||
+            hipMemcpy(src, v[i].second.data(), v[i].second.size(), hipMemcpyHostToDevice) != hipSuccess) {
+          ok = false;
+          break;
+        }
+        bufs.push_back(src);
+        XMsg h;
+        h.skey = 1000 + i;
+        h.bi = 0;
+        h.flags = XF_TEXT;
+        std::string b = v[i].second;
+        x.send_bulk(std::move(h), src, b.size(), [b] { return b; });
+      }
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        while (ok && (got < (int)v.size() || sent < (int)v.size())) {
+          if (secs() > wait_s) ok = false;
+          cv.wait_for(lk, std::chrono::milliseconds(20));
+        }
+      }
+      rounds = x.rounds();
+      mesh = x.mesh_bulk();
+      x.request_stop();
+      x.join();
+      for (void* p : bufs) hipFree(p);
+    }
+    return py::dict(py::arg("ok") = ok, py::arg("bulk") = got, py::arg("sent") = sent, py::arg("rounds") = rounds,
+                    py::arg("mesh_finals") = mesh);
   });
   m.def("stop_server", &stop_server);
   m.def("json_roundtrip", [](const py::bytes& b) -> py::object {

@@ -115,8 +115,12 @@ struct FinItem {
   uint32_t seg_off, seg_cap;        // kept-segment scratch (device), entries
   uint32_t tl_off;                  // texts-kind: per-text stripped lengths at text_len[tl_off..]
 };
+// in_off != kNoStage: the text arrived on the host (a spread worker's final over the mesh);
+// its bytes are staged at fin_in[in_off] (host-mapped) and the item first copies them into
+// the slot's HBM content area, then reads them from there like any other text
+constexpr uint32_t kNoStage = 0xFFFFFFFFu;
 struct FinText {
-  uint32_t slot, len;
+  uint32_t slot, len, in_off, pad;
 };
 struct FinResult {
   uint32_t out_len, status, n_kept;  // status 1: escalate to the host path
@@ -164,7 +168,8 @@ class HipGrid {
   void calibrate_locked();
   std::atomic<double> clk_off_us_{__builtin_nan("")};
   bool interleave_ = true;  // doors' sub-grids XCD-local (blocks d, d + doors, ...)
-  double clk_rtt_us_ = 0, last_cal_ = 0;
+  // written by calibrate_locked (exclusive lock); read lock-free by housekeep() / stats()
+  std::atomic<double> clk_rtt_us_{0.0}, last_cal_{0.0};
   int device_, n_, wpd_, idle_ms_;
   std::shared_mutex mu_;
   std::atomic<bool> running_{false};
@@ -251,6 +256,7 @@ struct TickLane {
   uint8_t* d_segs = nullptr;  // int2 entries
   size_t segs_cap = 0;        // bytes
   uint64_t fin_launches = 0, fin_items = 0, fin_host = 0;  // launches that carried finalize work
+  uint64_t fin_staged = 0;  // mesh-delivered remote texts staged into finalize items
   // completion by polling the kernel-published sequence numbers (HipEngine::wait_results)
   uint32_t seq = 0;
   double ema_us = 40.0;  // launch-to-results time, smoothed
@@ -344,9 +350,13 @@ class HipEngine : public HostEngine {
   uint8_t* d_content_ = nullptr;
   // host mirrors (per slot; a slot is only touched by the lane it is busy on)
   std::vector<uint8_t> host_mode_;       // slot escalated to the host path
+  // spread owner: a remote stream's final text that came over the mesh, held in the slot's
+  // SlotCore::content and staged into the finalize item that reads it (fin_body copies it to
+  // HBM) — no synchronous copy in the io loop, no host finalize
+  std::vector<uint8_t> remote_host_;
   std::vector<uint32_t> content_len_;    // device content bytes per slot
   // stats
-  std::atomic<uint64_t> escalations_{0}, fin_host_{0};
+  std::atomic<uint64_t> escalations_{0}, fin_host_{0}, remote_dev_{0}, remote_staged_{0};
   int spin_us_ = 0;  // QMX_WAIT_SPIN_US: yield-poll before the blocking wait
   bool poll_ = true;  // QMX_WAIT=event: wait on a blocking-sync HIP event instead of polling
   int poll_us_ = 1;   // QMX_POLL_US: poll period once the expected kernel time has passed (MI355X A/Bs: 2 beats 6, 1 beats 2)
@@ -362,8 +372,6 @@ class HipEngine : public HostEngine {
 
  public:
   bool persistent() const { return persistent_; }
-  // off for spread placement: remote final texts land in the content arena by RCCL / DMA,
-  // outside the grid's release / acquire protocol
   void set_persistent(bool on);
 };
 

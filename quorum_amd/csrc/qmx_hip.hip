@@ -75,8 +75,8 @@ __device__ __forceinline__ void dbg_put(unsigned long long* p, unsigned long lon
   *(__attribute__((address_space(1))) unsigned long long*)p = v;
 }
 // s_waitcnt vmcnt(0) (expcnt and lgkmcnt left alone): this wave's vector memory accesses,
-// stores included, have completed
-__device__ __forceinline__ void wave_stores_done() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+// stores included, have completed; a compiler barrier too, so no store is moved past it
+__device__ __forceinline__ void wave_stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 #define QMX_STAMP(k)                                               \
   do {                                                             \
     if (P.dbg != nullptr && threadIdx.x == 0)                      \
@@ -2086,6 +2086,28 @@ struct FinArgs {
   int2* segs;              // device kept-segment scratch
 };
 
+// Spread owner: final texts that came over the mesh are staged in the host-mapped finalize
+// input (FinText::in_off).  Copy them into their shadow slots' HBM content areas first —
+// coalesced 16-B loads, one pass over PCIe — so fin_body reads every text from HBM alike.
+// (The writes are this workgroup's own, read back by it after the barrier: one CU, one L1.)
+__device__ __forceinline__ void fin_stage(const FinArgs& fa, int j, uint8_t* __restrict__ content,
+                                          uint32_t content_cap) {
+  const int tid = opaque_tid();
+  const FinItem it = fa.items[j];
+  bool any = false;
+  for (uint32_t i = 0; i < it.n_texts; ++i) {
+    const FinText ft = fa.texts[it.first_text + i];
+    if (ft.in_off == kNoStage || ft.len == 0) continue;
+    any = true;
+    const uint8_t* src = fa.fin_in + ft.in_off;
+    uint8_t* dst = content + (size_t)ft.slot * content_cap;
+    const int nv = ((uintptr_t)dst & 15) == 0 ? (int)(ft.len / 16) : 0;
+    for (int k = tid; k < nv; k += BS) ((uint4*)dst)[k] = ((const uint4*)src)[k];
+    for (int k = nv * 16 + tid; k < (int)ft.len; k += BS) dst[k] = src[k];
+  }
+  if (any) __syncthreads();  // (any is block-uniform)
+}
+
 __device__ __forceinline__ void fin_body(const FinArgs& fa, int j, const uint8_t* __restrict__ content, uint32_t content_cap,
                          const TagSet& ts_mem, FinShared& F) {
   const int tid = opaque_tid();
@@ -2236,11 +2258,12 @@ __device__ __forceinline__ void fin_body(const FinArgs& fa, int j, const uint8_t
 // ------------------------------------------------------------------------------------
 // the fused kernel: workgroups [0, n_tick) run one stream tile each, [n_tick, grid) one
 // finalize request each — one launch per tick for both (their LDS overlays: a workgroup is
-// one or the other).  Every workgroup publishes its result record last: all threads fence
-// their host-mapped stores (output, result record) at system scope, then thread 0 stores the
-// tick's sequence number into the record.  The host polls these sequence numbers instead of
-// waiting on a HIP event (no interrupt round trip, no HSA spin-wait per tick).  Every early
-// exit of tick_body / fin_body is block-uniform, so every thread reaches the fence.
+// one or the other).  Every workgroup publishes its result record last: every wave waits for
+// its own stores (output, content, state, result record), a barrier, then thread 0 stores the
+// tick's sequence number with a system-scope release (one L2 write-back per item).  The host
+// polls these sequence numbers instead of waiting on a HIP event (no interrupt round trip, no
+// HSA spin-wait per tick).  Every early exit of tick_body / fin_body is block-uniform, so
+// every thread reaches the barrier.
 // ------------------------------------------------------------------------------------
 union TickLds {
   TickShared t;
@@ -2262,18 +2285,22 @@ __device__ __forceinline__ void run_item(int k, const WorkItem* __restrict__ ite
       res[k].t0 = t0;
       res[k].t1 = __builtin_amdgcn_s_memrealtime();
     }
-    __threadfence_system();
+    // publish: every wave waits for its OWN stores (output, content, slot state, the record),
+    // then the barrier, then ONE system-scope release by thread 0 (one L2 write-back per
+    // item; a __threadfence_system() per thread was one per wave, nine per item)
+    wave_stores_done();
     __syncthreads();
     if (Pk.dbg != nullptr && threadIdx.x == 0) dbg_put(&Pk.dbg[k * kDbg + 27], __builtin_amdgcn_s_memrealtime());
     if (threadIdx.x == 0) __hip_atomic_store(&res[k].seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   } else {
     const int j = (int)(k - n_tick);
+    fin_stage(fa, j, content, Pk.content_cap);
     fin_body(fa, j, content, Pk.content_cap, Pk.ts, U.f);
     if (threadIdx.x == 0) {
       fa.res[j].t0 = t0;
       fa.res[j].t1 = __builtin_amdgcn_s_memrealtime();
     }
-    __threadfence_system();
+    wave_stores_done();
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(&fa.res[j].seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -2763,6 +2790,7 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
     lanes_.push_back(std::move(L));
   }
   host_mode_.assign(max_slots_, 0);
+  remote_host_.assign(max_slots_, 0);
   content_len_.assign(max_slots_, 0);
 }
 
@@ -2908,6 +2936,7 @@ void HipEngine::build_params(TickLane& L, int64_t created) {
 void HipEngine::on_free(int slot) {
   if (slot >= 0 && slot < max_slots_) {
     host_mode_[slot] = 0;
+    remote_host_[slot] = 0;
     content_len_[slot] = 0;
   }
 }
@@ -2930,33 +2959,33 @@ void* HipEngine::content_device_ptr(int slot, size_t* cap) {
 
 size_t HipEngine::content_size(int slot) {
   if (slot < 0 || slot >= (int)nslots()) return 0;
-  if (slot >= max_slots_ || host_mode_[slot]) return core_[slot].content.size();
+  if (slot >= max_slots_ || host_mode_[slot] || remote_host_[slot]) return core_[slot].content.size();
   return content_len_[slot];
 }
 
-// Spread placement: a remote stream's final text in this (owner) rank's shadow slot.  From
-// RCCL it is already in the slot's HBM area (bytes == nullptr); over the mesh it is copied
-// there (or kept on the host when it does not fit), so the fused finalize reads it like
-// any local stream.
+// Spread placement: a remote stream's final text in this (owner) rank's shadow slot, which is
+// never fed upstream bytes and is finalized on the GPU like any local stream:
+//  * RCCL (bytes == nullptr): the round already wrote it into the slot's HBM content area —
+//    its stream was synchronised before the exchange delivered X_BULK, and the finalize that
+//    reads it goes out in a later tick, whose items start with a system-scope acquire (the
+//    running grid sees it like the host-written tile bytes);
+//  * the mesh (bytes): kept with the slot and staged into the finalize item's host-mapped
+//    input (prep_finalize), which the item copies into the HBM area first (fin_stage) — no
+//    synchronous copy in the io loop;
+//  * a text longer than the slot's HBM area takes the host path.
 void HipEngine::set_remote_content(int slot, const std::string* bytes, size_t len) {
   if (slot < 0 || slot >= (int)nslots()) return;
-  if (grid_) {
-    // loop ticks: the grid runs on while a remote text lands in HBM by RCCL (or would by a
-    // DMA copy), outside the release / acquire protocol its items use — so the text is kept
-    // on the host, and the session's finalize takes the host path (prep_finalize), reading
-    // nothing of it from the content arena
-    core_[slot].content = bytes ? *bytes : device_content(slot, (uint32_t)len);
-    if (slot < max_slots_) host_mode_[slot] = 1;
-    return;
-  }
-  if (slot >= max_slots_ || (bytes && len > content_cap_)) {
+  if (slot >= max_slots_ || len > content_cap_) {
     if (slot < max_slots_) host_mode_[slot] = 1;
     core_[slot].content = bytes ? *bytes : std::string();
     return;
   }
-  if (bytes && len) {
-    HIP_CHECK(hipSetDevice(device_));
-    HIP_CHECK(hipMemcpy(d_content_ + (size_t)slot * content_cap_, bytes->data(), len, hipMemcpyHostToDevice));
+  if (bytes) {
+    core_[slot].content = *bytes;
+    remote_host_[slot] = 1;
+    ++remote_staged_;
+  } else {
+    ++remote_dev_;
   }
   content_len_[slot] = (uint32_t)len;
 }
@@ -2973,7 +3002,8 @@ void HipEngine::escalate(int slot, bool fresh) {
   } else {
     c.fs = FilterState();
   }
-  c.content = device_content(slot, content_len_[slot]);
+  if (!remote_host_[slot]) c.content = device_content(slot, content_len_[slot]);
+  remote_host_[slot] = 0;
   host_mode_[slot] = 1;
   ++escalations_;
 }
@@ -2982,7 +3012,7 @@ std::string HipEngine::text(int slot) {
   if (slot < 0 || slot >= (int)nslots()) return std::string();
   const SlotCore& c = core_[slot];
   if (c.aborted) return std::string();
-  if (slot >= max_slots_ || host_mode_[slot]) return c.content;
+  if (slot >= max_slots_ || host_mode_[slot] || remote_host_[slot]) return c.content;
   return device_content(slot, content_len_[slot]);
 }
 
@@ -3561,6 +3591,8 @@ std::vector<const FinalizeReq*> HipEngine::prep_finalize(TickLane& L, std::vecto
     gpu.push_back(&r);
     ntext += r.slots.size();
     in_bytes += ((r.joiner.size() + 15) & ~(size_t)15) + 256 + 64;
+    for (int s : r.slots)
+      if (remote_host_[s] && !core_[s].aborted) in_bytes += (content_len_[s] + 15) & ~(size_t)15;
   }
   if (gpu.empty()) return gpu;
   const int n = (int)gpu.size();
@@ -3580,7 +3612,14 @@ std::vector<const FinalizeReq*> HipEngine::prep_finalize(TickLane& L, std::vecto
     it.tl_off = (uint32_t)t_off;
     for (int s : r.slots) {
       const uint32_t len = core_[s].aborted ? 0u : content_len_[s];
-      L.h_fint[t_off++] = FinText{(uint32_t)s, len};
+      uint32_t stage = kNoStage;
+      if (remote_host_[s] && len) {  // a mesh-delivered final: the item copies it to HBM first
+        stage = (uint32_t)in_off;
+        std::memcpy(L.h_fin_in + in_off, core_[s].content.data(), len);
+        in_off += (len + 15) & ~(size_t)15;
+        ++L.fin_staged;
+      }
+      L.h_fint[t_off++] = FinText{(uint32_t)s, len, stage, 0};
       total += len;
       longest = std::max(longest, (size_t)len);
     }
@@ -3687,6 +3726,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["poll_fallbacks"] += (double)L.poll_fallbacks;
     m["fin_launches"] += (double)L.fin_launches;  // tick launches that also carried finalize work
     m["fin_items"] += (double)L.fin_items;
+    m["fin_staged_texts"] += (double)L.fin_staged;  // mesh-delivered remote finals staged into items
     for (int k = 1; k < 21; ++k) stage[k] += L.stage_us[k];
     cyc += L.clk_cycles;
     cus += L.clk_us;
@@ -3707,6 +3747,8 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   m["clk_us"] = cus;
   m["escalations"] = (double)escalations_.load();
   m["fin_host"] = (double)fin_host_.load();
+  m["remote_texts_hbm"] = (double)remote_dev_.load();        // spread owner: finals an RCCL round put in HBM
+  m["remote_texts_staged"] = (double)remote_staged_.load();  // ... that came over the mesh
   m["lanes"] = (double)lanes_.size();
   m["fin_separate_launches"] = 0.0;  // finalize no longer has a launch (or a wait) of its own
   if (grid_ && door_ == 0)  // the shared grid's counters, once per process
@@ -3783,7 +3825,10 @@ void HipGrid::launch_locked() {
   last_post_.store(steady_s(), std::memory_order_relaxed);
   running_.store(true, std::memory_order_release);
   ++launches_;
-  calibrate_locked();
+  // calibration reuses door 0's descriptor: never while a tick posted there is still unrelayed
+  // (a revived grid or a relaunch after an idle exit picks that tick up from `base`; writing
+  // the calibration tick over its descriptor would run an empty tick in its place)
+  if (__atomic_load_n(&h_doors_[0].relayed, __ATOMIC_ACQUIRE) == h_doors_[0].posted) calibrate_locked();
 }
 
 // Clock calibration (timing only): empty ticks on door 0, each timed on the host from the
@@ -3813,8 +3858,8 @@ void HipGrid::calibrate_locked() {
     }
   }
   clk_off_us_.store(off, std::memory_order_relaxed);
-  clk_rtt_us_ = best;
-  last_cal_ = steady_s();
+  clk_rtt_us_.store(best, std::memory_order_relaxed);
+  last_cal_.store(steady_s(), std::memory_order_relaxed);
 }
 
 // Under the exclusive lock (no door is posting): every posted tick relayed, then a stop tick
@@ -3865,7 +3910,7 @@ void HipGrid::housekeep() {
   }
   const uint32_t b = beat_.fetch_add(1, std::memory_order_relaxed) + 1;
   for (int d = 0; d < n_; ++d) __atomic_store_n(&h_doors_[d].beat, b, __ATOMIC_RELAXED);
-  if (steady_s() - last_cal_ > 1.0) {  // the two clocks drift apart by ~us per second
+  if (steady_s() - last_cal_.load(std::memory_order_relaxed) > 1.0) {  // the two clocks drift apart by ~us per second
     std::unique_lock<std::shared_mutex> ex(mu_, std::try_to_lock);
     if (ex.owns_lock() && running_.load(std::memory_order_relaxed)) {
       // door 0's tick in flight (if any) must have been relayed: calibration reuses the door
@@ -3890,7 +3935,7 @@ bool HipGrid::revive_if_exited() {
 std::unordered_map<std::string, double> HipGrid::stats() {
   return {{"grid_launches", (double)launches_.load()}, {"grid_stops", (double)stops_.load()},
           {"grid_revivals", (double)revivals_.load()}, {"grid_doors", (double)n_},
-          {"grid_clock_rtt_us", clk_rtt_us_}, {"grid_xcd_local", interleave_ ? 1.0 : 0.0},
+          {"grid_clock_rtt_us", clk_rtt_us_.load(std::memory_order_relaxed)}, {"grid_xcd_local", interleave_ ? 1.0 : 0.0},
           {"grid_wg_per_door", (double)wpd_}};
 }
 

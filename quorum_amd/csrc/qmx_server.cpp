@@ -572,10 +572,11 @@ class GpuHub {
     lanes_ = std::max(1, std::min(cfg.tick_lanes, 8));
     if (cfg.engine == "hip") {
       HipEngine* he = new HipEngine(cfg.tags, cfg.device, cfg.tile, cfg.max_slots, cfg.content_cap, lanes_);
+      // (spread placement: an RCCL round writes a remote final text into the content arena
+      // and its stream is synchronised before the text is applied; the finalize that reads it
+      // is a later tick, whose items start with a system-scope acquire — one-shot launches and
+      // persistent grids alike)
       eng_.reset(he);
-      // spread placement writes remote final texts into the content arena with RCCL / DMA:
-      // one-shot launches (each launch's acquire) keep those visible
-      if (cfg.world > 1 && cfg.placement == "spread" && he->persistent()) he->set_persistent(false);
     } else
       eng_.reset(new CpuEngine(cfg.tags));  // shared CPU engine: exercises the hub routing on CPU
     if (cfg.verify) ver_.reset(new Verifier(cfg.tags));
@@ -2928,6 +2929,11 @@ class Loop {
   const ServerCfg& cfg_;
   int idx_;
   int ep_ = -1, lfd_ = -1, afd_ = -1, evfd_ = -1;
+  // loop ticks: the ticks this loop has on the GPU.  Declared before eng_, so destroyed
+  // after it: an AsyncCpuEngine's worker may still hold pointers to queued jobs until the
+  // engine's destructor has joined it (a loop that leaves run() by an exception skips the
+  // drain at its end)
+  HostEngine::Job job_[2];
   std::unique_ptr<HostEngine> eng_;  // CPU engine (no GPU hub)
   std::unique_ptr<Verifier> ver_;
   GpuHub* hub_ = nullptr;            // shared HIP engine
@@ -2935,7 +2941,6 @@ class Loop {
   HipEngine* heng_ = nullptr;        // loop ticks: eng_ as this loop's HIP engine
   HostEngine* aeng_ = nullptr;       // loop ticks: eng_, driven asynchronously (HIP grid / AsyncCpuEngine)
   int loop_slots_ = 0;
-  HostEngine::Job job_[2];           // loop ticks: the ticks this loop has on the GPU
   bool job_live_[2] = {false, false};
   int jobs_live_ = 0;
   double job_t_post_[2] = {0, 0};
@@ -3083,9 +3088,10 @@ int run_server(const ServerCfg& cfg0) {
   const bool hip = cfg.engine == "hip";
   const bool spread = cfg.world > 1 && cfg.placement == "spread";
   // hip: loop ticks unless asked for lanes (tick_mode / an explicit shared engine).  Spread
-  // placement included: a remote stream's final text is kept on the owner's host and its
-  // session finalized there (HipEngine::set_remote_content) — lanes instead use one-shot
-  // launches, whose kernel boundaries order the RCCL / DMA writes.  Ranks sharing one GPU
+  // placement included: a remote stream's final text lands in the owner's HBM shadow slot (an
+  // RCCL round, synchronised before it is applied) or is staged into the finalize item that
+  // reads it (the mesh), and the session finalizes in the grid like any other
+  // (HipEngine::set_remote_content).  Ranks sharing one GPU
   // (rehearsals) split the grid budget: HipGrid sizes itself from QMX_GPU_SHARERS, and a grid
   // that does not fit falls back to lanes below.
   (void)spread;

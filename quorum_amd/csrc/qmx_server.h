@@ -38,7 +38,8 @@ struct ServerCfg {
   int tick_lanes = 2;      // shared engine: tick threads, each with its own HIP stream + arenas
   // hip: "loops" = every io loop owns an engine and posts its own ticks into one multi-door
   // persistent grid (HipGrid), "lanes" = the shared engine + tick-lane threads (GpuHub),
-  // "auto" = loops unless sessions spread across ranks
+  // "auto" = loops (spread placement included); lanes only when asked (tick_mode "lanes",
+  // shared_engine = 1) or when the grid does not fit the GPU
   std::string tick_mode = "auto";
   int device = 0;
   int tile = 16384, max_slots = 4096, content_cap = 1 << 20;

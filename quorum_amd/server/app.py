@@ -346,4 +346,7 @@ def create_app(config_provider: Callable[[], Dict[str, Any]], pool: Optional[Ups
     async def metrics_endpoint():
         return Response(content=metrics.render(), media_type="text/plain; version=0.0.4")
 
+    from .schemas import install_openapi
+
+    install_openapi(app)  # request / response / error component schemas in /openapi.json
     return app

@@ -224,7 +224,8 @@ class RuntimeConfig:
     tick_mode: hip engine: "loops" (every io loop owns an engine and posts its own ticks into
                one shared multi-door persistent grid, applying the results itself — no tick
                thread in between) | "lanes" (one shared engine ticked by `tick_lanes` threads)
-               | "auto" (loops, except spread placement across ranks: lanes) — QMX_TICK_MODE
+               | "auto" (loops — spread placement included; lanes only with tick_mode "lanes", an
+               explicit shared engine, or a grid that does not fit the GPU) — QMX_TICK_MODE
     log_content: allow prompts / per-backend answers in the ``aggregation`` log (off: user
                data; see utils/logging_setup.py) — QMX_LOG_CONTENT
     watch_config: the supervisor polls the config file and rolls a new worker generation in

@@ -194,3 +194,31 @@ def test_env_config_path(tmp_path, monkeypatch):
     p.write_text(yaml.dump({"primary_backends": [], "settings": {"timeout": 5}}))
     monkeypatch.setenv("QMX_CONFIG", str(p))
     assert load_config()["settings"]["timeout"] == 5
+
+
+def test_openapi_component_schemas(upstream):
+    """/openapi.json carries the request, completion, stream-chunk, usage and error schemas
+    (the reference's vendored spec: CreateChatCompletionRequest, CreateChatCompletionStreamResponse,
+    CompletionUsage — api_reference/chat_completions.yaml:1437, :398, :1968), referenced from
+    both chat routes; the committed api_reference/openapi.json is that document."""
+    import os
+
+    c = make_client(CFG_BLANK, upstream)
+    doc = c.get("/openapi.json").json()
+    comps = doc["components"]["schemas"]
+    for name in ("CreateChatCompletionRequest", "CreateChatCompletionResponse", "CreateChatCompletionStreamResponse",
+                 "CompletionUsage", "ErrorResponse", "ChatMessage"):
+        assert name in comps, name
+    assert set(comps["CompletionUsage"]["required"]) == {"prompt_tokens", "completion_tokens", "total_tokens"}
+    assert comps["CreateChatCompletionRequest"]["required"] == ["messages"]
+    for path in ("/chat/completions", "/v1/chat/completions"):
+        op = doc["paths"][path]["post"]
+        assert op["requestBody"]["content"]["application/json"]["schema"]["$ref"].endswith(
+            "/CreateChatCompletionRequest")
+        ok = op["responses"]["200"]["content"]
+        assert ok["text/event-stream"]["schema"]["$ref"].endswith("/CreateChatCompletionStreamResponse")
+        for code in ("400", "401", "500"):
+            assert op["responses"][code]["content"]["application/json"]["schema"]["$ref"].endswith("/ErrorResponse")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    committed = json.load(open(os.path.join(root, "api_reference", "openapi.json")))
+    assert committed["components"]["schemas"] == comps

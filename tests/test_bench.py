@@ -244,3 +244,31 @@ def test_breakdown_loop_tick_fields():
     assert bd["stage_us_per_item"]["stage4_us"] == 6.0
     assert bd["shader_mhz"] == 2400.0
     assert bd["tick_wall_us_avg"] == 50.0
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_aggregate4_spread_finals_through_rounds(tmp_path, world):
+    """BASELINE config 3 in the timed region: 4 backends, aggregate strategy, sessions sharded
+    over the ranks AND each session's backend streams spread over them, with every remote
+    final text moved by a bulk round (``--eager-bytes 0``: rank-0 manifests, then RCCL
+    ncclSend/ncclRecv on a GPU node — here the tcpbulk executor, ranks sharing no GPU).
+    Every response is validated; every rank ran rounds; no text fell back to the mesh; the
+    owner finalized the merged sessions on its engine (finalize_host 0)."""
+    port = _free_port()
+    env = dict(_env(), QMX_BENCH_NDEV="0")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, BENCH, "--gpus", str(world), "--scenario", "aggregate4", "--placement", "spread",
+                        "--eager-bytes", "0", "--steps", "2", "--warmup", "1", "--batch", "128", "--threads", "2",
+                        "--conns", "8", "--port", str(port)],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    res = json.loads(_json_lines(r.stdout)[0])
+    assert res["valid"] is True and res["invalid"] == 0 and res["n_gpus"] == world
+    assert "ep%d" % world in res["config"]["parallelism"] and "TCPBULK" in res["config"]["parallelism"]
+    for row in res["breakdown_per_rank"]:
+        x = row["exchange"]
+        assert x["remote_streams"] > 0 and x["bulk_rounds"] > 0 and x["round_us_avg"] > 0, row
+        assert x["eager_finals"] == 0 and x["mesh_finals"] == 0, row
+        assert x["delta_mismatch"] == 0 and x["worker_nodata"] == 0, row
+        assert row["finalize_host"] == 0, row

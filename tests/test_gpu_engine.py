@@ -27,7 +27,19 @@ def _hip(tags, **kw):
     return NativeEngine("hip", tags, device=0, **kw)
 
 
-def _check(seed, n_streams, hip_kw=None, max_piece=None):
+def _gpu_did_it(eng, escalations=0):
+    """The HIP engine did the work itself: no stream migrated to the host path (beyond the
+    `escalations` a test provokes on purpose) and every finalize ran in fused GPU items."""
+    st = eng._e.kernel_stats()
+    if escalations is not None:
+        assert st["escalations"] == escalations, st
+    assert st["fin_host"] == 0 and st["fin_items"] >= 2, st
+    return st
+
+
+def _check(seed, n_streams, hip_kw=None, max_piece=None, escalations=0):
+    """HIP vs CPU engine on random streams; escalations=None: the case provokes host-path
+    migrations (tiny tiles, content overflow), so their number is not pinned."""
     rng = random.Random(seed)
     tags = rng.sample(["think", "reason", "reasoning", "thought", "x"], rng.randint(1, 4))
     raw = [H.rand_stream(rng) for _ in range(n_streams)]
@@ -36,7 +48,10 @@ def _check(seed, n_streams, hip_kw=None, max_piece=None):
     emit = [rng.random() < 0.8 for _ in raw]
     tseed = rng.randint(0, 10**9)
     cpu = H.run_engine(NativeEngine("cpu", tags), streams, filt, emit, random.Random(tseed))
-    hip = H.run_engine(_hip(tags, **(hip_kw or {})), streams, filt, emit, random.Random(tseed))
+    eng = _hip(tags, **(hip_kw or {}))
+    hip = H.run_engine(eng, streams, filt, emit, random.Random(tseed))
+    if escalations is not None:
+        _gpu_did_it(eng, escalations)
     (c, cf, ct), (g, gf, gt) = cpu, hip
     for i, (a, b) in enumerate(zip(c, g)):
         assert a[1] == b[1], ("flags", i, raw[i])
@@ -60,8 +75,10 @@ def test_hip_matches_cpu_wide_tags(ext, seed):
     emit = [rng.random() < 0.9 for _ in raw]
     tseed = rng.randint(0, 10**9)
     cpu = H.run_engine(NativeEngine("cpu", tags), streams, filt, emit, random.Random(tseed))
-    hip = H.run_engine(_hip(tags), streams, filt, emit, random.Random(tseed))
+    eng = _hip(tags)
+    hip = H.run_engine(eng, streams, filt, emit, random.Random(tseed))
     assert hip == cpu, (tags, raw)
+    _gpu_did_it(eng)
 
 
 @pytest.mark.parametrize("seed", range(60))
@@ -94,19 +111,21 @@ def test_hip_clean_content_envelopes(ext, seed):
     emit = [True] * len(raw)
     tseed = rng.randint(0, 10**9)
     cpu = H.run_engine(NativeEngine("cpu", ["think"]), streams, filt, emit, random.Random(tseed), indices=idx)
-    hip = H.run_engine(_hip(["think"]), streams, filt, emit, random.Random(tseed), indices=idx)
+    eng = _hip(["think"])
+    hip = H.run_engine(eng, streams, filt, emit, random.Random(tseed), indices=idx)
     assert hip == cpu
+    _gpu_did_it(eng)
 
 
 def test_hip_small_tiles_and_escalation(ext):
     """Tiny tiles force MORE/requeue and oversize-event escalation to the host path."""
     for seed in range(20):
-        _check(2000 + seed, 5, hip_kw={"tile_bytes": 1024}, max_piece=3000)
+        _check(2000 + seed, 5, hip_kw={"tile_bytes": 1024}, max_piece=3000, escalations=None)
 
 
 def test_hip_content_overflow_escalates(ext):
     for seed in range(10):
-        _check(3000 + seed, 4, hip_kw={"content_cap": 64})
+        _check(3000 + seed, 4, hip_kw={"content_cap": 64}, escalations=None)
 
 
 def test_hip_many_lt_candidates(ext):

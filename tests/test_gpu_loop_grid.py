@@ -122,3 +122,92 @@ def test_grid_small_tiles_and_overflow(ext):
                            streams, filt, emit, random.Random(tseed))
         assert got == cpu, seed
     grid.stop()
+
+
+def test_grid_revives_with_a_tick_pending_on_door_0(ext):
+    """The grid's own idle exit (no host heartbeat for 2 s) while the next tick is posted on
+    door 0: the engine's wait revives the grid, the relaunch picks that tick up from where
+    the relay left off, and the clock calibration that every launch runs on door 0 must not
+    overwrite its descriptor (it did: the tick was lost and the wait failed after 10 s)."""
+    grid = ext.HipGrid(0, 2, 2, idle_ms=60000)  # the host never stops it: only the kernel's own exit
+    tags = ["think", "reason"]
+    eng = NativeEngine("hip", tags, device=0, max_slots=64, grid=grid, door=0)
+    for rnd in range(2):
+        tags_, streams, filt, emit, tseed = _case(800 + rnd, 4)
+        cpu = H.run_engine(NativeEngine("cpu", tags), streams, filt, emit, random.Random(tseed))
+        t0 = time.monotonic()
+        got = H.run_engine(eng, streams, filt, emit, random.Random(tseed))
+        assert got == cpu, rnd
+        assert time.monotonic() - t0 < 8.0
+        if rnd == 0:
+            time.sleep(2.6)  # no housekeep(): every relay idles out on its own
+    assert grid.stats()["grid_revivals"] >= 1, grid.stats()
+    grid.stop()
+
+
+FIN_TEXT_PIECES = ["<think>", "</think>", "<reason>", "</reason>", "<THINK>", "a", "b c", "é", "\U0001F600",
+                   " ", "\n", "　", '"', "\\", "<", ">", "x" * 40]
+
+
+@pytest.mark.parametrize("placement", ["rccl", "mesh", "mixed"])
+def test_grid_remote_finals_finalize_on_gpu(ext, placement):
+    """Spread owner under loop ticks: remote streams' final texts in shadow slots finalize in
+    fused GPU items (fin_host == 0), byte-equal to the CPU engine given the same texts —
+    RCCL-delivered texts (a world-1 loopback: manifests, epoch, ncclSend/ncclRecv into the
+    slots' own HBM areas while the grid runs) and mesh-delivered texts (staged into the
+    finalize items, which copy them to HBM first)."""
+    from live_upstream import free_port_block
+
+    from quorum_amd.ops.engine import FinalizeRequest
+
+    grid = ext.HipGrid(0, 2, 4)
+    tags = ["think", "reason", "reasoning", "thought"]
+    hip = NativeEngine("hip", tags, device=0, max_slots=64, content_cap=1 << 18, grid=grid, door=0)
+    cpu = NativeEngine("cpu", tags)
+    rng = random.Random({"rccl": 1, "mesh": 2, "mixed": 3}[placement])
+    texts = []
+    for k in range(7):
+        n = [1, 3, 40, 200, 900, 3000, 12000][k]
+        texts.append("".join(rng.choice(FIN_TEXT_PIECES) for _ in range(n)).encode("utf-8"))
+    hs = [hip.open(i, False, False) for i in range(len(texts))]
+    cs = [cpu.open(i, False, False) for i in range(len(texts))]
+    via_rccl = [placement == "rccl" or (placement == "mixed" and i % 2 == 0) for i in range(len(texts))]
+    items = []
+    for i, b in enumerate(texts):
+        if via_rccl[i]:
+            ptr, cap = hip._e.content_device_ptr(hs[i])
+            assert ptr and cap >= len(b)
+            items.append((ptr, b))
+    if items:
+        res = ext.rccl_deliver({"port": free_port_block(1), "device": 0, "timeout": 60.0}, items)
+        assert res["ok"] and res["bulk"] == len(items) and res["rounds"] >= 1 and res["mesh_finals"] == 0, res
+    for i, b in enumerate(texts):
+        hip._e.set_remote_content(hs[i], None if via_rccl[i] else b, len(b))
+        cpu._e.set_remote_content(cs[i], b, len(b))
+
+    def finalize(eng, slots, strip, kind):
+        fid = eng.submit_finalize(FinalizeRequest(slots, strip, kind, "\n--\n", H.CREATED))
+        for _ in range(100):
+            _res, fres = eng.tick(H.CREATED)
+            for f, payload in fres:
+                if f == fid:
+                    return payload
+        raise AssertionError("finalize never completed")
+
+    for strip in (True, False):
+        for kind in ("event", "texts"):
+            for sub in (list(range(len(texts))), [0, 5, 6], [3]):
+                g = finalize(hip, [hs[i] for i in sub], strip, kind)
+                c = finalize(cpu, [cs[i] for i in sub], strip, kind)
+                assert g == c, (strip, kind, sub)
+    for i, b in enumerate(texts):
+        assert hip._e.text(hs[i]) == b
+    st = hip._e.kernel_stats()
+    n_r = sum(via_rccl)
+    assert st["fin_host"] == 0 and st["escalations"] == 0, st
+    assert st["remote_texts_hbm"] == n_r and st["remote_texts_staged"] == len(texts) - n_r, st
+    if n_r < len(texts):
+        assert st["fin_staged_texts"] > 0, st
+    for s in hs:
+        hip.release(s)
+    grid.stop()

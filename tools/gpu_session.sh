@@ -18,10 +18,15 @@
 #   refscenarios          the same for aggregate4, highqps8, failure
 #   prof                  rocprofv3 --kernel-trace --stats of a short headline bench
 #   pmc:C1,C2,...         rocprofv3 --pmc pass (one block-limited counter set) on kbench
+#   pmce:ENV=V:C1,C2      the same pass under extra env (e.g. QMX_KFAST=7: one fast path off)
+#   pmcgrid:C1,C2,...     rocprofv3 --pmc on the production kernel (kbench --grid: qmx_tick_persistent),
+#                         counters per dispatch and per tick
 #   kbench                tools/kbench.py in-kernel stage split (QMX_STAGE_TIMING)
+#   kbenchgrid            the same on the persistent grid (the production kernel)
 #   multirank=N           bench.py under torch.distributed.run with N ranks sharing GPU 0
 #   spread=N              same, --placement spread over the TCP exchange
 #   cpuprof               headline bench with the in-process CPU profiler on the proxy
+#   cpuprofsc:SCENARIO    the same for a scenario (aggregate4, highqps8, failure, ...)
 #   probe:NAME            tools/probes/NAME (built beforehand), e.g. probe:doorbell_probe
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -123,6 +128,37 @@ for step in "$@"; do
         || { echo "pmc $ctr failed"; tail -10 $OUT/pmc_$slug.log; exit 1; }
       python3 tools/pmc_summary.py $(find $OUT/pmc_$slug -name '*counter_collection.csv') > $OUT/pmc_$slug.md 2>&1
       grep -v rocclr $OUT/pmc_$slug.md | head -30 ;;
+    pmce:*)  # pmce:ENV=V[,ENV=V]:C1,C2 — a one-shot kbench counter pass under extra env
+      rest=${step#pmce:}; e=${rest%%:*}; ctr=${rest#*:}
+      slug=$(echo "$e:$ctr" | tr -c 'a-zA-Z0-9' '_' | cut -c1-80)
+      env ${e//,/ } QMX_PERSISTENT=0 timeout -s KILL 120 rocprofv3 --pmc ${ctr//,/ } -d $OUT/pmce_$slug -o pmc --output-format csv -- \
+        python3 tools/kbench.py --slots 256 --iters 10 > $OUT/pmce_$slug.log 2>&1 \
+        || { echo "pmce $e $ctr failed"; tail -10 $OUT/pmce_$slug.log; exit 1; }
+      python3 tools/pmc_summary.py $(find $OUT/pmce_$slug -name '*counter_collection.csv') > $OUT/pmce_$slug.md 2>&1
+      echo "-- $e"; grep -v rocclr $OUT/pmce_$slug.md | grep qmx | head -12 ;;
+    pmcgrid:*)  # counters of the production kernel (qmx_tick_persistent: one dispatch, many ticks)
+      ctr=${step#pmcgrid:}; slug=$(echo "$ctr" | tr -c 'a-zA-Z0-9' '_' | cut -c1-60)
+      timeout -s KILL 120 rocprofv3 --pmc ${ctr//,/ } -d $OUT/pmcg_$slug -o pmc --output-format csv -- \
+        python3 tools/kbench.py --grid 16 --slots 3 --iters 400 --combos ft > $OUT/pmcg_$slug.log 2>&1 \
+        || { echo "pmcgrid $ctr failed"; tail -10 $OUT/pmcg_$slug.log; exit 1; }
+      nt=$(python3 -c "
+import json
+t=0
+for l in open('$OUT/pmcg_$slug.log'):
+    if l.startswith('{') and 'grid_ticks' in l: t += json.loads(l).get('grid_ticks') or 0
+print(int(t))")
+      python3 tools/pmc_summary.py --per-tick $nt $(find $OUT/pmcg_$slug -name '*counter_collection.csv') > $OUT/pmcg_$slug.md 2>&1
+      grep -v rocclr $OUT/pmcg_$slug.md | head -30 ;;
+    kbenchgrid)  # in-kernel stage split of the production kernel (persistent grid)
+      QMX_STAGE_TIMING=1 timeout -k 10 300 python tools/kbench.py --grid 16 --slots 1,3,22 --iters 100 --combos ft > $OUT/kbenchgrid.jsonl 2>&1 \
+        || { echo "kbenchgrid failed"; tail -5 $OUT/kbenchgrid.jsonl; exit 1; }
+      grep -v '^{"grid_stats' $OUT/kbenchgrid.jsonl | python3 -c "
+import json, sys
+for l in sys.stdin:
+    if not l.startswith('{'): continue
+    d=json.loads(l); st=d.get('stage_us_per_item',{})
+    print(d['slots'], 'wall', d['wall_us_p50'], 'kern', d.get('kernel_us_avg'), 'fence', st.get('stage_fence_us'), [st.get('stage%d_us'%k) for k in range(1,11)])
+" ;;
     kbench)
       QMX_PERSISTENT=0 QMX_STAGE_TIMING=1 timeout -k 10 300 python tools/kbench.py --slots 1,22,64,256 --iters 20 > $OUT/kbench.jsonl 2>&1 \
         || { echo "kbench failed"; tail -5 $OUT/kbench.jsonl; exit 1; }
@@ -164,6 +200,12 @@ for r in s.get('per_rank',[]): print('  ', r)
       bench cpuprof 300 QMX_PROF=$PWD/$OUT/cpu_hip.%p.txt QMX_PROF_US=100 -- --steps 20 --warmup 2 || exit 1
       for f in $OUT/cpu_hip.*.txt; do python3 tools/cpuprof.py $f --top 30 --json $f.json > $f.summary 2>&1 || true; done
       head -30 $OUT/cpu_hip.*.summary ;;
+    cpuprofsc:*)  # a scenario with the in-process CPU profiler on the proxy (where its CPU goes)
+      SC=${step#cpuprofsc:}
+      bench cpuprof_$SC 300 QMX_PROF=$PWD/$OUT/cpu_$SC.%p.txt QMX_PROF_US=100 -- --scenario $SC --steps 10 --warmup 2 \
+        --batch 16384 || exit 1
+      for f in $OUT/cpu_$SC.*.txt; do python3 tools/cpuprof.py $f --top 40 --json $f.json > $f.summary 2>&1 || true; done
+      head -45 $OUT/cpu_$SC.*.summary ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -35,6 +35,11 @@ def main():
     ap.add_argument("--slots", default="1,16,64,256,1024")
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--engine", default="hip")
+    ap.add_argument("--grid", type=int, default=0,
+                    help="N > 0: post the ticks into door 0 of an N-door persistent grid (HipGrid, the loop-tick "
+                         "production kernel qmx_tick_persistent) instead of one-shot launches")
+    ap.add_argument("--combos", default="ft,f,t",
+                    help="(filter, emit) combinations: ft = filter+emit, f = filter only, t = emit only")
     ap.add_argument("--events-per-tick", type=int, default=0,
                     help="stream the body N events per tick (steady-state serving shape); 0 = whole body in one tick")
     args = ap.parse_args()
@@ -43,9 +48,16 @@ def main():
     body = mock_stream()
     tags = ["think", "reason", "reasoning", "thought"]
     results = []
-    for filt, emit in ((True, True), (False, True), (True, False)):
+    grid = None
+    if args.grid > 0:
+        from quorum_amd.ops import native
+
+        grid = native.require().HipGrid(0, args.grid, 8)
+    combos = {"ft": (True, True), "f": (True, False), "t": (False, True)}
+    for filt, emit in [combos[c] for c in args.combos.split(",")]:
         for n in [int(x) for x in args.slots.split(",")]:
-            eng = NativeEngine(args.engine, tags, device=0, max_slots=4096, content_cap=1 << 16)
+            kw = {"grid": grid, "door": 0} if grid is not None else {}
+            eng = NativeEngine(args.engine, tags, device=0, max_slots=4096, content_cap=1 << 16, **kw)
             walls = []
             evs = [e + b"\n\n" for e in body.split(b"\n\n") if e]
             k = args.events_per_tick or len(evs)
@@ -80,8 +92,14 @@ def main():
                                                     "s3_cycles_full", "s3_cycles_template", "s3_cycles_lex", "s3_cycles_hole")
                                           if k in st}
                 rec["MB_per_s"] = round(n * len(body) / len(pieces) / (st["kernel_ms"] / max(st["launches"], 1)) / 1e3, 1)
+            if grid is not None:
+                rec["grid_ticks"] = st.get("grid_ticks")
+                rec["grid_launches"] = st.get("grid_launches")
             results.append(rec)
             print(json.dumps(rec), flush=True)
+    if grid is not None:  # the grid's one dispatch ends here: its counters cover every tick above
+        grid.stop()
+        print(json.dumps({"grid_stats": grid.stats()}), flush=True)
     return results
 
 
