@@ -379,6 +379,10 @@ def breakdown(m0, m1, elapsed):
                              for k, v in d.items() if k.startswith("qmx_syscalls_total")}
         if d.get("qmx_requests_total") else {},
         "exchange_rounds": int(d.get("qmx_exchange_rounds_total", 0.0)),
+        # deltas held for their stream's next output (more bytes already waiting) instead of a
+        # client send of their own, per request
+        "coalesced_per_req": (round(d.get("qmx_output_coalesced_total", 0.0) / d["qmx_requests_total"], 2)
+                              if d.get("qmx_requests_total") else None),
         # spread placement (EP): how the remote streams' finals moved — bulk rounds (RCCL
         # ncclSend/ncclRecv HBM -> HBM, or tcpbulk in rehearsals) vs the mesh — what the rounds
         # cost, and whether the owner finalized them on the GPU (HBM-resident / staged texts)
@@ -480,6 +484,10 @@ def spread_summary(rows) -> dict:
            "delta_mismatch": sum(tot(a, b, "delta_mismatch") for a, b in passes[:4]),
            "worker_nodata": sum(tot(a, b, "worker_nodata") for a, b in passes[:4]),
            "peer_downs": sum(tot(a, b, "peer_downs") for a, b in passes[:4]),
+           # merged sessions finalized on the owner's host instead of its GPU (0 expected)
+           "finalize_host": sum(tot(a, b, "finalize_host") for a, b in passes[:4]),
+           "remote_texts_gpu": {"hbm": sum(tot(a, b, "remote_texts_hbm") for a, b in passes[:4]),
+                                "staged": sum(tot(a, b, "remote_texts_staged") for a, b in passes[:4])},
            "remote_ends": ends("main", "load", "remote_ends"),
            "p50_latency_ms": med([get(r, "main", "load", "p50_latency_ms") for r in rows]),
            "hops_us_loaded": hops("main", "load", "hops_us"),
@@ -504,7 +512,8 @@ def spread_summary(rows) -> dict:
 
     def compact(d):
         keep = ("requests", "invalid", "p50_latency_ms", "remote_streams", "eager_finals", "bulk_rounds", "mesh_finals",
-                "delta_mismatch", "worker_nodata", "remote_ends", "up_failures", "hops_us", "error")
+                "delta_mismatch", "worker_nodata", "remote_ends", "up_failures", "hops_us", "finalize_host",
+                "remote_texts_hbm", "remote_texts_staged", "error")
         return {k: v for k, v in (d or {}).items() if k in keep and v}
 
     def rank_error(r):
@@ -583,6 +592,11 @@ def spread_counters(d) -> dict:
             "delta_mismatch": d.get("qmx_spread_delta_mismatch_total", 0.0),
             "worker_nodata": d.get("qmx_spread_worker_nodata_total", 0.0),
             "peer_downs": d.get("qmx_exchange_peer_downs_total", 0.0),
+            # the owner's finalize of merged sessions: on the host (should stay 0: remote texts
+            # sit in HBM after an RCCL round, or are staged into the GPU finalize items)
+            "finalize_host": d.get("qmx_kernel_fin_host", 0.0),
+            "remote_texts_hbm": d.get("qmx_kernel_remote_texts_hbm", 0.0),
+            "remote_texts_staged": d.get("qmx_kernel_remote_texts_staged", 0.0),
             # how this rank's remote streams ended (owner side), and its upstream failures by
             # class (worker side included)
             "remote_ends": {k.split('"')[1]: v for k, v in d.items() if k.startswith("qmx_spread_remote_ends_total") and v},

@@ -460,6 +460,13 @@ bool HostEngine::has_work() {
   return false;
 }
 
+bool HostEngine::pending(int slot) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (slot < 0 || slot >= (int)meta_.size()) return false;
+  const Meta& m = meta_[slot];
+  return m.live && (m.dirty || m.busy || !m.incoming.empty());
+}
+
 bool HostEngine::job_take(Job& j, bool allow_fin) {
   j.work.clear();
   j.fin.clear();

@@ -176,6 +176,9 @@ class HostEngine {
   int submit_finalize(const std::vector<int>& slots, bool strip, bool texts, const std::string& joiner,
                       int64_t created);
   bool has_work();
+  // the slot has bytes the engine has not turned into results yet (fed and not taken by a
+  // tick, or in a tick still in flight): more output for its stream is on the way
+  bool pending(int slot);
   // One tick over every dirty slot that is not in flight on another lane.  `lane` picks the
   // engine's per-thread launch resources (HipEngine: stream + arenas), so several tick
   // threads can have kernels in flight at once over disjoint slot sets.  With `taken`, the

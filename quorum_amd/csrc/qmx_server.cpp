@@ -9,6 +9,7 @@
 #include <netinet/tcp.h>
 #include <signal.h>
 #include <sys/epoll.h>
+#include <sys/ioctl.h>
 #include <sys/eventfd.h>
 #include <sys/prctl.h>
 #include <sys/socket.h>
@@ -47,7 +48,8 @@ std::atomic<uint64_t> c_requests{0}, c_stream{0}, c_nonstream{0}, c_errors{0}, c
     c_tick_slots{0}, c_up_conns{0}, c_clients{0}, c_remote_streams{0},
     c_route_ns{0},  // tick lanes: tick returned -> results handed to the io loops + streams settled
     c_flush_ns{0}, c_flushes{0},  // io loop: oldest upstream bytes of a batch -> handed to the engine
-    c_apply_ns{0}, c_applies{0};  // io loop: a tick's results routed -> applied (sent to clients)
+    c_apply_ns{0}, c_applies{0},  // io loop: a tick's results routed -> applied (sent to clients)
+    c_coalesced{0};  // deltas held for their stream's next output instead of a send of their own
 // failures by class
 std::atomic<uint64_t> c_fail_connect{0}, c_fail_timeout{0}, c_fail_status{0}, c_fail_disconnect{0},
     c_fail_protocol{0}, c_stream_aborts{0},
@@ -333,6 +335,7 @@ struct Client {
   uint64_t serial = 0;       // per-loop connection serial (fd numbers are reused)
   double t_accept = 0;
   bool want_out = false;     // EPOLLOUT armed (socket buffer was full)
+  bool held = false;         // corked output held for a stream's next delta (a deferral entry is out)
 };
 
 enum UpMode { UP_ENGINE, UP_BUFFER, UP_PASS };
@@ -1010,8 +1013,12 @@ class Loop {
       if (it == clients_.end()) continue;
       Client* c = it->second.get();
       if (c->serial != deferq_[i].serial) continue;  // fd closed and reused by a new connection
-      if (c->queued || c->want_out || c->dead || c->out_off >= c->out.size()) continue;
+      if (c->queued || c->want_out || c->dead || c->out_off >= c->out.size()) {
+        c->held = false;
+        continue;
+      }
       if (deferq_[i].deadline <= t || g_drain.load()) {
+        c->held = false;
         c->queued = true;
         flushq_.push_back(c->fd);
         continue;
@@ -1214,8 +1221,16 @@ class Loop {
         if (s->kind == K_REMOTE) {
           post_owner(s, X_DATA, 0, 0, r.data(), r.size());  // framed from the view: one copy
           s->data_sent++;
+        } else if (s->cl) {
+          // output coalescing across ticks: once the session's first content is out (TTFT),
+          // a delta whose stream already has more bytes in the engine (fed, or in the other
+          // tick in flight) waits for that output (<= one tick) instead of its own send — a
+          // stream trickling in event by event otherwise costs a client send per tick.  A
+          // stream with nothing pending (the steady-state LLM pace) is sent at once.
+          const bool hold = coalesce_s_ > 0 && s->first_content && !(r.flags & (RF_DONE | RF_ABORTED)) &&
+                            (ops_pending(r.slot) || eng().pending(r.slot) || up_readable(s->bs[bi].up));
+          send_content(s, r.data(), r.size(), hold);
         }
-        else if (s->cl) send_content(s, r.data(), r.size());
       }
       r.hold = ViewRef();  // the bytes were copied (or dropped): the lane may reuse its arena
       if ((r.flags & RF_ABORTED)) c_stream_aborts++;
@@ -1399,6 +1414,14 @@ class Loop {
   void write_chunk(Client* c, const std::string& data) { write_chunk(c, data.data(), data.size()); }
   void write_chunk(Client* c, const char* data, size_t len) {
     if (c->dead || len == 0) return;
+    append_chunk(c, data, len);
+    if (!c->queued && !c->want_out) {
+      c->queued = true;
+      flushq_.push_back(c->fd);
+    }
+  }
+  void append_chunk(Client* c, const char* data, size_t len) {
+    if (c->dead || len == 0) return;
     if (c->out.size() == c->out_off) {
       c->out.clear();
       c->out_off = 0;
@@ -1408,10 +1431,6 @@ class Loop {
     c->out.append(h, n);
     c->out.append(data, len);
     c->out.append("\r\n", 2);
-    if (!c->queued && !c->want_out) {
-      c->queued = true;
-      flushq_.push_back(c->fd);
-    }
   }
   void flush_queued() {
     std::vector<int>& fds = scratch_flush_;
@@ -1422,6 +1441,7 @@ class Loop {
       if (it == clients_.end()) continue;
       Client* c = it->second.get();
       c->queued = false;
+      c->held = false;  // (held output leaves with this send; its deferral entry lapses)
       if (c->dead || c->want_out) continue;
       while (c->out_off < c->out.size()) {
         ssize_t w = send(c->fd, c->out.data() + c->out_off, c->out.size() - c->out_off, MSG_NOSIGNAL);
@@ -2142,12 +2162,36 @@ class Loop {
   }
   // content-bearing events: the first one closes the session's TTFT span
   void send_content(Session* s, const std::string& data) { send_content(s, data.data(), data.size()); }
-  void send_content(Session* s, const char* data, size_t len) {
+  void send_content(Session* s, const char* data, size_t len, bool hold = false) {
     if (!s->first_content) {
       s->first_content = true;
       h_ttft.observe(now_s() - s->t0);
     }
-    if (s->cl) write_chunk(s->cl, data, len);
+    if (!s->cl) return;
+    Client* c = s->cl;
+    if (!hold || c->queued || c->want_out || c->dead) return write_chunk(c, data, len);
+    // held: corked without queueing the client, for as long as its stream keeps having more
+    // bytes pending; the next unheld write to this client (the stream's last output, another
+    // stream's, the final / [DONE]) sends it all, and the deferral deadline bounds the wait
+    append_chunk(c, data, len);
+    if (!c->held) {
+      c->held = true;
+      deferq_.push_back(Deferred{c->fd, c->serial, now_s() + coalesce_s_});
+    }
+    c_coalesced++;
+  }
+  // the stream's upstream socket already holds unread bytes (its next events arrived while
+  // this tick ran): one FIONREAD instead of a client send per tick of a trickling stream
+  bool up_readable(const Up* u) const {
+    if (!u || u->fd < 0 || u->ssl) return false;
+    int n = 0;
+    return ioctl(u->fd, FIONREAD, &n) == 0 && n > 0;
+  }
+  // a FEED for this slot is queued in this iteration's engine ops (not handed over yet)
+  bool ops_pending(int slot) const {
+    for (const EngineOp& o : ops_)
+      if (o.slot == slot && o.kind == EngineOp::FEED) return true;
+    return false;
   }
   void start_parallel(Session* s, const std::vector<int>& valid) {
     c_stream++;
@@ -2861,6 +2905,7 @@ class Loop {
     put("qmx_upstream_connections_total", (double)c_up_conns.load());
     put("qmx_client_connections_total", (double)c_clients.load());
     put("qmx_ticks_total", (double)c_ticks.load());
+    put("qmx_output_coalesced_total", (double)c_coalesced.load());
     put("qmx_tick_slots_total", (double)c_tick_slots.load());
     put("qmx_tick_route_seconds_total", (double)c_route_ns.load() * 1e-9);
     put("qmx_flush_wait_seconds_total", (double)c_flush_ns.load() * 1e-9);
@@ -3018,6 +3063,12 @@ class Loop {
   const double role_defer_s_ = [] {
     const char* e = env_get("QMX_ROLE_DEFER_US");
     return (e ? atof(e) : 1000.0) * 1e-6;
+  }();
+  // output coalescing across ticks (apply): the longest a held delta waits for its stream's
+  // next output (QMX_COALESCE_US, 0: off — every tick's output is sent on its own)
+  const double coalesce_s_ = [] {
+    const char* e = env_get("QMX_COALESCE_US");
+    return (e ? atof(e) : 500.0) * 1e-6;
   }();
   std::vector<EngineOp> ops_;  // engine feed / finish / release of this iteration (flush_ops)
   const bool early_flush_ = env_flag("QMX_EARLY_FLUSH", true);  // A/B knob

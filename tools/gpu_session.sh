@@ -189,11 +189,22 @@ for l in open('$OUT/kbench.jsonl'):
       python3 -c "
 import json
 d=json.loads([l for l in open('$OUT/selfrank_$n.json') if l.startswith('{')][-1]); s=d.get('spread_check',{})
-print('per-rank pids', [r['pid'] for r in d.get('breakdown_per_rank',[])], 'spread', {k: s.get(k) for k in ('ok','requests','invalid','remote_streams','bulk_rounds','mesh_finals','delta_mismatch','worker_nodata','peer_downs','remote_ends','p50_latency_ms','eager_finals','probe_p50_latency_ms','local_probe_p50_latency_ms','hops_us_loaded','hops_us_probe','bulk_formed','rendezvous','errors')})
+print('per-rank pids', [r['pid'] for r in d.get('breakdown_per_rank',[])], 'spread', {k: s.get(k) for k in ('ok','requests','invalid','remote_streams','bulk_rounds','mesh_finals','delta_mismatch','worker_nodata','peer_downs','remote_ends','p50_latency_ms','eager_finals','probe_p50_latency_ms','local_probe_p50_latency_ms','hops_us_loaded','hops_us_probe','bulk_formed','rendezvous','finalize_host','remote_texts_gpu','errors')})
 for r in s.get('per_rank',[]): print('  ', r)
 " || true
       grep "qmx spread\|qmx exchange" $OUT/selfrank_$n.err | head -20
       [ $rc -eq 0 ] || { echo "step selfrank_$n failed rc=$rc"; tail -30 $OUT/selfrank_$n.err; exit 1; } ;;
+    selfsc=*)  # selfsc=N:ARGS — bench.py --gpus N (ranks sharing GPU 0) with extra args (commas = spaces)
+      rest=${step#selfsc=}; n=${rest%%:*}; a=${rest#*:}; slug=$(echo "$a" | tr -c 'a-zA-Z0-9' '_' | cut -c1-60)
+      QMX_BENCH_NDEV=${QMX_BENCH_NDEV:-1} timeout -k 10 400 python bench.py --gpus $n --threads 2 ${a//,/ } \
+        > $OUT/selfsc_${n}_$slug.json 2> $OUT/selfsc_${n}_$slug.err
+      rc=$?; summ selfsc_${n}_$slug $OUT/selfsc_${n}_$slug.json
+      python3 -c "
+import json
+d=json.loads([l for l in open('$OUT/selfsc_${n}_$slug.json') if l.startswith('{')][-1])
+for r in d.get('breakdown_per_rank',[]): print('  ', r['rank'], r['requests'], 'fin_host', r.get('finalize_host'), r.get('exchange'))
+" || true
+      [ $rc -eq 0 ] || { echo "step selfsc_$n failed rc=$rc"; tail -30 $OUT/selfsc_${n}_$slug.err; exit 1; } ;;
     spread=*)
       n=${step#spread=}; QMX_XCHG=tcp torchrun_bench spread_$n $n --steps 5 --warmup 1 --threads 2 --batch 4096 --placement spread || exit 1 ;;
     cpuprof)
