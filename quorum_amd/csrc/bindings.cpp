@@ -146,7 +146,8 @@ ServerCfg server_cfg_from(const py::dict& d) {
   gb("install_signals", c.install_signals);
   gi("rank", c.rank); gi("world", c.world); gs("placement", c.placement); gs("xchg", c.xchg);
   gs("xchg_addr", c.xchg_addr); gi("xchg_port", c.xchg_port); gi("xchg_bulk_port", c.xchg_bulk_port); gs("xchg_id_file", c.xchg_id_file);
-  gi("xchg_round_us", c.xchg_round_us); gi("xchg_eager_bytes", c.xchg_eager_bytes); gd("xchg_timeout", c.xchg_timeout);
+  gi("xchg_round_us", c.xchg_round_us); gi("xchg_eager_bytes", c.xchg_eager_bytes);
+  gi("xchg_links", c.xchg_links); gd("xchg_timeout", c.xchg_timeout);
   gd("drain_s", c.drain_s); gs("ready_file", c.ready_file); gb("verify", c.verify); gi("admin_port", c.admin_port);
   gi("shared_engine", c.shared_engine); gi("tick_lanes", c.tick_lanes); gs("tick_mode", c.tick_mode);
   gs("ca_file", c.ca_file); gb("tls_verify", c.tls_verify);

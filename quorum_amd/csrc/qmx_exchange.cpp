@@ -272,6 +272,44 @@ struct Exchange::Impl {
       v[0].a = r;
       X->deliver_(l, std::move(v));
     }
+    dial_links(r);
+  }
+  // the higher rank of a pair dials io loop l's link for every l once the pair's mesh
+  // connection formed (the peer's listener is up): blocking connect + hello, then the socket
+  // goes to loop l (X_LINK), which owns it from then on
+  void dial_links(int r) {
+    if (!X->o_.links || X->o_.rank <= r) return;
+    for (int l = 0; l < X->nloops_; ++l) {
+      int fd = socket(AF_INET, SOCK_STREAM, 0);
+      if (fd < 0) return;
+      timeval tv{1, 0};
+      setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));  // (bounds connect too)
+      sockaddr_in a{};
+      a.sin_family = AF_INET;
+      a.sin_port = htons((uint16_t)(X->o_.port + r));
+      inet_pton(AF_INET, X->o_.addr.c_str(), &a.sin_addr);
+      XMsg h;
+      h.type = F_HELLO;
+      h.a = X->o_.rank;
+      h.b = l + 1;  // b > 0: a link of loop b - 1 (0: the mesh connection)
+      const std::string f = frame(h);
+      if (connect(fd, (sockaddr*)&a, sizeof(a)) != 0 || send(fd, f.data(), f.size(), MSG_NOSIGNAL) != (ssize_t)f.size()) {
+        close(fd);
+        continue;  // (no link: that loop's sessions with r use the mesh)
+      }
+      set_nodelay(fd);
+      fcntl(fd, F_SETFL, fcntl(fd, F_GETFL) | O_NONBLOCK);
+      hand_link(l, r, fd, std::string());
+    }
+  }
+  void hand_link(int l, int r, int fd, std::string&& early) {
+    std::vector<XMsg> v(1);
+    v[0].type = X_LINK;
+    v[0].a = r;
+    v[0].b = fd;
+    v[0].payload = std::move(early);
+    X->links_++;
+    X->deliver_(l % X->nloops_, std::move(v));
   }
   bool all_up() const {
     for (int r = 0; r < X->o_.world; ++r)
@@ -626,6 +664,30 @@ void Exchange::append_frame(std::string& out, const XMsg& hdr, const char* paylo
   put_frame(out, hdr, payload, n);
 }
 
+size_t Exchange::parse_frames(const std::string& buf, std::vector<XMsg>& out) {
+  size_t p = 0;
+  while (buf.size() - p >= sizeof(WireHdr)) {
+    WireHdr h;
+    std::memcpy(&h, buf.data() + p, sizeof(h));
+    if (buf.size() - p - sizeof(h) < h.len) break;
+    XMsg m;
+    m.type = h.type;
+    m.flags = h.flags;
+    m.dst_loop = h.dst_loop;
+    m.src_loop = h.src_loop;
+    m.dst_rank = h.dst_rank;
+    m.src_rank = h.src_rank;
+    m.bi = h.bi;
+    m.skey = h.skey;
+    m.a = h.a;
+    m.b = h.b;
+    m.payload.assign(buf.data() + p + sizeof(h), h.len);
+    p += sizeof(h) + h.len;
+    if (m.type < F_HELLO) out.push_back(std::move(m));
+  }
+  return p;
+}
+
 void Exchange::post_frames(int dst, std::string& frames) {
   if (frames.empty()) return;
   if (stop_.load() || dst < 0 || dst >= o_.world) {
@@ -801,6 +863,17 @@ void Exchange::mesh_loop() {
           const int pr = h.a;
           if (h.type != F_HELLO || pr <= o_.rank || pr >= o_.world) {
             dead = true;
+          } else if (h.b > 0) {  // a per-loop link: the socket (and what followed its hello) goes to loop b - 1
+            epoll_ctl(I.ep, EPOLL_CTL_DEL, fd, nullptr);
+            std::string early = in.substr(sizeof(WireHdr) + h.len);
+            pend_in.erase(fd);
+            pending.erase(std::remove(pending.begin(), pending.end(), fd), pending.end());
+            if (!o_.links || h.b - 1 >= nloops_) {
+              close(fd);
+              continue;
+            }
+            I.hand_link(h.b - 1, pr, fd, std::move(early));
+            continue;
           } else {
             Impl::Peer& p = I.peers[pr];
             if (p.fd >= 0) I.mark_down(pr, "replaced by a new connection");  // a re-joined peer replaces its dead connection

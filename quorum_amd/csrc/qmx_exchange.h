@@ -46,6 +46,8 @@ enum XType : uint8_t {
                  //   messages sent before it; payload = the bytes when not written to HBM)
   X_SENT = 7,    // exchange → worker loop: the bulk left (flags XF_FAILED if it could not)
   X_UP = 8,      // exchange → loops: peer `a` (re)joined the mesh
+  X_LINK = 9,    // exchange → loop: a connected per-loop link to peer `a` (fd `b`; payload: bytes
+                 //   already read from it) — the loop owns the socket from here on
 };
 // X_FINAL / X_BULK / X_SENT flags
 enum : uint8_t { XF_TEXT = 1, XF_ABORTED = 2, XF_FAILED = 4 };
@@ -71,6 +73,10 @@ struct XOptions {
   int device = 0;
   int batch_us = 50;              // rank 0: announcements arriving within this window share a round
   double timeout_s = 30.0;        // bulk round / epoch formation slower than this = peer failure
+  // per-loop links: io loop l of every rank pair gets a TCP connection of its own (dialled by
+  // the higher rank once the pair's mesh connection forms), so a session's opens, deltas and
+  // eager finals go io loop → socket → io loop with no mesh thread on the data path
+  bool links = true;
 };
 
 // the mesh's view of one peer
@@ -89,6 +95,9 @@ class Exchange {
   // caller straight into a per-destination buffer (append_frame: one copy of each payload),
   // then handed over with one lock and one mesh-thread wake (post_frames clears `frames`).
   static void append_frame(std::string& out, const XMsg& hdr, const char* payload, size_t n);
+  // the complete frames at the front of `buf` → `out` (a link's receive side); returns the
+  // bytes consumed.  Mesh-internal frame types never travel on a link.
+  static size_t parse_frames(const std::string& buf, std::vector<XMsg>& out);
   void post_frames(int dst_rank, std::string& frames);
   // Worker: ship stream (hdr.skey, hdr.bi)'s final text to hdr.dst_rank.  `dev` points at
   // `len` bytes in HBM that stay valid until X_SENT comes back to hdr.src_loop; `host`
@@ -120,6 +129,7 @@ class Exchange {
   // texts a round carried whose sender finished the round but whose receiver missed them
   // (it failed the round on another peer): resent over the mesh on the receiver's report
   uint64_t rescued() const { return rescued_.load(); }
+  uint64_t links() const { return links_.load(); }  // per-loop links handed to the io loops
 
   struct Impl;
 
@@ -130,7 +140,7 @@ class Exchange {
   std::unique_ptr<Impl> im_;
   std::atomic<bool> stop_{false}, healthy_{false}, rccl_ok_{false};
   std::atomic<uint64_t> rounds_{0}, bytes_{0}, bulk_bytes_{0}, mesh_bulk_{0}, msgs_{0}, rccl_epoch_{0}, rejoins_{0},
-      downs_{0}, rescued_{0};
+      downs_{0}, rescued_{0}, links_{0};
   std::atomic<double> busy_us_{0};
   std::thread mesh_th_, bulk_th_;
   void mesh_loop();

@@ -49,6 +49,7 @@ std::atomic<uint64_t> c_requests{0}, c_stream{0}, c_nonstream{0}, c_errors{0}, c
     c_route_ns{0},  // tick lanes: tick returned -> results handed to the io loops + streams settled
     c_flush_ns{0}, c_flushes{0},  // io loop: oldest upstream bytes of a batch -> handed to the engine
     c_apply_ns{0}, c_applies{0},  // io loop: a tick's results routed -> applied (sent to clients)
+    c_link_msgs{0},  // spread: exchange messages sent over the io loops' own links (no mesh thread)
     c_coalesced{0};  // deltas held for their stream's next output instead of a send of their own
 // failures by class
 std::atomic<uint64_t> c_fail_connect{0}, c_fail_timeout{0}, c_fail_status{0}, c_fail_disconnect{0},
@@ -362,6 +363,7 @@ struct BState {
   int remote = -1;        // spread placement: rank running this stream (-1 = local)
   int rx_data = 0;        // spread: delta messages received from the worker
   double t_sp_open = 0, t_sp_last = 0;  // spread: X_OPEN queued / last delta applied (h_sp_*)
+  bool via_link = false;      // spread: this remote stream's messages use the io loop's link to its rank
   bool bulk_waiting = false;  // spread: the final text arrived before some of its deltas
   XMsg bulk_msg;
   Up* up = nullptr;
@@ -406,6 +408,7 @@ struct Session {
   uint64_t skey = 0;  // owner: key under which workers address this session
   int remote_n = 0;
   int owner_rank = -1, owner_loop = 0, shadow_bi = 0;  // worker (K_REMOTE)
+  bool via_link = false;  // worker: the X_OPEN came over this loop's link (replies take it too)
   uint64_t owner_skey = 0;
   int data_sent = 0;          // worker: delta messages posted to the owner
   bool bulk_pending = false;  // worker: the final text is in flight (the slot must stay)
@@ -1104,6 +1107,7 @@ class Loop {
     if (kind == 6) return on_accept(afd_);
     if (kind == 2) return on_results();
     if (kind == 5) return on_xmsgs();
+    if (kind == 7) return on_link(fd, e.events);
     if (kind == 3) {
       auto it = clients_.find(fd);
       if (it != clients_.end()) on_client(it->second.get(), e.events);
@@ -2227,6 +2231,7 @@ class Loop {
       const int target = spread ? (xch_->rank() + (int)i) % xch_->world() : -1;
       if (spread && target != xch_->rank() && xch_->peer_up(target)) {
         s->bs[i].remote = target;
+        s->bs[i].via_link = link_up(target);  // the whole stream keeps one path (message order)
         s->remote_n++;
         // the owner's shadow slot: the remote stream's final text lands in its HBM content
         // area (RCCL, HBM to HBM), so this rank's fused finalize merges remote and local
@@ -2259,7 +2264,7 @@ class Loop {
         m.a = valid[i];
         m.b = (int)(cfg_.timeout * 1000.0);
         m.payload = build_req(cfg_.backends[valid[i]], s->fwd, body);
-        xq(m);
+        xq(m, s->bs[i].via_link);
         s->bs[i].t_sp_open = now_s();
         continue;
       }
@@ -2334,17 +2339,131 @@ class Loop {
   }
   // mesh messages of this loop pass, framed per destination rank and handed to the exchange
   // once per pass (flush_x: one lock + one wake), not one locked post + wake per message
-  void xq(const XMsg& hdr, const char* payload, size_t n) {
+  // link: over this loop's own connection to the rank (a frame for a link that went down is
+  // dropped, as the mesh drops frames for a peer that is down: its sessions were failed)
+  void xq(const XMsg& hdr, const char* payload, size_t n, bool link) {
     if (!xch_) return;
+    if (link) {
+      if (hdr.dst_rank < 0 || hdr.dst_rank >= (int)xl_.size() || xl_[hdr.dst_rank].fd < 0) return;
+      XLink& L = xl_[hdr.dst_rank];
+      if (L.out_off == L.out.size()) {
+        L.out.clear();
+        L.out_off = 0;
+      }
+      Exchange::append_frame(L.out, hdr, payload, n);
+      xlpending_ = true;
+      c_link_msgs++;
+      return;
+    }
     if (xout_.size() < (size_t)xch_->world()) xout_.resize(xch_->world());
     Exchange::append_frame(xout_[hdr.dst_rank], hdr, payload, n);
     xpending_ = true;
   }
-  void xq(const XMsg& m) { xq(m, m.payload.data(), m.payload.size()); }
+  void xq(const XMsg& m, bool link) { xq(m, m.payload.data(), m.payload.size(), link); }
   void flush_x() {
+    if (xlpending_) {
+      xlpending_ = false;
+      for (int r = 0; r < (int)xl_.size(); ++r)
+        if (xl_[r].fd >= 0 && !xl_[r].want_out && xl_[r].out_off < xl_[r].out.size()) flush_link(r);
+    }
     if (!xpending_) return;
     xpending_ = false;
     for (int r = 0; r < (int)xout_.size(); ++r) xch_->post_frames(r, xout_[r]);
+  }
+  // ---- per-loop links (Exchange X_LINK): this loop's own socket to loop idx_ of each rank
+  struct XLink {
+    int fd = -1;
+    std::string in, out;
+    size_t out_off = 0;
+    bool want_out = false;
+  };
+  bool link_up(int r) const { return r >= 0 && r < (int)xl_.size() && xl_[r].fd >= 0; }
+  void on_link_msg(const XMsg& m) {  // X_LINK: adopt the socket (replacing a stale one)
+    const int r = m.a, fd = m.b;
+    if (!xch_ || r < 0 || r >= xch_->world()) {
+      close(fd);
+      return;
+    }
+    if (xl_.size() < (size_t)xch_->world()) xl_.resize(xch_->world());
+    if (xl_[r].fd >= 0) link_down(r, false);
+    xl_[r].fd = fd;
+    xl_[r].in = m.payload;
+    add(fd, EPOLLIN, tag(7, fd));
+    if (!xl_[r].in.empty()) read_link(r, false);
+  }
+  int link_of(int fd) const {
+    for (int r = 0; r < (int)xl_.size(); ++r)
+      if (xl_[r].fd == fd) return r;
+    return -1;
+  }
+  void on_link(int fd, uint32_t ev) {
+    const int r = link_of(fd);
+    if (r < 0) return;
+    if (ev & EPOLLOUT) flush_link(r);
+    if (xl_[r].fd >= 0 && (ev & (EPOLLIN | EPOLLHUP | EPOLLERR))) read_link(r, true);
+  }
+  void read_link(int r, bool do_recv) {
+    XLink& L = xl_[r];
+    bool dead = false;
+    while (do_recv) {
+      char buf[65536];
+      ssize_t n = recv(L.fd, buf, sizeof(buf), 0);
+      cnt(SC_RECV);
+      if (n > 0) {
+        L.in.append(buf, (size_t)n);
+        if (n < (ssize_t)sizeof(buf)) break;
+        continue;
+      }
+      if (n == 0 || (errno != EAGAIN && errno != EWOULDBLOCK)) dead = true;
+      break;
+    }
+    std::vector<XMsg> msgs;
+    const size_t used = Exchange::parse_frames(L.in, msgs);
+    L.in.erase(0, used);
+    if (!msgs.empty()) handle_x(msgs, true);
+    if (dead) link_down(r, true);
+  }
+  void flush_link(int r) {
+    XLink& L = xl_[r];
+    while (L.fd >= 0 && L.out_off < L.out.size()) {
+      ssize_t w = send(L.fd, L.out.data() + L.out_off, L.out.size() - L.out_off, MSG_NOSIGNAL);
+      cnt(SC_UP_SEND);
+      if (w > 0) {
+        L.out_off += (size_t)w;
+        continue;
+      }
+      if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+        if (!L.want_out) {
+          L.want_out = true;
+          mod(L.fd, EPOLLIN | EPOLLOUT, tag(7, L.fd));
+        }
+        return;
+      }
+      return link_down(r, true);
+    }
+    if (L.fd >= 0) {
+      L.out.clear();
+      L.out_off = 0;
+      if (L.want_out) {
+        L.want_out = false;
+        mod(L.fd, EPOLLIN, tag(7, L.fd));
+      }
+    }
+  }
+  // a link closed: its streams end as for a peer that left this loop's reach (X_DOWN); new
+  // sessions use the mesh until the exchange hands over a new link
+  void link_down(int r, bool fail_streams) {
+    XLink& L = xl_[r];
+    if (L.fd < 0) return;
+    epoll_ctl(ep_, EPOLL_CTL_DEL, L.fd, nullptr);
+    cnt(SC_EPOLL_CTL);
+    close(L.fd);
+    L = XLink();
+    if (!fail_streams) return;
+    std::vector<XMsg> v(1);
+    v[0].type = X_DOWN;
+    v[0].a = r;
+    handle_x(v, true);
   }
   void post_owner(Session* s, uint8_t type, uint8_t flags, int a, const char* payload, size_t n, int b = 0) {
     if (!xch_) return;
@@ -2359,7 +2478,7 @@ class Loop {
     m.skey = s->owner_skey;
     m.a = a;
     m.b = b;
-    xq(m, payload, n);
+    xq(m, payload, n, s->via_link);
   }
   // owner: a remote stream ends with `sent` deltas announced by its worker; anything else
   // than the count received means deltas were lost or are still missing
@@ -2382,8 +2501,16 @@ class Loop {
       std::lock_guard<std::mutex> g(xmu_);
       in.swap(xin_);
     }
+    handle_x(in, false);
+  }
+  // exchange messages from the mesh thread (link = false) or this loop's own links
+  void handle_x(std::vector<XMsg>& in, bool link) {
     for (auto& m : in) {
       if (m.type == X_UP) continue;  // a peer (re)joined: new sessions may place streams there
+      if (m.type == X_LINK) {
+        on_link_msg(m);
+        continue;
+      }
       if (m.type == X_DOWN) {
         // peer m.a (or, a = -1, every peer) is unreachable: fail the streams it runs for
         // our sessions, drop the streams we run for its sessions (a worker whose final
@@ -2411,6 +2538,7 @@ class Loop {
         s->owner_loop = m.src_loop;
         s->owner_skey = m.skey;
         s->shadow_bi = m.bi;
+        s->via_link = link;
         s->filter = m.flags & 1;
         s->emit = (m.flags & 2) != 0;
         s->bs.resize(1);
@@ -2861,7 +2989,7 @@ class Loop {
         m.dst_loop = m.src_loop = (uint16_t)idx_;
         m.bi = i;
         m.skey = s->skey;
-        xq(m);
+        xq(m, s->bs[i].via_link);
       }
     }
     for (int i = 0; i < (int)s->bs.size(); ++i) {
@@ -2906,6 +3034,7 @@ class Loop {
     put("qmx_client_connections_total", (double)c_clients.load());
     put("qmx_ticks_total", (double)c_ticks.load());
     put("qmx_output_coalesced_total", (double)c_coalesced.load());
+    put("qmx_exchange_link_messages_total", (double)c_link_msgs.load());
     put("qmx_tick_slots_total", (double)c_tick_slots.load());
     put("qmx_tick_route_seconds_total", (double)c_route_ns.load() * 1e-9);
     put("qmx_flush_wait_seconds_total", (double)c_flush_ns.load() * 1e-9);
@@ -2943,7 +3072,8 @@ class Loop {
       put("qmx_exchange_bulk_bytes_total", (double)xch_->bulk_bytes());  // final texts, HBM to HBM
       put("qmx_exchange_mesh_finals_total", (double)xch_->mesh_bulk());  // final texts over the mesh
       put("qmx_exchange_epochs_total", (double)xch_->epochs());
-      put("qmx_exchange_rescued_total", (double)xch_->rescued());  // resent on the receiver's report
+      put("qmx_exchange_rescued_total", (double)xch_->rescued());
+      put("qmx_exchange_links_total", (double)xch_->links());  // per-loop links handed to the io loops  // resent on the receiver's report
       put("qmx_exchange_rejoins_total", (double)xch_->rejoins());
       put("qmx_exchange_peer_downs_total", (double)xch_->downs());
       put("qmx_exchange_busy_us_total", xch_->busy_us());
@@ -3041,6 +3171,8 @@ class Loop {
   std::vector<XMsg> xin_;
   std::vector<std::string> xout_;  // per destination rank: frames of this loop pass
   bool xpending_ = false;
+  std::vector<XLink> xl_;  // per rank: this loop's link (fd -1: none yet / down)
+  bool xlpending_ = false;
   uint64_t next_skey_ = 1;
   std::unordered_map<uint64_t, Session*> rsess_;            // owner sessions with remote streams
   std::map<std::pair<uint64_t, int>, Session*> shadow_;     // worker streams by (owner key, bi)
@@ -3181,6 +3313,8 @@ int run_server(const ServerCfg& cfg0) {
     o.device = cfg.device;
     o.batch_us = cfg.xchg_round_us;
     o.timeout_s = cfg.xchg_timeout;
+    // per-loop links (0: every session message via the mesh thread)
+    o.links = cfg.xchg_links >= 0 ? cfg.xchg_links != 0 : env_flag("QMX_XCHG_LINKS", true);
     std::vector<Loop*> lp;
     for (auto& l : loops) lp.push_back(l.get());
     xch.reset(new Exchange(o, (int)lp.size(), [lp](int l, std::vector<XMsg>&& v) { lp[l]->x_deliver(std::move(v)); }));

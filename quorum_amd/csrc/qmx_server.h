@@ -75,6 +75,7 @@ struct ServerCfg {
   // round, no rank-0 manifest — the MPI eager protocol); a larger one takes a bulk round
   // (rendezvous: manifest + RCCL / socket transfer).  0: every final text takes a round
   int xchg_eager_bytes = 4096;
+  int xchg_links = -1;  // per-loop exchange links: 1 on, 0 off, -1 QMX_XCHG_LINKS (default on)
   double xchg_timeout = 30.0;
   // lifecycle: SIGTERM drains (no new connections; in-flight sessions finish, at most
   // drain_s seconds), SIGINT / stop_server() stop at once; ready_file is written once

@@ -63,4 +63,7 @@ def cluster_config(placement: str, exchange: str, round_us: int, timeout: float,
         "xchg_timeout": float(e.get("QMX_XCHG_TIMEOUT", str(timeout))),
         # final texts up to this size ride the mesh behind their deltas (eager, no round)
         "xchg_eager_bytes": int(e.get("QMX_XCHG_EAGER_BYTES", str(eager_bytes))),
+        # per-loop links: io loop l of each rank pair on a connection of its own (0: the mesh
+        # thread carries every session message)
+        "xchg_links": int(e.get("QMX_XCHG_LINKS", "1")),
     }

@@ -38,7 +38,8 @@ THINK = [sse_chunk({"role": "assistant"}), sse_chunk({"content": "<think>"}), ss
 
 
 @contextlib.contextmanager
-def native_cluster(cfg, world: int, placement: str = "spread", xchg: str = "tcp", eager=None, tick_mode=None):
+def native_cluster(cfg, world: int, placement: str = "spread", xchg: str = "tcp", eager=None, tick_mode=None,
+                   links=None):
     """`world` native ranks in-process (threads), TCP exchange on a free port block.
     ``xchg="tcpbulk"``: final texts move in rank-0-numbered bulk rounds (the RCCL round
     protocol with a socket executor) instead of riding the mesh.  ``eager``: the largest final
@@ -72,6 +73,8 @@ def native_cluster(cfg, world: int, placement: str = "spread", xchg: str = "tcp"
                 else:
                     os.environ[k] = v
         d["install_signals"] = False
+        if links is not None:  # per-loop links on / off (off: every message through the mesh thread)
+            d["xchg_links"] = 1 if links else 0
         if tick_mode is not None:
             d["tick_mode"] = tick_mode
         cfgs.append(d)
@@ -167,13 +170,16 @@ SPREAD_CASES = {
 }
 
 
-@pytest.mark.parametrize("world,xchg,eager", [(2, "tcp", None), (3, "tcp", 0), (2, "tcpbulk", 0), (4, "tcpbulk", 0),
-                                               (3, "tcpbulk", None)])
+@pytest.mark.parametrize("world,xchg,eager,links", [(2, "tcp", None, True), (3, "tcp", 0, True),
+                                                     (2, "tcpbulk", 0, True), (4, "tcpbulk", 0, True),
+                                                     (3, "tcpbulk", None, True), (2, "tcp", None, False),
+                                                     (3, "tcpbulk", 0, False)])
 @pytest.mark.parametrize("name", sorted(SPREAD_CASES))
-def test_spread_matches_local(name, world, xchg, eager):
+def test_spread_matches_local(name, world, xchg, eager, links):
     """Spread responses equal single-rank ones, with every final-text path: eager (short texts
     ride the mesh behind their deltas: the default), mesh bulk (tcp, eager off) and bulk
-    rounds (tcpbulk, eager off)."""
+    rounds (tcpbulk, eager off) — session messages over the io loops' own links (default) or
+    through the mesh thread (links off)."""
     n, block, strategy, behs = SPREAD_CASES[name]
     live, ports = _live({f"b{i + 1}": b for i, b in enumerate(behs)})
     try:
@@ -183,7 +189,7 @@ def test_spread_matches_local(name, world, xchg, eager):
             ref = httpx.post(f"http://127.0.0.1:{p}/chat/completions", json=req, headers=AUTH, timeout=30)
         ref_calls = sorted(json.dumps(c["body"], sort_keys=True) for c in live.calls)
         live.calls.clear()
-        with native_cluster(cfg, world, xchg=xchg, eager=eager) as cports:
+        with native_cluster(cfg, world, xchg=xchg, eager=eager, links=links) as cports:
             # (in-process ranks share one process's counters, across tests too: deltas)
             m0 = [httpx.get(f"http://127.0.0.1:{p}/metrics").text for p in cports]
             for owner in range(world):  # every rank as session owner
@@ -200,6 +206,9 @@ def test_spread_matches_local(name, world, xchg, eager):
         remote = float([ln for ln in m.splitlines() if ln.startswith("qmx_remote_streams_total")][0].split()[1])
         assert remote >= 1, m
         assert _metric(m, "qmx_spread_delta_mismatch_total") == 0
+        link_msgs = _metric(ms[0], "qmx_exchange_link_messages_total") - _metric(m0[0], "qmx_exchange_link_messages_total")
+        assert (link_msgs > 0) == links, link_msgs
+
         def total(k):
             # exchange counters are per rank (summed); server counters are per process, which
             # the in-process ranks share (rank 0's delta)
@@ -341,8 +350,11 @@ def test_idle_cluster_exchanges_nothing():
             a = snap(cports)
             time.sleep(1.0)
             b = snap(cports)
-        assert a["qmx_exchange_messages_total"] > 0  # the traffic did use the mesh
+        # the traffic did cross ranks: over the io loops' own links (the default) and the mesh
+        # (control: epochs, links' set-up); idle, neither moves
+        assert a["qmx_exchange_link_messages_total"] > 0 and a["qmx_exchange_links_total"] > 0
         assert b["qmx_exchange_messages_total"] == a["qmx_exchange_messages_total"], (a, b)
+        assert b["qmx_exchange_link_messages_total"] == a["qmx_exchange_link_messages_total"], (a, b)
         assert b["qmx_exchange_rounds_total"] == a["qmx_exchange_rounds_total"] == 0  # tcp: no RCCL rounds
         assert b["qmx_exchange_peers_up"] == 9  # 3 ranks x 3
     finally:
