@@ -39,10 +39,12 @@ sys.path.insert(0, ROOT)
 BASELINE_SOURCE_SAME = "reference proxy, same box + same harness (bench.py --impl reference)"
 BASELINE_SOURCE_SURVEY = "reference proxy, survey container (8 vCPU, Python harness; SURVEY §6)"
 
-# port layout above --port: +7.. exchange mesh, +50 the spread check's proxies (+57.. its mesh),
+# port layout above --port: +7.. exchange mesh, +50 the spread check's proxies (+57.. its mesh;
+# +20 / +80 its rendezvous / local sets), +60 the config-3 pass (+67.. its mesh; sets run one at a time),
 # +100 + 10 rank + i mock backends, +200 + rank / +230 + rank each rank's own admin port
 # (headline / spread check)
-ADMIN_OFF, SPREAD_ADMIN_OFF, LOCAL_ADMIN_OFF, RDV_ADMIN_OFF = 200, 230, 240, 250
+ADMIN_OFF, SPREAD_ADMIN_OFF, LOCAL_ADMIN_OFF, RDV_ADMIN_OFF, C3_ADMIN_OFF = 200, 230, 240, 250, 260
+CONFIG3_REQUESTS = 4096  # per rank: the config-3 pass after the headline (spread, RCCL rounds)
 PROBE_REQUESTS = 256  # spread check: requests of the one-connection latency probes
 
 # BASELINE.json configs.  "headline" is the driver's metric; the others are measured with
@@ -505,6 +507,10 @@ def spread_summary(rows) -> dict:
                           "p50_latency_ms": med([get(r, "rendezvous", "load", "p50_latency_ms") for r in rows]),
                           "probe_p50_latency_ms": med([get(r, "rendezvous", "probe", "p50_latency_ms") for r in rows]),
                           "hops_us_probe": hops("rendezvous", "probe", "hops_us")}}
+    degraded = [f"rank {i}: {get(r, 'rendezvous', 'degraded')}" for i, r in enumerate(rows)
+                if get(r, "rendezvous", "degraded")]
+    if degraded:  # the round protocol did not run somewhere (finals took the mesh, validated)
+        out["degraded"] = degraded[:8]
     errs = [f"rank {i} {k}: {get(r, k, 'error')}" for i, r in enumerate(rows) for k in ("main", "rendezvous", "local")
             if get(r, k, "error")]
     if errs or any(r.get("error") for r in rows):
@@ -581,12 +587,89 @@ def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports
             "local": local}
 
 
+def config3_check(args, rank, world, engine, device, bin_dir, tmp, mock_ports, dist, n_dev):
+    """Outside the headline's timed region, N > 1: BASELINE config 3 measured — 4 mock
+    backends, streaming aggregate strategy, sessions sharded over the ranks AND each
+    session's backend streams spread over them (backend i on rank owner + i), with EVERY
+    remote final text moved by a bulk round (exchange_eager_bytes 0): RCCL ncclSend /
+    ncclRecv HBM -> HBM on a GPU node (tcpbulk when ranks share a GPU), then the owner's
+    fused GPU finalize (K3 / K4 texts for the aggregator prompt).  One timed, validated pass
+    per rank; its req/s, TTFT, round counts and costs are reported under ``config3``."""
+    from quorum_amd.parallel.exchange import exchange_env
+
+    sc = SCENARIOS["aggregate4"]
+    on_gpu = n_dev >= world
+    xchg = os.environ.get("QMX_XCHG") or ("rccl" if on_gpu and engine == "hip" else "tcpbulk")
+    if xchg == "rccl" and not (on_gpu and engine == "hip"):
+        xchg = "tcpbulk"
+    extra, prep_err = [], None
+    ports = list(mock_ports)
+    try:
+        for i in range(len(ports), sc["n"]):  # the headline ran 2 backends: 2 more mocks
+            p = args.port + 100 + rank * 10 + i
+            extra.append(subprocess.Popen([os.path.join(bin_dir, "qmx_mock"), "--port", str(p), "--threads",
+                                           str(args.mock_threads), "--tokens", "20", "--think", "1"],
+                                          stderr=subprocess.DEVNULL, start_new_session=True))
+            ports.append(p)
+        spec = os.path.join(tmp, "expect_config3.txt")
+        expect_spec(spec, sc, False, mock_expected(bin_dir))
+    except Exception as e:  # noqa: BLE001
+        prep_err = repr(e)[:300]
+    try:
+        if not torch_min_flag(dist, prep_err is None, on_gpu):
+            return {"ok": False, "error": prep_err or "another rank failed to prepare the config-3 pass"}
+        nonce = [str(time.time_ns()) if rank == 0 else None]
+        dist.broadcast_object_list(nonce, src=0)
+        xenv = dict(exchange_env(rank, world, args.port + 60, nonce[0]), QMX_XCHG=xchg, QMX_XCHG_EAGER_BYTES="0",
+                    QMX_XCHG_TIMEOUT=os.environ.get("QMX_XCHG_TIMEOUT", "3"))
+        ctx = {"args": args, "rank": rank, "dist": dist, "on_gpu": on_gpu, "tmp": tmp, "mock_ports": ports, "sc": sc,
+               "engine": engine, "device": device, "bin_dir": bin_dir, "spec": spec}
+        res = run_set(ctx, "config3", "spread", args.port + 60, args.port + C3_ADMIN_OFF + rank, xenv,
+                      [("load", 16, CONFIG3_REQUESTS)], want_bulk=True)
+        res["transport"] = xchg
+        return res
+    finally:
+        _kill(extra)
+
+
+def config3_summary(rows) -> dict:
+    """The config-3 pass of every rank: node req/s (total requests / slowest rank's wall),
+    validation, and how the remote finals moved (rounds, their mean duration, bytes)."""
+    loads = [(r or {}).get("load") or {} for r in rows]
+    walls = [l["requests"] / l["req_s"] for l in loads if l.get("req_s")]
+    reqs = sum(int(l.get("requests", 0)) for l in loads)
+    out = {"ok": all((r or {}).get("ok") for r in rows), "transport": (rows[0] or {}).get("transport"),
+           "scenario": "aggregate4 + placement spread, exchange_eager_bytes 0 (every remote final through a round)",
+           "requests": reqs, "req_s": round(reqs / max(walls), 1) if walls else None,
+           "p50_ttft_ms": (round(statistics.median(l["p50_ttft_ms"] for l in loads if l.get("p50_ttft_ms") is not None), 3)
+                           if any(l.get("p50_ttft_ms") is not None for l in loads) else None),
+           "invalid": sum(int(l.get("invalid", 0)) for l in loads),
+           "bulk_rounds": int(sum(l.get("bulk_rounds", 0) for l in loads)),
+           "bulk_final_MB": round(sum(l.get("bulk_final_bytes", 0) for l in loads) / 1e6, 3),
+           "mesh_finals": int(sum(l.get("mesh_finals", 0) for l in loads)),
+           "finalize_host": int(sum(l.get("finalize_host", 0) for l in loads)),
+           "remote_texts_gpu": {"hbm": int(sum(l.get("remote_texts_hbm", 0) for l in loads)),
+                                "staged": int(sum(l.get("remote_texts_staged", 0) for l in loads))},
+           "delta_mismatch": int(sum(l.get("delta_mismatch", 0) for l in loads)),
+           "per_rank": [{"requests": l.get("requests"), "req_s": l.get("req_s"), "bulk_rounds": l.get("bulk_rounds"),
+                         "round_us_avg": l.get("round_us_avg"), "hops_us": l.get("hops_us")} for l in loads]}
+    errs = [f"rank {i}: {(r or {}).get('error')}" for i, r in enumerate(rows) if (r or {}).get("error")]
+    if errs:
+        out["errors"] = errs[:8]
+    deg = [f"rank {i}: {(r or {}).get('degraded')}" for i, r in enumerate(rows) if (r or {}).get("degraded")]
+    if deg:
+        out["degraded"] = deg[:8]
+    return out
+
+
 def spread_counters(d) -> dict:
     """A spread proxy's /metrics delta over one pass: how its remote streams moved and ended."""
     return {"remote_streams": d.get("qmx_remote_streams_total", 0.0),
             "eager_finals": d.get("qmx_spread_eager_finals_total", 0.0),
             "bulk_rounds": d.get("qmx_exchange_rounds_total", 0.0),
             "bulk_final_bytes": d.get("qmx_exchange_bulk_bytes_total", 0.0),
+            "round_us_avg": (round(d.get("qmx_exchange_busy_us_total", 0.0) / d["qmx_exchange_rounds_total"], 1)
+                             if d.get("qmx_exchange_rounds_total") else None),
             "mesh_finals": d.get("qmx_exchange_mesh_finals_total", 0.0),
             "mesh_messages": d.get("qmx_exchange_messages_total", 0.0),
             "delta_mismatch": d.get("qmx_spread_delta_mismatch_total", 0.0),
@@ -687,11 +770,12 @@ def run_set(ctx, label, placement, port, admin, xenv, passes, want_bulk=False) -
     if err is None and not up:
         err = f"another rank's {label} set failed"
     if err is None and want_bulk:
-        # the rendezvous set exists to run the round protocol: no communicator or no round
-        # on this rank is a failure, not a silent mesh fallback
+        # the rendezvous set exists to run the round protocol: no communicator, or no round on
+        # this rank, is reported as DEGRADED (its finals fell back to the mesh and were still
+        # validated), never as a silent pass — and never hidden inside "ok"
         rounds = sum((res.get(p[0]) or {}).get("bulk_rounds", 0) for p in passes)
         if not res.get("bulk_formed") or rounds <= 0:
-            err = f"{label}: bulk rounds did not run (formed {res.get('bulk_formed')}, rounds {rounds})"
+            res["degraded"] = f"{label}: bulk rounds did not run (formed {res.get('bulk_formed')}, rounds {rounds})"
     res["ok"] = err is None and all((res.get(p[0]) or {}).get("ok") for p in passes)
     if err:
         res["error"] = err
@@ -972,7 +1056,7 @@ def main() -> int:
             # a remote stream whose delta count disagrees with its worker's, or a worker stream
             # that sent no delta for content it had, is a broken run even if the bytes validated
             bad += int(bd["exchange"]["delta_mismatch"] + bd["exchange"]["worker_nodata"])
-        spread = None
+        spread = c3_rows = None
         if (dist is not None and world > 1 and args.spread_check and args.impl == "native"
                 and args.placement == "local"):
             _kill(proxy_procs)  # done measuring; the check brings up its own proxy set
@@ -981,6 +1065,9 @@ def main() -> int:
             spread_rows = [None] * world
             dist.all_gather_object(spread_rows, spread)
             spread = spread_rows
+            c3 = config3_check(args, rank, world, engine, device, bin_dir, tmp, mock_ports, dist, n_dev)
+            c3_rows = [None] * world
+            dist.all_gather_object(c3_rows, c3)
         local = [elapsed, float(stats["completed"]), float(stats["ttft_p50_ms"]), float(stats["ttft_p99_ms"]),
                  float(stats["errors"] + stats["non200"]), float(stats["ttfb_p50_ms"]), float(stats["lat_p50_ms"]),
                  float(len(dead)), float(stats["invalid"]), float(stats["no_content"]), float(stats["validated"]),
@@ -996,6 +1083,8 @@ def main() -> int:
         headline_ok = ok
         if spread is not None:  # a failed spread check fails the run (its responses are validated too)
             ok = ok and all(r.get("ok") for r in spread)
+        if c3_rows is not None:  # so does an invalid config-3 response (RCCL not forming: degraded)
+            ok = ok and all((r or {}).get("ok") for r in c3_rows)
         # per-rank breakdowns, each scraped from that rank's own proxy (admin port)
         bd_rows = [bd]
         if dist is not None:
@@ -1062,6 +1151,8 @@ def main() -> int:
                 res["exited"] = dead or dead_warm
             if spread is not None:  # outside the timed region; per rank, each from its own proxy
                 res["spread_check"] = spread_summary(spread)
+            if c3_rows is not None:  # BASELINE config 3, timed on its own (RCCL rounds on a GPU node)
+                res["config3"] = config3_summary(c3_rows)
             print(json.dumps(res), flush=True)
     finally:
         _kill(procs)

@@ -2492,7 +2492,9 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* doors, PCtl* ct
       if (tid < kWords)
         __hip_atomic_store((uint32_t*)&ctl->d + tid, ((const uint32_t*)&D)[tid], __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-      if (tid == 0) __hip_atomic_store(&ctl->next[c & 3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // item 0 is the relay's own (no claim round trip on the first item's path): the
+      // others claim from 1
+      if (tid == 0) __hip_atomic_store(&ctl->next[c & 3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __threadfence();
       __syncthreads();
       if (tid == 0) {
@@ -2521,9 +2523,13 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* doors, PCtl* ct
     const int total = (int)(n_tick + __builtin_amdgcn_readfirstlane(D.n_fin));
     const uint32_t seq = __builtin_amdgcn_readfirstlane(D.seq);
     // items are claimed from the tick's counter, not dealt by workgroup index: a workgroup
-    // that is not resident (the CUs are shared with other grids / kernels) holds up nothing
+    // that is not resident (the CUs are shared with other grids / kernels) holds up nothing.
+    // The relay runs item 0 without a claim (it reset the counter to 1 before publishing).
+    bool own0 = relay;
     for (;;) {
-      if (tid == 0) cmd = __hip_atomic_fetch_add(&ctl->next[seq & 3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0)
+        cmd = own0 ? 0u : __hip_atomic_fetch_add(&ctl->next[seq & 3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      own0 = false;
       __syncthreads();
       const int k = (int)cmd;
       __syncthreads();  // cmd is rewritten by the next claim

@@ -139,6 +139,12 @@ def test_bench_gpus_flag_self_launches_ranks(tmp_path):
     assert sc["bulk_rounds"] > 0 and sc["mesh_finals"] == 0
     assert sc["rendezvous"]["remote_ends"] == {"text": 4 * 512}
     assert len({x["pid"] for x in sc["per_rank"]}) == 4
+    # BASELINE config 3 after the spread check: aggregate4, spread, every remote final through
+    # a bulk round (tcpbulk: the ranks share no GPU), every response validated
+    c3 = res["config3"]
+    assert c3["ok"] is True and c3["invalid"] == 0 and c3["requests"] == 4 * 4096 and c3["req_s"] > 0, c3
+    assert c3["transport"] == "tcpbulk" and c3["bulk_rounds"] > 0 and c3["mesh_finals"] == 0, c3
+    assert c3["delta_mismatch"] == 0 and "degraded" not in c3, c3
     # one-session latency probes, every response validated: the eager default, rendezvous
     # (every text through a round) and the same config placed locally
     assert None not in (sc["probe_p50_latency_ms"], sc["local_probe_p50_latency_ms"],
