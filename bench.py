@@ -1126,8 +1126,10 @@ def main() -> int:
                            # the default) or hand streams to tick-lane threads ("lanes")
                            "tick_mode": os.environ.get("QMX_TICK_MODE", "auto") if engine == "hip" else None,
                            "io_threads_per_rank": args.threads, "cpu_pinning": pinning,
+                           # the node's xGMI topology, only when every rank has a GPU of its own
+                           # (a rehearsal's ranks share one: no link claim to make)
                            "gpu_links": ({k: v for k, v in link_summary().items() if k != "links_per_gpu"}
-                                         if world > 1 else None)},
+                                         if world > 1 and n_dev >= world else None)},
                 "p50_ttft_ms": round(p50, 3),
                 "p99_ttft_ms": round(max(r[3] for r in rows), 3),
                 "p50_ttfb_ms": round(statistics.median(r[5] for r in rows), 3),
