@@ -149,10 +149,13 @@ for l in open('$OUT/pmcg_$slug.log'):
 print(int(t))")
       python3 tools/pmc_summary.py --per-tick $nt $(find $OUT/pmcg_$slug -name '*counter_collection.csv') > $OUT/pmcg_$slug.md 2>&1
       grep -v rocclr $OUT/pmcg_$slug.md | head -30 ;;
-    kbenchgrid)  # in-kernel stage split of the production kernel (persistent grid)
-      QMX_STAGE_TIMING=1 timeout -k 10 300 python tools/kbench.py --grid 16 --slots 1,3,22 --iters 100 --combos ft > $OUT/kbenchgrid.jsonl 2>&1 \
-        || { echo "kbenchgrid failed"; tail -5 $OUT/kbenchgrid.jsonl; exit 1; }
-      grep -v '^{"grid_stats' $OUT/kbenchgrid.jsonl | python3 -c "
+    kbenchgrid|kbenchgrid:*)  # in-kernel stage split of the production kernel (persistent grid); :ENV=V,... extra env
+      e=""; kslug=""
+      if [ "$step" != kbenchgrid ]; then e=${step#kbenchgrid:}; kslug=_$(echo "$e" | tr -c 'a-zA-Z0-9' '_' | cut -c1-40); fi
+      env ${e//,/ } QMX_STAGE_TIMING=1 timeout -k 10 300 python tools/kbench.py --grid 16 --slots 1,3,22 --iters 100 --combos ft > $OUT/kbenchgrid$kslug.jsonl 2>&1 \
+        || { echo "kbenchgrid failed"; tail -5 $OUT/kbenchgrid$kslug.jsonl; exit 1; }
+      echo "-- $e"
+      grep -v '^{"grid_stats' $OUT/kbenchgrid$kslug.jsonl | python3 -c "
 import json, sys
 for l in sys.stdin:
     if not l.startswith('{'): continue
