@@ -111,8 +111,7 @@ enum : int {
   V_START = 0, V_NSEP, V_LASTSEP, V_ABORT, V_NEV, V_CONSUMED, V_STATUS, V_NDELTA, V_YLEN, V_NCAND,
   V_NTOK, V_BAIL, V_DEPTH0, V_TAILLEN, V_NEWTAIL, V_NEWDEPTH, V_WLEN, V_NEMIT, V_ETOT, V_OUTLEN,
   V_TPLPRE, V_TPLSUF, V_TPLK, V_NEXTEV, V_NFULL, V_NTPL, V_CFULL, V_CTPL, V_CLEX, V_NHOLE, V_CHOLE, V_S4W,
-  V_HCLAIM,  // hole-template slots this workgroup wrote (bit per slot): one writer per slot
-  V_S2W       // S1 + S2 fused (QMX_KFAST bit 16): wave 0 framed the tile right after S1
+  V_HCLAIM  // hole-template slots this workgroup wrote (bit per slot): one writer per slot
 };
 
 // LDS byte reader that fetches one aligned 64-bit word per 8 sequential bytes: a byte-serial
@@ -934,9 +933,8 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   if (tid < tail_len) Z[tid] = state[it.slot].tail[tid];
 
   // ---- S1: leading whitespace at stream start ---------------------------------------
-  // (one thread; with QMX_KFAST bit 16, wave 0 goes straight on into S2's one-wave framing
-  // of the common tile — S1's and S2's block barriers become one)
-  auto s1 = [&]() {
+  // (fusing it with S2's one-wave framing into one barrier measured no faster: r4/d)
+  if (tid == 0) {
     int pos = 0;
     bool started = it.flags & WF_STARTED;
     bool wait = false;
@@ -956,17 +954,6 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       s.v[V_CONSUMED] = pos;
       if (eof) s.v[V_STATUS] |= WS_DONE;
     }
-    return !wait && (P.fast & 1) && (pos & 7) == 0 && in_len - pos <= 4096;
-  };
-  const bool fuse12 = (P.fast & 16) != 0;
-  if (fuse12) {
-    if (tid < 64) {
-      if (tid == 0) s.v[V_S2W] = s1() ? 1 : 0;
-      wave_fence();
-      if (__builtin_amdgcn_readfirstlane(s.v[V_S2W])) s2_wave(s, s.v[V_START], in_len, eof);
-    }
-  } else if (tid == 0) {
-    s1();
   }
   __syncthreads();
   if (s.v[V_BAIL]) {
@@ -990,10 +977,8 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   // over stride-C chunks were bank-conflicted LDS reads, three passes over every byte.
   const int flen0 = in_len - start;
   const int C8 = (((flen0 + BS - 1) / BS) + 7) & ~7;
-  const bool s2_done = fuse12 && s.v[V_S2W];  // framed by wave 0 right after S1
-  const bool s2_wave_ok = s2_done || ((P.fast & 1) && (start & 7) == 0 && flen0 <= 4096);
-  if (s2_done) {
-  } else if (s2_wave_ok) {
+  const bool s2_wave_ok = (P.fast & 1) && (start & 7) == 0 && flen0 <= 4096;
+  if (s2_wave_ok) {
     if (tid < 64) s2_wave(s, start, in_len, eof);
   } else if ((start & 7) == 0 && C8 <= 32) {
     const int lo = min(start + tid * C8, in_len), hi = min(lo + C8, in_len);
@@ -1091,7 +1076,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       s.v[V_NSEP] = nsep;
     }
   }
-  if (!s2_done) __syncthreads();
+  __syncthreads();
   if (!s2_wave_ok) {  // (s2_wave finalises on its own lane 0)
     if (tid == 0) s2_finalize(s, start, in_len, eof);
     __syncthreads();

@@ -278,3 +278,31 @@ def test_bench_aggregate4_spread_finals_through_rounds(tmp_path, world):
         assert x["eager_finals"] == 0 and x["mesh_finals"] == 0, row
         assert x["delta_mismatch"] == 0 and x["worker_nodata"] == 0, row
         assert row["finalize_host"] == 0, row
+
+
+def test_spread_and_config3_summaries_report_degraded_and_invariants():
+    """The summaries never hide a broken invariant or a round protocol that did not run: a
+    rendezvous set without bulk rounds is DEGRADED (its finals took the mesh, still
+    validated), a delta mismatch fails its pass, and config3's node req/s divides the total
+    by the slowest rank's wall."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    ok_pass = {"ok": True, "requests": 100, "invalid": 0, "p50_latency_ms": 1.0, "remote_streams": 100,
+               "delta_mismatch": 0, "worker_nodata": 0, "bulk_rounds": 0, "finalize_host": 0,
+               "remote_texts_staged": 100, "remote_texts_hbm": 0}
+    row = {"ok": True, "transport": "rccl", "main": {"load": ok_pass, "probe": ok_pass},
+           "rendezvous": {"load": ok_pass, "probe": ok_pass, "bulk_formed": False,
+                          "degraded": "spread_rendezvous: bulk rounds did not run (formed False, rounds 0)"},
+           "local": {"probe": ok_pass}}
+    out = b.spread_summary([row, row])
+    assert out["ok"] is True and out["degraded"] and "bulk rounds did not run" in out["degraded"][0]
+    assert out["finalize_host"] == 0 and out["remote_texts_gpu"]["staged"] == 800
+    c3 = b.config3_summary([{"ok": True, "transport": "rccl",
+                             "load": dict(ok_pass, req_s=50.0, bulk_rounds=7, p50_ttft_ms=0.3)},
+                            {"ok": True, "transport": "rccl",
+                             "load": dict(ok_pass, req_s=25.0, bulk_rounds=5, p50_ttft_ms=0.5)}])
+    assert c3["requests"] == 200 and c3["req_s"] == 50.0  # 200 requests / the slower rank's 4 s
+    assert c3["bulk_rounds"] == 12 and c3["ok"] is True and "degraded" not in c3
