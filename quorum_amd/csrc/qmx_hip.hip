@@ -2499,7 +2499,10 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* doors, PCtl* ct
       // item 0 is the relay's own (no claim round trip on the first item's path): the
       // others claim from 1
       if (tid == 0) __hip_atomic_store(&ctl->next[c & 3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __threadfence();
+      // each wave's own stores done (descriptor words, counter, parameters), then the barrier:
+      // thread 0's agent-scope release of ctl->seq below is the one L2 write-back (a
+      // __threadfence() per thread was one per wave)
+      wave_stores_done();
       __syncthreads();
       if (tid == 0) {
         __hip_atomic_store(&door->t_relayed, (uint64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
