@@ -2295,7 +2295,16 @@ __device__ __forceinline__ void run_item(int k, const WorkItem* __restrict__ ite
     wave_stores_done();
     __syncthreads();
     if (Pk.dbg != nullptr && threadIdx.x == 0) dbg_put(&Pk.dbg[k * kDbg + 27], __builtin_amdgcn_s_memrealtime());
-    if (threadIdx.x == 0) __hip_atomic_store(&res[k].seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) {
+      if (Pk.fast & 64) {
+        // EXPERIMENT (QMX_KFAST bit 64): the host-memory stores are complete (vmcnt(0) per
+        // wave + barrier); publish the sequence number first, write the L2 back after
+        __hip_atomic_store(&res[k].seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      } else {
+        __hip_atomic_store(&res[k].seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
   } else {
     const int j = (int)(k - n_tick);
     fin_stage(fa, j, content, Pk.content_cap);

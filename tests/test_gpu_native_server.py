@@ -113,3 +113,46 @@ def test_native_hip_grid_sizing(sharers, want_grid, monkeypatch):
         assert doors == 4 and wpd == (2 if sharers == "16" else 8), (doors, wpd)
     else:
         assert doors is None and (_metric(m, "qmx_kernel_launches") or 0) > 0
+
+
+@pytest.mark.parametrize("xchg,eager", [("tcp", None), ("tcpbulk", 0)])
+@pytest.mark.parametrize("name", ["concat_think", "concat_null_abort", "aggregate_4", "concat_4_one_fails"])
+def test_hip_spread_cluster_matches_local(name, xchg, eager, monkeypatch):
+    """Spread placement on the HIP engine: 2 in-process ranks sharing GPU 0 (loop ticks, a
+    grid each), session messages on per-loop links, remote finals eager over the link or
+    through tcpbulk rounds.  Every response equals the single-rank HIP server's, and every
+    rank finalized its merged sessions on the GPU: fin_host stays 0 while remote texts were
+    staged into finalize items."""
+    import httpx
+
+    import test_native_spread as S
+    from live_upstream import native_server
+
+    monkeypatch.setenv("QMX_GPU_SHARERS", "2")  # two grids on one GPU (set before any server starts)
+    n, block, strategy, behs = S.SPREAD_CASES[name]
+    live, ports = S._live({f"b{i + 1}": b for i, b in enumerate(behs)})
+    try:
+        cfg = S._cfg(n, block, strategy, [f"http://127.0.0.1:{ports[f'b{i + 1}']}/v1" for i in range(n)])
+        req = {"messages": S.MSG, "stream": True}
+        with native_server(cfg, engine="hip") as p:
+            ref = httpx.post(f"http://127.0.0.1:{p}/chat/completions", json=req, headers=S.AUTH, timeout=30)
+        with S.native_cluster(cfg, 2, xchg=xchg, eager=eager, engine="hip") as cports:
+            m0 = [httpx.get(f"http://127.0.0.1:{p}/metrics").text for p in cports]
+            for owner in range(2):
+                for _ in range(3):
+                    r = httpx.post(f"http://127.0.0.1:{cports[owner]}/chat/completions", json=req, headers=S.AUTH,
+                                   timeout=30)
+                    assert r.status_code == ref.status_code
+                    assert S._split(S._events(r.text)) == S._split(S._events(ref.text)), (name, owner)
+            ms = [httpx.get(f"http://127.0.0.1:{p}/metrics").text for p in cports]
+
+        def delta(k):
+            return sum((_metric(ms[r], k) or 0.0) - (_metric(m0[r], k) or 0.0) for r in range(2))
+
+        assert delta("qmx_kernel_fin_host") == 0
+        assert delta("qmx_spread_delta_mismatch_total") == 0
+        if name in ("concat_think", "aggregate_4"):  # finals with text from the remote rank
+            assert delta("qmx_kernel_remote_texts_staged") + delta("qmx_kernel_remote_texts_hbm") > 0
+            assert delta("qmx_kernel_fin_items") > 0
+    finally:
+        live.close()

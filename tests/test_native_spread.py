@@ -39,7 +39,7 @@ THINK = [sse_chunk({"role": "assistant"}), sse_chunk({"content": "<think>"}), ss
 
 @contextlib.contextmanager
 def native_cluster(cfg, world: int, placement: str = "spread", xchg: str = "tcp", eager=None, tick_mode=None,
-                   links=None):
+                   links=None, engine: str = "cpu"):
     """`world` native ranks in-process (threads), TCP exchange on a free port block.
     ``xchg="tcpbulk"``: final texts move in rank-0-numbered bulk rounds (the RCCL round
     protocol with a socket executor) instead of riding the mesh.  ``eager``: the largest final
@@ -65,7 +65,7 @@ def native_cluster(cfg, world: int, placement: str = "spread", xchg: str = "tcp"
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
         try:
-            d = native_config(cfg, "127.0.0.1", ports[r], "cpu", 0, 1)
+            d = native_config(cfg, "127.0.0.1", ports[r], engine, 0, 1)
         finally:
             for k, v in old.items():
                 if v is None:
