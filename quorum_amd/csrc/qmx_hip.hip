@@ -77,6 +77,24 @@ __device__ __forceinline__ void dbg_put(unsigned long long* p, unsigned long lon
 // s_waitcnt vmcnt(0) (expcnt and lgkmcnt left alone): this wave's vector memory accesses,
 // stores included, have completed; a compiler barrier too, so no store is moved past it
 __device__ __forceinline__ void wave_stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// Publish a sequence number: the release fence (buffer_wbl2: this XCD's L2 written back to
+// memory), a HARD wait for that write-back, then the store.  The memory legalizer follows
+// buffer_wbl2 with a wait of its own, but the waitcnt pass may drop it when it believes no
+// vector memory access is outstanding (it does not count the write-back): with a flag load
+// waited just before, the persistent kernel's item publish was emitted as wbl2 + store with
+// no wait between, and the host read the previous tick's output bytes behind a new sequence
+// number (1-7 mislabelled deltas per 2.6M responses).  tests/test_isa.py checks the built
+// code object for any write-back not waited before the next store.
+__device__ __forceinline__ void publish_system(uint32_t* p, uint32_t v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void publish_agent(uint32_t* p, uint32_t v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 #define QMX_STAMP(k)                                               \
   do {                                                             \
     if (P.dbg != nullptr && threadIdx.x == 0)                      \
@@ -2295,16 +2313,7 @@ __device__ __forceinline__ void run_item(int k, const WorkItem* __restrict__ ite
     wave_stores_done();
     __syncthreads();
     if (Pk.dbg != nullptr && threadIdx.x == 0) dbg_put(&Pk.dbg[k * kDbg + 27], __builtin_amdgcn_s_memrealtime());
-    if (threadIdx.x == 0) {
-      if (Pk.fast & 64) {
-        // EXPERIMENT (QMX_KFAST bit 64): the host-memory stores are complete (vmcnt(0) per
-        // wave + barrier); publish the sequence number first, write the L2 back after
-        __hip_atomic_store(&res[k].seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      } else {
-        __hip_atomic_store(&res[k].seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
+    if (threadIdx.x == 0) publish_system(&res[k].seq, seq);
   } else {
     const int j = (int)(k - n_tick);
     fin_stage(fa, j, content, Pk.content_cap);
@@ -2315,7 +2324,7 @@ __device__ __forceinline__ void run_item(int k, const WorkItem* __restrict__ ite
     }
     wave_stores_done();
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(&fa.res[j].seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) publish_system(&fa.res[j].seq, seq);
   }
 }
 
@@ -2518,7 +2527,7 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* doors, PCtl* ct
                            __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&door->relayed, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (D.stop) __hip_atomic_store(&door->exits, (2u << 16) | (gen & 0xffffu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&ctl->seq, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        publish_agent(&ctl->seq, c);
       }
     }
     if (D.stop) return;  // D is block-uniform (LDS, written before the barrier)

@@ -249,7 +249,22 @@ class Supervisor:
         self.term(old)  # drain
         self.retiring += old
 
+    def snapshot_initial(self) -> None:
+        """The first generation runs a byte copy of the config too: a worker that imports
+        slowly must not read the live file while an editor (or a test) rewrites it for the
+        next reload — it would load a truncated file.  The copy is raw, so an unreadable or
+        invalid initial config keeps load_config's reference fallback."""
+        import shutil
+
+        try:
+            snap = os.path.join(self.tmp, "config.gen0" + (os.path.splitext(self.config)[1] or ".yaml"))
+            shutil.copyfile(self.config, snap)
+            self.active = snap
+        except OSError:
+            pass  # missing file: the workers' load_config falls back to the default config
+
     def run(self) -> int:
+        self.snapshot_initial()
         self.current = self.spawn()
 
         def on_hup(*_):

@@ -609,10 +609,22 @@ void finish_request(Conn& c, std::vector<double>& ttft, std::vector<double>& ttf
     std::string why = validate(c.status, c.body);
     if (!why.empty()) {
       const long n = g_invalid.fetch_add(1);
-      if (n < 5)
+      if (n < 5) {
         fprintf(stderr, "qmx_loadgen: invalid response (%s): %.600s\n", why.c_str(),
                 c.body.size() > 600 ? (c.body.substr(0, 300) + " ... " + c.body.substr(c.body.size() - 280)).c_str()
                                     : c.body.c_str());
+        // QMX_LOADGEN_DUMP=FILE: the whole body of each of the first invalid responses
+        if (const char* dp = getenv("QMX_LOADGEN_DUMP")) {
+          static std::mutex mu;
+          std::lock_guard<std::mutex> lk(mu);
+          if (FILE* f = fopen(dp, "a")) {
+            fprintf(f, "=== invalid response %ld (%s), status %d, %zu B\n", n, why.c_str(), c.status, c.body.size());
+            fwrite(c.body.data(), 1, c.body.size(), f);
+            fputs("\n=== end\n", f);
+            fclose(f);
+          }
+        }
+      }
     }
   }
   g_done++;

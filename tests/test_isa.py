@@ -1,0 +1,82 @@
+"""Machine-code checks of the built gfx950 code object (no GPU needed).
+
+The tick kernels publish each result with a sequence number written after an L2 write-back
+(``buffer_wbl2``, the release fence of ``publish_system`` / ``publish_agent`` in
+``csrc/qmx_hip.hip``).  The write-back is itself a vector memory operation: the store that
+publishes must wait for it (``s_waitcnt vmcnt(0)``), or the host can see the new sequence
+number before the output bytes reach memory.  The compiler's waitcnt pass once dropped that
+wait (a flag load had been waited just before, and the pass does not count the write-back):
+the headline bench then returned 1-7 deltas per 2.6M responses from the previous tick's
+output.  This test disassembles the in-tree extension and fails on any write-back that is
+not waited for before the next store or control transfer.
+"""
+import re
+import shutil
+import subprocess
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parent.parent
+LLVM = Path("/opt/rocm/lib/llvm/bin")
+TOOLS = [LLVM / "llvm-objcopy", LLVM / "clang-offload-bundler", LLVM / "llvm-objdump"]
+
+
+def _extension():
+    sos = sorted((REPO / "quorum_amd").glob("_qmx*.so"))
+    return sos[0] if sos else None
+
+
+@pytest.fixture(scope="module")
+def disasm(tmp_path_factory):
+    so = _extension()
+    if so is None or not all(t.exists() for t in TOOLS):
+        pytest.skip("extension not built or LLVM tools missing")
+    d = tmp_path_factory.mktemp("isa")
+    fat, co = d / "fat.bin", d / "dev.co"
+    subprocess.run([str(TOOLS[0]), f"--dump-section=.hip_fatbin={fat}", str(so), str(d / "host.so")],
+                   check=True, capture_output=True)
+    targets = subprocess.run([str(TOOLS[1]), "--list", "--type=o", f"--input={fat}"], check=True,
+                             capture_output=True, text=True).stdout.split()
+    gfx = [t for t in targets if t.endswith("gfx950")]
+    assert gfx, f"no gfx950 code object in {so.name}: {targets}"
+    subprocess.run([str(TOOLS[1]), "--unbundle", "--type=o", f"--input={fat}", f"--targets={gfx[0]}",
+                    f"--output={co}"], check=True, capture_output=True)
+    out = subprocess.run([str(TOOLS[2]), "-d", "--no-show-raw-insn", str(co)], check=True,
+                         capture_output=True, text=True).stdout
+    return out.splitlines()
+
+
+_STORE = re.compile(r"^\s*(global_store|flat_store|buffer_store|global_atomic|flat_atomic|buffer_atomic)")
+_LEAVE = re.compile(r"^\s*(s_branch|s_cbranch|s_setpc|s_endpgm|s_swappc)")
+_WAIT = re.compile(r"^\s*s_waitcnt\b.*\bvmcnt\(0\)")
+
+
+def unwaited_writebacks(lines):
+    """(line, what) for every buffer_wbl2 reaching a store or a control transfer before an
+    s_waitcnt vmcnt(0)."""
+    bad = []
+    for i, l in enumerate(lines):
+        if "buffer_wbl2" not in l:
+            continue
+        for j in range(i + 1, min(i + 64, len(lines))):
+            m = lines[j]
+            if _WAIT.match(m):
+                break
+            if _STORE.match(m) or _LEAVE.match(m):
+                bad.append((i + 1, m.strip().split("//")[0].strip()))
+                break
+    return bad
+
+
+def test_unwaited_writeback_detector():
+    ok = ["\tbuffer_wbl2 sc0 sc1", "\ts_waitcnt vmcnt(0)", "\tglobal_store_dword v1, v2, s[0:1] sc0 sc1"]
+    bad = ["\tbuffer_wbl2 sc0 sc1", "\tglobal_store_dword v43, v217, s[0:1] offset:16 sc0 sc1"]
+    assert unwaited_writebacks(ok) == []
+    assert unwaited_writebacks(bad) == [(1, "global_store_dword v43, v217, s[0:1] offset:16 sc0 sc1")]
+
+
+def test_every_l2_writeback_is_waited_before_publishing(disasm):
+    n = sum("buffer_wbl2" in l for l in disasm)
+    assert n >= 4, "expected the tick / finalize / relay publishes in the code object"
+    assert unwaited_writebacks(disasm) == []

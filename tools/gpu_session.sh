@@ -97,6 +97,15 @@ for step in "$@"; do
     bench|bench=*)
       n=${step#bench}; n=${n#=}; n=${n:-1}
       for i in $(seq 1 $n); do bench bench_$i 300 QMX_NOP=1 -- || exit 1; done ;;
+    hunt=*)  # N headline runs that go on past an INVALID run (exit 1 with a JSON line saying
+             # valid false); the whole body of each invalid response -> invalid_bodies.txt.
+             # Any other failure (timeout, crash, no JSON line) ends the session as usual.
+      n=${step#hunt=}
+      for i in $(seq 1 $n); do
+        bench hunt_$i 300 QMX_NOP=1 QMX_LOADGEN_DUMP=$OUT/invalid_bodies.txt -- && continue
+        grep -q '"valid": false' $OUT/hunt_$i.json 2>/dev/null || exit 1
+        echo "hunt_$i invalid: kept going"
+      done ;;
     bench:*)
       a=${step#bench:}; slug=$(echo "$a" | tr -c 'a-zA-Z0-9' '_')
       bench bench_$slug 300 QMX_NOP=1 -- ${a//,/ } || exit 1 ;;
