@@ -56,6 +56,10 @@ struct HoleTpl {
   uint16_t hs[kHoleMax], he[kHoleMax];        // hole i = bytes[hs[i], he[i])
   uint8_t num[kHoleMax];                      // 1: hole i is a number, 0: a string body
   uint8_t pad0[10];
+  // the tick kernel's S3a test per 8-byte word of the first 256 bytes, bit per byte:
+  // string-hole bytes (bits 0-7), number-hole bytes (8-15), first bytes of multi-digit
+  // number holes (16-23) — built with the template (wave_hole_publish), copied with it
+  uint32_t wmask[32];
   uint32_t claim;  // launch sequence number of the last writer (its own 16 B: a copy skips it)
   uint32_t pad1[3];
 };
@@ -234,7 +238,7 @@ struct TickLane {
   double item_us = 0, start_spread_us = 0;
   double items_host_us = 0;
   double relay_us = 0, pickup_us = 0, grid_span_us = 0, grid_ticks = 0;  // persistent: doorbell seen -> ...  // host: result records -> slot state + SSE strings (process_item)  // per tick: mean item run, last item start - first
-  double stage_us[21] = {0};  // [20]: an item's system-scope release fence (stage timing)
+  double stage_us[24] = {0};  // [20]: an item's system-scope release fence (stage timing)
   double clk_cycles = 0, clk_us = 0;
   // finalize arenas (fused into this lane's tick launches)
   FinItem* h_fin = nullptr;

@@ -55,13 +55,13 @@ constexpr int TILE_MAX = 16384;
 constexpr int MAX_EV = 512;  // events per tile (more → WS_MORE requeue); keeps LDS < 80 KiB (2 WG/CU)
 constexpr int MAX_CAND = 1024;
 constexpr int PAD = 16;
-constexpr int kSpecTile = 4096;  // tile bytes loaded before the work item is known (256 threads x 16 B)
+constexpr int kSpecTile = BS * 16;  // tile bytes loaded before the work item is known (16 B per thread: a whole headline stream, ~4.9 KB, in the same PCIe round trip as the item)
 constexpr int TOK_CAP = 512;
 // QMX_STAGE_TIMING record per work item: stamps 0-12, S3 counters 13-20, sub-stage stamps
 // 21 (S3a done), 22 (S3 loop done), 23 (s4_wave: matched), 24 (s4_wave: cuts), 25 (s4_wave:
 // token list + depth scan done), 26 (S6 write: output window filled, host stores next),
 // 27 (the item's system-scope release fence done: its cost is 27 minus the result's t1)
-constexpr int kDbg = 28;
+constexpr int kDbg = 32;
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 
@@ -76,6 +76,11 @@ __device__ __forceinline__ void dbg_put(unsigned long long* p, unsigned long lon
 }
 // s_waitcnt vmcnt(0) (expcnt and lgkmcnt left alone): this wave's vector memory accesses,
 // stores included, have completed; a compiler barrier too, so no store is moved past it
+// bit i of m (i < 8) -> byte i of the result 0xff
+__device__ __forceinline__ uint64_t byte_mask8(uint32_t m) {
+  const uint64_t x = ((uint64_t)m * 0x0101010101010101ull) & 0x8040201008040201ull;  // byte i: bit i or 0
+  return (((x + 0x7f7f7f7f7f7f7f7full) & 0x8080808080808080ull) >> 7) * 0xffull;
+}
 __device__ __forceinline__ void wave_stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // Publish a sequence number: the release fence (buffer_wbl2: this XCD's L2 written back to
 // memory), a HARD wait for that write-back, then the store.  The memory legalizer follows
@@ -129,7 +134,9 @@ enum : int {
   V_START = 0, V_NSEP, V_LASTSEP, V_ABORT, V_NEV, V_CONSUMED, V_STATUS, V_NDELTA, V_YLEN, V_NCAND,
   V_NTOK, V_BAIL, V_DEPTH0, V_TAILLEN, V_NEWTAIL, V_NEWDEPTH, V_WLEN, V_NEMIT, V_ETOT, V_OUTLEN,
   V_TPLPRE, V_TPLSUF, V_TPLK, V_NEXTEV, V_NFULL, V_NTPL, V_CFULL, V_CTPL, V_CLEX, V_NHOLE, V_CHOLE, V_S4W,
-  V_HCLAIM  // hole-template slots this workgroup wrote (bit per slot): one writer per slot
+  V_HCLAIM,  // hole-template slots this workgroup wrote (bit per slot): one writer per slot
+  V_UNRES,   // events S3a left for the loop
+  V_HMATCH   // hole templates S3a matched (bit per slot)
 };
 
 // LDS byte reader that fetches one aligned 64-bit word per 8 sequential bytes: a byte-serial
@@ -546,6 +553,28 @@ __device__ inline void wave_hole_publish(const uint8_t* x, int e0, int e1, const
     D.he[k] = (uint16_t)((hstr ? nxt : nend) - e0);
     D.num[k] = hnum ? 1 : 0;
   }
+  // S3a's byte classes of word `lane` (< 32): the holes' bounds from their owner lanes
+  {
+    const int ha = (hstr ? pos + 1 : pos) - e0, hb = (hstr ? nxt : nend) - e0;
+    const int o = lane * 8;
+    uint32_t sm = 0, nm = 0, zm = 0;
+    for (uint64_t m = H; m; m &= m - 1) {
+      const int L = __ffsll((unsigned long long)m) - 1;
+      const int a = __builtin_amdgcn_readlane(ha, L), e = __builtin_amdgcn_readlane(hb, L);
+      const bool isnum = (__builtin_amdgcn_readlane((int)hnum, L)) != 0;
+      const int lo = max(a, o) - o, up = min(e, o + 8) - o;
+      if (lo < up) {
+        const uint32_t m8 = ((1u << up) - 1u) & ~((1u << lo) - 1u);
+        if (isnum) {
+          nm |= m8;
+          if (a >= o && e - a > 1) zm |= 1u << (a - o);
+        } else {
+          sm |= m8;
+        }
+      }
+    }
+    if (lane < 32) D.wmask[lane] = sm | (nm << 8) | (zm << 16);
+  }
   if (lane == 0) {
     D.nh = (uint8_t)nh;
     D.kind = (uint8_t)kind;
@@ -589,6 +618,7 @@ __device__ inline void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "
 __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth0, const KParams& P,
                         unsigned long long* dbg) {
   const int lane = threadIdx.x & 63;
+  if (dbg != nullptr && lane == 0) dbg_put(&dbg[28], __builtin_amdgcn_s_memrealtime());
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
   // candidates: every '<' of Z, in position order — 8 bytes per lane (SWAR compare on one
   // ds_read_b64; Z is 8-byte aligned with readable bytes past Zn), 512 bytes per step
@@ -614,6 +644,7 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
   }
   if (lane < nc) s.cand_tok[lane] = 0;
   wave_fence();
+  if (dbg != nullptr && lane == 0) dbg_put(&dbg[29], __builtin_amdgcn_s_memrealtime());
   {
     const v4i bf0 = build_pattern_frag(P, 0), bf1 = build_pattern_frag(P, P.npat > 16 ? 1 : 0);
     for (int g = 0; g * 16 < nc; ++g) mfma_match_group(Z, Zn, s.cand, nc, g, P, bf0, bf1, s.cand_tok);
@@ -908,6 +939,8 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     s.v[V_NEXTEV] = 0;
     s.v[V_NFULL] = s.v[V_NTPL] = s.v[V_CFULL] = s.v[V_CTPL] = s.v[V_CLEX] = s.v[V_NHOLE] = s.v[V_CHOLE] = 0;
     s.v[V_HCLAIM] = 0;
+    s.v[V_UNRES] = 0;
+    s.v[V_HMATCH] = 0;
     for (int q = 0; q < BS / 64; ++q) wtpl[q][0] = -1;
     if (fresh) {
       s.v[V_DEPTH0] = 0;
@@ -1116,25 +1149,40 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   // need a real string scan ('"', '\\', control bytes, non-ASCII).  An event that passes has
   // the template's parse with an escape-free body — exactly wave_tpl_match + wave_str_body's
   // answer for it — at ~4 dependent LDS round trips instead of an atomic claim, two ballot
-  // passes and LDS atomics per event.  Everything else (0xFF) goes through the loop below.
+  // passes and LDS atomics per event.
+  // S3a (b): in the same layout, the other shapes of a burst — "data: [DONE]" and the
+  // backend's hole templates (role / finish events; wave_hole_exact + wave_hole_samelen's
+  // test: literal bytes equal, string-hole bytes printable ASCII other than '"' and '\\',
+  // number-hole bytes digits without a leading zero).  Everything else (0xFE / 0xFF) goes
+  // through the loop below, which is skipped when nothing is left (V_UNRES).
   {
     // half a wave per event (32 lanes x 8 bytes: events up to 256 bytes), two per wave
     const int hw = tid >> 5, lane = tid & 31;
+    const bool upper = (tid >> 5) & 1;
     const int tp = s.v[V_TPLPRE], ts = s.v[V_TPLSUF];
-    int newest = -1, nm = 0;
+    const bool fast = (P.fast & 2) != 0;
+    const uint64_t hi = 0x8080808080808080ull, one = 0x0101010101010101ull;
+    auto half_clear = [upper](uint64_t m) { return (upper ? (m >> 32) : (m & 0xffffffffull)) == 0; };
+    int newest = -1, nm = 0, nhole = 0, unres = 0;
+    uint32_t hmatch = 0;
     for (int kb = 0; kb < nev; kb += BS / 32) {
       const int k = kb + hw;
       const bool have = k < nev;
       const int e0 = have ? s.ev_a[k] : 0, e1 = have ? s.ev_b[k] : 0, L = e1 - e0;
-      bool ok = have && (P.fast & 2) && tp > 0 && L >= tp + ts && L <= 256;
+      const int o = lane * 8;
+      const bool word = have && fast && L <= 256 && o < L;
+      const int nb = min(8, L - o);
+      const uint64_t valid = !word ? 0ull : nb == 8 ? ~0ull : ((1ull << (8 * nb)) - 1);
+      const uint64_t ev = word ? lds_window8(s.A, e0 + o, e1) : 0ull;
+      const uint64_t q = ev ^ 0x2222222222222222ull, b = ev ^ 0x5c5c5c5c5c5c5c5cull;
+      // any '"', '\\', byte < 0x20 or >= 0x80 (the zero / less-than tricks only ever err
+      // towards "bad", which just sends the event down the exact path)
+      const uint64_t odd = (((q - one) & ~q) | ((b - one) & ~b) | ((ev - 0x20 * one) & ~ev) | ev) & hi;
+      bool ok = have && fast && tp > 0 && L >= tp + ts && L <= 256;
       bool shape_bad = false;  // the prefix / suffix words differ (not just an odd body byte)
       {
         bool bad = false, sbad = false;
-        const int o = lane * 8;
         if (ok && o < L) {
-          const int nb = min(8, L - o);
-          const uint64_t valid = nb == 8 ? ~0ull : ((1ull << (8 * nb)) - 1);
-          const uint64_t ev = lds_window8(s.A, e0 + o, e1);
           const int pe = min(max(tp - o, 0), 8);  // prefix bytes of this word
           const uint64_t pmask = pe == 8 ? ~0ull : ((1ull << (8 * pe)) - 1);
           const int ss = (L - ts) - o;  // the suffix starts at byte ss of this word
@@ -1147,51 +1195,105 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
           }
           const uint64_t tw = pe > 0 ? ((const uint64_t*)s.tpl)[lane] : 0ull;  // (lane < 32: o < 256)
           const uint64_t bmask = valid & ~pmask & ~smask;
-          const uint64_t hi = 0x8080808080808080ull, one = 0x0101010101010101ull;
-          const uint64_t q = ev ^ 0x2222222222222222ull, b = ev ^ 0x5c5c5c5c5c5c5c5cull;
-          // any '"', '\\', byte < 0x20 or >= 0x80 (the zero / less-than tricks only ever err
-          // towards "bad", which just sends the event down the exact path)
-          const uint64_t odd = (((q - one) & ~q) | ((b - one) & ~b) | ((ev - 0x20 * one) & ~ev) | ev) & hi;
           sbad = ((ev ^ tw) & pmask) != 0 || ((ev ^ sw) & smask) != 0;
           bad = sbad || (odd & bmask) != 0;
         }
         const uint64_t bm = __ballot(bad), sm = __ballot(sbad);
-        const bool upper = (tid >> 5) & 1;
-        ok = ok && (upper ? (bm >> 32) : (bm & 0xffffffffull)) == 0;  // this half's lanes
-        shape_bad = (upper ? (sm >> 32) : (sm & 0xffffffffull)) != 0 || L < tp + ts;
+        ok = ok && half_clear(bm);  // this half's lanes
+        shape_bad = !half_clear(sm) || L < tp + ts;
+      }
+      // (b) the event's other possible shapes (block-uniform fast flag; ballots wave-wide)
+      const bool try_b = have && !ok && fast && L <= 256;
+      bool done_ev = false;
+      int hq = -1;
+      if (fast) {
+        const bool dbad = !(try_b && L == 12) || (lane == 0 && ev != 0x445b203a61746164ull) ||  // "data: [D"
+                          (lane == 1 && ev != 0x5d454e4full);                                    // "ONE]"
+        done_ev = try_b && half_clear(__ballot(dbad));
+        // DEL (0x7f) and number-hole digits, SWAR like `odd`
+        const uint64_t dl = ev ^ 0x7f7f7f7f7f7f7f7full, x7 = ev & 0x7f7f7f7f7f7f7f7full;
+        const uint64_t strbad = odd | (((dl - one) & ~dl) & hi);
+        const uint64_t digit = ((x7 + 0x5050505050505050ull) & ~(x7 + 0x4646464646464646ull) & ~ev) & hi;
+        // a byte '0' (first bytes of multi-digit number holes may not be one)
+        const uint64_t z0 = ev ^ 0x3030303030303030ull, zero = ((z0 - one) & ~z0) & hi;
+        for (int qi = 0; qi < kHoleTpls; ++qi) {
+          const HoleTpl& T = U.htpl[qi];
+          const int n = T.len;
+          const bool cand = try_b && !done_ev && hq < 0 && n == L && n > 0 && (T.kind == EV_CONTENT || T.kind == EV_SKIP);
+          bool bad = !cand;
+          if (cand && o < L) {
+            const uint32_t hm = T.wmask[lane];
+            const uint64_t smask = byte_mask8(hm & 0xffu), nmask = byte_mask8((hm >> 8) & 0xffu),
+                           zmask = byte_mask8((hm >> 16) & 0xffu);
+            const uint64_t tw = ((const uint64_t*)T.bytes)[lane];
+            const uint64_t lit = valid & ~(smask | nmask);
+            bad = ((ev ^ tw) & lit) != 0 || (strbad & smask) != 0 || ((~digit & hi) & nmask) != 0 ||
+                  (zero & zmask) != 0;
+          }
+          if (half_clear(__ballot(bad)) && cand) hq = qi;
+        }
       }
       // unresolved: 0xFE when the stream template cannot match (its prefix / suffix differ:
       // the loop skips its own template compare), 0xFF otherwise (an escaped or non-ASCII
       // body the loop's exact string check may still accept, or no check ran)
-      const bool examined = (P.fast & 2) && tp > 0 && L <= 256 && shape_bad;
-      if (lane == 0 && have) {
-        s.ev_kind[k] = ok ? (uint8_t)EV_CONTENT : examined ? (uint8_t)0xFE : (uint8_t)0xFF;
-        if (ok) {
-          s.ev_sa[k] = (uint16_t)(e0 + tp);
-          s.ev_sb[k] = (uint16_t)(e1 - ts);
-          s.ev_dl[k] = (uint16_t)(L - tp - ts);
+      const bool examined = fast && tp > 0 && L <= 256 && shape_bad;
+      int kind = -1, sa = 0, sb = 0;
+      if (ok) {
+        kind = EV_CONTENT;
+        sa = e0 + tp;
+        sb = e1 - ts;
+      } else if (done_ev) {
+        kind = EV_SKIP;
+      } else if (hq >= 0) {
+        const HoleTpl& T = U.htpl[hq];
+        kind = T.kind;
+        if (kind == EV_CONTENT) {
+          sa = e0 + T.hs[T.target];
+          sb = e0 + T.he[T.target];
         }
       }
-      if (ok) {
-        newest = k;
-        ++nm;
+      if (lane == 0 && have) {
+        s.ev_kind[k] = kind >= 0 ? (uint8_t)kind : examined ? (uint8_t)0xFE : (uint8_t)0xFF;
+        if (kind == EV_CONTENT) {
+          s.ev_sa[k] = (uint16_t)sa;
+          s.ev_sb[k] = (uint16_t)sb;
+          s.ev_dl[k] = (uint16_t)(sb - sa);  // escape-free body (checked above)
+        }
       }
+      if (have && kind < 0) ++unres;
+      if (hq >= 0 && !ok && !done_ev) {
+        ++nhole;
+        hmatch |= 1u << hq;
+      }
+      if (ok) ++nm;
+      // the tile's newest content event (template or hole match) becomes the template
+      if (kind == EV_CONTENT && sa - e0 <= TPL_PRE_MAX && e1 - sb <= TPL_SUF_MAX) newest = k;
     }
-    if (lane == 0 && nm > 0) {  // (both half-waves)
-      atomicAdd(&s.v[V_NTPL], nm);
-      atomicMax(&s.v[V_TPLK], newest);  // the tile's newest content event becomes the template
+    if (lane == 0) {  // (both half-waves)
+      if (nm > 0) atomicAdd(&s.v[V_NTPL], nm);
+      if (newest >= 0) atomicMax(&s.v[V_TPLK], newest);
+      if (nhole > 0) {
+        atomicAdd(&s.v[V_NHOLE], nhole);
+        atomicOr(&s.v[V_HMATCH], (int)hmatch);
+      }
+      if (unres > 0) atomicAdd(&s.v[V_UNRES], unres);
     }
   }
   __syncthreads();
   QMX_STAMP(21);
   {
     const int w = tid >> 6, lane = tid & 63;
+    // a hole template S3a matched is carried into the launch's write table (as the loop's
+    // matches are, wave_hole_carry): wave w carries template w
+    if (pub && w < kHoleTpls && ((s.v[V_HMATCH] >> w) & 1))
+      wave_hole_carry(U.htpl[w], &btpl_wr[it.index].hole[w], w, &s.v[V_HCLAIM]);
+    const bool loop = s.v[V_UNRES] > 0;  // (block-uniform: read after the barrier)
     const LdsWords rd(s.A);
     const int tp = s.v[V_TPLPRE], ts = s.v[V_TPLSUF];
     bool published = false;
     int hint = w;  // template that matched last (tried first)
     int hhint = 0;  // hole template that matched last
-    while (true) {
+    while (loop) {
       int g = 0;
       if (lane == 0) g = atomicAdd(&s.v[V_NEXTEV], 1);
       g = __builtin_amdgcn_readfirstlane(g);
@@ -1438,12 +1540,23 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       }
     }
     __syncthreads();
-    {  // escape-free contents: one wave per event, 64 bytes per step
+    {  // escape-free contents: one wave per event, 64 bytes per step; each lane fetches one
+       // of its wave's events' (offset, start, length) up front (nev <= MAX_EV = 8 x 64), so
+       // an event costs no dependent LDS read but its bytes'
       const int w = tid >> 6, lane = tid & 63;
-      for (int k = w; k < nev; k += BS / 64) {
-        const int off = s.ev_a[k];
+      const int kl = w + (BS / 64) * lane;
+      int off_l = 0xFFFF, sa_l = 0, n_l = 0;
+      if (kl < nev) {
+        off_l = s.ev_a[kl];
+        if (off_l != 0xFFFF) {
+          sa_l = s.ev_sa[kl];
+          n_l = s.ev_sb[kl] - sa_l;
+        }
+      }
+      for (int i = 0; w + (BS / 64) * i < nev; ++i) {
+        const int off = __builtin_amdgcn_readlane(off_l, i);
         if (off == 0xFFFF) continue;
-        const int sa = s.ev_sa[k], n = s.ev_sb[k] - sa;
+        const int sa = __builtin_amdgcn_readlane(sa_l, i), n = __builtin_amdgcn_readlane(n_l, i);
         for (int x = lane; x < n; x += 64) Z[tail_len + off + x] = s.A[sa + x];
       }
     }
@@ -1859,19 +1972,42 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       if (clean) {
         const int ix = (int)it.index;
         const int p1 = P.pre1_len, wave = tid >> 6, lane = tid & 63;
-        for (int k = wave; k < n_emit; k += BS / 64) {
-          const int j = s.ejx[k];
-          const int cs = j ? (int)s.wpos[j - 1] : 0, cl = (int)s.wpos[j] - cs;
-          uint8_t* ev = O + k * EVL + cs;  // the event's start: k envelopes + earlier content
-          // three wave-uniform copies (prefix, content, suffix): measured faster than one
-          // fused per-byte source select with every load issued up front (divergent selects)
-          for (int b = lane; b < PRE; b += 64) {
-            const int d = b - p1, r = ndig - 1 - d;  // index digit, most significant first
-            const int dv = r == 2 ? ix / 100 : r == 1 ? (ix / 10) % 10 : ix % 10;
-            ev[b] = b < p1 ? (uint8_t)P.pre1[b] : d < ndig ? (uint8_t)('0' + dv) : (uint8_t)P.pre2[d - ndig];
+        // the envelope bytes are the same for every event of the item (one backend index):
+        // each lane holds its prefix bytes lane + 64r (PRE <= 227: r < 4) and suffix byte
+        // (SUF <= 48) in registers, read once — the per-event copies then store without
+        // reading P; and each lane fetches one event's (start, length) for its wave up front
+        // (n_emit <= MAX_EV = 8 waves x 64 lanes), so an event costs no dependent LDS read
+        // but its content bytes'
+        static_assert(sizeof(P.pre1) + 3 + sizeof(P.pre2) <= 256 && sizeof(P.suf) <= 64 && MAX_EV <= BS,
+                      "envelope bytes per lane / events per wave lane");
+        uint32_t pw = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int b = lane + 64 * r;
+          if (b < PRE) {
+            const int d = b - p1, q = ndig - 1 - d;  // index digit, most significant first
+            const int dv = q == 2 ? ix / 100 : q == 1 ? (ix / 10) % 10 : ix % 10;
+            const uint32_t ch = b < p1 ? (uint8_t)P.pre1[b] : d < ndig ? (uint8_t)('0' + dv) : (uint8_t)P.pre2[d - ndig];
+            pw |= ch << (8 * r);
           }
+        }
+        const uint8_t sch = lane < SUF ? (uint8_t)P.suf[lane] : 0;
+        const int kl = wave + (BS / 64) * lane;
+        int cs_l = 0, cl_l = 0;
+        if (kl < n_emit) {
+          const int j = s.ejx[kl];
+          cs_l = j ? (int)s.wpos[j - 1] : 0;
+          cl_l = (int)s.wpos[j] - cs_l;
+        }
+        for (int i = 0; wave + (BS / 64) * i < n_emit; ++i) {
+          const int k = wave + (BS / 64) * i;
+          const int cs = __builtin_amdgcn_readlane(cs_l, i), cl = __builtin_amdgcn_readlane(cl_l, i);
+          uint8_t* ev = O + k * EVL + cs;  // the event's start: k envelopes + earlier content
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (lane + 64 * r < PRE) ev[lane + 64 * r] = (uint8_t)(pw >> (8 * r));
           for (int b = lane; b < cl; b += 64) ev[PRE + b] = W[cs + b];
-          for (int b = lane; b < SUF; b += 64) ev[PRE + cl + b] = (uint8_t)P.suf[b];
+          if (lane < SUF) ev[PRE + cl + lane] = sch;
         }
       } else {
       // envelopes: fully parallel over (emitted event, envelope byte)
@@ -3491,6 +3627,9 @@ void HipEngine::complete(HipJob& J, std::vector<SlotResult>& results, std::vecto
         sub(17, 25, 24);
         sub(18, 9, 26);   // S6 write: output window fill / host-memory stores
         sub(19, 26, 10);
+        sub(21, 5, 28);   // s4_wave: call entry / candidate scan / MFMA match
+        sub(22, 28, 29);
+        sub(23, 29, 23);
         if (d[27] && d[27] >= B.h_res[i].t1 && B.h_res[i].t1) L.stage_us[20] += (double)(d[27] - B.h_res[i].t1) * 0.01;
       }
       L.stage_n += n;
@@ -3719,7 +3858,7 @@ void HipEngine::collect_finalize(TickLane& L, const std::vector<const FinalizeRe
 
 std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   std::unordered_map<std::string, double> m;
-  double stage[21] = {0}, cyc = 0, cus = 0;
+  double stage[24] = {0}, cyc = 0, cus = 0;
   for (auto& Lp : lanes_) {
     TickLane& L = *Lp;
     std::lock_guard<std::mutex> lg(L.mu);
@@ -3758,7 +3897,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["fin_launches"] += (double)L.fin_launches;  // tick launches that also carried finalize work
     m["fin_items"] += (double)L.fin_items;
     m["fin_staged_texts"] += (double)L.fin_staged;  // mesh-delivered remote finals staged into items
-    for (int k = 1; k < 21; ++k) stage[k] += L.stage_us[k];
+    for (int k = 1; k < 24; ++k) stage[k] += L.stage_us[k];
     cyc += L.clk_cycles;
     cus += L.clk_us;
   }
@@ -3772,6 +3911,9 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   m["stage_s4hold_us"] = stage[17];
   m["stage_s6fill_us"] = stage[18];
   m["stage_s6store_us"] = stage[19];
+  m["stage_s4entry_us"] = stage[21];
+  m["stage_s4scan_us"] = stage[22];
+  m["stage_s4mfma_us"] = stage[23];
   m["stage_fence_us"] = stage[20];  // the item's system-scope release fence (L2 write-back)
   m["shader_mhz"] = cus > 0 ? cyc / cus : 0.0;
   m["clk_cycles"] = cyc;  // summable across engines (/metrics sums the io loops' engines)

@@ -480,3 +480,48 @@ def test_hip_hole_samelen(ext, monkeypatch):
                 eng.release(sl)
     assert got["hip"] == got["cpu"]
     assert hip._e.kernel_stats().get("s3_hole_hits", 0) > 50
+
+
+# 12-byte events next to S3a's "data: [DONE]" word compare, and longer / shorter spellings
+DONE_LIKE = [b"data: [DONE]", b"data: [DONX]", b"data: {DONE}", b"data:  [DONE", b"Data: [DONE]", b"data: [done]",
+             b"data:[DONE] ", b"data: [DONE] ", b"data:[DONE]", b'data: "DONE"', b"data: [DON\xc3\x89]", b"data: 123456"]
+
+
+def test_hip_done_and_twelve_byte_events(ext, monkeypatch):
+    """S3a resolves an exact ``data: [DONE]`` event itself; every other event of that length
+    (and the spellings the full parse strips to [DONE]) must come out as the CPU engine has
+    them, mixed with hole-template role / finish events."""
+    monkeypatch.setenv("QMX_STAGE_TIMING", "1")
+    rng = random.Random(31)
+    hip, cpu = _hip(["think"]), NativeEngine("cpu", ["think"])
+    got = {"hip": {}, "cpu": {}}
+    for rnd in range(4):
+        bodies = []
+        for k in range(20):
+            id_ = b"chatcmpl-" + bytes(rng.choice(b"abcdef0123456789") for _ in range(14))
+            evs = [_oai_event(id_, b"1700000000", b"mock", b'{"role": "assistant", "content": ""}')]
+            for _ in range(rng.randint(1, 5)):
+                evs.append(_oai_event(id_, b"1700000000", b"mock", b'{"content": "tok"}'))
+                if rnd >= 1 and rng.random() < 0.3:
+                    evs.append(rng.choice(DONE_LIKE) + b"\n\n")
+            evs.append(_oai_event(id_, b"1700000000", b"mock", b"{}", finish=b'"stop"'))
+            evs.append((rng.choice(DONE_LIKE) if rnd >= 1 and rng.random() < 0.5 else b"data: [DONE]") + b"\n\n")
+            bodies.append(b"".join(evs))
+        for name, eng in (("hip", hip), ("cpu", cpu)):
+            slots = [eng.open(k % 2, True, True) for k in range(len(bodies))]
+            for sl, body in zip(slots, bodies):
+                eng.feed(sl, body)
+                eng.finish(sl)
+            acc = {sl: [b"", 0] for sl in slots}
+            for _ in range(50):
+                res, _ = eng.tick(H.CREATED)
+                for sl, data, fl in res:
+                    acc[sl][0] += data
+                    acc[sl][1] |= fl
+                if not eng.has_work():
+                    break
+            for k, sl in enumerate(slots):
+                got[name][(rnd, k)] = tuple(acc[sl])
+                eng.release(sl)
+    assert got["hip"] == got["cpu"]
+    assert hip._e.kernel_stats()["escalations"] == 0
