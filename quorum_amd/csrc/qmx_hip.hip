@@ -295,28 +295,39 @@ __device__ inline void mfma_match_group(const uint8_t* Z, int Zn, const uint16_t
   }
   // the window's bytes themselves (ASCII-lowercased, the tags' IGNORECASE) as base-8 digits
   // d0, d1 (0..7) and d2 (0..3), and d0² + d1² + d2² (<= 107: int8) — feature group kg of the
-  // A operand; no per-byte table lookup
-  int8_t bytes[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const uint32_t zb = (uint32_t)((j < 8 ? w0 : w1) >> ((j & 7) * 8)) & 0xffu;
-    const int d0 = zb & 7, d1 = (zb >> 3) & 7, d2 = zb >> 6;
-    bytes[j] = (int8_t)(kg == 0 ? d0 : kg == 1 ? d1 : kg == 2 ? d2 : d0 * d0 + d1 * d1 + d2 * d2);
-  }
+  // A operand.  Four bytes per 32-bit word at once: digits by shift-and-mask, squares by a
+  // v_perm_b32 byte lookup (the 8-entry table {0,1,4,...,49} as two words), the group's
+  // feature by a per-lane select — a per-byte loop with a per-lane branch on kg compiled to
+  // ~1,000 masked instructions per group (2 us of the filter stage, r4/i)
   v4i a;
-  __builtin_memcpy(&a, bytes, 16);
-  const int nblk = P.npat > 16 ? 2 : 1;
+  {
+    const uint32_t sq_lo = 0x09040100u, sq_hi = 0x31241910u;  // d² for d = 0..7
+    const uint32_t h[4] = {(uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t d0 = h[q] & 0x07070707u, d1 = (h[q] >> 3) & 0x07070707u, d2 = (h[q] >> 6) & 0x03030303u;
+      const uint32_t sq = __builtin_amdgcn_perm(sq_hi, sq_lo, d0) + __builtin_amdgcn_perm(sq_hi, sq_lo, d1) +
+                          __builtin_amdgcn_perm(sq_hi, sq_lo, d2);  // bytewise: <= 107, no carries
+      a[q] = (int)(kg == 0 ? d0 : kg == 1 ? d1 : kg == 2 ? d2 : sq);
+    }
+  }
+  const int npat = P.npat, nts = P.ts.n;
+  const int nblk = npat > 16 ? 2 : 1;
   for (int blk = 0; blk < nblk; ++blk) {
+    // this lane's pattern column: its match value, length and token id read before the MFMA
+    // (after it, every read of P would wait behind the previous row's cand_tok store)
+    const int t = 16 * blk + (l & 15);
+    const bool tv = t < npat;
+    const int negE = tv ? -P.pat_E[t] : 0, plen = tv ? pattern_len(P.ts, t) : 0;
+    const int8_t tok = (int8_t)(t < nts ? t + 1 : -(t - nts + 1));
     v4i acc = {0, 0, 0, 0};
     acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, blk ? bf1 : bf0, acc, 0, 0, 0);
-    const int t = 16 * blk + (l & 15);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       int row = 4 * (l >> 4) + i;
       int cc = g * 16 + row;
-      if (t < P.npat && cc < ncand && acc[i] == -P.pat_E[t] &&
-          (pattern_len(P.ts, t) <= kWindow || pattern_tail_ok(Z, Zn, (int)cand[cc], t, P)))
-        cand_tok[cc] = (int8_t)(t < P.ts.n ? t + 1 : -(t - P.ts.n + 1));
+      if (tv && cc < ncand && acc[i] == negE && (plen <= kWindow || pattern_tail_ok(Z, Zn, (int)cand[cc], t, P)))
+        cand_tok[cc] = tok;
     }
   }
 }
@@ -651,7 +662,10 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
   }
   wave_fence();
   if (dbg != nullptr && lane == 0) dbg_put(&dbg[23], __builtin_amdgcn_s_memrealtime());
-  // tokens and the depth before each (candidates in order, non-tokens the scan identity)
+  // tokens and the depth before each (candidates in order, non-tokens the scan identity);
+  // candidate lane c also keeps, in registers, its position, token id / length and the depth
+  // before it — the holdback cuts below read them with v_readlane, not LDS searches
+  int cpos = 0, ctok = 0, cplen = 0, cdep = 0, fdep;
   {
     const int id = lane < nc ? (int)s.cand_tok[lane] : 0;
     const uint64_t m = __ballot(id != 0);
@@ -663,18 +677,46 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
     ex.x = __shfl_up(x.x, 1, 64);
     ex.y = __shfl_up(x.y, 1, 64);
     if (lane == 0) ex = make_int2(0, 0);
+    cpos = lane < nc ? (int)s.cand[lane] : 0;
+    ctok = id;
+    cplen = id != 0 ? tok_plen(P, id) : 0;
+    cdep = max(depth0 + ex.x, ex.y);
+    fdep = __builtin_amdgcn_readlane(max(depth0 + x.x, x.y), 63);
     if (id != 0) {
-      s.tok_pos[k] = s.cand[lane];
+      s.tok_pos[k] = (uint16_t)cpos;
       s.tok_id[k] = (int8_t)id;
-      s.tok_len[k] = (uint8_t)tok_plen(P, id);
-      s.tok_dep[k] = (int16_t)max(depth0 + ex.x, ex.y);
+      s.tok_len[k] = (uint8_t)cplen;
+      s.tok_dep[k] = (int16_t)cdep;
     }
     if (lane == 63) {
       const int nt = __popcll(m);
       s.v[V_NTOK] = nt;
-      s.tok_dep[nt] = (int16_t)max(depth0 + x.x, x.y);
+      s.tok_dep[nt] = (int16_t)fdep;
     }
   }
+  // hold_cut from the candidate registers: the last candidate before e (positions ascend),
+  // its token / length and the depth before it; then the same decisions as hold_cut
+  auto hold_cut_r = [&](int e, bool for_tail, int* q_out) -> int {
+    int q = -1, tk = 0, pl = 0, dq = 0;
+    for (int k = 0; k < nc; ++k) {  // (uniform bound, nc <= 63)
+      const int ck = __builtin_amdgcn_readlane(cpos, k), tkk = __builtin_amdgcn_readlane(ctok, k);
+      const int plk = __builtin_amdgcn_readlane(cplen, k), dqk = __builtin_amdgcn_readlane(cdep, k);
+      const bool b = ck < e;
+      q = b ? ck : q;
+      tk = b ? tkk : tk;
+      pl = b ? plk : pl;
+      dq = b ? dqk : dq;
+    }
+    *q_out = -1;
+    if (q < 0) return e;
+    if (tk != 0 && q + pl <= e) return e;  // completed token
+    if (!pattern_prefix_w(Z, q, e, P, dq == 0)) return e;
+    if (dq == 0 || for_tail) {
+      *q_out = q;
+      return dq == 0 ? q : e;
+    }
+    return e;
+  };
   wave_fence();
   const int ntok = __builtin_amdgcn_readfirstlane(s.v[V_NTOK]);
   if (dbg != nullptr && lane == 0) dbg_put(&dbg[25], __builtin_amdgcn_s_memrealtime());
@@ -685,10 +727,10 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
   if (lane < ndelta || (tail_here && lane == ndelta)) {
     const bool is_tail = lane == ndelta;
     int q;
-    const int c = hold_cut(s, Z, nc, ntok, is_tail ? Zn : (int)s.dl_end[lane], P, is_tail, &q);
+    const int c = hold_cut_r(is_tail ? Zn : (int)s.dl_end[lane], is_tail, &q);
     if (is_tail) {
       s.v[V_NEWTAIL] = q;
-      s.v[V_NEWDEPTH] = s.tok_dep[ntok];
+      s.v[V_NEWDEPTH] = fdep;
     } else {
       cut = c;
       s.cut[lane] = (uint16_t)cut;
@@ -696,9 +738,9 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
   }
   if (!tail_here && lane == 0) {  // 64 deltas: the tail after them, on lane 0
     int q;
-    hold_cut(s, Z, nc, ntok, Zn, P, true, &q);
+    hold_cut_r(Zn, true, &q);
     s.v[V_NEWTAIL] = q;
-    s.v[V_NEWDEPTH] = s.tok_dep[ntok];
+    s.v[V_NEWDEPTH] = fdep;
   }
   const int cutN = __shfl(cut, ndelta - 1, 64);
   if (dbg != nullptr && lane == 0) dbg_put(&dbg[24], __builtin_amdgcn_s_memrealtime());
@@ -811,56 +853,63 @@ __device__ inline uint64_t nl_mask64(const uint8_t* x, int lo, int len) {
 
 // S2 on wave 0 (tiles up to 4 KiB past the leading whitespace: a streaming tick, or a whole
 // short response): the block path's newline-run framing with DPP wave scans instead of block
-// scans and the finalize on lane 0 — one block barrier instead of five
+// scans and the finalize on lane 0 — one block barrier instead of five.  4 KiB per pass (64
+// lanes x <= 64 bytes, one 64-bit newline mask per lane); the newline-run state, the
+// separator count and the last separator carry from pass to pass.
 __device__ inline void s2_wave(Smem& s, int start, int in_len, bool eof) {
   const int lane = threadIdx.x & 63;
-  const int flen = in_len - start;
-  const int C8 = (((flen + 63) / 64) + 7) & ~7;  // <= 64
-  const int lo = min(start + lane * C8, in_len), hi = min(lo + C8, in_len), len = hi - lo;
-  const uint64_t nm = nl_mask64(s.A, lo, len);
-  const uint64_t valid = len >= 64 ? ~0ull : ((1ull << len) - 1ull);
-  const uint64_t inv = ~nm & valid;
-  const bool all_nl = inv == 0;
-  const int trail = all_nl ? len : len - 64 + __clzll(inv);
-  const bool next_nl = hi < in_len && s.A[hi] == '\n';
-  const int2 run = all_nl ? make_int2(1, len) : make_int2(0, trail);
-  const int2 incl = wave_incl_pair(run, RunOp());
-  int2 ex;
-  ex.x = __shfl_up(incl.x, 1, 64);
-  ex.y = __shfl_up(incl.y, 1, 64);
-  if (lane == 0) ex = make_int2(1, 0);
-  // separators: "\n" at an even position of its newline run, followed by a "\n"
-  auto each_sep = [&](auto&& f) {
-    uint64_t m = nm;
-    while (m) {
-      const int r0 = __ffsll((unsigned long long)m) - 1;
-      const uint64_t rest = ~(m >> r0);
-      const int L = rest == 0 ? 64 - r0 : __ffsll((unsigned long long)rest) - 1;
-      const int c = r0 == 0 ? ex.y : 0;
-      const bool ext = r0 + L == len && next_nl;
-      for (int i = 0; i < L; ++i)
-        if (!((c + i) & 1) && (i + 1 < L || ext)) f(lo + r0 + i);
-      m &= ~(L >= 64 ? ~0ull : (((1ull << L) - 1ull) << r0));
-    }
-  };
-  int cnt = 0, last = -1;
-  each_sep([&](int p) {
-    ++cnt;
-    last = p;
-  });
-  const int ci = wave_incl_sum(cnt);
-  int k = ci - cnt;
-  const int nsep = __shfl(ci, 63, 64);
-  each_sep([&](int p) {
-    if (k < MAX_EV) s.ev_b[k] = (uint16_t)p;
-    if (k + 1 < MAX_EV) s.ev_a[k + 1] = (uint16_t)(p + 2);
-    ++k;
-  });
-  int lastsep = last;  // the tile's last separator: a wave max
-  for (int o = 32; o > 0; o >>= 1) lastsep = max(lastsep, __shfl_xor(lastsep, o, 64));
+  int2 carry = make_int2(1, 0);  // newline run ending at the pass's start (none before `start`)
+  int kb = 0, lastsep = -1;      // separators of earlier passes / the last one
+  for (int base = start; base < in_len; base += 64 * 64) {
+    const int end = min(base + 64 * 64, in_len);
+    const int C8 = ((((end - base) + 63) / 64) + 7) & ~7;  // <= 64
+    const int lo = min(base + lane * C8, end), hi = min(lo + C8, end), len = hi - lo;
+    const uint64_t nm = nl_mask64(s.A, lo, len);
+    const uint64_t valid = len >= 64 ? ~0ull : ((1ull << len) - 1ull);
+    const uint64_t inv = ~nm & valid;
+    const bool all_nl = inv == 0;
+    const int trail = all_nl ? len : len - 64 + __clzll(inv);
+    const bool next_nl = hi < in_len && s.A[hi] == '\n';
+    const int2 run = all_nl ? make_int2(1, len) : make_int2(0, trail);
+    const int2 incl = wave_incl_pair(run, RunOp());
+    int2 ex;
+    ex.x = __shfl_up(incl.x, 1, 64);
+    ex.y = __shfl_up(incl.y, 1, 64);
+    ex = lane == 0 ? carry : RunOp()(carry, ex);
+    // separators: "\n" at an even position of its newline run, followed by a "\n"
+    auto each_sep = [&](auto&& f) {
+      uint64_t m = nm;
+      while (m) {
+        const int r0 = __ffsll((unsigned long long)m) - 1;
+        const uint64_t rest = ~(m >> r0);
+        const int L = rest == 0 ? 64 - r0 : __ffsll((unsigned long long)rest) - 1;
+        const int c = r0 == 0 ? ex.y : 0;
+        const bool ext = r0 + L == len && next_nl;
+        for (int i = 0; i < L; ++i)
+          if (!((c + i) & 1) && (i + 1 < L || ext)) f(lo + r0 + i);
+        m &= ~(L >= 64 ? ~0ull : (((1ull << L) - 1ull) << r0));
+      }
+    };
+    int cnt = 0, last = -1;
+    each_sep([&](int p) {
+      ++cnt;
+      last = p;
+    });
+    const int ci = wave_incl_sum(cnt);
+    int k = kb + ci - cnt;
+    each_sep([&](int p) {
+      if (k < MAX_EV) s.ev_b[k] = (uint16_t)p;
+      if (k + 1 < MAX_EV) s.ev_a[k + 1] = (uint16_t)(p + 2);
+      ++k;
+    });
+    for (int o = 32; o > 0; o >>= 1) last = max(last, __shfl_xor(last, o, 64));  // a wave max
+    lastsep = max(lastsep, last);
+    kb += __shfl(ci, 63, 64);
+    carry = RunOp()(carry, make_int2(__shfl(incl.x, 63, 64), __shfl(incl.y, 63, 64)));
+  }
   if (lane == 0) {
     s.ev_a[0] = (uint16_t)start;
-    s.v[V_NSEP] = nsep;
+    s.v[V_NSEP] = kb;
     s.v[V_LASTSEP] = lastsep;
   }
   wave_fence();
@@ -1028,7 +1077,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   // over stride-C chunks were bank-conflicted LDS reads, three passes over every byte.
   const int flen0 = in_len - start;
   const int C8 = (((flen0 + BS - 1) / BS) + 7) & ~7;
-  const bool s2_wave_ok = (P.fast & 1) && (start & 7) == 0 && flen0 <= 4096;
+  const bool s2_wave_ok = (P.fast & 1) && (start & 7) == 0 && flen0 <= 4096;  // (two passes, 4.9 KB: 3.7 us vs the block path's 2.7, r4/i)
   if (s2_wave_ok) {
     if (tid < 64) s2_wave(s, start, in_len, eof);
   } else if ((start & 7) == 0 && C8 <= 32) {
@@ -1165,6 +1214,13 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     auto half_clear = [upper](uint64_t m) { return (upper ? (m >> 32) : (m & 0xffffffffull)) == 0; };
     int newest = -1, nm = 0, nhole = 0, unres = 0;
     uint32_t hmatch = 0;
+    // the hole templates' lengths, 0 for none / a kind S3a does not resolve (item-invariant)
+    int hl[kHoleTpls];
+#pragma unroll
+    for (int qi = 0; qi < kHoleTpls; ++qi) {
+      const HoleTpl& T = U.htpl[qi];
+      hl[qi] = (T.kind == EV_CONTENT || T.kind == EV_SKIP) ? (int)T.len : 0;
+    }
     for (int kb = 0; kb < nev; kb += BS / 32) {
       const int k = kb + hw;
       const bool have = k < nev;
@@ -1216,22 +1272,26 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
         const uint64_t digit = ((x7 + 0x5050505050505050ull) & ~(x7 + 0x4646464646464646ull) & ~ev) & hi;
         // a byte '0' (first bytes of multi-digit number holes may not be one)
         const uint64_t z0 = ev ^ 0x3030303030303030ull, zero = ((z0 - one) & ~z0) & hi;
+        // the templates are independent tests (no chain through the first match): every
+        // template's words are read up front, the first one whose half-wave is clear wins
+        uint32_t okm = 0;
+#pragma unroll
         for (int qi = 0; qi < kHoleTpls; ++qi) {
           const HoleTpl& T = U.htpl[qi];
-          const int n = T.len;
-          const bool cand = try_b && !done_ev && hq < 0 && n == L && n > 0 && (T.kind == EV_CONTENT || T.kind == EV_SKIP);
+          const bool cand = try_b && L > 0 && hl[qi] == L;
+          const uint32_t hm = T.wmask[lane];                           // (lane < 32)
+          const uint64_t tw = ((const uint64_t*)T.bytes)[lane];
           bool bad = !cand;
           if (cand && o < L) {
-            const uint32_t hm = T.wmask[lane];
             const uint64_t smask = byte_mask8(hm & 0xffu), nmask = byte_mask8((hm >> 8) & 0xffu),
                            zmask = byte_mask8((hm >> 16) & 0xffu);
-            const uint64_t tw = ((const uint64_t*)T.bytes)[lane];
             const uint64_t lit = valid & ~(smask | nmask);
             bad = ((ev ^ tw) & lit) != 0 || (strbad & smask) != 0 || ((~digit & hi) & nmask) != 0 ||
                   (zero & zmask) != 0;
           }
-          if (half_clear(__ballot(bad)) && cand) hq = qi;
+          if (half_clear(__ballot(bad)) && cand) okm |= 1u << qi;
         }
+        hq = done_ev || okm == 0 ? -1 : __ffs(okm) - 1;
       }
       // unresolved: 0xFE when the stream template cannot match (its prefix / suffix differ:
       // the loop skips its own template compare), 0xFF otherwise (an escaped or non-ASCII
@@ -1830,33 +1890,54 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       if (f) s.ejx[__popcll(m & below)] = (uint16_t)lane;
       const int C = (Wlen + 63) / 64;
       const int lo = min(lane * C, Wlen), hi = min(lo + C, Wlen);
-      int x = lo, e = 0;
-      while (x < hi && is_cont(W[x])) ++x;
-      while (x < hi) {
-        uint32_t cp;
-        x += wtf8_decode(W, x, Wlen, &cp);
-        e += escaped_len_cp(cp);
-      }
-      const int incl = wave_incl_sum(e);
-      const int excl = incl - e;
-      const int tot = __shfl(incl, 63, 64);
-      s.chunk_base[lane] = excl;  // the write phase's escaped-content chunks (64 of them here)
-      // (shuffles with every lane active: a lane's chunk base for its delta's escaped prefix)
-      const int t = (lane < ndelta && wp < Wlen && C > 0) ? wp / C : 0;
-      const int tbase = __shfl(excl, t, 64);
-      if (lane < ndelta) {
-        uint32_t ep = (uint32_t)tot;
-        if (wp < Wlen) {
-          int xx = min(t * C, Wlen), ee = tbase;
-          while (xx < wp && is_cont(W[xx])) ++xx;
-          while (xx < wp) {
-            uint32_t cp;
-            xx += wtf8_decode(W, xx, Wlen, &cp);
-            ee += escaped_len_cp(cp);
-          }
-          ep = (uint32_t)ee;
+      // clean content (printable ASCII without '"' or '\\': every byte escapes to itself) —
+      // escaped offsets are raw offsets, no decode walk: 8 bytes per lane per step (SWAR, the
+      // zero / less-than tricks only err towards "not clean")
+      bool dirty = false;
+      {
+        const uint64_t hb = 0x8080808080808080ull, one = 0x0101010101010101ull;
+        for (int x0 = lane * 8; x0 < Wlen; x0 += 64 * 8) {
+          const int nb = min(8, Wlen - x0);
+          const uint64_t w = lds_window8(W, x0, Wlen), vm = nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1);
+          const uint64_t q = w ^ 0x2222222222222222ull, b = w ^ 0x5c5c5c5c5c5c5c5cull, d = w ^ 0x7f7f7f7f7f7f7f7full;
+          const uint64_t odd = (((q - one) & ~q) | ((b - one) & ~b) | ((d - one) & ~d) | ((w - 0x20 * one) & ~w) | w) & hb;
+          dirty = dirty || (odd & vm) != 0;
         }
-        s.epos[lane] = ep;
+      }
+      int tot;
+      if (__ballot(dirty) == 0) {
+        tot = Wlen;
+        s.chunk_base[lane] = lo;
+        if (lane < ndelta) s.epos[lane] = (uint32_t)min(wp, Wlen);
+      } else {
+        int x = lo, e = 0;
+        while (x < hi && is_cont(W[x])) ++x;
+        while (x < hi) {
+          uint32_t cp;
+          x += wtf8_decode(W, x, Wlen, &cp);
+          e += escaped_len_cp(cp);
+        }
+        const int incl = wave_incl_sum(e);
+        const int excl = incl - e;
+        tot = __shfl(incl, 63, 64);
+        s.chunk_base[lane] = excl;  // the write phase's escaped-content chunks (64 of them here)
+        // (shuffles with every lane active: a lane's chunk base for its delta's escaped prefix)
+        const int t = (lane < ndelta && wp < Wlen && C > 0) ? wp / C : 0;
+        const int tbase = __shfl(excl, t, 64);
+        if (lane < ndelta) {
+          uint32_t ep = (uint32_t)tot;
+          if (wp < Wlen) {
+            int xx = min(t * C, Wlen), ee = tbase;
+            while (xx < wp && is_cont(W[xx])) ++xx;
+            while (xx < wp) {
+              uint32_t cp;
+              xx += wtf8_decode(W, xx, Wlen, &cp);
+              ee += escaped_len_cp(cp);
+            }
+            ep = (uint32_t)ee;
+          }
+          s.epos[lane] = ep;
+        }
       }
       if (lane == 0) {
         s.v[V_NEMIT] = __popcll(m);
