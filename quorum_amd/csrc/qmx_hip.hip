@@ -134,9 +134,7 @@ enum : int {
   V_START = 0, V_NSEP, V_LASTSEP, V_ABORT, V_NEV, V_CONSUMED, V_STATUS, V_NDELTA, V_YLEN, V_NCAND,
   V_NTOK, V_BAIL, V_DEPTH0, V_TAILLEN, V_NEWTAIL, V_NEWDEPTH, V_WLEN, V_NEMIT, V_ETOT, V_OUTLEN,
   V_TPLPRE, V_TPLSUF, V_TPLK, V_NEXTEV, V_NFULL, V_NTPL, V_CFULL, V_CTPL, V_CLEX, V_NHOLE, V_CHOLE, V_S4W,
-  V_HCLAIM,  // hole-template slots this workgroup wrote (bit per slot): one writer per slot
-  V_UNRES,   // events S3a left for the loop
-  V_HMATCH   // hole templates S3a matched (bit per slot)
+  V_HCLAIM  // hole-template slots this workgroup wrote (bit per slot): one writer per slot
 };
 
 // LDS byte reader that fetches one aligned 64-bit word per 8 sequential bytes: a byte-serial
@@ -922,6 +920,7 @@ struct TickShared {
   uint16_t TKP[BS / 64][TOK_CAP];              // per-wave token buffers (positions)
   alignas(8) uint8_t TKT[BS / 64][TOK_CAP];    // token bytes (type | key id | flags)
   int wtpl[BS / 64][4];  // S3: per-wave in-tile templates {p0, tp, s0, ts} (p0 < 0: none)
+  int s3w[BS / 64][4];   // S3a per wave: events left for the loop, hole templates matched, newest content event
   HoleTpl htpl[kHoleTpls];  // S3: this item's backend hole templates (previous launch's)
 };
 
@@ -988,8 +987,6 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     s.v[V_NEXTEV] = 0;
     s.v[V_NFULL] = s.v[V_NTPL] = s.v[V_CFULL] = s.v[V_CTPL] = s.v[V_CLEX] = s.v[V_NHOLE] = s.v[V_CHOLE] = 0;
     s.v[V_HCLAIM] = 0;
-    s.v[V_UNRES] = 0;
-    s.v[V_HMATCH] = 0;
     for (int q = 0; q < BS / 64; ++q) wtpl[q][0] = -1;
     if (fresh) {
       s.v[V_DEPTH0] = 0;
@@ -1124,7 +1121,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     each_sep([&](int p) {
       if (k < MAX_EV) s.ev_b[k] = (uint16_t)p;
       if (k + 1 < MAX_EV) s.ev_a[k + 1] = (uint16_t)(p + 2);
-      atomicMax(&s.v[V_LASTSEP], p);
+      if (k == nsep - 1) s.v[V_LASTSEP] = p;  // the last separator's writer (no LDS atomics)
       ++k;
     });
     if (tid == 0) {
@@ -1163,7 +1160,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
         if (!(r & 1) && p + 1 < in_len && rd[p + 1] == '\n') {
           if (k < MAX_EV) s.ev_b[k] = (uint16_t)p;
           if (k + 1 < MAX_EV) s.ev_a[k + 1] = (uint16_t)(p + 2);
-          atomicMax(&s.v[V_LASTSEP], p);
+          if (k == nsep - 1) s.v[V_LASTSEP] = p;
           ++k;
         }
         ++r;
@@ -1262,7 +1259,9 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       const bool try_b = have && !ok && fast && L <= 256;
       bool done_ev = false;
       int hq = -1;
-      if (fast) {
+      // (wave-uniform: a wave whose two events both matched the content template — the bulk
+      // of a burst — skips the whole section; S3a is VALU-bound with 8 waves on 4 SIMDs)
+      if (fast && __ballot(try_b) != 0) {
         const bool dbad = !(try_b && L == 12) || (lane == 0 && ev != 0x445b203a61746164ull) ||  // "data: [D"
                           (lane == 1 && ev != 0x5d454e4full);                                    // "ONE]"
         done_ev = try_b && half_clear(__ballot(dbad));
@@ -1329,25 +1328,44 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       // the tile's newest content event (template or hole match) becomes the template
       if (kind == EV_CONTENT && sa - e0 <= TPL_PRE_MAX && e1 - sb <= TPL_SUF_MAX) newest = k;
     }
-    if (lane == 0) {  // (both half-waves)
-      if (nm > 0) atomicAdd(&s.v[V_NTPL], nm);
-      if (newest >= 0) atomicMax(&s.v[V_TPLK], newest);
-      if (nhole > 0) {
-        atomicAdd(&s.v[V_NHOLE], nhole);
-        atomicOr(&s.v[V_HMATCH], (int)hmatch);
+    // per wave, not per half-wave LDS atomics on shared words (32 of them serialised at the
+    // LDS): the upper half's values come over by readlane, lane 0 stores the wave's slot
+    {
+      const int w = tid >> 6;
+      const int unres2 = unres + __builtin_amdgcn_readlane(unres, 32);
+      const int newest2 = max(newest, __builtin_amdgcn_readlane(newest, 32));
+      const uint32_t hm2 = hmatch | (uint32_t)__builtin_amdgcn_readlane((int)hmatch, 32);
+      if ((tid & 63) == 0) {
+        U.s3w[w][0] = unres2;
+        U.s3w[w][1] = (int)hm2;
+        U.s3w[w][2] = newest2;
+        if (P.dbg != nullptr) {  // (stage-timing counters)
+          atomicAdd(&s.v[V_NTPL], nm + __builtin_amdgcn_readlane(nm, 32));
+          atomicAdd(&s.v[V_NHOLE], nhole + __builtin_amdgcn_readlane(nhole, 32));
+        }
       }
-      if (unres > 0) atomicAdd(&s.v[V_UNRES], unres);
     }
   }
   __syncthreads();
   QMX_STAMP(21);
   {
     const int w = tid >> 6, lane = tid & 63;
+    // S3a's per-wave results: events left for the loop, hole templates matched, the newest
+    // content event (block-uniform: read after the barrier)
+    int unres_all = 0, newest_all = -1;
+    uint32_t hm_all = 0;
+#pragma unroll
+    for (int q = 0; q < BS / 64; ++q) {
+      unres_all += U.s3w[q][0];
+      hm_all |= (uint32_t)U.s3w[q][1];
+      newest_all = max(newest_all, U.s3w[q][2]);
+    }
+    if (tid == 0 && newest_all >= 0) atomicMax(&s.v[V_TPLK], newest_all);
     // a hole template S3a matched is carried into the launch's write table (as the loop's
     // matches are, wave_hole_carry): wave w carries template w
-    if (pub && w < kHoleTpls && ((s.v[V_HMATCH] >> w) & 1))
+    if (pub && w < kHoleTpls && ((hm_all >> w) & 1))
       wave_hole_carry(U.htpl[w], &btpl_wr[it.index].hole[w], w, &s.v[V_HCLAIM]);
-    const bool loop = s.v[V_UNRES] > 0;  // (block-uniform: read after the barrier)
+    const bool loop = unres_all > 0;
     const LdsWords rd(s.A);
     const int tp = s.v[V_TPLPRE], ts = s.v[V_TPLSUF];
     bool published = false;
@@ -3939,7 +3957,7 @@ void HipEngine::collect_finalize(TickLane& L, const std::vector<const FinalizeRe
 
 std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   std::unordered_map<std::string, double> m;
-  double stage[24] = {0}, cyc = 0, cus = 0;
+  double stage[25] = {0}, cyc = 0, cus = 0;
   for (auto& Lp : lanes_) {
     TickLane& L = *Lp;
     std::lock_guard<std::mutex> lg(L.mu);
@@ -3978,7 +3996,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["fin_launches"] += (double)L.fin_launches;  // tick launches that also carried finalize work
     m["fin_items"] += (double)L.fin_items;
     m["fin_staged_texts"] += (double)L.fin_staged;  // mesh-delivered remote finals staged into items
-    for (int k = 1; k < 24; ++k) stage[k] += L.stage_us[k];
+    for (int k = 1; k < 25; ++k) stage[k] += L.stage_us[k];
     cyc += L.clk_cycles;
     cus += L.clk_us;
   }
