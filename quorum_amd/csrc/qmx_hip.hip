@@ -1262,26 +1262,30 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       // (wave-uniform: a wave whose two events both matched the content template — the bulk
       // of a burst — skips the whole section; S3a is VALU-bound with 8 waves on 4 SIMDs)
       if (fast && __ballot(try_b) != 0) {
-        const bool dbad = !(try_b && L == 12) || (lane == 0 && ev != 0x445b203a61746164ull) ||  // "data: [D"
-                          (lane == 1 && ev != 0x5d454e4full);                                    // "ONE]"
-        done_ev = try_b && half_clear(__ballot(dbad));
-        // DEL (0x7f) and number-hole digits, SWAR like `odd`
-        const uint64_t dl = ev ^ 0x7f7f7f7f7f7f7f7full, x7 = ev & 0x7f7f7f7f7f7f7f7full;
-        const uint64_t strbad = odd | (((dl - one) & ~dl) & hi);
-        const uint64_t digit = ((x7 + 0x5050505050505050ull) & ~(x7 + 0x4646464646464646ull) & ~ev) & hi;
-        // a byte '0' (first bytes of multi-digit number holes may not be one)
-        const uint64_t z0 = ev ^ 0x3030303030303030ull, zero = ((z0 - one) & ~z0) & hi;
-        // the templates are independent tests (no chain through the first match): every
-        // template's words are read up front, the first one whose half-wave is clear wins
+        // each test only when some lane of the wave needs it (wave-uniform skips)
+        if (__ballot(try_b && L == 12) != 0) {
+          const bool dbad = !(try_b && L == 12) || (lane == 0 && ev != 0x445b203a61746164ull) ||  // "data: [D"
+                            (lane == 1 && ev != 0x5d454e4full);                                    // "ONE]"
+          done_ev = try_b && half_clear(__ballot(dbad));
+        }
+        // the templates are independent tests (no chain through the first match); the first
+        // one whose half-wave is clear wins.  Usually one template has the event's length.
         uint32_t okm = 0;
 #pragma unroll
         for (int qi = 0; qi < kHoleTpls; ++qi) {
+          const bool cand = try_b && !done_ev && L > 0 && hl[qi] == L;
+          if (__ballot(cand) == 0) continue;
           const HoleTpl& T = U.htpl[qi];
-          const bool cand = try_b && L > 0 && hl[qi] == L;
-          const uint32_t hm = T.wmask[lane];                           // (lane < 32)
-          const uint64_t tw = ((const uint64_t*)T.bytes)[lane];
           bool bad = !cand;
           if (cand && o < L) {
+            const uint32_t hm = T.wmask[lane];  // (lane < 32)
+            const uint64_t tw = ((const uint64_t*)T.bytes)[lane];
+            // DEL (0x7f) and number-hole digits, SWAR like `odd`; a byte '0' (the first byte of
+            // a multi-digit number hole may not be one)
+            const uint64_t dl = ev ^ 0x7f7f7f7f7f7f7f7full, x7 = ev & 0x7f7f7f7f7f7f7f7full;
+            const uint64_t strbad = odd | (((dl - one) & ~dl) & hi);
+            const uint64_t digit = ((x7 + 0x5050505050505050ull) & ~(x7 + 0x4646464646464646ull) & ~ev) & hi;
+            const uint64_t z0 = ev ^ 0x3030303030303030ull, zero = ((z0 - one) & ~z0) & hi;
             const uint64_t smask = byte_mask8(hm & 0xffu), nmask = byte_mask8((hm >> 8) & 0xffu),
                            zmask = byte_mask8((hm >> 16) & 0xffu);
             const uint64_t lit = valid & ~(smask | nmask);
