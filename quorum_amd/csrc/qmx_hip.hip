@@ -125,6 +125,7 @@ struct Smem {
   int16_t tok_dep[MAX_CAND + 1];
   int32_t chunk_base[BS + 1];
   int32_t scr[2 * (BS / 64)];  // block scans: one (pair) partial per wave
+  int32_t scr2[2 * (BS / 64)];  // a second scan's partials (no barrier between the two)
   int32_t v[40];
   alignas(16) uint8_t tpl[TPL_BYTES];  // this stream's event shape template
 };
@@ -192,6 +193,9 @@ __device__ inline int2 wave_incl_pair(int2 x, Op op) {
   return x;
 }
 
+// tail_barrier = false: the caller guarantees a block barrier before anything writes `scr`
+// again (its own later barrier, or the next scan uses another scratch array)
+template <bool tail_barrier = true>
 __device__ inline int block_excl_sum(int v, int32_t* scr, int* total) {
   int w = threadIdx.x >> 6;
   const int x = wave_incl_sum(v);
@@ -204,13 +208,13 @@ __device__ inline int block_excl_sum(int v, int32_t* scr, int* total) {
     if (i < w) base += s;
     tot += s;
   }
-  __syncthreads();
+  if (tail_barrier) __syncthreads();
   *total = tot;
   return base + x - v;
 }
 
 // generic pair monoid scan: T = int2 {a, b}
-template <class Op>
+template <class Op, bool tail_barrier = true>
 __device__ inline int2 block_excl_pair(int2 v, int2 ident, Op op, int32_t* scr, int2* total) {
   int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int2 x = wave_incl_pair(v, op);
@@ -226,7 +230,7 @@ __device__ inline int2 block_excl_pair(int2 v, int2 ident, Op op, int32_t* scr, 
     if (i < w) base = op(base, s);
     tot = op(tot, s);
   }
-  __syncthreads();
+  if (tail_barrier) __syncthreads();
   int2 ex;
   ex.x = __shfl_up(x.x, 1, 64);
   ex.y = __shfl_up(x.y, 1, 64);
@@ -1099,7 +1103,8 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     const bool next_nl = hi < in_len && s.A[hi] == '\n';
     int2 run = all_nl ? make_int2(1, len) : make_int2(0, trail);
     int2 tot2;
-    int2 ex = block_excl_pair(run, make_int2(1, 0), RunOp(), s.scr, &tot2);
+    // (no tail barriers: the count scan below uses scr2, and S2's barrier follows it)
+    int2 ex = block_excl_pair<RunOp, false>(run, make_int2(1, 0), RunOp(), s.scr, &tot2);
     // separators: "\n" at an even position of its newline run, followed by a "\n"
     auto each_sep = [&](auto&& f) {
       uint32_t m = nm;
@@ -1117,7 +1122,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     int cnt = 0;
     each_sep([&](int) { ++cnt; });
     int nsep;
-    int k = block_excl_sum(cnt, s.scr, &nsep);
+    int k = block_excl_sum<false>(cnt, s.scr2, &nsep);
     each_sep([&](int p) {
       if (k < MAX_EV) s.ev_b[k] = (uint16_t)p;
       if (k + 1 < MAX_EV) s.ev_a[k + 1] = (uint16_t)(p + 2);
@@ -1602,7 +1607,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       loc += pk;
     }
     int tot;
-    int base = block_excl_sum(loc, s.scr, &tot);
+    int base = block_excl_sum<false>(loc, s.scr, &tot);  // (the barrier below follows)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       int k = tid * 4 + i;
