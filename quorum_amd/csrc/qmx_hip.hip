@@ -696,6 +696,35 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
       s.tok_dep[nt] = (int16_t)fdep;
     }
   }
+  // pattern_prefix_w from registers: lane t holds pattern t's length and first two 8-byte
+  // words (every default tag's pattern fits 16 bytes; longer ones read further words from P)
+  const int npw = 2 * P.ts.n;  // (<= 2 * kMaxTags <= 64 lanes)
+  const int pl_l = lane < npw ? pattern_len(P.ts, lane) : 0;
+  const uint64_t pw0_l = lane < npw ? P.pw[lane][0] : 0ull, pw1_l = lane < npw ? P.pw[lane][1] : 0ull;
+  auto prefix_r = [&](int q, int e, bool opens_only) -> bool {
+    const int m = e - q;
+    if (m <= 0 || m > kMaxTail) return m <= 0;
+    const int np = opens_only ? P.ts.n : npw;
+    const uint64_t z0 = lower8(lds_window8(Z, q, e)), z1 = m > 8 ? lower8(lds_window8(Z, q + 8, e)) : 0ull;
+    const uint64_t m0 = m >= 8 ? ~0ull : ((1ull << (8 * m)) - 1);
+    const uint64_t m1 = m >= 16 ? ~0ull : m <= 8 ? 0ull : ((1ull << (8 * (m - 8))) - 1);
+    bool found = false;
+    for (int t = 0; t < np; ++t) {  // (uniform bound)
+      const int plen = __builtin_amdgcn_readlane(pl_l, t);
+      const uint64_t a0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pw0_l >> 32), t) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pw0_l, t);
+      const uint64_t a1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pw1_l >> 32), t) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pw1_l, t);
+      bool ok = !found && m <= plen && z0 == (a0 & m0) && (m <= 8 || z1 == (a1 & m1));
+      for (int w = 2; ok && 8 * w < m; ++w) {  // (patterns longer than 16 bytes)
+        const int nb = min(8, m - 8 * w);
+        const uint64_t mw = nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1);
+        ok = lower8(lds_window8(Z, q + 8 * w, e)) == (P.pw[t][w] & mw);
+      }
+      found = found || ok;
+    }
+    return found;
+  };
   // hold_cut from the candidate registers: the last candidate before e (positions ascend),
   // its token / length and the depth before it; then the same decisions as hold_cut
   auto hold_cut_r = [&](int e, bool for_tail, int* q_out) -> int {
@@ -712,7 +741,7 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
     *q_out = -1;
     if (q < 0) return e;
     if (tk != 0 && q + pl <= e) return e;  // completed token
-    if (!pattern_prefix_w(Z, q, e, P, dq == 0)) return e;
+    if (!prefix_r(q, e, dq == 0)) return e;
     if (dq == 0 || for_tail) {
       *q_out = q;
       return dq == 0 ? q : e;
