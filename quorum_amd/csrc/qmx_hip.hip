@@ -77,9 +77,13 @@ __device__ __forceinline__ void dbg_put(unsigned long long* p, unsigned long lon
 // s_waitcnt vmcnt(0) (expcnt and lgkmcnt left alone): this wave's vector memory accesses,
 // stores included, have completed; a compiler barrier too, so no store is moved past it
 // bit i of m (i < 8) -> byte i of the result 0xff
+// (shifts and masks per 32-bit half, no 64-bit multiply: v_mul_lo_u32 is quarter rate)
+__device__ __forceinline__ uint32_t byte_mask4(uint32_t n) {  // bits 0-3 -> bytes 0-3
+  const uint32_t t = (n | (n << 7) | (n << 14) | (n << 21)) & 0x01010101u;
+  return (t << 8) - t;  // each byte 0 or 1 -> 0x00 or 0xff (mod 2^32)
+}
 __device__ __forceinline__ uint64_t byte_mask8(uint32_t m) {
-  const uint64_t x = ((uint64_t)m * 0x0101010101010101ull) & 0x8040201008040201ull;  // byte i: bit i or 0
-  return (((x + 0x7f7f7f7f7f7f7f7full) & 0x8080808080808080ull) >> 7) * 0xffull;
+  return ((uint64_t)byte_mask4((m >> 4) & 0xfu) << 32) | byte_mask4(m & 0xfu);
 }
 __device__ __forceinline__ void wave_stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // Publish a sequence number: the release fence (buffer_wbl2: this XCD's L2 written back to
@@ -655,6 +659,23 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
     nc += __shfl(incl, 63, 64);
     if (nc > 63) return false;  // (lane k owns token k AND the gap after it: ntok <= 63)
   }
+  if (nc == 0) {
+    // no '<' anywhere in Z (the block path's no-candidate case; a held tail starts with '<', so
+    // none is pending): outside a think block every byte is kept in place (W = Z: the caller
+    // sees V_S4W = 2), inside one every byte is dropped — the usual streaming tick
+    const bool keep = depth0 == 0;
+    if (lane < ndelta) {
+      s.cut[lane] = s.dl_end[lane];
+      s.wpos[lane] = keep ? s.dl_end[lane] : 0;
+    }
+    if (lane == 0) {
+      s.v[V_WLEN] = keep ? Zn : 0;
+      s.v[V_NEWTAIL] = -1;
+      s.v[V_NEWDEPTH] = depth0;
+      s.v[V_S4W] = 2;
+    }
+    return true;
+  }
   if (lane < nc) s.cand_tok[lane] = 0;
   wave_fence();
   if (dbg != nullptr && lane == 0) dbg_put(&dbg[29], __builtin_amdgcn_s_memrealtime());
@@ -1020,6 +1041,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     s.v[V_NEXTEV] = 0;
     s.v[V_NFULL] = s.v[V_NTPL] = s.v[V_CFULL] = s.v[V_CTPL] = s.v[V_CLEX] = s.v[V_NHOLE] = s.v[V_CHOLE] = 0;
     s.v[V_HCLAIM] = 0;
+    s.v[V_S4W] = 0;  // (s4_wave's "no candidates" mark: LDS outlives the previous item)
     for (int q = 0; q < BS / 64; ++q) wtpl[q][0] = -1;
     if (fresh) {
       s.v[V_DEPTH0] = 0;
@@ -1698,12 +1720,12 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   if ((P.fast & 4) && filt && ndelta > 0 && Zn <= 2048 && ndelta <= 64) {  // the common tile: one wave (s4_wave)
     if (tid < 64) {
       const bool ok = s4_wave(s, Z, Zn, ndelta, depth0, P, P.dbg != nullptr ? P.dbg + bi * kDbg : nullptr);
-      if (tid == 0) s.v[V_S4W] = ok ? 1 : 0;
+      if (tid == 0 && s.v[V_S4W] != 2) s.v[V_S4W] = ok ? 1 : 0;  // (2: no candidates, W = Z)
     }
     __syncthreads();
     if (s.v[V_S4W]) {
       s4_done = true;
-      W = s.A;
+      W = s.v[V_S4W] == 2 ? Z : s.A;
     }
   }
   if (filt && ndelta > 0 && !s4_done) {
