@@ -1082,45 +1082,41 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   QMX_STAMP(1);
   const int tail_len = filt ? s.v[V_TAILLEN] : 0;
   uint8_t* Z = s.B + PAD;
-  if (tid < tail_len) Z[tid] = state[it.slot].tail[tid];
+  {  // the holdback tail (<= kMaxTail = 64 bytes) by the last wave: wave 0 frames the tile next
+    static_assert(kMaxTail <= 64, "one wave copies the tail");
+    const int tt = tid - (BS - 64);
+    if (tt >= 0 && tt < tail_len) Z[tt] = state[it.slot].tail[tt];
+  }
 
   // ---- S1: leading whitespace at stream start ---------------------------------------
-  // (fusing it with S2's one-wave framing into one barrier measured no faster: r4/d)
-  if (tid == 0) {
-    int pos = 0;
-    bool started = it.flags & WF_STARTED;
-    bool wait = false;
-    if (!started) {
-      while (pos < in_len) {
-        int w = ws_at(s.A, pos, in_len);
-        if (w <= 0) break;
-        pos += w;
-      }
-      bool undecided = pos < in_len && ws_at(s.A, pos, in_len) < 0;
-      if (pos >= in_len || (undecided && !eof)) wait = true;
-      else s.v[V_STATUS] |= WS_STARTED;
+  // Every thread decides it from the tile's first bytes (broadcast LDS reads): no barrier to
+  // publish one thread's answer.  (Fusing S1 into S2's one-wave framing measured no faster, r4/d.)
+  int start = 0;
+  bool wait = false;
+  if (!(it.flags & WF_STARTED)) {
+    while (start < in_len) {
+      const int w = ws_at(s.A, start, in_len);
+      if (w <= 0) break;
+      start += w;
     }
-    s.v[V_START] = pos;
-    s.v[V_BAIL] = wait ? 1 : 0;
-    if (wait) {
-      s.v[V_CONSUMED] = pos;
-      if (eof) s.v[V_STATUS] |= WS_DONE;
-    }
+    const bool undecided = start < in_len && ws_at(s.A, start, in_len) < 0;
+    wait = start >= in_len || (undecided && !eof);
+    if (!wait && tid == 0) s.v[V_STATUS] |= WS_STARTED;
   }
-  __syncthreads();
-  if (s.v[V_BAIL]) {
-    if (tid == 0 && fresh) {
-      state[it.slot].depth = 0;
-      state[it.slot].tail_len = 0;
-      state[it.slot].tpl_pre = state[it.slot].tpl_suf = 0;
-    }
+  if (wait) {  // (block-uniform)
     if (tid == 0) {
-      WorkResult r{(uint32_t)s.v[V_CONSUMED], 0u, (uint32_t)s.v[V_STATUS], it.content_len};
+      if (fresh) {
+        state[it.slot].depth = 0;
+        state[it.slot].tail_len = 0;
+        state[it.slot].tpl_pre = state[it.slot].tpl_suf = 0;
+      }
+      s.v[V_CONSUMED] = start;
+      if (eof) s.v[V_STATUS] |= WS_DONE;
+      WorkResult r{(uint32_t)start, 0u, (uint32_t)s.v[V_STATUS], it.content_len};
       res[bi] = r;
     }
     return;
   }
-  const int start = s.v[V_START];
   QMX_STAMP(2);
 
   // ---- S2: framing -----------------------------------------------------------------
@@ -1648,33 +1644,47 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   QMX_STAMP(4);
   const int kab = s.v[V_ABORT];
   {
-    int loc = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int k = tid * 4 + i;
-      int pk = 0;
-      if (k < nev && k < kab && s.ev_kind[k] == EV_CONTENT) pk = (1 << 16) | s.ev_dl[k];
-      packed_local[i] = loc;
-      loc += pk;
-    }
-    int tot;
-    int base = block_excl_sum<false>(loc, s.scr, &tot);  // (the barrier below follows)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int k = tid * 4 + i;
-      if (k < nev && k < kab && s.ev_kind[k] == EV_CONTENT) {
-        int pre = base + packed_local[i];
-        int j = pre >> 16, doff = pre & 0xFFFF;
-        int dl = s.ev_dl[k];
-        s.dl_end[j] = (uint16_t)(tail_len + doff + dl);
-        if (dl == s.ev_sb[k] - s.ev_sa[k]) {  // escape-free (every escape shrinks): copied below
-          s.ev_a[k] = (uint16_t)doff;
-        } else {
-          json_unescape(LdsWords(s.A), s.ev_sa[k], s.ev_sb[k], Z + tail_len + doff);
-          s.ev_a[k] = 0xFFFF;
-        }
-      } else if (k < nev) {
+    // each content event's delta index and offset in Z (a prefix sum of (1, escaped length)
+    // pairs); unescaped bodies are written here, escape-free ones copied below by waves
+    auto place = [&](int k, int pre) {
+      const int j = pre >> 16, doff = pre & 0xFFFF;
+      const int dl = s.ev_dl[k];
+      s.dl_end[j] = (uint16_t)(tail_len + doff + dl);
+      if (dl == s.ev_sb[k] - s.ev_sa[k]) {  // escape-free (every escape shrinks): copied below
+        s.ev_a[k] = (uint16_t)doff;
+      } else {
+        json_unescape(LdsWords(s.A), s.ev_sa[k], s.ev_sb[k], Z + tail_len + doff);
         s.ev_a[k] = 0xFFFF;
+      }
+    };
+    int tot = 0;
+    if (nev <= 64) {
+      // the common tile: wave 0, an event per lane, one DPP scan — no block scan barrier
+      if (tid < 64) {
+        const int k = tid;
+        const bool c = k < nev && k < kab && s.ev_kind[k] == EV_CONTENT;
+        const int pk = c ? ((1 << 16) | (int)s.ev_dl[k]) : 0;
+        const int incl = wave_incl_sum(pk);
+        tot = __shfl(incl, 63, 64);
+        if (c) place(k, incl - pk);
+        else if (k < nev) s.ev_a[k] = 0xFFFF;
+      }
+    } else {
+      int loc = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int k = tid * 4 + i;
+        int pk = 0;
+        if (k < nev && k < kab && s.ev_kind[k] == EV_CONTENT) pk = (1 << 16) | s.ev_dl[k];
+        packed_local[i] = loc;
+        loc += pk;
+      }
+      int base = block_excl_sum<false>(loc, s.scr, &tot);  // (the barrier below follows)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int k = tid * 4 + i;
+        if (k < nev && k < kab && s.ev_kind[k] == EV_CONTENT) place(k, base + packed_local[i]);
+        else if (k < nev) s.ev_a[k] = 0xFFFF;
       }
     }
     __syncthreads();
