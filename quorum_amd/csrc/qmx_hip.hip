@@ -851,7 +851,9 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
 
 // S2's last step (one thread): events of the tile from the separators, what it consumed,
 // and whether the stream is done / has more events than one tile holds
-__device__ inline void s2_finalize(Smem& s, int start, int in_len, bool eof) {
+// owner = false: only the event list (identical writes from every wave's lane 0), not the
+// result's consumed count and status bits (thread 0's)
+__device__ inline void s2_finalize(Smem& s, int start, int in_len, bool eof, bool owner = true) {
   int nsep = s.v[V_NSEP];
   int nev, consumed;
   bool done = false, more = false;
@@ -881,6 +883,7 @@ __device__ inline void s2_finalize(Smem& s, int start, int in_len, bool eof) {
     }
   }
   s.v[V_NEV] = nev;
+  if (!owner) return;
   s.v[V_CONSUMED] = consumed;
   if (done) s.v[V_STATUS] |= WS_DONE;
   if (more) s.v[V_STATUS] |= WS_MORE;
@@ -1227,8 +1230,10 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   }
   __syncthreads();
   if (!s2_wave_ok) {  // (s2_wave finalises on its own lane 0)
-    if (tid == 0) s2_finalize(s, start, in_len, eof);
-    __syncthreads();
+    // every wave's lane 0 finalises (the same event list) and its wave reads it after a wave
+    // fence — no second block barrier to publish one thread's answer
+    if ((tid & 63) == 0) s2_finalize(s, start, in_len, eof, tid == 0);
+    wave_fence();
   }
   QMX_STAMP(3);
   const int nev = s.v[V_NEV];
