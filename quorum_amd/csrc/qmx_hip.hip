@@ -1409,11 +1409,11 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   }
   __syncthreads();
   QMX_STAMP(21);
+  // S3a's per-wave results: events left for the loop, hole templates matched, the newest
+  // content event (block-uniform: read after the barrier)
+  int unres_all = 0, newest_all = -1;
   {
     const int w = tid >> 6, lane = tid & 63;
-    // S3a's per-wave results: events left for the loop, hole templates matched, the newest
-    // content event (block-uniform: read after the barrier)
-    int unres_all = 0, newest_all = -1;
     uint32_t hm_all = 0;
 #pragma unroll
     for (int q = 0; q < BS / 64; ++q) {
@@ -1610,10 +1610,12 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       }
     }
   }
-  __syncthreads();
+  // the loop's results (event kinds, V_TPLK) need a barrier; without the loop every thread
+  // already has the newest content event, and S3a's writes were published by its barrier
+  if (unres_all > 0) __syncthreads();
   QMX_STAMP(22);
   {  // persist the newest template now: S4 reuses the input tile
-    const int tk = s.v[V_TPLK];
+    const int tk = unres_all > 0 ? s.v[V_TPLK] : newest_all;
     if (tk >= 0) {
       const int e0 = s.ev_a[tk], pre = s.ev_sa[tk] - e0, e1 = s.ev_b[tk], suf = e1 - s.ev_sb[tk];
       DevSlot& ds = state[it.slot];
@@ -1650,16 +1652,19 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   const int kab = s.v[V_ABORT];
   {
     // each content event's delta index and offset in Z (a prefix sum of (1, escaped length)
-    // pairs); unescaped bodies are written here, escape-free ones copied below by waves
+    // pairs); unescaped bodies are written here, escape-free ones copied below by waves.  The
+    // copy offset replaces the event's ev_dl (read here by the same thread, by nobody after),
+    // not its ev_a: other waves may still be reading ev_a in the template persist above
+    // (the one-wave path has no block barrier in between)
     auto place = [&](int k, int pre) {
       const int j = pre >> 16, doff = pre & 0xFFFF;
       const int dl = s.ev_dl[k];
       s.dl_end[j] = (uint16_t)(tail_len + doff + dl);
       if (dl == s.ev_sb[k] - s.ev_sa[k]) {  // escape-free (every escape shrinks): copied below
-        s.ev_a[k] = (uint16_t)doff;
+        s.ev_dl[k] = (uint16_t)doff;
       } else {
         json_unescape(LdsWords(s.A), s.ev_sa[k], s.ev_sb[k], Z + tail_len + doff);
-        s.ev_a[k] = 0xFFFF;
+        s.ev_dl[k] = 0xFFFF;
       }
     };
     int tot = 0;
@@ -1672,7 +1677,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
         const int incl = wave_incl_sum(pk);
         tot = __shfl(incl, 63, 64);
         if (c) place(k, incl - pk);
-        else if (k < nev) s.ev_a[k] = 0xFFFF;
+        else if (k < nev) s.ev_dl[k] = 0xFFFF;
       }
     } else {
       int loc = 0;
@@ -1689,7 +1694,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       for (int i = 0; i < 4; ++i) {
         int k = tid * 4 + i;
         if (k < nev && k < kab && s.ev_kind[k] == EV_CONTENT) place(k, base + packed_local[i]);
-        else if (k < nev) s.ev_a[k] = 0xFFFF;
+        else if (k < nev) s.ev_dl[k] = 0xFFFF;
       }
     }
     __syncthreads();
@@ -1700,7 +1705,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       const int kl = w + (BS / 64) * lane;
       int off_l = 0xFFFF, sa_l = 0, n_l = 0;
       if (kl < nev) {
-        off_l = s.ev_a[kl];
+        off_l = s.ev_dl[kl];
         if (off_l != 0xFFFF) {
           sa_l = s.ev_sa[kl];
           n_l = s.ev_sb[kl] - sa_l;

@@ -19,7 +19,7 @@ import pytest
 
 REPO = Path(__file__).resolve().parent.parent
 LLVM = Path("/opt/rocm/lib/llvm/bin")
-TOOLS = [LLVM / "llvm-objcopy", LLVM / "clang-offload-bundler", LLVM / "llvm-objdump"]
+TOOLS = [LLVM / "llvm-objcopy", LLVM / "clang-offload-bundler", LLVM / "llvm-objdump", LLVM / "llvm-readelf"]
 
 
 def _extension():
@@ -28,7 +28,8 @@ def _extension():
 
 
 @pytest.fixture(scope="module")
-def disasm(tmp_path_factory):
+def code_object(tmp_path_factory):
+    """The in-tree extension's gfx950 code object (path)."""
     so = _extension()
     if so is None or not all(t.exists() for t in TOOLS):
         pytest.skip("extension not built or LLVM tools missing")
@@ -42,9 +43,50 @@ def disasm(tmp_path_factory):
     assert gfx, f"no gfx950 code object in {so.name}: {targets}"
     subprocess.run([str(TOOLS[1]), "--unbundle", "--type=o", f"--input={fat}", f"--targets={gfx[0]}",
                     f"--output={co}"], check=True, capture_output=True)
-    out = subprocess.run([str(TOOLS[2]), "-d", "--no-show-raw-insn", str(co)], check=True,
+    return co
+
+
+@pytest.fixture(scope="module")
+def disasm(code_object):
+    out = subprocess.run([str(TOOLS[2]), "-d", "--no-show-raw-insn", str(code_object)], check=True,
                          capture_output=True, text=True).stdout
     return out.splitlines()
+
+
+def kernel_resources(notes: str):
+    """{kernel symbol: {field: int}} from `llvm-readelf --notes` (the AMDHSA metadata: one YAML
+    map per kernel, a `- ` item each, its keys sorted — some before `.name`)."""
+    out, cur = [], None
+    for line in notes.splitlines():
+        if re.match(r"\s*-\s+\.", line):  # a new kernel's map begins
+            cur = {}
+            out.append(cur)
+        if cur is None:
+            continue
+        m = re.match(r"\s*-?\s*\.name:\s+(\S+)", line)
+        if m:
+            cur["name"] = m.group(1)
+            continue
+        m = re.match(r"\s*-?\s*\.(private_segment_fixed_size|vgpr_count|vgpr_spill_count|sgpr_spill_count|"
+                     r"group_segment_fixed_size):\s+(\d+)", line)
+        if m:
+            cur[m.group(1)] = int(m.group(2))
+    return {d["name"]: d for d in out if "name" in d}
+
+
+def test_tick_kernels_have_no_scratch(code_object):
+    """The tick kernels (one-shot and persistent) keep everything in registers and LDS: no
+    private (scratch) memory and no VGPR spills — a spill to scratch is HBM traffic on every
+    item's critical path.  (SGPR spills go to VGPR lanes, not memory.)"""
+    notes = subprocess.run([str(LLVM / "llvm-readelf"), "--notes", str(code_object)], check=True,
+                           capture_output=True, text=True).stdout
+    res = kernel_resources(notes)
+    ticks = {k: v for k, v in res.items() if "qmx_tick_kernel" in k or "qmx_tick_persistent" in k}
+    assert len(ticks) == 2, sorted(res)
+    for name, r in ticks.items():
+        assert r.get("private_segment_fixed_size") == 0, (name, r)
+        assert r.get("vgpr_spill_count", 0) == 0, (name, r)
+        assert r.get("group_segment_fixed_size", 0) <= 160 * 1024, (name, r)  # one CU's LDS
 
 
 _STORE = re.compile(r"^\s*(global_store|flat_store|buffer_store|global_atomic|flat_atomic|buffer_atomic)")
