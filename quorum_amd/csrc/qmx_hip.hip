@@ -139,7 +139,8 @@ enum : int {
   V_START = 0, V_NSEP, V_LASTSEP, V_ABORT, V_NEV, V_CONSUMED, V_STATUS, V_NDELTA, V_YLEN, V_NCAND,
   V_NTOK, V_BAIL, V_DEPTH0, V_TAILLEN, V_NEWTAIL, V_NEWDEPTH, V_WLEN, V_NEMIT, V_ETOT, V_OUTLEN,
   V_TPLPRE, V_TPLSUF, V_TPLK, V_NEXTEV, V_NFULL, V_NTPL, V_CFULL, V_CTPL, V_CLEX, V_NHOLE, V_CHOLE, V_S4W,
-  V_HCLAIM  // hole-template slots this workgroup wrote (bit per slot): one writer per slot
+  V_HCLAIM,  // hole-template slots this workgroup wrote (bit per slot): one writer per slot
+  V_S6W      // the sizing ran on wave 0 right after s4_wave
 };
 
 // LDS byte reader that fetches one aligned 64-bit word per 8 sequential bytes: a byte-serial
@@ -991,6 +992,76 @@ __device__ __forceinline__ int opaque_tid() {
   return t;
 }
 
+// S6 sizing on one wave (the common tile: <= 64 deltas, W <= 2048 bytes): emitted-delta
+// ballot, per-lane chunks of escaped lengths with a DPP scan, each delta's escaped prefix.
+// Called by wave 0 — right after s4_wave when the filter ran on one wave (no barrier between
+// the two), else after the filter's barrier.
+__device__ inline void s6_size_wave(Smem& s, const uint8_t* W, int Wlen, int ndelta) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const int wp = lane < ndelta ? (int)s.wpos[lane] : 0;
+    const int prev = __shfl_up(wp, 1, 64);
+    const bool f = lane < ndelta && wp > (lane ? prev : 0);
+    const uint64_t m = __ballot(f);
+    if (lane < ndelta) s.eidx[lane] = (uint16_t)__popcll(m & below);
+    if (f) s.ejx[__popcll(m & below)] = (uint16_t)lane;
+    const int C = (Wlen + 63) / 64;
+    const int lo = min(lane * C, Wlen), hi = min(lo + C, Wlen);
+    // clean content (printable ASCII without '"' or '\\': every byte escapes to itself) —
+    // escaped offsets are raw offsets, no decode walk: 8 bytes per lane per step (SWAR, the
+    // zero / less-than tricks only err towards "not clean")
+    bool dirty = false;
+    {
+      const uint64_t hb = 0x8080808080808080ull, one = 0x0101010101010101ull;
+      for (int x0 = lane * 8; x0 < Wlen; x0 += 64 * 8) {
+        const int nb = min(8, Wlen - x0);
+        const uint64_t w = lds_window8(W, x0, Wlen), vm = nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1);
+        const uint64_t q = w ^ 0x2222222222222222ull, b = w ^ 0x5c5c5c5c5c5c5c5cull, d = w ^ 0x7f7f7f7f7f7f7f7full;
+        const uint64_t odd = (((q - one) & ~q) | ((b - one) & ~b) | ((d - one) & ~d) | ((w - 0x20 * one) & ~w) | w) & hb;
+        dirty = dirty || (odd & vm) != 0;
+      }
+    }
+    int tot;
+    if (__ballot(dirty) == 0) {
+      tot = Wlen;
+      s.chunk_base[lane] = lo;
+      if (lane < ndelta) s.epos[lane] = (uint32_t)min(wp, Wlen);
+    } else {
+      int x = lo, e = 0;
+      while (x < hi && is_cont(W[x])) ++x;
+      while (x < hi) {
+        uint32_t cp;
+        x += wtf8_decode(W, x, Wlen, &cp);
+        e += escaped_len_cp(cp);
+      }
+      const int incl = wave_incl_sum(e);
+      const int excl = incl - e;
+      tot = __shfl(incl, 63, 64);
+      s.chunk_base[lane] = excl;  // the write phase's escaped-content chunks (64 of them here)
+      // (shuffles with every lane active: a lane's chunk base for its delta's escaped prefix)
+      const int t = (lane < ndelta && wp < Wlen && C > 0) ? wp / C : 0;
+      const int tbase = __shfl(excl, t, 64);
+      if (lane < ndelta) {
+        uint32_t ep = (uint32_t)tot;
+        if (wp < Wlen) {
+          int xx = min(t * C, Wlen), ee = tbase;
+          while (xx < wp && is_cont(W[xx])) ++xx;
+          while (xx < wp) {
+            uint32_t cp;
+            xx += wtf8_decode(W, xx, Wlen, &cp);
+            ee += escaped_len_cp(cp);
+          }
+          ep = (uint32_t)ee;
+        }
+        s.epos[lane] = ep;
+      }
+    }
+  if (lane == 0) {
+    s.v[V_NEMIT] = __popcll(m);
+    s.v[V_ETOT] = tot;
+  }
+}
+
 __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, const uint8_t* __restrict__ in,
                                           uint8_t* __restrict__ out, WorkResult* __restrict__ res,
                                           DevSlot* __restrict__ state, uint8_t* __restrict__ content,
@@ -1045,6 +1116,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     s.v[V_NFULL] = s.v[V_NTPL] = s.v[V_CFULL] = s.v[V_CTPL] = s.v[V_CLEX] = s.v[V_NHOLE] = s.v[V_CHOLE] = 0;
     s.v[V_HCLAIM] = 0;
     s.v[V_S4W] = 0;  // (s4_wave's "no candidates" mark: LDS outlives the previous item)
+    s.v[V_S6W] = 0;
     for (int q = 0; q < BS / 64; ++q) wtpl[q][0] = -1;
     if (fresh) {
       s.v[V_DEPTH0] = 0;
@@ -1741,6 +1813,13 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     if (tid < 64) {
       const bool ok = s4_wave(s, Z, Zn, ndelta, depth0, P, P.dbg != nullptr ? P.dbg + bi * kDbg : nullptr);
       if (tid == 0 && s.v[V_S4W] != 2) s.v[V_S4W] = ok ? 1 : 0;  // (2: no candidates, W = Z)
+      // the sizing on the same wave at once (the filter's own results: no barrier between)
+      wave_fence();
+      const int wl = __builtin_amdgcn_readfirstlane(s.v[V_WLEN]);
+      if (ok && (P.fast & 8) && emit && wl <= 2048) {
+        s6_size_wave(s, s.v[V_S4W] == 2 ? Z : s.A, wl, ndelta);
+        if (tid == 0) s.v[V_S6W] = 1;
+      }
     }
     __syncthreads();
     if (s.v[V_S4W]) {
@@ -1974,74 +2053,13 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   bool s6_wave = false;  // sizing ran on wave 0: 64 escaped-content chunks instead of BS
   const int ndig = it.index >= 100 ? 3 : it.index >= 10 ? 2 : 1;
   const int PRE = P.pre1_len + ndig + P.pre2_len, SUF = P.suf_len, EVL = PRE + SUF;
-  if ((P.fast & 8) && emit && ndelta > 0 && ndelta <= 64 && Wlen <= 2048) {
-    // the common tile on wave 0 alone (as s4_wave): emitted-delta ballot, per-lane chunks of
-    // escaped lengths with a DPP scan, each delta's escaped prefix; one barrier for the block
-    if (tid < 64) {
-      const int lane = tid;
-      const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-      const int wp = lane < ndelta ? (int)s.wpos[lane] : 0;
-      const int prev = __shfl_up(wp, 1, 64);
-      const bool f = lane < ndelta && wp > (lane ? prev : 0);
-      const uint64_t m = __ballot(f);
-      if (lane < ndelta) s.eidx[lane] = (uint16_t)__popcll(m & below);
-      if (f) s.ejx[__popcll(m & below)] = (uint16_t)lane;
-      const int C = (Wlen + 63) / 64;
-      const int lo = min(lane * C, Wlen), hi = min(lo + C, Wlen);
-      // clean content (printable ASCII without '"' or '\\': every byte escapes to itself) —
-      // escaped offsets are raw offsets, no decode walk: 8 bytes per lane per step (SWAR, the
-      // zero / less-than tricks only err towards "not clean")
-      bool dirty = false;
-      {
-        const uint64_t hb = 0x8080808080808080ull, one = 0x0101010101010101ull;
-        for (int x0 = lane * 8; x0 < Wlen; x0 += 64 * 8) {
-          const int nb = min(8, Wlen - x0);
-          const uint64_t w = lds_window8(W, x0, Wlen), vm = nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1);
-          const uint64_t q = w ^ 0x2222222222222222ull, b = w ^ 0x5c5c5c5c5c5c5c5cull, d = w ^ 0x7f7f7f7f7f7f7f7full;
-          const uint64_t odd = (((q - one) & ~q) | ((b - one) & ~b) | ((d - one) & ~d) | ((w - 0x20 * one) & ~w) | w) & hb;
-          dirty = dirty || (odd & vm) != 0;
-        }
-      }
-      int tot;
-      if (__ballot(dirty) == 0) {
-        tot = Wlen;
-        s.chunk_base[lane] = lo;
-        if (lane < ndelta) s.epos[lane] = (uint32_t)min(wp, Wlen);
-      } else {
-        int x = lo, e = 0;
-        while (x < hi && is_cont(W[x])) ++x;
-        while (x < hi) {
-          uint32_t cp;
-          x += wtf8_decode(W, x, Wlen, &cp);
-          e += escaped_len_cp(cp);
-        }
-        const int incl = wave_incl_sum(e);
-        const int excl = incl - e;
-        tot = __shfl(incl, 63, 64);
-        s.chunk_base[lane] = excl;  // the write phase's escaped-content chunks (64 of them here)
-        // (shuffles with every lane active: a lane's chunk base for its delta's escaped prefix)
-        const int t = (lane < ndelta && wp < Wlen && C > 0) ? wp / C : 0;
-        const int tbase = __shfl(excl, t, 64);
-        if (lane < ndelta) {
-          uint32_t ep = (uint32_t)tot;
-          if (wp < Wlen) {
-            int xx = min(t * C, Wlen), ee = tbase;
-            while (xx < wp && is_cont(W[xx])) ++xx;
-            while (xx < wp) {
-              uint32_t cp;
-              xx += wtf8_decode(W, xx, Wlen, &cp);
-              ee += escaped_len_cp(cp);
-            }
-            ep = (uint32_t)ee;
-          }
-          s.epos[lane] = ep;
-        }
-      }
-      if (lane == 0) {
-        s.v[V_NEMIT] = __popcll(m);
-        s.v[V_ETOT] = tot;
-      }
-    }
+  if (s.v[V_S6W]) {  // sized by wave 0 right after the one-wave filter
+    n_emit = s.v[V_NEMIT];
+    etot = s.v[V_ETOT];
+    s6_wave = true;
+  } else if ((P.fast & 8) && emit && ndelta > 0 && ndelta <= 64 && Wlen <= 2048) {
+    // the common tile on wave 0 alone (s6_size_wave), then one barrier for the block
+    if (tid < 64 && !s.v[V_S6W]) s6_size_wave(s, W, Wlen, ndelta);
     __syncthreads();
     n_emit = s.v[V_NEMIT];
     etot = s.v[V_ETOT];
