@@ -1686,14 +1686,19 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   // already has the newest content event, and S3a's writes were published by its barrier
   if (unres_all > 0) __syncthreads();
   QMX_STAMP(22);
-  {  // persist the newest template now: S4 reuses the input tile
+  // persist the newest template now (S4 reuses the input tile) — on waves 4-7: wave 0 goes on
+  // to the content placement (its reads of ev_a / ev_sa / ev_b / ev_sb and of A are not
+  // written before the placement's barrier, which every wave passes after this)
+  if (tid >= BS - TPL_PRE_MAX) {
+    static_assert(TPL_PRE_MAX <= BS && TPL_BYTES / 16 <= TPL_PRE_MAX, "template persist threads");
+    const int pt = tid - (BS - TPL_PRE_MAX);
     const int tk = unres_all > 0 ? s.v[V_TPLK] : newest_all;
     if (tk >= 0) {
       const int e0 = s.ev_a[tk], pre = s.ev_sa[tk] - e0, e1 = s.ev_b[tk], suf = e1 - s.ev_sb[tk];
       DevSlot& ds = state[it.slot];
-      if (tid < pre) ds.tpl[tid] = s.A[e0 + tid];
-      if (tid < suf) ds.tpl[TPL_PRE_MAX + tid] = s.A[e1 - suf + tid];
-      if (tid == 0) {
+      if (pt < pre) ds.tpl[pt] = s.A[e0 + pt];
+      if (pt < suf) ds.tpl[TPL_PRE_MAX + pt] = s.A[e1 - suf + pt];
+      if (pt == 0) {
         ds.tpl_pre = (uint16_t)pre;
         ds.tpl_suf = (uint16_t)suf;
       }
@@ -1702,21 +1707,21 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       // boundary in between).  No claim: a global atomic here cost every item a round trip.
       if (pub) {
         BackendTpl& bw = btpl_wr[it.index];
-        if (tid < pre) bw.tpl[tid] = s.A[e0 + tid];
-        if (tid < suf) bw.tpl[TPL_PRE_MAX + tid] = s.A[e1 - suf + tid];
-        if (tid == 0) {
+        if (pt < pre) bw.tpl[pt] = s.A[e0 + pt];
+        if (pt < suf) bw.tpl[TPL_PRE_MAX + pt] = s.A[e1 - suf + pt];
+        if (pt == 0) {
           bw.pre = (uint16_t)pre;
           bw.suf = (uint16_t)suf;
         }
       }
     } else if (borrow) {  // keep the backend's template as the stream's own
       DevSlot& ds = state[it.slot];
-      if (tid < TPL_BYTES / 16) ((uint4*)ds.tpl)[tid] = ((const uint4*)s.tpl)[tid];
-      if (tid == 0) {
+      if (pt < TPL_BYTES / 16) ((uint4*)ds.tpl)[pt] = ((const uint4*)s.tpl)[pt];
+      if (pt == 0) {
         ds.tpl_pre = (uint16_t)s.v[V_TPLPRE];
         ds.tpl_suf = (uint16_t)s.v[V_TPLSUF];
       }
-    } else if (fresh && tid == 0) {
+    } else if (fresh && pt == 0) {
       state[it.slot].tpl_pre = state[it.slot].tpl_suf = 0;
     }
   }
