@@ -1079,12 +1079,16 @@ def main() -> int:
             rows = [g.cpu().tolist() for g in gathered]
         else:
             rows = [local]
-        ok = all(r[11] == 0 for r in rows)
-        headline_ok = ok
-        if spread is not None:  # a failed spread check fails the run (its responses are validated too)
-            ok = ok and all(r.get("ok") for r in spread)
-        if c3_rows is not None:  # so does an invalid config-3 response (RCCL not forming: degraded)
-            ok = ok and all((r or {}).get("ok") for r in c3_rows)
+        headline_ok = all(r[11] == 0 for r in rows)
+        # the post-timing checks (spread placement, config 3: other configs than the headline's,
+        # each validated response by response) are reported on their own: a failed check is
+        # `checks_ok: false` in the JSON line and a warning, not a lost headline measurement
+        checks_ok = True
+        if spread is not None:
+            checks_ok = checks_ok and all(r.get("ok") for r in spread)
+        if c3_rows is not None:  # (RCCL not forming is "degraded", still ok: finals took the mesh)
+            checks_ok = checks_ok and all((r or {}).get("ok") for r in c3_rows)
+        ok = headline_ok
         # per-rank breakdowns, each scraped from that rank's own proxy (admin port)
         bd_rows = [bd]
         if dist is not None:
@@ -1142,6 +1146,7 @@ def main() -> int:
                 "processes_exited": int(sum(r[7] for r in rows)),
                 "valid": ok,
                 "headline_valid": headline_ok,
+                "checks_ok": checks_ok,
                 "baseline_p50_ttft_ms": sc.get("baseline_ttft_ms"),
                 # rank 0's proxy counters over the timed region (SURVEY §5.1 time breakdown),
                 # scraped from its own admin port
@@ -1160,6 +1165,11 @@ def main() -> int:
         _kill(procs)
         if dist is not None:
             dist.destroy_process_group()
+    if spread is not None or c3_rows is not None:
+        if not checks_ok:
+            print("bench: a post-timing check FAILED (spread placement and/or config 3): see 'spread_check' / "
+                  "'config3' and 'checks_ok' in the JSON line; the headline measurement is unaffected",
+                  file=sys.stderr, flush=True)
     if not ok:
         print("bench: INVALID run (responses failed validation, requests missing, or a server process "
               "exited): see 'invalid' / 'exited' in the JSON line", file=sys.stderr, flush=True)

@@ -99,10 +99,12 @@ def test_bench_two_ranks_spread_check_failure_is_agreed(tmp_path):
                         "--gpus", "2", "--steps", "1", "--warmup", "0", "--batch", "64", "--threads", "2",
                         "--conns", "8", "--port", str(port)],
                        cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
-    # the headline responses were fine, but a failed spread check fails the run
-    assert r.returncode == 1, (r.stdout[-2000:], r.stderr[-3000:])
+    # the headline responses were fine: the run is valid, the failed spread check is reported
+    # on its own (checks_ok false, a warning on stderr) instead of losing the measurement
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert "post-timing check FAILED" in r.stderr
     res = _check(_json_lines(r.stdout)[0], 2, 1, 0)
-    assert res["headline_valid"] is True and res["valid"] is False
+    assert res["headline_valid"] is True and res["valid"] is True and res["checks_ok"] is False
     sc = res["spread_check"]
     assert sc["ok"] is False
     assert "injected" in sc["per_rank"][1]["error"] and "another rank's spread set failed" in sc["per_rank"][0]["error"]
