@@ -12,6 +12,8 @@
 #   smoke                 __graft_entry__.smoke()
 #   bench[=N]             headline bench.py N times (default 1)            -> bench_<i>.json
 #   bench:ARGS            one bench.py run with extra args (commas = spaces) -> bench_<slug>.json
+#   hunt=N                N headline runs that go on past an invalid one; whole invalid bodies
+#                         -> invalid_bodies.txt (QMX_LOADGEN_DUMP)
 #   ab:NAME:ENV:ARGS      one bench.py run under extra env (commas = spaces) -> ab_<NAME>.json
 #   scenarios             aggregate4, highqps8, failure, paced (10 steps each)
 #   reference             the upstream proxy under the same harness (bench.py --impl reference)
