@@ -1131,17 +1131,31 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   // of a new session then matches its content events at once instead of lexing the first
   // ones; a template is only ever a real parsed event's bytes around its content string,
   // and a match re-validates the string, so whose it is never changes a result)
-  const bool own_tpl = !fresh && state[it.slot].tpl_pre != 0;
-  const BackendTpl* bt = (!own_tpl && btpl_rd != nullptr && it.index < (uint32_t)kBackendTpl)
-                             ? &btpl_rd[it.index] : nullptr;
-  const bool borrow = bt != nullptr && bt->pre != 0;
+  // Both candidates' lengths and bytes are requested at once, right after the work item: the
+  // choice (own, else the backend's) is made when they are in registers — one dependent
+  // round trip to device memory instead of three (lengths, then the other lengths, then bytes)
+  const BackendTpl* bt = (btpl_rd != nullptr && it.index < (uint32_t)kBackendTpl) ? &btpl_rd[it.index] : nullptr;
+  uint32_t st_pre = 0, st_suf = 0, b_pre = 0, b_suf = 0;
+  uint4 st_w = make_uint4(0, 0, 0, 0), b_w = make_uint4(0, 0, 0, 0);
+  if (!fresh) {
+    st_pre = state[it.slot].tpl_pre;
+    st_suf = state[it.slot].tpl_suf;
+    if (tid < TPL_BYTES / 16) st_w = ((const uint4*)state[it.slot].tpl)[tid];
+  }
+  if (bt != nullptr) {
+    b_pre = bt->pre;
+    b_suf = bt->suf;
+    if (tid < TPL_BYTES / 16) b_w = ((const uint4*)bt->tpl)[tid];
+  }
+  const bool own_tpl = !fresh && st_pre != 0;
+  const bool borrow = !own_tpl && bt != nullptr && b_pre != 0;
   if (tid == 0) {
-    s.v[V_TPLPRE] = own_tpl ? state[it.slot].tpl_pre : borrow ? bt->pre : 0;
-    s.v[V_TPLSUF] = own_tpl ? state[it.slot].tpl_suf : borrow ? bt->suf : 0;
+    s.v[V_TPLPRE] = own_tpl ? st_pre : borrow ? b_pre : 0;
+    s.v[V_TPLSUF] = own_tpl ? st_suf : borrow ? b_suf : 0;
   }
   if (tid < TPL_BYTES / 16) {
-    if (own_tpl) ((uint4*)s.tpl)[tid] = ((const uint4*)state[it.slot].tpl)[tid];
-    else if (borrow) ((uint4*)s.tpl)[tid] = ((const uint4*)bt->tpl)[tid];
+    if (own_tpl) ((uint4*)s.tpl)[tid] = st_w;
+    else if (borrow) ((uint4*)s.tpl)[tid] = b_w;
   }
   {  // the backend's hole templates (role / content / finish shapes of other streams)
     constexpr int kHW = (int)(sizeof(HoleTpl) * kHoleTpls / 16);
