@@ -166,7 +166,15 @@ struct LdsWords {
 // instead of a ds_bpermute round trip per __shfl_up), then a cross-wave combine in LDS
 // ------------------------------------------------------------------------------------
 #define QMX_DPP(old, v, ctrl, rm) __builtin_amdgcn_update_dpp((old), (v), (ctrl), (rm), 0xf, false)
-enum : int { DPP_SHR1 = 0x111, DPP_SHR2 = 0x112, DPP_SHR4 = 0x114, DPP_SHR8 = 0x118, DPP_BC15 = 0x142, DPP_BC31 = 0x143 };
+enum : int { DPP_SHR1 = 0x111, DPP_SHR2 = 0x112, DPP_SHR4 = 0x114, DPP_SHR8 = 0x118, DPP_BC15 = 0x142, DPP_BC31 = 0x143,
+             DPP_WSHR1 = 0x138 };
+
+// Wave-wide moves without an LDS round trip (HIP's __shfl / __shfl_up are ds_bpermute: an
+// LDS instruction and a wait on a dependent chain).  Every lane of the wave must be active.
+// lane 63's value in every lane (v_readlane into a scalar register)
+__device__ __forceinline__ int wave_last(int x) { return __builtin_amdgcn_readlane(x, 63); }
+// lane - 1's value (DPP wave_shr:1); lane 0 gets `first`
+__device__ __forceinline__ int wave_prev(int x, int first) { return QMX_DPP(first, x, DPP_WSHR1, 0xf); }
 
 __device__ inline int wave_incl_sum(int x) {
   x += QMX_DPP(0, x, DPP_SHR1, 0xf);  // lanes whose source is outside the row / a masked row get 0
@@ -236,10 +244,7 @@ __device__ inline int2 block_excl_pair(int2 v, int2 ident, Op op, int32_t* scr, 
     tot = op(tot, s);
   }
   if (tail_barrier) __syncthreads();
-  int2 ex;
-  ex.x = __shfl_up(x.x, 1, 64);
-  ex.y = __shfl_up(x.y, 1, 64);
-  if (lane == 0) ex = ident;
+  const int2 ex = make_int2(wave_prev(x.x, ident.x), wave_prev(x.y, ident.y));
   *total = tot;
   return op(base, ex);
 }
@@ -657,7 +662,7 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
     int k = nc + incl - cnt;
     for (uint32_t m = lm; m; m &= m - 1, ++k)
       if (k < 64) s.cand[k] = (uint16_t)(x0 + __ffs(m) - 1);
-    nc += __shfl(incl, 63, 64);
+    nc += wave_last(incl);
     if (nc > 63) return false;  // (lane k owns token k AND the gap after it: ntok <= 63)
   }
   if (nc == 0) {
@@ -697,10 +702,7 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
     DepthOp op;
     int2 x = id > 0 ? make_int2(1, 1) : id < 0 ? make_int2(-1, 0) : make_int2(0, 0);
     x = wave_incl_pair(x, op);
-    int2 ex;
-    ex.x = __shfl_up(x.x, 1, 64);
-    ex.y = __shfl_up(x.y, 1, 64);
-    if (lane == 0) ex = make_int2(0, 0);
+    const int2 ex = make_int2(wave_prev(x.x, 0), wave_prev(x.y, 0));
     cpos = lane < nc ? (int)s.cand[lane] : 0;
     ctok = id;
     cplen = id != 0 ? tok_plen(P, id) : 0;
@@ -795,7 +797,7 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
     s.v[V_NEWTAIL] = q;
     s.v[V_NEWDEPTH] = fdep;
   }
-  const int cutN = __shfl(cut, ndelta - 1, 64);
+  const int cutN = __builtin_amdgcn_readlane(cut, max(ndelta - 1, 0));
   if (dbg != nullptr && lane == 0) dbg_put(&dbg[24], __builtin_amdgcn_s_memrealtime());
   // compaction of the kept bytes of [0, cutN) into A, by segments (kept_at's cases): lane k
   // owns the gap before token k (kept at depth 0) and token k itself (kept when it is a
@@ -820,15 +822,17 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
   const int gl = gk ? ge - gs : 0, tl = tk ? te - ts0 : 0;
   const int incl = wave_incl_sum(gl + tl);
   const int ob = incl - gl - tl;  // output offset of this lane's gap (its token follows it)
-  const int out = __shfl(incl, 63, 64);
+  const int out = wave_last(incl);
   for (uint64_t m = __ballot(gl > 0); m; m &= m - 1) {
     const int k = __ffsll((unsigned long long)m) - 1;
-    const int a = __shfl(gs, k, 64), n = __shfl(gl, k, 64), o = __shfl(ob, k, 64);
+    const int a = __builtin_amdgcn_readlane(gs, k), n = __builtin_amdgcn_readlane(gl, k),
+              o = __builtin_amdgcn_readlane(ob, k);
     for (int x = lane; x < n; x += 64) s.A[o + x] = Z[a + x];
   }
   for (uint64_t m = __ballot(tl > 0); m; m &= m - 1) {
     const int k = __ffsll((unsigned long long)m) - 1;
-    const int a = __shfl(ts0, k, 64), n = __shfl(tl, k, 64), o = __shfl(ob, k, 64) + __shfl(gl, k, 64);
+    const int a = __builtin_amdgcn_readlane(ts0, k), n = __builtin_amdgcn_readlane(tl, k),
+              o = __builtin_amdgcn_readlane(ob, k) + __builtin_amdgcn_readlane(gl, k);
     for (int x = lane; x < n; x += 64) s.A[o + x] = Z[a + x];
   }
   // kept bytes before each delta's cut: the segment that holds cut - 1
@@ -928,9 +932,7 @@ __device__ inline void s2_wave(Smem& s, int start, int in_len, bool eof) {
     const bool next_nl = hi < in_len && s.A[hi] == '\n';
     const int2 run = all_nl ? make_int2(1, len) : make_int2(0, trail);
     const int2 incl = wave_incl_pair(run, RunOp());
-    int2 ex;
-    ex.x = __shfl_up(incl.x, 1, 64);
-    ex.y = __shfl_up(incl.y, 1, 64);
+    int2 ex = make_int2(wave_prev(incl.x, 0), wave_prev(incl.y, 0));
     ex = lane == 0 ? carry : RunOp()(carry, ex);
     // separators: "\n" at an even position of its newline run, followed by a "\n"
     auto each_sep = [&](auto&& f) {
@@ -958,10 +960,11 @@ __device__ inline void s2_wave(Smem& s, int start, int in_len, bool eof) {
       if (k + 1 < MAX_EV) s.ev_a[k + 1] = (uint16_t)(p + 2);
       ++k;
     });
-    for (int o = 32; o > 0; o >>= 1) last = max(last, __shfl_xor(last, o, 64));  // a wave max
-    lastsep = max(lastsep, last);
-    kb += __shfl(ci, 63, 64);
-    carry = RunOp()(carry, make_int2(__shfl(incl.x, 63, 64), __shfl(incl.y, 63, 64)));
+    // the pass's last separator: the highest lane that has one (lanes own ascending ranges)
+    const uint64_t lm = __ballot(last >= 0);
+    if (lm != 0) lastsep = __builtin_amdgcn_readlane(last, 63 - __clzll(lm));
+    kb += wave_last(ci);
+    carry = RunOp()(carry, make_int2(wave_last(incl.x), wave_last(incl.y)));
   }
   if (lane == 0) {
     s.ev_a[0] = (uint16_t)start;
@@ -1000,8 +1003,8 @@ __device__ inline void s6_size_wave(Smem& s, const uint8_t* W, int Wlen, int nde
     const int lane = threadIdx.x & 63;
     const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
     const int wp = lane < ndelta ? (int)s.wpos[lane] : 0;
-    const int prev = __shfl_up(wp, 1, 64);
-    const bool f = lane < ndelta && wp > (lane ? prev : 0);
+    const int prev = wave_prev(wp, 0);
+    const bool f = lane < ndelta && wp > prev;
     const uint64_t m = __ballot(f);
     if (lane < ndelta) s.eidx[lane] = (uint16_t)__popcll(m & below);
     if (f) s.ejx[__popcll(m & below)] = (uint16_t)lane;
@@ -1036,7 +1039,7 @@ __device__ inline void s6_size_wave(Smem& s, const uint8_t* W, int Wlen, int nde
       }
       const int incl = wave_incl_sum(e);
       const int excl = incl - e;
-      tot = __shfl(incl, 63, 64);
+      tot = wave_last(incl);
       s.chunk_base[lane] = excl;  // the write phase's escaped-content chunks (64 of them here)
       // (shuffles with every lane active: a lane's chunk base for its delta's escaped prefix)
       const int t = (lane < ndelta && wp < Wlen && C > 0) ? wp / C : 0;
@@ -1766,7 +1769,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
         const bool c = k < nev && k < kab && s.ev_kind[k] == EV_CONTENT;
         const int pk = c ? ((1 << 16) | (int)s.ev_dl[k]) : 0;
         const int incl = wave_incl_sum(pk);
-        tot = __shfl(incl, 63, 64);
+        tot = wave_last(incl);
         if (c) place(k, incl - pk);
         else if (k < nev) s.ev_dl[k] = 0xFFFF;
       }
@@ -1928,10 +1931,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
         DepthOp op;
         int2 x = id > 0 ? make_int2(1, 1) : id < 0 ? make_int2(-1, 0) : make_int2(0, 0);
         x = wave_incl_pair(x, op);
-        int2 ex;
-        ex.x = __shfl_up(x.x, 1, 64);
-        ex.y = __shfl_up(x.y, 1, 64);
-        if (lane == 0) ex = make_int2(0, 0);
+        const int2 ex = make_int2(wave_prev(x.x, 0), wave_prev(x.y, 0));
         if (id != 0) {
           s.tok_pos[k] = s.cand[lane];
           s.tok_id[k] = (int8_t)id;
