@@ -725,33 +725,13 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
   const int npw = 2 * P.ts.n;  // (<= 2 * kMaxTags <= 64 lanes)
   const int pl_l = lane < npw ? pattern_len(P.ts, lane) : 0;
   const uint64_t pw0_l = lane < npw ? P.pw[lane][0] : 0ull, pw1_l = lane < npw ? P.pw[lane][1] : 0ull;
-  auto prefix_r = [&](int q, int e, bool opens_only) -> bool {
-    const int m = e - q;
-    if (m <= 0 || m > kMaxTail) return m <= 0;
-    const int np = opens_only ? P.ts.n : npw;
-    const uint64_t z0 = lower8(lds_window8(Z, q, e)), z1 = m > 8 ? lower8(lds_window8(Z, q + 8, e)) : 0ull;
-    const uint64_t m0 = m >= 8 ? ~0ull : ((1ull << (8 * m)) - 1);
-    const uint64_t m1 = m >= 16 ? ~0ull : m <= 8 ? 0ull : ((1ull << (8 * (m - 8))) - 1);
-    bool found = false;
-    for (int t = 0; t < np; ++t) {  // (uniform bound)
-      const int plen = __builtin_amdgcn_readlane(pl_l, t);
-      const uint64_t a0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pw0_l >> 32), t) << 32) |
-                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pw0_l, t);
-      const uint64_t a1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(pw1_l >> 32), t) << 32) |
-                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)pw1_l, t);
-      bool ok = !found && m <= plen && z0 == (a0 & m0) && (m <= 8 || z1 == (a1 & m1));
-      for (int w = 2; ok && 8 * w < m; ++w) {  // (patterns longer than 16 bytes)
-        const int nb = min(8, m - 8 * w);
-        const uint64_t mw = nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1);
-        ok = lower8(lds_window8(Z, q + 8 * w, e)) == (P.pw[t][w] & mw);
-      }
-      found = found || ok;
-    }
-    return found;
-  };
-  // hold_cut from the candidate registers: the last candidate before e (positions ascend),
-  // its token / length and the depth before it; then the same decisions as hold_cut
-  auto hold_cut_r = [&](int e, bool for_tail, int* q_out) -> int {
+  // hold_cut, wave-wide (every lane calls it; `active` lanes get an answer): the last
+  // candidate before e from the candidate registers (positions ascend), its token / length and
+  // the depth before it; then, for each lane whose candidate could still open a tag, the
+  // tag-prefix test runs lane-parallel over the patterns — lane t tests pattern t against that
+  // lane's window and a ballot answers (a loop over the patterns on each lane, with v_readlane
+  // of every pattern word, cost ~1.4 us per headline tile); then the same decisions as hold_cut
+  auto hold_cut_w = [&](int e, bool active, bool for_tail, int* q_out) -> int {
     int q = -1, tk = 0, pl = 0, dq = 0;
     for (int k = 0; k < nc; ++k) {  // (uniform bound, nc <= 63)
       const int ck = __builtin_amdgcn_readlane(cpos, k), tkk = __builtin_amdgcn_readlane(ctok, k);
@@ -762,10 +742,28 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
       pl = b ? plk : pl;
       dq = b ? dqk : dq;
     }
+    // (q < e, so the window is never empty; longer than kMaxTail bytes it is no tag prefix)
+    const bool need = active && q >= 0 && !(tk != 0 && q + pl <= e) && e - q <= kMaxTail;
+    bool pref = false;
+    for (uint64_t bm = __ballot(need); bm; bm &= bm - 1) {
+      const int j = __ffsll((unsigned long long)bm) - 1;
+      const int qj = __builtin_amdgcn_readlane(q, j), m = __builtin_amdgcn_readlane(e, j) - qj;
+      const int np = __builtin_amdgcn_readlane(dq, j) == 0 ? P.ts.n : npw;  // (opens only at depth 0)
+      const uint64_t z0 = lower8(lds_window8(Z, qj, qj + m)), z1 = m > 8 ? lower8(lds_window8(Z, qj + 8, qj + m)) : 0ull;
+      const uint64_t m0 = m >= 8 ? ~0ull : ((1ull << (8 * m)) - 1);
+      const uint64_t m1 = m >= 16 ? ~0ull : m <= 8 ? 0ull : ((1ull << (8 * (m - 8))) - 1);
+      bool ok = lane < np && m <= pl_l && z0 == (pw0_l & m0) && (m <= 8 || z1 == (pw1_l & m1));
+      for (int w = 2; 8 * w < m; ++w) {  // (uniform: windows longer than 16 bytes)
+        const int nb = min(8, m - 8 * w);
+        const uint64_t mw = nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1);
+        const uint64_t zw = lower8(lds_window8(Z, qj + 8 * w, qj + m));
+        if (ok) ok = zw == (P.pw[lane][w] & mw);
+      }
+      const bool f = __ballot(ok) != 0;
+      if (lane == j) pref = f;
+    }
     *q_out = -1;
-    if (q < 0) return e;
-    if (tk != 0 && q + pl <= e) return e;  // completed token
-    if (!prefix_r(q, e, dq == 0)) return e;
+    if (!need || !pref) return e;  // no candidate, a completed token, or no tag prefix
     if (dq == 0 || for_tail) {
       *q_out = q;
       return dq == 0 ? q : e;
@@ -775,27 +773,29 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
   wave_fence();
   const int ntok = __builtin_amdgcn_readfirstlane(s.v[V_NTOK]);
   if (dbg != nullptr && lane == 0) dbg_put(&dbg[25], __builtin_amdgcn_s_memrealtime());
-  // a cut per delta (lane j) and the new holdback tail (lane ndelta, in the same pass: the
-  // searches are chains of dependent LDS reads, so a second pass would double their latency)
+  // a cut per delta (lane j) and the new holdback tail (lane ndelta, in the same pass)
   int cut = 0;
   const bool tail_here = ndelta < 64;  // a free lane for the tail: lane ndelta
-  if (lane < ndelta || (tail_here && lane == ndelta)) {
-    const bool is_tail = lane == ndelta;
+  {
+    const bool is_tail = tail_here && lane == ndelta;
+    const int e = is_tail ? Zn : lane < ndelta ? (int)s.dl_end[lane] : 0;
     int q;
-    const int c = hold_cut_r(is_tail ? Zn : (int)s.dl_end[lane], is_tail, &q);
+    const int c = hold_cut_w(e, lane < ndelta || is_tail, is_tail, &q);
     if (is_tail) {
       s.v[V_NEWTAIL] = q;
       s.v[V_NEWDEPTH] = fdep;
-    } else {
+    } else if (lane < ndelta) {
       cut = c;
       s.cut[lane] = (uint16_t)cut;
     }
   }
-  if (!tail_here && lane == 0) {  // 64 deltas: the tail after them, on lane 0
+  if (!tail_here) {  // 64 deltas: the tail after them, on lane 0
     int q;
-    hold_cut_r(Zn, true, &q);
-    s.v[V_NEWTAIL] = q;
-    s.v[V_NEWDEPTH] = fdep;
+    hold_cut_w(Zn, lane == 0, true, &q);
+    if (lane == 0) {
+      s.v[V_NEWTAIL] = q;
+      s.v[V_NEWDEPTH] = fdep;
+    }
   }
   const int cutN = __builtin_amdgcn_readlane(cut, max(ndelta - 1, 0));
   if (dbg != nullptr && lane == 0) dbg_put(&dbg[24], __builtin_amdgcn_s_memrealtime());

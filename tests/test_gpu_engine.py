@@ -487,6 +487,34 @@ DONE_LIKE = [b"data: [DONE]", b"data: [DONX]", b"data: {DONE}", b"data:  [DONE",
              b"data:[DONE] ", b"data: [DONE] ", b"data:[DONE]", b'data: "DONE"', b"data: [DON\xc3\x89]", b"data: 123456"]
 
 
+LONG_TAGS = ["extended_reasoning_block", "a_very_long_reasoning_tag_name_for_tests"]  # 24 / 40 bytes
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_hip_long_tag_holdback_matches_cpu(ext, seed):
+    """Streamed think filter with tags longer than 16 bytes, their openings and closings cut
+    at random offsets across events and ticks: held-back tails longer than the two pattern
+    words the one-wave filter keeps in registers (the tag-prefix test reads the further words),
+    so the streamed deltas, flags and final content equal the CPU engine's."""
+    rng = random.Random(3100 + seed)
+    tags = ["think"] + LONG_TAGS
+    pieces = ["<think>", "</think>", "x", " word", "<", "</", "é", "<ext", "</a_very"]
+    for t in LONG_TAGS:
+        pieces += [f"<{t}>", f"</{t}>", f"<{t.upper()}>", f"<{t[:20]}", f"</{t[:30]}"]
+    streams = []
+    for _ in range(24):
+        txt = "".join(rng.choice(pieces) for _ in range(rng.randint(4, 30)))
+        cuts = sorted(rng.sample(range(1, len(txt)), min(len(txt) - 1, rng.randint(1, 14))))
+        body = b"".join(H.event_bytes(rng, txt[a:b]) for a, b in zip([0] + cuts, cuts + [len(txt)]))
+        streams.append(H.split_random(rng, body, rng.choice([60, 500, 5000])))
+    n = len(streams)
+    c = H.run_engine(NativeEngine("cpu", tags), streams, [True] * n, [True] * n, random.Random(5))
+    g = H.run_engine(_hip(tags), streams, [True] * n, [True] * n, random.Random(5))
+    for i in range(n):
+        assert c[0][i] == g[0][i], i
+    assert c[1:] == g[1:]
+
+
 def test_hip_done_and_twelve_byte_events(ext, monkeypatch):
     """S3a resolves an exact ``data: [DONE]`` event itself; every other event of that length
     (and the spellings the full parse strips to [DONE]) must come out as the CPU engine has
