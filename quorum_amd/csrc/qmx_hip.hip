@@ -694,10 +694,11 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
   // tokens and the depth before each (candidates in order, non-tokens the scan identity);
   // candidate lane c also keeps, in registers, its position, token id / length and the depth
   // before it — the holdback cuts below read them with v_readlane, not LDS searches
-  int cpos = 0, ctok = 0, cplen = 0, cdep = 0, fdep;
+  int cpos = 0, ctok = 0, cplen = 0, cdep = 0, fdep, ntok;
   {
     const int id = lane < nc ? (int)s.cand_tok[lane] : 0;
     const uint64_t m = __ballot(id != 0);
+    ntok = __popcll(m);  // (from the ballot: no LDS round trip through V_NTOK)
     const int k = __popcll(m & below);
     DepthOp op;
     int2 x = id > 0 ? make_int2(1, 1) : id < 0 ? make_int2(-1, 0) : make_int2(0, 0);
@@ -715,9 +716,8 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
       s.tok_dep[k] = (int16_t)cdep;
     }
     if (lane == 63) {
-      const int nt = __popcll(m);
-      s.v[V_NTOK] = nt;
-      s.tok_dep[nt] = (int16_t)fdep;
+      s.v[V_NTOK] = ntok;
+      s.tok_dep[ntok] = (int16_t)fdep;
     }
   }
   // pattern_prefix_w from registers: lane t holds pattern t's length and first two 8-byte
@@ -771,7 +771,6 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
     return e;
   };
   wave_fence();
-  const int ntok = __builtin_amdgcn_readfirstlane(s.v[V_NTOK]);
   if (dbg != nullptr && lane == 0) dbg_put(&dbg[25], __builtin_amdgcn_s_memrealtime());
   // a cut per delta (lane j) and the new holdback tail (lane ndelta, in the same pass)
   int cut = 0;
