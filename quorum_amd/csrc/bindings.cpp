@@ -503,4 +503,5 @@ PYBIND11_MODULE(_qmx, m) {
          py::arg("ndoors") = 1, py::keep_alive<1, 8>());
   bind_engine(he);
   he.def("kernel_stats", &HipEngine::kernel_stats);
+  he.def("debug_poison_results", &HipEngine::debug_poison_results, py::arg("ahead") = 1);
 }

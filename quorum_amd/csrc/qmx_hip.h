@@ -366,6 +366,7 @@ class HipEngine : public HostEngine {
   int poll_us_ = 1;   // QMX_POLL_US: poll period once the expected kernel time has passed (MI355X A/Bs: 2 beats 6, 1 beats 2)
   bool persistent_ = true;   // a long-lived grid per lane, ticks posted by doorbell (QMX_PERSISTENT=0: a launch per tick)
   bool views_ = true;         // QMX_VIEWS=0: results copy their SSE bytes on the lane thread
+  bool keep_stale_records_ = false;  // QMX_DEBUG_STALE_RECORDS: no record clearing before a post (test control)
   bool stage_timing_ = false;  // QMX_STAGE_TIMING: per-item stage stamps (tools/kbench.py)
   int p_grid_ = 64;          // QMX_PERSISTENT_WG: workgroups per lane grid (1 per CU: 256 VGPRs)
   int p_idle_ms_ = 50;       // the grid exits after this long without a tick
@@ -377,6 +378,12 @@ class HipEngine : public HostEngine {
  public:
   bool persistent() const { return persistent_; }
   void set_persistent(bool on);
+  // Test hook: fill every result record of every buffer set (and the finalize records) as
+  // pinned pages recycled from an earlier engine would be — records that claim the sequence
+  // number of the `ahead`-th next post with done/empty results.  An engine that trusted its
+  // records' initial contents would complete that tick at once with wrong results
+  // (tests/test_gpu_engine.py::test_hip_stale_result_records).  Call with no tick in flight.
+  void debug_poison_results(int ahead);
 };
 
 }  // namespace qmx

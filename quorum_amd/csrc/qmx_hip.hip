@@ -3073,6 +3073,7 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
   if (const char* gs = env_get("QMX_GPU_SHARERS")) persistent_ = atoi(gs) <= 1;
   if (const char* pe = env_get("QMX_PERSISTENT")) persistent_ = atoi(pe) != 0;
   if (const char* va = env_get("QMX_VIEWS")) views_ = atoi(va) != 0;
+  keep_stale_records_ = env_get("QMX_DEBUG_STALE_RECORDS") != nullptr;
   stage_timing_ = env_get("QMX_STAGE_TIMING") != nullptr;  // read once: getenv scans the environment
   if (const char* pw = env_get("QMX_PERSISTENT_WG")) p_grid_ = std::min(std::max(8, atoi(pw)), 1024);
   if (const char* pi = env_get("QMX_PERSISTENT_IDLE_MS")) p_idle_ms_ = std::min(std::max(5, atoi(pi)), 1000);
@@ -3166,6 +3167,7 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
       B.items_cap = 1024;
       HIP_CHECK(hipHostMalloc((void**)&B.h_items, sizeof(WorkItem) * B.items_cap, hipHostMallocMapped));
       HIP_CHECK(hipHostMalloc((void**)&B.h_res, sizeof(WorkResult) * B.items_cap, hipHostMallocMapped));
+      std::memset((void*)B.h_res, 0, sizeof(WorkResult) * B.items_cap);  // (pages may be recycled)
     }
     for (int a = 0; a < 3; ++a) L->outs.push_back(new TickLane::OutArena());
     ensure_out(*L, arena0);
@@ -3238,6 +3240,29 @@ void HipEngine::set_persistent(bool on) {
       stop_persistent(*L);
     }
   persistent_ = on;
+}
+
+void HipEngine::debug_poison_results(int ahead) {
+  for (auto& Lp : lanes_) {
+    TickLane& L = *Lp;
+    std::lock_guard<std::mutex> lg(L.mu);
+    // a sequence number a coming post will use: door 0's counter (loop ticks: an idle
+    // engine's next post goes to its first door) or the lane's own
+    uint32_t s = (grid_ ? grid_->door(door_)->posted : L.seq) + (uint32_t)std::max(1, ahead);
+    if (s == 0) s = 1;
+    for (TickLane::Buf& B : L.bufs)
+      for (size_t i = 0; i < B.items_cap; ++i) {
+        WorkResult r{};
+        r.status = WS_DONE;  // "done, nothing consumed, no output"
+        r.seq = s;
+        B.h_res[i] = r;
+      }
+    for (size_t i = 0; i < L.finres_cap; ++i) {
+      FinResult r{};
+      r.seq = s;
+      L.h_finres[i] = r;
+    }
+  }
 }
 
 uint32_t HipEngine::next_seq(TickLane& L) {
@@ -3473,6 +3498,7 @@ void HipEngine::prepare(HipJob& J) {
     B.items_cap = work.size() * 2;
     HIP_CHECK(hipHostMalloc((void**)&B.h_items, sizeof(WorkItem) * B.items_cap, hipHostMallocMapped));
     HIP_CHECK(hipHostMalloc((void**)&B.h_res, sizeof(WorkResult) * B.items_cap, hipHostMallocMapped));
+    std::memset((void*)B.h_res, 0, sizeof(WorkResult) * B.items_cap);  // (pages may be recycled)
   }
   size_t in_off = 0, in_bytes = 0, out_off = 0;
   uint32_t pub_mask = 0;  // backend indices with a publishing item in this tick
@@ -3544,6 +3570,19 @@ void HipEngine::prepare(HipJob& J) {
   // finalize requests ride the same launch: workgroups [n, n + m)
   J.fin_gpu = prep_finalize(L, *J.fin, J.fin_host);
   J.m = (int)J.fin_gpu.size();
+  // Completion is "record i holds this tick's sequence number", so no record may hold it
+  // before this tick's kernel writes it.  Sequence numbers restart with every engine, and
+  // pinned host pages freed by an earlier engine in the same process come back from
+  // hipHostMalloc with its records in them: a record left at seq v completed tick v of the
+  // new engine the moment it was posted (stale consumed / out_len / status, output bytes the
+  // kernel was still writing).  That is how backend 1's delta came out labelled
+  // chatcmpl-parallel-0 once (profiles/r4/q).  Every record this tick will publish is cleared
+  // first; the buffer set and the finalize arenas are this job's alone until complete().
+  // (QMX_DEBUG_STALE_RECORDS=1 skips it: the negative control of the stale-record tests)
+  if (!keep_stale_records_) {
+    for (int i = 0; i < n; ++i) __atomic_store_n(&B.h_res[i].seq, 0u, __ATOMIC_RELAXED);
+    for (int i = 0; i < J.m; ++i) __atomic_store_n(&L.h_finres[i].seq, 0u, __ATOMIC_RELAXED);
+  }
   if (n + J.m > 0) {
     if (J.created != L.params_created) {  // envelopes carry the second: rebuilt + uploaded once a second
       build_params(L, J.created);
@@ -3949,6 +3988,7 @@ static void grow_mapped(HipEngine* e, T** p, size_t* cap, size_t need, void (Hip
   if (*p) (e->*retire)(*p);
   *cap = std::max(need, *cap * 2);
   HIP_CHECK(hipHostMalloc((void**)p, sizeof(T) * *cap + 64, hipHostMallocMapped));
+  std::memset((void*)*p, 0, sizeof(T) * *cap + 64);  // (pinned pages may come back recycled)
 }
 static void grow_device(HipEngine* e, uint8_t** p, size_t* cap, size_t need, void (HipEngine::*retire)(void*)) {
   if (need <= *cap) return;

@@ -483,6 +483,17 @@ class Verifier {
     std::lock_guard<std::mutex> g(mu_);
     auto it = map_.find(slot);
     if (it == map_.end()) return;
+    if (!it->second.compared && !it->second.acc[0].empty()) {
+      // released before both sides terminated (a failed sibling backend's slot, a client that
+      // left): what the primary emitted must still be a prefix of the oracle's output for the
+      // same feeds — a spurious event on a stream that never terminates is caught here
+      drain_locked(last_created_);
+      Track& t = map_[slot];
+      const std::string a0 = norm(t.acc[0]), a1 = norm(t.acc[1]);
+      c_verify_checked++;
+      if (a1.compare(0, a0.size(), a0) != 0) report("released stream", slot, t.acc[0], t.acc[1]);
+      it = map_.find(slot);
+    }
     rmap_.erase(it->second.shadow);
     cpu_.release(it->second.shadow);
     map_.erase(it);
@@ -505,16 +516,8 @@ class Verifier {
     }
     fin_[cpu_.submit_finalize(sh, strip, texts, joiner, created)] = fid;
   }
-  // tick thread, right after the primary engine's tick(created)
-  void check(int64_t created, const std::vector<SlotResult>& r, const std::vector<FinalizeRes>& f) {
-    std::lock_guard<std::mutex> g(mu_);
-    for (auto& x : r) {
-      auto it = map_.find(x.slot);
-      if (it == map_.end() || it->second.gen != x.gen) continue;  // stale: slot re-opened
-      it->second.acc[0].append(x.data(), x.size());
-      it->second.term[0] |= x.flags & (RF_DONE | RF_ABORTED);
-    }
-    for (auto& x : f) pfin_[x.id] = x;
+  // the oracle ticked until it has nothing left: its outputs appended to the tracks
+  void drain_locked(int64_t created, std::vector<FinalizeRes>* sf_out = nullptr) {
     std::vector<SlotResult> sr;
     std::vector<FinalizeRes> sf;
     for (int k = 0; k < 64 && cpu_.has_work(); ++k) cpu_.tick(created, sr, sf);
@@ -525,6 +528,25 @@ class Verifier {
       t.acc[1].append(x.data(), x.size());
       t.term[1] |= x.flags & (RF_DONE | RF_ABORTED);
     }
+    if (sf_out) {
+      for (auto& x : sf) sf_out->push_back(std::move(x));
+    } else {
+      for (auto& x : sf) pending_sf_.push_back(std::move(x));
+    }
+  }
+  // tick thread, right after the primary engine's tick(created)
+  void check(int64_t created, const std::vector<SlotResult>& r, const std::vector<FinalizeRes>& f) {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& x : r) {
+      auto it = map_.find(x.slot);
+      if (it == map_.end() || it->second.gen != x.gen) continue;  // stale: slot re-opened
+      it->second.acc[0].append(x.data(), x.size());
+      it->second.term[0] |= x.flags & (RF_DONE | RF_ABORTED);
+    }
+    for (auto& x : f) pfin_[x.id] = x;
+    last_created_ = created;
+    std::vector<FinalizeRes> sf;
+    drain_locked(created, &sf);
     for (auto& kv : map_) {
       Track& t = kv.second;
       if (t.compared || !t.term[0] || !t.term[1]) continue;
@@ -532,6 +554,8 @@ class Verifier {
       c_verify_checked++;
       if (t.term[0] != t.term[1] || norm(t.acc[0]) != norm(t.acc[1])) report("stream", kv.first, t.acc[0], t.acc[1]);
     }
+    for (auto& x : pending_sf_) sf.push_back(std::move(x));
+    pending_sf_.clear();
     for (auto& x : sf) {
       auto it = fin_.find(x.id);
       if (it == fin_.end()) continue;
@@ -584,6 +608,8 @@ class Verifier {
   }
   std::mutex mu_;
   CpuEngine cpu_;
+  int64_t last_created_ = 0;
+  std::vector<FinalizeRes> pending_sf_;  // oracle finalize results drained by a release
   std::unordered_map<int, Track> map_;
   std::unordered_map<int, int> rmap_, fin_;
   std::unordered_map<int, FinalizeRes> pfin_, sfin_;

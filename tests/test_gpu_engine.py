@@ -278,6 +278,55 @@ def test_hip_finalize_long_texts_many_texts_on_gpu(ext, seed):
         assert st["fin_separate_launches"] == 0, st  # finalize rides the tick launch
 
 
+class _Poisoned:
+    """An engine whose result records are refilled before every tick with the sequence number
+    that tick will publish (done, nothing consumed, no output) — what pinned pages recycled
+    from an earlier engine in the same process hold.  Completion must still come from this
+    tick's own kernel writes."""
+
+    def __init__(self, eng):
+        self._eng = eng
+
+    def __getattr__(self, k):
+        return getattr(self._eng, k)
+
+    def tick(self, created):
+        self._eng._e.debug_poison_results(1)
+        return self._eng.tick(created)
+
+
+@pytest.mark.parametrize("control", [False, True])
+@pytest.mark.parametrize("persistent", ["1", "0"])
+def test_hip_stale_result_records(ext, monkeypatch, persistent, control):
+    """Root cause of the one mislabelled delta of profiles/r4/q (backend 1's text under
+    chatcmpl-parallel-0, lanes mode): sequence numbers restart with every engine, and a new
+    engine's hipHostMalloc'd result records could hold a freed engine's records, so a record
+    already equal to a new tick's number "completed" it at post time.  prepare() now clears
+    every record the tick publishes.  control: the clearing switched off
+    (QMX_DEBUG_STALE_RECORDS, the code before the fix) — the results must then differ, so
+    the poison reproduces the failure on demand, in one-shot and persistent launches."""
+    monkeypatch.setenv("QMX_PERSISTENT", persistent)
+    if control:
+        monkeypatch.setenv("QMX_DEBUG_STALE_RECORDS", "1")
+    differ = 0
+    for seed in (31, 32, 33):
+        rng = random.Random(seed)
+        tags = ["think", "reason"]
+        raw = [H.rand_stream(rng) for _ in range(6)]
+        streams = [H.split_random(rng, r, rng.choice([17, 64, 400])) for r in raw]
+        n = len(streams)
+        cpu = H.run_engine(NativeEngine("cpu", tags), streams, [True] * n, [True] * n, random.Random(seed))
+        eng = _hip(tags)
+        hip = H.run_engine(_Poisoned(eng), streams, [True] * n, [True] * n, random.Random(seed))
+        if control:
+            differ += hip != cpu
+            continue
+        assert hip == cpu, seed
+        _gpu_did_it(eng)
+    if control:
+        assert differ == 3, differ
+
+
 def test_hip_engine_stats(ext):
     eng = _hip(["think"])
     slot = eng.open(0, True, True)

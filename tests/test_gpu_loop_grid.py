@@ -112,6 +112,40 @@ def test_grid_idle_stop_and_relaunch(ext):
     grid.stop()
 
 
+@pytest.mark.parametrize("control", [False, True])
+def test_grid_stale_result_records(ext, monkeypatch, control):
+    """A door engine's result records refilled before every tick with the sequence number the
+    door's next post uses (a freed engine's recycled pinned pages): results still equal the
+    CPU engine's, because every record a tick publishes is cleared before the post
+    (tests/test_gpu_engine.py::test_hip_stale_result_records has the story).  control: the
+    clearing switched off (QMX_DEBUG_STALE_RECORDS) — every case then goes wrong."""
+    if control:
+        monkeypatch.setenv("QMX_DEBUG_STALE_RECORDS", "1")
+    grid = ext.HipGrid(0, 2, 4)
+    tags = ["think", "reason", "reasoning", "thought"]
+    eng = NativeEngine("hip", tags, device=0, max_slots=256, grid=grid, door=0, ndoors=2)
+
+    class Poisoned:
+        def __getattr__(self, k):
+            return getattr(eng, k)
+
+        def tick(self, created):
+            eng._e.debug_poison_results(1)
+            return eng.tick(created)
+
+    differ = 0
+    for seed in range(40, 44):
+        tags_, streams, filt, emit, tseed = _case(seed)
+        cpu = H.run_engine(NativeEngine("cpu", tags_), streams, filt, emit, random.Random(tseed))
+        got = H.run_engine(Poisoned(), streams, filt, emit, random.Random(tseed))
+        differ += got != cpu
+        if not control:
+            assert got == cpu, seed
+    grid.stop()
+    if control:
+        assert differ == 4, differ
+
+
 def test_grid_small_tiles_and_overflow(ext):
     grid = ext.HipGrid(0, 2, 4)
     for seed in range(6):
