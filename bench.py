@@ -70,6 +70,20 @@ SCENARIOS = {
     # steady-state serving shape: backends pace their events (10 ms apart, like a decoding
     # LLM), many concurrent sessions, each tick sees a few events of many streams.  TTFT is
     # bounded below by the mock's own first-content time (5 events x 10 ms = 50 ms).
+    # BASELINE config 1: 1 mock backend, non-streaming, the C++ CPU engine (no GPU work: one
+    # valid backend is quorum's passthrough, oai_proxy.py:1130-1137, 1356-1380 — the upstream
+    # JSON plus "backend": name; the load generator checks message content, usage and that key)
+    "nonstream1": dict(n=1, strategy="concatenate", hide_final=False, skip=False, faults={}, timeout=30,
+                       stream=False, engine="cpu", baseline=19.5, baseline_ttft_ms=811.0,
+                       baseline_source=BASELINE_SOURCE_SURVEY,
+                       desc="1 mock backend, non-streaming concatenate (passthrough), CPU engine"),
+    # the harness alone: the load generator straight against one mock backend, no proxy, same
+    # validation (every content byte of the mock's stream) — SURVEY §6 row 1 / §7.4 item 4.
+    # Every other scenario also measures this after its timed region (harness_ceiling).
+    "direct": dict(n=1, strategy="concatenate", hide_final=False, skip=True, faults={}, timeout=30, direct=True,
+                   batch=131072, baseline=319.0, baseline_ttft_ms=18.9, baseline_source="direct mock backend under the "
+                   "survey's Python harness (SURVEY §6 row 1: the harness ceiling there)",
+                   desc="harness ceiling: load generator -> 1 mock backend, no proxy"),
     "paced": dict(n=2, strategy="concatenate", hide_final=False, skip=True, faults={}, timeout=30,
                   mock_args=["--delay-us", "10000"], conns=1024, baseline=None,
                   desc="2 mock backends pacing events 10 ms apart (first content at 50 ms), 1024 sessions "
@@ -216,6 +230,21 @@ def mock_expected(bin_dir) -> dict:
 def expect_spec(path: str, sc: dict, skip_final: bool, exp: dict, path_prefix: str = "chatcmpl-parallel") -> None:
     """Write qmx_loadgen's --expect file for a scenario: the exact event contract every
     response must satisfy (role first, [DONE] last, per-backend content, final event)."""
+    if sc.get("direct"):  # the mock's own stream: every content byte, its role / stop events skipped
+        lines = ["role 0", "done 1", "empty allowed", f"stream chatcmpl-mock exact {exp['raw_text'].encode().hex()}",
+                 "final absent", "error absent"]
+        with open(path, "w") as f:
+            f.write("\n".join(lines) + "\n")
+        return
+    if not sc.get("stream", True):
+        if sc["n"] != 1:
+            raise ValueError("non-streaming bench scenarios are single-backend (passthrough)")
+        u = exp["usage"]
+        lines = ["json 1", f"message {exp['message'].encode().hex()}", f"usage {u[0]} {u[1]} {u[2]}",
+                 f"field backend {'LLM1'.encode().hex()}"]
+        with open(path, "w") as f:
+            f.write("\n".join(lines) + "\n")
+        return
     sep = "\n" + "\n-------------\n"  # streaming final joiner: "\n" + separator (oai_proxy.py:834-841)
     text = exp["stream_text"]
     faulty = set(sc["faults"])
@@ -238,10 +267,10 @@ def expect_spec(path: str, sc: dict, skip_final: bool, exp: dict, path_prefix: s
         f.write("\n".join(lines) + "\n")
 
 
-def loadgen(bin_dir, port, conns, requests, threads, timeout, expect=None, path="/v1/chat/completions"):
+def loadgen(bin_dir, port, conns, requests, threads, timeout, expect=None, path="/v1/chat/completions", stream=True):
     cmd = [os.path.join(bin_dir, "qmx_loadgen"), "--port", str(port), "--conns", str(conns),
            "--requests", str(requests), "--threads", str(threads), "--timeout", str(timeout),
-           "--path", path]
+           "--path", path, "--stream", "1" if stream else "0"]
     if expect:
         cmd += ["--expect", expect]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout + 60)
@@ -250,6 +279,39 @@ def loadgen(bin_dir, port, conns, requests, threads, timeout, expect=None, path=
     if out.stderr.strip():
         print(out.stderr.strip()[-3000:], file=sys.stderr, flush=True)  # the first invalid responses
     return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def wait_port(host: str, port: int, timeout: float) -> bool:
+    """A TCP listener answers on host:port (the direct check's mock: no /health route)."""
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        try:
+            with socket.create_connection((host, port), timeout=1):
+                return True
+        except OSError:
+            time.sleep(0.05)
+    return False
+
+
+def harness_ceiling(bin_dir, mock_port, args, mock_proc, tmp) -> dict:
+    """The load generator straight against one mock backend for ``args.ceiling`` seconds, with
+    the bench's connections, threads and validation (every content byte of the mock's stream):
+    what the harness alone sustains on this box, next to the proxied number."""
+    import resource
+
+    spec = os.path.join(tmp, "expect_direct.txt")
+    expect_spec(spec, SCENARIOS["direct"], True, mock_expected(bin_dir))
+    ru0 = resource.getrusage(resource.RUSAGE_CHILDREN)
+    m0 = cpu_seconds(mock_proc.pid)
+    st = loadgen(bin_dir, mock_port, args.conns, 10**9, args.lg_threads, args.ceiling, spec)
+    ru1 = resource.getrusage(resource.RUSAGE_CHILDREN)
+    el = max(st["elapsed_s"], 1e-9)
+    return {"req_s": round(st["completed"] / el, 1), "seconds": round(el, 3), "completed": st["completed"],
+            "invalid": st["invalid"], "errors": st["errors"] + st["non200"], "p50_ttft_ms": st["ttft_p50_ms"],
+            "cores_busy": {"loadgen": round((ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime) / el, 2),
+                           "mock": round((cpu_seconds(mock_proc.pid) - m0) / el, 2)},
+            "what": "qmx_loadgen -> mock 0 directly (no proxy), same conns / threads / validation; a proxied "
+                    "request of the scenario costs the mocks one stream per backend"}
 
 
 def exit_status(p) -> dict:
@@ -877,6 +939,9 @@ def main() -> int:
                     help="N > 1: after the timed steps, validate spread placement (RCCL finals) end to end")
     ap.add_argument("--placement", default="local", choices=["local", "spread"],
                     help="spread: a session's backend streams run on consecutive ranks (RCCL exchange)")
+    ap.add_argument("--ceiling", type=float, default=2.0,
+                    help="seconds of the harness-ceiling check after the timed region (the load generator straight "
+                         "against one mock, no proxy: harness_ceiling_req_s); 0 skips it")
     ap.add_argument("--eager-bytes", type=int, default=-1,
                     help="spread: final texts up to this size ride the mesh behind their deltas (-1: the "
                          "production default, 4 KiB); 0 sends every remote final text through a bulk round "
@@ -933,8 +998,10 @@ def main() -> int:
     except (OSError, RuntimeError, ValueError, AttributeError) as e:  # placement is an optimisation only
         pinning = {"pinned": False, "error": repr(e)}
     engine = args.engine
-    if engine == "auto":
-        engine = "hip" if n_dev else "cpu"
+    if engine == "auto":  # BASELINE config 1 is the CPU plumbing path; the rest run on the GPU
+        engine = sc.get("engine") or ("hip" if n_dev else "cpu")
+    direct = bool(sc.get("direct"))
+    stream = bool(sc.get("stream", True))
 
     from quorum_amd.ops import build as qbuild
 
@@ -980,7 +1047,10 @@ def main() -> int:
         # file says when it listens, and /metrics is scraped there — never through the shared
         # port, where any rank's proxy may answer
         admin_port = args.port + ADMIN_OFF + rank
-        if args.impl == "reference":
+        if direct:  # no proxy: the load generator talks to the mock itself
+            proxy_port = mock_ports[0]
+            proxy_procs = []
+        elif args.impl == "reference":
             proxy_port = args.port + rank  # uvicorn binds without SO_REUSEPORT: a port per rank
             proxy_procs = [spawn_reference(args.ref_root, tmp, cfg_path, proxy_port)]
             admin_port = proxy_port
@@ -993,7 +1063,9 @@ def main() -> int:
                 p.ready_file = f"{env['QMX_READY_FILE']}.{p.pid}"
         procs += proxy_procs
         _trace("workers spawned")
-        if args.impl == "reference":
+        if direct:
+            up = wait_port("127.0.0.1", proxy_port, 30)
+        elif args.impl == "reference":
             up = wait_healthy("127.0.0.1", proxy_port, 180)
         else:
             up = wait_ready(proxy_procs, 180)
@@ -1013,11 +1085,11 @@ def main() -> int:
         if dist is not None:
             _barrier(dist, coll_cuda)
         # the reference has no /v1 prefix (oai_proxy.py:959); qmx serves both
-        path = "/chat/completions" if args.impl == "reference" else "/v1/chat/completions"
+        path = "/chat/completions" if args.impl == "reference" and not direct else "/v1/chat/completions"
         warm = {}
         if args.warmup > 0:
             warm = loadgen(bin_dir, proxy_port, args.conns, args.warmup * args.batch, args.lg_threads, args.timeout,
-                           spec_path, path)
+                           spec_path, path, stream)
 
         def casualties():
             return [dict(exit_status(q), role="mock" if i < len(mock_procs) else "proxy")
@@ -1031,19 +1103,20 @@ def main() -> int:
             _barrier(dist, coll_cuda)
         if use_cuda:
             torch.cuda.synchronize()
-        m0 = scrape(admin_port) if args.impl == "native" else {}
+        scraped = args.impl == "native" and not direct
+        m0 = scrape(admin_port) if scraped else {}
         c0 = cpu_snapshot(mock_procs, proxy_procs)
         t0 = time.perf_counter()
         stats = loadgen(bin_dir, proxy_port, args.conns, args.steps * args.batch, args.lg_threads, args.timeout,
-                        spec_path, path)
+                        spec_path, path, stream)
         if use_cuda:
             torch.cuda.synchronize()
         if dist is not None:
             _barrier(dist, coll_cuda)
         elapsed = time.perf_counter() - t0
         c1 = cpu_snapshot(mock_procs, proxy_procs)
-        bd = breakdown(m0, scrape(admin_port), elapsed) if args.impl == "native" else {}
-        bd["pid"] = proxy_procs[0].pid
+        bd = breakdown(m0, scrape(admin_port), elapsed) if scraped else {}
+        bd["pid"] = proxy_procs[0].pid if proxy_procs else None
         bd.update(cpu_breakdown(c0, c1, stats["completed"], elapsed))
         dead = casualties()
         if dead and not dead_warm:
@@ -1056,9 +1129,14 @@ def main() -> int:
             # a remote stream whose delta count disagrees with its worker's, or a worker stream
             # that sent no delta for content it had, is a broken run even if the bytes validated
             bad += int(bd["exchange"]["delta_mismatch"] + bd["exchange"]["worker_nodata"])
+        # the harness alone, right after the timed region: the same load generator (connections,
+        # threads, validation) straight against this rank's first mock backend, no proxy
+        ceiling = None
+        if args.ceiling > 0 and not direct and not dead:
+            ceiling = harness_ceiling(bin_dir, mock_ports[0], args, mock_procs[0], tmp)
         spread = c3_rows = None
         if (dist is not None and world > 1 and args.spread_check and args.impl == "native"
-                and args.placement == "local"):
+                and args.placement == "local" and not direct):
             _kill(proxy_procs)  # done measuring; the check brings up its own proxy set
             spread = spread_check(args, SCENARIOS["headline"], rank, world, engine, device, bin_dir, tmp,
                                   mock_ports, dist, n_dev)
@@ -1091,9 +1169,12 @@ def main() -> int:
         ok = headline_ok
         # per-rank breakdowns, each scraped from that rank's own proxy (admin port)
         bd_rows = [bd]
+        ceil_rows = [ceiling]
         if dist is not None:
             bd_rows = [None] * world
             dist.all_gather_object(bd_rows, bd)
+            ceil_rows = [None] * world
+            dist.all_gather_object(ceil_rows, ceiling)
         if rank == 0:
             max_el = max(r[0] for r in rows)
             total = sum(r[1] for r in rows)
@@ -1102,7 +1183,9 @@ def main() -> int:
             baseline = sc["baseline"] if args.impl != "reference" else None
             res = {
                 "metric": "proxied req/sec (whole node) + p50 TTFT, 2-backend concatenate stream at 1/2/4/8 GPU"
-                          if args.scenario == "headline" else f"proxied req/sec (whole node) + p50 TTFT, {args.scenario}",
+                          if args.scenario == "headline" else
+                          "harness ceiling req/sec (load generator -> mock backend, no proxy) + p50 TTFT" if direct else
+                          f"proxied req/sec (whole node) + p50 TTFT, {args.scenario}",
                 "value": round(value, 3),
                 "unit": "req/s",
                 "n_gpus": world,
@@ -1124,7 +1207,8 @@ def main() -> int:
                                           + (f" + ep{world} (backend streams spread over ranks, "
                                                 f"{xchg_kind.upper()} exchange)"
                                              if args.placement == "spread" and world > 1 else ""),
-                           "impl": args.impl, "engine": engine if args.impl != "reference" else "reference",
+                           "impl": "none (no proxy)" if direct else args.impl,
+                           "engine": None if direct else engine if args.impl != "reference" else "reference",
                            "conns_per_rank": args.conns,
                            # hip: io loops post their own ticks into one multi-door grid ("loops",
                            # the default) or hand streams to tick-lane threads ("lanes")
@@ -1152,6 +1236,12 @@ def main() -> int:
                 # scraped from its own admin port
                 "breakdown_one_rank": bd,
             }
+            if any(c for c in ceil_rows):
+                # what the harness alone sustains on this box (sum over ranks): the proxied number
+                # above is only meaningful well below it
+                cr = [c for c in ceil_rows if c]
+                res["harness_ceiling_req_s"] = round(sum(c["req_s"] for c in cr), 1)
+                res["harness_ceiling"] = dict(cr[0], ranks=len(cr)) if len(cr) == 1 else {"per_rank": cr}
             if world > 1:  # every rank's own proxy: distinct pids, its own counters
                 res["breakdown_per_rank"] = [compact_breakdown(r, b, row) for r, (b, row) in enumerate(zip(bd_rows, rows))]
             if dead or dead_warm:

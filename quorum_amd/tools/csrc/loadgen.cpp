@@ -19,6 +19,12 @@
 //     stream <id> exact|prefix <hex>
 //     final absent | final any <hex> [<hex> ...]
 //     error allowed|absent         the all-failed "error" event
+//     empty allowed                events without content are skipped (a backend's own role /
+//                                  stop events: the direct harness-ceiling check, no proxy)
+//     json 1                       non-streaming: the body is one JSON completion, checked by
+//     message <hex>                  choices[0].message.content,
+//     usage <p> <c> <t>              the usage totals,
+//     field <key> <hex>              and top-level string fields (e.g. "backend")
 //
 // --abort-rate P: a request is abandoned (socket closed mid-stream, right after its first
 // content event) with probability P — client-abort churn for the data plane's session
@@ -64,6 +70,16 @@ struct Spec {
   bool final_absent = true;
   std::vector<std::string> final_any;
   bool error_allowed = false;
+  // direct (no proxy: the harness ceiling): events with empty / no content are skipped (the
+  // mock's own role and stop events), any event id accumulates into its stream's spec
+  bool empty_allowed = false;
+  // non-streaming JSON body (BASELINE config 1): choices[0].message.content, usage totals and
+  // top-level string fields (the passthrough's "backend") must equal these
+  bool json = false;
+  bool have_message = false;
+  std::string message;
+  long usage[3] = {-1, -1, -1};
+  std::vector<std::pair<std::string, std::string>> fields;
 };
 
 struct Opts {
@@ -397,6 +413,8 @@ int fast_event(const char* a, const char* b, std::string* id, std::string* conte
   static const char kP0[] = "{\"id\": \"";
   static const char kP1[] = "\", \"object\": \"chat.completion.chunk\", \"created\": ";
   static const char kP2[] = ", \"model\": \"parallel-proxy\", \"choices\": [{\"index\": 0, \"delta\": {";
+  static const char kP2m[] = ", \"model\": \"";
+  static const char kP2c[] = "\", \"choices\": [{\"index\": 0, \"delta\": {";
   static const char kRole[] = "\"role\": \"assistant\"}, \"finish_reason\": null}]}";
   static const char kCont[] = "\"content\": ";
   static const char kEndNull[] = "}, \"finish_reason\": null}]}";
@@ -417,7 +435,17 @@ int fast_event(const char* a, const char* b, std::string* id, std::string* conte
   const char* d = a;
   while (a < b && *a >= '0' && *a <= '9') ++a;
   if (a == d) return 0;
-  if (!eat(kP2, sizeof(kP2) - 1)) return 0;
+  if (!eat(kP2, sizeof(kP2) - 1)) {
+    // another backend's envelope (the direct harness check: the mock's own "model"): the
+    // same shape around any escape-free model string
+    if (!eat(kP2m, sizeof(kP2m) - 1)) return 0;
+    const char* mq = (const char*)memchr(a, '"', b - a);
+    if (!mq) return 0;
+    for (const char* x = a; x < mq; ++x)
+      if (*x == '\\' || (unsigned char)*x < 0x20) return 0;
+    a = mq;
+    if (!eat(kP2c, sizeof(kP2c) - 1)) return 0;
+  }
   if (eat(kRole, sizeof(kRole) - 1)) return a == b ? 1 : 0;
   if (!eat(kCont, sizeof(kCont) - 1)) return 0;
   const size_t n0 = content_out->size();
@@ -451,10 +479,103 @@ int fast_event(const char* a, const char* b, std::string* id, std::string* conte
   return 0;
 }
 
+// Non-streaming body: {"choices": [{"message": {"content": "..."}, ...}], "usage": {...}, ...}
+std::string validate_json(const std::string& body) {
+  const Spec& S = g.spec;
+  JR r{body.data(), body.data() + body.size()};
+  r.ws();
+  if (!r.lit("{")) return "body is not a JSON object";
+  std::string content;
+  bool have_content = false;
+  long usage[3] = {-1, -1, -1};
+  std::vector<std::pair<std::string, std::string>> strs;
+  auto read_int = [&](long* v) {
+    r.ws();
+    const char* s0 = r.p;
+    while (r.p < r.e && (*r.p == '-' || (*r.p >= '0' && *r.p <= '9'))) ++r.p;
+    if (r.p == s0) return false;
+    *v = strtol(std::string(s0, r.p - s0).c_str(), nullptr, 10);
+    return true;
+  };
+  // generic object walk: f(key) consumes the value or returns false to skip it
+  auto object = [&](auto&& self, auto&& f) -> bool {
+    r.ws();
+    if (!r.lit("{")) return false;
+    r.ws();
+    if (r.p < r.e && *r.p == '}') {
+      ++r.p;
+      return true;
+    }
+    while (true) {
+      std::string key;
+      if (!r.str(&key)) return false;
+      r.ws();
+      if (!r.lit(":")) return false;
+      r.ws();
+      int took = f(key);
+      if (took < 0) return false;
+      if (took == 0 && !r.skip_value()) return false;
+      r.ws();
+      if (r.p < r.e && *r.p == ',') {
+        ++r.p;
+        continue;
+      }
+      return r.lit("}");
+    }
+    (void)self;
+  };
+  r.p = body.data();
+  bool ok = object(object, [&](const std::string& k) -> int {
+    if (k == "choices") {
+      if (!r.lit("[")) return -1;
+      bool ok1 = object(object, [&](const std::string& k2) -> int {
+        if (k2 != "message") return 0;
+        return object(object, [&](const std::string& k3) -> int {
+                 if (k3 != "content") return 0;
+                 if (!r.str(&content)) return -1;
+                 have_content = true;
+                 return 1;
+               }) ? 1 : -1;
+      });
+      if (!ok1) return -1;
+      r.ws();
+      return r.lit("]") ? 1 : -1;  // exactly one choice
+    }
+    if (k == "usage") {
+      return object(object, [&](const std::string& k2) -> int {
+               const int i = k2 == "prompt_tokens" ? 0 : k2 == "completion_tokens" ? 1 : k2 == "total_tokens" ? 2 : -1;
+               if (i < 0) return 0;
+               return read_int(&usage[i]) ? 1 : -1;
+             }) ? 1 : -1;
+    }
+    for (auto& f : S.fields)
+      if (f.first == k && r.p < r.e && *r.p == '"') {
+        std::string v;
+        if (!r.str(&v)) return -1;
+        strs.emplace_back(k, v);
+        return 1;
+      }
+    return 0;
+  });
+  r.ws();
+  if (!ok || !r.ok || r.p != r.e) return "malformed JSON body";
+  if (!have_content) return "no choices[0].message.content";
+  if (S.have_message && content != S.message) return "message content differs (" + std::to_string(content.size()) + " B)";
+  for (int i = 0; i < 3; ++i)
+    if (S.usage[i] >= 0 && usage[i] != S.usage[i]) return "usage differs";
+  for (auto& f : S.fields) {
+    bool found = false;
+    for (auto& x : strs) found = found || (x.first == f.first && x.second == f.second);
+    if (!found) return "field " + f.first + " differs";
+  }
+  return std::string();
+}
+
 // returns "" when the response satisfies the spec, else a short reason
 std::string validate(int status, const std::string& body) {
   const Spec& S = g.spec;
   if (status != 200) return "status " + std::to_string(status);
+  if (S.json) return validate_json(body);
   std::vector<std::string> acc(S.streams.size());
   std::vector<int> nev(S.streams.size(), 0);
   bool saw_done = false, saw_final = false, saw_error = false;
@@ -517,6 +638,7 @@ std::string validate(int status, const std::string& body) {
     }
     size_t si = 0;
     while (si < S.streams.size() && S.streams[si].id != ev.id) ++si;
+    if ((!ev.has_content || ev.content.empty()) && S.empty_allowed) continue;  // a backend's role / stop event
     if (si == S.streams.size()) return "unexpected event id " + ev.id;
     if (!ev.has_content || ev.content.empty()) return "delta event without content (" + ev.id + ")";
     if (saw_final) return "delta after the final event";
@@ -862,6 +984,23 @@ bool load_spec(const std::string& path) {
       std::string m;
       ss >> m;
       S.error_allowed = m == "allowed";
+    } else if (kw == "empty") {
+      std::string m;
+      ss >> m;
+      S.empty_allowed = m == "allowed";
+    } else if (kw == "json") {
+      ss >> S.json;
+    } else if (kw == "message") {
+      std::string hex;
+      ss >> hex;
+      S.have_message = true;
+      S.message = hex == "-" ? std::string() : unhex(hex);
+    } else if (kw == "usage") {
+      ss >> S.usage[0] >> S.usage[1] >> S.usage[2];
+    } else if (kw == "field") {
+      std::string k, hex;
+      ss >> k >> hex;
+      S.fields.emplace_back(k, unhex(hex));
     } else {
       fprintf(stderr, "qmx_loadgen: unknown spec directive %s\n", kw.c_str());
       return false;

@@ -8,7 +8,8 @@
 //
 //   qmx_mock --port 9101 [--threads 2] [--tokens 20] [--think 1] [--delay-us 0]
 //   qmx_mock --print-expected 1 [--tokens 20] [--think 1]   # JSON: what clients should see
-//       {"stream_text": <content outside the think block>, "message": <non-stream content>}
+//       {"stream_text": <content outside the think block>, "message": <non-stream content>,
+//        "raw_text": <every streamed content byte>, "usage": [prompt, completion, total]}
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netinet/in.h>
@@ -59,6 +60,7 @@ std::string chunk(const std::string& s) {
 
 std::vector<std::string> g_events;  // SSE events of one streamed response
 std::string g_visible;              // concatenated content outside the think block
+std::string g_raw;                  // every content byte of the stream (think block included)
 std::string g_message;              // non-streaming message content
 std::string g_stream_all;           // full chunked streamed response (no delay path)
 std::string g_json_resp;            // non-streaming response
@@ -85,6 +87,7 @@ void build_responses() {
     g_events.push_back(sse_event("{\"content\": \"" + w + "\"}"));
   }
   g_visible = full;
+  g_raw = std::string(g.think ? "<think>let me reason about the request carefully before answering</think>" : "") + full;
   g_message = std::string(g.think ? "<think>let me reason</think>" : "") + full;
   g_events.push_back(sse_event("{}", "\"stop\""));
   g_events.push_back("data: [DONE]\n\n");
@@ -333,7 +336,8 @@ int main(int argc, char** argv) {
     auto js = [](const std::string& x) {  // the texts are ASCII without quotes / backslashes
       return "\"" + x + "\"";
     };
-    printf("{\"stream_text\": %s, \"message\": %s}\n", js(g_visible).c_str(), js(g_message).c_str());
+    printf("{\"stream_text\": %s, \"message\": %s, \"raw_text\": %s, \"usage\": [9, %d, %d]}\n",
+           js(g_visible).c_str(), js(g_message).c_str(), js(g_raw).c_str(), g.tokens, 9 + g.tokens);
     return 0;
   }
   std::vector<std::thread> ts;

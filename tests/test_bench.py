@@ -229,6 +229,38 @@ def test_bench_reference_same_harness(tmp_path):
     assert res["vs_baseline"] is None
 
 
+@pytest.mark.parametrize("impl", ["native", "reference"])
+def test_bench_nonstream1_config1(tmp_path, impl):
+    """BASELINE config 1 (1 mock backend, non-streaming, CPU): every JSON body validated
+    (message, usage, "backend" key), for the native proxy and the unmodified reference under
+    the same harness; the harness ceiling rides along."""
+    if impl == "reference" and not os.path.isdir("/root/reference/src/quorum"):
+        pytest.skip("reference checkout not present")
+    port = _free_port()
+    r = subprocess.run([sys.executable, BENCH, "--scenario", "nonstream1", "--impl", impl, "--steps", "1",
+                        "--warmup", "0", "--batch", "16" if impl == "reference" else "400", "--threads", "2",
+                        "--conns", "4", "--port", str(port), "--ceiling", "0.5"],
+                       cwd=str(tmp_path), env=_env(), capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(_json_lines(r.stdout)[0])
+    assert res["valid"] and res["invalid"] == 0 and res["validated"] == (16 if impl == "reference" else 400)
+    assert res["config"]["engine"] == ("cpu" if impl == "native" else "reference")
+    assert res["harness_ceiling_req_s"] > 0 and res["harness_ceiling"]["invalid"] == 0
+
+
+def test_bench_direct_harness_ceiling(tmp_path):
+    """--scenario direct: the load generator straight against a mock (no proxy), every
+    content byte of the mock's stream validated."""
+    port = _free_port()
+    r = subprocess.run([sys.executable, BENCH, "--scenario", "direct", "--steps", "1", "--warmup", "0", "--batch",
+                        "500", "--conns", "4", "--port", str(port)],
+                       cwd=str(tmp_path), env=_env(), capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(_json_lines(r.stdout)[0])
+    assert res["valid"] and res["validated"] == 500 and res["config"]["impl"] == "none (no proxy)"
+    assert res["breakdown_one_rank"]["cores_busy"]["proxy"] == 0.0
+
+
 def test_breakdown_loop_tick_fields():
     """bench.breakdown on two synthetic /metrics scrapes: the loop-tick hops (calibrated
     clocks), S3's event paths per item and the shader clock come from summable counters (the

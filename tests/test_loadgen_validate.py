@@ -32,7 +32,7 @@ def good_body(final=None):
     return out + "data: [DONE]\n\n"
 
 
-def _serve(body: str, status=200):
+def _serve(body: str, status=200, ctype="text/event-stream"):
     data = body.encode()
 
     class H(BaseHTTPRequestHandler):
@@ -44,7 +44,7 @@ def _serve(body: str, status=200):
         def do_POST(self):
             self.rfile.read(int(self.headers.get("content-length", "0")))
             self.send_response(status)
-            self.send_header("content-type", "text/event-stream")
+            self.send_header("content-type", ctype)
             self.send_header("transfer-encoding", "chunked")
             self.end_headers()
             for i in range(0, len(data), 37):  # odd chunk boundaries: split events / UTF-8
@@ -70,12 +70,12 @@ def _spec(tmp_path, final="absent", modes=("exact", "exact")):
     return str(p)
 
 
-def _run(body, spec, status=200, n=6):
+def _run(body, spec, status=200, n=6, stream=True):
     lg = str([t for t in qbuild.build_tools() if t.name == "qmx_loadgen"][0])
-    srv = _serve(body, status)
+    srv = _serve(body, status, "text/event-stream" if stream else "application/json")
     try:
         out = subprocess.run([lg, "--port", str(srv.server_address[1]), "--conns", "2", "--requests", str(n),
-                              "--threads", "1", "--timeout", "30", "--expect", spec],
+                              "--threads", "1", "--timeout", "30", "--expect", spec, "--stream", str(int(stream))],
                              capture_output=True, text=True, timeout=60)
     finally:
         srv.shutdown()
@@ -116,3 +116,56 @@ def test_prefix_mode_and_status(tmp_path):
     assert r["invalid"] == 0, err  # a stream allowed to fail may stop early
     r, _ = _run(good_body(), _spec(tmp_path), status=500)
     assert r["invalid"] == 6 and r["non200"] == 6
+
+
+MSG_TEXT = "<think>t</think>Answer é \"q\""
+
+
+def completion(content=MSG_TEXT, usage=(9, 20, 29), backend="LLM1", extra=None):
+    d = {"id": "c1", "object": "chat.completion", "created": 1, "model": "m",
+         "choices": [{"index": 0, "message": {"role": "assistant", "content": content}, "logprobs": None,
+                      "finish_reason": "stop"}]}
+    if usage is not None:
+        d["usage"] = {"prompt_tokens": usage[0], "completion_tokens": usage[1], "total_tokens": usage[2]}
+    if backend is not None:
+        d["backend"] = backend
+    d.update(extra or {})
+    return json.dumps(d)
+
+
+def _json_spec(tmp_path):
+    p = tmp_path / "spec_json.txt"
+    p.write_text(f"json 1\nmessage {MSG_TEXT.encode().hex()}\nusage 9 20 29\nfield backend {b'LLM1'.hex()}\n")
+    return str(p)
+
+
+def test_nonstream_json_bodies(tmp_path):
+    """BASELINE config 1 (non-streaming passthrough): the load generator checks the JSON
+    completion — message content, usage totals and the passthrough's "backend" key."""
+    r, err = _run(completion(), _json_spec(tmp_path), stream=False)
+    assert r["completed"] == r["validated"] == 6 and r["invalid"] == 0, err
+    for bad in (completion(content="other"), completion(usage=(9, 20, 30)), completion(usage=None),
+                completion(backend="LLM2"), completion(backend=None), completion()[:-1],
+                completion().replace('"choices": [{', '"choices": [{"x": 1}, {'), "[]"):
+        r, err = _run(bad, _json_spec(tmp_path), stream=False)
+        assert r["invalid"] == r["completed"] == 6, (bad, err)
+
+
+def test_direct_mode_skips_backend_role_and_stop(tmp_path):
+    """The harness-ceiling check validates a backend's own stream: role / stop events without
+    content are skipped, every content byte (think block included) must arrive."""
+    raw = "<think>x</think>Hi"
+
+    def mev(delta, finish=None):
+        d = {"id": "chatcmpl-mock", "object": "chat.completion.chunk", "created": 1, "model": "mock",
+             "choices": [{"index": 0, "delta": delta, "finish_reason": finish}]}
+        return "data: " + json.dumps(d) + "\n\n"
+
+    body = mev({"role": "assistant", "content": ""}) + mev({"content": raw[:9]}) + mev({"content": raw[9:]})
+    body += mev({}, "stop") + "data: [DONE]\n\n"
+    p = tmp_path / "spec_direct.txt"
+    p.write_text(f"role 0\ndone 1\nempty allowed\nstream chatcmpl-mock exact {raw.encode().hex()}\nfinal absent\n")
+    r, err = _run(body, str(p))
+    assert r["invalid"] == 0 and r["validated"] == 6, err
+    r, err = _run(body.replace("Hi", "Ho"), str(p))
+    assert r["invalid"] == 6, err

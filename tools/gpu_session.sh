@@ -15,9 +15,9 @@
 #   hunt=N                N headline runs that go on past an invalid one; whole invalid bodies
 #                         -> invalid_bodies.txt (QMX_LOADGEN_DUMP)
 #   ab:NAME:ENV:ARGS      one bench.py run under extra env (commas = spaces) -> ab_<NAME>.json
-#   scenarios             aggregate4, highqps8, failure, paced (10 steps each)
+#   scenarios             aggregate4, highqps8, failure, paced, nonstream1, direct (10 steps each)
 #   reference             the upstream proxy under the same harness (bench.py --impl reference)
-#   refscenarios          the same for aggregate4, highqps8, failure
+#   refscenarios          the same for nonstream1, aggregate4, highqps8, failure
 #   prof                  rocprofv3 --kernel-trace --stats of a short headline bench
 #   pmc:C1,C2,...         rocprofv3 --pmc pass (one block-limited counter set) on kbench
 #   pmce:ENV=V:C1,C2      the same pass under extra env (e.g. QMX_KFAST=7: one fast path off)
@@ -115,13 +115,13 @@ for step in "$@"; do
       rest=${step#ab:}; name=${rest%%:*}; rest=${rest#*:}; envs=${rest%%:*}; a=${rest#*:}
       bench ab_$name 300 ${envs//,/ } -- ${a//,/ } || exit 1 ;;
     scenarios)
-      for SC in aggregate4 highqps8 failure paced; do
+      for SC in aggregate4 highqps8 failure paced nonstream1 direct; do
         bench sc_$SC 300 QMX_NOP=1 -- --scenario $SC --steps 10 --warmup 2 $( [ $SC = paced ] || echo --batch 16384 ) || exit 1
       done ;;
     reference)
       bench reference 600 QMX_NOP=1 -- --impl reference --steps 10 --warmup 1 --batch 64 || exit 1 ;;
     refscenarios)  # the upstream proxy on every BASELINE scenario, same harness
-      for SC in aggregate4 highqps8 failure; do
+      for SC in nonstream1 aggregate4 highqps8 failure; do
         bench ref_$SC 600 QMX_NOP=1 -- --impl reference --scenario $SC --steps 5 --warmup 1 --batch 32 || exit 1
       done ;;
     prof)
