@@ -134,6 +134,7 @@ struct Exchange::Impl {
   struct Sink {
     void* dev = nullptr;
     size_t cap = 0;
+    int pinned = 0;  // RCCL rounds receiving straight into dev right now (forget_bulk waits)
   };
   struct Manifest {
     int round = 0, epoch = 0;
@@ -167,8 +168,18 @@ struct Exchange::Impl {
     bool round_over = false;  // the sender's round ended (its executor no longer reads s.dev)
     bool sender_ok = false;   // ... and succeeded on the sender's side
     int8_t verdict = -1;      // the receiver's report: -1 not yet, 0 missed, 1 got
+    double over_at = 0;       // when round_over was set (the report sweep's clock)
   };
   std::map<Key, Await> await;
+  // A report can arrive before its send moved into `await`: a receiver on another epoch acks
+  // "missed" as soon as it reads the manifest, while this rank is still in its previous
+  // round (two in flight).  Kept, keyed by the send, with its round, and applied when the
+  // send moves into `await` for that round (dropping it would leave the send waiting forever).
+  struct EarlyReport {
+    int round = 0;
+    int8_t verdict = -1;
+  };
+  std::map<Key, EarlyReport> early;
   std::vector<Send> resend;  // missed by their receiver: over the mesh (bulk thread)
   std::vector<int> downs_q;  // peers that left the mesh since the bulk thread last looked
   std::deque<Manifest> manifests;
@@ -495,7 +506,12 @@ struct Exchange::Impl {
             WireAck a;
             std::memcpy(&a, m.payload.data() + k * sizeof(WireAck), sizeof(a));
             auto it = await.find({a.skey, a.bi});
-            if (it == await.end()) continue;  // (sent over the mesh already: a fallback manifest)
+            if (it == await.end()) {
+              // still waiting for its round here: keep the report for it; otherwise it was sent
+              // over the mesh already (a fallback manifest) and nothing waits for it
+              if (sends.count({a.skey, a.bi})) early[{a.skey, a.bi}] = EarlyReport{m.a, (int8_t)(a.got ? 1 : 0)};
+              continue;
+            }
             it->second.verdict = a.got ? 1 : 0;
             if (it->second.round_over) wake_bulk |= settle(it, per);
           }
@@ -774,11 +790,25 @@ void Exchange::send_bulk(XMsg&& hdr, const void* dev, size_t len, std::function<
 
 void Exchange::expect_bulk(uint64_t skey, int bi, void* dev, size_t cap) {
   std::lock_guard<std::mutex> g(im_->bmu);
-  im_->sinks[{skey, bi}] = Impl::Sink{dev, cap};
+  Impl::Sink& k = im_->sinks[{skey, bi}];  // (a re-registration keeps its pins)
+  k.dev = dev;
+  k.cap = cap;
 }
 void Exchange::forget_bulk(uint64_t skey, int bi) {
-  std::lock_guard<std::mutex> g(im_->bmu);
-  im_->sinks.erase({skey, bi});
+  // a round receiving into this sink right now writes it until the round is over: wait (a
+  // session that ends while its remote final is in flight — a client that left — is rare,
+  // and a round is bounded by timeout_s), so a returned forget_bulk() means no later write
+  // into the released slot
+  std::unique_lock<std::mutex> g(im_->bmu);
+  for (;;) {
+    auto it = im_->sinks.find({skey, bi});
+    if (it == im_->sinks.end()) return;
+    if (it->second.pinned <= 0 || stop_.load()) {
+      im_->sinks.erase(it);
+      return;
+    }
+    im_->bcv.wait_for(g, std::chrono::milliseconds(1));
+  }
 }
 
 void Exchange::request_stop() {
@@ -961,8 +991,9 @@ struct BulkOp {
   bool send;
   const void* src;  // send: HBM (device executors) or host bytes; nullptr: a vanished send
   std::string host;  // send (host executors): the bytes; receive: filled on completion
-  size_t off = 0;    // receive (device executors): staging offset
   bool done = false; // receive (host executors): its bytes are all in, whatever the round does
+  void* sink = nullptr;  // receive (device executors): the owner's HBM shadow slot, pinned for
+                         // the round; nullptr: no sink registered — received and discarded
 };
 
 struct BulkExec {
@@ -973,15 +1004,22 @@ struct BulkExec {
   virtual bool formed() const = 0;
   virtual bool start(int round, std::vector<BulkOp>& ops) = 0;
   virtual int progress() = 0;  // 1 complete, 0 in flight, -1 failed
-  // device executors: copy a completed receive from staging into the owner's sink
-  virtual bool to_sink(const BulkOp&, void*) { return false; }
 };
 
 class RcclExec : public BulkExec {
  public:
-  RcclExec(int device, int world, int rank) : device_(device), world_(world), rank_(rank) {
+  // Receives land straight in the owners' shadow slots (BulkOp::sink): no staging copy, no
+  // synchronisation per text — the round's completion (one stream query) is the only wait.
+  // The discard buffer (a receive without a sink) and the zero buffer (a vanished send) are
+  // allocated here, once, at the longest text a round can carry: nothing is allocated, and
+  // so nothing synchronises the device, inside a round.
+  RcclExec(int device, int world, int rank, size_t max_text)
+      : device_(device), world_(world), rank_(rank), cap_(std::max<size_t>(max_text, 256)) {
     XHIP(hipSetDevice(device_));
     XHIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    XHIP(hipMalloc(&scratch_, cap_));
+    XHIP(hipMalloc(&zeros_, cap_));
+    XHIP(hipMemset(zeros_, 0, cap_));
   }
   ~RcclExec() override {
     drop();
@@ -1008,44 +1046,20 @@ class RcclExec : public BulkExec {
     if (st_) hipStreamSynchronize(st_);  // the aborted communicator's kernels have been flushed
   }
   bool start(int, std::vector<BulkOp>& ops) override {
-    size_t need = 256, zero = 0;
-    for (auto& o : ops) {
-      if (!o.send) need += (o.e->len + 255) & ~(size_t)255;
-      else if (!o.src) zero = std::max(zero, (size_t)o.e->len);
-    }
-    if (need > cap_) {
-      if (scratch_) hipFree(scratch_);
-      cap_ = std::max(need, cap_ * 2);
-      if (hipMalloc(&scratch_, cap_) != hipSuccess) {
-        scratch_ = nullptr;
-        cap_ = 0;
-        return false;
-      }
-    }
-    // a vanished send (its text already left over the mesh) still posts its len bytes, or
-    // the pair desyncs: zeros from a buffer of its own, as long as the longest such send
-    if (zero > zcap_) {
-      if (zeros_) hipFree(zeros_);
-      zcap_ = std::max(zero, 2 * zcap_);
-      if (hipMalloc(&zeros_, zcap_) != hipSuccess || hipMemsetAsync(zeros_, 0, zcap_, st_) != hipSuccess) {
-        if (zeros_) hipFree(zeros_);
-        zeros_ = nullptr;
-        zcap_ = 0;
-        return false;
-      }
-    }
+    for (auto& o : ops)  // (a text is never longer than a content slot: max_text)
+      if (o.e->len > cap_ && (o.send ? !o.src : !o.sink)) return false;
     if (ncclGroupStart() != ncclSuccess) return false;
     bool ok = true;
-    size_t off = 0;
     for (auto& o : ops) {
       ncclResult_t r;
       if (o.send) {
+        // a vanished send (its text already left over the mesh) still posts its len bytes,
+        // or the pair desyncs: zeros
         const void* src = o.src ? o.src : (const void*)zeros_;
         r = ncclSend(src, o.e->len, ncclUint8, o.e->dst, comm_, st_);
       } else {
-        o.off = off;
-        r = ncclRecv(scratch_ + off, o.e->len, ncclUint8, o.e->src, comm_, st_);
-        off += (o.e->len + 255) & ~(size_t)255;
+        // discards share one buffer: their bytes are never read
+        r = ncclRecv(o.sink ? o.sink : (void*)scratch_, o.e->len, ncclUint8, o.e->src, comm_, st_);
       }
       if (r != ncclSuccess && r != ncclInProgress) ok = false;
     }
@@ -1057,11 +1071,6 @@ class RcclExec : public BulkExec {
     hipError_t e = hipStreamQuery(st_);
     if (e == hipSuccess) return 1;
     return e == hipErrorNotReady ? 0 : -1;
-  }
-  bool to_sink(const BulkOp& o, void* dst) override {
-    if (!o.e->len) return true;
-    return hipMemcpyAsync(dst, scratch_ + o.off, o.e->len, hipMemcpyDeviceToDevice, st_) == hipSuccess &&
-           hipStreamSynchronize(st_) == hipSuccess;
   }
 
  private:
@@ -1077,10 +1086,9 @@ class RcclExec : public BulkExec {
   int device_, world_, rank_;
   ncclComm_t comm_ = nullptr;
   hipStream_t st_ = nullptr;
-  uint8_t* scratch_ = nullptr;
-  size_t cap_ = 0;
-  uint8_t* zeros_ = nullptr;  // vanished sends' bytes
-  size_t zcap_ = 0;
+  size_t cap_ = 0;             // max_text: the discard and zero buffers' size
+  uint8_t* scratch_ = nullptr;  // discarded receives
+  uint8_t* zeros_ = nullptr;    // vanished sends' bytes
 };
 
 #pragma pack(push, 1)
@@ -1301,7 +1309,7 @@ void Exchange::bulk_loop() {
   Impl& I = *im_;
   std::unique_ptr<BulkExec> ex;
   try {
-    if (o_.transport == "rccl") ex.reset(new RcclExec(o_.device, o_.world, o_.rank));
+    if (o_.transport == "rccl") ex.reset(new RcclExec(o_.device, o_.world, o_.rank, o_.max_text));
     else ex.reset(new TcpExec(o_.addr, o_.bulk_port > 0 ? o_.bulk_port : o_.port + o_.world, o_.world, o_.rank));
   } catch (const std::exception& e) {
     fprintf(stderr, "qmx exchange (rank %d): %s — bulk transfers use the mesh\n", o_.rank, e.what());
@@ -1406,7 +1414,24 @@ void Exchange::bulk_loop() {
         mf = std::move(I.manifests.front());
         I.manifests.pop_front();
       }
-      rs.swap(I.resend);
+      // a carried send whose round is over and whose report never came (lost with a
+      // connection that re-formed, a receiver that restarted): after timeout_s it is treated
+      // as missed and resent over the mesh — the receiver drops a duplicate
+      const double tnow = now_s();
+      for (auto it = I.await.begin(); it != I.await.end();) {
+        auto nx = std::next(it);
+        if (it->second.round_over && it->second.verdict < 0 && tnow - it->second.over_at > o_.timeout_s) {
+          it->second.verdict = 0;
+          I.settle(it, out);
+        }
+        it = nx;
+      }
+      for (auto it = I.early.begin(); it != I.early.end();) {  // reports whose send left otherwise
+        auto nx = std::next(it);
+        if (!I.sends.count(it->first)) I.early.erase(it);
+        it = nx;
+      }
+      rs.swap(I.resend);  // (with the sweep's)
       for (int r : I.downs_q) {
         // a receiver that left can neither take nor report a carried send: release them
         for (auto it = I.await.begin(); it != I.await.end();) {
@@ -1476,6 +1501,11 @@ void Exchange::bulk_loop() {
             Impl::Await& w = I.await[it->first];
             w.s = std::move(it->second);
             w.dst = e.dst;
+            auto er = I.early.find(it->first);
+            if (er != I.early.end()) {  // its receiver reported already (see Impl::early)
+              if (er->second.round == mf.round) w.verdict = er->second.verdict;
+              I.early.erase(er);
+            }
             carried.push_back(it->first);
             I.sends.erase(it);
           }
@@ -1487,7 +1517,18 @@ void Exchange::bulk_loop() {
         }
         ops.push_back(std::move(o));
       }
-      if (e.dst == o_.rank) ops.push_back(BulkOp{&e, false, nullptr, std::string()});
+      if (e.dst == o_.rank) {
+        BulkOp o{&e, false, nullptr, std::string()};
+        if (ex->device()) {  // straight into the owner's shadow slot, pinned until the round is over
+          std::lock_guard<std::mutex> g(I.bmu);
+          auto it = I.sinks.find({e.skey, e.bi});
+          if (it != I.sinks.end() && it->second.dev && it->second.cap >= e.len) {
+            o.sink = it->second.dev;
+            ++it->second.pinned;
+          }
+        }
+        ops.push_back(std::move(o));
+      }
     }
     bool ok;
     if (stall_round > 0 && mf.round == stall_round && !stalled) {
@@ -1545,14 +1586,15 @@ void Exchange::bulk_loop() {
         XMsg v;
         bool deliver = true;
         if (ex->device()) {
+          // the bytes are already in the owner's shadow slot (the round's stream completed)
           std::lock_guard<std::mutex> g(I.bmu);
           auto it = I.sinks.find({e.skey, e.bi});
-          if (it == I.sinks.end() || !it->second.dev || it->second.cap < e.len) {
-            deliver = false;  // session gone: nobody needs the text (reported got)
-          } else if (!ex->to_sink(o, it->second.dev)) {
-            // HBM → HBM into the owner's shadow slot; complete before the lock drops, so a
-            // forget_bulk() that returns guarantees no later write into a released slot
-            deliver = got = false;  // (the sender resends over the mesh)
+          if (!o.sink) {
+            // no sink when the round started: discarded.  A sink registered since (a late
+            // expect_bulk) must not wait forever: reported missed, the sender resends over
+            // the mesh; no sink at all: the session is gone, nobody needs the text (got)
+            deliver = false;
+            if (it != I.sinks.end()) got = false;
           }
         } else {
           v.payload = std::move(o.host);  // host executor: the bytes ride the delivery
@@ -1571,6 +1613,21 @@ void Exchange::bulk_loop() {
       }
       ack(e, got);
     }
+    // the round is over (and, failed, its communicator aborted and its stream drained): no
+    // more writes into the pinned sinks — a waiting forget_bulk() may release them now
+    {
+      bool unpinned = false;
+      std::lock_guard<std::mutex> g(I.bmu);
+      for (auto& o : ops) {
+        if (o.send || !o.sink) continue;
+        auto it = I.sinks.find({o.e->skey, o.e->bi});
+        if (it != I.sinks.end() && it->second.pinned > 0) {
+          --it->second.pinned;
+          unpinned = true;
+        }
+      }
+      if (unpinned) I.bcv.notify_all();
+    }
     deliver_all();
     send_reports(mf.round);
     // our sends: the round is over; each is settled by its receiver's report
@@ -1582,6 +1639,7 @@ void Exchange::bulk_loop() {
         if (it == I.await.end()) continue;
         if (ok) bulk_bytes_ += it->second.s.len;
         it->second.round_over = true;
+        it->second.over_at = now_s();
         it->second.sender_ok = ok;
         if (it->second.verdict >= 0) wake |= I.settle(it, out);
       }

@@ -73,6 +73,9 @@ struct XOptions {
   int device = 0;
   int batch_us = 50;              // rank 0: announcements arriving within this window share a round
   double timeout_s = 30.0;        // bulk round / epoch formation slower than this = peer failure
+  // rccl: the longest final text a round can carry (the engines' per-slot content capacity):
+  // the executor's discard / zero buffers are allocated once at this size, never in a round
+  size_t max_text = 1u << 20;
   // per-loop links: io loop l of every rank pair gets a TCP connection of its own (dialled by
   // the higher rank once the pair's mesh connection forms), so a session's opens, deltas and
   // eager finals go io loop → socket → io loop with no mesh thread on the data path

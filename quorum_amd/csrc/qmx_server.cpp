@@ -2439,7 +2439,10 @@ class Loop {
       return;
     }
     if (xl_.size() < (size_t)xch_->world()) xl_.resize(xch_->world());
-    if (xl_[r].fd >= 0) link_down(r, false);
+    // a stale link (the pair's mesh connection re-formed): its unsent frames and unparsed bytes
+    // go with it, so the streams that travelled on it are failed (as for a link that broke);
+    // streams on the mesh are unaffected
+    if (xl_[r].fd >= 0) link_down(r, true, true);
     xl_[r].fd = fd;
     xl_[r].in = m.payload;
     add(fd, EPOLLIN, tag(7, fd));
@@ -2506,7 +2509,9 @@ class Loop {
   }
   // a link closed: its streams end as for a peer that left this loop's reach (X_DOWN); new
   // sessions use the mesh until the exchange hands over a new link
-  void link_down(int r, bool fail_streams) {
+  // link_only: fail only the streams that travelled on the link (their frames may be lost
+  // with it); otherwise every stream shared with rank r, as for a rank that left
+  void link_down(int r, bool fail_streams, bool link_only = false) {
     XLink& L = xl_[r];
     if (L.fd < 0) return;
     epoll_ctl(ep_, EPOLL_CTL_DEL, L.fd, nullptr);
@@ -2517,6 +2522,7 @@ class Loop {
     std::vector<XMsg> v(1);
     v[0].type = X_DOWN;
     v[0].a = r;
+    v[0].b = link_only ? 1 : 0;
     handle_x(v, true);
   }
   void post_owner(Session* s, uint8_t type, uint8_t flags, int a, const char* payload, size_t n, int b = 0) {
@@ -2569,14 +2575,19 @@ class Loop {
         // peer m.a (or, a = -1, every peer) is unreachable: fail the streams it runs for
         // our sessions, drop the streams we run for its sessions (a worker whose final
         // text is in flight waits for X_SENT, which the exchange always sends)
+        // (b = 1: a replaced link — only the streams that used it)
+        const bool link_only = m.b == 1;
         std::vector<Session*> owners, shadows;
         for (auto& kv : rsess_) owners.push_back(kv.second);
         for (auto& kv : shadow_) shadows.push_back(kv.second);
         for (Session* s : shadows)
-          if (sessions_.count(s) && (m.a < 0 || s->owner_rank == m.a) && !s->bulk_pending) end_session(s);
+          if (sessions_.count(s) && (m.a < 0 || s->owner_rank == m.a) && !s->bulk_pending &&
+              (!link_only || s->via_link))
+            end_session(s);
         for (Session* s : owners) {
           for (int i = 0; i < (int)s->bs.size() && sessions_.count(s); ++i)
-            if (s->bs[i].remote >= 0 && (m.a < 0 || s->bs[i].remote == m.a) && s->bs[i].state == 0) {
+            if (s->bs[i].remote >= 0 && (m.a < 0 || s->bs[i].remote == m.a) && s->bs[i].state == 0 &&
+                (!link_only || s->bs[i].via_link)) {
               c_sp_down++;
               fail_backend(s, i, 500, "rank exchange failed", "proxy_error");
             }
@@ -3367,6 +3378,7 @@ int run_server(const ServerCfg& cfg0) {
     o.device = cfg.device;
     o.batch_us = cfg.xchg_round_us;
     o.timeout_s = cfg.xchg_timeout;
+    o.max_text = (size_t)cfg.content_cap;
     // per-loop links (0: every session message via the mesh thread)
     o.links = cfg.xchg_links >= 0 ? cfg.xchg_links != 0 : env_flag("QMX_XCHG_LINKS", true);
     std::vector<Loop*> lp;
