@@ -67,6 +67,13 @@ SCENARIOS = {
                     baseline=21.14, baseline_ttft_ms=620.5, baseline_source=BASELINE_SOURCE_SAME,
                     desc="2 mock backends, backend 2 injects 30% HTTP 500 / 20% mid-stream "
                                        "disconnect / 10% content:null; 2 s timeout"),
+    # config 5 as round 4 measured it: the faulty backend writes each event on its own (a
+    # trickling upstream: a receive and a tick per event); "failure" writes a response at once
+    "failure_trickle": dict(n=2, strategy="concatenate", hide_final=False, skip=False, timeout=2,
+                            faults={1: ["--fail-rate", "0.3", "--drop-rate", "0.2", "--null-rate", "0.1",
+                                        "--trickle", "1"]},
+                            baseline=21.14, baseline_ttft_ms=620.5, baseline_source=BASELINE_SOURCE_SAME,
+                            desc="config 5 with the faulty backend trickling its events (one write each)"),
     # steady-state serving shape: backends pace their events (10 ms apart, like a decoding
     # LLM), many concurrent sessions, each tick sees a few events of many streams.  TTFT is
     # bounded below by the mock's own first-content time (5 events x 10 ms = 50 ms).

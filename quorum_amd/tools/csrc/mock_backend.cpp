@@ -4,7 +4,8 @@
 // survey's benchmark shape: role event, 4 split think fragments, N content
 // tokens, stop, [DONE], sent with chunked transfer encoding; optional per-event delay.
 // Fault knobs (BASELINE config 5): --fail-rate (HTTP 500), --stall-ms (never answer),
-// --drop-rate (close mid-stream), --null-rate (content:null event).
+// --drop-rate (close mid-stream), --null-rate (content:null event); --trickle 1 writes a
+// faulty response event by event instead of at once.
 //
 //   qmx_mock --port 9101 [--threads 2] [--tokens 20] [--think 1] [--delay-us 0]
 //   qmx_mock --print-expected 1 [--tokens 20] [--think 1]   # JSON: what clients should see
@@ -43,6 +44,10 @@ struct Opts {
   double drop_rate = 0.0;
   double null_rate = 0.0;
   long stall_ms = 0;
+  // faulty responses without a per-event delay: written at once like every other response
+  // (0, the default) or event by event, each write a timer tick of its own (1: the round-4
+  // behaviour, which made a faulty backend trickle; --delay-us paces events explicitly)
+  int trickle = 0;
   std::string name = "mock";
 } g;
 
@@ -119,6 +124,7 @@ struct Conn {
   bool drop_after = false;
   int drop_at = -1;
   bool stalled = false;
+  bool close_after = false;  // a mid-stream drop written at once: close once it is out
 };
 
 using Clock = std::chrono::steady_clock;
@@ -236,6 +242,22 @@ void worker(int tid) {
         if (!flush(c)) return false;
         continue;
       }
+      if (g.delay_us <= 0 && !g.trickle) {
+        // faults drawn per response exactly as the event-by-event path draws them (null on
+        // event 2, a drop at the middle event), the response written at once
+        const bool null2 = g.null_rate > 0 && U(rng) < g.null_rate;
+        c.out += kStreamHdr;
+        const int end = c.drop_at >= 0 ? c.drop_at : (int)g_events.size();
+        for (int i = 0; i < end; ++i) c.out += chunk(i == 2 && null2 ? sse_event("{\"content\": null}") : g_events[i]);
+        if (c.drop_at >= 0) {  // mid-stream disconnect: the first half, then the connection closes
+          c.close_after = true;
+          if (!flush(c)) return false;
+          return !c.out.empty();  // all out: close now; else once EPOLLOUT drained it
+        }
+        c.out += "0\r\n\r\n";
+        if (!flush(c)) return false;
+        continue;
+      }
       c.out += kStreamHdr;
       c.next_event = 0;
       if (!send_event(c)) return false;
@@ -273,6 +295,7 @@ void worker(int tid) {
       bool ok = true;
       if (evs[i].events & EPOLLOUT) {
         ok = flush(c);
+        if (ok && c.out.empty() && c.close_after) ok = false;  // a dropped stream's first half is out
         if (ok && c.out.empty()) {
           epoll_event e{};
           e.events = EPOLLIN;
@@ -292,7 +315,7 @@ void worker(int tid) {
           else if (errno != EAGAIN && errno != EWOULDBLOCK) ok = false;
           break;
         }
-        if (ok && c.next_event < 0 && !c.stalled) ok = handle(c);
+        if (ok && c.next_event < 0 && !c.stalled && !c.close_after) ok = handle(c);
       }
       if (!ok) close_conn(fd);
     }
@@ -328,6 +351,7 @@ int main(int argc, char** argv) {
     else if (k == "--drop-rate") g.drop_rate = atof(v.c_str());
     else if (k == "--null-rate") g.null_rate = atof(v.c_str());
     else if (k == "--stall-ms") g.stall_ms = atol(v.c_str());
+    else if (k == "--trickle") g.trickle = atoi(v.c_str());
     else if (k == "--name") g.name = v;
     else if (k == "--print-expected") print_expected = atoi(v.c_str()) != 0;
   }
