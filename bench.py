@@ -81,8 +81,8 @@ SCENARIOS = {
     # valid backend is quorum's passthrough, oai_proxy.py:1130-1137, 1356-1380 — the upstream
     # JSON plus "backend": name; the load generator checks message content, usage and that key)
     "nonstream1": dict(n=1, strategy="concatenate", hide_final=False, skip=False, faults={}, timeout=30,
-                       stream=False, engine="cpu", baseline=19.5, baseline_ttft_ms=811.0,
-                       baseline_source=BASELINE_SOURCE_SURVEY,
+                       stream=False, engine="cpu", baseline=56.647, baseline_ttft_ms=282.2,
+                       baseline_source=BASELINE_SOURCE_SAME,
                        desc="1 mock backend, non-streaming concatenate (passthrough), CPU engine"),
     # the harness alone: the load generator straight against one mock backend, no proxy, same
     # validation (every content byte of the mock's stream) — SURVEY §6 row 1 / §7.4 item 4.

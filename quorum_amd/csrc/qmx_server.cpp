@@ -992,7 +992,7 @@ class Loop {
         dispatch(evs[i]);
         // a long batch: tick results that arrived meanwhile are applied now, not after it
         if ((i & 7) == 7 && early_flush_ && rq_pending_.load(std::memory_order_acquire)) on_results(false);
-        if ((i & 1) == 1 && jobs_live_ && any_ready()) loop_tick();
+        if ((i + 1) % check_every_ == 0 && jobs_live_ && any_ready()) loop_tick();
       }
       if (g_drain.load() && drain_step()) break;
       if ((hub_ || aeng_) && early_flush_) {
@@ -1286,10 +1286,11 @@ class Loop {
           // stream trickling in event by event otherwise costs a client send per tick.  A
           // stream with nothing pending (the steady-state LLM pace) is sent at once.
           const bool hold = coalesce_s_ > 0 && s->first_content && !(r.flags & (RF_DONE | RF_ABORTED)) &&
-                            (ops_pending(r.slot) || eng().pending(r.slot) || up_readable(s->bs[bi].up));
+                            more_pending(r.slot, s->bs[bi].up);
           send_content(s, r.data(), r.size(), hold);
         }
-      }
+      } else if (s->cl && s->cl->held && s->kind != K_REMOTE && !more_pending(r.slot, s->bs[bi].up))
+        release_held(s->cl);  // its stream's held delta waited for this tick, which had nothing
       r.hold = ViewRef();  // the bytes were copied (or dropped): the lane may reuse its arena
       if ((r.flags & RF_ABORTED)) c_stream_aborts++;
       if ((r.flags & (RF_DONE | RF_ABORTED)) && s->bs[bi].state == 0) {
@@ -2237,6 +2238,22 @@ class Loop {
       deferq_.push_back(Deferred{c->fd, c->serial, now_s() + coalesce_s_});
     }
     c_coalesced++;
+  }
+  // more output for this stream is on its way: bytes fed this iteration, in the engine (fed,
+  // or in a tick in flight), or unread on its upstream socket.  The cheap look first; with
+  // the shared engine (tick lanes) the FIONREAD before the engine lock the lanes also take
+  bool more_pending(int slot, const Up* up) {
+    if (ops_pending(slot)) return true;
+    if (hub_) return up_readable(up) || eng().pending(slot);
+    return eng().pending(slot) || up_readable(up);
+  }
+  // a held client's corked output goes out with this iteration's flush (as at its deadline)
+  void release_held(Client* c) {
+    if (!c->held || c->queued || c->dead) return;
+    c->held = false;
+    if (c->out_off >= c->out.size() || c->want_out) return;
+    c->queued = true;
+    flushq_.push_back(c->fd);
   }
   // the stream's upstream socket already holds unread bytes (its next events arrived while
   // this tick ran): one FIONREAD instead of a client send per tick of a trickling stream
@@ -3202,6 +3219,13 @@ class Loop {
   // loop ticks: also look for results between the new requests an iteration parses (parsing
   // and the upstream sends are an iteration's longest stretch without a look);
   // QMX_LOOP_REQ_CHECK=0 turns it off (A/B)
+  // loop ticks: results are looked for after every check_every_-th event of a batch
+  // (QMX_LOOP_CHECK_EVERY, default 1: the look is a few host-memory loads, while an event's
+  // handling — a request parse with its upstream sends, a client write — runs several us)
+  const int check_every_ = [] {
+    const char* e = env_get("QMX_LOOP_CHECK_EVERY");
+    return e ? std::max(1, atoi(e)) : 1;
+  }();
   const bool req_check_ = [] {
     const char* e = env_get("QMX_LOOP_REQ_CHECK");
     return !e || atoi(e) != 0;
