@@ -286,11 +286,19 @@ struct Exchange::Impl {
     dial_links(r);
   }
   // the higher rank of a pair dials io loop l's link for every l once the pair's mesh
-  // connection formed (the peer's listener is up): blocking connect + hello, then the socket
-  // goes to loop l (X_LINK), which owns it from then on
+  // connection formed (the peer's listener is up): connect + hello, then the socket goes to
+  // loop l (X_LINK), which owns it from then on.  On a helper thread: a blocking connect to an
+  // unresponsive peer (up to 1 s per loop) must not stall the mesh thread's heartbeats,
+  // reports and session frames for every other peer.
+  std::mutex dmu;
+  std::vector<std::thread> dialers;  // joined by Exchange::join()
   void dial_links(int r) {
     if (!X->o_.links || X->o_.rank <= r) return;
-    for (int l = 0; l < X->nloops_; ++l) {
+    std::lock_guard<std::mutex> g(dmu);
+    dialers.emplace_back([this, r] { dial_links_now(r); });
+  }
+  void dial_links_now(int r) {
+    for (int l = 0; l < X->nloops_ && !X->stop_.load(); ++l) {
       int fd = socket(AF_INET, SOCK_STREAM, 0);
       if (fd < 0) return;
       timeval tv{1, 0};
@@ -819,6 +827,13 @@ void Exchange::request_stop() {
 void Exchange::join() {
   if (mesh_th_.joinable()) mesh_th_.join();
   if (bulk_th_.joinable()) bulk_th_.join();
+  std::vector<std::thread> ds;
+  {
+    std::lock_guard<std::mutex> g(im_->dmu);
+    ds.swap(im_->dialers);
+  }
+  for (auto& t : ds)
+    if (t.joinable()) t.join();
 }
 
 // ------------------------------------------------------------------ the mesh thread
