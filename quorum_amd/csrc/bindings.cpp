@@ -236,7 +236,7 @@ PYBIND11_MODULE(_qmx, m) {
     bool ok = true;
     int bad = 0, dups = 0, n_data = 0, n_bulk = 0, n_sent = 0;
     double data_us = 0, wall = 0;
-    uint64_t rounds_done = 0, mesh_finals = 0, epochs = 0, w2_rounds = 0, w2_mesh = 0, rescued = 0;
+    uint64_t rounds_done = 0, mesh_finals = 0, epochs = 0, w2_rounds = 0, w2_mesh = 0, rescued = 0, sweeps = 0, early_reports = 0;
     std::string why;
     {
       py::gil_scoped_release nogil;
@@ -364,6 +364,8 @@ PYBIND11_MODULE(_qmx, m) {
       mesh_finals = x.mesh_bulk();
       epochs = x.epochs();
       rescued = x.rescued();
+      sweeps = x.sweeps();
+      early_reports = x.early_reports();
       // linger so peers still waiting for our bytes (or reports) get them, then stop
       std::this_thread::sleep_for(std::chrono::milliseconds(300));
       {  // nothing may arrive twice, not even late
@@ -383,7 +385,7 @@ PYBIND11_MODULE(_qmx, m) {
                     py::arg("sent") = n_sent, py::arg("data_wall_us") = data_us, py::arg("wall_s") = wall,
                     py::arg("rccl_rounds") = rounds_done, py::arg("mesh_finals") = mesh_finals,
                     py::arg("epochs") = epochs, py::arg("wave2_rounds") = w2_rounds,
-                    py::arg("wave2_mesh_finals") = w2_mesh, py::arg("rescued") = rescued,
+                    py::arg("wave2_mesh_finals") = w2_mesh, py::arg("rescued") = rescued, py::arg("sweeps") = sweeps, py::arg("early_reports") = early_reports,
                     py::arg("why") = why);
   });
   // One-rank RCCL rounds into given HBM sinks (GPU tests of the owner's remote-final path):

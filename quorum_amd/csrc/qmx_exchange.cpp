@@ -180,6 +180,9 @@ struct Exchange::Impl {
     int8_t verdict = -1;
   };
   std::map<Key, EarlyReport> early;
+  // QMX_XCHG_DEBUG_DROP_EARLY: drop such reports as the round-4 code did (the negative
+  // control of tests/test_native_spread.py::test_exchange_early_missed_report_is_kept)
+  const bool drop_early = env_get("QMX_XCHG_DEBUG_DROP_EARLY") != nullptr;
   std::vector<Send> resend;  // missed by their receiver: over the mesh (bulk thread)
   std::vector<int> downs_q;  // peers that left the mesh since the bulk thread last looked
   std::deque<Manifest> manifests;
@@ -517,7 +520,10 @@ struct Exchange::Impl {
             if (it == await.end()) {
               // still waiting for its round here: keep the report for it; otherwise it was sent
               // over the mesh already (a fallback manifest) and nothing waits for it
-              if (sends.count({a.skey, a.bi})) early[{a.skey, a.bi}] = EarlyReport{m.a, (int8_t)(a.got ? 1 : 0)};
+              if (sends.count({a.skey, a.bi})) {
+                X->early_reports_++;
+                if (!drop_early) early[{a.skey, a.bi}] = EarlyReport{m.a, (int8_t)(a.got ? 1 : 0)};
+              }
               continue;
             }
             it->second.verdict = a.got ? 1 : 0;
@@ -1335,6 +1341,16 @@ void Exchange::bulk_loop() {
   // fault injection: every rank of global round N hangs in it (posts nothing) until the
   // round times out — once per process
   const int stall_round = env_get("QMX_XCHG_FAULT_STALL_ROUND") ? atoi(env_get("QMX_XCHG_FAULT_STALL_ROUND")) : 0;
+  // QMX_XCHG_FAULT_EARLY_MISSED=R:N (fault injection): in the first global round >= N in which
+  // rank R receives, R behaves as a rank on another epoch — it reports every receive of the
+  // round missed the moment it reads the manifest and sends its own texts over the mesh —
+  // while every other rank carries its sends of that round 100 ms late, so R's report
+  // arrives before they move into `await`
+  int early_r = -1, early_n = 0;
+  bool early_done = false;
+  if (const char* em = env_get("QMX_XCHG_FAULT_EARLY_MISSED")) {
+    if (sscanf(em, "%d:%d", &early_r, &early_n) != 2) early_r = -1;
+  }
   std::vector<std::vector<XMsg>> out(nloops_);
   auto deliver_all = [&] {
     for (int l = 0; l < nloops_; ++l)
@@ -1430,13 +1446,19 @@ void Exchange::bulk_loop() {
         I.manifests.pop_front();
       }
       // a carried send whose round is over and whose report never came (lost with a
-      // connection that re-formed, a receiver that restarted): after timeout_s it is treated
-      // as missed and resent over the mesh — the receiver drops a duplicate
+      // connection that re-formed, a receiver that restarted) is treated as missed and resent
+      // over the mesh — the receiver drops a duplicate.  After 3 x timeout_s: the receiver's
+      // own round may legitimately end up to a round timeout after the sender's (it waits for
+      // a third rank the sender had no transfer with), and starts later too
       const double tnow = now_s();
       for (auto it = I.await.begin(); it != I.await.end();) {
         auto nx = std::next(it);
-        if (it->second.round_over && it->second.verdict < 0 && tnow - it->second.over_at > o_.timeout_s) {
+        if (it->second.round_over && it->second.verdict < 0 && tnow - it->second.over_at > 3.0 * o_.timeout_s) {
           it->second.verdict = 0;
+          if (sweeps_++ < 10)
+            fprintf(stderr, "qmx exchange (rank %d): no receiver report for skey %llx bi %d (to rank %d) %.1f s "
+                    "after its round: resent over the mesh\n", o_.rank, (unsigned long long)it->first.first,
+                    it->first.second, it->second.dst, tnow - it->second.over_at);
           I.settle(it, out);
         }
         it = nx;
@@ -1486,7 +1508,13 @@ void Exchange::bulk_loop() {
       }
     }
     if (mf.es.empty() && !mf.fallback) continue;
-    if (mf.fallback || !ex->formed() || mf.epoch != epoch) {
+    bool fault_round = false;
+    if (early_r >= 0 && mf.round >= early_n && !mf.fallback && !early_done)
+      for (const WireEntry& e : mf.es) fault_round = fault_round || e.dst == early_r;
+    early_done = early_done || fault_round;
+    const bool fault_skip = fault_round && early_r == o_.rank;
+    if (fault_round && early_r != o_.rank) std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    if (mf.fallback || !ex->formed() || mf.epoch != epoch || fault_skip) {
       for (const WireEntry& e : mf.es) {
         if (e.src == o_.rank) mesh_fallback(e);
         // (a fallback manifest goes to senders only; otherwise the sender may be executing

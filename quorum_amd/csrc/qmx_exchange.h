@@ -132,6 +132,10 @@ class Exchange {
   // texts a round carried whose sender finished the round but whose receiver missed them
   // (it failed the round on another peer): resent over the mesh on the receiver's report
   uint64_t rescued() const { return rescued_.load(); }
+  // carried sends whose receiver never reported, resent over the mesh after timeout_s
+  uint64_t sweeps() const { return sweeps_.load(); }
+  // receiver reports that arrived before their send was carried (kept until it is)
+  uint64_t early_reports() const { return early_reports_.load(); }
   uint64_t links() const { return links_.load(); }  // per-loop links handed to the io loops
 
   struct Impl;
@@ -143,7 +147,7 @@ class Exchange {
   std::unique_ptr<Impl> im_;
   std::atomic<bool> stop_{false}, healthy_{false}, rccl_ok_{false};
   std::atomic<uint64_t> rounds_{0}, bytes_{0}, bulk_bytes_{0}, mesh_bulk_{0}, msgs_{0}, rccl_epoch_{0}, rejoins_{0},
-      downs_{0}, rescued_{0}, links_{0};
+      downs_{0}, rescued_{0}, links_{0}, sweeps_{0}, early_reports_{0};
   std::atomic<double> busy_us_{0};
   std::thread mesh_th_, bulk_th_;
   void mesh_loop();

@@ -324,6 +324,32 @@ def test_exchange_bulk_round_stall_falls_back_and_reforms(world):
         assert v["wave2_rounds"] > 0 and v["wave2_mesh_finals"] == 0, v  # ... and carries traffic
 
 
+@pytest.mark.parametrize("control", [False, True])
+def test_exchange_early_missed_report_is_kept(control):
+    """A receiver on another epoch reports "missed" as soon as it reads a round's manifest,
+    while its sender is still in its previous round: the report arrives before the send moves
+    into `await` (round-4 advisor finding: it was dropped, and the send waited forever).
+    QMX_XCHG_FAULT_EARLY_MISSED=1:3 — in the first global round >= 3 in which rank 1 receives,
+    it acts as such a receiver (its own sends take the mesh) and every other rank carries its
+    sends 100 ms late.  Every text
+    must arrive exactly once, each missed one resent at its round's end from the kept report,
+    never by the stale-await sweep (sweeps == 0).  control: the early reports dropped
+    (QMX_XCHG_DEBUG_DROP_EARLY, the round-4 behaviour) — only the sweep recovers them."""
+    env = {"QMX_XCHG_FAULT_EARLY_MISSED": "1:3"}
+    if control:
+        env["QMX_XCHG_DEBUG_DROP_EARLY"] = "1"
+    res = _selftest(3, "tcpbulk", 24, env=env, round_timeout=0.5, min_epochs=2, pace_ms=3.0)
+    assert sum(v["early_reports"] for v in res.values()) > 0, res  # the fault hit the path
+    sweeps = sum(v["sweeps"] for v in res.values())
+    if control:  # dropped reports: those texts wait for the sweep (3 round timeouts), or the test's end
+        assert sweeps > 0 or any(v["bulk"] < 24 * 2 for v in res.values()), res
+        return
+    assert all(v["ok"] for v in res.values()), res
+    for v in res.values():
+        assert v["bad"] == 0 and v["dups"] == 0 and v["bulk"] == v["sent"] == 24 * 2, v
+    assert sweeps == 0, res
+
+
 def test_idle_cluster_exchanges_nothing():
     """Event-driven exchange: once the traffic stops, a 3-rank cluster sends no mesh message
     and runs no bulk round (the r1 design paced all-gather rounds forever)."""
