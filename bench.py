@@ -431,8 +431,12 @@ def breakdown(m0, m1, elapsed):
                         for k in ("relay", "pickup", "grid_span")} if d.get("qmx_kernel_grid_ticks") else None,
         # loop ticks, host and device clocks calibrated against each other (HipGrid): the host's
         # post -> the relay saw it, the last item done -> the io loop took the results
-        "tick_hops_us_avg": {k: round(d.get(f"qmx_kernel_{k}_us", 0.0) / d["qmx_kernel_hop_ticks"], 1)
-                             for k in ("post_seen", "done_host")} if d.get("qmx_kernel_hop_ticks") else None,
+        # (clock_window: the offset's remaining uncertainty, upper − lower bound per 100 ms window)
+        "tick_hops_us_avg": dict({k: round(d.get(f"qmx_kernel_{k}_us", 0.0) / d["qmx_kernel_hop_ticks"], 1)
+                                  for k in ("post_seen", "done_host")},
+                                 clock_window=round(d["qmx_kernel_clock_window_us"] / d["qmx_kernel_clock_windows"], 2)
+                                 if d.get("qmx_kernel_clock_windows") else None)
+        if d.get("qmx_kernel_hop_ticks") else None,
         "tick_route_us_avg": round(1e6 * d.get("qmx_tick_route_seconds_total", 0.0) / ticks, 1) if ticks else None,
         # kernel seconds per wall second, SUMMED over the tick lanes (two lanes with kernels in
         # flight at once count twice): a lane-occupancy figure, not the GPU's busy fraction

@@ -267,6 +267,8 @@ struct TickLane {
   double span_ema_us = 30.0;  // kernel span per tick (device clock), smoothed: pipelined lanes
   double lead_ema_us = 8.0;   // persistent: doorbell seen -> first item started (device clock), smoothed
   double post_seen_us = 0, done_host_us = 0, hop_ticks = 0;  // loop ticks: host <-> device hops (calibrated)
+  // loop ticks: clock-offset bounds (host us − device us) from the ticks themselves, per 100 ms window
+  double clo = -1e300, chi = 1e300, clo_prev = -1e300, cwin_t0 = 0, cwin_sum = 0, cwin_n = 0;
   bool timing_pending = false;
   uint64_t poll_fallbacks = 0;
   // persistent mode (QMX_PERSISTENT=1): the lane's long-lived grid and its doorbell

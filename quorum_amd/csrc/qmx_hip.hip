@@ -3814,11 +3814,33 @@ void HipEngine::complete(HipJob& J, std::vector<SlotResult>& results, std::vecto
         const uint64_t tr = __atomic_load_n(&dr->t_relayed, __ATOMIC_ACQUIRE);
         if (ts && tr >= ts && a >= tr && b >= a) {
           L.lead_ema_us = 0.85 * L.lead_ema_us + 0.15 * std::min((double)(a - ts) * 1e-2, 500.0);
-          const double off = grid_ ? grid_->clock_offset_us() : __builtin_nan("");
-          if (off == off) {  // calibrated: the hops between the two clocks
+          if (grid_) {
+            // the hops between the two clocks.  Every tick bounds the clock offset (host time −
+            // device time): the relay saw the doorbell after the host posted it (off >= post −
+            // seen) and the host took the results after the last item finished (off <= now −
+            // done).  The offset used is the largest lower bound of the current 100 ms window
+            // (and the previous one: drift between the host clock and the 100 MHz device
+            // clock stays far below a microsecond there), which includes this tick's: no hop
+            // can come out negative.  The window's upper − lower bound is the uncertainty left
+            // (clock_window_us); the symmetric round-trip calibration (HipGrid::calibrate) it
+            // replaces read post -> seen 1.1 us too short (r4: negative).
             const double post_h = std::chrono::duration<double, std::micro>(J.tp1.time_since_epoch()).count();
-            const double seen_h = (double)ts * 1e-2 + off, done_h = (double)b * 1e-2 + off;
             const double now_h = std::chrono::duration<double, std::micro>(HC::now().time_since_epoch()).count();
+            const double lo = post_h - (double)ts * 1e-2, hi = now_h - (double)b * 1e-2;
+            if (now_h - L.cwin_t0 > 1e5) {  // a new window
+              L.clo_prev = L.clo;
+              if (L.clo > -1e299 && L.chi < 1e299 && L.chi >= L.clo) {
+                L.cwin_sum += L.chi - L.clo;
+                ++L.cwin_n;
+              }
+              L.clo = -1e300;
+              L.chi = 1e300;
+              L.cwin_t0 = now_h;
+            }
+            L.clo = std::max(L.clo, lo);
+            L.chi = std::min(L.chi, hi);
+            const double off = std::max(L.clo, L.clo_prev);
+            const double seen_h = (double)ts * 1e-2 + off, done_h = (double)b * 1e-2 + off;
             if (seen_h >= post_h - 5.0 && now_h >= done_h - 5.0) {
               L.post_seen_us += seen_h - post_h;
               L.done_host_us += now_h - done_h;
@@ -4146,6 +4168,8 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["post_seen_us"] += L.post_seen_us;  // loop ticks: host post -> relay saw it (calibrated clocks)
     m["done_host_us"] += L.done_host_us;  // last item done -> the io loop took the results
     m["hop_ticks"] += L.hop_ticks;
+    m["clock_window_us"] += L.cwin_sum;  // summed over 100 ms windows (mean: / clock_windows)
+    m["clock_windows"] += L.cwin_n;
     m["start_spread_us"] += L.start_spread_us;
     m["process_us"] += L.process_us;
     m["poll_fallbacks"] += (double)L.poll_fallbacks;

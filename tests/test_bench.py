@@ -277,9 +277,10 @@ def test_breakdown_loop_tick_fields():
               qmx_kernel_done_host_us=1400.0, qmx_kernel_stage_items=40.0, qmx_kernel_s3_events=1080.0,
               qmx_kernel_s3_full_parses=0.0, qmx_kernel_s3_template_hits=960.0, qmx_kernel_s3_hole_hits=80.0,
               qmx_kernel_stage4_us=240.0, qmx_kernel_clk_cycles=2.4e6, qmx_kernel_clk_us=1000.0,
-              qmx_tick_seconds_count=110.0, qmx_tick_seconds_sum=5.5e-3)
+              qmx_tick_seconds_count=110.0, qmx_tick_seconds_sum=5.5e-3, qmx_kernel_clock_window_us=12.0,
+              qmx_kernel_clock_windows=40.0)
     bd = bench.breakdown(m0, m1, 1.0)
-    assert bd["tick_hops_us_avg"] == {"post_seen": 1.5, "done_host": 13.0}
+    assert bd["tick_hops_us_avg"] == {"post_seen": 1.5, "done_host": 13.0, "clock_window": 0.3}
     assert bd["s3_per_item"] == {"events": 27.0, "full_parses": 0.0, "template_hits": 24.0, "hole_hits": 2.0}
     assert bd["stage_us_per_item"]["stage4_us"] == 6.0
     assert bd["shader_mhz"] == 2400.0
