@@ -808,18 +808,26 @@ void Exchange::expect_bulk(uint64_t skey, int bi, void* dev, size_t cap) {
   k.dev = dev;
   k.cap = cap;
 }
-void Exchange::forget_bulk(uint64_t skey, int bi) {
+bool Exchange::forget_bulk(uint64_t skey, int bi) {
   // a round receiving into this sink right now writes it until the round is over: wait (a
   // session that ends while its remote final is in flight — a client that left — is rare,
-  // and a round is bounded by timeout_s), so a returned forget_bulk() means no later write
-  // into the released slot
+  // and a round is bounded by timeout_s), so a true return means no later write into the
+  // released slot.  A round that outlives twice its timeout (its communicator could not be
+  // drained) returns false: the caller must not reuse the slot (it leaks it, loudly).
   std::unique_lock<std::mutex> g(im_->bmu);
+  const double t0 = now_s();
   for (;;) {
     auto it = im_->sinks.find({skey, bi});
-    if (it == im_->sinks.end()) return;
+    if (it == im_->sinks.end()) return true;
     if (it->second.pinned <= 0 || stop_.load()) {
       im_->sinks.erase(it);
-      return;
+      return true;
+    }
+    if (now_s() - t0 > 2.0 * o_.timeout_s + 1.0) {
+      fprintf(stderr, "qmx exchange (rank %d): a bulk round still writes into the shadow slot of session %llx "
+              "stream %d after %.1f s: the slot is not reused\n", o_.rank, (unsigned long long)skey, bi,
+              now_s() - t0);
+      return false;
     }
     im_->bcv.wait_for(g, std::chrono::milliseconds(1));
   }

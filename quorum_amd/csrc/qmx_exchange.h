@@ -109,7 +109,9 @@ class Exchange {
   // Owner: a bulk for (skey, bi) lands at `dev` (HBM, capacity `cap`); nullptr / a mesh
   // transfer delivers the bytes in X_BULK's payload instead.
   void expect_bulk(uint64_t skey, int bi, void* dev, size_t cap);
-  void forget_bulk(uint64_t skey, int bi);
+  // false: a round is still writing into the sink (stuck past twice its timeout) — the
+  // caller must not reuse the slot
+  bool forget_bulk(uint64_t skey, int bi);
   void request_stop();
   void join();
   bool healthy() const { return healthy_.load(); }  // the mesh formed once and is running

@@ -3081,11 +3081,11 @@ class Loop {
         b.up = nullptr;
       }
       // a shadow slot: no RCCL round may write into it once released (forget_bulk waits
-      // for a copy in progress)
-      if (b.remote >= 0 && xch_ && s->skey) xch_->forget_bulk(s->skey, i);
+      // for a round receiving into it; a round stuck past twice its timeout: the slot leaks)
+      const bool reusable = !(b.remote >= 0 && xch_ && s->skey) || xch_->forget_bulk(s->skey, i);
       if (b.slot >= 0) {
         slot_owner_.erase(b.slot);
-        e_release(b.slot);
+        if (reusable) e_release(b.slot);
         b.slot = -1;
       }
     }
