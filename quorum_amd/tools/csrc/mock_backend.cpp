@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <strings.h>
 #include <map>
 #include <queue>
 #include <random>
@@ -211,17 +212,19 @@ void worker(int tid) {
       if (he == std::string::npos) return true;
       size_t cl = 0;
       {
-        // case-insensitive content-length
-        std::string h = c.in.substr(0, he);
-        for (auto& ch : h) ch = (char)tolower(ch);
-        size_t p = h.find("content-length:");
-        if (p != std::string::npos) cl = strtoul(h.c_str() + p + 15, nullptr, 10);
+        // case-insensitive content-length, found in place (no copy of the headers)
+        static const char kCl[] = "content-length:";
+        for (size_t i = 0; i + sizeof(kCl) - 1 <= he; ++i) {
+          if ((c.in[i] | 0x20) != 'c' || strncasecmp(c.in.data() + i, kCl, sizeof(kCl) - 1) != 0) continue;
+          cl = strtoul(c.in.data() + i + sizeof(kCl) - 1, nullptr, 10);
+          break;
+        }
       }
       if (c.in.size() < he + 4 + cl) return true;
-      std::string body = c.in.substr(he + 4, cl);
+      const char* body = c.in.data() + he + 4;
+      const bool stream = memmem(body, cl, "\"stream\": true", 14) != nullptr ||
+                          memmem(body, cl, "\"stream\":true", 13) != nullptr;
       c.in.erase(0, he + 4 + cl);
-      bool stream = body.find("\"stream\": true") != std::string::npos ||
-                    body.find("\"stream\":true") != std::string::npos;
       if (g.stall_ms > 0) {
         c.stalled = true;
         continue;
