@@ -25,6 +25,8 @@
 #                         counters per dispatch and per tick
 #   kbench                tools/kbench.py in-kernel stage split (QMX_STAGE_TIMING)
 #   kbenchgrid            the same on the persistent grid (the production kernel)
+#   kbenchshape:SHAPE     the grid stage split on another stream shape (tools/kbench.py --shape: tagdense)
+#   pmcshape:SHAPE:C,...  rocprofv3 --pmc on the production kernel for that shape, per tick
 #   multirank=N           bench.py under torch.distributed.run with N ranks sharing GPU 0
 #   spread=N              same, --placement spread over the TCP exchange
 #   cpuprof               headline bench with the in-process CPU profiler on the proxy
@@ -173,6 +175,24 @@ for l in sys.stdin:
     d=json.loads(l); st=d.get('stage_us_per_item',{})
     print(d['slots'], 'wall', d['wall_us_p50'], 'kern', d.get('kernel_us_avg'), 'fence', st.get('stage_fence_us'), [st.get('stage%d_us'%k) for k in range(1,11)])
 " ;;
+    kbenchshape:*)  # kbenchshape:SHAPE — stage split of the production kernel on another stream shape
+      shp=${step#kbenchshape:}
+      QMX_STAGE_TIMING=1 timeout -k 10 300 python tools/kbench.py --grid 16 --slots 1,3 --iters 100 --combos ft --shape $shp > $OUT/kbench_$shp.jsonl 2>&1 \
+        || { echo "kbenchshape failed"; tail -5 $OUT/kbench_$shp.jsonl; exit 1; }
+      grep -v '^{"grid_stats' $OUT/kbench_$shp.jsonl | python3 -c "
+import json, sys
+for l in sys.stdin:
+    if not l.startswith('{'): continue
+    d=json.loads(l); st=d.get('stage_us_per_item',{})
+    print(d['shape'], d['slots'], 'wall', d['wall_us_p50'], 'kern', d.get('kernel_us_avg'), [st.get('stage%d_us'%k) for k in range(1,11)], {k[6:-3]: v for k, v in st.items() if k.startswith('stage_s4')})
+" ;;
+    pmcshape:*)  # pmcshape:SHAPE:C1,C2 — counters of qmx_tick_persistent on another stream shape, per tick
+      rest=${step#pmcshape:}; shp=${rest%%:*}; ctr=${rest#*:}; slug=$(echo "${shp}_$ctr" | tr -c 'a-zA-Z0-9' '_' | cut -c1-60)
+      timeout -s KILL 120 rocprofv3 --pmc ${ctr//,/ } -d $OUT/pmcs_$slug -o pmc --output-format csv -- \
+        python3 tools/kbench.py --grid 16 --slots 3 --iters 400 --combos ft --shape $shp > $OUT/pmcs_$slug.log 2>&1 \
+        || { echo "pmcshape $ctr failed"; tail -10 $OUT/pmcs_$slug.log; exit 1; }
+      python3 tools/pmc_summary.py --per-tick 400 $(find $OUT/pmcs_$slug -name '*counter_collection.csv') > $OUT/pmcs_$slug.md 2>&1
+      grep -v rocclr $OUT/pmcs_$slug.md | head -14 ;;
     kbench)
       QMX_PERSISTENT=0 QMX_STAGE_TIMING=1 timeout -k 10 300 python tools/kbench.py --slots 1,22,64,256 --iters 20 > $OUT/kbench.jsonl 2>&1 \
         || { echo "kbench failed"; tail -5 $OUT/kbench.jsonl; exit 1; }

@@ -30,6 +30,24 @@ def mock_stream(tokens=20, think=True):
     return b"".join(out)
 
 
+def tagdense_stream(tokens=20):
+    """Tag-dense content (markup / code the filter must scan: every token has '<' bytes —
+    real tags, near misses, comparisons, nested think blocks): the shape where the MFMA
+    matcher does the work (one v_mfma_i32_16x16x64_i8 per 16 '<' candidates)."""
+    def ev(delta, finish="null"):
+        return ('data: {"id": "chatcmpl-mock", "object": "chat.completion.chunk", "created": 1700000000, '
+                '"model": "mock", "choices": [{"index": 0, "delta": %s, "finish_reason": %s}]}\n\n'
+                % (delta, finish)).encode()
+    pieces = ["<div><b>x</b> <think>a<reason>b</reason>c</think> y",
+              " if (a < b && c <d) <thin> <thought>t</thought> ",
+              "<reasoning>r</REASONING> <Think>z</THINK> <th", "ink>k</think> <table><tr><td>1</td></tr>",
+              " <thoughts> <reason-> <reasonin> </ <<think>q</think>>"]
+    out = [ev('{"role": "assistant", "content": ""}')]
+    out += [ev('{"content": "%s"}' % pieces[i % len(pieces)]) for i in range(tokens)]
+    out += [ev("{}", '"stop"'), b"data: [DONE]\n\n"]
+    return b"".join(out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--slots", default="1,16,64,256,1024")
@@ -40,12 +58,14 @@ def main():
                          "production kernel qmx_tick_persistent) instead of one-shot launches")
     ap.add_argument("--combos", default="ft,f,t",
                     help="(filter, emit) combinations: ft = filter+emit, f = filter only, t = emit only")
+    ap.add_argument("--shape", default="mock", choices=["mock", "tagdense"],
+                    help="mock: the benchmark's upstream stream; tagdense: '<'-heavy content (MFMA matcher load)")
     ap.add_argument("--events-per-tick", type=int, default=0,
                     help="stream the body N events per tick (steady-state serving shape); 0 = whole body in one tick")
     args = ap.parse_args()
     from quorum_amd.ops.native import NativeEngine
 
-    body = mock_stream()
+    body = mock_stream() if args.shape == "mock" else tagdense_stream()
     tags = ["think", "reason", "reasoning", "thought"]
     results = []
     grid = None
@@ -76,7 +96,8 @@ def main():
                     eng.release(s)
             st = eng._e.kernel_stats() if args.engine == "hip" else {}
             walls.sort()
-            rec = {"filter": filt, "emit": emit, "slots": n, "bytes_per_slot": len(body), "events_per_tick": k,
+            rec = {"filter": filt, "emit": emit, "shape": args.shape, "slots": n, "bytes_per_slot": len(body),
+                   "events_per_tick": k,
                    "wall_us_p50": round(1e6 * walls[len(walls) // 2], 1),
                    "wall_us_min": round(1e6 * walls[0], 1)}
             if st:
