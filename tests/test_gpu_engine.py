@@ -278,6 +278,29 @@ def test_hip_finalize_long_texts_many_texts_on_gpu(ext, seed):
         assert st["fin_separate_launches"] == 0, st  # finalize rides the tick launch
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_hip_tagdense_matches_cpu(ext, seed):
+    """tools/kbench.py's tag-dense shape (120 '<' per 5 KB stream: tags, near misses, nested
+    and split think blocks — eight MFMA match groups per tile) through the HIP engine, split
+    at random points, byte-equal to the C++ CPU engine with no host escalation."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import kbench
+
+    rng = random.Random(900 + seed)
+    tags = ["think", "reason", "reasoning", "thought"]
+    raw = kbench.tagdense_stream(tokens=rng.randint(10, 40))
+    streams = [H.split_random(rng, raw, rng.choice([64, 400, 6000])) for _ in range(6)]
+    n = len(streams)
+    cpu = H.run_engine(NativeEngine("cpu", tags), streams, [True] * n, [True] * n, random.Random(seed))
+    eng = _hip(tags)
+    hip = H.run_engine(eng, streams, [True] * n, [True] * n, random.Random(seed))
+    assert hip == cpu
+    _gpu_did_it(eng)
+
+
 class _Poisoned:
     """An engine whose result records are refilled before every tick with the sequence number
     that tick will publish (done, nothing consumed, no output) — what pinned pages recycled
