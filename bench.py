@@ -389,6 +389,27 @@ def cpu_seconds(pid: int) -> float:
         return 0.0
 
 
+def cgroup_cpu_stat() -> dict:
+    """The job's cgroup CPU accounting (cgroup v2 cpu.stat + cpu.max): a CPU quota throttles
+    every process of the job for the rest of a period once it is used up — latency spikes the
+    breakdown should show, not hide."""
+    out = {}
+    for path, keys in (("/sys/fs/cgroup/cpu.stat", ("usage_usec", "nr_periods", "nr_throttled", "throttled_usec")),):
+        try:
+            for ln in open(path):
+                k, _, v = ln.partition(" ")
+                if k in keys:
+                    out[k] = int(v)
+        except (OSError, ValueError):
+            pass
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        out["quota_cpus"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return out
+
+
 def cpu_snapshot(mock_procs, proxy_procs):
     import resource
 
@@ -1117,6 +1138,7 @@ def main() -> int:
         scraped = args.impl == "native" and not direct
         m0 = scrape(admin_port) if scraped else {}
         c0 = cpu_snapshot(mock_procs, proxy_procs)
+        g0 = cgroup_cpu_stat()
         t0 = time.perf_counter()
         stats = loadgen(bin_dir, proxy_port, args.conns, args.steps * args.batch, args.lg_threads, args.timeout,
                         spec_path, path, stream)
@@ -1126,9 +1148,16 @@ def main() -> int:
             _barrier(dist, coll_cuda)
         elapsed = time.perf_counter() - t0
         c1 = cpu_snapshot(mock_procs, proxy_procs)
+        g1 = cgroup_cpu_stat()
         bd = breakdown(m0, scrape(admin_port), elapsed) if scraped else {}
         bd["pid"] = proxy_procs[0].pid if proxy_procs else None
         bd.update(cpu_breakdown(c0, c1, stats["completed"], elapsed))
+        if g0 and g1:  # the whole job's CPU over the timed region, and any quota throttling
+            bd["cgroup"] = {"quota_cpus": g1.get("quota_cpus"),
+                            "cores_busy": round((g1.get("usage_usec", 0) - g0.get("usage_usec", 0)) / 1e6 / elapsed, 2)
+                            if elapsed else None,
+                            "throttled_periods": g1.get("nr_throttled", 0) - g0.get("nr_throttled", 0),
+                            "throttled_ms": round((g1.get("throttled_usec", 0) - g0.get("throttled_usec", 0)) / 1e3, 1)}
         dead = casualties()
         if dead and not dead_warm:
             print(f"bench rank {rank}: server process(es) exited during the timed steps: {dead}", file=sys.stderr,
