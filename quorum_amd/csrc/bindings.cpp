@@ -141,6 +141,9 @@ ServerCfg server_cfg_from(const py::dict& d) {
   gs("intermediate_separator", c.intermediate_separator); gs("query_format", c.query_format);
   gs("source_label_format", c.source_label_format); gb("include_original_query", c.include_original_query);
   gb("include_source_names", c.include_source_names); gs("env_api_key", c.env_api_key);
+  gb("documented", c.documented); gb("strip_intermediate", c.strip_intermediate);
+  gb("hide_aggregator_think", c.hide_aggregator_think); gb("sources_all", c.sources_all);
+  if (d.contains("sources")) c.sources = py::cast<std::vector<std::string>>(d["sources"]);
   gb("api_key_from_env", c.api_key_from_env); gs("openapi_json", c.openapi_json); gs("docs_html", c.docs_html);
   gs("redoc_html", c.redoc_html); gs("oauth2_redirect_html", c.oauth2_redirect_html);
   gb("install_signals", c.install_signals);

@@ -421,6 +421,7 @@ struct Session {
   int fin_id = -1;
   bool fin_texts = false;
   std::vector<std::string> texts;
+  std::vector<std::string> text_names;  // documented semantics: each text's backend name
   Up* agg = nullptr;
   // single-stream passthrough
   // body with "model" replaced = mpre + dumps(model) + mpost (built once per request,
@@ -2400,10 +2401,30 @@ class Loop {
     // (spread owners included: remote streams' texts sit in their shadow slots)
     std::vector<int> g = good_slots(s);
     bool texts = !cfg_.aggregator_name.empty();
+    bool strip = cfg_.hide_final;
+    if (texts && cfg_.documented) {
+      // documented semantics: only the source backends feed the aggregator, stripped with
+      // strip_intermediate_thinking; the finalize keeps the texts of slots with content, in
+      // slot order, so their backends' names are known here (the prompt's source labels)
+      g.clear();
+      s->text_names.clear();
+      for (auto& b : s->bs)
+        if (b.state == 1 && !b.aborted && is_source(b.backend)) {
+          g.push_back(b.slot);
+          if (eng().content_size(b.slot) > 0) s->text_names.push_back(cfg_.backends[b.backend].name);
+        }
+      strip = strip || cfg_.strip_intermediate;
+    }
     s->fin_texts = texts;
-    s->fin_id = e_submit(g, cfg_.hide_final, texts, "\n" + cfg_.separator, (int64_t)time(nullptr));
+    s->fin_id = e_submit(g, strip, texts, "\n" + cfg_.separator, (int64_t)time(nullptr));
     fin_owner_[s->fin_id] = {s, -1};
     kick();
+  }
+  bool is_source(int backend) const {
+    if (cfg_.sources_all) return true;
+    for (const auto& n : cfg_.sources)
+      if (n == cfg_.backends[backend].name) return true;
+    return false;
   }
   void post_owner(Session* s, uint8_t type, uint8_t flags, int a, const std::string& payload, int b = 0) {
     post_owner(s, type, flags, a, payload.data(), payload.size(), b);
@@ -2766,7 +2787,9 @@ class Loop {
     for (size_t i = 0; i < s->texts.size(); ++i) {
       if (cfg_.include_source_names) {
         std::string lab;
-        if (!py_format(cfg_.source_label_format, "backend_name", "LLM" + std::to_string(i + 1), lab))
+        const std::string name = cfg_.documented && i < s->text_names.size() ? s->text_names[i]
+                                                                              : "LLM" + std::to_string(i + 1);
+        if (!py_format(cfg_.source_label_format, "backend_name", name, lab))
           return aggregate_result(s, JVal::str(joined(s->texts, exc_joiner)));
         parts.push_back(lab + s->texts[i]);
       } else {
@@ -2829,6 +2852,8 @@ class Loop {
       if (ch && ch->t == JVal::ARR && !ch->a.empty()) {
         const JVal* msg = ch->a[0].get("message");
         const JVal* ct = msg ? msg->get("content") : nullptr;
+        if (ct && cfg_.documented && cfg_.hide_aggregator_think && ct->t == JVal::STR)
+          return aggregate_result(s, JVal::str(strip_final(ts_, (const uint8_t*)ct->s.data(), ct->s.size())));
         if (ct) return aggregate_result(s, *ct);
       }
     }
@@ -2953,6 +2978,8 @@ class Loop {
       return end_session(s);
     }
     // parallel combine (quorum :1191-1341)
+    const bool agg = !cfg_.aggregator_name.empty();
+    const bool strip = cfg_.hide_final || (cfg_.documented && agg && cfg_.strip_intermediate);
     std::vector<std::string> processed;
     std::string err;
     for (BState* b : ok) {
@@ -2974,10 +3001,10 @@ class Loop {
         break;
       }
       if (content->t != JVal::STR) {
-        err = cfg_.hide_final ? "expected string or bytes-like object" : "sequence item 0: expected str instance";
+        err = strip ? "expected string or bytes-like object" : "sequence item 0: expected str instance";
         break;
       }
-      processed.push_back(cfg_.hide_final ? strip_final(ts_, (const uint8_t*)content->s.data(),
+      processed.push_back(strip ? strip_final(ts_, (const uint8_t*)content->s.data(),
                                                         content->s.size())
                                           : content->s);
     }
@@ -2985,9 +3012,26 @@ class Loop {
       if (s->cl) respond(s->cl, 500, "application/json", err_json("Error combining responses: " + err, "proxy_error"));
       return end_session(s);
     }
+    if (cfg_.documented) {
+      std::vector<std::string> names, kept;
+      for (size_t i = 0; i < ok.size(); ++i)
+        if (!agg || is_source(ok[i]->backend)) {
+          names.push_back(cfg_.backends[ok[i]->backend].name);
+          kept.push_back(std::move(processed[i]));
+        }
+      processed.swap(kept);
+      if (processed.empty()) {
+        if (s->cl) respond(s->cl, 500, "application/json", err_json("All source backends failed", "proxy_error"));
+        return end_session(s);
+      }
+      bool sup = cfg_.suppress;
+      if (const JVal* v = s->body.get("suppress_individual_responses")) sup = v->truthy();
+      if (sup && !agg) return finish_nonstream_combined(s, JVal::str(processed[0]));  // "only the first"
+      s->text_names = std::move(names);
+    }
     s->texts = processed;
     s->fin_texts = true;
-    if (!cfg_.aggregator_name.empty()) return start_aggregator(s, cfg_.separator);
+    if (agg) return start_aggregator(s, cfg_.separator);
     finish_nonstream_combined(s, JVal::str(joined(processed, cfg_.separator)));
   }
   void finish_nonstream_combined(Session* s, const JVal& combined) {

@@ -55,6 +55,12 @@ struct ServerCfg {
   std::string aggregator_name;  // empty = none
   std::string prompt_template, intermediate_separator, query_format, source_label_format;
   bool include_original_query = true, include_source_names = false;
+  // semantics "documented" (utils/config.py SEMANTICS): the flags of the reference's
+  // docs/aggregate_behaviour.md, which its code ignores — source_backends (sources_all false:
+  // only `sources` feed the aggregator), strip_intermediate_thinking, hide_aggregator_thinking,
+  // backend-name source labels, non-stream suppress = the first response
+  bool documented = false, strip_intermediate = false, hide_aggregator_think = false, sources_all = true;
+  std::vector<std::string> sources;
   std::string env_api_key;         // static OPENAI_API_KEY (tests; api_key_from_env = false)
   bool api_key_from_env = false;   // read OPENAI_API_KEY per request, as quorum (oai_proxy.py:981)
   // FastAPI's default documentation routes of the reference app (oai_proxy.py:70): the

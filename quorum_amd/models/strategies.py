@@ -11,13 +11,17 @@ Semantics kept from quorum: labels are ``LLM{i+1}`` by posi
 the *successful* texts; ``source_backends`` is parsed but all valid backends are sources;
 the aggregator is consulted whenever ``strategy.aggregate.aggregator_backend`` is set,
 whatever strategy is selected; the aggregator's answer is returned as-is (no strip).
+With ``semantics: documented`` (utils/config.py SEMANTICS) the flags of the reference's
+docs/aggregate_behaviour.md apply instead: labels carry the backend's name, only
+``source_backends`` feed the aggregator (callers filter), their texts are stripped with
+``strip_intermediate_thinking`` (callers strip) and the answer with ``hide_aggregator_thinking``.
 """
 from __future__ import annotations
 
 import json
 import logging
 import os
-from typing import Any, Dict, List, Optional
+from typing import Any, Callable, Dict, List, Optional
 
 from ..server.transport import UpstreamPool, call_backend
 from ..utils.logging_setup import log_content, redact
@@ -39,12 +43,14 @@ def first_user_message(json_body: Dict[str, Any]) -> Any:
 def build_aggregator_prompt(source_responses: List[str], user_query: Any, separator: str,
                             include_original_query: bool, query_format: str,
                             include_source_names: bool, source_label_format: str,
-                            prompt_template: str) -> str:
-    """reference oai_proxy.py:406-423."""
+                            prompt_template: str, source_names: Optional[List[str]] = None) -> str:
+    """reference oai_proxy.py:406-423; ``source_names`` (documented mode) replaces the
+    positional ``LLM{i+1}`` labels with the backends' names."""
     parts = []
     for i, text in enumerate(source_responses):
         if include_source_names:
-            parts.append(source_label_format.format(backend_name=f"LLM{i + 1}") + text)
+            label = source_names[i] if source_names is not None else f"LLM{i + 1}"
+            parts.append(source_label_format.format(backend_name=label) + text)
         else:
             parts.append(text)
     prompt = query_format.format(query=user_query) if include_original_query else ""
@@ -86,13 +92,17 @@ async def aggregate_responses(
     prompt_template: str = DEFAULT_PROMPT_TEMPLATE,
     headers: Optional[Dict[str, str]] = None,
     pool: Optional[UpstreamPool] = None,
+    source_names: Optional[List[str]] = None,
+    strip_answer: Optional[Callable[[str], str]] = None,
 ) -> str:
     """Synthesis call to the aggregator backend; plain join on any failure.
 
-    Unlike quorum this never logs the Authorization header (oai_proxy.py:468 does)."""
+    Unlike quorum this never logs the Authorization header (oai_proxy.py:468 does).
+    ``strip_answer`` (documented ``hide_aggregator_thinking``) applies to a string answer."""
     prompt = build_aggregator_prompt(source_responses, user_query, separator,
                                      include_original_query, query_format,
-                                     include_source_names, source_label_format, prompt_template)
+                                     include_source_names, source_label_format, prompt_template,
+                                     source_names)
     clean = aggregator_headers(headers)
     if clean is None:
         aggregation_logger.error("no Authorization header or OPENAI_API_KEY for the aggregator")
@@ -106,6 +116,8 @@ async def aggregate_responses(
         res = await call_backend(aggregator_backend, json.dumps(body).encode(), clean, 60.0, pool=pool)
         if res["status_code"] == 200:
             out = res["content"]["choices"][0]["message"]["content"]
+            if strip_answer is not None and isinstance(out, str):
+                out = strip_answer(out)
             if log_content():
                 aggregation_logger.info("aggregator result: %s", out)
             return out
@@ -117,7 +129,8 @@ async def aggregate_responses(
 
 async def combine_finals(texts: List[str], cfg: Dict[str, Any], agg: AggregateSettings,
                          json_body: Dict[str, Any], headers: Dict[str, str], joiner: str,
-                         pool: Optional[UpstreamPool] = None) -> str:
+                         pool: Optional[UpstreamPool] = None, source_names: Optional[List[str]] = None,
+                         strip_answer: Optional[Callable[[str], str]] = None) -> str:
     """Final combine shared by stream (joiner = "\\n"+sep) and non-stream (joiner = sep)."""
     from ..utils.config import find_backend
 
@@ -130,7 +143,8 @@ async def combine_finals(texts: List[str], cfg: Dict[str, Any], agg: AggregateSe
             return await aggregate_responses(
                 texts, backend, first_user_message(json_body), agg.intermediate_separator,
                 agg.include_original_query, agg.query_format, agg.include_source_names,
-                agg.source_label_format, agg.prompt_template, headers, pool=pool)
+                agg.source_label_format, agg.prompt_template, headers, pool=pool,
+                source_names=source_names, strip_answer=strip_answer)
         except Exception as exc:  # noqa: BLE001 - reference :832-834 / :1275-1279
             aggregation_logger.error("error during aggregation: %s", exc)
             return joiner.join(texts)

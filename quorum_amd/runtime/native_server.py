@@ -62,6 +62,9 @@ def native_config(cfg: Dict[str, Any], host: str, port: int, engine: str, device
         "source_label_format": str(agg.source_label_format),
         "include_original_query": bool(agg.include_original_query),
         "include_source_names": bool(agg.include_source_names),
+        "documented": bool(agg.documented), "strip_intermediate": bool(agg.strip_intermediate_thinking),
+        "hide_aggregator_think": bool(agg.hide_aggregator_thinking),
+        "sources_all": agg.sources() is None, "sources": list(agg.sources() or []),
         "env_api_key": "", "api_key_from_env": True,  # per request, as quorum (oai_proxy.py:981)
         "backends": backends,
         "drain_s": float(rt.drain_timeout), "verify": bool(rt.verify),

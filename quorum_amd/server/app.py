@@ -176,10 +176,16 @@ class ProxyService:
                 joiner = "\n" + flags.separator
                 good = sess.good_slots()
                 if agg.aggregator_backend:
-                    texts = await ticker.finalize(FinalizeRequest(good, bool(flags.hide_final_think), "texts"))
+                    names, strip_answer = None, None
+                    if agg.documented:
+                        texts, names, strip_answer = await self._documented_sources(
+                            ticker, sess, backends, good, agg, flags, rt)
+                    else:
+                        texts = await ticker.finalize(FinalizeRequest(good, bool(flags.hide_final_think), "texts"))
                     if texts:
                         combined = await combine_finals(texts, cfg, agg, json_body, headers, joiner,
-                                                        pool=self._pool())
+                                                        pool=self._pool(), source_names=names,
+                                                        strip_answer=strip_answer)
                         yield ref.final_event(int(time.time()), combined)
                     else:
                         yield ref.error_event(int(time.time()))
@@ -193,6 +199,26 @@ class ProxyService:
                 if not t.done():
                     t.cancel()
             ticker.release(sess)
+
+    @staticmethod
+    async def _documented_sources(ticker, sess, backends, good, agg, flags, rt):
+        """``semantics: documented`` aggregator inputs: the texts of the ``source_backends``
+        among the good slots, stripped when ``strip_intermediate_thinking`` (or
+        hide_final_think) is set, with their backends' names; one finalize per slot keeps each
+        kept text paired with its backend (a slot with no content contributes nothing, as in
+        the batched finalize)."""
+        name_of = {slot: b.get("name") for slot, b in zip(sess.slots, backends)}
+        src = agg.sources()
+        if src is not None:
+            good = [s for s in good if name_of[s] in src]
+        strip = bool(flags.hide_final_think or agg.strip_intermediate_thinking)
+        texts, names = [], []
+        for slot in good:
+            t = await ticker.finalize(FinalizeRequest([slot], strip, "texts"))
+            if t:
+                texts.append(t[0])
+                names.append(name_of[slot])
+        return texts, names, _answer_stripper(agg, rt, flags)
 
     # ------------------------------------------------------------------
     async def single_stream(self, cfg, backend, body, json_body, headers, timeout) -> Response:
@@ -219,7 +245,8 @@ class ProxyService:
                 return _json_error(f"All backends failed. First error: {error_message(responses[0])}",
                                    "proxy_error", 500)
             if parallel:
-                return await self._combine_non_stream(cfg, ok, json_body, headers)
+                names = [b.get("name") for b, r in zip(backends, responses) if r["status_code"] == 200]
+                return await self._combine_non_stream(cfg, ok, json_body, headers, names)
             first = ok[0]
             ctype = first["headers"].get("content-type", "application/json")
             content = json.dumps(first["content"]) if isinstance(first["content"], (dict, list)) \
@@ -233,16 +260,27 @@ class ProxyService:
         except Exception as exc:  # noqa: BLE001 - reference :1381-1394
             return _json_error(f"Error processing request: {exc}", "proxy_error", 500)
 
-    async def _combine_non_stream(self, cfg, ok, json_body, headers) -> Response:
+    async def _combine_non_stream(self, cfg, ok, json_body, headers, names) -> Response:
         flags = resolve_flags(cfg, json_body)
         try:
             rt = self._runtime(cfg)
             stripper = _stripper(rt, flags.thinking_tags)
-            processed = [stripper(r["content"]["choices"][0]["message"]["content"],
-                                  flags.hide_final_think) for r in ok]
             agg = resolve_aggregate(cfg)
-            combined = await combine_finals(processed, cfg, agg, json_body, headers, flags.separator,
-                                            pool=self._pool())
+            doc = agg.documented
+            strip = flags.hide_final_think or bool(doc and agg.aggregator_backend and agg.strip_intermediate_thinking)
+            processed = [stripper(r["content"]["choices"][0]["message"]["content"], strip) for r in ok]
+            src = agg.sources() if agg.aggregator_backend else None
+            if src is not None:  # documented source_backends
+                keep = [i for i, n in enumerate(names) if n in src]
+                processed, names = [processed[i] for i in keep], [names[i] for i in keep]
+                if not processed:
+                    return _json_error("All source backends failed", "proxy_error", 500)
+            if doc and flags.suppress_individual_responses and not agg.aggregator_backend:
+                combined = processed[0]  # documented: "only the first response"
+            else:
+                combined = await combine_finals(processed, cfg, agg, json_body, headers, flags.separator,
+                                                pool=self._pool(), source_names=names if doc else None,
+                                                strip_answer=_answer_stripper(agg, rt, flags))
             usage = {k: sum(r["content"]["usage"][k] for r in ok)
                      for k in ("prompt_tokens", "completion_tokens", "total_tokens")}
             first = ok[0]["content"]
@@ -260,6 +298,14 @@ class ProxyService:
         except Exception as exc:  # noqa: BLE001 - reference :1342-1355
             logger.error("error combining responses: %s", exc)
             return _json_error(f"Error combining responses: {exc}", "proxy_error", 500)
+
+
+def _answer_stripper(agg, rt: RuntimeConfig, flags):
+    """documented ``hide_aggregator_thinking``: the aggregator's answer loses its thinking."""
+    if not (agg.documented and agg.hide_aggregator_thinking):
+        return None
+    strip = _stripper(rt, flags.thinking_tags)
+    return lambda text: strip(text, True)
 
 
 def _stripper(rt: RuntimeConfig, tags: List[str]):

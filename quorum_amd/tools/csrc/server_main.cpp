@@ -75,6 +75,12 @@ int main(int argc, char** argv) {
   c.source_label_format = gs(d, "source_label_format", "");
   c.include_original_query = gb(d, "include_original_query", true);
   c.include_source_names = gb(d, "include_source_names", false);
+  c.documented = gb(d, "documented", false);
+  c.strip_intermediate = gb(d, "strip_intermediate", false);
+  c.hide_aggregator_think = gb(d, "hide_aggregator_think", false);
+  c.sources_all = gb(d, "sources_all", true);
+  if (const JVal* t = d.get("sources"))
+    for (auto& x : t->a) c.sources.push_back(x.s);
   c.env_api_key = gs(d, "env_api_key", "");
   c.api_key_from_env = gb(d, "api_key_from_env", false);
   c.openapi_json = gs(d, "openapi_json", "");

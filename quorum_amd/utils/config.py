@@ -98,12 +98,34 @@ def validate_config(cfg: Dict[str, Any]) -> List[str]:
     if "strategy" in cfg and sel not in (cfg.get("strategy") or {}):
         warnings.append(f"selected strategy {sel!r} has no block under 'strategy'; defaults apply")
     agg = (cfg.get("strategy") or {}).get("aggregate") or {}
-    for unused in ("strip_intermediate_thinking", "hide_aggregator_thinking"):
-        if unused in agg:
-            warnings.append(f"strategy.aggregate.{unused} is accepted but, as in quorum, has no effect")
+    sem = cfg.get("semantics", "reference")
+    if sem not in SEMANTICS:
+        raise ConfigError(f"semantics must be one of {SEMANTICS}, not {sem!r}")
+    if sem == "reference":
+        for unused in ("strip_intermediate_thinking", "hide_aggregator_thinking"):
+            if unused in agg:
+                warnings.append(f"strategy.aggregate.{unused} is accepted but, as in quorum, has no effect "
+                                "(set semantics: documented to honour it)")
+    else:
+        src = agg.get("source_backends", "all")
+        for n in ([src] if isinstance(src, str) and src != "all" else src if isinstance(src, list) else []):
+            if n not in names:
+                warnings.append(f"source_backends names {n!r}, which is not a primary backend")
     if agg.get("aggregator_backend") and agg["aggregator_backend"] not in names:
         warnings.append(f"aggregator_backend {agg['aggregator_backend']!r} is not a primary backend")
     return warnings
+
+
+# ``semantics``: "reference" (default) reproduces quorum's code, including the flags its docs
+# describe but its code ignores; "documented" honours those flags as docs/aggregate_behaviour.md
+# describes them (SURVEY §2.8 "documented behaviour"): source_backends, strip_intermediate_thinking,
+# hide_aggregator_thinking, backend-name source labels, and the non-stream
+# suppress_individual_responses ("only the first response").
+SEMANTICS = ("reference", "documented")
+
+
+def documented(cfg: Dict[str, Any]) -> bool:
+    return (cfg or {}).get("semantics", "reference") == "documented"
 
 
 def strategy_name(cfg: Dict[str, Any]) -> str:
@@ -140,6 +162,18 @@ class AggregateSettings:
     query_format: str = DEFAULT_QUERY_FORMAT
     include_source_names: bool = False
     source_label_format: str = DEFAULT_SOURCE_LABEL_FORMAT
+    # honoured only with ``semantics: documented`` (see SEMANTICS above)
+    documented: bool = False
+    strip_intermediate_thinking: bool = False
+    hide_aggregator_thinking: bool = False
+
+    def sources(self) -> Optional[List[str]]:
+        """Backend names whose texts feed the aggregator (documented mode); None = all."""
+        if not self.documented or self.source_backends == "all" or self.source_backends is None:
+            return None
+        if isinstance(self.source_backends, str):
+            return [self.source_backends]
+        return [str(n) for n in self.source_backends]
 
 
 def resolve_flags(cfg: Dict[str, Any], body: Optional[Dict[str, Any]] = None) -> StrategyFlags:
@@ -173,6 +207,9 @@ def resolve_aggregate(cfg: Dict[str, Any]) -> AggregateSettings:
         query_format=block.get("query_format", DEFAULT_QUERY_FORMAT),
         include_source_names=block.get("include_source_names", False),
         source_label_format=block.get("source_label_format", DEFAULT_SOURCE_LABEL_FORMAT),
+        documented=documented(cfg),
+        strip_intermediate_thinking=bool(block.get("strip_intermediate_thinking", False)),
+        hide_aggregator_thinking=bool(block.get("hide_aggregator_thinking", False)),
     )
 
 

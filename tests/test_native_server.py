@@ -149,6 +149,73 @@ SCENARIOS = {
                        {"model": "gpt-4", "messages": MSG, "temperature": 0.7, "n": 1}, AUTH),
     "no_valid_backend": ({"primary_backends": [{"name": "a", "url": "", "model": "m"}], "settings": {"timeout": 3}},
                          {}, {"messages": MSG}, AUTH),
+    # the flags quorum's docs describe but its code ignores (reference semantics: no effect)
+    "par_stream_aggregate_doc_flags_ignored": (cfg_parallel(3, strategy="aggregate", block=dict(
+        AGG, source_backends=["LLM1", "LLM3"], strip_intermediate_thinking=True, hide_aggregator_thinking=True,
+        hide_intermediate_think=False)),
+        {"b1.test": ("refuse",), "b2.test": ("stream", 200, sse_stream(["<think>t2</think>two"])),
+         "b3.test": lambda body: (("stream", 200, sse_stream(["three"])) if body.get("stream")
+                                  else ("json", 200, completion("<think>a</think>SYN")))},
+        {"messages": MSG, "stream": True}, AUTH),
+}
+
+
+def _doc(cfg):
+    cfg = copy.deepcopy(cfg)
+    cfg["semantics"] = "documented"
+    return cfg
+
+
+# hide_intermediate_think off: the streamed texts keep their thinking, so the strip before the
+# aggregator is strip_intermediate_thinking's doing
+DOC_AGG = dict(AGG, source_backends=["LLM1", "LLM3"], strip_intermediate_thinking=True,
+               hide_aggregator_thinking=True, hide_intermediate_think=False)
+
+
+def _agg_b3(stream_text, answer):
+    return lambda body: (("stream", 200, sse_stream([stream_text])) if body.get("stream")
+                         else ("json", 200, completion(answer, cid="agg")))
+
+
+# ``semantics: documented`` (utils/config.py SEMANTICS): the reference's
+# docs/aggregate_behaviour.md flags honoured; python app vs native server, plus the expected
+# aggregator prompt / answer (test_documented_semantics_expectations)
+DOC_SCENARIOS = {
+    "doc_stream_sources_strip_hide": (_doc(cfg_parallel(3, strategy="aggregate", block=DOC_AGG)),
+                                      {"b1.test": ("stream", 200, sse_stream(["<think>t1</think>one"])),
+                                       "b2.test": ("stream", 200, sse_stream(["two"])),
+                                       "b3.test": _agg_b3("<reason>r</reason>three", "<think>a</think>SYN")},
+                                      {"messages": MSG, "stream": True}, AUTH),
+    "doc_stream_labels_after_failure": (_doc(cfg_parallel(3, strategy="aggregate", block=AGG)),
+                                        {"b1.test": ("refuse",), "b2.test": ("stream", 200, sse_stream(["two"])),
+                                         "b3.test": _agg_b3("three", "SYN")},
+                                        {"messages": MSG, "stream": True}, AUTH),
+    "doc_stream_empty_source_dropped": (_doc(cfg_parallel(3, strategy="aggregate", block=dict(
+        AGG, source_backends=["LLM1", "LLM2"]))),
+        {"b1.test": ("stream", 200, sse_stream([])), "b2.test": ("stream", 200, sse_stream(["two"])),
+         "b3.test": _agg_b3("three", "SYN")},
+        {"messages": MSG, "stream": True}, AUTH),
+    "doc_stream_no_source": (_doc(cfg_parallel(3, strategy="aggregate", block=dict(AGG, source_backends="LLM1"))),
+                             {"b1.test": ("refuse",), "b2.test": ("stream", 200, sse_stream(["two"])),
+                              "b3.test": _agg_b3("three", "SYN")},
+                             {"messages": MSG, "stream": True}, AUTH),
+    "doc_nonstream_suppress_first": (_doc(cfg_parallel(2, block=CONCAT)),
+                                     {"b1.test": ("json", 200, completion("first", usage=(1, 2, 3))),
+                                      "b2.test": ("json", 200, completion("second", usage=(4, 5, 9)))},
+                                     {"messages": MSG, "suppress_individual_responses": True}, AUTH),
+    "doc_nonstream_no_suppress": (_doc(cfg_parallel(2, block=CONCAT)),
+                                  {"b1.test": ("json", 200, completion("first")),
+                                   "b2.test": ("json", 200, completion("second"))},
+                                  {"messages": MSG}, AUTH),
+    "doc_nonstream_aggregate": (_doc(cfg_parallel(3, strategy="aggregate", block=DOC_AGG)),
+                                {"b1.test": ("json", 200, completion("<think>t1</think>R1")),
+                                 "b2.test": ("json", 200, completion("R2")),
+                                 "b3.test": ("json", 200, completion("<thought>x</thought>SYNTH", cid="agg"))},
+                                {"messages": MSG}, AUTH),
+    "doc_nonstream_no_source": (_doc(cfg_parallel(3, strategy="aggregate", block=dict(AGG, source_backends=["LLM1"]))),
+                                {"b1.test": ("text", 502, "bad"), "b2.test": ("json", 200, completion("R2")),
+                                 "b3.test": ("json", 200, completion("SYNTH"))},
+                                {"messages": MSG}, AUTH),
 }
 
 
@@ -227,7 +294,73 @@ def _native_side(cfg, ups, req, hdrs, tick_mode=None):
 @pytest.mark.parametrize("name", sorted(SCENARIOS))
 def test_native_matches_python(name, tick_mode):
     """tick_mode "loops": the io loops' asynchronous tick path (jobs polled, two in flight)."""
-    cfg, ups, req, hdrs = SCENARIOS[name]
+    _compare(SCENARIOS[name], name, tick_mode)
+
+
+@pytest.mark.parametrize("name", sorted(DOC_SCENARIOS))
+def test_native_matches_python_documented(name):
+    _compare(DOC_SCENARIOS[name], name, "loops")
+
+
+def _aggregator_prompt(calls):
+    ps = [c["body"]["messages"][0]["content"] for c in calls
+          if c["body"] and c["body"].get("stream") is False and c["host"].startswith("b3")]
+    return ps[0] if ps else None
+
+
+def _final_content(res):
+    status, ctype, body = res
+    if ctype == "text/event-stream":
+        fin = [e for e in body if isinstance(e, dict) and e.get("id") in ("chatcmpl-parallel-final", "error")]
+        return fin[0]["choices"][0]["delta"]["content"]
+    return body["choices"][0]["message"]["content"] if status == 200 else body["error"]["message"]
+
+
+# name -> (final content, substrings the aggregator prompt holds, substrings it must not hold)
+DOC_EXPECT = {
+    "doc_stream_sources_strip_hide": ("SYN", ["Response from LLM1:\none", "Response from LLM3:\nthree"],
+                                      ["two", "<think>", "<reason>"]),
+    "doc_stream_labels_after_failure": ("SYN", ["Response from LLM2:\ntwo", "Response from LLM3:\nthree"],
+                                        ["LLM1"]),
+    "doc_stream_empty_source_dropped": ("SYN", ["Response from LLM2:\ntwo"], ["LLM1", "three"]),
+    "doc_stream_no_source": ("Error: All backends failed to provide content", None, None),
+    "doc_nonstream_suppress_first": ("first", None, None),
+    "doc_nonstream_no_suppress": ("first\n-------------\nsecond", None, None),
+    "doc_nonstream_aggregate": ("SYNTH", ["Response from LLM1:\nR1"], ["R2", "<think>"]),
+    "doc_nonstream_no_source": ("All source backends failed", None, None),
+}
+
+
+@pytest.mark.parametrize("name", sorted(DOC_SCENARIOS))
+def test_documented_semantics_expectations(name):
+    """What the documented flags do (reference docs/aggregate_behaviour.md), checked on the
+    native server's output and the aggregator request it sent."""
+    cfg, ups, req, hdrs = DOC_SCENARIOS[name]
+    nat, calls = _native_side(cfg, ups, req, hdrs, "loops")
+    final, has, lacks = DOC_EXPECT[name]
+    assert _final_content(nat) == final, nat
+    prompt = _aggregator_prompt(calls)
+    if has is None:
+        assert prompt is None
+        return
+    for x in has:
+        assert x in prompt, (x, prompt)
+    for x in lacks:
+        assert x not in prompt, (x, prompt)
+
+
+def test_reference_semantics_ignore_doc_flags():
+    """Without ``semantics: documented`` the flags have no effect, as in quorum (the same
+    scenario runs against the reference itself in test_reference_conformance.py)."""
+    cfg, ups, req, hdrs = SCENARIOS["par_stream_aggregate_doc_flags_ignored"]
+    nat, calls = _native_side(cfg, ups, req, hdrs, "loops")
+    assert _final_content(nat) == "<think>a</think>SYN"
+    prompt = _aggregator_prompt(calls)
+    assert "Response from LLM1:\n<think>t2</think>two" in prompt and "Response from LLM2:\nthree" in prompt
+
+
+def _compare(scn, name, tick_mode):
+    cfg, ups, req, hdrs = scn
     py, py_calls = _python_side(cfg, ups, req, hdrs)
     nat, nat_calls = _native_side(cfg, ups, req, hdrs, tick_mode)
     if py[1] == "text/event-stream" and py[0] == 200:

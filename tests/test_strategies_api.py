@@ -191,3 +191,42 @@ def test_prompt_builder_template_braces():
     agg = resolve_aggregate({"strategy": {"aggregate": {"prompt_template": "A {{intermediate_results}} B"}}})
     p = build_aggregator_prompt(["x", "y"], "q", "|", False, "", False, "", agg.prompt_template)
     assert p == "A {x|y} B"
+
+
+def test_validate_config_semantics():
+    """``semantics``: reference (default) warns that the documented-only flags do nothing;
+    documented checks source_backends names; anything else is an error."""
+    import pytest
+
+    from quorum_amd.utils.config import ConfigError, validate_config
+
+    cfg = cfg_parallel(3, strategy="aggregate", block=dict(AGG, source_backends=["LLM1", "nope"]))
+    w = validate_config(cfg)
+    assert any("strip_intermediate_thinking" in x and "semantics: documented" in x for x in w)
+    assert not any("nope" in x for x in w)
+    cfg["semantics"] = "documented"
+    w = validate_config(cfg)
+    assert any("'nope'" in x for x in w) and not any("has no effect" in x for x in w)
+    cfg["semantics"] = "docs"
+    with pytest.raises(ConfigError):
+        validate_config(cfg)
+
+
+def test_documented_semantics_python_app(upstream):
+    """The FastAPI app with ``semantics: documented`` (non-stream aggregate): only the source
+    backends reach the aggregator, stripped, labelled with their names; the answer loses its
+    thinking (reference docs/aggregate_behaviour.md)."""
+    cfg = cfg_parallel(3, strategy="aggregate", block=dict(AGG, source_backends=["LLM2", "LLM3"]))
+    cfg["semantics"] = "documented"
+    upstream.json("b1.test", completion("one"))
+    upstream.json("b2.test", completion("<think>t</think>two"))
+    upstream.route("b3.test", lambda request, body: httpx.Response(
+        200, json=completion("<reason>r</reason>SYN" if body.get("stream") is False else "three")))
+    c = make_client(cfg, upstream)
+    r = c.post("/chat/completions", json={"messages": MSG}, headers=AUTH)
+    assert r.status_code == 200, r.text
+    assert r.json()["choices"][0]["message"]["content"] == "SYN"
+    prompts = [c["body"]["messages"][0]["content"] for c in upstream.calls if c["body"].get("stream") is False]
+    assert len(prompts) == 1
+    assert "Response from LLM2:\ntwo" in prompts[0] and "Response from LLM3:\nthree" in prompts[0]
+    assert "LLM1" not in prompts[0] and "<think>" not in prompts[0]
