@@ -86,6 +86,7 @@ struct KParams {
   TagSet ts;
   int npat;
   int32_t pat_E[2 * kMaxTags];  // Σ_j m(q0²+q1²) over the window part of each pattern (match iff dot == -E)
+  int32_t plen[2 * kMaxTags];   // pattern_len(ts, t), 0 past npat (a load with no dependence on ts.n)
   // byte → matcher code: 1..94 for the bytes that occur in patterns (letters folded), 95 for
   // every other byte (never equal to a pattern byte), 0 past the end of the text
   alignas(16) uint8_t code[256];
@@ -238,7 +239,7 @@ struct TickLane {
   double item_us = 0, start_spread_us = 0;
   double items_host_us = 0;
   double relay_us = 0, pickup_us = 0, grid_span_us = 0, grid_ticks = 0;  // persistent: doorbell seen -> ...  // host: result records -> slot state + SSE strings (process_item)  // per tick: mean item run, last item start - first
-  double stage_us[25] = {0};  // [20]: an item's system-scope release fence (stage timing)
+  double stage_us[30] = {0};  // [20]: an item's system-scope release fence (stage timing)
   double clk_cycles = 0, clk_us = 0;
   // finalize arenas (fused into this lane's tick launches)
   FinItem* h_fin = nullptr;

@@ -61,7 +61,7 @@ constexpr int TOK_CAP = 512;
 // 21 (S3a done), 22 (S3 loop done), 23 (s4_wave: matched), 24 (s4_wave: cuts), 25 (s4_wave:
 // token list + depth scan done), 26 (S6 write: output window filled, host stores next),
 // 27 (the item's system-scope release fence done: its cost is 27 minus the result's t1)
-constexpr int kDbg = 32;
+constexpr int kDbg = 40;
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 
@@ -132,6 +132,10 @@ struct Smem {
   int32_t scr2[2 * (BS / 64)];  // a second scan's partials (no barrier between the two)
   int32_t v[40];
   alignas(16) uint8_t tpl[TPL_BYTES];  // this stream's event shape template
+  // this item's SSE envelope (prefix with the index digits at 0, suffix at 256), written by
+  // waves 1-7 while wave 0 runs the one-wave filter: S6's fill then loads its bytes without
+  // the digit / envelope-part selection in its path
+  alignas(16) uint8_t env[256 + 64];
 };
 static_assert(TPL_BYTES == kTplBytes, "template size");
 
@@ -292,8 +296,32 @@ __device__ inline bool pattern_tail_ok(const uint8_t* Z, int Zn, int p, int t, c
 // the pattern's first 16 bytes  <=>  the window equals them (all of a tag up to 13 bytes;
 // longer patterns then compare their tail).  Distinct tags never both match at
 // one '<' (make_tagset), so at most one column of a row survives.
+// PatCol: this lane's pattern column of each block (t = 16·blk + lane % 16) — its match value
+// −E and length — read from KParams once per tile, ahead of the candidate scan
+struct PatCol {
+  int negE[2], plen[2];
+};
+__device__ inline PatCol pattern_cols(const KParams& P) {
+  PatCol c;
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    // (no dependence on P.npat: entries past it are zero, and the match tests t < npat)
+    const int t = 16 * blk + (threadIdx.x & 15);
+    c.negE[blk] = -P.pat_E[t];
+    c.plen[blk] = P.plen[t];
+  }
+  return c;
+}
+__device__ inline void mfma_match_group(const uint8_t* Z, int Zn, const uint16_t* cand, int ncand, int g,
+                                        const KParams& P, v4i bf0, v4i bf1, const PatCol& pc, int npat, int nts,
+                                        int8_t* cand_tok);
 __device__ inline void mfma_match_group(const uint8_t* Z, int Zn, const uint16_t* cand, int ncand, int g,
                                         const KParams& P, v4i bf0, v4i bf1, int8_t* cand_tok) {
+  mfma_match_group(Z, Zn, cand, ncand, g, P, bf0, bf1, pattern_cols(P), P.npat, P.ts.n, cand_tok);
+}
+__device__ inline void mfma_match_group(const uint8_t* Z, int Zn, const uint16_t* cand, int ncand, int g,
+                                        const KParams& P, v4i bf0, v4i bf1, const PatCol& pc, int npat, int nts,
+                                        int8_t* cand_tok) {
   int l = threadIdx.x & 63, r = l & 15, kg = l >> 4;
   int c = g * 16 + r;
   int p = c < ncand ? (int)cand[c] : -1;
@@ -323,14 +351,12 @@ __device__ inline void mfma_match_group(const uint8_t* Z, int Zn, const uint16_t
       a[q] = (int)(kg == 0 ? d0 : kg == 1 ? d1 : kg == 2 ? d2 : sq);
     }
   }
-  const int npat = P.npat, nts = P.ts.n;
   const int nblk = npat > 16 ? 2 : 1;
   for (int blk = 0; blk < nblk; ++blk) {
-    // this lane's pattern column: its match value, length and token id read before the MFMA
-    // (after it, every read of P would wait behind the previous row's cand_tok store)
+    // this lane's pattern column: its match value, length (pc: read ahead) and token id
     const int t = 16 * blk + (l & 15);
     const bool tv = t < npat;
-    const int negE = tv ? -P.pat_E[t] : 0, plen = tv ? pattern_len(P.ts, t) : 0;
+    const int negE = blk ? pc.negE[1] : pc.negE[0], plen = blk ? pc.plen[1] : pc.plen[0];  // (no dynamic index)
     const int8_t tok = (int8_t)(t < nts ? t + 1 : -(t - nts + 1));
     v4i acc = {0, 0, 0, 0};
     acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, blk ? bf1 : bf0, acc, 0, 0, 0);
@@ -643,6 +669,16 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
   const int lane = threadIdx.x & 63;
   if (dbg != nullptr && lane == 0) dbg_put(&dbg[28], __builtin_amdgcn_s_memrealtime());
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  // the filter's KParams reads (the item's LDS copy), issued together before the candidate
+  // scan and none depending on another (no P.npat / P.ts.n first): their latency overlaps
+  // the scan instead of heading the MFMA match and the holdback cuts
+  const v4i bf0 = build_pattern_frag(P, 0), bf1 = build_pattern_frag(P, 1);  // (block 1 unused when npat <= 16)
+  const PatCol pc = pattern_cols(P);
+  // pattern_prefix_w from registers: lane t holds pattern t's length and first two 8-byte
+  // words (every default tag's pattern fits 16 bytes; longer ones read further words from P)
+  // (lanes past 2·ts.n read zero entries: no dependence on P.ts.n)
+  const int pl_l = lane < 2 * kMaxTags ? P.plen[lane] : 0;
+  const uint64_t pw0_l = lane < 2 * kMaxTags ? P.pw[lane][0] : 0ull, pw1_l = lane < 2 * kMaxTags ? P.pw[lane][1] : 0ull;
   // candidates: every '<' of Z, in position order — 8 bytes per lane (SWAR compare on one
   // ds_read_b64; Z is 8-byte aligned with readable bytes past Zn), 512 bytes per step
   int nc = 0;
@@ -682,13 +718,13 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
     }
     return true;
   }
+  // (read after the scan: only the match and the cuts use them)
+  const int npat = P.npat, nts = P.ts.n;
+  const int npw = 2 * nts;  // (<= 2 * kMaxTags <= 64 lanes)
   if (lane < nc) s.cand_tok[lane] = 0;
   wave_fence();
   if (dbg != nullptr && lane == 0) dbg_put(&dbg[29], __builtin_amdgcn_s_memrealtime());
-  {
-    const v4i bf0 = build_pattern_frag(P, 0), bf1 = build_pattern_frag(P, P.npat > 16 ? 1 : 0);
-    for (int g = 0; g * 16 < nc; ++g) mfma_match_group(Z, Zn, s.cand, nc, g, P, bf0, bf1, s.cand_tok);
-  }
+  for (int g = 0; g * 16 < nc; ++g) mfma_match_group(Z, Zn, s.cand, nc, g, P, bf0, bf1, pc, npat, nts, s.cand_tok);
   wave_fence();
   if (dbg != nullptr && lane == 0) dbg_put(&dbg[23], __builtin_amdgcn_s_memrealtime());
   // tokens and the depth before each (candidates in order, non-tokens the scan identity);
@@ -706,7 +742,10 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
     const int2 ex = make_int2(wave_prev(x.x, 0), wave_prev(x.y, 0));
     cpos = lane < nc ? (int)s.cand[lane] : 0;
     ctok = id;
-    cplen = id != 0 ? tok_plen(P, id) : 0;
+    // the token's pattern length from lane (pattern index)'s pl_l: no KParams read here
+    const int pidx = id > 0 ? id - 1 : id < 0 ? nts - id - 1 : 0;
+    const int plx = __shfl(pl_l, pidx, 64);
+    cplen = id != 0 ? plx : 0;
     cdep = max(depth0 + ex.x, ex.y);
     fdep = __builtin_amdgcn_readlane(max(depth0 + x.x, x.y), 63);
     if (id != 0) {
@@ -720,11 +759,6 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
       s.tok_dep[ntok] = (int16_t)fdep;
     }
   }
-  // pattern_prefix_w from registers: lane t holds pattern t's length and first two 8-byte
-  // words (every default tag's pattern fits 16 bytes; longer ones read further words from P)
-  const int npw = 2 * P.ts.n;  // (<= 2 * kMaxTags <= 64 lanes)
-  const int pl_l = lane < npw ? pattern_len(P.ts, lane) : 0;
-  const uint64_t pw0_l = lane < npw ? P.pw[lane][0] : 0ull, pw1_l = lane < npw ? P.pw[lane][1] : 0ull;
   // hold_cut, wave-wide (every lane calls it; `active` lanes get an answer): the last
   // candidate before e from the candidate registers (positions ascend), its token / length and
   // the depth before it; then, for each lane whose candidate could still open a tag, the
@@ -742,13 +776,21 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
       pl = b ? plk : pl;
       dq = b ? dqk : dq;
     }
+    if (dbg != nullptr && lane == 0) dbg_put(&dbg[30], __builtin_amdgcn_s_memrealtime());
     // (q < e, so the window is never empty; longer than kMaxTail bytes it is no tag prefix)
     const bool need = active && q >= 0 && !(tk != 0 && q + pl <= e) && e - q <= kMaxTail;
-    bool pref = false;
-    for (uint64_t bm = __ballot(need); bm; bm &= bm - 1) {
+    // a token that completes later in Z (the cut falls inside it: q + pl > e) answers its own
+    // test — Z[q, e) is a proper prefix of its pattern, which counts for an open tag always
+    // and for a close tag inside a block (np = npw).  Only a '<' that is no complete token
+    // (tk == 0: a tag cut off at the end of Z, or no tag) and a close tag at depth 0 (a prefix
+    // of some open tag?) take the lane-parallel pattern test (a tag split across deltas — the
+    // usual "<thi" | "nk>" — cost ~0.35 us of dependent LDS reads and ballots per delta)
+    const bool implied = tk > 0 || (tk < 0 && dq != 0);
+    bool pref = implied;
+    for (uint64_t bm = __ballot(need && !implied); bm; bm &= bm - 1) {
       const int j = __ffsll((unsigned long long)bm) - 1;
       const int qj = __builtin_amdgcn_readlane(q, j), m = __builtin_amdgcn_readlane(e, j) - qj;
-      const int np = __builtin_amdgcn_readlane(dq, j) == 0 ? P.ts.n : npw;  // (opens only at depth 0)
+      const int np = __builtin_amdgcn_readlane(dq, j) == 0 ? nts : npw;  // (opens only at depth 0)
       const uint64_t z0 = lower8(lds_window8(Z, qj, qj + m)), z1 = m > 8 ? lower8(lds_window8(Z, qj + 8, qj + m)) : 0ull;
       const uint64_t m0 = m >= 8 ? ~0ull : ((1ull << (8 * m)) - 1);
       const uint64_t m1 = m >= 16 ? ~0ull : m <= 8 ? 0ull : ((1ull << (8 * (m - 8))) - 1);
@@ -762,6 +804,7 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
       const bool f = __ballot(ok) != 0;
       if (lane == j) pref = f;
     }
+    if (dbg != nullptr && lane == 0) dbg_put(&dbg[31], __builtin_amdgcn_s_memrealtime());
     *q_out = -1;
     if (!need || !pref) return e;  // no candidate, a completed token, or no tag prefix
     if (dq == 0 || for_tail) {
@@ -836,7 +879,16 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
   }
   // kept bytes before each delta's cut: the segment that holds cut - 1
   const int c = lane < ndelta ? cut : 0;
-  const int kk = c > 0 && c < cutN ? tok_upper(s, ntok, c - 1) : 0;  // tokens starting before c
+  // tokens starting before c: a walk over the token lanes' positions (ts0: tok_pos clamped to
+  // cutN, the same answer for c - 1 < cutN) — the binary search's dependent LDS reads only
+  // for token-dense tiles
+  int kk = 0;
+  if (ntok <= 16) {
+    for (int k = 0; k < ntok; ++k) kk += __builtin_amdgcn_readlane(ts0, k) <= c - 1 ? 1 : 0;
+    kk = c > 0 && c < cutN ? kk : 0;
+  } else {
+    kk = c > 0 && c < cutN ? tok_upper(s, ntok, c - 1) : 0;
+  }
   const int pk = kk > 0 ? kk - 1 : 0;
   const int p_gs = __shfl(gs, kk, 64), p_ob = __shfl(ob, kk, 64), p_gk = __shfl((int)gk, kk, 64);
   const int q_ts = __shfl(ts0, pk, 64), q_te = __shfl(te, pk, 64), q_ob = __shfl(ob, pk, 64),
@@ -850,6 +902,7 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
     s.wpos[lane] = (uint16_t)wp;
   }
   if (lane == 0) s.v[V_WLEN] = out;
+  if (dbg != nullptr && lane == 0) dbg_put(&dbg[32], __builtin_amdgcn_s_memrealtime());
   return true;
 }
 
@@ -1830,7 +1883,19 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
   const uint8_t* W = Z;  // identity when not filtering
   int ncand = 0, ntok = 0;
   bool s4_done = false;
+  const bool env_ready = (P.fast & 4) && filt && ndelta > 0 && Zn <= 2048 && ndelta <= 64 && emit;
   if ((P.fast & 4) && filt && ndelta > 0 && Zn <= 2048 && ndelta <= 64) {  // the common tile: one wave (s4_wave)
+    if (tid >= 64 && env_ready) {
+      // the idle waves: the item's envelope bytes, assembled off the fill's path
+      const int b = tid - 64, ix = (int)it.index, p1 = P.pre1_len;
+      const int nd = ix >= 100 ? 3 : ix >= 10 ? 2 : 1, pre = p1 + nd + P.pre2_len;
+      if (b < pre) {
+        const int d = b - p1, q = nd - 1 - d;  // index digit, most significant first
+        const int dv = q == 2 ? ix / 100 : q == 1 ? (ix / 10) % 10 : ix % 10;
+        s.env[b] = b < p1 ? (uint8_t)P.pre1[b] : d < nd ? (uint8_t)('0' + dv) : (uint8_t)P.pre2[d - nd];
+      }
+      if (b < P.suf_len) s.env[256 + b] = (uint8_t)P.suf[b];
+    }
     if (tid < 64) {
       const bool ok = s4_wave(s, Z, Zn, ndelta, depth0, P, P.dbg != nullptr ? P.dbg + bi * kDbg : nullptr);
       if (tid == 0 && s.v[V_S4W] != 2) s.v[V_S4W] = ok ? 1 : 0;  // (2: no candidates, W = Z)
@@ -1840,6 +1905,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       if (ok && (P.fast & 8) && emit && wl <= 2048) {
         s6_size_wave(s, s.v[V_S4W] == 2 ? Z : s.A, wl, ndelta);
         if (tid == 0) s.v[V_S6W] = 1;
+        if (P.dbg != nullptr && tid == 0) dbg_put(&P.dbg[bi * kDbg + 33], __builtin_amdgcn_s_memrealtime());
       }
     }
     __syncthreads();
@@ -2196,17 +2262,25 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
         static_assert(sizeof(P.pre1) + 3 + sizeof(P.pre2) <= 256 && sizeof(P.suf) <= 64 && MAX_EV <= BS,
                       "envelope bytes per lane / events per wave lane");
         uint32_t pw = 0;
+        uint8_t sch = 0;
+        if (env_ready) {  // staged in LDS during the filter
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int b = lane + 64 * r;
-          if (b < PRE) {
-            const int d = b - p1, q = ndig - 1 - d;  // index digit, most significant first
-            const int dv = q == 2 ? ix / 100 : q == 1 ? (ix / 10) % 10 : ix % 10;
-            const uint32_t ch = b < p1 ? (uint8_t)P.pre1[b] : d < ndig ? (uint8_t)('0' + dv) : (uint8_t)P.pre2[d - ndig];
-            pw |= ch << (8 * r);
+          for (int r = 0; r < 4; ++r)
+            if (lane + 64 * r < PRE) pw |= (uint32_t)s.env[lane + 64 * r] << (8 * r);
+          sch = lane < SUF ? s.env[256 + lane] : 0;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int b = lane + 64 * r;
+            if (b < PRE) {
+              const int d = b - p1, q = ndig - 1 - d;  // index digit, most significant first
+              const int dv = q == 2 ? ix / 100 : q == 1 ? (ix / 10) % 10 : ix % 10;
+              const uint32_t ch = b < p1 ? (uint8_t)P.pre1[b] : d < ndig ? (uint8_t)('0' + dv) : (uint8_t)P.pre2[d - ndig];
+              pw |= ch << (8 * r);
+            }
           }
+          sch = lane < SUF ? (uint8_t)P.suf[lane] : 0;
         }
-        const uint8_t sch = lane < SUF ? (uint8_t)P.suf[lane] : 0;
         const int kl = wave + (BS / 64) * lane;
         int cs_l = 0, cl_l = 0;
         if (kl < n_emit) {
@@ -2770,6 +2844,7 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* doors, PCtl* ct
   __shared__ TickLds U;
   __shared__ TickDesc D;
   __shared__ uint32_t cmd;  // new tick's sequence number, 0: exit
+  __shared__ uint32_t pre_k;  // a worker's first item of the tick, claimed with the descriptor read
   // door of this workgroup: blocks [d·wpd, (d+1)·wpd) — or, interleaved, blocks d, d + ndoors,
   // d + 2·ndoors, ...: the dispatcher deals block b to XCD b % 8, so with a multiple of 8
   // doors every door's sub-grid (and, tick after tick, its io loop's slot state, templates and
@@ -2851,6 +2926,10 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* doors, PCtl* ct
         // invalidation per workgroup (the caches are per CU / per XCD), not one per wave
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         w = __hip_atomic_load((uint32_t*)&ctl->d + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the first claim rides with the descriptor read (after the same acquire: the relay
+        // reset the counter before publishing the tick) — one round trip to the L2 before
+        // this workgroup's first item instead of two (r5: start spread 1.3 us per tick)
+        if (tid == 0) pre_k = __hip_atomic_fetch_add(&ctl->next[c & 3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       ((uint32_t*)&D)[tid] = w;
     }
@@ -2901,11 +2980,13 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* doors, PCtl* ct
     // items are claimed from the tick's counter, not dealt by workgroup index: a workgroup
     // that is not resident (the CUs are shared with other grids / kernels) holds up nothing.
     // The relay runs item 0 without a claim (it reset the counter to 1 before publishing).
-    bool own0 = relay;
+    // A worker's first item was claimed with the descriptor read (pre_k).
+    bool first = true;
     for (;;) {
       if (tid == 0)
-        cmd = own0 ? 0u : __hip_atomic_fetch_add(&ctl->next[seq & 3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      own0 = false;
+        cmd = first ? (relay ? 0u : pre_k)
+                    : __hip_atomic_fetch_add(&ctl->next[seq & 3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      first = false;
       __syncthreads();
       const int k = (int)cmd;
       __syncthreads();  // cmd is rewritten by the next claim
@@ -3122,6 +3203,7 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
       for (int k = 0; k < 3; ++k) E += digits(b, k) * digits(b, k);
     }
     base_params_.pat_E[p] = E;
+    base_params_.plen[p] = pattern_len(ts_, p);
   }
   base_params_.content_cap = content_cap_;
   for (int p = 0; p < base_params_.npat; ++p)
@@ -3906,6 +3988,12 @@ void HipEngine::complete(HipJob& J, std::vector<SlotResult>& results, std::vecto
         sub(21, 5, 28);   // s4_wave: call entry / candidate scan / MFMA match
         sub(22, 28, 29);
         sub(23, 29, 23);
+        sub(24, 25, 30);  // s4 holdback: candidate walk / prefix tests / cut stores
+        sub(25, 30, 31);
+        sub(26, 31, 24);
+        sub(27, 24, 32);  // s4 compaction / s6 sizing on wave 0 / the stage's barrier
+        sub(28, 32, 33);
+        sub(29, 33, 7);
         if (d[27] && d[27] >= B.h_res[i].t1 && B.h_res[i].t1) L.stage_us[20] += (double)(d[27] - B.h_res[i].t1) * 0.01;
       }
       L.stage_n += n;
@@ -4135,7 +4223,7 @@ void HipEngine::collect_finalize(TickLane& L, const std::vector<const FinalizeRe
 
 std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   std::unordered_map<std::string, double> m;
-  double stage[25] = {0}, cyc = 0, cus = 0;
+  double stage[30] = {0}, cyc = 0, cus = 0;
   for (auto& Lp : lanes_) {
     TickLane& L = *Lp;
     std::lock_guard<std::mutex> lg(L.mu);
@@ -4176,7 +4264,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["fin_launches"] += (double)L.fin_launches;  // tick launches that also carried finalize work
     m["fin_items"] += (double)L.fin_items;
     m["fin_staged_texts"] += (double)L.fin_staged;  // mesh-delivered remote finals staged into items
-    for (int k = 1; k < 25; ++k) stage[k] += L.stage_us[k];
+    for (int k = 1; k < 30; ++k) stage[k] += L.stage_us[k];
     cyc += L.clk_cycles;
     cus += L.clk_us;
   }
@@ -4193,6 +4281,12 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   m["stage_s4entry_us"] = stage[21];
   m["stage_s4scan_us"] = stage[22];
   m["stage_s4mfma_us"] = stage[23];
+  m["stage_s4holdwalk_us"] = stage[24];
+  m["stage_s4holdpref_us"] = stage[25];
+  m["stage_s4holdstore_us"] = stage[26];
+  m["stage_s4compact_us"] = stage[27];
+  m["stage_s6size_us"] = stage[28];
+  m["stage_s4barrier_us"] = stage[29];
   m["stage_fence_us"] = stage[20];  // the item's system-scope release fence (L2 write-back)
   m["shader_mhz"] = cus > 0 ? cyc / cus : 0.0;
   m["clk_cycles"] = cyc;  // summable across engines (/metrics sums the io loops' engines)
