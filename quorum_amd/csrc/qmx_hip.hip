@@ -1288,6 +1288,37 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     }
     const uint32_t valid = len >= 32 ? 0xffffffffu : ((1u << len) - 1u);
     nm &= valid;
+    // one-scan path: with no run of three or more newlines in the frame (SSE separates events
+    // with exactly "\n\n"), a separator is a "\n\n" not preceded by '\n' — decided from the
+    // chunk's mask and its neighbour bytes, no run scan.  Any triple newline (each is seen by
+    // the thread whose chunk holds its first byte: two bytes of look-ahead) rides in the count
+    // scan's total and sends the whole block down the run-scan path below (block-uniform).
+    {
+      const bool n1 = hi < in_len && s.A[hi] == '\n', n2 = hi + 1 < in_len && s.A[hi + 1] == '\n';
+      const bool pnl = lo > start && s.A[lo - 1] == '\n';
+      const uint64_t vm = len >= 32 ? 0xffffffffull : ((1ull << len) - 1ull);
+      const uint64_t ext = (uint64_t)nm | ((uint64_t)n1 << len) | ((uint64_t)n2 << (len + 1));
+      const uint64_t prevm = (ext << 1) | (pnl ? 1ull : 0ull);  // bit i: byte lo + i - 1 is '\n'
+      const bool triple = (ext & (ext >> 1) & (ext >> 2) & vm) != 0;
+      const uint64_t seps = ext & (ext >> 1) & ~prevm & vm;
+      int tot1;
+      int k = block_excl_sum<false>(__popcll(seps) + (triple ? (1 << 20) : 0), s.scr2, &tot1);
+      if (tot1 < (1 << 20)) {  // (block-uniform)
+        for (uint64_t m = seps; m; m &= m - 1) {
+          const int p = lo + __ffsll((unsigned long long)m) - 1;
+          if (k < MAX_EV) s.ev_b[k] = (uint16_t)p;
+          if (k + 1 < MAX_EV) s.ev_a[k + 1] = (uint16_t)(p + 2);
+          if (k == tot1 - 1) s.v[V_LASTSEP] = p;
+          ++k;
+        }
+        if (tid == 0) {
+          s.ev_a[0] = (uint16_t)start;
+          s.v[V_NSEP] = tot1;
+        }
+        goto s2_framed;
+      }
+    }
+    {
     const uint32_t inv = ~nm & valid;
     const bool all_nl = inv == 0;
     const int trail = all_nl ? len : len - 32 + __clz(inv);  // newlines at the chunk's end
@@ -1324,6 +1355,8 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       s.ev_a[0] = (uint16_t)start;
       s.v[V_NSEP] = nsep;
     }
+    }
+  s2_framed:;
   } else {
     int flen = in_len - start;
     int C = (flen + BS - 1) / BS;
@@ -1530,6 +1563,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       // the tile's newest content event (template or hole match) becomes the template
       if (kind == EV_CONTENT && sa - e0 <= TPL_PRE_MAX && e1 - sb <= TPL_SUF_MAX) newest = k;
     }
+    if (P.dbg != nullptr && tid == 0) dbg_put(&P.dbg[bi * kDbg + 34], __builtin_amdgcn_s_memrealtime());
     // per wave, not per half-wave LDS atomics on shared words (32 of them serialised at the
     // LDS): the upper half's values come over by readlane, lane 0 stores the wave's slot
     {
@@ -3994,6 +4028,8 @@ void HipEngine::complete(HipJob& J, std::vector<SlotResult>& results, std::vecto
         sub(27, 24, 32);  // s4 compaction / s6 sizing on wave 0 / the stage's barrier
         sub(28, 32, 33);
         sub(29, 33, 7);
+        sub(30, 3, 34);   // S3a: wave 0's own events / the wait for the slowest wave
+        sub(31, 34, 21);
         if (d[27] && d[27] >= B.h_res[i].t1 && B.h_res[i].t1) L.stage_us[20] += (double)(d[27] - B.h_res[i].t1) * 0.01;
       }
       L.stage_n += n;
@@ -4223,7 +4259,7 @@ void HipEngine::collect_finalize(TickLane& L, const std::vector<const FinalizeRe
 
 std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   std::unordered_map<std::string, double> m;
-  double stage[30] = {0}, cyc = 0, cus = 0;
+  double stage[32] = {0}, cyc = 0, cus = 0;
   for (auto& Lp : lanes_) {
     TickLane& L = *Lp;
     std::lock_guard<std::mutex> lg(L.mu);
@@ -4264,7 +4300,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["fin_launches"] += (double)L.fin_launches;  // tick launches that also carried finalize work
     m["fin_items"] += (double)L.fin_items;
     m["fin_staged_texts"] += (double)L.fin_staged;  // mesh-delivered remote finals staged into items
-    for (int k = 1; k < 30; ++k) stage[k] += L.stage_us[k];
+    for (int k = 1; k < 32; ++k) stage[k] += L.stage_us[k];
     cyc += L.clk_cycles;
     cus += L.clk_us;
   }
@@ -4287,6 +4323,8 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   m["stage_s4compact_us"] = stage[27];
   m["stage_s6size_us"] = stage[28];
   m["stage_s4barrier_us"] = stage[29];
+  m["stage_s3awave0_us"] = stage[30];
+  m["stage_s3await_us"] = stage[31];
   m["stage_fence_us"] = stage[20];  // the item's system-scope release fence (L2 write-back)
   m["shader_mhz"] = cus > 0 ? cyc / cus : 0.0;
   m["clk_cycles"] = cyc;  // summable across engines (/metrics sums the io loops' engines)
