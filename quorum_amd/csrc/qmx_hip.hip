@@ -1449,10 +1449,19 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       const HoleTpl& T = U.htpl[qi];
       hl[qi] = (T.kind == EV_CONTENT || T.kind == EV_SKIP) ? (int)T.len : 0;
     }
+    // loop-invariant: this lane's template prefix word; the next round's event bounds are
+    // read while this round's event is examined (one LDS round trip less per round)
+    const uint64_t tw0 = ((const uint64_t*)s.tpl)[lane];  // (lane < 32: o < 256)
+    int ne0 = hw < nev ? s.ev_a[hw] : 0, ne1 = hw < nev ? s.ev_b[hw] : 0;
     for (int kb = 0; kb < nev; kb += BS / 32) {
       const int k = kb + hw;
       const bool have = k < nev;
-      const int e0 = have ? s.ev_a[k] : 0, e1 = have ? s.ev_b[k] : 0, L = e1 - e0;
+      const int e0 = ne0, e1 = ne1, L = e1 - e0;
+      {
+        const int kn = k + BS / 32;
+        ne0 = kn < nev ? s.ev_a[kn] : 0;
+        ne1 = kn < nev ? s.ev_b[kn] : 0;
+      }
       const int o = lane * 8;
       const bool word = have && fast && L <= 256 && o < L;
       const int nb = min(8, L - o);
@@ -1477,7 +1486,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
             sw = ss >= 0 ? lds_window8(s.tpl + TPL_PRE_MAX, 0, ts) << (8 * ss)
                          : lds_window8(s.tpl + TPL_PRE_MAX, -ss, ts);
           }
-          const uint64_t tw = pe > 0 ? ((const uint64_t*)s.tpl)[lane] : 0ull;  // (lane < 32: o < 256)
+          const uint64_t tw = pe > 0 ? tw0 : 0ull;
           const uint64_t bmask = valid & ~pmask & ~smask;
           sbad = ((ev ^ tw) & pmask) != 0 || ((ev ^ sw) & smask) != 0;
           bad = sbad || (odd & bmask) != 0;
