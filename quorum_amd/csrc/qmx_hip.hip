@@ -1453,7 +1453,9 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
     // read while this round's event is examined (one LDS round trip less per round)
     const uint64_t tw0 = ((const uint64_t*)s.tpl)[lane];  // (lane < 32: o < 256)
     int ne0 = hw < nev ? s.ev_a[hw] : 0, ne1 = hw < nev ? s.ev_b[hw] : 0;
+    if (P.dbg != nullptr && tid == 0) dbg_put(&P.dbg[bi * kDbg + 35], __builtin_amdgcn_s_memrealtime());
     for (int kb = 0; kb < nev; kb += BS / 32) {
+      if (P.dbg != nullptr && tid == 0 && kb == BS / 32) dbg_put(&P.dbg[bi * kDbg + 36], __builtin_amdgcn_s_memrealtime());
       const int k = kb + hw;
       const bool have = k < nev;
       const int e0 = ne0, e1 = ne1, L = e1 - e0;
@@ -1606,6 +1608,13 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       newest_all = max(newest_all, U.s3w[q][2]);
     }
     if (tid == 0 && newest_all >= 0) atomicMax(&s.v[V_TPLK], newest_all);
+    if (P.dbg != nullptr && tid == 0) {  // (stage timing) which events S3a left to the loop
+      unsigned long long cat = 0;
+      for (int k = 0; k < nev; ++k)
+        if (s.ev_kind[k] >= 0xFE) cat |= k == 0 ? 1ull : k == nev - 1 ? 2ull : k == nev - 2 ? 4ull : 8ull;
+      P.dbg[bi * kDbg + 37] = (unsigned long long)unres_all;
+      P.dbg[bi * kDbg + 38] = cat;
+    }
     // a hole template S3a matched is carried into the launch's write table (as the loop's
     // matches are, wave_hole_carry): wave w carries template w
     if (pub && w < kHoleTpls && ((hm_all >> w) & 1))
@@ -4039,6 +4048,9 @@ void HipEngine::complete(HipJob& J, std::vector<SlotResult>& results, std::vecto
         sub(29, 33, 7);
         sub(30, 3, 34);   // S3a: wave 0's own events / the wait for the slowest wave
         sub(31, 34, 21);
+        sub(32, 3, 35);   // S3a on wave 0: before its rounds / round 1 / the rest
+        sub(33, 35, 36);
+        sub(34, 36, 34);
         if (d[27] && d[27] >= B.h_res[i].t1 && B.h_res[i].t1) L.stage_us[20] += (double)(d[27] - B.h_res[i].t1) * 0.01;
       }
       L.stage_n += n;
@@ -4051,6 +4063,8 @@ void HipEngine::complete(HipJob& J, std::vector<SlotResult>& results, std::vecto
         L.s3_cyc_lex += B.h_dbg[kDbg * i + 18];
         L.s3_hole += B.h_dbg[kDbg * i + 19];
         L.s3_cyc_hole += B.h_dbg[kDbg * i + 20];
+        L.s3a_unres += B.h_dbg[kDbg * i + 37];
+        for (int c = 0; c < 4; ++c) L.s3a_unres_cat[c] += (B.h_dbg[kDbg * i + 38] >> c) & 1;
       }
     }
   }
@@ -4268,7 +4282,7 @@ void HipEngine::collect_finalize(TickLane& L, const std::vector<const FinalizeRe
 
 std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   std::unordered_map<std::string, double> m;
-  double stage[32] = {0}, cyc = 0, cus = 0;
+  double stage[35] = {0}, cyc = 0, cus = 0;
   for (auto& Lp : lanes_) {
     TickLane& L = *Lp;
     std::lock_guard<std::mutex> lg(L.mu);
@@ -4289,6 +4303,11 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["s3_cycles_lex"] += (double)L.s3_cyc_lex;
     m["s3_hole_hits"] += (double)L.s3_hole;
     m["s3_cycles_hole"] += (double)L.s3_cyc_hole;
+    m["s3a_unresolved"] += (double)L.s3a_unres;  // events S3a left to the loop; items where that was the
+    m["s3a_unres_first"] += (double)L.s3a_unres_cat[0];  // first / last / second-to-last / another event
+    m["s3a_unres_last"] += (double)L.s3a_unres_cat[1];
+    m["s3a_unres_last2"] += (double)L.s3a_unres_cat[2];
+    m["s3a_unres_other"] += (double)L.s3a_unres_cat[3];
     m["host_prep_us"] += L.host_prep_us;
     m["gpu_wait_us"] += L.gpu_wait_us;
     m["first_result_us"] += L.first_result_us;
@@ -4309,7 +4328,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["fin_launches"] += (double)L.fin_launches;  // tick launches that also carried finalize work
     m["fin_items"] += (double)L.fin_items;
     m["fin_staged_texts"] += (double)L.fin_staged;  // mesh-delivered remote finals staged into items
-    for (int k = 1; k < 32; ++k) stage[k] += L.stage_us[k];
+    for (int k = 1; k < 35; ++k) stage[k] += L.stage_us[k];
     cyc += L.clk_cycles;
     cus += L.clk_us;
   }
@@ -4334,6 +4353,9 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   m["stage_s4barrier_us"] = stage[29];
   m["stage_s3awave0_us"] = stage[30];
   m["stage_s3await_us"] = stage[31];
+  m["stage_s3apre_us"] = stage[32];
+  m["stage_s3around1_us"] = stage[33];
+  m["stage_s3arest_us"] = stage[34];
   m["stage_fence_us"] = stage[20];  // the item's system-scope release fence (L2 write-back)
   m["shader_mhz"] = cus > 0 ? cyc / cus : 0.0;
   m["clk_cycles"] = cyc;  // summable across engines (/metrics sums the io loops' engines)

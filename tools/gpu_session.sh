@@ -184,7 +184,7 @@ import json, sys
 for l in sys.stdin:
     if not l.startswith('{'): continue
     d=json.loads(l); st=d.get('stage_us_per_item',{})
-    print(d['shape'], d['slots'], 'wall', d['wall_us_p50'], 'kern', d.get('kernel_us_avg'), [st.get('stage%d_us'%k) for k in range(1,11)], {k[6:-3]: v for k, v in st.items() if k.startswith(('stage_s4', 'stage_s6', 'stage_s3'))})
+    print(d['shape'], d['slots'], 'wall', d['wall_us_p50'], 'kern', d.get('kernel_us_avg'), [st.get('stage%d_us'%k) for k in range(1,11)], {k[6:-3]: v for k, v in st.items() if k.startswith(('stage_s4', 'stage_s6', 'stage_s3'))}, d.get('s3_per_item'))
 " ;;
     pmcshape:*)  # pmcshape:SHAPE:C1,C2 — counters of qmx_tick_persistent on another stream shape, per tick
       rest=${step#pmcshape:}; shp=${rest%%:*}; ctr=${rest#*:}; slug=$(echo "${shp}_$ctr" | tr -c 'a-zA-Z0-9' '_' | cut -c1-60)
