@@ -234,7 +234,7 @@ struct TickLane {
   uint64_t launches = 0, items = 0, h2d_bytes = 0, d2h_bytes = 0;
   uint64_t s3_full = 0, s3_tpl = 0, s3_events = 0, stage_n = 0;  // QMX_STAGE_TIMING: S3 path counters
   uint64_t s3_cyc_full = 0, s3_cyc_tpl = 0, s3_cyc_lex = 0, s3_hole = 0, s3_cyc_hole = 0;  // S3 wave cycles: full parse / templates / lexer
-  uint64_t s3a_unres = 0, s3a_unres_cat[4] = {0, 0, 0, 0};  // stage timing: events S3a left to its loop
+  uint64_t s3a_unres = 0;  // stage timing: events S3a left to its loop
   double kernel_ms = 0.0, host_prep_us = 0, gpu_wait_us = 0, process_us = 0;  // host-side tick breakdown
   double first_result_us = 0;  // tick posted -> first result record seen by the host
   double item_us = 0, start_spread_us = 0;

@@ -1608,13 +1608,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
       newest_all = max(newest_all, U.s3w[q][2]);
     }
     if (tid == 0 && newest_all >= 0) atomicMax(&s.v[V_TPLK], newest_all);
-    if (P.dbg != nullptr && tid == 0) {  // (stage timing) which events S3a left to the loop
-      unsigned long long cat = 0;
-      for (int k = 0; k < nev; ++k)
-        if (s.ev_kind[k] >= 0xFE) cat |= k == 0 ? 1ull : k == nev - 1 ? 2ull : k == nev - 2 ? 4ull : 8ull;
-      P.dbg[bi * kDbg + 37] = (unsigned long long)unres_all;
-      P.dbg[bi * kDbg + 38] = cat;
-    }
+    if (P.dbg != nullptr && tid == 0) P.dbg[bi * kDbg + 37] = (unsigned long long)unres_all;  // (stage timing)
     // a hole template S3a matched is carried into the launch's write table (as the loop's
     // matches are, wave_hole_carry): wave w carries template w
     if (pub && w < kHoleTpls && ((hm_all >> w) & 1))
@@ -4064,7 +4058,6 @@ void HipEngine::complete(HipJob& J, std::vector<SlotResult>& results, std::vecto
         L.s3_hole += B.h_dbg[kDbg * i + 19];
         L.s3_cyc_hole += B.h_dbg[kDbg * i + 20];
         L.s3a_unres += B.h_dbg[kDbg * i + 37];
-        for (int c = 0; c < 4; ++c) L.s3a_unres_cat[c] += (B.h_dbg[kDbg * i + 38] >> c) & 1;
       }
     }
   }
@@ -4303,11 +4296,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["s3_cycles_lex"] += (double)L.s3_cyc_lex;
     m["s3_hole_hits"] += (double)L.s3_hole;
     m["s3_cycles_hole"] += (double)L.s3_cyc_hole;
-    m["s3a_unresolved"] += (double)L.s3a_unres;  // events S3a left to the loop; items where that was the
-    m["s3a_unres_first"] += (double)L.s3a_unres_cat[0];  // first / last / second-to-last / another event
-    m["s3a_unres_last"] += (double)L.s3a_unres_cat[1];
-    m["s3a_unres_last2"] += (double)L.s3a_unres_cat[2];
-    m["s3a_unres_other"] += (double)L.s3a_unres_cat[3];
+    m["s3a_unresolved"] += (double)L.s3a_unres;  // events S3a left to its loop (stage timing)
     m["host_prep_us"] += L.host_prep_us;
     m["gpu_wait_us"] += L.gpu_wait_us;
     m["first_result_us"] += L.first_result_us;

@@ -111,8 +111,7 @@ def main():
                     rec["s3_per_item"] = {k: round(st[k] / st["stage_items"], 2)
                                           for k in ("s3_events", "s3_full_parses", "s3_template_hits", "s3_hole_hits",
                                                     "s3_cycles_full", "s3_cycles_template", "s3_cycles_lex", "s3_cycles_hole",
-                                                    "s3a_unresolved", "s3a_unres_first", "s3a_unres_last", "s3a_unres_last2",
-                                                    "s3a_unres_other")
+                                                    "s3a_unresolved")
                                           if k in st}
                 rec["MB_per_s"] = round(n * len(body) / len(pieces) / (st["kernel_ms"] / max(st["launches"], 1)) / 1e3, 1)
             if grid is not None:
