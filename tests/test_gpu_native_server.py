@@ -22,6 +22,22 @@ def test_native_hip_matches_python(name, tick_mode, monkeypatch):
     assert ext.server_counters()["verify_mismatches"] == before
 
 
+@pytest.mark.parametrize("name", sorted(T.DOC_SCENARIOS))
+def test_native_hip_documented_semantics(name, monkeypatch):
+    """``semantics: documented`` on the HIP engine (the strip before the aggregator runs in
+    the fused finalize's texts kind; the slot's content size names its source), verify mode
+    on: python app == native server, and the expected prompt and answer."""
+    from quorum_amd.ops import native
+
+    ext = native.require()
+    before = ext.server_counters()["verify_mismatches"]
+    monkeypatch.setattr(T, "ENGINE", "hip")
+    monkeypatch.setattr(T, "VERIFY", True)
+    T.test_native_matches_python_documented(name)
+    T.test_documented_semantics_expectations(name)
+    assert ext.server_counters()["verify_mismatches"] == before
+
+
 def test_native_hip_keepalive(monkeypatch):
     import live_upstream as L
     orig = L.native_server

@@ -22,7 +22,7 @@
 #   pmc:C1,C2,...         rocprofv3 --pmc pass (one block-limited counter set) on kbench
 #   pmce:ENV=V:C1,C2      the same pass under extra env (e.g. QMX_KFAST=7: one fast path off)
 #   pmcgrid:C1,C2,...     rocprofv3 --pmc on the production kernel (kbench --grid: qmx_tick_persistent),
-#                         counters per dispatch and per tick
+#                         counters per dispatch and per tick (KB_GRID doors, default 16; KB_SLOTS streams)
 #   kbench                tools/kbench.py in-kernel stage split (QMX_STAGE_TIMING)
 #   kbenchgrid            the same on the persistent grid (the production kernel)
 #   kbenchshape:SHAPE     the grid stage split on another stream shape (tools/kbench.py --shape: tagdense)
@@ -152,7 +152,7 @@ for step in "$@"; do
     pmcgrid:*)  # counters of the production kernel (qmx_tick_persistent: one dispatch, many ticks)
       ctr=${step#pmcgrid:}; slug=$(echo "$ctr" | tr -c 'a-zA-Z0-9' '_' | cut -c1-60)
       timeout -s KILL 120 rocprofv3 --pmc ${ctr//,/ } -d $OUT/pmcg_$slug -o pmc --output-format csv -- \
-        python3 tools/kbench.py --grid 16 --slots 3 --iters 400 --combos ft > $OUT/pmcg_$slug.log 2>&1 \
+        python3 tools/kbench.py --grid ${KB_GRID:-16} --slots ${KB_SLOTS:-3} --iters 400 --combos ft > $OUT/pmcg_$slug.log 2>&1 \
         || { echo "pmcgrid $ctr failed"; tail -10 $OUT/pmcg_$slug.log; exit 1; }
       nt=$(python3 -c "
 import json
