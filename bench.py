@@ -496,6 +496,7 @@ def breakdown(m0, m1, elapsed):
                       "worker_nodata": int(d.get("qmx_spread_worker_nodata_total", 0.0)),
                       "remote_texts_hbm": int(d.get("qmx_kernel_remote_texts_hbm", 0.0)),
                       "remote_texts_staged": int(d.get("qmx_kernel_remote_texts_staged", 0.0)),
+                      "remote_texts_copied": int(d.get("qmx_kernel_remote_texts_copied", 0.0)),
                       "hops_us": hop_means(d)}
                      if d.get("qmx_remote_streams_total") else None),
         # where a request's time goes (server-side means over the timed region): upstream
@@ -583,7 +584,8 @@ def spread_summary(rows) -> dict:
            # merged sessions finalized on the owner's host instead of its GPU (0 expected)
            "finalize_host": sum(tot(a, b, "finalize_host") for a, b in passes[:4]),
            "remote_texts_gpu": {"hbm": sum(tot(a, b, "remote_texts_hbm") for a, b in passes[:4]),
-                                "staged": sum(tot(a, b, "remote_texts_staged") for a, b in passes[:4])},
+                                "staged": sum(tot(a, b, "remote_texts_staged") for a, b in passes[:4]),
+                                "copied": sum(tot(a, b, "remote_texts_copied") for a, b in passes[:4])},
            "remote_ends": ends("main", "load", "remote_ends"),
            "p50_latency_ms": med([get(r, "main", "load", "p50_latency_ms") for r in rows]),
            "hops_us_loaded": hops("main", "load", "hops_us"),
@@ -613,7 +615,7 @@ def spread_summary(rows) -> dict:
     def compact(d):
         keep = ("requests", "invalid", "p50_latency_ms", "remote_streams", "eager_finals", "bulk_rounds", "mesh_finals",
                 "delta_mismatch", "worker_nodata", "remote_ends", "up_failures", "hops_us", "finalize_host",
-                "remote_texts_hbm", "remote_texts_staged", "error")
+                "remote_texts_hbm", "remote_texts_staged", "remote_texts_copied", "error")
         return {k: v for k, v in (d or {}).items() if k in keep and v}
 
     def rank_error(r):
@@ -743,7 +745,8 @@ def config3_summary(rows) -> dict:
            "mesh_finals": int(sum(l.get("mesh_finals", 0) for l in loads)),
            "finalize_host": int(sum(l.get("finalize_host", 0) for l in loads)),
            "remote_texts_gpu": {"hbm": int(sum(l.get("remote_texts_hbm", 0) for l in loads)),
-                                "staged": int(sum(l.get("remote_texts_staged", 0) for l in loads))},
+                                "staged": int(sum(l.get("remote_texts_staged", 0) for l in loads)),
+                                "copied": int(sum(l.get("remote_texts_copied", 0) for l in loads))},
            "delta_mismatch": int(sum(l.get("delta_mismatch", 0) for l in loads)),
            "per_rank": [{"requests": l.get("requests"), "req_s": l.get("req_s"), "bulk_rounds": l.get("bulk_rounds"),
                          "round_us_avg": l.get("round_us_avg"), "hops_us": l.get("hops_us")} for l in loads]}
@@ -774,6 +777,7 @@ def spread_counters(d) -> dict:
             "finalize_host": d.get("qmx_kernel_fin_host", 0.0),
             "remote_texts_hbm": d.get("qmx_kernel_remote_texts_hbm", 0.0),
             "remote_texts_staged": d.get("qmx_kernel_remote_texts_staged", 0.0),
+            "remote_texts_copied": d.get("qmx_kernel_remote_texts_copied", 0.0),
             # how this rank's remote streams ended (owner side), and its upstream failures by
             # class (worker side included)
             "remote_ends": {k.split('"')[1]: v for k, v in d.items() if k.startswith("qmx_spread_remote_ends_total") and v},

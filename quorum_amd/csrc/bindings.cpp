@@ -509,4 +509,5 @@ PYBIND11_MODULE(_qmx, m) {
   bind_engine(he);
   he.def("kernel_stats", &HipEngine::kernel_stats);
   he.def("debug_poison_results", &HipEngine::debug_poison_results, py::arg("ahead") = 1);
+  he.def("set_remote_hbm_direct", &HipEngine::set_remote_hbm_direct, py::arg("on"));
 }

@@ -299,6 +299,14 @@ class HipEngine : public HostEngine {
   void* content_device_ptr(int slot, size_t* cap) override;
   size_t content_size(int slot) override;
   void set_remote_content(int slot, const std::string* bytes, size_t len) override;
+  // An RCCL round's final text in this slot's HBM content area: read there by the next
+  // finalize item (direct), or first copied to the host and staged like a mesh-delivered
+  // text.  A peer GPU's writes into coarse-grained HBM are coherent with this device's L2
+  // only at dispatch boundaries, which a persistent grid does not cross: the server keeps the
+  // host copy at world > 1 unless QMX_REMOTE_HBM=1 (world 1: RCCL's own kernel on this
+  // device wrote the bytes through this L2, direct is exact).
+  void set_remote_hbm_direct(bool on) { remote_hbm_direct_ = on; }
+  bool remote_hbm_direct() const { return remote_hbm_direct_; }
   std::unordered_map<std::string, double> kernel_stats();
   int lanes() const { return (int)lanes_.size(); }
 
@@ -364,7 +372,8 @@ class HipEngine : public HostEngine {
   std::vector<uint8_t> remote_host_;
   std::vector<uint32_t> content_len_;    // device content bytes per slot
   // stats
-  std::atomic<uint64_t> escalations_{0}, fin_host_{0}, remote_dev_{0}, remote_staged_{0};
+  std::atomic<uint64_t> escalations_{0}, fin_host_{0}, remote_dev_{0}, remote_staged_{0}, remote_copied_{0};
+  bool remote_hbm_direct_ = true;
   int spin_us_ = 0;  // QMX_WAIT_SPIN_US: yield-poll before the blocking wait
   bool poll_ = true;  // QMX_WAIT=event: wait on a blocking-sync HIP event instead of polling
   int poll_us_ = 1;   // QMX_POLL_US: poll period once the expected kernel time has passed (MI355X A/Bs: 2 beats 6, 1 beats 2)

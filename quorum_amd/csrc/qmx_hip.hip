@@ -3519,6 +3519,12 @@ void HipEngine::set_remote_content(int slot, const std::string* bytes, size_t le
     core_[slot].content = *bytes;
     remote_host_[slot] = 1;
     ++remote_staged_;
+  } else if (!remote_hbm_direct_) {
+    // (the round's stream was synchronised before the text is applied; this copy is a new
+    // dispatch on the device, so it sees the peer's writes)
+    core_[slot].content = device_content(slot, len);
+    remote_host_[slot] = 1;
+    ++remote_copied_;
   } else {
     ++remote_dev_;
   }
@@ -4353,6 +4359,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   m["fin_host"] = (double)fin_host_.load();
   m["remote_texts_hbm"] = (double)remote_dev_.load();        // spread owner: finals an RCCL round put in HBM
   m["remote_texts_staged"] = (double)remote_staged_.load();  // ... that came over the mesh
+  m["remote_texts_copied"] = (double)remote_copied_.load();  // ... an RCCL round wrote, copied to the host (world > 1)
   m["lanes"] = (double)lanes_.size();
   m["fin_separate_launches"] = 0.0;  // finalize no longer has a launch (or a wait) of its own
   if (grid_ && door_ == 0)  // the shared grid's counters, once per process

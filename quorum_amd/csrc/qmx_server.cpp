@@ -626,6 +626,17 @@ class Verifier {
 // has the next kernel in flight for the bytes that arrived meanwhile (the tick kernel is
 // latency-bound: two launches in flight cost the GPU nothing and halve the tick period).
 // --------------------------------------------------------------------------------------
+// Round-delivered remote finals read straight from HBM (HipEngine::set_remote_hbm_direct):
+// tcpbulk rounds copy them in from the host (a runtime dispatch on this device: coherent), and
+// RCCL at world 1 is its own kernel on this device; RCCL at world > 1 (a peer GPU's writes)
+// only with QMX_REMOTE_HBM=1 until a multi-GPU run has pinned it
+static bool remote_hbm_direct(const ServerCfg& cfg) {
+  if (const char* e = env_get("QMX_REMOTE_HBM")) return atoi(e) != 0;
+  const char* x = env_get("QMX_XCHG");
+  const std::string t = x && *x ? x : cfg.xchg;
+  return cfg.world <= 1 || t != "rccl";
+}
+
 class GpuHub {
  public:
   using Sink = std::function<void(ResultBatch&&)>;
@@ -633,6 +644,7 @@ class GpuHub {
     lanes_ = std::max(1, std::min(cfg.tick_lanes, 8));
     if (cfg.engine == "hip") {
       HipEngine* he = new HipEngine(cfg.tags, cfg.device, cfg.tile, cfg.max_slots, cfg.content_cap, lanes_);
+      he->set_remote_hbm_direct(remote_hbm_direct(cfg));
       // (spread placement: an RCCL round writes a remote final text into the content arena
       // and its stream is synchronised before the text is applied; the finalize that reads it
       // is a later tick, whose items start with a system-scope acquire — one-shot launches and
@@ -1121,6 +1133,7 @@ class Loop {
         const int per = std::max(128, cfg_.max_slots / std::max(1, cfg_.threads));
         heng_ = new HipEngine(cfg_.tags, cfg_.device, cfg_.tile, per, cfg_.content_cap, 1, grid_,
                               idx_ * loop_doors_, loop_doors_);
+        heng_->set_remote_hbm_direct(remote_hbm_direct(cfg_));
         eng_.reset(heng_);
         aeng_ = heng_;
         loop_slots_ = per;

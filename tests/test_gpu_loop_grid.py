@@ -183,13 +183,17 @@ FIN_TEXT_PIECES = ["<think>", "</think>", "<reason>", "</reason>", "<THINK>", "a
                    " ", "\n", "　", '"', "\\", "<", ">", "x" * 40]
 
 
-@pytest.mark.parametrize("placement", ["rccl", "mesh", "mixed"])
+@pytest.mark.parametrize("placement", ["rccl", "mesh", "mixed", "rccl_hostcopy"])
 def test_grid_remote_finals_finalize_on_gpu(ext, placement):
     """Spread owner under loop ticks: remote streams' final texts in shadow slots finalize in
     fused GPU items (fin_host == 0), byte-equal to the CPU engine given the same texts —
     RCCL-delivered texts (a world-1 loopback: manifests, epoch, ncclSend/ncclRecv into the
     slots' own HBM areas while the grid runs) and mesh-delivered texts (staged into the
-    finalize items, which copy them to HBM first)."""
+    finalize items, which copy them to HBM first).  rccl_hostcopy: the world > 1 default
+    (set_remote_hbm_direct(False)): an RCCL text is copied to the host and staged like a
+    mesh-delivered one."""
+    hostcopy = placement == "rccl_hostcopy"
+    placement = "rccl" if hostcopy else placement
     from live_upstream import free_port_block
 
     from quorum_amd.ops.engine import FinalizeRequest
@@ -197,6 +201,8 @@ def test_grid_remote_finals_finalize_on_gpu(ext, placement):
     grid = ext.HipGrid(0, 2, 4)
     tags = ["think", "reason", "reasoning", "thought"]
     hip = NativeEngine("hip", tags, device=0, max_slots=64, content_cap=1 << 18, grid=grid, door=0)
+    if hostcopy:
+        hip._e.set_remote_hbm_direct(False)
     cpu = NativeEngine("cpu", tags)
     rng = random.Random({"rccl": 1, "mesh": 2, "mixed": 3}[placement])
     texts = []
@@ -239,7 +245,11 @@ def test_grid_remote_finals_finalize_on_gpu(ext, placement):
     st = hip._e.kernel_stats()
     n_r = sum(via_rccl)
     assert st["fin_host"] == 0 and st["escalations"] == 0, st
-    assert st["remote_texts_hbm"] == n_r and st["remote_texts_staged"] == len(texts) - n_r, st
+    if hostcopy:
+        assert st["remote_texts_hbm"] == 0 and st["remote_texts_copied"] == n_r, st
+        assert st["fin_staged_texts"] > 0, st
+    else:
+        assert st["remote_texts_hbm"] == n_r and st["remote_texts_staged"] == len(texts) - n_r, st
     if n_r < len(texts):
         assert st["fin_staged_texts"] > 0, st
     for s in hs:

@@ -168,7 +168,8 @@ def test_hip_spread_cluster_matches_local(name, xchg, eager, monkeypatch):
         assert delta("qmx_kernel_fin_host") == 0
         assert delta("qmx_spread_delta_mismatch_total") == 0
         if name in ("concat_think", "aggregate_4"):  # finals with text from the remote rank
-            assert delta("qmx_kernel_remote_texts_staged") + delta("qmx_kernel_remote_texts_hbm") > 0
+            assert (delta("qmx_kernel_remote_texts_staged") + delta("qmx_kernel_remote_texts_hbm")
+                    + delta("qmx_kernel_remote_texts_copied")) > 0
             assert delta("qmx_kernel_fin_items") > 0
     finally:
         live.close()
