@@ -479,6 +479,13 @@ def breakdown(m0, m1, elapsed):
         # client send of their own, per request
         "coalesced_per_req": (round(d.get("qmx_output_coalesced_total", 0.0) / d["qmx_requests_total"], 2)
                               if d.get("qmx_requests_total") else None),
+        # the latency those holds added (hold start -> released) and the share the coalescing
+        # deadline released rather than the stream's next output
+        "hold_us_avg": (round(1e6 * d["qmx_output_hold_seconds_sum"] / d["qmx_output_hold_seconds_count"], 1)
+                        if d.get("qmx_output_hold_seconds_count") else None),
+        "hold_deadline_share": (round(d.get("qmx_output_hold_deadline_total", 0.0)
+                                      / d["qmx_output_hold_seconds_count"], 3)
+                                if d.get("qmx_output_hold_seconds_count") else None),
         # spread placement (EP): how the remote streams' finals moved — bulk rounds (RCCL
         # ncclSend/ncclRecv HBM -> HBM, or tcpbulk in rehearsals) vs the mesh — what the rounds
         # cost, and whether the owner finalized them on the GPU (HBM-resident / staged texts)

@@ -50,7 +50,9 @@ std::atomic<uint64_t> c_requests{0}, c_stream{0}, c_nonstream{0}, c_errors{0}, c
     c_flush_ns{0}, c_flushes{0},  // io loop: oldest upstream bytes of a batch -> handed to the engine
     c_apply_ns{0}, c_applies{0},  // io loop: a tick's results routed -> applied (sent to clients)
     c_link_msgs{0},  // spread: exchange messages sent over the io loops' own links (no mesh thread)
-    c_coalesced{0};  // deltas held for their stream's next output instead of a send of their own
+    c_coalesced{0},  // deltas held for their stream's next output instead of a send of their own
+    c_hold_ns{0}, c_holds{0},  // a client's held (corked) output: hold start -> released (its added latency)
+    c_hold_deadline{0};        // ... released by the coalescing deadline, not by its stream
 // failures by class
 std::atomic<uint64_t> c_fail_connect{0}, c_fail_timeout{0}, c_fail_status{0}, c_fail_disconnect{0},
     c_fail_protocol{0}, c_stream_aborts{0},
@@ -365,6 +367,7 @@ struct Client {
   double t_accept = 0;
   bool want_out = false;     // EPOLLOUT armed (socket buffer was full)
   bool held = false;         // corked output held for a stream's next delta (a deferral entry is out)
+  double held_t0 = 0;        // when the hold began (qmx_output_hold_seconds)
 };
 
 enum UpMode { UP_ENGINE, UP_BUFFER, UP_PASS };
@@ -1084,11 +1087,12 @@ class Loop {
       Client* c = it->second.get();
       if (c->serial != deferq_[i].serial) continue;  // fd closed and reused by a new connection
       if (c->queued || c->want_out || c->dead || c->out_off >= c->out.size()) {
-        c->held = false;
+        unhold(c);
         continue;
       }
       if (deferq_[i].deadline <= t || g_drain.load()) {
-        c->held = false;
+        if (c->held) c_hold_deadline++;
+        unhold(c);
         c->queued = true;
         flushq_.push_back(c->fd);
         continue;
@@ -1514,7 +1518,7 @@ class Loop {
       if (it == clients_.end()) continue;
       Client* c = it->second.get();
       c->queued = false;
-      c->held = false;  // (held output leaves with this send; its deferral entry lapses)
+      unhold(c);  // (held output leaves with this send; its deferral entry lapses)
       if (c->dead || c->want_out) continue;
       while (c->out_off < c->out.size()) {
         ssize_t w = send(c->fd, c->out.data() + c->out_off, c->out.size() - c->out_off, MSG_NOSIGNAL);
@@ -2249,6 +2253,7 @@ class Loop {
     append_chunk(c, data, len);
     if (!c->held) {
       c->held = true;
+      c->held_t0 = now_s();
       deferq_.push_back(Deferred{c->fd, c->serial, now_s() + coalesce_s_});
     }
     c_coalesced++;
@@ -2261,10 +2266,16 @@ class Loop {
     if (hub_) return up_readable(up) || eng().pending(slot);
     return eng().pending(slot) || up_readable(up);
   }
+  void unhold(Client* c) {
+    if (!c->held) return;
+    c->held = false;
+    c_hold_ns += (uint64_t)(1e9 * std::max(0.0, now_s() - c->held_t0));
+    c_holds++;
+  }
   // a held client's corked output goes out with this iteration's flush (as at its deadline)
   void release_held(Client* c) {
     if (!c->held || c->queued || c->dead) return;
-    c->held = false;
+    unhold(c);
     if (c->out_off >= c->out.size() || c->want_out) return;
     c->queued = true;
     flushq_.push_back(c->fd);
@@ -3173,6 +3184,9 @@ class Loop {
     put("qmx_client_connections_total", (double)c_clients.load());
     put("qmx_ticks_total", (double)c_ticks.load());
     put("qmx_output_coalesced_total", (double)c_coalesced.load());
+    put("qmx_output_hold_seconds_sum", (double)c_hold_ns.load() * 1e-9);  // latency the holds added
+    put("qmx_output_hold_seconds_count", (double)c_holds.load());
+    put("qmx_output_hold_deadline_total", (double)c_hold_deadline.load());
     put("qmx_exchange_link_messages_total", (double)c_link_msgs.load());
     put("qmx_tick_slots_total", (double)c_tick_slots.load());
     put("qmx_tick_route_seconds_total", (double)c_route_ns.load() * 1e-9);

@@ -718,21 +718,27 @@ def test_native_output_coalescing_trickling_stream():
                 c2 = copy.deepcopy(cfg)
                 for i, name in enumerate(("b1.test", "b2.test")):
                     c2["primary_backends"][i]["url"] = f"http://127.0.0.1:{live.serve(name, ups[name])}/v1"
-                def held_total(text):
-                    return sum(float(ln.split()[-1]) for ln in text.splitlines()
-                               if ln.startswith("qmx_output_coalesced_total"))
+                def held_total(text, name="qmx_output_coalesced_total"):
+                    return sum(float(ln.split()[-1]) for ln in text.splitlines() if ln.startswith(name + " "))
 
                 with native_server(c2, tick_mode="loops") as port:
                     with httpx.Client(base_url=f"http://127.0.0.1:{port}", timeout=30) as cl:
-                        h0 = held_total(cl.get("/metrics").text)  # (process-wide counter: a delta)
+                        m0 = cl.get("/metrics").text  # (process-wide counters: deltas)
                         for _ in range(20):
                             r = cl.post("/chat/completions", json=req, headers=AUTH)
                             st, ct, evs = _normalize(r.status_code, r.headers.get("content-type"), r.content)
                             assert (st, ct, _per_stream(evs)) == want
-                        held = held_total(cl.get("/metrics").text) - h0
+                        m1 = cl.get("/metrics").text
+                held = held_total(m1) - held_total(m0)
+                holds = held_total(m1, "qmx_output_hold_seconds_count") - held_total(m0, "qmx_output_hold_seconds_count")
+                hold_s = held_total(m1, "qmx_output_hold_seconds_sum") - held_total(m0, "qmx_output_hold_seconds_sum")
                 # (whether a piece lands while a CPU tick runs is timing; the GPU bench's failure
                 # scenario, whose ticks take ~45 us, shows the holds — bench breakdown)
                 assert held == 0 if us == "0" else held >= 0, (us, held)
+                # every hold is accounted when it ends; none outlasts the deadline by much
+                # (the 1 ms epoll timeout bounds the lateness)
+                assert holds <= held and (us != "0" or holds == 0), (us, held, holds)
+                assert holds == 0 or hold_s / holds < 0.0025 + int(us) * 1e-6, (holds, hold_s)
             finally:
                 live.close()
     finally:
