@@ -201,6 +201,46 @@ def pin_rank(torch, world: int, local_rank: int, n_dev: int):
     return {"numa_nodes": nodes, "pinned": True, "cpus": len(plan[local_rank])}
 
 
+def pin_single(torch, n_dev: int):
+    """One rank: bind the bench — proxy, mocks and load generator inherit it — to a compact CPU
+    set on the GPU's NUMA node (QMX_BENCH_CPUS, default ``compact-smt``):
+
+    * ``compact-smt``: both hardware threads of as many physical cores as the job's CPU quota
+      needs, rounded up to whole last-level caches (on the MI355X box: a quota of 16 CPUs =
+      one 8-core CCD), cores in L3 order.  The proxy and its loopback peers then share one L3
+      instead of wherever the scheduler scatters them over a 256-thread machine: headline
+      365-381k req/s against 268-298k unbound, proxy CPU 17.4 vs 22-25 us per request
+      (profiles/r5/pinning).  Partial CCDs measured slower (`compact-smt@24`: 223k);
+    * ``compact`` / ``compact-smt@N``: one thread per core / N CPUs;
+    * a cpulist (``64-79``): exactly those; ``none``: no binding."""
+    spec = os.environ.get("QMX_BENCH_CPUS", "compact-smt")
+    if not spec or spec == "none":
+        return None
+    from quorum_amd.parallel.topology import compact_cpus, llc_cpus, parse_cpulist, pci_numa_node
+
+    allowed = sorted(os.sched_getaffinity(0))
+    if spec.startswith("compact"):
+        node = 0
+        if n_dev:
+            pr = torch.cuda.get_device_properties(0)
+            node = max(0, pci_numa_node(pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id))
+        kind, _, n = spec.partition("@")  # compact[-smt][@N CPUs]
+        if n:
+            want = int(n)
+        else:  # the quota, rounded up to whole last-level caches
+            llc = max(1, llc_cpus(node))
+            want = -(-available_cores() // llc) * llc
+        if want >= len(allowed):
+            return {"pinned": False, "spec": spec, "reason": "the set would be every allowed CPU"}
+        cpus = compact_cpus(want, node, allowed, smt=kind == "compact-smt")
+    else:
+        cpus = [c for c in parse_cpulist(spec) if c in set(allowed)]
+    if not cpus:
+        return {"pinned": False, "spec": spec}
+    os.sched_setaffinity(0, cpus)
+    return {"pinned": True, "spec": spec, "cpus": len(cpus), "first": cpus[0], "last": cpus[-1]}
+
+
 def write_config(path: str, mock_ports, skip_final: bool, tile: int, sc=None, placement="local") -> None:
     import yaml
 
@@ -1038,6 +1078,8 @@ def main() -> int:
     _trace("init_process_group")
     try:
         pinning = pin_rank(torch, world, local_rank, n_dev)
+        if pinning is None and world == 1:
+            pinning = pin_single(torch, n_dev)
     except (OSError, RuntimeError, ValueError, AttributeError) as e:  # placement is an optimisation only
         pinning = {"pinned": False, "error": repr(e)}
     engine = args.engine

@@ -197,6 +197,49 @@ def rank_cpus(gpu_nodes: List[int], local_rank: int, allowed: Optional[List[int]
     return sorted(c for key in keys[lo:hi] for c in cores[key])
 
 
+def _llc_key(cpu: int, root: Path) -> str:
+    try:
+        return (root / f"cpu{cpu}" / "cache" / "index3" / "shared_cpu_list").read_text().strip()
+    except OSError:
+        return ""
+
+
+def llc_cpus(node: int, node_root: Path = NUMA_NODES, cpu_root: Path = CPU_DEVICES) -> int:
+    """Hardware threads sharing the last-level cache with the node's first CPU (0: unknown)."""
+    cpus = node_cpus(node, node_root)
+    if not cpus:
+        return 0
+    k = _llc_key(cpus[0], cpu_root)
+    return len(parse_cpulist(k)) if k else 0
+
+
+def compact_cpus(n: int, node: int, allowed: Optional[List[int]] = None, smt: bool = False,
+                 node_root: Path = NUMA_NODES, cpu_root: Path = CPU_DEVICES) -> Optional[List[int]]:
+    """``n`` CPUs of NUMA node ``node`` packed into as few last-level caches (CCDs) as they
+    fit: one hardware thread per physical core (``smt``: both siblings of n / 2 cores), cores
+    in LLC order.  A single-rank bench whose job quota is ``n`` CPUs on a many-core box then
+    keeps its proxy, mocks and load generator — loopback TCP peers — on shared L3s instead of
+    wherever the scheduler scatters them.  None when the node has too few cores."""
+    ok = set(allowed) if allowed is not None else None
+    cpus = [c for c in node_cpus(node, node_root) if ok is None or c in ok]
+    cores: Dict[tuple, List[int]] = {}
+    for c in cpus:
+        cores.setdefault(_core_key(c, cpu_root), []).append(c)
+    def llc_first(cpu: int) -> int:  # an L3 is named by its lowest CPU
+        k = _llc_key(cpu, cpu_root)
+        return min(parse_cpulist(k)) if k else cpu
+
+    keys = sorted(cores, key=lambda k: (llc_first(min(cores[k])), min(cores[k])))
+    out: List[int] = []
+    for k in keys:
+        if len(out) >= n:
+            break
+        out.extend(sorted(cores[k]) if smt else [min(cores[k])])
+    if len(out) < n:
+        return None
+    return sorted(out[:n])
+
+
 def gpu_numa_nodes(root: Path = KFD_TOPOLOGY, pci_root: Path = PCI_DEVICES) -> List[int]:
     """NUMA node of every GPU in KFD order, from the KFD node's PCI address (``domain`` +
     ``location_id`` = bus << 8 | devfn) — no HIP call, so a launcher can plan before any

@@ -108,6 +108,26 @@ def test_rank_cpus_split_by_numa_node(tmp_path):
     assert topology.plan_rank_cpus([0, -1], allowed, **kw) is None
 
 
+def test_compact_cpus_pack_last_level_caches(tmp_path):
+    """compact_cpus (bench.py pin_single): N CPUs of the GPU's node on the fewest L3s — both
+    SMT siblings per core (smt) or one thread per core — cores in L3 order."""
+    _fake_numa(tmp_path, {0: 8, 1: 8})  # cpus 0-31: node 0 cores 0-7 (+16-23), node 1 8-15 (+24-31)
+    for c in range(32):  # two 4-core L3s per node: cores {0-3}, {4-7}, {8-11}, {12-15}
+        core = c % 16
+        lo = core - core % 4
+        cache = tmp_path / "cpu" / f"cpu{c}" / "cache" / "index3"
+        cache.mkdir(parents=True)
+        cache.joinpath("shared_cpu_list").write_text(f"{lo}-{lo + 3},{lo + 16}-{lo + 19}\n")
+    kw = dict(node_root=tmp_path / "node", cpu_root=tmp_path / "cpu")
+    assert topology.llc_cpus(1, **kw) == 8
+    assert topology.compact_cpus(8, 1, smt=True, **kw) == [8, 9, 10, 11, 24, 25, 26, 27]  # one L3
+    assert topology.compact_cpus(4, 0, **kw) == [0, 1, 2, 3]
+    assert topology.compact_cpus(6, 0, **kw) == [0, 1, 2, 3, 4, 5]
+    assert topology.compact_cpus(16, 0, smt=True, **kw) == list(range(8)) + list(range(16, 24))
+    assert topology.compact_cpus(17, 0, smt=True, **kw) is None  # more than the node holds
+    assert topology.compact_cpus(4, 0, allowed=[2, 3, 18, 19, 5], smt=True, **kw) == [2, 3, 18, 19]
+
+
 def test_gpu_numa_nodes_from_kfd(tmp_path):
     _fake_kfd(tmp_path / "kfd", 2)
     for g, (bus, node) in enumerate([(0x05, 0), (0xE5, 1)], start=1):
