@@ -207,7 +207,8 @@ def pin_single(torch, n_dev: int):
 
     * ``compact-smt``: both hardware threads of as many physical cores as the job's CPU quota
       needs, rounded up to whole last-level caches (on the MI355X box: a quota of 16 CPUs =
-      one 8-core CCD), cores in L3 order.  The proxy and its loopback peers then share one L3
+      one 8-core CCD), the least-loaded L3s first (a 0.2 s /proc/stat sample: the host is
+      shared with other jobs).  The proxy and its loopback peers then share one L3
       instead of wherever the scheduler scatters them over a 256-thread machine: headline
       365-381k req/s against 268-298k unbound, proxy CPU 17.4 vs 22-25 us per request
       (profiles/r5/pinning).  Partial CCDs measured slower (`compact-smt@24`: 223k);
@@ -216,7 +217,7 @@ def pin_single(torch, n_dev: int):
     spec = os.environ.get("QMX_BENCH_CPUS", "compact-smt")
     if not spec or spec == "none":
         return None
-    from quorum_amd.parallel.topology import compact_cpus, llc_cpus, parse_cpulist, pci_numa_node
+    from quorum_amd.parallel.topology import compact_cpus, cpu_busy, llc_cpus, parse_cpulist, pci_numa_node
 
     allowed = sorted(os.sched_getaffinity(0))
     if spec.startswith("compact"):
@@ -232,7 +233,8 @@ def pin_single(torch, n_dev: int):
             want = -(-available_cores() // llc) * llc
         if want >= len(allowed):
             return {"pinned": False, "spec": spec, "reason": "the set would be every allowed CPU"}
-        cpus = compact_cpus(want, node, allowed, smt=kind == "compact-smt")
+        # the least-loaded L3s of the node (the host's other tenants), packed
+        cpus = compact_cpus(want, node, allowed, smt=kind == "compact-smt", busy=cpu_busy())
     else:
         cpus = [c for c in parse_cpulist(spec) if c in set(allowed)]
     if not cpus:

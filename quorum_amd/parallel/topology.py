@@ -213,23 +213,57 @@ def llc_cpus(node: int, node_root: Path = NUMA_NODES, cpu_root: Path = CPU_DEVIC
     return len(parse_cpulist(k)) if k else 0
 
 
+def cpu_busy(interval: float = 0.2, stat: Path = Path("/proc/stat")) -> Dict[int, float]:
+    """Per-CPU busy fraction over ``interval`` seconds (/proc/stat; {} when unreadable)."""
+    import time
+
+    def read() -> Dict[int, tuple]:
+        out = {}
+        try:
+            for line in stat.read_text().splitlines():
+                f = line.split()
+                if f and f[0].startswith("cpu") and f[0] != "cpu":
+                    v = [int(x) for x in f[1:]]
+                    idle = v[3] + (v[4] if len(v) > 4 else 0)
+                    out[int(f[0][3:])] = (sum(v), idle)
+        except (OSError, ValueError):
+            return {}
+        return out
+
+    a = read()
+    time.sleep(interval)
+    b = read()
+    busy = {}
+    for c, (t1, i1) in b.items():
+        t0, i0 = a.get(c, (t1, i1))
+        busy[c] = 1.0 - (i1 - i0) / (t1 - t0) if t1 > t0 else 0.0
+    return busy
+
+
 def compact_cpus(n: int, node: int, allowed: Optional[List[int]] = None, smt: bool = False,
-                 node_root: Path = NUMA_NODES, cpu_root: Path = CPU_DEVICES) -> Optional[List[int]]:
+                 node_root: Path = NUMA_NODES, cpu_root: Path = CPU_DEVICES,
+                 busy: Optional[Dict[int, float]] = None) -> Optional[List[int]]:
     """``n`` CPUs of NUMA node ``node`` packed into as few last-level caches (CCDs) as they
     fit: one hardware thread per physical core (``smt``: both siblings of n / 2 cores), cores
     in LLC order.  A single-rank bench whose job quota is ``n`` CPUs on a many-core box then
     keeps its proxy, mocks and load generator — loopback TCP peers — on shared L3s instead of
-    wherever the scheduler scatters them.  None when the node has too few cores."""
+    wherever the scheduler scatters them.  ``busy`` (cpu_busy: other tenants' load on a shared
+    host) orders the L3s least-loaded first.  None when the node has too few cores."""
     ok = set(allowed) if allowed is not None else None
     cpus = [c for c in node_cpus(node, node_root) if ok is None or c in ok]
     cores: Dict[tuple, List[int]] = {}
     for c in cpus:
         cores.setdefault(_core_key(c, cpu_root), []).append(c)
-    def llc_first(cpu: int) -> int:  # an L3 is named by its lowest CPU
+    def llc_of(cpu: int) -> List[int]:
         k = _llc_key(cpu, cpu_root)
-        return min(parse_cpulist(k)) if k else cpu
+        return parse_cpulist(k) if k else [cpu]
 
-    keys = sorted(cores, key=lambda k: (llc_first(min(cores[k])), min(cores[k])))
+    def llc_rank(cpu: int) -> tuple:  # an L3 by its load, then by its lowest CPU
+        members = llc_of(cpu)
+        load = round(sum((busy or {}).get(c, 0.0) for c in members), 1)
+        return (load, min(members))
+
+    keys = sorted(cores, key=lambda k: (llc_rank(min(cores[k])), min(cores[k])))
     out: List[int] = []
     for k in keys:
         if len(out) >= n:

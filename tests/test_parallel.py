@@ -126,6 +126,13 @@ def test_compact_cpus_pack_last_level_caches(tmp_path):
     assert topology.compact_cpus(16, 0, smt=True, **kw) == list(range(8)) + list(range(16, 24))
     assert topology.compact_cpus(17, 0, smt=True, **kw) is None  # more than the node holds
     assert topology.compact_cpus(4, 0, allowed=[2, 3, 18, 19, 5], smt=True, **kw) == [2, 3, 18, 19]
+    # another tenant keeps the first L3 busy: the next one is taken
+    busy = {c: 0.9 for c in (0, 1, 2, 3, 16, 17, 18, 19)}
+    assert topology.compact_cpus(8, 0, smt=True, busy=busy, **kw) == [4, 5, 6, 7, 20, 21, 22, 23]
+    stat = tmp_path / "stat"
+    stat.write_text("cpu  1 2 3 4\ncpu0 10 0 10 80 0\ncpu1 0 0 0 100 0\n")
+    b = topology.cpu_busy(0.0, stat)
+    assert set(b) == {0, 1}  # (no time passed between the samples: 0 busy)
 
 
 def test_gpu_numa_nodes_from_kfd(tmp_path):
