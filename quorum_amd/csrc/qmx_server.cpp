@@ -994,6 +994,7 @@ class Loop {
       } else {
         n = epoll_wait(ep_, evs.data(), (int)evs.size(), to);
       }
+      tnow_ = now_s();  // this iteration's clock (lnow): stamps and timeouts, not hop timing
       if (lazy_wake_ && hub_) {
         in_wait_.store(false, std::memory_order_seq_cst);
         if (rq_pending_.load(std::memory_order_acquire)) on_results(false);
@@ -1314,7 +1315,7 @@ class Loop {
       if ((r.flags & (RF_DONE | RF_ABORTED)) && s->bs[bi].state == 0) {
         s->bs[bi].state = 1;
         s->bs[bi].aborted = (r.flags & RF_ABORTED) != 0;
-        if (s->bs[bi].t_fed > 0) h_engine.observe(now_s() - s->bs[bi].t_fed);
+        if (s->bs[bi].t_fed > 0) h_engine.observe(lnow() - s->bs[bi].t_fed);
         s->finished++;
       }
       if (s->stage == 0 && s->finished == (int)s->bs.size()) begin_final(s);
@@ -1418,7 +1419,7 @@ class Loop {
       auto c = std::make_unique<Client>();
       c->fd = fd;
       c->serial = ++next_serial_;
-      c->t_accept = now_s();
+      c->t_accept = lnow();
       add(fd, EPOLLIN, tag(3, fd));
       clients_[fd] = std::move(c);
       c_clients++;
@@ -1666,7 +1667,7 @@ class Loop {
     c_requests++;
     c->served++;
     auto s = std::make_unique<Session>();
-    s->t0 = now_s();
+    s->t0 = lnow();
     std::string perr;
     if (!json_parse(body.data(), body.size(), s->body, &perr)) {
       c_errors++;
@@ -1824,7 +1825,7 @@ class Loop {
     u->rp.keep_headers = mode != UP_ENGINE;
     u->req = std::move(req);
     u->timeout = timeout;
-    u->last_io = now_s();
+    u->last_io = lnow();
     u->t_open = u->last_io;
     u->deadline = cfg_.total_timeout > 0 ? u->last_io + cfg_.total_timeout : 0;
     if (!be.resolved || (be.https && !tls_)) return nullptr;
@@ -1901,7 +1902,7 @@ class Loop {
         int w = SSL_write(u->ssl, u->req.data() + u->req_off, (int)(u->req.size() - u->req_off));
         if (w > 0) {
           u->req_off += w;
-          u->last_io = now_s();
+          u->last_io = lnow();
           continue;
         }
         int e = SSL_get_error(u->ssl, w);
@@ -1921,7 +1922,7 @@ class Loop {
       cnt(SC_UP_SEND);
       if (w > 0) {
         u->req_off += w;
-        u->last_io = now_s();
+        u->last_io = lnow();
         continue;
       }
       if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
@@ -1983,9 +1984,9 @@ class Loop {
       while (true) {
         ssize_t r = up_read(u, buf, sizeof(buf));
         if (r > 0) {
-          if (!u->got_bytes) h_upstream_ttfb.observe(now_s() - u->t_open);
+          if (!u->got_bytes) h_upstream_ttfb.observe(lnow() - u->t_open);
           u->got_bytes = true;
-          u->last_io = now_s();
+          u->last_io = lnow();
           if (u->rp.feed(buf, r, body) < 0) {
             c_fail_protocol++;
             return up_error(u, "invalid HTTP response");
@@ -2110,7 +2111,7 @@ class Loop {
   void on_up_body(Up* u, std::string& body) {
     Session* s = u->sess;
     if (u->rp.status == 200 && u->mode == UP_ENGINE) {
-      if (s->bs[u->bi].t_fed == 0) s->bs[u->bi].t_fed = now_s();
+      if (s->bs[u->bi].t_fed == 0) s->bs[u->bi].t_fed = lnow();
       e_feed_move(s->bs[u->bi].slot, body);  // the engine takes the buffer (no copy)
       kick();
       return;
@@ -2242,7 +2243,7 @@ class Loop {
   void send_content(Session* s, const char* data, size_t len, bool hold = false) {
     if (!s->first_content) {
       s->first_content = true;
-      h_ttft.observe(now_s() - s->t0);
+      h_ttft.observe(lnow() - s->t0);
     }
     if (!s->cl) return;
     Client* c = s->cl;
@@ -2253,8 +2254,8 @@ class Loop {
     append_chunk(c, data, len);
     if (!c->held) {
       c->held = true;
-      c->held_t0 = now_s();
-      deferq_.push_back(Deferred{c->fd, c->serial, now_s() + coalesce_s_});
+      c->held_t0 = lnow();
+      deferq_.push_back(Deferred{c->fd, c->serial, lnow() + coalesce_s_});
     }
     c_coalesced++;
   }
@@ -2269,7 +2270,7 @@ class Loop {
   void unhold(Client* c) {
     if (!c->held) return;
     c->held = false;
-    c_hold_ns += (uint64_t)(1e9 * std::max(0.0, now_s() - c->held_t0));
+    c_hold_ns += (uint64_t)(1e9 * std::max(0.0, lnow() - c->held_t0));
     c_holds++;
   }
   // a held client's corked output goes out with this iteration's flush (as at its deadline)
@@ -3367,6 +3368,8 @@ class Loop {
   const bool lazy_wake_ = env_flag("QMX_LAZY_WAKE", false);   // A/B knob (see attach_hub)
   std::atomic<bool> in_wait_{false};                          // in epoll_wait (lazy wake)
   double ops_t0_ = 0;  // the oldest unflushed FEED op (flush-wait timing)
+  double tnow_ = now_s();  // refreshed after every epoll wait (lnow: stamps and timeouts)
+  double lnow() const { return tnow_; }
   int64_t role_sec_ = -1;      // second of the cached SSE head + role event
   std::string role_head_;
   // fault injection (tests): drop every Nth stream result's SSE bytes before it is sent
