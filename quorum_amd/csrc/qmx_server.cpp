@@ -118,12 +118,35 @@ inline bool env_flag(const char* name, bool dflt) {
 // has a colon, building each key and value string once (no per-line/per-field temporaries).
 // ASCII lower case (what tolower does in the C locale, inline: no locale lookup per byte)
 inline char alow(unsigned char c) { return (char)(c - 'A' < 26u ? c | 0x20 : c); }
+// "\r\n" / "\r\n\r\n" in [p, p+n): memchr for the '\r' (vectorised) and a look at the next
+// bytes — glibc's memmem sets up a two-way search per call, which for these 2- and 4-byte
+// needles over short HTTP heads and chunk-size lines cost more than the search itself
+inline const char* find_crlf(const char* p, size_t n) {
+  const char* e = p + n;
+  while (p < e) {
+    const char* r = (const char*)memchr(p, '\r', (size_t)(e - p));
+    if (!r || r + 1 >= e) return nullptr;
+    if (r[1] == '\n') return r;
+    p = r + 1;
+  }
+  return nullptr;
+}
+inline const char* find_crlfcrlf(const char* p, size_t n) {
+  const char* e = p + n;
+  while (p < e) {
+    const char* r = find_crlf(p, (size_t)(e - p));
+    if (!r || r + 3 >= e) return nullptr;
+    if (r[2] == '\r' && r[3] == '\n') return r;
+    p = r + 2;
+  }
+  return nullptr;
+}
 template <class F>
 void for_each_header(const char* p, size_t n, F&& f) {
   auto ws = [](char ch) { return ch == ' ' || ch == '\t'; };
   size_t pos = 0;
   while (pos < n) {
-    const char* e0 = (const char*)memmem(p + pos, n - pos, "\r\n", 2);
+    const char* e0 = find_crlf(p + pos, n - pos);
     size_t e = e0 ? (size_t)(e0 - p) : n;
     const char* colon = (const char*)memchr(p + pos, ':', e - pos);
     if (colon) {
@@ -256,7 +279,10 @@ struct RespParser {
     }
     out.reserve(out.size() + n);  // at most n body bytes arrive with n bytes
     auto find = [&](const char* pat, size_t pl, size_t from) -> size_t {
-      const void* f = from <= len ? memmem(d + from, len - from, pat, pl) : nullptr;
+      if (from > len) return std::string::npos;
+      const void* f = pl == 2 && pat[0] == '\r' && pat[1] == '\n' ? find_crlf(d + from, len - from)
+                      : pl == 4 && memcmp(pat, "\r\n\r\n", 4) == 0 ? find_crlfcrlf(d + from, len - from)
+                                                                  : memmem(d + from, len - from, pat, pl);
       return f ? (size_t)((const char*)f - d) : std::string::npos;
     };
     size_t i = 0;
@@ -267,7 +293,7 @@ struct RespParser {
         const char* hp = d + i;
         size_t hn = he - i;
         i = he + 4;
-        const char* le0 = (const char*)memmem(hp, hn, "\r\n", 2);
+        const char* le0 = find_crlf(hp, hn);
         size_t le = le0 ? (size_t)(le0 - hp) : hn;
         if (le < 12 || memcmp(hp, "HTTP/", 5) != 0) return -1;
         status = 0;
