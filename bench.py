@@ -1011,9 +1011,11 @@ def main() -> int:
     ap.add_argument("--threads", type=int, default=0,
                     help="native impl: io threads per rank (0: min(8, cores / (2 x ranks)), at least 2 — "
                          "the node's cores are shared by every rank's proxy, mocks and load generator)")
-    # 3 load-generator threads: every response is validated (the envelope fast path costs
-    # ~2-5 us per response), two threads saturate near 110k req/s on the MI355X box
-    ap.add_argument("--lg-threads", type=int, default=3)
+    # load-generator threads (every response is validated; the envelope fast path costs ~2-5
+    # us per response): 0 = 4 when the bench is bound to a compact CPU set (408-425k req/s vs
+    # 372-374k with 3, p50 TTFT 0.12 vs 0.15 ms), else 3 (unbound, a 4th thread measured
+    # slower: 261k vs 301k) — profiles/r5/pinning
+    ap.add_argument("--lg-threads", type=int, default=0)
     ap.add_argument("--mock-threads", type=int, default=2)
     ap.add_argument("--skip-final", type=int, default=1)
     ap.add_argument("--tile", type=int, default=16384)
@@ -1084,6 +1086,8 @@ def main() -> int:
             pinning = pin_single(torch, n_dev)
     except (OSError, RuntimeError, ValueError, AttributeError) as e:  # placement is an optimisation only
         pinning = {"pinned": False, "error": repr(e)}
+    if args.lg_threads <= 0:
+        args.lg_threads = 4 if (pinning or {}).get("pinned") else 3
     engine = args.engine
     if engine == "auto":  # BASELINE config 1 is the CPU plumbing path; the rest run on the GPU
         engine = sc.get("engine") or ("hip" if n_dev else "cpu")
@@ -1308,7 +1312,8 @@ def main() -> int:
                            # hip: io loops post their own ticks into one multi-door grid ("loops",
                            # the default) or hand streams to tick-lane threads ("lanes")
                            "tick_mode": os.environ.get("QMX_TICK_MODE", "auto") if engine == "hip" else None,
-                           "io_threads_per_rank": args.threads, "cpu_pinning": pinning,
+                           "io_threads_per_rank": args.threads, "loadgen_threads": args.lg_threads,
+                           "mock_threads": args.mock_threads, "cpu_pinning": pinning,
                            # the node's xGMI topology, only when every rank has a GPU of its own
                            # (a rehearsal's ranks share one: no link claim to make)
                            "gpu_links": ({k: v for k, v in link_summary().items() if k != "links_per_gpu"}
