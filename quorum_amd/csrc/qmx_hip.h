@@ -240,7 +240,7 @@ struct TickLane {
   double item_us = 0, start_spread_us = 0;
   double items_host_us = 0;
   double relay_us = 0, pickup_us = 0, grid_span_us = 0, grid_ticks = 0;  // persistent: doorbell seen -> ...  // host: result records -> slot state + SSE strings (process_item)  // per tick: mean item run, last item start - first
-  double stage_us[35] = {0};  // [20]: an item's system-scope release fence (stage timing)
+  double stage_us[38] = {0};  // [20]: an item's system-scope release fence (stage timing)
   double clk_cycles = 0, clk_us = 0;
   // finalize arenas (fused into this lane's tick launches)
   FinItem* h_fin = nullptr;

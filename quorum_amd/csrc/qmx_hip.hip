@@ -1498,6 +1498,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
         shape_bad = !half_clear(sm) || L < tp + ts;
       }
       // (b) the event's other possible shapes (block-uniform fast flag; ballots wave-wide)
+      if (P.dbg != nullptr && tid == 0 && kb == 0) dbg_put(&P.dbg[bi * kDbg + 38], __builtin_amdgcn_s_memrealtime());
       const bool try_b = have && !ok && fast && L <= 256;
       bool done_ev = false;
       int hq = -1;
@@ -1538,6 +1539,7 @@ __device__ __forceinline__ void tick_body(const WorkItem* __restrict__ items, co
         }
         hq = done_ev || okm == 0 ? -1 : __ffs(okm) - 1;
       }
+      if (P.dbg != nullptr && tid == 0 && kb == 0) dbg_put(&P.dbg[bi * kDbg + 39], __builtin_amdgcn_s_memrealtime());
       // unresolved: 0xFE when the stream template cannot match (its prefix / suffix differ:
       // the loop skips its own template compare), 0xFF otherwise (an escaped or non-ASCII
       // body the loop's exact string check may still accept, or no check ran)
@@ -4051,6 +4053,9 @@ void HipEngine::complete(HipJob& J, std::vector<SlotResult>& results, std::vecto
         sub(32, 3, 35);   // S3a on wave 0: before its rounds / round 1 / the rest
         sub(33, 35, 36);
         sub(34, 36, 34);
+        sub(35, 35, 38);  // S3a round 1 on wave 0: content-template compare / other shapes (b) / the rest
+        sub(36, 38, 39);
+        sub(37, 39, 36);
         if (d[27] && d[27] >= B.h_res[i].t1 && B.h_res[i].t1) L.stage_us[20] += (double)(d[27] - B.h_res[i].t1) * 0.01;
       }
       L.stage_n += n;
@@ -4281,7 +4286,7 @@ void HipEngine::collect_finalize(TickLane& L, const std::vector<const FinalizeRe
 
 std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   std::unordered_map<std::string, double> m;
-  double stage[35] = {0}, cyc = 0, cus = 0;
+  double stage[38] = {0}, cyc = 0, cus = 0;
   for (auto& Lp : lanes_) {
     TickLane& L = *Lp;
     std::lock_guard<std::mutex> lg(L.mu);
@@ -4323,7 +4328,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
     m["fin_launches"] += (double)L.fin_launches;  // tick launches that also carried finalize work
     m["fin_items"] += (double)L.fin_items;
     m["fin_staged_texts"] += (double)L.fin_staged;  // mesh-delivered remote finals staged into items
-    for (int k = 1; k < 35; ++k) stage[k] += L.stage_us[k];
+    for (int k = 1; k < 38; ++k) stage[k] += L.stage_us[k];
     cyc += L.clk_cycles;
     cus += L.clk_us;
   }
@@ -4351,6 +4356,9 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   m["stage_s3apre_us"] = stage[32];
   m["stage_s3around1_us"] = stage[33];
   m["stage_s3arest_us"] = stage[34];
+  m["stage_s3ar1tpl_us"] = stage[35];
+  m["stage_s3ar1b_us"] = stage[36];
+  m["stage_s3ar1end_us"] = stage[37];
   m["stage_fence_us"] = stage[20];  // the item's system-scope release fence (L2 write-back)
   m["shader_mhz"] = cus > 0 ? cyc / cus : 0.0;
   m["clk_cycles"] = cyc;  // summable across engines (/metrics sums the io loops' engines)
