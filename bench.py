@@ -177,14 +177,17 @@ def available_cores() -> int:
 
 
 def pin_rank(torch, world: int, local_rank: int, n_dev: int):
-    """One rank per GPU on a multi-socket node: bind this rank (and the proxy, mocks and load
-    generator it spawns) to its GPU's NUMA node, splitting the node's cores between the ranks
-    whose GPUs hang off it (parallel/topology.py).  Skipped for one rank, for rehearsals
-    with more ranks than GPUs, when NUMA information is missing or would strand cores, and
-    with QMX_BENCH_PIN=0."""
+    """One rank per GPU: bind this rank (and the proxy, mocks and load generator it spawns) to
+    a compact CPU set on its GPU's NUMA node — whole L3s, both SMT threads, its share of the
+    job's CPU quota rounded up to whole L3s and at most two (one rank measured the same on one
+    or two CCDs and slower spread further: profiles/r5/pinning), ranks sharing a node on
+    consecutive L3s (parallel/topology.py rank_llc_cpus); where that does not fit, the node's
+    cores split between its ranks (rank_cpus).  Skipped for one rank (pin_single), for
+    rehearsals with more ranks than GPUs, when NUMA information is missing, and with
+    QMX_BENCH_PIN=0."""
     if world <= 1 or n_dev == 0 or os.environ.get("QMX_BENCH_PIN", "1") == "0":
         return None
-    from quorum_amd.parallel.topology import pci_numa_node, plan_rank_cpus
+    from quorum_amd.parallel.topology import llc_cpus, pci_numa_node, plan_rank_cpus, rank_llc_cpus
 
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     if n_dev < local_world:
@@ -194,11 +197,21 @@ def pin_rank(torch, world: int, local_rank: int, n_dev: int):
         pr = torch.cuda.get_device_properties(r)
         nodes.append(pci_numa_node(pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id))
     allowed = sorted(os.sched_getaffinity(0))
-    plan = plan_rank_cpus(nodes, allowed)
-    if plan is None or not plan[local_rank]:
+    llc = llc_cpus(max(0, nodes[local_rank]))  # 0: no cache topology -> the node split
+    cpus = None
+    if llc > 0:
+        share = max(1, available_cores() // max(1, local_world))
+        per_rank = min(-(-share // llc) * llc, 2 * llc)
+        cpus = rank_llc_cpus(nodes, local_rank, per_rank, allowed)
+    how = "llc"
+    if not cpus:
+        plan = plan_rank_cpus(nodes, allowed)
+        cpus = plan[local_rank] if plan else None
+        how = "node"
+    if not cpus:
         return {"numa_nodes": nodes, "pinned": False}
-    os.sched_setaffinity(0, plan[local_rank])
-    return {"numa_nodes": nodes, "pinned": True, "cpus": len(plan[local_rank])}
+    os.sched_setaffinity(0, cpus)
+    return {"numa_nodes": nodes, "pinned": True, "how": how, "cpus": len(cpus), "first": cpus[0], "last": cpus[-1]}
 
 
 def pin_single(torch, n_dev: int):

@@ -274,6 +274,33 @@ def compact_cpus(n: int, node: int, allowed: Optional[List[int]] = None, smt: bo
     return sorted(out[:n])
 
 
+def rank_llc_cpus(gpu_nodes: List[int], local_rank: int, per_rank: int, allowed: Optional[List[int]] = None,
+                  node_root: Path = NUMA_NODES, cpu_root: Path = CPU_DEVICES) -> Optional[List[int]]:
+    """``local_rank``'s compact CPU set: whole last-level caches (both SMT threads of their
+    cores) of its GPU's NUMA node, ``per_rank`` CPUs rounded up to whole L3s; the ranks whose
+    GPUs share the node take consecutive L3s in CPU order (every rank computes the same,
+    disjoint split without talking to the others).  None when the node is unknown or has too
+    few L3s for its ranks."""
+    node = gpu_nodes[local_rank] if 0 <= local_rank < len(gpu_nodes) else -1
+    if node < 0 or per_rank <= 0:
+        return None
+    ok = set(allowed) if allowed is not None else None
+    cpus = [c for c in node_cpus(node, node_root) if ok is None or c in ok]
+    groups: Dict[str, List[int]] = {}
+    for c in cpus:
+        groups.setdefault(_llc_key(c, cpu_root) or f"cpu{c}", []).append(c)
+    order = sorted(groups.values(), key=min)
+    if not order:
+        return None
+    llc = max(len(g) for g in order)
+    k = max(1, -(-per_rank // llc))
+    peers = [r for r, n in enumerate(gpu_nodes) if n == node]
+    p = peers.index(local_rank)
+    if (p + 1) * k > len(order):
+        return None
+    return sorted(c for g in order[p * k:(p + 1) * k] for c in g)
+
+
 def gpu_numa_nodes(root: Path = KFD_TOPOLOGY, pci_root: Path = PCI_DEVICES) -> List[int]:
     """NUMA node of every GPU in KFD order, from the KFD node's PCI address (``domain`` +
     ``location_id`` = bus << 8 | devfn) — no HIP call, so a launcher can plan before any

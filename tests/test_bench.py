@@ -193,8 +193,24 @@ def test_pin_rank_numa_plan(monkeypatch):
     monkeypatch.setattr(os, "sched_setaffinity", lambda pid, cpus: got.setdefault("cpus", list(cpus)))
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
     monkeypatch.delenv("QMX_BENCH_PIN", raising=False)
+    # no L3 topology -> the node split (plan_rank_cpus)
+    monkeypatch.setattr(topology, "llc_cpus", lambda node: 0)
     r = bench.pin_rank(fake_torch, 8, 5, 8)
-    assert r == {"numa_nodes": [0, 0, 0, 0, 1, 1, 1, 1], "pinned": True, "cpus": 1} and got["cpus"] == [5]
+    assert r["numa_nodes"] == [0, 0, 0, 0, 1, 1, 1, 1] and r["pinned"] and r["how"] == "node" and r["cpus"] == 1
+    assert got.pop("cpus") == [5]
+    # L3s known: whole L3s, the quota share rounded up (16 CPUs of a 128-CPU quota over 8 ranks)
+    monkeypatch.setattr(topology, "llc_cpus", lambda node: 16)
+    monkeypatch.setattr(bench, "available_cores", lambda: 128)
+    seen = {}
+    monkeypatch.setattr(topology, "rank_llc_cpus",
+                        lambda nodes, rank, per, allowed: seen.setdefault("per", per) and list(range(64, 80)))
+    r = bench.pin_rank(fake_torch, 8, 5, 8)
+    assert r["how"] == "llc" and r["cpus"] == 16 and seen["per"] == 16 and got.pop("cpus") == list(range(64, 80))
+    monkeypatch.setattr(bench, "available_cores", lambda: 256)  # no quota: at most two L3s per rank
+    seen.clear()
+    bench.pin_rank(fake_torch, 8, 5, 8)
+    assert seen["per"] == 32
+    got.clear()
     assert bench.pin_rank(fake_torch, 1, 0, 8) is None
     assert bench.pin_rank(fake_torch, 8, 0, 1) is None  # more ranks than GPUs
     monkeypatch.setenv("QMX_BENCH_PIN", "0")

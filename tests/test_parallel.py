@@ -135,6 +135,26 @@ def test_compact_cpus_pack_last_level_caches(tmp_path):
     assert set(b) == {0, 1}  # (no time passed between the samples: 0 busy)
 
 
+def test_rank_llc_cpus_disjoint_compact_sets(tmp_path):
+    """rank_llc_cpus (bench.py pin_rank): every rank whole L3s of its GPU's node, ranks of one
+    node on consecutive, disjoint L3s; too many ranks for the node's L3s -> None."""
+    _fake_numa(tmp_path, {0: 8, 1: 8})
+    for c in range(32):  # 4-core L3s: {0-3,16-19}, {4-7,20-23}, {8-11,24-27}, {12-15,28-31}
+        core = c % 16
+        lo = core - core % 4
+        cache = tmp_path / "cpu" / f"cpu{c}" / "cache" / "index3"
+        cache.mkdir(parents=True)
+        cache.joinpath("shared_cpu_list").write_text(f"{lo}-{lo + 3},{lo + 16}-{lo + 19}\n")
+    kw = dict(node_root=tmp_path / "node", cpu_root=tmp_path / "cpu")
+    nodes = [0, 0, 1, 1]
+    sets = [topology.rank_llc_cpus(nodes, r, 8, **kw) for r in range(4)]
+    assert sets[0] == [0, 1, 2, 3, 16, 17, 18, 19] and sets[1] == [4, 5, 6, 7, 20, 21, 22, 23]
+    assert sets[2] == [8, 9, 10, 11, 24, 25, 26, 27] and sets[3] == [12, 13, 14, 15, 28, 29, 30, 31]
+    assert topology.rank_llc_cpus([0, 0], 1, 9, **kw) is None  # 2 L3s each: node 0 holds 2
+    assert topology.rank_llc_cpus([0], 0, 9, **kw) == list(range(8)) + list(range(16, 24))
+    assert topology.rank_llc_cpus([-1], 0, 8, **kw) is None
+
+
 def test_gpu_numa_nodes_from_kfd(tmp_path):
     _fake_kfd(tmp_path / "kfd", 2)
     for g, (bus, node) in enumerate([(0x05, 0), (0xE5, 1)], start=1):
