@@ -44,6 +44,7 @@ BASELINE_SOURCE_SURVEY = "reference proxy, survey container (8 vCPU, Python harn
 # +100 + 10 rank + i mock backends, +200 + rank / +230 + rank each rank's own admin port
 # (headline / spread check)
 ADMIN_OFF, SPREAD_ADMIN_OFF, LOCAL_ADMIN_OFF, RDV_ADMIN_OFF, C3_ADMIN_OFF = 200, 230, 240, 250, 260
+RANK_PORT_OFF = 300  # QMX_BENCH_RANK_PORTS: rank r's proxy and load generator on port + 300 + r
 CONFIG3_REQUESTS = 4096  # per rank: the config-3 pass after the headline (spread, RCCL rounds)
 PROBE_REQUESTS = 256  # spread check: requests of the one-connection latency probes
 
@@ -190,10 +191,16 @@ def pin_rank(torch, world: int, local_rank: int, n_dev: int):
     from quorum_amd.parallel.topology import llc_cpus, pci_numa_node, plan_rank_cpus, rank_llc_cpus
 
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-    if n_dev < local_world:
+    rehearse = os.environ.get("QMX_BENCH_PIN_REHEARSE") == "1"  # ranks sharing GPU 0, bound as if on its node
+    if n_dev < local_world and not rehearse:
         return None
     nodes = []
-    for r in range(local_world):
+    if n_dev < local_world:  # rehearsal: every rank on GPU 0's node (KFD topology: no HIP call here)
+        from quorum_amd.parallel.topology import gpu_numa_nodes
+
+        g = gpu_numa_nodes()
+        nodes = [max(0, g[0]) if g else 0] * local_world
+    for r in range(len(nodes), local_world):
         pr = torch.cuda.get_device_properties(r)
         nodes.append(pci_numa_node(pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id))
     allowed = sorted(os.sched_getaffinity(0))
@@ -1161,7 +1168,11 @@ def main() -> int:
         else:
             env["QMX_READY_FILE"] = os.path.join(tmp, "ready")
             env["QMX_ADMIN_PORT"] = str(admin_port)
-            proxy_procs = spawn_workers(cfg_path, "127.0.0.1", args.port, args.workers, engine,
+            if world > 1 and os.environ.get("QMX_BENCH_RANK_PORTS") == "1":
+                # client-side sharding: this rank's load generator drives this rank's proxy
+                # only (its own port), not every rank's through the shared SO_REUSEPORT port
+                proxy_port = args.port + RANK_PORT_OFF + rank
+            proxy_procs = spawn_workers(cfg_path, "127.0.0.1", proxy_port, args.workers, engine,
                                         device, impl=args.impl, threads=args.threads, env=env)
             for p in proxy_procs:
                 p.ready_file = f"{env['QMX_READY_FILE']}.{p.pid}"
