@@ -44,7 +44,7 @@ BASELINE_SOURCE_SURVEY = "reference proxy, survey container (8 vCPU, Python harn
 # +100 + 10 rank + i mock backends, +200 + rank / +230 + rank each rank's own admin port
 # (headline / spread check)
 ADMIN_OFF, SPREAD_ADMIN_OFF, LOCAL_ADMIN_OFF, RDV_ADMIN_OFF, C3_ADMIN_OFF = 200, 230, 240, 250, 260
-RANK_PORT_OFF = 300  # QMX_BENCH_RANK_PORTS: rank r's proxy and load generator on port + 300 + r
+RANK_PORT_OFF = 300  # multi-rank: rank r's proxy and load generator on port + 300 + r (QMX_BENCH_RANK_PORTS)
 CONFIG3_REQUESTS = 4096  # per rank: the config-3 pass after the headline (spread, RCCL rounds)
 PROBE_REQUESTS = 256  # spread check: requests of the one-connection latency probes
 
@@ -1168,9 +1168,13 @@ def main() -> int:
         else:
             env["QMX_READY_FILE"] = os.path.join(tmp, "ready")
             env["QMX_ADMIN_PORT"] = str(admin_port)
-            if world > 1 and os.environ.get("QMX_BENCH_RANK_PORTS") == "1":
+            if world > 1 and os.environ.get("QMX_BENCH_RANK_PORTS", "1") != "0":
                 # client-side sharding: this rank's load generator drives this rank's proxy
-                # only (its own port), not every rank's through the shared SO_REUSEPORT port
+                # only (its own port), not every rank's through the shared SO_REUSEPORT port —
+                # the same per-rank share of sessions, without the co-located client's loopback
+                # crossing L3s and sockets to the other ranks' proxies.  Rehearsal on one GPU,
+                # ranks bound to L3s (QMX_BENCH_PIN_REHEARSE): 229k -> 318k req/s at 2 ranks,
+                # 464k -> 589k at 4 (profiles/r5/rankports); QMX_BENCH_RANK_PORTS=0: shared port
                 proxy_port = args.port + RANK_PORT_OFF + rank
             proxy_procs = spawn_workers(cfg_path, "127.0.0.1", proxy_port, args.workers, engine,
                                         device, impl=args.impl, threads=args.threads, env=env)
@@ -1326,7 +1330,10 @@ def main() -> int:
                         "expected event contract",
                 "config": {"model": f"{sc['desc']}, skip_final_aggregation={skip_final}",
                            "global_batch": args.batch * world, "seq_len": 26,
-                           "parallelism": f"dp{world} (sessions sharded over GPUs via SO_REUSEPORT)"
+                           "parallelism": f"dp{world} (sessions sharded over GPUs: "
+                                          + ("each rank's clients on its own port)"
+                                             if world > 1 and proxy_port == args.port + RANK_PORT_OFF + rank
+                                             else "SO_REUSEPORT)")
                                           + (f" + ep{world} (backend streams spread over ranks, "
                                                 f"{xchg_kind.upper()} exchange)"
                                              if args.placement == "spread" and world > 1 else ""),
