@@ -243,7 +243,11 @@ def test_native_drain_finishes_inflight(tmp_path):
                     res["body"] = b"".join(r.iter_bytes())
         th = threading.Thread(target=client)
         th.start()
-        time.sleep(0.3)
+        # SIGTERM once the stream is in flight (its head arrived), not after a fixed sleep: on
+        # a loaded machine the client may not have connected yet and would meet a closed port
+        t_end = time.time() + 10
+        while "status" not in res and time.time() < t_end:
+            time.sleep(0.01)
         os.kill(w.pid, signal.SIGTERM)
         th.join(timeout=20)
         assert res.get("status") == 200
