@@ -357,3 +357,43 @@ def test_spread_and_config3_summaries_report_degraded_and_invariants():
                              "load": dict(ok_pass, req_s=25.0, bulk_rounds=5, p50_ttft_ms=0.5)}])
     assert c3["requests"] == 200 and c3["req_s"] == 50.0  # 200 requests / the slower rank's 4 s
     assert c3["bulk_rounds"] == 12 and c3["ok"] is True and "degraded" not in c3
+
+
+def test_pin_single_specs(monkeypatch):
+    """bench.pin_single (one rank): ``compact-smt`` takes the quota rounded up to whole L3s
+    on the GPU's node, ``@N`` a given count, a cpulist exactly those CPUs (within the
+    affinity set), ``none`` nothing; a set that would be every allowed CPU binds nothing."""
+    import importlib.util
+
+    from quorum_amd.parallel import topology
+
+    spec = importlib.util.spec_from_file_location("qmx_bench_mod2", BENCH)
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    got = {}
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(256)))
+    monkeypatch.setattr(os, "sched_setaffinity", lambda pid, cpus: got.__setitem__("cpus", list(cpus)))
+    monkeypatch.setattr(topology, "llc_cpus", lambda node: 16)
+    monkeypatch.setattr(topology, "cpu_busy", lambda: {})
+    asked = {}
+
+    def compact(n, node, allowed, smt=False, busy=None):
+        asked.update(n=n, node=node, smt=smt)
+        return list(range(64, 64 + n))
+
+    monkeypatch.setattr(topology, "compact_cpus", compact)
+    monkeypatch.setattr(bench, "available_cores", lambda: 12)
+    monkeypatch.delenv("QMX_BENCH_CPUS", raising=False)
+    r = bench.pin_single(None, 0)  # no GPU: node 0
+    assert r["pinned"] and asked == {"n": 16, "node": 0, "smt": True} and got.pop("cpus") == list(range(64, 80))
+    monkeypatch.setenv("QMX_BENCH_CPUS", "compact@8")
+    r = bench.pin_single(None, 0)
+    assert asked["n"] == 8 and not asked["smt"] and r["cpus"] == 8
+    monkeypatch.setenv("QMX_BENCH_CPUS", "8-11,300")
+    r = bench.pin_single(None, 0)
+    assert got.pop("cpus") == [8, 9, 10, 11] and r["cpus"] == 4
+    monkeypatch.setenv("QMX_BENCH_CPUS", "none")
+    assert bench.pin_single(None, 0) is None
+    monkeypatch.delenv("QMX_BENCH_CPUS")
+    monkeypatch.setattr(bench, "available_cores", lambda: 256)  # the whole machine: nothing to gain
+    assert bench.pin_single(None, 0)["pinned"] is False
