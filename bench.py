@@ -566,6 +566,11 @@ def breakdown(m0, m1, elapsed):
                       "remote_texts_hbm": int(d.get("qmx_kernel_remote_texts_hbm", 0.0)),
                       "remote_texts_staged": int(d.get("qmx_kernel_remote_texts_staged", 0.0)),
                       "remote_texts_copied": int(d.get("qmx_kernel_remote_texts_copied", 0.0)),
+                      # (RCCL at world > 1) copied HBM -> host by the exchange's bulk thread, and
+                      # of them by an io loop instead (must stay 0: a device copy on the loop)
+                      "host_copied_by_exchange": int(d.get("qmx_exchange_host_copied_total", 0.0)),
+                      "copied_inline": int(d.get("qmx_kernel_remote_texts_copied_inline", 0.0)),
+                      "release_deferred": int(d.get("qmx_spread_release_deferred_total", 0.0)),
                       "hops_us": hop_means(d)}
                      if d.get("qmx_remote_streams_total") else None),
         # where a request's time goes (server-side means over the timed region): upstream
@@ -599,6 +604,29 @@ def breakdown(m0, m1, elapsed):
                         if d.get("qmx_kernel_stage_items") else None),
         "shader_mhz": (round(d["qmx_kernel_clk_cycles"] / d["qmx_kernel_clk_us"], 1)
                        if d.get("qmx_kernel_clk_us") else None),
+        # io-loop passes (epoll return -> next wait) over 1 / 5 ms in the timed region, and the
+        # longest pass the process has had (not a delta): a blocked loop shows here
+        # loop ticks: grid (re)launches and idle stops in the timed region, and the longest of
+        # each the process had — every io loop that posts meanwhile waits for them
+        "grid": ({"launches": int(d.get("qmx_kernel_grid_launches", 0.0)),
+                  "stops": int(d.get("qmx_kernel_grid_stops", 0.0)),
+                  "launch_ms_max": round(1e-3 * m1.get("qmx_kernel_grid_launch_us_max", 0.0), 2),
+                  "calibrate_ms_max": round(1e-3 * m1.get("qmx_kernel_grid_launch_calibrate_us_max", 0.0), 2),
+                  "stop_ms_max": round(1e-3 * m1.get("qmx_kernel_grid_stop_us_max", 0.0), 2)}
+                 if "qmx_kernel_grid_launches" in m1 else None),
+        "runtime_allocs": int(d.get("qmx_kernel_runtime_allocs", 0.0)),
+        "runtime_alloc_ms": round(1e-3 * d.get("qmx_kernel_runtime_alloc_us", 0.0), 2),
+        "loop_passes_over_1ms": int(d.get("qmx_loop_passes_over_1ms_total", 0.0)),
+        "loop_passes_over_5ms": int(d.get("qmx_loop_passes_over_5ms_total", 0.0)),
+        "loop_pass_max_ms": round(1e3 * m1.get("qmx_loop_pass_max_seconds", 0.0), 2),
+        # HIP streams of the proxy process vs the hardware queues per priority level: a persistent
+        # grid on an exclusive (highest-priority) stream has its queue to itself (qmx_streams.h)
+        "hip_streams": ({"shared": int(m1.get("qmx_kernel_streams_shared", 0.0)),
+                         "exclusive": int(m1.get("qmx_kernel_streams_exclusive", 0.0)),
+                         "hw_queues_per_priority": int(m1.get("qmx_kernel_hw_queues_per_priority", 0.0)),
+                         "grid_queue_exclusive": bool(m1.get("qmx_kernel_grid_queue_exclusive", 0.0)),
+                         "grid_queue_ok": bool(m1.get("qmx_kernel_grid_queue_ok", 0.0))}
+                        if "qmx_kernel_hw_queues_per_priority" in m1 else None),
     }
 
 
@@ -1140,9 +1168,13 @@ def main() -> int:
         if n_dev:  # processes sharing this rank's GPU (persistent tick grids need it alone)
             env["QMX_GPU_SHARERS"] = str(max(1, -(-int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) // n_dev)))
         xchg_kind = None
-        if args.placement == "spread" and world > 1:
+        # QMX_SPREAD_SELF=1 at one rank (GPU rehearsal of the multi-rank path): the odd backends
+        # of every session go through the rank's own exchange, final texts in RCCL rounds to itself
+        self_spread = args.placement == "spread" and world == 1 and os.environ.get("QMX_SPREAD_SELF") == "1"
+        if args.placement == "spread" and (world > 1 or self_spread):
             nonce = [str(time.time_ns()) if rank == 0 else None]
-            dist.broadcast_object_list(nonce, src=0)
+            if world > 1:
+                dist.broadcast_object_list(nonce, src=0)
             env.update(exchange_env(rank, world, args.port, nonce[0]))
             # RCCL needs one GPU per rank: ranks sharing a GPU (a rehearsal) run the same bulk
             # rounds with the socket executor
@@ -1336,7 +1368,9 @@ def main() -> int:
                                              else "SO_REUSEPORT)")
                                           + (f" + ep{world} (backend streams spread over ranks, "
                                                 f"{xchg_kind.upper()} exchange)"
-                                             if args.placement == "spread" and world > 1 else ""),
+                                             if args.placement == "spread" and world > 1 else
+                                             f" + self spread ({xchg_kind.upper()} rounds to itself)"
+                                             if self_spread else ""),
                            "impl": "none (no proxy)" if direct else args.impl,
                            "engine": None if direct else engine if args.impl != "reference" else "reference",
                            "conns_per_rank": args.conns,
@@ -1348,7 +1382,10 @@ def main() -> int:
                            # the node's xGMI topology, only when every rank has a GPU of its own
                            # (a rehearsal's ranks share one: no link claim to make)
                            "gpu_links": ({k: v for k, v in link_summary().items() if k != "links_per_gpu"}
-                                         if world > 1 and n_dev >= world else None)},
+                                         if world > 1 and n_dev >= world else None),
+                           # rank 0's proxy: HIP streams vs hardware queues per priority level
+                           "hip_queues": bd.get("hip_streams"),
+                           "self_spread": bool(self_spread) or None},
                 "p50_ttft_ms": round(p50, 3),
                 "p99_ttft_ms": round(max(r[3] for r in rows), 3),
                 "p50_ttfb_ms": round(statistics.median(r[5] for r in rows), 3),

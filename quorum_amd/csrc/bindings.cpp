@@ -497,6 +497,9 @@ PYBIND11_MODULE(_qmx, m) {
       .def("stop", &HipGrid::stop, py::call_guard<py::gil_scoped_release>())
       .def("stats", &HipGrid::stats);
   m.def("_free_doors", [](HipEngine& e) { return e.free_doors(); });
+  m.def("stream_stats", &stream_stats);
+  m.def("stream_probe", &stream_probe, py::arg("n"), py::arg("wait_ms") = 200.0,
+        py::call_guard<py::gil_scoped_release>());
   py::class_<HipEngine> he(m, "HipEngine");
   he.def(py::init([](const std::vector<std::string>& tags, int device, int tile, int max_slots, int content_cap,
                       int lanes, HipGrid* grid, int door, int ndoors) {

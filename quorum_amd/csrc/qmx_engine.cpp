@@ -551,7 +551,7 @@ size_t HostEngine::content_size(int slot) {
   return core_[slot].content.size();
 }
 
-void HostEngine::set_remote_content(int slot, const std::string* bytes, size_t len) {
+void HostEngine::set_remote_content(int slot, const std::string* bytes, size_t len, bool /*host_copied*/) {
   if (slot < 0 || slot >= (int)nslots()) return;
   core_[slot].content = bytes ? *bytes : std::string(len, '\0');
 }

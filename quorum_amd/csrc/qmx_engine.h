@@ -232,13 +232,14 @@ class HostEngine {
   // Spread placement (qmx_exchange.h): a stream whose final text another rank produced.
   // content_device_ptr: the slot's HBM content area (nullptr: host engine / host path);
   // content_size: filtered content bytes so far; set_remote_content: the slot's content
-  // becomes `len` bytes — *bytes if given, else already written into the HBM area.
+  // becomes `len` bytes — *bytes if given, else already written into the HBM area;
+  // host_copied: *bytes are a host copy of what a bulk round wrote into that area (counters).
   virtual void* content_device_ptr(int /*slot*/, size_t* cap) {
     *cap = 0;
     return nullptr;
   }
   virtual size_t content_size(int slot);
-  virtual void set_remote_content(int slot, const std::string* bytes, size_t len);
+  virtual void set_remote_content(int slot, const std::string* bytes, size_t len, bool host_copied = false);
 
   const TagSet& tagset() const { return ts_; }
 

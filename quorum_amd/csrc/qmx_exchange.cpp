@@ -3,6 +3,7 @@
 #include "qmx_env.h"
 #include "qmx_exchange.h"
 #include "qmx_prof.h"
+#include "qmx_streams.h"
 
 #include <arpa/inet.h>
 #include <errno.h>
@@ -134,7 +135,11 @@ struct Exchange::Impl {
   struct Sink {
     void* dev = nullptr;
     size_t cap = 0;
-    int pinned = 0;  // RCCL rounds receiving straight into dev right now (forget_bulk waits)
+    int pinned = 0;  // RCCL rounds receiving straight into dev right now
+    // forget_bulk() while pinned: no new round pins it; the last unpin erases it and, with a
+    // slot, delivers X_RELEASE{a = release_slot} to release_loop
+    bool forgotten = false;
+    int release_slot = -1, release_loop = -1;
   };
   struct Manifest {
     int round = 0, epoch = 0;
@@ -808,29 +813,27 @@ void Exchange::expect_bulk(uint64_t skey, int bi, void* dev, size_t cap) {
   k.dev = dev;
   k.cap = cap;
 }
-bool Exchange::forget_bulk(uint64_t skey, int bi) {
-  // a round receiving into this sink right now writes it until the round is over: wait (a
-  // session that ends while its remote final is in flight — a client that left — is rare,
-  // and a round is bounded by timeout_s), so a true return means no later write into the
-  // released slot.  A round that outlives twice its timeout (its communicator could not be
-  // drained) returns false: the caller must not reuse the slot (it leaks it, loudly).
-  std::unique_lock<std::mutex> g(im_->bmu);
-  const double t0 = now_s();
-  for (;;) {
-    auto it = im_->sinks.find({skey, bi});
-    if (it == im_->sinks.end()) return true;
-    if (it->second.pinned <= 0 || stop_.load()) {
-      im_->sinks.erase(it);
-      return true;
-    }
-    if (now_s() - t0 > 2.0 * o_.timeout_s + 1.0) {
-      fprintf(stderr, "qmx exchange (rank %d): a bulk round still writes into the shadow slot of session %llx "
-              "stream %d after %.1f s: the slot is not reused\n", o_.rank, (unsigned long long)skey, bi,
-              now_s() - t0);
-      return false;
-    }
-    im_->bcv.wait_for(g, std::chrono::milliseconds(1));
+bool Exchange::forget_bulk(uint64_t skey, int bi, int slot, int loop) {
+  // Never waits: the caller is an io loop (session teardown, a remote final applied), and a
+  // round stuck on a failed peer can take up to its timeout — every connection, upstream and
+  // tick of that loop would wait with it.  A sink a round is writing into right now is marked
+  // instead; the bulk thread erases it when the round is over and hands the slot back to its
+  // loop (X_RELEASE).  A round that never ends keeps the slot: it is not reused (leaked).
+  std::lock_guard<std::mutex> g(im_->bmu);
+  auto it = im_->sinks.find({skey, bi});
+  if (it == im_->sinks.end()) return true;
+  Impl::Sink& k = it->second;
+  if (k.pinned <= 0 || stop_.load()) {
+    im_->sinks.erase(it);
+    return true;
   }
+  k.forgotten = true;
+  if (slot >= 0) {
+    k.release_slot = slot;
+    k.release_loop = loop;
+    deferred_releases_++;
+  }
+  return false;
 }
 
 void Exchange::request_stop() {
@@ -1023,10 +1026,19 @@ struct BulkOp {
   bool done = false; // receive (host executors): its bytes are all in, whatever the round does
   void* sink = nullptr;  // receive (device executors): the owner's HBM shadow slot, pinned for
                          // the round; nullptr: no sink registered — received and discarded
+  bool pinned = false;   // receive: its sink is pinned for the round (any executor: the owner's
+                         // slot is not released while a round is receiving for it)
+};
+
+struct CopyReq {  // copy_out: `len` bytes at `dev` (HBM) into *out
+  const void* dev;
+  size_t len;
+  std::string* out;
 };
 
 struct BulkExec {
   virtual ~BulkExec() = default;
+  virtual bool copy_out(std::vector<CopyReq>&) { return false; }  // device executors
   virtual bool device() const = 0;
   virtual bool form(const std::string& id, int epoch, double timeout_s, const std::atomic<bool>& stop) = 0;
   virtual void drop() = 0;
@@ -1045,7 +1057,7 @@ class RcclExec : public BulkExec {
   RcclExec(int device, int world, int rank, size_t max_text)
       : device_(device), world_(world), rank_(rank), cap_(std::max<size_t>(max_text, 256)) {
     XHIP(hipSetDevice(device_));
-    XHIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    st_ = stream_create(StreamKind::Shared);  // (a persistent grid's queue is never shared: qmx_streams.h)
     XHIP(hipMalloc(&scratch_, cap_));
     XHIP(hipMalloc(&zeros_, cap_));
     XHIP(hipMemset(zeros_, 0, cap_));
@@ -1054,7 +1066,8 @@ class RcclExec : public BulkExec {
     drop();
     if (scratch_) hipFree(scratch_);
     if (zeros_) hipFree(zeros_);
-    if (st_) hipStreamDestroy(st_);
+    if (stage_) hipHostFree(stage_);
+    stream_destroy(st_, StreamKind::Shared);
   }
   bool device() const override { return true; }
   bool formed() const override { return comm_ != nullptr; }
@@ -1101,6 +1114,32 @@ class RcclExec : public BulkExec {
     if (e == hipSuccess) return 1;
     return e == hipErrorNotReady ? 0 : -1;
   }
+  // A completed round's received texts, HBM → host: every copy queued on the round's own
+  // stream into one pinned staging buffer, then one synchronisation.  The copy is a new
+  // dispatch on this device, so it reads what a peer GPU wrote into HBM.
+  bool copy_out(std::vector<CopyReq>& req) override {
+    size_t need = 0;
+    for (const CopyReq& r : req) need += (r.len + 63) & ~(size_t)63;
+    if (need > stage_cap_) {
+      if (stage_) hipHostFree(stage_);
+      stage_ = nullptr;
+      stage_cap_ = 0;
+      if (hipHostMalloc((void**)&stage_, need, hipHostMallocDefault) != hipSuccess) return false;
+      stage_cap_ = need;
+    }
+    size_t off = 0;
+    for (const CopyReq& r : req) {
+      if (hipMemcpyAsync(stage_ + off, r.dev, r.len, hipMemcpyDeviceToHost, st_) != hipSuccess) return false;
+      off += (r.len + 63) & ~(size_t)63;
+    }
+    if (hipStreamSynchronize(st_) != hipSuccess) return false;
+    off = 0;
+    for (CopyReq& r : req) {
+      r.out->assign((const char*)stage_ + off, r.len);
+      off += (r.len + 63) & ~(size_t)63;
+    }
+    return true;
+  }
 
  private:
   bool ready(double deadline, const std::atomic<bool>& stop) {  // non-blocking communicator settled
@@ -1118,6 +1157,8 @@ class RcclExec : public BulkExec {
   size_t cap_ = 0;             // max_text: the discard and zero buffers' size
   uint8_t* scratch_ = nullptr;  // discarded receives
   uint8_t* zeros_ = nullptr;    // vanished sends' bytes
+  uint8_t* stage_ = nullptr;    // copy_out's pinned staging (grows to the largest batch)
+  size_t stage_cap_ = 0;
 };
 
 #pragma pack(push, 1)
@@ -1570,11 +1611,14 @@ void Exchange::bulk_loop() {
       }
       if (e.dst == o_.rank) {
         BulkOp o{&e, false, nullptr, std::string()};
-        if (ex->device()) {  // straight into the owner's shadow slot, pinned until the round is over
+        {  // device executors receive straight into the owner's shadow slot; every executor
+           // pins the sink until the round is over (forget_bulk defers the slot's release)
           std::lock_guard<std::mutex> g(I.bmu);
           auto it = I.sinks.find({e.skey, e.bi});
-          if (it != I.sinks.end() && it->second.dev && it->second.cap >= e.len) {
-            o.sink = it->second.dev;
+          if (it != I.sinks.end() && !it->second.forgotten &&
+              (!ex->device() || (it->second.dev && it->second.cap >= e.len))) {
+            if (ex->device()) o.sink = it->second.dev;
+            o.pinned = true;
             ++it->second.pinned;
           }
         }
@@ -1626,12 +1670,37 @@ void Exchange::bulk_loop() {
     } else {
       rounds_++;
     }
+    // host copies (XOptions::host_copy): the received texts leave HBM here, on the bulk thread,
+    // in one batch on the round's stream, while their sinks are still pinned — the owner's io
+    // loop gets the bytes and never copies
+    std::vector<std::string> copied;
+    std::vector<char> copy_ok;
+    if (ok && ex->device() && o_.host_copy) {
+      copied.resize(ops.size());
+      copy_ok.assign(ops.size(), 0);
+      std::vector<CopyReq> req;
+      std::vector<size_t> which;
+      for (size_t k = 0; k < ops.size(); ++k)
+        if (!ops[k].send && ops[k].sink && ops[k].e->len) {
+          req.push_back(CopyReq{ops[k].sink, ops[k].e->len, &copied[k]});
+          which.push_back(k);
+        }
+      if (!req.empty() && ex->copy_out(req)) {
+        for (size_t k : which) copy_ok[k] = 1;
+        host_copied_ += req.size();
+      } else if (!req.empty()) {
+        fprintf(stderr, "qmx exchange (rank %d): host copy of round %d's %zu texts failed — reported missed\n",
+                o_.rank, mf.round, req.size());
+      }
+    }
     // receives: deliver what arrived (all of them, or — a failed round — the transfers a
     // host executor completed), and tell every sender which of its texts got here
-    for (auto& o : ops) {
+    for (size_t k = 0; k < ops.size(); ++k) {
+      BulkOp& o = ops[k];
       if (o.send) continue;
       const WireEntry& e = *o.e;
       bool got = ok || o.done;
+      bool hostcopy = false;
       if (got) {
         bulk_bytes_ += e.len;
         XMsg v;
@@ -1645,14 +1714,22 @@ void Exchange::bulk_loop() {
             // expect_bulk) must not wait forever: reported missed, the sender resends over
             // the mesh; no sink at all: the session is gone, nobody needs the text (got)
             deliver = false;
-            if (it != I.sinks.end()) got = false;
+            if (it != I.sinks.end() && !it->second.forgotten) got = false;
+          } else if (o_.host_copy && e.len) {
+            if (copy_ok[k]) {
+              v.payload = std::move(copied[k]);
+              hostcopy = true;
+            } else {  // the copy failed: the sender resends over the mesh
+              deliver = false;
+              got = false;
+            }
           }
         } else {
           v.payload = std::move(o.host);  // host executor: the bytes ride the delivery
         }
         if (deliver) {
           v.type = X_BULK;
-          v.flags = e.flags;
+          v.flags = (uint8_t)(e.flags | (hostcopy ? XF_HOSTCOPY : 0));
           v.skey = e.skey;
           v.bi = e.bi;
           v.a = (int32_t)e.len;  // device executors: already in the owner's HBM content arena
@@ -1665,19 +1742,25 @@ void Exchange::bulk_loop() {
       ack(e, got);
     }
     // the round is over (and, failed, its communicator aborted and its stream drained): no
-    // more writes into the pinned sinks — a waiting forget_bulk() may release them now
+    // more writes into the pinned sinks — a sink its owner forgot meanwhile is erased and its
+    // slot handed back to the owner's loop (forget_bulk)
     {
-      bool unpinned = false;
       std::lock_guard<std::mutex> g(I.bmu);
       for (auto& o : ops) {
-        if (o.send || !o.sink) continue;
+        if (o.send || !o.pinned) continue;
         auto it = I.sinks.find({o.e->skey, o.e->bi});
-        if (it != I.sinks.end() && it->second.pinned > 0) {
-          --it->second.pinned;
-          unpinned = true;
+        if (it == I.sinks.end() || it->second.pinned <= 0) continue;
+        if (--it->second.pinned > 0 || !it->second.forgotten) continue;
+        if (it->second.release_slot >= 0) {
+          XMsg r;
+          r.type = X_RELEASE;
+          r.a = it->second.release_slot;
+          r.skey = it->first.first;
+          r.bi = it->first.second;
+          out[(size_t)std::max(0, it->second.release_loop) % nloops_].push_back(std::move(r));
         }
+        I.sinks.erase(it);
       }
-      if (unpinned) I.bcv.notify_all();
     }
     deliver_all();
     send_reports(mf.round);

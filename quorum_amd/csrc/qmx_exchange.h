@@ -48,9 +48,12 @@ enum XType : uint8_t {
   X_UP = 8,      // exchange → loops: peer `a` (re)joined the mesh
   X_LINK = 9,    // exchange → loop: a connected per-loop link to peer `a` (fd `b`; payload: bytes
                  //   already read from it) — the loop owns the socket from here on
+  X_RELEASE = 10,  // exchange → owner loop: the round that was writing into shadow slot `a` is
+                   //   over — the slot whose release forget_bulk() deferred may be released now
 };
-// X_FINAL / X_BULK / X_SENT flags
-enum : uint8_t { XF_TEXT = 1, XF_ABORTED = 2, XF_FAILED = 4 };
+// X_FINAL / X_BULK / X_SENT flags (XF_HOSTCOPY: an X_BULK whose bytes a bulk round put in HBM
+// and the bulk thread copied out — XOptions::host_copy)
+enum : uint8_t { XF_TEXT = 1, XF_ABORTED = 2, XF_FAILED = 4, XF_HOSTCOPY = 8 };
 
 struct XMsg {
   uint8_t type = 0, flags = 0;
@@ -80,6 +83,12 @@ struct XOptions {
   // the higher rank once the pair's mesh connection forms), so a session's opens, deltas and
   // eager finals go io loop → socket → io loop with no mesh thread on the data path
   bool links = true;
+  // device executors: every received text is copied HBM → host by the bulk thread as soon as
+  // its round completes (one batch on the executor's stream) and X_BULK carries the bytes, so
+  // the owner's io loop never issues a copy of its own.  For RCCL at world > 1, where a peer
+  // GPU wrote the bytes and a persistent grid cannot be relied on to see them in HBM
+  // (HipEngine::set_remote_hbm_direct)
+  bool host_copy = false;
 };
 
 // the mesh's view of one peer
@@ -109,9 +118,12 @@ class Exchange {
   // Owner: a bulk for (skey, bi) lands at `dev` (HBM, capacity `cap`); nullptr / a mesh
   // transfer delivers the bytes in X_BULK's payload instead.
   void expect_bulk(uint64_t skey, int bi, void* dev, size_t cap);
-  // false: a round is still writing into the sink (stuck past twice its timeout) — the
-  // caller must not reuse the slot
-  bool forget_bulk(uint64_t skey, int bi);
+  // The owner is done with (skey, bi)'s sink.  Never blocks.  true: no round writes into it,
+  // the slot may be reused now.  false: a round is writing into it right now — the slot must
+  // not be reused yet; when that round is over the exchange delivers X_RELEASE (a = `slot`) to
+  // io loop `loop` (slot < 0: nothing is delivered, and a later forget_bulk decides).  Either
+  // way no new round pins the sink.
+  bool forget_bulk(uint64_t skey, int bi, int slot = -1, int loop = -1);
   void request_stop();
   void join();
   bool healthy() const { return healthy_.load(); }  // the mesh formed once and is running
@@ -139,6 +151,8 @@ class Exchange {
   // receiver reports that arrived before their send was carried (kept until it is)
   uint64_t early_reports() const { return early_reports_.load(); }
   uint64_t links() const { return links_.load(); }  // per-loop links handed to the io loops
+  uint64_t host_copied() const { return host_copied_.load(); }  // received texts copied HBM → host (host_copy)
+  uint64_t deferred_releases() const { return deferred_releases_.load(); }  // forget_bulk → X_RELEASE
 
   struct Impl;
 
@@ -149,7 +163,7 @@ class Exchange {
   std::unique_ptr<Impl> im_;
   std::atomic<bool> stop_{false}, healthy_{false}, rccl_ok_{false};
   std::atomic<uint64_t> rounds_{0}, bytes_{0}, bulk_bytes_{0}, mesh_bulk_{0}, msgs_{0}, rccl_epoch_{0}, rejoins_{0},
-      downs_{0}, rescued_{0}, links_{0}, sweeps_{0}, early_reports_{0};
+      downs_{0}, rescued_{0}, links_{0}, sweeps_{0}, early_reports_{0}, host_copied_{0}, deferred_releases_{0};
   std::atomic<double> busy_us_{0};
   std::thread mesh_th_, bulk_th_;
   void mesh_loop();

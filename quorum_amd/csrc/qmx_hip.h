@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "qmx_engine.h"
+#include "qmx_streams.h"
 
 namespace qmx {
 
@@ -185,6 +186,7 @@ class HipGrid {
   PDoor* h_doors_ = nullptr;  // host-mapped, n_ of them
   PCtl* d_ctls_ = nullptr;    // device, n_ of them
   std::atomic<uint64_t> launches_{0}, stops_{0}, revivals_{0};
+  double launch_us_max_ = 0, launch_cal_us_max_ = 0, launch_us_sum_ = 0, stop_us_max_ = 0;  // under mu_ (exclusive)
 };
 
 // Launch resources of one tick lane: a tick thread owns a lane (HIP stream, events,
@@ -192,7 +194,8 @@ class HipGrid {
 // tick kernels in flight at once over disjoint slot sets (HostEngine busy flags).
 struct TickLane {
   std::mutex mu;  // held by the lane's tick for its whole process(); kernel_stats() reads under it
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // none for a door of the shared grid (loop ticks)
+  StreamKind skind = StreamKind::Shared;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evb = nullptr;
   KParams params;
   uint64_t params_ver = 1;  // bumped whenever `params` changes (each Buf uploads its own copy)
@@ -298,7 +301,7 @@ class HipEngine : public HostEngine {
   std::string text(int slot) override;
   void* content_device_ptr(int slot, size_t* cap) override;
   size_t content_size(int slot) override;
-  void set_remote_content(int slot, const std::string* bytes, size_t len) override;
+  void set_remote_content(int slot, const std::string* bytes, size_t len, bool host_copied = false) override;
   // An RCCL round's final text in this slot's HBM content area: read there by the next
   // finalize item (direct), or first copied to the host and staged like a mesh-delivered
   // text.  A peer GPU's writes into coarse-grained HBM are coherent with this device's L2
@@ -352,6 +355,15 @@ class HipEngine : public HostEngine {
   // which a persistent grid would hold up)
   void retire_host(void* p);
   void retire_dev(void* p);
+  void note_alloc(double t0, size_t bytes);
+  std::atomic<uint64_t> allocs_{0}, alloc_bytes_{0};
+  std::atomic<double> alloc_us_{0.0}, alloc_max_us_{0.0};
+
+ public:
+  void* halloc(size_t bytes);  // pinned + mapped host memory (timed: kernel_stats runtime_alloc_*)
+  void* dalloc(size_t bytes);  // device memory (timed)
+
+ private:
   std::vector<void*> grave_host_, grave_dev_;
   std::mutex grave_mu_;
 
@@ -372,7 +384,8 @@ class HipEngine : public HostEngine {
   std::vector<uint8_t> remote_host_;
   std::vector<uint32_t> content_len_;    // device content bytes per slot
   // stats
-  std::atomic<uint64_t> escalations_{0}, fin_host_{0}, remote_dev_{0}, remote_staged_{0}, remote_copied_{0};
+  std::atomic<uint64_t> escalations_{0}, fin_host_{0}, remote_dev_{0}, remote_staged_{0}, remote_copied_{0},
+      remote_copied_inline_{0};
   bool remote_hbm_direct_ = true;
   int spin_us_ = 0;  // QMX_WAIT_SPIN_US: yield-poll before the blocking wait
   bool poll_ = true;  // QMX_WAIT=event: wait on a blocking-sync HIP event instead of polling

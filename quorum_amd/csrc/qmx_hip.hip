@@ -21,6 +21,7 @@
 // Semantics: SURVEY §2.7 (reference src/quorum/oai_proxy.py:262-371, 578-673).
 #include "qmx_env.h"
 #include "qmx_hip.h"
+#include "qmx_streams.h"
 
 #include <rocprofiler-sdk-roctx/roctx.h>
 
@@ -3065,6 +3066,114 @@ static double steady_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// ---- stream registry (qmx_streams.h) -----------------------------------------------------
+namespace {
+std::atomic<int> g_streams_shared{0}, g_streams_excl{0};
+std::atomic<uint64_t> g_streams_created{0};
+}  // namespace
+
+bool exclusive_queues() {
+  const char* q = env_get("QMX_GRID_QUEUE");
+  if (q && std::string(q) == "shared") return false;
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return false;
+  return least != greatest;
+}
+
+hipStream_t stream_create(StreamKind kind) {
+  hipStream_t s = nullptr;
+  if (kind == StreamKind::Exclusive && exclusive_queues()) {
+    int least = 0, greatest = 0;
+    HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest));
+  } else {
+    HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  }
+  (kind == StreamKind::Exclusive ? g_streams_excl : g_streams_shared).fetch_add(1);
+  g_streams_created.fetch_add(1);
+  return s;
+}
+
+void stream_destroy(hipStream_t s, StreamKind kind) {
+  if (!s) return;
+  hipStreamDestroy(s);
+  (kind == StreamKind::Exclusive ? g_streams_excl : g_streams_shared).fetch_sub(1);
+}
+
+__global__ void qmx_touch(uint32_t* mark) {
+  if (threadIdx.x == 0) __hip_atomic_store(mark, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+std::unordered_map<std::string, double> stream_probe(int n, double wait_ms) {
+  n = std::max(1, std::min(n, 64));
+  uint32_t* marks = nullptr;
+  HIP_CHECK(hipHostMalloc((void**)&marks, 4 * (size_t)(n + 1), hipHostMallocMapped));
+  std::memset(marks, 0, 4 * (size_t)(n + 1));
+  uint8_t* dsrc = nullptr;
+  HIP_CHECK(hipMalloc((void**)&dsrc, 4096));
+  std::vector<uint8_t> host(4096);
+  std::vector<hipStream_t> st;
+  for (int i = 0; i < n; ++i) st.push_back(stream_create(StreamKind::Shared));
+  const double t0 = steady_s();
+  for (int i = 0; i < n; ++i) {
+    hipLaunchKernelGGL(qmx_touch, dim3(1), dim3(64), 0, st[i], marks + i);
+    HIP_CHECK(hipGetLastError());
+  }
+  hipEvent_t ev;
+  HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  HIP_CHECK(hipMemcpyAsync(host.data(), dsrc, 4096, hipMemcpyDeviceToHost, 0));
+  HIP_CHECK(hipEventRecord(ev, 0));
+  auto done = [&](int i) { return __atomic_load_n(marks + i, __ATOMIC_ACQUIRE) != 0; };
+  double last = 0;
+  int ndone = 0;
+  bool null_done = false;
+  while (steady_s() - t0 < 1e-3 * wait_ms) {
+    ndone = 0;
+    for (int i = 0; i < n; ++i) ndone += done(i);
+    null_done = hipEventQuery(ev) == hipSuccess;
+    if (ndone == n && null_done) {
+      last = 1e3 * (steady_s() - t0);
+      break;
+    }
+    sched_yield();
+  }
+  // drain before the streams go (a blocked one completes once whatever holds its queue leaves)
+  const double t1 = steady_s();
+  bool drained = false;
+  while (steady_s() - t1 < 5.0) {
+    bool all = hipEventQuery(ev) == hipSuccess;
+    for (int i = 0; i < n && all; ++i) all = done(i);
+    if (all) {
+      drained = true;
+      break;
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  }
+  if (drained) {
+    for (hipStream_t s : st) stream_destroy(s, StreamKind::Shared);
+    hipEventDestroy(ev);
+    hipFree(dsrc);
+    hipHostFree(marks);
+  }  // (else leaked: destroying a stream with work queued would wait for it)
+  return {{"streams", (double)n}, {"completed", (double)ndone}, {"null_stream_copy_done", null_done ? 1.0 : 0.0},
+          {"all_done_ms", last}, {"drained", drained ? 1.0 : 0.0}};
+}
+
+std::unordered_map<std::string, double> stream_stats() {
+  const char* hq = env_get("GPU_MAX_HW_QUEUES");
+  const int queues = hq ? std::max(1, atoi(hq)) : 4;  // HIP's default
+  const int ex = g_streams_excl.load(), sh = g_streams_shared.load();
+  const bool own = exclusive_queues();
+  return {{"streams_shared", (double)sh},
+          {"streams_exclusive", (double)ex},
+          {"streams_created", (double)g_streams_created.load()},
+          {"hw_queues_per_priority", (double)queues},
+          {"grid_queue_exclusive", own ? 1.0 : 0.0},
+          // every persistent grid alone on a queue: exclusive streams have a priority level of
+          // their own and fit its pool
+          {"grid_queue_ok", own && ex <= queues ? 1.0 : 0.0}};
+}
+
 // Wait for a lane's stream without pinning a core: the io loops share the CPU with the tick
 // threads.  A blocking-sync event sleeps on the completion interrupt: measured on MI355X
 // (tools/probes/launch_bench.hip) launch+wait = 11 us, vs 18 us spinning
@@ -3210,10 +3319,11 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
     // HIP streams share GPU_MAX_HW_QUEUES hardware queues round-robin, and a persistent grid
     // holds its queue: a second lane's grid on the same queue would wait for the first to
     // idle out (MI355X, 4 lanes / 4 queues: the first result of a tick came 100 us late).
-    // Persistent lanes need a queue each, with one left for everything else.
+    // Persistent lanes need a queue each: on exclusive (highest-priority) streams that level's
+    // pool holds only them; on shared streams one queue stays for everything else.
     const char* hq = env_get("GPU_MAX_HW_QUEUES");
     const int queues = hq ? std::max(1, atoi(hq)) : 4;
-    if (persistent_ && lanes > queues - 1) persistent_ = false;
+    if (persistent_ && lanes > (exclusive_queues() ? queues : queues - 1)) persistent_ = false;
   }
   if (grid_) {  // the shared grid is the only way this engine's ticks run
     persistent_ = false;
@@ -3273,10 +3383,15 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
     }
   for (int i = 0; i < std::max(1, lanes); ++i) {
     std::unique_ptr<TickLane> L(new TickLane());
-    HIP_CHECK(hipStreamCreateWithFlags(&L->stream, hipStreamNonBlocking));
-    HIP_CHECK(hipEventCreate(&L->ev0));
-    HIP_CHECK(hipEventCreate(&L->ev1));
-    HIP_CHECK(hipEventCreateWithFlags(&L->evb, hipEventBlockingSync | hipEventDisableTiming));
+    if (!grid_) {
+      // loop ticks (a door of the shared grid) launch nothing of their own: no stream, no
+      // events.  A lane whose ticks may run on a persistent grid holds its queue: exclusive
+      L->skind = persistent_ ? StreamKind::Exclusive : StreamKind::Shared;
+      L->stream = stream_create(L->skind);
+      HIP_CHECK(hipEventCreate(&L->ev0));
+      HIP_CHECK(hipEventCreate(&L->ev1));
+      HIP_CHECK(hipEventCreateWithFlags(&L->evb, hipEventBlockingSync | hipEventDisableTiming));
+    }
     L->params = base_params_;
     HIP_CHECK(hipMalloc((void**)&L->d_btpl, sizeof(BackendTpl) * 2 * kBackendTpl * ndoors_));
     HIP_CHECK(hipMemset(L->d_btpl, 0, sizeof(BackendTpl) * 2 * kBackendTpl * ndoors_));
@@ -3346,12 +3461,36 @@ HipEngine::~HipEngine() {
     if (L->ev0) hipEventDestroy(L->ev0);
     if (L->ev1) hipEventDestroy(L->ev1);
     if (L->evb) hipEventDestroy(L->evb);
-    if (L->stream) hipStreamDestroy(L->stream);
+    stream_destroy(L->stream, L->skind);
   }
   for (void* p : grave_host_) hipHostFree(p);
   for (void* p : grave_dev_) hipFree(p);
   if (d_state_) hipFree(d_state_);
   if (d_content_) hipFree(d_content_);
+}
+
+// Arena growth while serving (the io loop's or lane's thread): timed, because a pinned
+// allocation can take milliseconds and the thread serves sockets (kernel_stats: runtime_allocs)
+void* HipEngine::halloc(size_t bytes) {
+  const double t0 = steady_s();
+  void* p = nullptr;
+  HIP_CHECK(hipHostMalloc(&p, bytes, hipHostMallocMapped));
+  note_alloc(t0, bytes);
+  return p;
+}
+void* HipEngine::dalloc(size_t bytes) {
+  const double t0 = steady_s();
+  void* p = nullptr;
+  HIP_CHECK(hipMalloc(&p, bytes));
+  note_alloc(t0, bytes);
+  return p;
+}
+void HipEngine::note_alloc(double t0, size_t bytes) {
+  const double us = 1e6 * (steady_s() - t0);
+  allocs_.fetch_add(1, std::memory_order_relaxed);
+  alloc_bytes_.fetch_add(bytes, std::memory_order_relaxed);
+  alloc_us_.store(alloc_us_.load(std::memory_order_relaxed) + us, std::memory_order_relaxed);
+  if (us > alloc_max_us_.load(std::memory_order_relaxed)) alloc_max_us_.store(us, std::memory_order_relaxed);
 }
 
 void HipEngine::retire_host(void* p) {
@@ -3430,7 +3569,7 @@ void HipEngine::ensure_in(TickLane::Buf& B, size_t bytes) {
   if (bytes <= B.in_cap) return;
   if (B.h_in) retire_host(B.h_in);
   B.in_cap = std::max(bytes, B.in_cap * 2);
-  HIP_CHECK(hipHostMalloc((void**)&B.h_in, B.in_cap + 64, hipHostMallocMapped));
+  B.h_in = (uint8_t*)halloc(B.in_cap + 64);
 }
 void HipEngine::ensure_out(TickLane& L, size_t bytes) {
   const auto t0 = std::chrono::steady_clock::now();
@@ -3444,7 +3583,7 @@ void HipEngine::ensure_out(TickLane& L, size_t bytes) {
       if (bytes > a->cap) {
         if (a->p) retire_host(a->p);
         a->cap = std::max(bytes, a->cap * 2);
-        HIP_CHECK(hipHostMalloc((void**)&a->p, a->cap + 64, hipHostMallocMapped));
+        a->p = (uint8_t*)halloc(a->cap + 64);
       }
       L.out = a;
       L.h_out = a->p;
@@ -3509,8 +3648,10 @@ size_t HipEngine::content_size(int slot) {
 //  * the mesh (bytes): kept with the slot and staged into the finalize item's host-mapped
 //    input (prep_finalize), which the item copies into the HBM area first (fin_stage) — no
 //    synchronous copy in the io loop;
+//  * an RCCL text at world > 1 (host_copied): the exchange's bulk thread copied it out of HBM
+//    right after its round (XOptions::host_copy) — staged like a mesh text;
 //  * a text longer than the slot's HBM area takes the host path.
-void HipEngine::set_remote_content(int slot, const std::string* bytes, size_t len) {
+void HipEngine::set_remote_content(int slot, const std::string* bytes, size_t len, bool host_copied) {
   if (slot < 0 || slot >= (int)nslots()) return;
   if (slot >= max_slots_ || len > content_cap_) {
     if (slot < max_slots_) host_mode_[slot] = 1;
@@ -3520,13 +3661,15 @@ void HipEngine::set_remote_content(int slot, const std::string* bytes, size_t le
   if (bytes) {
     core_[slot].content = *bytes;
     remote_host_[slot] = 1;
-    ++remote_staged_;
+    ++(host_copied ? remote_copied_ : remote_staged_);
   } else if (!remote_hbm_direct_) {
+    // no host copy came with it (a caller other than the server's exchange path): copy here.
     // (the round's stream was synchronised before the text is applied; this copy is a new
     // dispatch on the device, so it sees the peer's writes)
     core_[slot].content = device_content(slot, len);
     remote_host_[slot] = 1;
     ++remote_copied_;
+    ++remote_copied_inline_;
   } else {
     ++remote_dev_;
   }
@@ -3632,8 +3775,8 @@ void HipEngine::prepare(HipJob& J) {
     retire_host(B.h_items);
     retire_host(B.h_res);
     B.items_cap = work.size() * 2;
-    HIP_CHECK(hipHostMalloc((void**)&B.h_items, sizeof(WorkItem) * B.items_cap, hipHostMallocMapped));
-    HIP_CHECK(hipHostMalloc((void**)&B.h_res, sizeof(WorkResult) * B.items_cap, hipHostMallocMapped));
+    B.h_items = (WorkItem*)halloc(sizeof(WorkItem) * B.items_cap);
+    B.h_res = (WorkResult*)halloc(sizeof(WorkResult) * B.items_cap);
     std::memset((void*)B.h_res, 0, sizeof(WorkResult) * B.items_cap);  // (pages may be recycled)
   }
   size_t in_off = 0, in_bytes = 0, out_off = 0;
@@ -4160,14 +4303,14 @@ static void grow_mapped(HipEngine* e, T** p, size_t* cap, size_t need, void (Hip
   if (need <= *cap) return;
   if (*p) (e->*retire)(*p);
   *cap = std::max(need, *cap * 2);
-  HIP_CHECK(hipHostMalloc((void**)p, sizeof(T) * *cap + 64, hipHostMallocMapped));
+  *p = (T*)e->halloc(sizeof(T) * *cap + 64);
   std::memset((void*)*p, 0, sizeof(T) * *cap + 64);  // (pinned pages may come back recycled)
 }
 static void grow_device(HipEngine* e, uint8_t** p, size_t* cap, size_t need, void (HipEngine::*retire)(void*)) {
   if (need <= *cap) return;
   if (*p) (e->*retire)(*p);
   *cap = std::max(need, *cap * 2);
-  HIP_CHECK(hipMalloc((void**)p, *cap + 64));
+  *p = (uint8_t*)e->dalloc(*cap + 64);
 }
 
 // Finalize items of a tick, staged in the lane's arenas for the fused launch.  Sessions whose
@@ -4368,10 +4511,17 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   m["remote_texts_hbm"] = (double)remote_dev_.load();        // spread owner: finals an RCCL round put in HBM
   m["remote_texts_staged"] = (double)remote_staged_.load();  // ... that came over the mesh
   m["remote_texts_copied"] = (double)remote_copied_.load();  // ... an RCCL round wrote, copied to the host (world > 1)
+  m["remote_texts_copied_inline"] = (double)remote_copied_inline_.load();
+  m["runtime_allocs"] = (double)allocs_.load();  // arena growths while serving
+  m["runtime_alloc_MB"] = 1e-6 * (double)alloc_bytes_.load();
+  m["runtime_alloc_us"] = alloc_us_.load();
+  m["runtime_alloc_max_us"] = alloc_max_us_.load();  // ... of them by the engine's caller (not the exchange)
   m["lanes"] = (double)lanes_.size();
   m["fin_separate_launches"] = 0.0;  // finalize no longer has a launch (or a wait) of its own
   if (grid_ && door_ == 0)  // the shared grid's counters, once per process
     for (auto& kv : grid_->stats()) m[kv.first] += kv.second;
+  if (!grid_ || door_ == 0)  // the process's HIP streams and queue limit, once per process
+    for (auto& kv : stream_stats()) m[kv.first] = kv.second;
   return m;
 }
 
@@ -4398,7 +4548,7 @@ HipGrid::HipGrid(int device, int doors, int wg_per_door, int idle_ms)
   const char* x = env_get("QMX_GRID_XCD");
   interleave_ = (x ? atoi(x) != 0 : true) && n_ % 8 == 0;
   HIP_CHECK(hipSetDevice(device_));
-  HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  stream_ = stream_create(StreamKind::Exclusive);  // the grid holds its queue: nothing may queue behind it
   HIP_CHECK(hipHostMalloc((void**)&h_doors_, sizeof(PDoor) * (size_t)n_, hipHostMallocMapped));
   std::memset((void*)h_doors_, 0, sizeof(PDoor) * (size_t)n_);
   HIP_CHECK(hipMalloc((void**)&d_ctls_, sizeof(PCtl) * (size_t)n_));
@@ -4415,7 +4565,7 @@ HipGrid::~HipGrid() {
   if (stream_) hipStreamSynchronize(stream_);
   if (h_doors_) hipHostFree(h_doors_);
   if (d_ctls_) hipFree(d_ctls_);
-  if (stream_) hipStreamDestroy(stream_);
+  stream_destroy(stream_, StreamKind::Exclusive);
 }
 
 PDoor* HipGrid::door(int d) const { return h_doors_ + d; }
@@ -4435,6 +4585,7 @@ void HipGrid::note_post() { last_post_.store(steady_s(), std::memory_order_relax
 // Each sub-grid starts from the last tick its door's relay saw: a tick posted to a grid that
 // left without relaying it (the host's heartbeat stopped) is picked up by the new launch.
 void HipGrid::launch_locked() {
+  const double t0 = steady_s();
   HIP_CHECK(hipSetDevice(device_));
   for (int d = 0; d < n_; ++d) h_doors_[d].base = __atomic_load_n(&h_doors_[d].relayed, __ATOMIC_ACQUIRE);
   const uint32_t idle_ticks = 2000u * 100000u;  // 2 s at 100 MHz: only a host that stopped beating
@@ -4444,10 +4595,16 @@ void HipGrid::launch_locked() {
   last_post_.store(steady_s(), std::memory_order_relaxed);
   running_.store(true, std::memory_order_release);
   ++launches_;
+  const double t1 = steady_s();
   // calibration reuses door 0's descriptor: never while a tick posted there is still unrelayed
   // (a revived grid or a relaunch after an idle exit picks that tick up from `base`; writing
   // the calibration tick over its descriptor would run an empty tick in its place)
   if (__atomic_load_n(&h_doors_[0].relayed, __ATOMIC_ACQUIRE) == h_doors_[0].posted) calibrate_locked();
+  // (every door's poster waits for this under the grid lock: its cost is io-loop stall time)
+  const double t2 = steady_s();
+  launch_us_max_ = std::max(launch_us_max_, 1e6 * (t1 - t0));
+  launch_cal_us_max_ = std::max(launch_cal_us_max_, 1e6 * (t2 - t1));
+  launch_us_sum_ += 1e6 * (t2 - t0);
 }
 
 // Clock calibration (timing only): empty ticks on door 0, each timed on the host from the
@@ -4511,6 +4668,7 @@ void HipGrid::stop_locked() {
   }
   running_.store(false, std::memory_order_release);
   ++stops_;
+  stop_us_max_ = std::max(stop_us_max_, 1e6 * (steady_s() - t0));
 }
 
 void HipGrid::stop() {
@@ -4555,7 +4713,10 @@ std::unordered_map<std::string, double> HipGrid::stats() {
   return {{"grid_launches", (double)launches_.load()}, {"grid_stops", (double)stops_.load()},
           {"grid_revivals", (double)revivals_.load()}, {"grid_doors", (double)n_},
           {"grid_clock_rtt_us", clk_rtt_us_.load(std::memory_order_relaxed)}, {"grid_xcd_local", interleave_ ? 1.0 : 0.0},
-          {"grid_wg_per_door", (double)wpd_}};
+          {"grid_wg_per_door", (double)wpd_},
+          // (written under the exclusive lock; a torn read of a double is harmless here)
+          {"grid_launch_us_max", launch_us_max_}, {"grid_launch_calibrate_us_max", launch_cal_us_max_},
+          {"grid_launch_us_sum", launch_us_sum_}, {"grid_stop_us_max", stop_us_max_}};
 }
 
 }  // namespace qmx

@@ -9,6 +9,9 @@
 #include <netinet/tcp.h>
 #include <signal.h>
 #include <sys/epoll.h>
+#include <sys/syscall.h>
+#include <dirent.h>
+#include <sys/resource.h>
 #include <sys/ioctl.h>
 #include <sys/eventfd.h>
 #include <sys/prctl.h>
@@ -62,7 +65,11 @@ std::atomic<uint64_t> c_fail_connect{0}, c_fail_timeout{0}, c_fail_status{0}, c_
 // before it applies the stream's final (X_BULK / X_FINAL carry the worker's count in b)
 std::atomic<uint64_t> c_sp_failed{0}, c_sp_aborted{0}, c_sp_empty{0}, c_sp_text{0}, c_sp_down{0},
     c_sp_delta_mismatch{0}, c_sp_nodata{0} /* worker: content but no delta sent */,
-    c_sp_eager{0} /* worker: final texts sent eagerly over the mesh (no round) */;
+    c_sp_eager{0} /* worker: final texts sent eagerly over the mesh (no round) */,
+    c_sp_release_deferred{0} /* owner: shadow slots released after the round writing them (X_RELEASE) */;
+// io loop passes (epoll return -> next wait) longer than 1 ms / 5 ms: anything that blocks a
+// loop (a synchronous device copy, a lock held by another thread) shows here
+std::atomic<uint64_t> c_loop_pass_1ms{0}, c_loop_pass_5ms{0};
 std::atomic<int> g_sp_logs{0};  // rate limit: the first 20 anomalies are logged with their state
 
 // Prometheus histogram with lock-free buckets (seconds)
@@ -940,6 +947,10 @@ class Loop {
   void attach_loops(const std::vector<Loop*>* ls) { loops_ = ls; }
   std::mutex smu_;
   std::unordered_map<std::string, double> snap_;  // engine stats snapshot (read by /metrics on any loop)
+  std::atomic<double> pass_max_{0.0};  // this loop's longest pass over 1 ms (/metrics)
+  // QMX_LOOP_STALL_LOG watchdog: the running pass's start (0: waiting in epoll) and the thread
+  std::atomic<double> pass_t0_{0.0};
+  std::atomic<int> tid_{0};
   // syscalls issued by this loop's thread (single writer; /metrics reads them from any loop)
   enum { SC_CLIENT_SEND, SC_UP_SEND, SC_RECV, SC_EPOLL_WAIT, SC_EPOLL_CTL, SC_WAKE_READ, SC_N };
   std::atomic<uint64_t> sc_[SC_N] = {};
@@ -974,6 +985,7 @@ class Loop {
   void run() {
     prof_thread();
     crash_thread();
+    tid_.store((int)syscall(SYS_gettid));
     setup();
     if (++g_ready == cfg_.threads && !cfg_.ready_file.empty()) {
       FILE* f = fopen(cfg_.ready_file.c_str(), "w");  // supervisor: this generation is serving
@@ -1021,6 +1033,10 @@ class Loop {
         n = epoll_wait(ep_, evs.data(), (int)evs.size(), to);
       }
       tnow_ = now_s();  // this iteration's clock (lnow): stamps and timeouts, not hop timing
+      if (stall_log_) pass_t0_.store(tnow_, std::memory_order_relaxed);
+      double ph[7] = {0, 0, 0, 0, 0, 0, 0};  // QMX_LOOP_STALL_LOG: phase ends of this pass
+      rusage ru0{};
+      if (stall_log_) getrusage(RUSAGE_THREAD, &ru0);
       if (lazy_wake_ && hub_) {
         in_wait_.store(false, std::memory_order_seq_cst);
         if (rq_pending_.load(std::memory_order_acquire)) on_results(false);
@@ -1031,12 +1047,26 @@ class Loop {
       // is busy most of the time, and a tick's results waiting out a whole event batch were
       // most of its done -> taken time (tick_hops_us_avg)
       if (jobs_live_ && any_ready()) loop_tick();
+      if (stall_log_) ph[0] = now_s();
+      double ev_max = 0;
+      int ev_kind = -1;
       for (int i = 0; i < n; ++i) {
-        dispatch(evs[i]);
+        if (stall_log_) {
+          const double e0 = now_s();
+          dispatch(evs[i]);
+          const double de = now_s() - e0;
+          if (de > ev_max) {
+            ev_max = de;
+            ev_kind = (int)(evs[i].data.u64 >> 32);
+          }
+        } else {
+          dispatch(evs[i]);
+        }
         // a long batch: tick results that arrived meanwhile are applied now, not after it
         if ((i & 7) == 7 && early_flush_ && rq_pending_.load(std::memory_order_acquire)) on_results(false);
         if ((i + 1) % check_every_ == 0 && jobs_live_ && any_ready()) loop_tick();
       }
+      if (stall_log_) ph[1] = now_s();
       if (g_drain.load() && drain_step()) break;
       if ((hub_ || aeng_) && early_flush_) {
         // upstream bytes to the tick lanes and finished responses to their clients before
@@ -1050,6 +1080,7 @@ class Loop {
         }
         if (!flushq_.empty()) flush_queued();
       }
+      if (stall_log_) ph[2] = now_s();
       if (!pending_requests_.empty()) {
         std::vector<int>& fds = scratch_fds_;  // swapped each iteration: both buffers keep their capacity
         fds.clear();
@@ -1061,6 +1092,7 @@ class Loop {
         }
       }
       double t = now_s();
+      if (stall_log_) ph[3] = t;
       if (t - last_sweep > 0.1) {
         sweep_timeouts(t);
         last_sweep = t;
@@ -1079,6 +1111,7 @@ class Loop {
           }
         }
       }
+      if (stall_log_) ph[4] = now_s();
       flush_ops();
       if (aeng_) {
         loop_tick();
@@ -1092,10 +1125,43 @@ class Loop {
         kick_ = false;
         hub_->kick();
       }
+      if (stall_log_) ph[5] = now_s();
       if (!deferq_.empty()) release_deferred(now_s());
       if (!flushq_.empty()) flush_queued();
       if (!pending_close_.empty()) reap_clients();
       flush_x();
+      const double pass = now_s() - tnow_;
+      if (stall_log_) pass_t0_.store(0.0, std::memory_order_relaxed);
+      if (pass > 1e-3) {
+        c_loop_pass_1ms++;
+        if (pass > 5e-3) c_loop_pass_5ms++;
+        if (pass > pass_max_.load(std::memory_order_relaxed)) pass_max_.store(pass, std::memory_order_relaxed);
+        if (stall_log_ && pass > 5e-3 && stall_logs_++ < 50) {
+          // on the CPU or blocked: this thread's CPU time, context switches (voluntary: it
+          // slept on something; involuntary: preempted) and page faults over the pass
+          rusage ru1{};
+          getrusage(RUSAGE_THREAD, &ru1);
+          auto tv = [](const timeval& t) { return 1e3 * t.tv_sec + 1e-3 * t.tv_usec; };
+          fprintf(stderr, "qmx loop %d: stalled pass: cpu %.2f ms (user %.2f), vcsw %ld, ivcsw %ld, minflt %ld, majflt %ld\n",
+                  idx_, tv(ru1.ru_utime) + tv(ru1.ru_stime) - tv(ru0.ru_utime) - tv(ru0.ru_stime),
+                  tv(ru1.ru_utime) - tv(ru0.ru_utime), ru1.ru_nvcsw - ru0.ru_nvcsw, ru1.ru_nivcsw - ru0.ru_nivcsw,
+                  ru1.ru_minflt - ru0.ru_minflt, ru1.ru_majflt - ru0.ru_majflt);
+          ph[6] = tnow_ + pass;
+          double prev = tnow_, d[7];
+          for (int k = 0; k < 7; ++k) {
+            d[k] = ph[k] > 0 ? 1e3 * (ph[k] - prev) : 0.0;
+            if (ph[k] > 0) prev = ph[k];
+          }
+          fprintf(stderr, "qmx loop %d: %.2f ms pass (%d events): results %.2f, events %.2f, early flush %.2f, "
+                  "requests %.2f, sweep %.2f, flush+tick %.2f, output %.2f ms; engine allocs %.0f (%.0f us); "
+                  "grid launches %.0f stops %.0f; slowest event kind %d (%.2f ms)\n", idx_,
+                  1e3 * pass, n, d[0], d[1], d[2], d[3], d[4], d[5], d[6],
+                  heng_ ? heng_->kernel_stats()["runtime_allocs"] : 0.0,
+                  heng_ ? heng_->kernel_stats()["runtime_alloc_us"] : 0.0,
+                  grid_ ? grid_->stats()["grid_launches"] : 0.0, grid_ ? grid_->stats()["grid_stops"] : 0.0, ev_kind,
+                  1e3 * ev_max);
+        }
+      }
     }
     // ticks still on the GPU complete before the engine (and its arenas) can go
     for (int w = 0; jobs_live_ && w < 200000; ++w) {
@@ -2344,7 +2410,7 @@ class Loop {
     s->bs.resize(valid.size());
     // spread placement (EP analog): backend i of a session owned by rank r runs on rank
     // (r + i) % world; its deltas and final text come back through the exchange (R1)
-    const bool spread = xch_ && xch_->healthy() && xch_->world() > 1;
+    const bool spread = xch_ && xch_->healthy() && (xch_->world() > 1 || self_spread_);
     if (spread) {
       s->skey = ((uint64_t)xch_->rank() << 56) | ((uint64_t)idx_ << 48) | next_skey_++;
       rsess_[s->skey] = s;
@@ -2352,7 +2418,9 @@ class Loop {
     for (size_t i = 0; i < valid.size(); ++i) {
       s->bs[i].backend = valid[i];
       const int target = spread ? (xch_->rank() + (int)i) % xch_->world() : -1;
-      if (spread && target != xch_->rank() && xch_->peer_up(target)) {
+      // (self spread: every odd backend of a one-rank deployment goes through its own
+      // exchange — opens, deltas and RCCL rounds to itself)
+      if (spread && (target != xch_->rank() || (self_spread_ && (i & 1))) && xch_->peer_up(target)) {
         s->bs[i].remote = target;
         s->bs[i].via_link = link_up(target);  // the whole stream keeps one path (message order)
         s->remote_n++;
@@ -2656,6 +2724,10 @@ class Loop {
   void handle_x(std::vector<XMsg>& in, bool link) {
     for (auto& m : in) {
       if (m.type == X_UP) continue;  // a peer (re)joined: new sessions may place streams there
+      if (m.type == X_RELEASE) {  // a deferred shadow-slot release: its round is over
+        if (m.a >= 0) e_release(m.a);
+        continue;
+      }
       if (m.type == X_LINK) {
         on_link_msg(m);
         continue;
@@ -2777,7 +2849,8 @@ class Loop {
     // over the mesh the bytes are in the payload; an RCCL round already wrote them to HBM
     // (a final text is never empty: an empty one travels as X_FINAL)
     const bool bytes = !m.payload.empty();
-    eng().set_remote_content(b.slot, bytes ? &m.payload : nullptr, bytes ? m.payload.size() : (size_t)m.a);
+    eng().set_remote_content(b.slot, bytes ? &m.payload : nullptr, bytes ? m.payload.size() : (size_t)m.a,
+                             (m.flags & XF_HOSTCOPY) != 0);
     xch_->forget_bulk(s->skey, bi);
     b.state = 1;
     b.aborted = false;
@@ -3175,12 +3248,14 @@ class Loop {
         drop_up(b.up, false);
         b.up = nullptr;
       }
-      // a shadow slot: no RCCL round may write into it once released (forget_bulk waits
-      // for a round receiving into it; a round stuck past twice its timeout: the slot leaks)
-      const bool reusable = !(b.remote >= 0 && xch_ && s->skey) || xch_->forget_bulk(s->skey, i);
+      // a shadow slot: no RCCL round may write into it once released.  A round receiving
+      // into it right now keeps it: the exchange hands it back with X_RELEASE when that round
+      // is over (never a wait here: a round stuck on a failed peer lasts up to its timeout)
+      const bool reusable = !(b.remote >= 0 && xch_ && s->skey) || xch_->forget_bulk(s->skey, i, b.slot, idx_);
       if (b.slot >= 0) {
         slot_owner_.erase(b.slot);
         if (reusable) e_release(b.slot);
+        else c_sp_release_deferred++;
         b.slot = -1;
       }
     }
@@ -3229,6 +3304,14 @@ class Loop {
     put("qmx_spread_delta_mismatch_total", (double)c_sp_delta_mismatch.load());
     put("qmx_spread_worker_nodata_total", (double)c_sp_nodata.load());
     put("qmx_spread_eager_finals_total", (double)c_sp_eager.load());
+    put("qmx_spread_release_deferred_total", (double)c_sp_release_deferred.load());
+    put("qmx_loop_passes_over_1ms_total", (double)c_loop_pass_1ms.load());
+    put("qmx_loop_passes_over_5ms_total", (double)c_loop_pass_5ms.load());
+    {
+      double mx = 0;
+      for (Loop* l : *loops_) mx = std::max(mx, l->pass_max_.load(std::memory_order_relaxed));
+      put("qmx_loop_pass_max_seconds", mx);
+    }
     m += "qmx_upstream_failures_by_class_total{class=\"connect\"} " + std::to_string(c_fail_connect.load()) + "\n";
     m += "qmx_upstream_failures_by_class_total{class=\"timeout\"} " + std::to_string(c_fail_timeout.load()) + "\n";
     m += "qmx_upstream_failures_by_class_total{class=\"http_status\"} " + std::to_string(c_fail_status.load()) + "\n";
@@ -3259,6 +3342,8 @@ class Loop {
       put("qmx_exchange_busy_us_total", xch_->busy_us());
       put("qmx_exchange_healthy", xch_->healthy() ? 1.0 : 0.0);
       put("qmx_exchange_rccl_active", xch_->rccl_active() ? 1.0 : 0.0);
+      put("qmx_exchange_host_copied_total", (double)xch_->host_copied());  // texts copied HBM -> host by the bulk thread
+      put("qmx_exchange_deferred_releases_total", (double)xch_->deferred_releases());
       int up = 0;
       for (int r = 0; r < xch_->world(); ++r) up += xch_->peer_up(r);
       put("qmx_exchange_peers_up", (double)up);
@@ -3391,6 +3476,13 @@ class Loop {
   }();
   std::vector<EngineOp> ops_;  // engine feed / finish / release of this iteration (flush_ops)
   const bool early_flush_ = env_flag("QMX_EARLY_FLUSH", true);  // A/B knob
+  // QMX_SPREAD_SELF=1 with placement spread at world 1 (rehearsal / GPU test): the odd
+  // backends of every session run through this rank's own exchange, as if on a peer rank —
+  // mesh frames to itself, worker sessions on this loop, final texts in RCCL rounds to itself
+  // (the world > 1 path, HBM sinks and host copies included, on one GPU)
+  const bool self_spread_ = env_flag("QMX_SPREAD_SELF", false);
+  const bool stall_log_ = env_flag("QMX_LOOP_STALL_LOG", false);  // passes over 5 ms: phase split on stderr
+  int stall_logs_ = 0;
   const bool lazy_wake_ = env_flag("QMX_LAZY_WAKE", false);   // A/B knob (see attach_hub)
   std::atomic<bool> in_wait_{false};                          // in epoll_wait (lazy wake)
   double ops_t0_ = 0;  // the oldest unflushed FEED op (flush-wait timing)
@@ -3412,6 +3504,33 @@ void on_signal(int sig) {
 }
 
 }  // namespace
+
+// The kernel grows a process's file-descriptor table by doubling it when a new fd does not
+// fit, and in a multi-threaded process the growth waits for an RCU grace period
+// (expand_files -> synchronize_rcu) while every other thread that allocates an fd waits for
+// the resize.  Measured on the MI355X box (QMX_LOOP_STALL_LOG watchdog, /proc/<tid>/wchan):
+// all 8 io loops parked in expand_files inside socket()/accept4() for 70-200 ms at a time as
+// client and upstream connections grew the table — and the grid, with nothing posted for
+// 50 ms, idled out meanwhile.  Growing the table once here, before any io loop runs, to the
+// fd limit (at most 2^17 entries, ~1 MiB) leaves nothing to grow while serving.
+// The soft fd limit is raised to the hard one first (capped the same way): a proxy holds a
+// client socket, its upstream sockets and keep-alive pools, and 1024 is a common default.
+static void presize_fd_table() {
+  rlimit rl{};
+  if (getrlimit(RLIMIT_NOFILE, &rl) != 0) return;
+  if (rl.rlim_cur < rl.rlim_max && rl.rlim_cur < ((rlim_t)1 << 17)) {
+    rlimit up = rl;
+    up.rlim_cur = std::min<rlim_t>(rl.rlim_max, (rlim_t)1 << 17);
+    if (setrlimit(RLIMIT_NOFILE, &up) == 0) rl = up;
+  }
+  const long want = (long)std::min<rlim_t>(rl.rlim_cur, (rlim_t)1 << 17);
+  if (want <= 1024) return;
+  const int fd = open("/dev/null", O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return;
+  const int hi = dup3(fd, (int)want - 1, O_CLOEXEC);  // the table now covers [0, want)
+  if (hi >= 0) close(hi);
+  close(fd);
+}
 
 int run_server(const ServerCfg& cfg0) {
   env_refresh();  // before any thread: the io loops, lanes and exchange read this snapshot
@@ -3441,6 +3560,7 @@ int run_server(const ServerCfg& cfg0) {
     SSL_CTX_set_mode(tls, SSL_MODE_ENABLE_PARTIAL_WRITE | SSL_MODE_ACCEPT_MOVING_WRITE_BUFFER);
   }
   signal(SIGPIPE, SIG_IGN);
+  presize_fd_table();
   if (cfg.install_signals) {
     struct sigaction sa {};
     sa.sa_handler = on_signal;
@@ -3491,7 +3611,8 @@ int run_server(const ServerCfg& cfg0) {
   }
   if (hub) hub->start();
   std::unique_ptr<Exchange> xch;
-  if (cfg.world > 1 && cfg.placement == "spread") {
+  const bool self_spread = cfg.world == 1 && cfg.placement == "spread" && env_flag("QMX_SPREAD_SELF", false);
+  if ((cfg.world > 1 || self_spread) && cfg.placement == "spread") {
     XOptions o;
     o.rank = cfg.rank;
     o.world = cfg.world;
@@ -3503,12 +3624,62 @@ int run_server(const ServerCfg& cfg0) {
     o.batch_us = cfg.xchg_round_us;
     o.timeout_s = cfg.xchg_timeout;
     o.max_text = (size_t)cfg.content_cap;
+    // RCCL texts a persistent grid must not read from HBM (a peer GPU wrote them): copied out
+    // by the bulk thread after their round, never by an io loop
+    o.host_copy = hip && o.transport == "rccl" && !remote_hbm_direct(cfg);
     // per-loop links (0: every session message via the mesh thread)
     o.links = cfg.xchg_links >= 0 ? cfg.xchg_links != 0 : env_flag("QMX_XCHG_LINKS", true);
     std::vector<Loop*> lp;
     for (auto& l : loops) lp.push_back(l.get());
     xch.reset(new Exchange(o, (int)lp.size(), [lp](int l, std::vector<XMsg>&& v) { lp[l]->x_deliver(std::move(v)); }));
     for (auto& l : loops) l->attach_exchange(xch.get());
+  }
+  // QMX_LOOP_STALL_LOG: a watchdog samples, for an io loop stuck in one pass for over 20 ms,
+  // what the kernel has that thread (and every other thread of the process) waiting in:
+  // /proc/self/task/<tid>/wchan and .../syscall — the blocking call and the lock behind it
+  std::thread watchdog;
+  std::atomic<bool> wd_stop{false};
+  if (env_flag("QMX_LOOP_STALL_LOG", false)) {
+    watchdog = std::thread([&loops, &wd_stop] {
+      auto slurp = [](const std::string& path) {
+        std::string out;
+        if (FILE* f = fopen(path.c_str(), "r")) {
+          char b[512];
+          size_t n = fread(b, 1, sizeof(b) - 1, f);
+          fclose(f);
+          out.assign(b, n);
+          while (!out.empty() && (out.back() == '\n' || out.back() == ' ')) out.pop_back();
+        }
+        return out;
+      };
+      int dumps = 0;
+      std::vector<double> seen(loops.size(), 0.0);
+      while (!wd_stop.load() && dumps < 20) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(5));
+        const double t = now_s();
+        for (size_t i = 0; i < loops.size(); ++i) {
+          const double t0 = loops[i]->pass_t0_.load(std::memory_order_relaxed);
+          if (t0 <= 0 || t - t0 < 0.02 || seen[i] == t0) continue;
+          seen[i] = t0;
+          ++dumps;
+          std::string msg = "qmx watchdog: loop " + std::to_string(i) + " in one pass for " +
+                            std::to_string((int)(1e3 * (t - t0))) + " ms; threads (tid comm wchan | syscall):";
+          if (DIR* d = opendir("/proc/self/task")) {
+            while (dirent* e = readdir(d)) {
+              if (e->d_name[0] == '.') continue;
+              const std::string base = std::string("/proc/self/task/") + e->d_name;
+              const std::string w = slurp(base + "/wchan");
+              if (w.empty() || w == "0") continue;  // running
+              const std::string sc = slurp(base + "/syscall");
+              msg += "\n   " + std::string(e->d_name) + " " + slurp(base + "/comm") + " " + w + " | " + sc.substr(0, 60);
+            }
+            closedir(d);
+          }
+          fprintf(stderr, "%s\n", msg.c_str());
+          break;
+        }
+      }
+    });
   }
   for (auto& l : loops) {
     Loop* lp = l.get();
@@ -3522,6 +3693,8 @@ int run_server(const ServerCfg& cfg0) {
     });
   }
   for (auto& t : ts) t.join();
+  wd_stop.store(true);
+  if (watchdog.joinable()) watchdog.join();
   prof_stop();
   if (xch) {
     xch->request_stop();  // keeps taking part in rounds until every rank has stopped

@@ -39,13 +39,15 @@ THINK = [sse_chunk({"role": "assistant"}), sse_chunk({"content": "<think>"}), ss
 
 @contextlib.contextmanager
 def native_cluster(cfg, world: int, placement: str = "spread", xchg: str = "tcp", eager=None, tick_mode=None,
-                   links=None, engine: str = "cpu"):
+                   links=None, engine: str = "cpu", run_env=None):
     """`world` native ranks in-process (threads), TCP exchange on a free port block.
     ``xchg="tcpbulk"``: final texts move in rank-0-numbered bulk rounds (the RCCL round
     protocol with a socket executor) instead of riding the mesh.  ``eager``: the largest final
     text that rides the mesh behind its deltas instead (None: the default; 0: none).
     ``tick_mode="loops"``: every rank's io loops drive their own engine asynchronously (the
-    loop-tick protocol, AsyncCpuEngine on the CPU) while remote streams come and go."""
+    loop-tick protocol, AsyncCpuEngine on the CPU) while remote streams come and go.
+    ``run_env``: environment set while the servers start (they snapshot it then) and restored
+    after they stopped."""
     from quorum_amd.runtime.native_server import native_config
 
     ext = native.require()
@@ -62,6 +64,7 @@ def native_cluster(cfg, world: int, placement: str = "spread", xchg: str = "tcp"
                "QMX_XCHG_ROUND_US": "100"}
         if eager is not None:
             env["QMX_XCHG_EAGER_BYTES"] = str(eager)
+        env.update(run_env or {})
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
         try:
@@ -78,6 +81,8 @@ def native_cluster(cfg, world: int, placement: str = "spread", xchg: str = "tcp"
         if tick_mode is not None:
             d["tick_mode"] = tick_mode
         cfgs.append(d)
+    saved = {k: os.environ.get(k) for k in (run_env or {})}
+    os.environ.update(run_env or {})
     for d in cfgs:
         th = threading.Thread(target=ext.run_server, args=(d,), daemon=True)
         th.start()
@@ -105,6 +110,11 @@ def native_cluster(cfg, world: int, placement: str = "spread", xchg: str = "tcp"
         ext.stop_server()
         for th in threads:
             th.join(timeout=15)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 def _metric(text, name):
@@ -225,6 +235,95 @@ def test_spread_matches_local(name, world, xchg, eager, links):
                 assert (total("qmx_exchange_rounds_total") > 0) == (texts > 0)
             else:
                 assert total("qmx_exchange_mesh_finals_total") == texts
+    finally:
+        live.close()
+
+
+@pytest.mark.parametrize("xchg,eager", [("tcp", None), ("tcp", 0), ("tcpbulk", 0)])
+@pytest.mark.parametrize("name", ["concat_think", "aggregate_4", "concat_null_abort"])
+def test_self_spread_matches_local(name, xchg, eager):
+    """QMX_SPREAD_SELF at world 1: every odd backend runs through the rank's own exchange (mesh
+    frames to itself, a worker session on the same loop, final texts eager / over the mesh /
+    in bulk rounds to itself) — the multi-rank path on one rank, as the GPU test runs it with
+    RCCL.  Responses equal the local server's, and the odd streams really went remote."""
+    n, block, strategy, behs = SPREAD_CASES[name]
+    live, ports = _live({f"b{i + 1}": b for i, b in enumerate(behs)})
+    try:
+        cfg = _cfg(n, block, strategy, [f"http://127.0.0.1:{ports[f'b{i + 1}']}/v1" for i in range(n)])
+        req = {"messages": MSG, "stream": True}
+        with native_server(cfg) as p:
+            ref = httpx.post(f"http://127.0.0.1:{p}/chat/completions", json=req, headers=AUTH, timeout=30)
+        with native_cluster(cfg, 1, xchg=xchg, eager=eager, run_env={"QMX_SPREAD_SELF": "1"}) as cports:
+            m0 = httpx.get(f"http://127.0.0.1:{cports[0]}/metrics").text
+            for _ in range(3):
+                r = httpx.post(f"http://127.0.0.1:{cports[0]}/chat/completions", json=req, headers=AUTH, timeout=30)
+                assert r.status_code == ref.status_code
+                assert _split(_events(r.text)) == _split(_events(ref.text)), name
+            m = httpx.get(f"http://127.0.0.1:{cports[0]}/metrics").text
+
+        def d(k):
+            return _metric(m, k) - _metric(m0, k)
+        assert d("qmx_remote_streams_total") == 3 * (n // 2), m
+        assert _metric(m, "qmx_spread_delta_mismatch_total") == 0
+        texts = d("qmx_spread_remote_ends_total{how=\"text\"}")
+        if xchg == "tcpbulk":
+            assert d("qmx_exchange_rounds_total") > 0 or texts == 0
+            assert d("qmx_exchange_mesh_finals_total") == 0
+    finally:
+        live.close()
+
+
+def test_session_end_during_stalled_round_does_not_block_its_loop():
+    """Advisor finding (round 5): forget_bulk() made the io loop wait, up to twice the round
+    timeout, for a round still receiving into a leaving session's shadow slot — every other
+    connection on that loop froze meanwhile.  Now the release is deferred: the slot stays
+    pinned, the loop goes on, and the exchange hands the slot back (X_RELEASE) when the round
+    is over.  One io loop, self spread (backend 2 of every session through the rank's own
+    exchange), bulk round 1 stalled for its 3 s timeout (QMX_XCHG_FAULT_STALL_ROUND=1): client
+    A leaves while its final text is in that round; client B, on the same loop, must get its
+    first delta at once, and every slot must come back."""
+    import socket
+
+    behs = [("stream", 200, THINK), ("stream", 200, sse_stream(["x", "y", "z"]))]
+    live, ports = _live({"b1": behs[0], "b2": behs[1]})
+    try:
+        cfg = _cfg(2, dict(CONCAT, skip_final_aggregation=False), "concatenate",
+                   [f"http://127.0.0.1:{ports['b1']}/v1", f"http://127.0.0.1:{ports['b2']}/v1"])
+        env = {"QMX_SPREAD_SELF": "1", "QMX_XCHG_FAULT_STALL_ROUND": "1", "QMX_XCHG_TIMEOUT": "3"}
+        with native_cluster(cfg, 1, xchg="tcpbulk", eager=0, run_env=env) as cports:
+            base = f"http://127.0.0.1:{cports[0]}"
+            m0 = httpx.get(base + "/metrics").text
+            body = json.dumps({"messages": MSG, "stream": True}).encode()
+            a = socket.create_connection(("127.0.0.1", cports[0]))
+            a.sendall(b"POST /chat/completions HTTP/1.1\r\nHost: x\r\nAuthorization: Bearer test-key\r\n"
+                      b"Content-Type: application/json\r\nContent-Length: " + str(len(body)).encode() +
+                      b"\r\n\r\n" + body)
+            got = b""
+            t0 = time.time()
+            while b'"content": "x"' not in got and time.time() - t0 < 5:  # backend 2's deltas came back
+                got += a.recv(65536)
+            time.sleep(0.3)  # its final text is announced and sits in the stalled round 1
+            a.close()
+            time.sleep(0.2)
+            t1 = time.time()
+            assert httpx.get(base + "/health", timeout=2).status_code == 200
+            first = None
+            with httpx.Client(base_url=base) as c:
+                with c.stream("POST", "/chat/completions", json={"messages": MSG, "stream": True}, headers=AUTH,
+                              timeout=30) as r:
+                    for chunk in r.iter_text():
+                        if first is None and '"content"' in chunk:
+                            first = time.time() - t1
+            assert first is not None and first < 1.0, first  # the loop was not held by A's round
+            t2 = time.time()
+            while time.time() - t2 < 10:
+                m = httpx.get(base + "/metrics").text
+                if _metric(m, "qmx_engine_free") >= _metric(m0, "qmx_engine_free"):
+                    break
+                time.sleep(0.1)
+        assert _metric(m, "qmx_spread_release_deferred_total") - _metric(m0, "qmx_spread_release_deferred_total") >= 1, m
+        assert _metric(m, "qmx_exchange_deferred_releases_total") >= 1
+        assert _metric(m, "qmx_engine_free") >= _metric(m0, "qmx_engine_free"), "a shadow slot was never released"
     finally:
         live.close()
 
