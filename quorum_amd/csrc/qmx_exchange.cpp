@@ -298,15 +298,50 @@ struct Exchange::Impl {
   // loop l (X_LINK), which owns it from then on.  On a helper thread: a blocking connect to an
   // unresponsive peer (up to 1 s per loop) must not stall the mesh thread's heartbeats,
   // reports and session frames for every other peer.
+  //
+  // A peer whose mesh connection flaps re-dials its links while an earlier dialer may still be
+  // connecting.  Every dial of peer r has a generation (this process's start time in ns plus a
+  // counter: a restarted process's are larger), sent in each link's hello (skey):
+  //  * here, a dialer that is no longer the newest for r hands no more links and stops;
+  //  * the accepting side keeps, per (peer, loop), the link of the newest generation it has
+  //    seen and closes an older one arriving late — so both ends keep the same socket.
+  // Finished dialers are joined at the next dial (at most one running per peer that matters).
+  struct Dialer {
+    std::thread th;
+    std::shared_ptr<std::atomic<bool>> done;
+  };
   std::mutex dmu;
-  std::vector<std::thread> dialers;  // joined by Exchange::join()
+  std::vector<Dialer> dialers;       // joined by Exchange::join()
+  std::map<int, uint64_t> dial_gen;  // peer -> newest dial generation (under dmu)
+  const uint64_t gen_base = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                std::chrono::system_clock::now().time_since_epoch()).count();
+  uint64_t gen_next = 0;
   void dial_links(int r) {
     if (!X->o_.links || X->o_.rank <= r) return;
     std::lock_guard<std::mutex> g(dmu);
-    dialers.emplace_back([this, r] { dial_links_now(r); });
+    for (auto it = dialers.begin(); it != dialers.end();) {  // reap finished dialers
+      if (it->done->load()) {
+        it->th.join();
+        it = dialers.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    const uint64_t gen = gen_base + ++gen_next;
+    dial_gen[r] = gen;
+    auto done = std::make_shared<std::atomic<bool>>(false);
+    dialers.push_back(Dialer{std::thread([this, r, gen, done] {
+                               dial_links_now(r, gen);
+                               done->store(true);
+                             }),
+                             done});
   }
-  void dial_links_now(int r) {
-    for (int l = 0; l < X->nloops_ && !X->stop_.load(); ++l) {
+  bool dial_current(int r, uint64_t gen) {
+    std::lock_guard<std::mutex> g(dmu);
+    return dial_gen[r] == gen;
+  }
+  void dial_links_now(int r, uint64_t gen) {
+    for (int l = 0; l < X->nloops_ && !X->stop_.load() && dial_current(r, gen); ++l) {
       int fd = socket(AF_INET, SOCK_STREAM, 0);
       if (fd < 0) return;
       timeval tv{1, 0};
@@ -319,6 +354,7 @@ struct Exchange::Impl {
       h.type = F_HELLO;
       h.a = X->o_.rank;
       h.b = l + 1;  // b > 0: a link of loop b - 1 (0: the mesh connection)
+      h.skey = gen;
       const std::string f = frame(h);
       if (connect(fd, (sockaddr*)&a, sizeof(a)) != 0 || send(fd, f.data(), f.size(), MSG_NOSIGNAL) != (ssize_t)f.size()) {
         close(fd);
@@ -326,7 +362,16 @@ struct Exchange::Impl {
       }
       set_nodelay(fd);
       fcntl(fd, F_SETFL, fcntl(fd, F_GETFL) | O_NONBLOCK);
-      hand_link(l, r, fd, std::string());
+      {
+        // handed only while this dial is the newest for r (a newer one replaces this loop's
+        // link on both ends: the acceptor keeps the higher generation)
+        std::lock_guard<std::mutex> g(dmu);
+        if (dial_gen[r] != gen) {
+          close(fd);
+          return;
+        }
+        hand_link(l, r, fd, std::string());
+      }
     }
   }
   void hand_link(int l, int r, int fd, std::string&& early) {
@@ -844,13 +889,13 @@ void Exchange::request_stop() {
 void Exchange::join() {
   if (mesh_th_.joinable()) mesh_th_.join();
   if (bulk_th_.joinable()) bulk_th_.join();
-  std::vector<std::thread> ds;
+  std::vector<Impl::Dialer> ds;
   {
     std::lock_guard<std::mutex> g(im_->dmu);
     ds.swap(im_->dialers);
   }
-  for (auto& t : ds)
-    if (t.joinable()) t.join();
+  for (auto& d : ds)
+    if (d.th.joinable()) d.th.join();
 }
 
 // ------------------------------------------------------------------ the mesh thread
@@ -868,6 +913,7 @@ void Exchange::mesh_loop() {
   for (int r = 0; r < o_.world; ++r) I.peers[r].next_dial = 0;
   std::vector<epoll_event> evs(64);
   std::vector<int> pending;  // accepted sockets waiting for their hello
+  std::map<std::pair<int, int>, uint64_t> link_gen;  // (peer, loop) -> newest link generation accepted
   std::map<int, std::string> pend_in;
   char buf[65536];
   while (!stop_.load()) {
@@ -930,10 +976,12 @@ void Exchange::mesh_loop() {
             std::string early = in.substr(sizeof(WireHdr) + h.len);
             pend_in.erase(fd);
             pending.erase(std::remove(pending.begin(), pending.end(), fd), pending.end());
-            if (!o_.links || h.b - 1 >= nloops_) {
-              close(fd);
+            uint64_t& newest = link_gen[{pr, h.b - 1}];
+            if (!o_.links || h.b - 1 >= nloops_ || h.skey < newest) {
+              close(fd);  // (an older dial's link arriving after a newer one: the dialer dropped it)
               continue;
             }
+            newest = h.skey;
             I.hand_link(h.b - 1, pr, fd, std::move(early));
             continue;
           } else {

@@ -174,6 +174,7 @@ class HipGrid {
   void calibrate_locked();
   std::atomic<double> clk_off_us_{__builtin_nan("")};
   bool interleave_ = true;  // doors' sub-grids XCD-local (blocks d, d + doors, ...)
+  int occ_ = 1;             // workgroups per CU the kernel variant allows (QMX_GRID_OCC)
   // written by calibrate_locked (exclusive lock); read lock-free by housekeep() / stats()
   std::atomic<double> clk_rtt_us_{0.0}, last_cal_{0.0};
   int device_, n_, wpd_, idle_ms_;

@@ -2888,8 +2888,14 @@ static_assert(offsetof(PDoor, beat) == offsetof(PDoor, posted) + 4, "posted + be
 // `door` / `ctl` are neither const nor __restrict__ and their words are read with atomic
 // loads: a readonly noalias kernel argument may be read through the scalar cache, which no
 // acquire fence invalidates — the next tick's descriptor would come back stale.
-__global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* doors, PCtl* ctls, int wpd, uint32_t gen,
-                                                          uint32_t idle_ticks, int interleave) {
+//
+// WPE: waves per SIMD the register allocation must allow.  2 (the default): one 512-thread
+// workgroup per CU (8 waves on 4 SIMDs), up to 256 VGPRs.  4: two workgroups per CU — at most
+// 128 VGPRs (some live values go to scratch) and 2 x 79 KB of the CU's 160 KB LDS; the grid
+// then counts its budget in workgroup slots (HipGrid, QMX_GRID_OCC=2).
+template <int WPE>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void qmx_tick_persistent(
+    PDoor* doors, PCtl* ctls, int wpd, uint32_t gen, uint32_t idle_ticks, int interleave) {
   __shared__ TickLds U;
   __shared__ TickDesc D;
   __shared__ uint32_t cmd;  // new tick's sequence number, 0: exit
@@ -3029,12 +3035,15 @@ __global__ __launch_bounds__(BS) void qmx_tick_persistent(PDoor* doors, PCtl* ct
     // items are claimed from the tick's counter, not dealt by workgroup index: a workgroup
     // that is not resident (the CUs are shared with other grids / kernels) holds up nothing.
     // The relay runs item 0 without a claim (it reset the counter to 1 before publishing).
-    // A worker's first item was claimed with the descriptor read (pre_k).
+    // A worker's first item was claimed with the descriptor read (pre_k).  Every claim of the
+    // tick — that first one, the relay's reset and the loop below — uses the counter of the
+    // relayed command c, never the descriptor's seq: one index, whatever the host numbers
+    // (the host posts D.seq == c today; a claim on another counter would skip or repeat items)
     bool first = true;
     for (;;) {
       if (tid == 0)
         cmd = first ? (relay ? 0u : pre_k)
-                    : __hip_atomic_fetch_add(&ctl->next[seq & 3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    : __hip_atomic_fetch_add(&ctl->next[c & 3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       first = false;
       __syncthreads();
       const int k = (int)cmd;
@@ -3101,7 +3110,9 @@ void stream_destroy(hipStream_t s, StreamKind kind) {
 }
 
 __global__ void qmx_touch(uint32_t* mark) {
-  if (threadIdx.x == 0) __hip_atomic_store(mark, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  // (relaxed: the mark carries no data to order — and a release store is emitted as an L2
+  // write-back the store does not wait for, which tests/test_isa.py rejects anywhere)
+  if (threadIdx.x == 0) __hip_atomic_store(mark, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 std::unordered_map<std::string, double> stream_probe(int n, double wait_ms) {
@@ -3242,7 +3253,7 @@ void HipEngine::wait_results(TickLane& L, int n, int m, uint32_t seq, const Work
         if (seq0 == 0) seq0 = (uint32_t)-1;  // (0 never names a tick)
         HIP_CHECK(hipStreamSynchronize(L.stream));  // the idle grid has left
         L.h_door->base = seq0;
-        hipLaunchKernelGGL(qmx_tick_persistent, dim3(p_grid_), dim3(BS), 0, L.stream, L.h_door, L.d_ctl, p_grid_,
+        hipLaunchKernelGGL(qmx_tick_persistent<2>, dim3(p_grid_), dim3(BS), 0, L.stream, L.h_door, L.d_ctl, p_grid_,
                            ++L.p_gen, (uint32_t)p_idle_ms_ * 100000u, 0);
         HIP_CHECK(hipGetLastError());
         L.p_last_post = steady_s();
@@ -3546,7 +3557,7 @@ void HipEngine::ensure_persistent(TickLane& L) {
   if (L.p_running && steady_s() - L.p_last_post > 0.4e-3 * p_idle_ms_) stop_persistent(L);
   if (L.p_running) return;
   L.h_door->base = L.seq;  // the value posted last before this launch
-  hipLaunchKernelGGL(qmx_tick_persistent, dim3(p_grid_), dim3(BS), 0, L.stream, L.h_door, L.d_ctl, p_grid_,
+  hipLaunchKernelGGL(qmx_tick_persistent<2>, dim3(p_grid_), dim3(BS), 0, L.stream, L.h_door, L.d_ctl, p_grid_,
                      ++L.p_gen, (uint32_t)p_idle_ms_ * 100000u, 0);
   HIP_CHECK(hipGetLastError());
   L.p_running = true;
@@ -4538,7 +4549,10 @@ HipGrid::HipGrid(int device, int doors, int wg_per_door, int idle_ms)
     // processes sharing the GPU (rank rehearsals) split that half between their grids
     const char* sh = env_get("QMX_GPU_SHARERS");
     const int sharers = sh ? std::max(1, atoi(sh)) : 1;
-    const int cus = std::max(1, pr.multiProcessorCount), budget = cus / 2 / sharers;
+    // QMX_GRID_OCC=2: the register-capped kernel, two workgroups per CU — the budget is half
+    // the device's workgroup slots, not half its CUs
+    if (const char* oc = env_get("QMX_GRID_OCC")) occ_ = atoi(oc) == 2 ? 2 : 1;
+    const int cus = std::max(1, pr.multiProcessorCount), budget = cus * occ_ / 2 / sharers;
     if (n_ * wpd_ > budget) wpd_ = std::max(1, budget / n_);
     if (n_ * wpd_ > budget) throw std::runtime_error("grid: " + std::to_string(n_) + " doors do not fit " +
                                                      std::to_string(cus) + " CUs shared by " +
@@ -4589,8 +4603,12 @@ void HipGrid::launch_locked() {
   HIP_CHECK(hipSetDevice(device_));
   for (int d = 0; d < n_; ++d) h_doors_[d].base = __atomic_load_n(&h_doors_[d].relayed, __ATOMIC_ACQUIRE);
   const uint32_t idle_ticks = 2000u * 100000u;  // 2 s at 100 MHz: only a host that stopped beating
-  hipLaunchKernelGGL(qmx_tick_persistent, dim3(n_ * wpd_), dim3(BS), 0, stream_, h_doors_, d_ctls_, wpd_, ++gen_,
-                     idle_ticks, interleave_ ? 1 : 0);
+  if (occ_ == 2)
+    hipLaunchKernelGGL(qmx_tick_persistent<4>, dim3(n_ * wpd_), dim3(BS), 0, stream_, h_doors_, d_ctls_, wpd_, ++gen_,
+                       idle_ticks, interleave_ ? 1 : 0);
+  else
+    hipLaunchKernelGGL(qmx_tick_persistent<2>, dim3(n_ * wpd_), dim3(BS), 0, stream_, h_doors_, d_ctls_, wpd_, ++gen_,
+                       idle_ticks, interleave_ ? 1 : 0);
   HIP_CHECK(hipGetLastError());
   last_post_.store(steady_s(), std::memory_order_relaxed);
   running_.store(true, std::memory_order_release);
@@ -4713,7 +4731,7 @@ std::unordered_map<std::string, double> HipGrid::stats() {
   return {{"grid_launches", (double)launches_.load()}, {"grid_stops", (double)stops_.load()},
           {"grid_revivals", (double)revivals_.load()}, {"grid_doors", (double)n_},
           {"grid_clock_rtt_us", clk_rtt_us_.load(std::memory_order_relaxed)}, {"grid_xcd_local", interleave_ ? 1.0 : 0.0},
-          {"grid_wg_per_door", (double)wpd_},
+          {"grid_wg_per_door", (double)wpd_}, {"grid_wg_per_cu", (double)occ_},
           // (written under the exclusive lock; a torn read of a double is harmless here)
           {"grid_launch_us_max", launch_us_max_}, {"grid_launch_calibrate_us_max", launch_cal_us_max_},
           {"grid_launch_us_sum", launch_us_sum_}, {"grid_stop_us_max", stop_us_max_}};

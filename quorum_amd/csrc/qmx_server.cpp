@@ -3596,7 +3596,10 @@ int run_server(const ServerCfg& cfg0) {
     const char* fl = env_get("QMX_LOOP_INFLIGHT");
     const int per_loop = fl ? std::min(std::max(atoi(fl), 1), 2) : 2;  // doors per loop (as Loop::loop_doors_)
     try {
-      grid.reset(new HipGrid(cfg.device, (int)loops.size() * per_loop, w ? std::max(1, atoi(w)) : 8,
+      // (QMX_GRID_OCC=2: two workgroups per CU — twice the workgroups per door by default)
+      const char* oc = env_get("QMX_GRID_OCC");
+      const int wpd0 = oc && atoi(oc) == 2 ? 16 : 8;
+      grid.reset(new HipGrid(cfg.device, (int)loops.size() * per_loop, w ? std::max(1, atoi(w)) : wpd0,
                              im ? atoi(im) : 50));
     } catch (const std::exception& e) {  // e.g. more io loops than a partitioned GPU has CUs
       fprintf(stderr, "qmx: loop ticks unavailable (%s) — tick lanes instead\n", e.what());

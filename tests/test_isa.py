@@ -74,19 +74,43 @@ def kernel_resources(notes: str):
     return {d["name"]: d for d in out if "name" in d}
 
 
-def test_tick_kernels_have_no_scratch(code_object):
-    """The tick kernels (one-shot and persistent) keep everything in registers and LDS: no
-    private (scratch) memory and no VGPR spills — a spill to scratch is HBM traffic on every
-    item's critical path.  (SGPR spills go to VGPR lanes, not memory.)"""
+def _tick_kernels(code_object):
     notes = subprocess.run([str(LLVM / "llvm-readelf"), "--notes", str(code_object)], check=True,
                            capture_output=True, text=True).stdout
     res = kernel_resources(notes)
-    ticks = {k: v for k, v in res.items() if "qmx_tick_kernel" in k or "qmx_tick_persistent" in k}
-    assert len(ticks) == 2, sorted(res)
+    return {k: v for k, v in res.items() if "qmx_tick_kernel" in k or "qmx_tick_persistent" in k}
+
+
+def test_tick_kernels_have_no_scratch(code_object):
+    """The production tick kernels (one-shot, and the persistent grid's default variant with
+    one workgroup per CU) keep everything in registers and LDS: no private (scratch) memory
+    and no VGPR spills — a spill to scratch is HBM traffic on every item's critical path.
+    (SGPR spills go to VGPR lanes, not memory.)  The register-capped two-workgroups-per-CU
+    variant (qmx_tick_persistent<4>, QMX_GRID_OCC=2) is allowed its measured scratch."""
+    ticks = _tick_kernels(code_object)
+    assert len(ticks) == 3, sorted(ticks)
     for name, r in ticks.items():
+        assert r.get("group_segment_fixed_size", 0) <= 160 * 1024, (name, r)  # one CU's LDS
+        if "ILi4E" in name:  # two per CU: 2 x LDS must fit one CU, at most 128 VGPRs
+            assert 2 * r["group_segment_fixed_size"] <= 160 * 1024, (name, r)
+            assert r["vgpr_count"] <= 128 and r.get("private_segment_fixed_size", 0) <= 512, (name, r)
+            continue
         assert r.get("private_segment_fixed_size") == 0, (name, r)
         assert r.get("vgpr_spill_count", 0) == 0, (name, r)
-        assert r.get("group_segment_fixed_size", 0) <= 160 * 1024, (name, r)  # one CU's LDS
+
+
+def test_tick_kernel_register_ceilings(code_object):
+    """Register use of the tick kernels may not creep up unnoticed (round-5 review: the
+    persistent kernel's SGPR spills went 367 -> 377 with no test to say so).  Ceilings a little
+    above the round-6 build: one-shot 171 VGPRs / 247 SGPR spills, persistent 256 / 376."""
+    ticks = _tick_kernels(code_object)
+    for name, r in ticks.items():
+        if "qmx_tick_kernel" in name:
+            assert r["vgpr_count"] <= 184 and r.get("sgpr_spill_count", 0) <= 270, (name, r)
+        elif "ILi2E" in name:
+            assert r["vgpr_count"] <= 256 and r.get("sgpr_spill_count", 0) <= 400, (name, r)
+        else:
+            assert r.get("sgpr_spill_count", 0) <= 400, (name, r)
 
 
 _STORE = re.compile(r"^\s*(global_store|flat_store|buffer_store|global_atomic|flat_atomic|buffer_atomic)")
