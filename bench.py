@@ -75,6 +75,15 @@ SCENARIOS = {
                                         "--trickle", "1"]},
                             baseline=21.14, baseline_ttft_ms=620.5, baseline_source=BASELINE_SOURCE_SAME,
                             desc="config 5 with the faulty backend trickling its events (one write each)"),
+    # the headline with per-token upstreams: both backends write every SSE event on its own,
+    # with no delay (a real LLM server flushes one event per token) — a receive and an engine
+    # feed per event instead of one per response.  The reference buffers whole bodies, so the
+    # write granularity does not change its work: its headline number is the baseline.
+    "trickle": dict(n=2, strategy="concatenate", hide_final=False, skip=True, faults={}, timeout=30,
+                    mock_args=["--trickle", "1"], baseline=21.071, baseline_ttft_ms=619.6,
+                    baseline_source=BASELINE_SOURCE_SAME,
+                    desc="2 mock backends writing each SSE event on its own (per-token upstream writes), "
+                         "streaming concatenate, hide_intermediate_think"),
     # steady-state serving shape: backends pace their events (10 ms apart, like a decoding
     # LLM), many concurrent sessions, each tick sees a few events of many streams.  TTFT is
     # bounded below by the mock's own first-content time (5 events x 10 ms = 50 ms).

@@ -70,6 +70,7 @@ std::atomic<uint64_t> c_sp_failed{0}, c_sp_aborted{0}, c_sp_empty{0}, c_sp_text{
 // io loop passes (epoll return -> next wait) longer than 1 ms / 5 ms: anything that blocks a
 // loop (a synchronous device copy, a lock held by another thread) shows here
 std::atomic<uint64_t> c_loop_pass_1ms{0}, c_loop_pass_5ms{0};
+std::atomic<uint64_t> c_paced{0};  // loop passes stretched by read pacing (QMX_READ_PACE_US)
 std::atomic<int> g_sp_logs{0};  // rate limit: the first 20 anomalies are logged with their state
 
 // Prometheus histogram with lock-free buckets (seconds)
@@ -998,6 +999,19 @@ class Loop {
     std::vector<epoll_event> evs(512);
     double last_sweep = now_s();
     while (!g_stop.load()) {
+      // read pacing (QMX_READ_PACE_US): a pass that read trickling upstreams — small reads of
+      // responses still in progress, one SSE event each — is stretched to the pace, so the
+      // events that arrive meanwhile come out of one receive per socket and one wait instead
+      // of one each.  Whole-response reads never trigger it.
+      if (pace_s_ > 0 && small_reads_ >= pace_min_reads_) {
+        const double due = tnow_ + pace_s_, t = now_s();
+        if (t < due) {
+          timespec ts{0, (long)((due - t) * 1e9)};
+          nanosleep(&ts, nullptr);
+          c_paced++;
+        }
+      }
+      small_reads_ = 0;
       // inline engine with work queued by the last iteration (e.g. a finalize submitted
       // while applying tick results): poll instead of sleeping
       int to = (!hub_ && !aeng_ && kick_) ? 0 : deferq_.empty() ? 50 : 1;
@@ -2083,6 +2097,7 @@ class Loop {
             c_fail_protocol++;
             return up_error(u, "invalid HTTP response");
           }
+          if (r < 2048 && !u->rp.done()) ++small_reads_;  // a trickling upstream (read pacing)
           // plain TCP, short read: drained (level-triggered epoll reports more data); a
           // complete response needs no EAGAIN probe either.  TLS keeps reading: its
           // records can sit decrypted inside the SSL object with the socket empty.
@@ -3307,6 +3322,7 @@ class Loop {
     put("qmx_spread_release_deferred_total", (double)c_sp_release_deferred.load());
     put("qmx_loop_passes_over_1ms_total", (double)c_loop_pass_1ms.load());
     put("qmx_loop_passes_over_5ms_total", (double)c_loop_pass_5ms.load());
+    put("qmx_loop_paced_total", (double)c_paced.load());
     {
       double mx = 0;
       for (Loop* l : *loops_) mx = std::max(mx, l->pass_max_.load(std::memory_order_relaxed));
@@ -3482,6 +3498,15 @@ class Loop {
   // (the world > 1 path, HBM sinks and host copies included, on one GPU)
   const bool self_spread_ = env_flag("QMX_SPREAD_SELF", false);
   const bool stall_log_ = env_flag("QMX_LOOP_STALL_LOG", false);  // passes over 5 ms: phase split on stderr
+  const double pace_s_ = [this] {
+    const char* e = env_get("QMX_READ_PACE_US");
+    return std::max(0.0, e ? atof(e) : (double)cfg_.read_pace_us) * 1e-6;
+  }();
+  const int pace_min_reads_ = [] {
+    const char* e = env_get("QMX_READ_PACE_MIN");
+    return e ? std::max(1, atoi(e)) : 2;
+  }();
+  int small_reads_ = 0;  // this pass: short reads of upstream responses still in progress
   int stall_logs_ = 0;
   const bool lazy_wake_ = env_flag("QMX_LAZY_WAKE", false);   // A/B knob (see attach_hub)
   std::atomic<bool> in_wait_{false};                          // in epoll_wait (lazy wake)

@@ -41,6 +41,10 @@ struct ServerCfg {
   // "auto" = loops (spread placement included); lanes only when asked (tick_mode "lanes",
   // shared_engine = 1) or when the grid does not fit the GPU
   std::string tick_mode = "auto";
+  // read pacing: a loop pass that read trickling upstreams (short reads of responses in
+  // progress) lasts at least this long, so events arriving meanwhile share receives, waits and
+  // client sends (0: off; QMX_READ_PACE_US overrides)
+  int read_pace_us = 50;
   int device = 0;
   int tile = 16384, max_slots = 4096, content_cap = 1 << 20;
   // config

@@ -71,6 +71,7 @@ def native_config(cfg: Dict[str, Any], host: str, port: int, engine: str, device
         "shared_engine": -1 if rt.shared_engine in ("auto", None) else int(bool(rt.shared_engine)),
         "tick_lanes": int(rt.tick_lanes),
         "tick_mode": str(rt.tick_mode or "auto"),
+        "read_pace_us": int(rt.read_pace_us),
         "ca_file": _ca_bundle(), "tls_verify": os.environ.get("QMX_TLS_VERIFY", "1") not in ("0", "false"),
         "ready_file": (os.environ["QMX_READY_FILE"] + f".{os.getpid()}") if os.environ.get("QMX_READY_FILE") else "",
         # QMX_ADMIN_PORT: this process's own /metrics + /health port (not SO_REUSEPORT-shared)

@@ -240,7 +240,7 @@ void worker(int tid) {
         continue;
       }
       c.drop_at = (g.drop_rate > 0 && U(rng) < g.drop_rate) ? (int)(g_events.size() / 2) : -1;
-      if (g.delay_us <= 0 && c.drop_at < 0 && g.null_rate <= 0) {
+      if (g.delay_us <= 0 && c.drop_at < 0 && g.null_rate <= 0 && !g.trickle) {
         c.out += g_stream_all;
         if (!flush(c)) return false;
         continue;

@@ -269,6 +269,12 @@ class RuntimeConfig:
                when its content changes (the reference's ``uvicorn --reload --reload-include
                "*.yaml"``, Makefile:4; here without dropping a request) — QMX_WATCH_CONFIG
     watch_interval: seconds between those polls
+    read_pace_us: an io-loop pass that read trickling upstreams (short reads of responses still
+               in progress: one SSE event per write, as LLM servers send tokens) lasts at least
+               this long, so the events that arrive meanwhile share one receive per socket, one
+               wait and one client send; whole-response reads never trigger it.  MI355X box,
+               headline-shaped trickle: 33k -> 41k req/s and 192 -> 82 us proxy CPU per request at
+               50 us, p50 TTFT +0.08 ms (profiles/r6/pacing).  0: off — QMX_READ_PACE_US
     """
 
     engine: str = "auto"
@@ -290,6 +296,7 @@ class RuntimeConfig:
     log_content: bool = False
     watch_config: bool = False
     watch_interval: float = 1.0
+    read_pace_us: int = 50
 
     @classmethod
     def from_config(cls, cfg: Dict[str, Any]) -> "RuntimeConfig":
@@ -309,5 +316,7 @@ class RuntimeConfig:
             rt["tick_lanes"] = int(os.environ["QMX_TICK_LANES"])
         if os.environ.get("QMX_TICK_MODE"):
             rt["tick_mode"] = os.environ["QMX_TICK_MODE"]
+        if os.environ.get("QMX_READ_PACE_US"):
+            rt["read_pace_us"] = int(os.environ["QMX_READ_PACE_US"])
         known = {k: v for k, v in rt.items() if k in cls.__dataclass_fields__}
         return cls(**known)
