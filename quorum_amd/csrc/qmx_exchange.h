@@ -129,6 +129,7 @@ class Exchange {
   bool healthy() const { return healthy_.load(); }  // the mesh formed once and is running
   bool peer_up(int r) const;
   int rank() const { return o_.rank; }
+  const std::string& transport() const { return o_.transport; }
   int world() const { return o_.world; }
   // the bulk communicator (RCCL or tcpbulk) of the current epoch is formed
   bool rccl_active() const { return rccl_epoch_.load() > 0 && rccl_ok_.load(); }

@@ -66,7 +66,8 @@ std::atomic<uint64_t> c_fail_connect{0}, c_fail_timeout{0}, c_fail_status{0}, c_
 std::atomic<uint64_t> c_sp_failed{0}, c_sp_aborted{0}, c_sp_empty{0}, c_sp_text{0}, c_sp_down{0},
     c_sp_delta_mismatch{0}, c_sp_nodata{0} /* worker: content but no delta sent */,
     c_sp_eager{0} /* worker: final texts sent eagerly over the mesh (no round) */,
-    c_sp_release_deferred{0} /* owner: shadow slots released after the round writing them (X_RELEASE) */;
+    c_sp_release_deferred{0} /* owner: shadow slots released after the round writing them (X_RELEASE) */,
+    c_sp_fetched{0} /* worker: final texts copied out of HBM by a tick's finalize item */;
 // io loop passes (epoll return -> next wait) longer than 1 ms / 5 ms: anything that blocks a
 // loop (a synchronous device copy, a lock held by another thread) shows here
 std::atomic<uint64_t> c_loop_pass_1ms{0}, c_loop_pass_5ms{0};
@@ -478,6 +479,10 @@ struct Session {
   uint64_t owner_skey = 0;
   int data_sent = 0;          // worker: delta messages posted to the owner
   bool bulk_pending = false;  // worker: the final text is in flight (the slot must stay)
+  // worker, HIP engine: the final text is being fetched from HBM by a texts-kind finalize item
+  // of the loop's next tick (no synchronous device copy on the io loop); then it is here
+  bool fetching = false, fetched = false;
+  std::string fetched_text;
   bool first_content = false;  // TTFT recorded
 };
 
@@ -2503,10 +2508,24 @@ class Loop {
         post_owner(s, X_FINAL, b.aborted ? XF_ABORTED : 0, 0, std::string(), s->data_sent);
         return end_session(s);
       }
-      if ((long long)len <= (long long)cfg_.xchg_eager_bytes) {
+      const bool eager = (long long)len <= (long long)cfg_.xchg_eager_bytes;
+      size_t cap0 = 0;
+      // the text's bytes are needed on the host (eager, or a host transport: tcp mesh /
+      // tcpbulk / RCCL not formed) and sit in HBM: the loop's next tick copies them out in a
+      // texts-kind finalize item (on_finalized resumes here).  A synchronous hipMemcpy per
+      // text on the io loop cost ~70 us of CPU each (4-rank spread profile, round 6)
+      const bool host_bytes = eager || !(xch_->transport() == "rccl" && xch_->rccl_active());
+      if (host_bytes && !s->fetched && eng().content_device_ptr(b.slot, &cap0) != nullptr) {
+        s->fetching = true;  // (on_finalized runs begin_final again when the text is in)
+        s->fin_id = e_submit({b.slot}, false, true, std::string(), (int64_t)time(nullptr));
+        fin_owner_[s->fin_id] = {s, -1};
+        kick();
+        return;
+      }
+      if (eager) {
         // eager: a short text rides this loop's mesh frames right behind the stream's deltas
         // (one hop, no rank-0 manifest); the owner applies it as it would a round's delivery
-        const std::string t = eng().text(b.slot);
+        const std::string t = s->fetched ? std::move(s->fetched_text) : eng().text(b.slot);
         post_owner(s, X_BULK, XF_TEXT, (int)t.size(), t.data(), t.size(), s->data_sent);
         c_sp_eager++;
         return end_session(s);
@@ -2528,7 +2547,12 @@ class Loop {
       const int slot = b.slot;
       s->bulk_pending = true;
       flush_x();  // the stream's deltas go out ahead of its final text
-      xch_->send_bulk(std::move(h), dev, len, [e, slot] { return e->text(slot); });
+      if (s->fetched) {  // host bytes already copied out by the tick: no device read on any thread
+        std::string t = std::move(s->fetched_text);
+        xch_->send_bulk(std::move(h), dev, len, [t] { return t; });
+      } else {
+        xch_->send_bulk(std::move(h), dev, len, [e, slot] { return e->text(slot); });
+      }
       return;
     }
     if (cfg_.skip_final) return finish_stream(s);
@@ -2873,7 +2897,15 @@ class Loop {
     if (s->stage == 0 && s->finished == (int)s->bs.size()) begin_final(s);
   }
   void on_finalized(Session* s, FinalizeRes& f, int /*bi*/) {
-    if (s->kind == K_NONSTREAM || s->kind == K_REMOTE) return;  // not used
+    if (s->kind == K_REMOTE) {  // a worker's final text, fetched from HBM: ship it now
+      if (!s->fetching) return;
+      s->fetching = false;
+      s->fetched = true;
+      s->fetched_text = f.texts.empty() ? std::string() : std::move(f.texts[0]);
+      c_sp_fetched++;
+      return begin_final(s);
+    }
+    if (s->kind == K_NONSTREAM) return;  // not used
     if (!s->fin_texts) {
       if (f.kind == 1) send_chunk(s, f.event);
       else send_chunk(s, error_event());
@@ -3320,6 +3352,7 @@ class Loop {
     put("qmx_spread_worker_nodata_total", (double)c_sp_nodata.load());
     put("qmx_spread_eager_finals_total", (double)c_sp_eager.load());
     put("qmx_spread_release_deferred_total", (double)c_sp_release_deferred.load());
+    put("qmx_spread_texts_fetched_total", (double)c_sp_fetched.load());
     put("qmx_loop_passes_over_1ms_total", (double)c_loop_pass_1ms.load());
     put("qmx_loop_passes_over_5ms_total", (double)c_loop_pass_5ms.load());
     put("qmx_loop_paced_total", (double)c_paced.load());

@@ -229,7 +229,7 @@ for r in s.get('per_rank',[]): print('  ', r)
       grep "qmx spread\|qmx exchange" $OUT/selfrank_$n.err | head -20
       [ $rc -eq 0 ] || { echo "step selfrank_$n failed rc=$rc"; tail -30 $OUT/selfrank_$n.err; exit 1; } ;;
     selfsc=*)  # selfsc=N:ARGS — bench.py --gpus N (ranks sharing GPU 0) with extra args (commas = spaces)
-      rest=${step#selfsc=}; n=${rest%%:*}; a=${rest#*:}; slug=$(echo "$a" | tr -c 'a-zA-Z0-9' '_' | cut -c1-60)
+      rest=${step#selfsc=}; n=${rest%%:*}; a=${rest#*:}; slug=$(echo "$a" | sed -e 's/--scenario,//; s/--steps,[0-9]*,//; s/--warmup,[0-9]*,//; s/--batch,[0-9]*,//' | tr -c 'a-zA-Z0-9' '_' | cut -c1-90)
       QMX_BENCH_NDEV=${QMX_BENCH_NDEV:-1} timeout -k 10 400 python bench.py --gpus $n --threads 2 ${a//,/ } \
         > $OUT/selfsc_${n}_$slug.json 2> $OUT/selfsc_${n}_$slug.err
       rc=$?; summ selfsc_${n}_$slug $OUT/selfsc_${n}_$slug.json
