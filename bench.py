@@ -213,21 +213,71 @@ def pin_rank(torch, world: int, local_rank: int, n_dev: int):
         pr = torch.cuda.get_device_properties(r)
         nodes.append(pci_numa_node(pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id))
     allowed = sorted(os.sched_getaffinity(0))
-    llc = llc_cpus(max(0, nodes[local_rank]))  # 0: no cache topology -> the node split
-    cpus = None
-    if llc > 0:
-        share = max(1, available_cores() // max(1, local_world))
-        per_rank = min(-(-share // llc) * llc, 2 * llc)
-        cpus = rank_llc_cpus(nodes, local_rank, per_rank, allowed)
-    how = "llc"
-    if not cpus:
-        plan = plan_rank_cpus(nodes, allowed)
-        cpus = plan[local_rank] if plan else None
-        how = "node"
+    cpus, how = rank_cpu_set(nodes, local_rank, allowed, available_cores())
     if not cpus:
         return {"numa_nodes": nodes, "pinned": False}
     os.sched_setaffinity(0, cpus)
     return {"numa_nodes": nodes, "pinned": True, "how": how, "cpus": len(cpus), "first": cpus[0], "last": cpus[-1]}
+
+
+def rank_cpu_set(nodes, local_rank: int, allowed, quota: int):
+    """(CPUs, how) a rank binds to (pin_rank; nothing is bound here): whole L3s of its GPU's
+    NUMA node, its share of the quota rounded up to whole L3s and at most two ("llc"); else
+    the node's cores split between its ranks ("node"); else (None, None)."""
+    from quorum_amd.parallel.topology import llc_cpus, plan_rank_cpus, rank_llc_cpus
+
+    llc = llc_cpus(max(0, nodes[local_rank]))  # 0: no cache topology -> the node split
+    if llc > 0:
+        share = max(1, quota // max(1, len(nodes)))
+        per_rank = min(-(-share // llc) * llc, 2 * llc)
+        # every rank decides alone: whole L3s only if EVERY rank of the node gets its own, or
+        # a rank that got L3s would overlap the ones that fell back to the node split
+        sets = [rank_llc_cpus(nodes, r, per_rank, allowed) for r in range(len(nodes))]
+        if all(sets):
+            return sets[local_rank], "llc"
+    plan = plan_rank_cpus(nodes, allowed)
+    if plan and plan[local_rank]:
+        return plan[local_rank], "node"
+    return None, None
+
+
+# Cores one rank's harness keeps busy at the headline's full rate on the MI355X box (proxy
+# 6.8, mocks 3.0, load generator 3.3: profiles/r6/engine_ab/bench_1.json `cores_busy`)
+HEADLINE_CORES_PER_RANK = 13.1
+
+
+def node_plan(world: int, sc: dict, args, quota: int, allowed, nodes) -> dict:
+    """What `bench.py --gpus world` will run on this node, per rank, without running it:
+    io threads, load-generator and mock threads, the CPU set and L3s each rank binds to, and
+    whether the job's CPU quota can feed `world` ranks at the one-GPU rate.  Every rank's
+    proxy, mocks and load generator share its CPU set, so a quota below world x
+    HEADLINE_CORES_PER_RANK makes the scaling curve measure the quota, not the GPUs."""
+    from quorum_amd.parallel.topology import _llc_key
+
+    threads = args.threads if args.threads > 0 else max(2, min(8, quota // (2 * world)))
+    ranks = []
+    seen, overlap = set(), False
+    for r in range(world):
+        cpus, how = rank_cpu_set(nodes, r, allowed, quota) if world > 1 else (None, None)
+        overlap = overlap or bool(seen & set(cpus or []))
+        seen |= set(cpus or [])
+        lg = args.lg_threads if args.lg_threads > 0 else (4 if cpus else 3)
+        mock = sc["n"] * args.mock_threads
+        l3s = sorted({_llc_key(c, __import__("quorum_amd.parallel.topology", fromlist=["x"]).CPU_DEVICES)
+                      for c in (cpus or [])})
+        ranks.append({"rank": r, "numa_node": nodes[r], "io_threads": threads, "loadgen_threads": lg,
+                      "mock_processes": sc["n"], "mock_threads": mock, "busy_threads": threads + lg + mock,
+                      "cpus": len(cpus) if cpus else None, "first": cpus[0] if cpus else None,
+                      "last": cpus[-1] if cpus else None, "l3s": len(l3s) if cpus else None, "how": how})
+    bound = sum(x["cpus"] or 0 for x in ranks)
+    demand = round(HEADLINE_CORES_PER_RANK * world, 1)
+    return {"world": world, "quota_cpus": quota, "allowed_cpus": len(allowed), "gpu_numa_nodes": nodes,
+            "ranks": ranks, "cpus_bound_total": bound,
+            "headline_cores_demand": demand,
+            # the curve measures GPUs only while the quota covers every rank's harness
+            "quota_bound": quota < demand,
+            "quota_needed_cpus": int(-(-demand // 1)),
+            "overlapping_sets": overlap}
 
 
 def pin_single(torch, n_dev: int):
@@ -1086,11 +1136,24 @@ def main() -> int:
     ap.add_argument("--ceiling", type=float, default=2.0,
                     help="seconds of the harness-ceiling check after the timed region (the load generator straight "
                          "against one mock, no proxy: harness_ceiling_req_s); 0 skips it")
+    ap.add_argument("--plan", action="store_true",
+                    help="print the per-rank thread / CPU plan for --gpus N on this node (QMX_SYSFS_ROOT: a "
+                         "copy of /sys; QMX_BENCH_QUOTA: the CPU quota) and exit — nothing is launched or bound")
     ap.add_argument("--eager-bytes", type=int, default=-1,
                     help="spread: final texts up to this size ride the mesh behind their deltas (-1: the "
                          "production default, 4 KiB); 0 sends every remote final text through a bulk round "
                          "(RCCL ncclSend/ncclRecv HBM -> HBM on GPUs; tcpbulk when ranks share a GPU)")
     args = ap.parse_args()
+    if args.plan:
+        from quorum_amd.parallel.topology import all_node_cpus, gpu_numa_nodes
+
+        world = args.gpus or 1
+        quota = int(os.environ.get("QMX_BENCH_QUOTA") or available_cores())
+        allowed = (all_node_cpus() if os.environ.get("QMX_SYSFS_ROOT") else sorted(os.sched_getaffinity(0)))
+        nodes = gpu_numa_nodes()
+        nodes = [max(0, nodes[r % len(nodes)]) if nodes else 0 for r in range(world)]
+        print(json.dumps(node_plan(world, SCENARIOS[args.scenario], args, quota, allowed, nodes)), flush=True)
+        return 0
     env_world = os.environ.get("WORLD_SIZE")
     if args.gpus is not None and args.gpus > 1 and env_world is None:
         return self_launch(args.gpus)

@@ -21,7 +21,10 @@ from dataclasses import dataclass
 from pathlib import Path
 from typing import Dict, List, Mapping, Optional
 
-KFD_TOPOLOGY = Path("/sys/class/kfd/kfd/topology/nodes")
+# QMX_SYSFS_ROOT: read the topology from a copy of /sys (tests and `bench.py --plan` on a
+# fake 8-GPU node); set before this module is imported
+SYSFS = Path(os.environ.get("QMX_SYSFS_ROOT", "/sys"))
+KFD_TOPOLOGY = SYSFS / "class/kfd/kfd/topology/nodes"
 # KFD io_link "type" values (kfd_topology.h: CRAT_IOLINK_TYPE_*)
 LINK_TYPES = {1: "hypertransport", 2: "pcie", 11: "xgmi"}
 
@@ -136,9 +139,19 @@ def summary(links: Optional[List[Link]] = None, n_gpus: Optional[int] = None,
 # (which poll the GPU's mapped result records) and — in bench.py — its load generator and
 # mock backends talk over loopback TCP, so keeping them on the GPU's NUMA node keeps both
 # the socket traffic and the mapped-memory polling socket-local.
-PCI_DEVICES = Path("/sys/bus/pci/devices")
-NUMA_NODES = Path("/sys/devices/system/node")
-CPU_DEVICES = Path("/sys/devices/system/cpu")
+PCI_DEVICES = SYSFS / "bus/pci/devices"
+NUMA_NODES = SYSFS / "devices/system/node"
+CPU_DEVICES = SYSFS / "devices/system/cpu"
+
+
+def all_node_cpus(root: Path = NUMA_NODES) -> List[int]:
+    """Every CPU of every NUMA node (the machine's CPUs as the topology reports them)."""
+    out: List[int] = []
+    if root.is_dir():
+        for p in sorted(root.iterdir()):
+            if p.name.startswith("node") and p.name[4:].isdigit():
+                out.extend(node_cpus(int(p.name[4:]), root))
+    return sorted(set(out))
 
 
 def parse_cpulist(s: str) -> List[int]:

@@ -397,3 +397,69 @@ def test_pin_single_specs(monkeypatch):
     monkeypatch.delenv("QMX_BENCH_CPUS")
     monkeypatch.setattr(bench, "available_cores", lambda: 256)  # the whole machine: nothing to gain
     assert bench.pin_single(None, 0)["pinned"] is False
+
+
+def _fake_mi355x_node(root):
+    """A copy of the sysfs an 8 x MI355X node shows: 2 sockets x 64 cores x 2 SMT (CPU c and
+    c + 128 are siblings), 16 CCDs of 8 cores (one L3 each), GPUs 0-3 on NUMA node 0 and 4-7
+    on node 1 (KFD nodes 2-9, their PCI functions' numa_node)."""
+    node = root / "devices/system/node"
+    for n in range(2):
+        d = node / f"node{n}"
+        d.mkdir(parents=True)
+        d.joinpath("cpulist").write_text(f"{64 * n}-{64 * n + 63},{128 + 64 * n}-{128 + 64 * n + 63}\n")
+    for c in range(256):
+        core = c % 128
+        t = root / f"devices/system/cpu/cpu{c}/topology"
+        t.mkdir(parents=True)
+        t.joinpath("physical_package_id").write_text(f"{core // 64}\n")
+        t.joinpath("core_id").write_text(f"{core % 64}\n")
+        k = core // 8
+        l3 = root / f"devices/system/cpu/cpu{c}/cache/index3"
+        l3.mkdir(parents=True)
+        l3.joinpath("shared_cpu_list").write_text(f"{8 * k}-{8 * k + 7},{128 + 8 * k}-{128 + 8 * k + 7}\n")
+    kfd = root / "class/kfd/kfd/topology/nodes"
+    for n in range(10):
+        d = kfd / str(n)
+        d.mkdir(parents=True)
+        if n < 2:
+            d.joinpath("properties").write_text("simd_count 0\n")
+            continue
+        g = n - 2
+        bus = [0x05, 0x15, 0x65, 0x75, 0x85, 0x95, 0xE5, 0xF5][g]
+        d.joinpath("properties").write_text(f"simd_count 1024\ndomain 0\nlocation_id {bus << 8}\n")
+        p = root / f"bus/pci/devices/0000:{bus:02x}:00.0"
+        p.mkdir(parents=True)
+        p.joinpath("numa_node").write_text("0\n" if g < 4 else "1\n")
+
+
+@pytest.mark.parametrize("quota", [128, 16])
+def test_bench_plan_for_8_gpus(tmp_path, quota):
+    """`bench.py --plan --gpus 8` on a fake 8-GPU node: what each rank runs and binds to,
+    before the driver's scaling run (round-5 review: the 8-GPU plan was never printed).  With
+    a 128-CPU quota every rank gets one CCD of its GPU's socket — 16 CPUs, disjoint, the
+    one-GPU bench's own shape (8 io threads, 4 load-generator threads, 2 x 2 mock threads) —
+    and the quota covers the harness.  With the one-GPU box's 16-CPU quota on the whole node,
+    the plan says the curve would measure the quota (quota_bound), not the GPUs."""
+    import json
+
+    _fake_mi355x_node(tmp_path)
+    env = dict(_env(), QMX_SYSFS_ROOT=str(tmp_path), QMX_BENCH_QUOTA=str(quota))
+    r = subprocess.run([sys.executable, BENCH, "--plan", "--gpus", "8"], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    plan = json.loads(r.stdout.strip().splitlines()[-1])
+    assert plan["world"] == 8 and plan["gpu_numa_nodes"] == [0, 0, 0, 0, 1, 1, 1, 1]
+    assert not plan["overlapping_sets"]
+    ranks = plan["ranks"]
+    for x in ranks:
+        assert x["how"] == "llc" and x["cpus"] == 16 and x["l3s"] == 1, x
+        lo = 0 if x["numa_node"] == 0 else 64  # the CCD is on the rank's GPU's socket
+        assert lo <= x["first"] < lo + 64 and x["last"] >= 128, x
+        assert x["mock_processes"] == 2 and x["mock_threads"] == 4
+    if quota == 128:
+        assert all(x["io_threads"] == 8 and x["loadgen_threads"] == 4 and x["busy_threads"] == 16 for x in ranks)
+        assert not plan["quota_bound"] and plan["cpus_bound_total"] == 128
+    else:
+        assert all(x["io_threads"] == 2 for x in ranks)
+        assert plan["quota_bound"] and plan["quota_needed_cpus"] > 100
