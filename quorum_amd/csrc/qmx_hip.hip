@@ -53,7 +53,7 @@ namespace qmx {
 
 constexpr int BS = 512;  // 8 waves: S3 spreads events over 8 waves; 2 waves per SIMD hide LDS latency (16 waves measured slower: S3 13.3 -> 15.6 us)
 constexpr int TILE_MAX = 16384;
-constexpr int MAX_EV = 512;  // events per tile (more → WS_MORE requeue); keeps LDS < 80 KiB (2 WG/CU)
+constexpr int MAX_EV = 512;  // events per tile (more → WS_MORE requeue); keeps LDS < 80 KiB (two fit a CU's 160 KB: the QMX_GRID_OCC=2 variant)
 constexpr int MAX_CAND = 1024;
 constexpr int PAD = 16;
 constexpr int kSpecTile = BS * 16;  // tile bytes loaded before the work item is known (16 B per thread: a whole headline stream, ~4.9 KB, in the same PCIe round trip as the item)
