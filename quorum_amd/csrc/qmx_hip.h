@@ -100,7 +100,8 @@ struct KParams {
   uint64_t pw[2 * kMaxTags][kMaxTail / 8];
   uint32_t content_cap;
   // single-wave fast paths of the common small tile (QMX_KFAST bit mask, default all):
-  // 1 S2 framing, 2 S3a template prepass, 4 S4 filter, 8 S6 sizing
+  // 1 S2 framing, 2 S3a template prepass, 4 S4 filter, 8 S6 sizing, 16 S4's VALU matcher
+  // for <= 4 candidates (else the MFMA matcher)
   uint32_t fast;
   int pre1_len, pre2_len, suf_len;
   char pre1[48];

@@ -371,6 +371,32 @@ __device__ inline void mfma_match_group(const uint8_t* Z, int Zn, const uint16_t
   }
 }
 
+// The same match for a handful of candidates (<= 4) and tags whose patterns fit the 16-byte
+// window (every default tag): lane (c, t) = (lane >> 4, lane & 15) compares candidate c's
+// lowercased window with pattern t on VALU, 8 bytes at a time under the pattern's length
+// mask — one step for all 64 pairs.  Measured (tools/probes/s3a_mfma_probe.hip): against one
+// or a few patterns VALU SWAR is several times cheaper than building the MFMA operands; the
+// MFMA matcher keeps the tiles with many '<' (16 candidate windows × 16 patterns per MFMA).
+// Bytes past Zn read as 0 (no pattern byte), as in mfma_match_group.  Pattern words and
+// lengths from the item's LDS copy of the parameters.
+__device__ inline void swar_match_small(const uint8_t* Z, int Zn, const uint16_t* cand, int ncand, int npat, int nts,
+                                        const KParams& P, int8_t* cand_tok) {
+  const int lane = threadIdx.x & 63, c = lane >> 4, t = lane & 15;
+  const uint64_t p0 = P.pw[t][0], p1 = P.pw[t][1];
+  const int L = P.plen[t];
+  const bool v = c < ncand && t < npat;
+  const int p = v ? (int)cand[c] : 0;
+  bool hit = false;
+  if (v) {
+    const uint64_t w0 = lower8(lds_window8(Z, p, Zn)), w1 = lower8(lds_window8(Z, p + 8, Zn));
+    const uint64_t m0 = L >= 8 ? ~0ull : ((1ull << (8 * L)) - 1ull);
+    const uint64_t m1 = L >= 16 ? ~0ull : L > 8 ? ((1ull << (8 * (L - 8))) - 1ull) : 0ull;
+    hit = L > 0 && ((w0 ^ p0) & m0) == 0 && ((w1 ^ p1) & m1) == 0;
+  }
+  // distinct tags never both match at one '<' (make_tagset): one writer per candidate
+  if (hit) cand_tok[c] = (int8_t)(t < nts ? t + 1 : -(t - nts + 1));
+}
+
 __device__ inline int tok_plen(const KParams& P, int id) {
   return id > 0 ? P.ts.len[id - 1] + 2 : P.ts.len[-id - 1] + 3;
 }
@@ -725,7 +751,13 @@ __device__ bool s4_wave(Smem& s, const uint8_t* Z, int Zn, int ndelta, int depth
   if (lane < nc) s.cand_tok[lane] = 0;
   wave_fence();
   if (dbg != nullptr && lane == 0) dbg_put(&dbg[29], __builtin_amdgcn_s_memrealtime());
-  for (int g = 0; g * 16 < nc; ++g) mfma_match_group(Z, Zn, s.cand, nc, g, P, bf0, bf1, pc, npat, nts, s.cand_tok);
+  // a few candidates and window-sized patterns (QMX_KFAST bit 16): VALU pairs; else MFMA
+  const bool small = (P.fast & 16) && nc <= 4 && npat <= 16 && __ballot(lane < npat && pl_l > kWindow) == 0;
+  if (small) {
+    swar_match_small(Z, Zn, s.cand, nc, npat, nts, P, s.cand_tok);
+  } else {
+    for (int g = 0; g * 16 < nc; ++g) mfma_match_group(Z, Zn, s.cand, nc, g, P, bf0, bf1, pc, npat, nts, s.cand_tok);
+  }
   wave_fence();
   if (dbg != nullptr && lane == 0) dbg_put(&dbg[23], __builtin_amdgcn_s_memrealtime());
   // tokens and the depth before each (candidates in order, non-tokens the scan identity);
@@ -3378,7 +3410,7 @@ HipEngine::HipEngine(const std::vector<std::string>& tags, int device, int tile_
   for (int p = 0; p < base_params_.npat; ++p)
     for (int j = 0; j < pattern_len(ts_, p); ++j)
       base_params_.pw[p][j >> 3] |= (uint64_t)pattern_byte(ts_, p, j) << (8 * (j & 7));
-  base_params_.fast = 15;
+  base_params_.fast = 31;
   if (const char* kf = env_get("QMX_KFAST")) base_params_.fast = (uint32_t)strtoul(kf, nullptr, 0);
   for (int blk = 0; blk < 2; ++blk)
     for (int l = 0; l < 64; ++l) {

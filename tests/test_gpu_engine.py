@@ -86,12 +86,13 @@ def test_hip_matches_cpu_random(ext, seed):
     _check(seed, 6)
 
 
-@pytest.mark.parametrize("kfast", [0, 14, 13, 11, 7])
+@pytest.mark.parametrize("kfast", [0, 30, 29, 27, 23, 15])
 @pytest.mark.parametrize("seed", range(6))
 def test_hip_fast_paths_off(ext, monkeypatch, kfast, seed):
     """Each single-wave fast path switched off in turn (QMX_KFAST: 1 S2 framing, 2 S3a, 4 S4,
-    8 S6 sizing): the block paths they shortcut — among them the block framing's one-scan
-    path and its run-scan fallback for triple newlines (ODD_EVENTS) — give the same bytes."""
+    8 S6 sizing, 16 S4's VALU matcher for <= 4 candidates — off: the MFMA matcher for every
+    tile): the block paths they shortcut — among them the block framing's one-scan path and
+    its run-scan fallback for triple newlines (ODD_EVENTS) — give the same bytes."""
     monkeypatch.setenv("QMX_KFAST", str(kfast))
     _check(5000 + seed, 12, max_piece=5000)
 
