@@ -283,3 +283,94 @@ def test_server_asan_abort_churn_shared_engine(san_bins, tmp_path):
     err = err.decode(errors="replace")
     assert srv.returncode == 0 and "AddressSanitizer" not in err and "runtime error" not in err, err[-4000:]
     assert r["aborted"] > 200 and r["invalid"] == 0 and r["errors"] == 0, (r, out.stderr[-2000:])
+
+
+def test_server_tsan_self_spread_rounds(tmp_path):
+    """ThreadSanitizer data plane with the exchange live: QMX_SPREAD_SELF at one rank sends the
+    odd backends through the rank's own exchange (mesh thread, tcpbulk round executor on the
+    bulk thread, four io loops), every final text through a round (eager 0), round 2 stalled
+    to its timeout (QMX_XCHG_FAULT_STALL_ROUND) while clients leave mid-response — the deferred
+    shadow-slot releases (forget_bulk -> X_RELEASE) and the mesh fallback run concurrently
+    with the loops.  Any data race report fails the test."""
+    import concurrent.futures as cf
+
+    from live_upstream import free_port_block
+    from quorum_amd.ops import build
+    from quorum_amd.runtime.native_server import native_config
+
+    tsan = build.build_tsan()
+    live = LiveUpstream()
+    stream = sse_stream(["Hel", "lo <think>x</think> wor", "ld"])
+    ports = [live.serve("a", ("stream", 200, stream)), live.serve("b", ("stream", 200, sse_stream(["x", "y"])))]
+    block = {"separator": "\n--\n", "hide_intermediate_think": True, "hide_final_think": True,
+             "thinking_tags": ["think"], "skip_final_aggregation": False}
+    cfg = cfg_parallel(2, block=block)
+    for b, p in zip(cfg["primary_backends"], ports):
+        b["url"] = f"http://127.0.0.1:{p}/v1"
+    cfg.setdefault("runtime", {})["placement"] = "spread"
+    port = free_port()
+    xenv = {"QMX_XCHG": "tcpbulk", "QMX_XCHG_PORT": str(free_port_block(2)), "QMX_XCHG_EAGER_BYTES": "0",
+            "QMX_XCHG_TIMEOUT": "2", "QMX_XCHG_ROUND_US": "100"}
+    old = {k: os.environ.get(k) for k in xenv}
+    os.environ.update(xenv)
+    try:
+        d = native_config(cfg, "127.0.0.1", port, "cpu", 0, 4)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    d.update(env_api_key="", api_key_from_env=False, tick_mode="loops")
+    path = tmp_path / "tsan_spread.json"
+    path.write_text(json.dumps(d))
+    env = dict(os.environ, **xenv, QMX_SPREAD_SELF="1", QMX_XCHG_FAULT_STALL_ROUND="2",
+               TSAN_OPTIONS="halt_on_error=0:second_deadlock_stack=1:report_signal_unsafe=0")
+    srv = subprocess.Popen([str(tsan), str(path)], stderr=subprocess.PIPE, env=env)
+    try:
+        t0 = time.time()
+        while time.time() - t0 < 60:
+            try:
+                m = httpx.get(f"http://127.0.0.1:{port}/metrics", timeout=1).text
+                if "qmx_exchange_rccl_active 1.000000" in m:
+                    break
+            except httpx.HTTPError:
+                pass
+            time.sleep(0.1)
+        req = {"messages": [{"role": "user", "content": "q"}], "stream": True}
+
+        def client(i):
+            if i % 3 == 0:  # a client that leaves mid-response (its final may be in a round)
+                s = socket.create_connection(("127.0.0.1", port))
+                body = json.dumps(req).encode()
+                s.sendall(b"POST /chat/completions HTTP/1.1\r\nhost: x\r\nauthorization: Bearer k\r\n"
+                          b"content-type: application/json\r\ncontent-length: %d\r\n\r\n%s" % (len(body), body))
+                s.recv(256)
+                s.close()
+                return True
+            with httpx.Client(base_url=f"http://127.0.0.1:{port}") as c:
+                for _ in range(6):
+                    r = c.post("/chat/completions", json=req, headers={"Authorization": "Bearer k"}, timeout=90)
+                    assert r.status_code == 200 and r.text.rstrip().endswith("data: [DONE]")
+            return True
+
+        with cf.ThreadPoolExecutor(6) as ex:
+            assert all(ex.map(client, range(12)))
+        m = httpx.get(f"http://127.0.0.1:{port}/metrics").text
+
+        def metric(k):
+            return float([ln for ln in m.splitlines() if ln.startswith(k + " ")][0].split()[1])
+        assert metric("qmx_remote_streams_total") > 0
+        assert metric("qmx_exchange_rounds_total") > 0           # finals moved in rounds ...
+        assert metric("qmx_exchange_mesh_finals_total") > 0      # ... and the stalled round's by the mesh
+    finally:
+        srv.send_signal(signal.SIGINT)
+        try:
+            _, err = srv.communicate(timeout=60)
+        except subprocess.TimeoutExpired:
+            srv.kill()
+            _, err = srv.communicate()
+        live.close()
+    err = err.decode(errors="replace")
+    assert "ThreadSanitizer" not in err, err[-6000:]
+    assert srv.returncode == 0, err[-3000:]
