@@ -1081,6 +1081,11 @@ class Loop {
         } else {
           dispatch(evs[i]);
         }
+        // QMX_EAGER_POST: upstream bytes go to a free door at once, not after the batch
+        if (eager_post_ && aeng_ && !ops_.empty() && (evs[i].data.u64 >> 32) == 4 && aeng_->free_doors() > 0) {
+          flush_ops();
+          loop_tick();
+        }
         // a long batch: tick results that arrived meanwhile are applied now, not after it
         if ((i & 7) == 7 && early_flush_ && rq_pending_.load(std::memory_order_acquire)) on_results(false);
         if ((i + 1) % check_every_ == 0 && jobs_live_ && any_ready()) loop_tick();
@@ -3531,6 +3536,8 @@ class Loop {
   // (the world > 1 path, HBM sinks and host copies included, on one GPU)
   const bool self_spread_ = env_flag("QMX_SPREAD_SELF", false);
   const bool stall_log_ = env_flag("QMX_LOOP_STALL_LOG", false);  // passes over 5 ms: phase split on stderr
+  // A/B knob (see the event loop): measured within noise (profiles/r6/eager_post), so off
+  const bool eager_post_ = env_flag("QMX_EAGER_POST", false);
   const double pace_s_ = [this] {
     const char* e = env_get("QMX_READ_PACE_US");
     return std::max(0.0, e ? atof(e) : (double)cfg_.read_pace_us) * 1e-6;
