@@ -64,11 +64,13 @@ def test_native_hip_random_sessions(seed, monkeypatch):
     assert ext.server_counters()["verify_mismatches"] == before
 
 
-def test_gpu_bench_headline_valid(tmp_path):
+@pytest.mark.parametrize("knob,port", [("", 23400), ("QMX_EAGER_POST=1", 23500)])
+def test_gpu_bench_headline_valid(tmp_path, knob, port):
     """The headline bench on the HIP engine (shared engine, pipelined tick lanes, persistent
     grids, result views) under full closed-loop load: every response is validated byte for
     byte by the load generator, so a lane that reuses an output arena too early, or any other
-    cross-tick corruption, fails here."""
+    cross-tick corruption, fails here.  QMX_EAGER_POST=1: an io loop posts upstream bytes to a
+    free door in the middle of its event batch (an A/B knob, off by default) — same bytes."""
     import json
     import os
     import subprocess
@@ -76,8 +78,11 @@ def test_gpu_bench_headline_valid(tmp_path):
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, QMX_BENCH_ENGINE="hip")
+    if knob:
+        k, v = knob.split("=")
+        env[k] = v
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "4", "--warmup", "1",
-                        "--batch", "8192", "--port", "23400"],
+                        "--batch", "8192", "--port", str(port)],
                        cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=180)
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert lines, r.stderr[-3000:]
