@@ -510,6 +510,19 @@ def cpu_seconds(pid: int) -> float:
         return 0.0
 
 
+def rss_mb(pid: int) -> dict:
+    """Resident memory of a live process (VmRSS) and its peak (VmHWM), MB, from /proc."""
+    out = {}
+    try:
+        for ln in open(f"/proc/{pid}/status"):
+            k, _, v = ln.partition(":")
+            if k in ("VmRSS", "VmHWM"):
+                out[k] = round(int(v.split()[0]) / 1024.0, 1)
+    except (OSError, ValueError, IndexError):
+        pass
+    return out
+
+
 def cgroup_cpu_stat() -> dict:
     """The job's cgroup CPU accounting (cgroup v2 cpu.stat + cpu.max): a CPU quota throttles
     every process of the job for the rest of a period once it is used up — latency spikes the
@@ -1329,6 +1342,7 @@ def main() -> int:
         scraped = args.impl == "native" and not direct
         m0 = scrape(admin_port) if scraped else {}
         c0 = cpu_snapshot(mock_procs, proxy_procs)
+        r0 = rss_mb(proxy_procs[0].pid) if proxy_procs else {}
         g0 = cgroup_cpu_stat()
         t0 = time.perf_counter()
         stats = loadgen(bin_dir, proxy_port, args.conns, args.steps * args.batch, args.lg_threads, args.timeout,
@@ -1343,6 +1357,9 @@ def main() -> int:
         bd = breakdown(m0, scrape(admin_port), elapsed) if scraped else {}
         bd["pid"] = proxy_procs[0].pid if proxy_procs else None
         bd.update(cpu_breakdown(c0, c1, stats["completed"], elapsed))
+        r1 = rss_mb(proxy_procs[0].pid) if proxy_procs else {}
+        if r0 and r1:  # rank 0's proxy: resident memory before / after the timed steps, and its peak
+            bd["proxy_rss_MB"] = {"start": r0.get("VmRSS"), "end": r1.get("VmRSS"), "peak": r1.get("VmHWM")}
         if g0 and g1:  # the whole job's CPU over the timed region, and any quota throttling
             bd["cgroup"] = {"quota_cpus": g1.get("quota_cpus"),
                             "cores_busy": round((g1.get("usage_usec", 0) - g0.get("usage_usec", 0)) / 1e6 / elapsed, 2)

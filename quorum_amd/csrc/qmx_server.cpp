@@ -929,6 +929,7 @@ class Loop {
  public:
   Loop(const ServerCfg& cfg, int idx) : cfg_(cfg), idx_(idx) { xfd_ = eventfd(0, EFD_NONBLOCK); }
   void attach_exchange(Exchange* x) { xch_ = x; }
+  int index() const { return idx_; }
   void attach_hub(GpuHub* h) {
     hub_ = h;
     if (h)
@@ -3702,13 +3703,16 @@ int run_server(const ServerCfg& cfg0) {
     xch.reset(new Exchange(o, (int)lp.size(), [lp](int l, std::vector<XMsg>&& v) { lp[l]->x_deliver(std::move(v)); }));
     for (auto& l : loops) l->attach_exchange(xch.get());
   }
-  // QMX_LOOP_STALL_LOG: a watchdog samples, for an io loop stuck in one pass for over 20 ms,
-  // what the kernel has that thread (and every other thread of the process) waiting in:
-  // /proc/self/task/<tid>/wchan and .../syscall — the blocking call and the lock behind it
+  // QMX_LOOP_STALL_LOG: a watchdog samples, for an io loop stuck in one pass for over 20 ms
+  // (QMX_LOOP_STALL_WATCH_MS), what the kernel has that thread (and every other thread of the
+  // process) waiting in: /proc/self/task/<tid>/wchan and .../syscall — the blocking call and
+  // the lock behind it
   std::thread watchdog;
   std::atomic<bool> wd_stop{false};
   if (env_flag("QMX_LOOP_STALL_LOG", false)) {
-    watchdog = std::thread([&loops, &wd_stop] {
+    const char* wm = env_get("QMX_LOOP_STALL_WATCH_MS");
+    const double watch_s = std::max(1.0, wm ? atof(wm) : 20.0) * 1e-3;
+    watchdog = std::thread([&loops, &wd_stop, watch_s] {
       auto slurp = [](const std::string& path) {
         std::string out;
         if (FILE* f = fopen(path.c_str(), "r")) {
@@ -3722,12 +3726,12 @@ int run_server(const ServerCfg& cfg0) {
       };
       int dumps = 0;
       std::vector<double> seen(loops.size(), 0.0);
-      while (!wd_stop.load() && dumps < 20) {
-        std::this_thread::sleep_for(std::chrono::milliseconds(5));
+      while (!wd_stop.load() && dumps < 60) {
+        std::this_thread::sleep_for(std::chrono::microseconds(std::min(5000, (int)(watch_s * 2.5e5))));
         const double t = now_s();
         for (size_t i = 0; i < loops.size(); ++i) {
           const double t0 = loops[i]->pass_t0_.load(std::memory_order_relaxed);
-          if (t0 <= 0 || t - t0 < 0.02 || seen[i] == t0) continue;
+          if (t0 <= 0 || t - t0 < watch_s || seen[i] == t0) continue;
           seen[i] = t0;
           ++dumps;
           std::string msg = "qmx watchdog: loop " + std::to_string(i) + " in one pass for " +
@@ -3752,6 +3756,9 @@ int run_server(const ServerCfg& cfg0) {
   for (auto& l : loops) {
     Loop* lp = l.get();
     ts.emplace_back([lp] {
+      char nm[16];  // "qmx-loop-N" in top -H, /proc/<pid>/task/*/comm and the stall watchdog
+      snprintf(nm, sizeof(nm), "qmx-loop-%d", lp->index());
+      pthread_setname_np(pthread_self(), nm);
       try {
         lp->run();
       } catch (const std::exception& e) {

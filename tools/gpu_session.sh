@@ -50,7 +50,7 @@ d = json.loads(lines[-1]); b = d.get("breakdown_one_rank", {})
 print(name, d["value"], "p50ttft", d.get("p50_ttft_ms"), "valid", d.get("valid"), d.get("validated"),
       "inv", d.get("invalid"), "nocont", d.get("no_content"), "kern", b.get("tick_kernel_us_avg"),
       "tickwall", b.get("tick_wall_us_avg"), "spt", b.get("streams_per_tick"), "fin", b.get("finalize_items_fused"), b.get("finalize_host"),
-      "proxy_cpu", b.get("proxy_cpu_ms_per_1k_req"), "lg_cpu", b.get("loadgen_cpu_ms_per_1k_req"))
+      "proxy_cpu", b.get("proxy_cpu_ms_per_1k_req"), "lg_cpu", b.get("loadgen_cpu_ms_per_1k_req"), "rss", b.get("proxy_rss_MB"), "p5ms", b.get("loop_passes_over_5ms"))
 EOF
 }
 bench() {  # name timeout env... -- args...
