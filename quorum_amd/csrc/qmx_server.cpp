@@ -2841,7 +2841,16 @@ class Loop {
         if (b.rx_data == 0 && b.t_sp_open > 0) h_sp_first.observe(t - b.t_sp_open);
         b.t_sp_last = t;
         b.rx_data++;
-        if (s->cl) send_content(s, m.payload);
+        if (s->cl) {
+          // the session's other streams arrive from other ranks, each in a pass of its own: after
+          // the first content (TTFT is not delayed), a remote delta waits corked (at most the
+          // coalescing deadline) while another stream of the session is still running — the
+          // last one's output sends them all, one client send instead of one per rank
+          bool hold = false;
+          if (spread_hold_ && coalesce_s_ > 0 && s->first_content)
+            for (size_t k = 0; k < s->bs.size() && !hold; ++k) hold = (int)k != m.bi && s->bs[k].state == 0;
+          send_content(s, m.payload.data(), m.payload.size(), hold);
+        }
         if (b.bulk_waiting && b.rx_data >= b.bulk_msg.b) {
           b.bulk_waiting = false;
           XMsg bm = std::move(b.bulk_msg);
@@ -3529,6 +3538,7 @@ class Loop {
     const char* e = env_get("QMX_COALESCE_US");
     return (e ? atof(e) : 500.0) * 1e-6;
   }();
+  const bool spread_hold_ = env_flag("QMX_SPREAD_HOLD", true);  // remote deltas coalesced (handle_x)
   std::vector<EngineOp> ops_;  // engine feed / finish / release of this iteration (flush_ops)
   const bool early_flush_ = env_flag("QMX_EARLY_FLUSH", true);  // A/B knob
   // QMX_SPREAD_SELF=1 with placement spread at world 1 (rehearsal / GPU test): the odd
