@@ -1421,8 +1421,12 @@ class Loop {
           // tick in flight) waits for that output (<= one tick) instead of its own send — a
           // stream trickling in event by event otherwise costs a client send per tick.  A
           // stream with nothing pending (the steady-state LLM pace) is sent at once.
-          const bool hold = coalesce_s_ > 0 && s->first_content && !(r.flags & (RF_DONE | RF_ABORTED)) &&
-                            more_pending(r.slot, s->bs[bi].up);
+          // An aggregated session's sources are followed by the aggregator's answer: their
+          // deltas after the first content wait for it (or the deadline) — one client send for
+          // the sources' progress and the answer's first output instead of one per tick.
+          const bool hold = coalesce_s_ > 0 && s->first_content &&
+                            ((!(r.flags & (RF_DONE | RF_ABORTED)) && more_pending(r.slot, s->bs[bi].up)) ||
+                             (s->stage == 0 && aggregated_));
           send_content(s, r.data(), r.size(), hold);
         }
       } else if (s->cl && s->cl->held && s->kind != K_REMOTE && !more_pending(r.slot, s->bs[bi].up))
@@ -2847,8 +2851,10 @@ class Loop {
           // coalescing deadline) while another stream of the session is still running — the
           // last one's output sends them all, one client send instead of one per rank
           bool hold = false;
-          if (spread_hold_ && coalesce_s_ > 0 && s->first_content)
+          if (spread_hold_ && coalesce_s_ > 0 && s->first_content) {
+            hold = s->stage == 0 && aggregated_;  // (the aggregator's answer follows: as in apply)
             for (size_t k = 0; k < s->bs.size() && !hold; ++k) hold = (int)k != m.bi && s->bs[k].state == 0;
+          }
           send_content(s, m.payload.data(), m.payload.size(), hold);
         }
         if (b.bulk_waiting && b.rx_data >= b.bulk_msg.b) {
@@ -3539,6 +3545,9 @@ class Loop {
     return (e ? atof(e) : 500.0) * 1e-6;
   }();
   const bool spread_hold_ = env_flag("QMX_SPREAD_HOLD", true);  // remote deltas coalesced (handle_x)
+  // every session's sources are followed by an aggregator call (apply / handle_x hold their
+  // deltas for it); QMX_AGG_HOLD=0 turns the hold off (A/B)
+  const bool aggregated_ = env_flag("QMX_AGG_HOLD", true) && !cfg_.skip_final && !cfg_.aggregator_name.empty();
   std::vector<EngineOp> ops_;  // engine feed / finish / release of this iteration (flush_ops)
   const bool early_flush_ = env_flag("QMX_EARLY_FLUSH", true);  // A/B knob
   // QMX_SPREAD_SELF=1 with placement spread at world 1 (rehearsal / GPU test): the odd
