@@ -53,7 +53,8 @@ enum XType : uint8_t {
 };
 // X_FINAL / X_BULK / X_SENT flags (XF_HOSTCOPY: an X_BULK whose bytes a bulk round put in HBM
 // and the bulk thread copied out — XOptions::host_copy)
-enum : uint8_t { XF_TEXT = 1, XF_ABORTED = 2, XF_FAILED = 4, XF_HOSTCOPY = 8 };
+// XF_LAST (X_DATA): the stream's last deltas — its tick carried the end of the response
+enum : uint8_t { XF_TEXT = 1, XF_ABORTED = 2, XF_FAILED = 4, XF_HOSTCOPY = 8, XF_LAST = 16 };
 
 struct XMsg {
   uint8_t type = 0, flags = 0;

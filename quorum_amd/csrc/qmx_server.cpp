@@ -1413,7 +1413,9 @@ class Loop {
         r.clear_sse();  // QMX_FAULT_DROP_DELTA: fault injection (the bench's validator must notice)
       if (!r.empty()) {
         if (s->kind == K_REMOTE) {
-          post_owner(s, X_DATA, 0, 0, r.data(), r.size());  // framed from the view: one copy
+          // framed from the view: one copy; XF_LAST: the owner may hold it for the session's
+          // other streams (handle_x), never a stream's earlier deltas
+          post_owner(s, X_DATA, (r.flags & (RF_DONE | RF_ABORTED)) ? XF_LAST : 0, 0, r.data(), r.size());
           s->data_sent++;
         } else if (s->cl) {
           // output coalescing across ticks: once the session's first content is out (TTFT),
@@ -1421,12 +1423,13 @@ class Loop {
           // tick in flight) waits for that output (<= one tick) instead of its own send — a
           // stream trickling in event by event otherwise costs a client send per tick.  A
           // stream with nothing pending (the steady-state LLM pace) is sent at once.
-          // An aggregated session's sources are followed by the aggregator's answer: their
-          // deltas after the first content wait for it (or the deadline) — one client send for
-          // the sources' progress and the answer's first output instead of one per tick.
+          // A stream's LAST output (its tick carried the end of the response) may also wait for
+          // the rest of its session: another stream still running, or, in an aggregated session,
+          // the aggregator's answer — one client send instead of one per tick.  A trickling
+          // stream's earlier deltas never wait for other streams (per-token latency unchanged).
+          const bool last = (r.flags & (RF_DONE | RF_ABORTED)) != 0;
           const bool hold = coalesce_s_ > 0 && s->first_content &&
-                            ((!(r.flags & (RF_DONE | RF_ABORTED)) && more_pending(r.slot, s->bs[bi].up)) ||
-                             (s->stage == 0 && aggregated_));
+                            (last ? session_hold(s, bi) : more_pending(r.slot, s->bs[bi].up));
           send_content(s, r.data(), r.size(), hold);
         }
       } else if (s->cl && s->cl->held && s->kind != K_REMOTE && !more_pending(r.slot, s->bs[bi].up))
@@ -2389,6 +2392,15 @@ class Loop {
     if (hub_) return up_readable(up) || eng().pending(slot);
     return eng().pending(slot) || up_readable(up);
   }
+  // a finished stream's output may wait for the rest of its session: another of its streams
+  // is still running, or (aggregated sessions, before the aggregator) the answer follows
+  bool session_hold(const Session* s, int bi) const {
+    if (s->stage == 0 && aggregated_) return true;
+    if (!session_hold_) return false;
+    for (size_t k = 0; k < s->bs.size(); ++k)
+      if ((int)k != bi && s->bs[k].state == 0) return true;
+    return false;
+  }
   void unhold(Client* c) {
     if (!c->held) return;
     c->held = false;
@@ -2847,14 +2859,10 @@ class Loop {
         b.rx_data++;
         if (s->cl) {
           // the session's other streams arrive from other ranks, each in a pass of its own: after
-          // the first content (TTFT is not delayed), a remote delta waits corked (at most the
-          // coalescing deadline) while another stream of the session is still running — the
-          // last one's output sends them all, one client send instead of one per rank
-          bool hold = false;
-          if (spread_hold_ && coalesce_s_ > 0 && s->first_content) {
-            hold = s->stage == 0 && aggregated_;  // (the aggregator's answer follows: as in apply)
-            for (size_t k = 0; k < s->bs.size() && !hold; ++k) hold = (int)k != m.bi && s->bs[k].state == 0;
-          }
+          // the first content (TTFT is not delayed), a remote stream's last deltas wait corked (at
+          // most the coalescing deadline) while the rest of the session is still to come — the
+          // last arrival's output sends them all, one client send instead of one per rank
+          const bool hold = coalesce_s_ > 0 && s->first_content && (m.flags & XF_LAST) && session_hold(s, m.bi);
           send_content(s, m.payload.data(), m.payload.size(), hold);
         }
         if (b.bulk_waiting && b.rx_data >= b.bulk_msg.b) {
@@ -3544,7 +3552,9 @@ class Loop {
     const char* e = env_get("QMX_COALESCE_US");
     return (e ? atof(e) : 500.0) * 1e-6;
   }();
-  const bool spread_hold_ = env_flag("QMX_SPREAD_HOLD", true);  // remote deltas coalesced (handle_x)
+  // a finished stream's last output waits for its session's other streams (session_hold);
+  // QMX_SESSION_HOLD=0 turns it off (A/B)
+  const bool session_hold_ = env_flag("QMX_SESSION_HOLD", true);
   // every session's sources are followed by an aggregator call (apply / handle_x hold their
   // deltas for it); QMX_AGG_HOLD=0 turns the hold off (A/B)
   const bool aggregated_ = env_flag("QMX_AGG_HOLD", true) && !cfg_.skip_final && !cfg_.aggregator_name.empty();
