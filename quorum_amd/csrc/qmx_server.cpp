@@ -1424,8 +1424,8 @@ class Loop {
           // stream trickling in event by event otherwise costs a client send per tick.  A
           // stream with nothing pending (the steady-state LLM pace) is sent at once.
           // A stream's LAST output (its tick carried the end of the response) may also wait for
-          // the rest of its session: another stream still running, or, in an aggregated session,
-          // the aggregator's answer — one client send instead of one per tick.  A trickling
+          // the rest of its session: another stream still running, or its final output (the
+          // final event / the aggregator's answer) — one client send instead of one per tick.  A trickling
           // stream's earlier deltas never wait for other streams (per-token latency unchanged).
           const bool last = (r.flags & (RF_DONE | RF_ABORTED)) != 0;
           const bool hold = coalesce_s_ > 0 && s->first_content &&
@@ -2393,9 +2393,10 @@ class Loop {
     return eng().pending(slot) || up_readable(up);
   }
   // a finished stream's output may wait for the rest of its session: another of its streams
-  // is still running, or (aggregated sessions, before the aggregator) the answer follows
+  // is still running, or (parallel sessions with a final output) the final event / the
+  // aggregator's answer follows
   bool session_hold(const Session* s, int bi) const {
-    if (s->stage == 0 && aggregated_) return true;
+    if (s->stage == 0 && s->kind == K_PAR && final_follows_) return true;
     if (!session_hold_) return false;
     for (size_t k = 0; k < s->bs.size(); ++k)
       if ((int)k != bi && s->bs[k].state == 0) return true;
@@ -3555,9 +3556,10 @@ class Loop {
   // a finished stream's last output waits for its session's other streams (session_hold);
   // QMX_SESSION_HOLD=0 turns it off (A/B)
   const bool session_hold_ = env_flag("QMX_SESSION_HOLD", true);
-  // every session's sources are followed by an aggregator call (apply / handle_x hold their
-  // deltas for it); QMX_AGG_HOLD=0 turns the hold off (A/B)
-  const bool aggregated_ = env_flag("QMX_AGG_HOLD", true) && !cfg_.skip_final && !cfg_.aggregator_name.empty();
+  // a parallel session's streams are followed by its final output (the concatenated final
+  // event, or the aggregator's answer): a stream's last deltas may wait for it (session_hold);
+  // QMX_FINAL_HOLD=0 turns the hold off (A/B)
+  const bool final_follows_ = env_flag("QMX_FINAL_HOLD", true) && !cfg_.skip_final;
   std::vector<EngineOp> ops_;  // engine feed / finish / release of this iteration (flush_ops)
   const bool early_flush_ = env_flag("QMX_EARLY_FLUSH", true);  // A/B knob
   // QMX_SPREAD_SELF=1 with placement spread at world 1 (rehearsal / GPU test): the odd

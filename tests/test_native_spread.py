@@ -490,7 +490,7 @@ def test_spread_remote_deltas_coalesce_client_sends():
     """Spread placement: a session's remote streams deliver their deltas from other ranks, each
     in an io-loop pass of its own.  After the session's first content, a remote stream's last
     deltas (XF_LAST) wait corked while the rest of the session is to come — another stream
-    still running (QMX_SESSION_HOLD) or the aggregator's answer (QMX_AGG_HOLD), both default
+    still running (QMX_SESSION_HOLD) or the aggregator's answer (QMX_FINAL_HOLD), both default
     on — so the last arrival sends them all: the same bytes, fewer client sends than off
     (the 4-rank aggregate4 rehearsal on the MI355X box: 4.4 -> 2.8 client sends per request,
     74-77k -> 91-93k req/s, profiles/r6/spread_hold)."""
@@ -501,7 +501,7 @@ def test_spread_remote_deltas_coalesce_client_sends():
         req = {"messages": MSG, "stream": True}
         runs = {}
         for hold in ("1", "0"):
-            with native_cluster(cfg, 4, run_env={"QMX_SESSION_HOLD": hold, "QMX_AGG_HOLD": hold}) as cports:
+            with native_cluster(cfg, 4, run_env={"QMX_SESSION_HOLD": hold, "QMX_FINAL_HOLD": hold}) as cports:
                 m0 = [httpx.get(f"http://127.0.0.1:{p}/metrics").text for p in cports]
                 bodies = [httpx.post(f"http://127.0.0.1:{cports[0]}/chat/completions", json=req, headers=AUTH,
                                      timeout=30).text for _ in range(24)]
