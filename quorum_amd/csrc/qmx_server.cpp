@@ -1041,7 +1041,9 @@ class Loop {
           // ready, or due within QMX_LOOP_SPIN_US: look again at once (no timer wake-up)
           n = epoll_wait(ep_, evs.data(), (int)evs.size(), 0);
         } else {
-          const double us = std::min(std::max(exp_us, (double)poll_us_), 1000.0 * std::max(to, 1));
+          // the timer ends where the spin window begins (a wake-up at the due time itself
+          // would land a timer's latency after it, past the window)
+          const double us = std::min(std::max(exp_us - spin_us_, (double)poll_us_), 1000.0 * std::max(to, 1));
           timespec ts{0, (long)(us * 1000.0)};
           n = epoll_pwait2(ep_, evs.data(), (int)evs.size(), &ts, nullptr);
           if (n < 0 && errno == ENOSYS) {  // a kernel before 5.11: sleep, then look
@@ -3473,10 +3475,13 @@ class Loop {
     return e ? std::max(1, atoi(e)) : 3;
   }();
   // a tick due within this many us is waited for by looking again at once, not by a timer
-  // (a timed wake-up of a sleeping thread costs several us more)
+  // (a timed wake-up of a sleeping thread lands ~2 us after its time); a longer wait sleeps
+  // until the window begins.  4 us (MI355X, profiles/r6/spin): done -> taken 4.7-4.9 ->
+  // 2.9-3.1 us with few connections (p50 TTFT 0.042 -> 0.039 ms at 1 connection, 0.050 ->
+  // 0.044 ms and +19% req/s at 8), within noise at the headline's 64 (loops are busy there)
   const double spin_us_ = [] {
     const char* e = env_get("QMX_LOOP_SPIN_US");
-    return e ? atof(e) : 0.0;
+    return e ? atof(e) : 4.0;
   }();
   // loop ticks: also look for results between the new requests an iteration parses (parsing
   // and the upstream sends are an iteration's longest stretch without a look);
