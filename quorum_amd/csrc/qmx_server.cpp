@@ -2113,11 +2113,15 @@ class Loop {
           if (!u->got_bytes) h_upstream_ttfb.observe(lnow() - u->t_open);
           u->got_bytes = true;
           u->last_io = lnow();
+          // a trickling upstream (read pacing): a short read of a response body already under
+          // way — not the read that carried the headers (a whole response written after its
+          // headers arrives as a header read and one body read, and never trickles)
+          const bool in_body = u->rp.phase != 0;
           if (u->rp.feed(buf, r, body) < 0) {
             c_fail_protocol++;
             return up_error(u, "invalid HTTP response");
           }
-          if (r < 2048 && !u->rp.done()) ++small_reads_;  // a trickling upstream (read pacing)
+          if (in_body && r < 2048 && !u->rp.done()) ++small_reads_;
           // plain TCP, short read: drained (level-triggered epoll reports more data); a
           // complete response needs no EAGAIN probe either.  TLS keeps reading: its
           // records can sit decrypted inside the SSL object with the socket empty.
