@@ -3005,8 +3005,13 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) 
     if (tid < kWords) {
       uint32_t w;
       if (relay) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // written by the host before `posted`
+        // written by the host before `posted`, which thread 0 saw before the barrier: these
+        // system-scope loads bypass the caches and are issued after that load returned.  The
+        // acquire (for the tick's host-written items and tiles) follows them, so its wait for
+        // thread 0's t_seen store — a PCIe write — overlaps the descriptor's round trip
+        // instead of preceding it
         w = __hip_atomic_load((uint32_t*)&door->d + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       } else {
         // system scope (not just agent): this is also the workgroup's acquire of the tick's
         // host-written items / tile bytes and of other XCDs' slot state — one cache
@@ -3039,13 +3044,18 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) 
       // __threadfence() per thread was one per wave)
       wave_stores_done();
       __syncthreads();
-      if (tid == 0) {
+      // the host-visible stamp and diagnostics (PCIe writes) from wave 1: a wave waits on its
+      // own counter, so wave 0's publish below does not wait for these writes to complete
+      // (they preceded it in wave 0 through r6).  The relay's item 0 publishes its result only
+      // after every wave's stores are done, so the host — which reads these after every result
+      // of the tick — sees this tick's values
+      if (tid == 64) {
         __hip_atomic_store(&door->t_relayed, (uint64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&door->relayed, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (D.stop) __hip_atomic_store(&door->exits, (2u << 16) | (gen & 0xffffu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        publish_agent(&ctl->seq, c);
       }
+      if (tid == 0) publish_agent(&ctl->seq, c);
     }
     if (D.stop) return;  // D is block-uniform (LDS, written before the barrier)
     last = c;  // (the tick's acquire: wave 0's fence above, ordered before every wave by the barrier)
@@ -4672,9 +4682,11 @@ void HipGrid::calibrate_locked() {
     D.d.stop = 0;
     D.d.params_src = nullptr;
     D.d.seq = s;
+    const uint64_t seen0 = __atomic_load_n(&D.t_seen, __ATOMIC_ACQUIRE);
     const double h0 = steady_s();
     __atomic_store_n(&D.posted, s, __ATOMIC_RELEASE);
-    while (__atomic_load_n(&D.relayed, __ATOMIC_ACQUIRE) != s)
+    // (the relay's wave 0 stores t_seen and its wave 1 `relayed`: the stamp is waited for too)
+    while (__atomic_load_n(&D.relayed, __ATOMIC_ACQUIRE) != s || __atomic_load_n(&D.t_seen, __ATOMIC_ACQUIRE) == seen0)
       if (steady_s() - h0 > 0.05) return;  // the grid is not answering: no calibration now
     const double h1 = steady_s();
     const double g = (double)__atomic_load_n(&D.t_seen, __ATOMIC_ACQUIRE) * 1e-2;  // 100 MHz -> us
