@@ -3631,6 +3631,9 @@ static void presize_fd_table() {
   }
   const long want = (long)std::min<rlim_t>(rl.rlim_cur, (rlim_t)1 << 17);
   if (want <= 1024) return;
+  // (dup3 onto an open descriptor would close it: the top slot must be free — it is, in a
+  // process that has not opened ~1e5 files before the server starts)
+  if (fcntl((int)want - 1, F_GETFD) != -1 || errno != EBADF) return;
   const int fd = open("/dev/null", O_RDONLY | O_CLOEXEC);
   if (fd < 0) return;
   const int hi = dup3(fd, (int)want - 1, O_CLOEXEC);  // the table now covers [0, want)
