@@ -2798,12 +2798,37 @@ union TickLds {
   FinShared f;
 };
 
+template <class T>
+__device__ __forceinline__ T* uni(T* p) {
+  typedef __attribute__((address_space(1))) T GT;
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (T*)(GT*)(((uint64_t)hi << 32) | lo);
+}
+
+// A finalize item's arguments as wave-uniform scalars, made where they are used: held in
+// registers across the whole item loop they add to the persistent kernel's SGPR spills
+__device__ __forceinline__ FinArgs fin_uni(const FinArgs& a) {
+  FinArgs f;
+  f.items = uni(a.items);
+  f.texts = uni(a.texts);
+  f.fin_in = uni(a.fin_in);
+  f.join = uni(a.join);
+  f.out_dev = uni(a.out_dev);
+  f.out_host = uni(a.out_host);
+  f.res = uni(a.res);
+  f.text_len = uni(a.text_len);
+  f.segs = uni(a.segs);
+  return f;
+}
+
 // One work item of a tick: k < n_tick a stream tile, else finalize request k - n_tick.
 // Publishes the item's result record last (fence + sequence number).
 __device__ __forceinline__ void run_item(int k, const WorkItem* __restrict__ items, const uint8_t* __restrict__ in,
                                          uint8_t* __restrict__ out, WorkResult* __restrict__ res,
                                          DevSlot* __restrict__ state, uint8_t* __restrict__ content,
-                                         const KParams& Pk, uint32_t seq, uint32_t n_tick, const FinArgs& fa,
+                                         const KParams& Pk, uint32_t seq, uint32_t n_tick, const FinArgs& fa_src,
                                          const BackendTpl* __restrict__ btpl_rd, BackendTpl* __restrict__ btpl_wr,
                                          TickLds& U) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -2822,6 +2847,7 @@ __device__ __forceinline__ void run_item(int k, const WorkItem* __restrict__ ite
     if (threadIdx.x == 0) publish_system(&res[k].seq, seq);
   } else {
     const int j = (int)(k - n_tick);
+    const FinArgs fa = fin_uni(fa_src);
     fin_stage(fa, j, content, Pk.content_cap);
     fin_body(fa, j, content, Pk.content_cap, Pk.ts, U.f);
     if (threadIdx.x == 0) {
@@ -2874,14 +2900,6 @@ __global__ __launch_bounds__(BS) void qmx_tick_kernel(const WorkItem* __restrict
 // memory, never LDS).  Saying so lets the compiler emit global_* instead of flat_* accesses
 // through the descriptor's pointers, as it does for kernel arguments: a flat access also
 // counts against lgkmcnt, so every LDS wait after it would wait for the memory access too.
-template <class T>
-__device__ __forceinline__ T* uni(T* p) {
-  typedef __attribute__((address_space(1))) T GT;
-  const uint64_t v = (uint64_t)p;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return (T*)(GT*)(((uint64_t)hi << 32) | lo);
-}
 
 struct TickDesc {
   const WorkItem* items;
@@ -3061,16 +3079,6 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) 
     last = c;  // (the tick's acquire: wave 0's fence above, ordered before every wave by the barrier)
     // descriptor fields read from LDS land in VGPRs: make them wave-uniform scalars again
     // (as kernel arguments are), or every address derived from them costs vector registers
-    FinArgs fa;
-    fa.items = uni(D.fa.items);
-    fa.texts = uni(D.fa.texts);
-    fa.fin_in = uni(D.fa.fin_in);
-    fa.join = uni(D.fa.join);
-    fa.out_dev = uni(D.fa.out_dev);
-    fa.out_host = uni(D.fa.out_host);
-    fa.res = uni(D.fa.res);
-    fa.text_len = uni(D.fa.text_len);
-    fa.segs = uni(D.fa.segs);
     const uint32_t n_tick = __builtin_amdgcn_readfirstlane(D.n_tick);
     const int total = (int)(n_tick + __builtin_amdgcn_readfirstlane(D.n_fin));
     const uint32_t seq = __builtin_amdgcn_readfirstlane(D.seq);
@@ -3097,7 +3105,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) 
       // unclobbered within the kernel)
       asm volatile("" ::: "memory");
       run_item(k, uni(D.items), uni(D.in), uni(D.out), uni(D.res), uni(D.state), uni(D.content), *uni(D.params), seq,
-               n_tick, fa, uni(D.btpl_rd), uni(D.btpl_wr), U);
+               n_tick, D.fa, uni(D.btpl_rd), uni(D.btpl_wr), U);
       __syncthreads();  // LDS is reused by the next item
     }
     __syncthreads();  // D / cmd are rewritten by thread 0 for the next tick
