@@ -810,8 +810,8 @@ def spread_check(args, sc, rank, world, engine, device, bin_dir, tmp, mock_ports
     * ``local`` (port + 80): the same config placed locally — the probe's control.
 
     Every response is validated; the exchange counters say which path moved the finals.
-    Failures are reported, never hidden (the run is then invalid), and do not touch the
-    headline numbers."""
+    Failures are reported, never hidden (``checks_ok: false`` and a warning), and do not
+    touch the headline measurement, whose validity covers the timed region."""
     from quorum_amd.parallel.exchange import exchange_env
 
     on_gpu = n_dev >= world
