@@ -604,6 +604,8 @@ def breakdown(m0, m1, elapsed):
         "h2d_MB": round(d.get("qmx_kernel_h2d_bytes", 0.0) / 1e6, 2),
         "d2h_MB": round(d.get("qmx_kernel_d2h_bytes", 0.0) / 1e6, 2),
         "escalations": int(d.get("qmx_kernel_escalations", 0.0)),
+        # streams opened on the host path by the latency mode (QMX_LIGHT_HOST)
+        "light_host_opens": int(d.get("qmx_kernel_light_host_opens", 0.0)),
         # io-loop syscalls per request (sends to clients / upstreams, recvs, epoll, wakeups)
         "syscalls_per_req": {k.split('"')[1]: round(v / d["qmx_requests_total"], 2)
                              for k, v in d.items() if k.startswith("qmx_syscalls_total")}

@@ -314,6 +314,11 @@ class HipEngine : public HostEngine {
   bool remote_hbm_direct() const { return remote_hbm_direct_; }
   std::unordered_map<std::string, double> kernel_stats();
   int lanes() const { return (int)lanes_.size(); }
+  // Latency mode for one stream, at its open (loop-tick mode: the io loop's own engine): the
+  // slot runs on the host path — the C++ engine inline in the loop's tick, byte-identical —
+  // instead of the GPU.  For light load, where a GPU tick's fixed ~23 us (doorbell, relay,
+  // one workgroup's 16 us kernel, publish) is most of a stream's TTFT (profiles/r6/lowload).
+  void host_open(int slot);
 
  protected:
   void run_tick(std::vector<Work>& work, std::vector<FinalizeReq>& fin, int64_t created,
@@ -387,7 +392,7 @@ class HipEngine : public HostEngine {
   std::vector<uint32_t> content_len_;    // device content bytes per slot
   // stats
   std::atomic<uint64_t> escalations_{0}, fin_host_{0}, remote_dev_{0}, remote_staged_{0}, remote_copied_{0},
-      remote_copied_inline_{0};
+      remote_copied_inline_{0}, light_opens_{0};
   bool remote_hbm_direct_ = true;
   int spin_us_ = 0;  // QMX_WAIT_SPIN_US: yield-poll before the blocking wait
   bool poll_ = true;  // QMX_WAIT=event: wait on a blocking-sync HIP event instead of polling

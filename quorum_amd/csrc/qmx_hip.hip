@@ -3737,6 +3737,16 @@ void HipEngine::set_remote_content(int slot, const std::string* bytes, size_t le
   content_len_[slot] = (uint32_t)len;
 }
 
+void HipEngine::host_open(int slot) {
+  // a fresh slot: filter state and content were reset by open(), nothing lives in HBM yet
+  if (slot >= 0 && slot < max_slots_) {
+    host_mode_[slot] = 1;
+    remote_host_[slot] = 0;
+    content_len_[slot] = 0;
+  }
+  ++light_opens_;
+}
+
 void HipEngine::escalate(int slot, bool fresh) {
   // migrate the slot to the host path: import filter state + content from HBM
   SlotCore& c = core_[slot];
@@ -4568,6 +4578,7 @@ std::unordered_map<std::string, double> HipEngine::kernel_stats() {
   m["clk_cycles"] = cyc;  // summable across engines (/metrics sums the io loops' engines)
   m["clk_us"] = cus;
   m["escalations"] = (double)escalations_.load();
+  m["light_host_opens"] = (double)light_opens_.load();  // streams opened on the host path (latency mode)
   m["fin_host"] = (double)fin_host_.load();
   m["remote_texts_hbm"] = (double)remote_dev_.load();        // spread owner: finals an RCCL round put in HBM
   m["remote_texts_staged"] = (double)remote_staged_.load();  // ... that came over the mesh

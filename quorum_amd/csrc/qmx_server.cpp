@@ -1469,6 +1469,12 @@ class Loop {
     } else {
       slot = eng_->open(index, f, e, &gen);
       if (heng_ && slot >= loop_slots_) c_host_path_opens++;  // beyond this loop's HBM slot state
+      // latency mode (QMX_LIGHT_HOST=N, opt-in): a stream of a session opened while this loop
+      // has no tick on the GPU and serves at most N sessions runs on the host path,
+      // byte-identical, without a GPU tick's fixed ~23 us.  Under load a loop nearly always has
+      // a tick in flight, so its streams go to the GPU as before (profiles/r6/lowload)
+      else if (heng_ && light_host_ > 0 && jobs_live_ == 0 && (int)sessions_.size() <= light_host_)
+        heng_->host_open(slot);
       if (ver_ && verify) ver_->open(slot, gen, index, f, e);
     }
     slot_owner_[slot] = SlotOwner{s, bi, gen};
@@ -3496,6 +3502,10 @@ class Loop {
   const int check_every_ = [] {
     const char* e = env_get("QMX_LOOP_CHECK_EVERY");
     return e ? std::max(1, atoi(e)) : 1;
+  }();
+  const int light_host_ = [] {
+    const char* e = env_get("QMX_LIGHT_HOST");
+    return e ? std::max(0, atoi(e)) : 0;
   }();
   const bool req_check_ = [] {
     const char* e = env_get("QMX_LOOP_REQ_CHECK");

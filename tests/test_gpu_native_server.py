@@ -64,6 +64,54 @@ def test_native_hip_random_sessions(seed, monkeypatch):
     assert ext.server_counters()["verify_mismatches"] == before
 
 
+@pytest.mark.parametrize("name", sorted(T.SCENARIOS))
+def test_native_hip_light_host_matches_python(name, monkeypatch):
+    """Latency mode (QMX_LIGHT_HOST=4): the scenarios' sessions come one at a time, so their
+    streams open on the HIP engine's host path — the C++ engine inline in the loop's tick —
+    and must still equal the FastAPI app byte for byte (verify mode on)."""
+    from quorum_amd.ops import native
+
+    ext = native.require()
+    before = ext.server_counters()["verify_mismatches"]
+    monkeypatch.setenv("QMX_LIGHT_HOST", "4")
+    monkeypatch.setattr(T, "ENGINE", "hip")
+    monkeypatch.setattr(T, "VERIFY", True)
+    T.test_native_matches_python(name, "loops")
+    assert ext.server_counters()["verify_mismatches"] == before
+
+
+@pytest.mark.parametrize("conns,light,port", [(2, "0", 23560), (2, "4", 23570), (64, "4", 23580)])
+def test_gpu_bench_light_host(tmp_path, conns, light, port):
+    """The latency mode under the bench's validation: at 2 connections with QMX_LIGHT_HOST=4
+    most streams open on the host path (none without it); at the headline's 64, host-path and
+    GPU streams mix on the same loops (a session opened between two ticks goes to the host) —
+    every response still valid.  The mode is opt-in: it costs the headline ~5% (r6 lowload)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, QMX_BENCH_ENGINE="hip", QMX_LIGHT_HOST=light)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "3", "--warmup", "1",
+                        "--batch", "4096", "--conns", str(conns), "--port", str(port), "--ceiling", "0"],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=180)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert lines, r.stderr[-3000:]
+    res = json.loads(lines[-1])
+    assert r.returncode == 0 and res["valid"] and res["invalid"] == 0, (res.get("invalid"), r.stderr[-2000:])
+    bd = res["breakdown_one_rank"]
+    streams = 2 * (3 + 1) * 4096  # two backends per request, warmup included
+    if light == "0":
+        assert bd["light_host_opens"] == 0 and bd["kernel_launches"] > 0, bd
+    elif conns == 2:
+        # (the engines' counters are snapshots up to 100 ms old — a fifth of this short run —
+        # and a finished session can outlive its response by its upstreams' last bytes)
+        assert bd["light_host_opens"] >= streams * 0.5, (bd["light_host_opens"], streams)
+    else:  # loops with ticks in flight: host-path and GPU streams mixed on the same loops, all valid
+        assert bd["kernel_launches"] > 0, bd
+
+
 @pytest.mark.parametrize("knob,port", [("", 23400), ("QMX_EAGER_POST=1", 23500)])
 def test_gpu_bench_headline_valid(tmp_path, knob, port):
     """The headline bench on the HIP engine (shared engine, pipelined tick lanes, persistent
