@@ -1469,12 +1469,14 @@ class Loop {
     } else {
       slot = eng_->open(index, f, e, &gen);
       if (heng_ && slot >= loop_slots_) c_host_path_opens++;  // beyond this loop's HBM slot state
-      // latency mode (QMX_LIGHT_HOST=N, opt-in): a stream of a session opened while this loop
-      // has no tick on the GPU and serves at most N sessions runs on the host path,
-      // byte-identical, without a GPU tick's fixed ~23 us.  Under load a loop nearly always has
-      // a tick in flight, so its streams go to the GPU as before (profiles/r6/lowload)
-      else if (heng_ && light_host_ > 0 && jobs_live_ == 0 && (int)sessions_.size() <= light_host_)
-        heng_->host_open(slot);
+      // latency mode (QMX_LIGHT_HOST=N, opt-in): a stream opened while this loop has no tick
+      // on the GPU and has served at most N sessions at a time lately (an average over its
+      // recent opens, so a momentary gap between two ticks under load does not count) runs on
+      // the host path, byte-identical, without a GPU tick's fixed ~23 us (profiles/r6/lowload)
+      else if (heng_ && light_host_ > 0) {
+        sess_ema_ = 0.95 * sess_ema_ + 0.05 * (double)sessions_.size();
+        if (jobs_live_ == 0 && sess_ema_ <= (double)light_host_) heng_->host_open(slot);
+      }
       if (ver_ && verify) ver_->open(slot, gen, index, f, e);
     }
     slot_owner_[slot] = SlotOwner{s, bi, gen};
@@ -3503,6 +3505,7 @@ class Loop {
     const char* e = env_get("QMX_LOOP_CHECK_EVERY");
     return e ? std::max(1, atoi(e)) : 1;
   }();
+  double sess_ema_ = 0;  // latency mode: sessions on this loop, averaged over its recent opens
   const int light_host_ = [] {
     const char* e = env_get("QMX_LIGHT_HOST");
     return e ? std::max(0, atoi(e)) : 0;

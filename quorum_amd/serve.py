@@ -74,6 +74,11 @@ def spawn_workers(config: str, host: str, port: int, workers: int, engine: str, 
     # per-loop engines (runtime.shared_engine: false) each own a HIP stream: give them
     # hardware queues of their own (HIP defaults to 4)
     e.setdefault("GPU_MAX_HW_QUEUES", str(min(16, max(4, threads))))
+    # the HIP engine's latency mode: on an idle loop (no tick on the GPU, <= 2 sessions at a
+    # time lately) a session's streams run on the host path — p50 TTFT 0.040 -> 0.018 ms at one
+    # connection, neutral at the headline's load (profiles/r6/lowload/light_host).  bench.py
+    # and in-process servers leave it off: they measure / test the GPU path itself
+    e.setdefault("QMX_LIGHT_HOST", "2")
     for _ in range(workers if impl == "python" else 1):
         if impl == "native":
             cmd = [sys.executable, "-m", "quorum_amd.serve", "--native-worker", "--config", config, "--host", host,
