@@ -1111,6 +1111,9 @@ def wait_ready(procs, timeout: float) -> bool:
 
 
 def main() -> int:
+    # the bench measures the GPU path itself: serve's latency mode (idle loops' streams on the
+    # HIP engine's host path) stays off unless asked for (QMX_LIGHT_HOST=N)
+    os.environ.setdefault("QMX_LIGHT_HOST", "0")
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
                     help="ranks (one per GPU); > 1 without WORLD_SIZE: launches them (torch.distributed.run)")
