@@ -275,3 +275,87 @@ def test_hip_spread_cluster_matches_local(name, xchg, eager, monkeypatch):
             assert delta("qmx_kernel_fin_items") > 0
     finally:
         live.close()
+
+
+@pytest.mark.parametrize("light", ["", "0"])
+def test_gpu_serve_latency_mode(tmp_path, light):
+    """`serve --impl native --engine hip` — the production launcher, with its default latency
+    mode (QMX_LIGHT_HOST=2 for its workers) or with it off: one client's sessions, one at a
+    time, give the same finals either way (the host path is the byte-identical C++ engine),
+    and /metrics says which path took them."""
+    import os
+    import signal
+    import subprocess
+    import sys
+    import time
+
+    import json
+
+    import httpx
+    import yaml
+
+    from conftest import cfg_parallel, sse_stream
+    from live_upstream import LiveUpstream, free_port
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    live = LiveUpstream()
+    pa = live.serve("a", ("stream", 200, sse_stream(["<think>x</think>", "AAA ", "aaa"])))
+    pb = live.serve("b", ("stream", 200, sse_stream(["BBB ", "<think>y</think>", "bbb"])))
+    cfg = cfg_parallel(2, block={"separator": "\n--\n", "hide_intermediate_think": True, "hide_final_think": False,
+                                 "thinking_tags": ["think"], "skip_final_aggregation": False})
+    cfg["primary_backends"][0]["url"] = f"http://127.0.0.1:{pa}/v1"
+    cfg["primary_backends"][1]["url"] = f"http://127.0.0.1:{pb}/v1"
+    path = str(tmp_path / "config.yaml")
+    with open(path, "w") as f:
+        yaml.safe_dump(cfg, f)
+    port = free_port()
+    env = dict(os.environ, PYTHONPATH=root)
+    env.pop("QMX_LIGHT_HOST", None)
+    if light:
+        env["QMX_LIGHT_HOST"] = light
+    sup = subprocess.Popen([sys.executable, "-m", "quorum_amd.serve", "--impl", "native", "--engine", "hip",
+                            "--config", path, "--port", str(port), "--threads", "2"], cwd=root, env=env,
+                           start_new_session=True)
+    try:
+        base = f"http://127.0.0.1:{port}"
+        t0 = time.time()
+        while True:
+            try:
+                if httpx.get(base + "/health", timeout=2).status_code == 200:
+                    break
+            except httpx.HTTPError:
+                pass
+            assert time.time() - t0 < 120 and sup.poll() is None, "serve did not come up"
+            time.sleep(0.2)
+        finals = set()
+        with httpx.Client(timeout=30) as c:
+            for _ in range(12):
+                r = c.post(base + "/chat/completions", json={"messages": [{"role": "user", "content": "hi"}],
+                                                             "stream": True}, headers={"Authorization": "Bearer k"})
+                assert r.status_code == 200 and r.text.rstrip().endswith("data: [DONE]")
+                for seg in r.text.split("\n\n"):
+                    if '"chatcmpl-parallel-final"' in seg:
+                        finals.add(json.loads(seg[6:])["choices"][0]["delta"]["content"])
+        # the C++ CPU engine's final for the same streams (the reference semantics' oracle)
+        from live_upstream import native_server as cpu_server
+        with cpu_server(cfg, engine="cpu") as cport:
+            rt = httpx.post(f"http://127.0.0.1:{cport}/chat/completions", headers={"Authorization": "Bearer k"},
+                            json={"messages": [{"role": "user", "content": "hi"}], "stream": True}, timeout=30).text
+        want = {json.loads(seg[6:])["choices"][0]["delta"]["content"] for seg in rt.split("\n\n")
+                if '"chatcmpl-parallel-final"' in seg}
+        assert len(want) == 1 and "AAA aaa" in next(iter(want)) and "think" not in next(iter(want)), want
+        assert finals == want, (finals, want)
+        time.sleep(0.3)  # the engines' counters are snapshots up to 100 ms old
+        m = httpx.get(base + "/metrics", timeout=5).text
+        opens = sum(float(ln.split()[-1]) for ln in m.splitlines() if ln.startswith("qmx_kernel_light_host_opens"))
+        if light == "0":
+            assert opens == 0, opens
+        else:
+            assert opens > 0, opens
+    finally:
+        os.killpg(sup.pid, signal.SIGTERM)
+        try:
+            sup.wait(timeout=20)
+        except subprocess.TimeoutExpired:
+            os.killpg(sup.pid, signal.SIGKILL)
+        live.close()
