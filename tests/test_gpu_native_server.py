@@ -107,7 +107,8 @@ def test_gpu_bench_light_host(tmp_path, conns, light, port):
     elif conns == 2:
         # (the engines' counters are snapshots up to 100 ms old — a fifth of this short run —
         # and a finished session can outlive its response by its upstreams' last bytes)
-        assert bd["light_host_opens"] >= streams * 0.5, (bd["light_host_opens"], streams)
+        # (r6: 72-86% of the streams at 1-8 connections on full-length runs)
+        assert bd["light_host_opens"] >= streams * 0.25, (bd["light_host_opens"], streams)
     else:  # loops with ticks in flight: host-path and GPU streams mixed on the same loops, all valid
         assert bd["kernel_launches"] > 0, bd
 
