@@ -153,7 +153,7 @@ ServerCfg server_cfg_from(const py::dict& d) {
   gi("xchg_links", c.xchg_links); gd("xchg_timeout", c.xchg_timeout);
   gd("drain_s", c.drain_s); gs("ready_file", c.ready_file); gb("verify", c.verify); gi("admin_port", c.admin_port);
   gi("shared_engine", c.shared_engine); gi("tick_lanes", c.tick_lanes); gs("tick_mode", c.tick_mode);
-  gi("read_pace_us", c.read_pace_us);
+  gi("read_pace_us", c.read_pace_us); gi("light_host", c.light_host);
   gs("ca_file", c.ca_file); gb("tls_verify", c.tls_verify);
   if (d.contains("backends")) {
     for (auto item : py::cast<py::list>(d["backends"])) {

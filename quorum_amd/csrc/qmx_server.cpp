@@ -3506,7 +3506,8 @@ class Loop {
     return e ? std::max(1, atoi(e)) : 1;
   }();
   double sess_ema_ = 0;  // latency mode: sessions on this loop, averaged over its recent opens
-  const int light_host_ = [] {
+  const int light_host_ = [this] {  // runtime.light_host_sessions, else QMX_LIGHT_HOST, else off
+    if (cfg_.light_host >= 0) return cfg_.light_host;
     const char* e = env_get("QMX_LIGHT_HOST");
     return e ? std::max(0, atoi(e)) : 0;
   }();

@@ -45,6 +45,9 @@ struct ServerCfg {
   // progress) lasts at least this long, so events arriving meanwhile share receives, waits and
   // client sends (0: off; QMX_READ_PACE_US overrides)
   int read_pace_us = 50;
+  // the HIP engine's latency mode: at most this many sessions per io loop lately, and no tick
+  // on the GPU, and a new session's streams run on the host path (-1: QMX_LIGHT_HOST, else 0)
+  int light_host = -1;
   int device = 0;
   int tile = 16384, max_slots = 4096, content_cap = 1 << 20;
   // config

@@ -72,6 +72,7 @@ def native_config(cfg: Dict[str, Any], host: str, port: int, engine: str, device
         "tick_lanes": int(rt.tick_lanes),
         "tick_mode": str(rt.tick_mode or "auto"),
         "read_pace_us": int(rt.read_pace_us),
+        "light_host": -1 if rt.light_host_sessions is None else int(rt.light_host_sessions),
         "ca_file": _ca_bundle(), "tls_verify": os.environ.get("QMX_TLS_VERIFY", "1") not in ("0", "false"),
         "ready_file": (os.environ["QMX_READY_FILE"] + f".{os.getpid()}") if os.environ.get("QMX_READY_FILE") else "",
         # QMX_ADMIN_PORT: this process's own /metrics + /health port (not SO_REUSEPORT-shared)

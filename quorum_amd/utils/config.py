@@ -275,6 +275,12 @@ class RuntimeConfig:
                wait and one client send; whole-response reads never trigger it.  MI355X box,
                headline-shaped trickle: 33k -> 41k req/s and 192 -> 82 us proxy CPU per request at
                50 us, p50 TTFT +0.08 ms (profiles/r6/pacing).  0: off — QMX_READ_PACE_US
+    light_host_sessions: the HIP engine's latency mode — a session opened on an io loop with no
+               tick on the GPU, which has served at most this many sessions at a time lately,
+               runs its streams on the host path (the byte-identical C++ engine, inline): p50
+               TTFT 0.040 -> 0.018 ms at one connection, neutral at the headline's load
+               (profiles/r6/lowload/light_host).  0: off; unset: QMX_LIGHT_HOST, which `serve`
+               sets to 2 for its workers and bench.py to 0
     """
 
     engine: str = "auto"
@@ -297,6 +303,7 @@ class RuntimeConfig:
     watch_config: bool = False
     watch_interval: float = 1.0
     read_pace_us: int = 50
+    light_host_sessions: Optional[int] = None
 
     @classmethod
     def from_config(cls, cfg: Dict[str, Any]) -> "RuntimeConfig":

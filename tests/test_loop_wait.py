@@ -2,6 +2,7 @@
 timer until the spin window before a tick's due time and only then looks without a timer.
 With no tick in flight it must block in epoll — the window may never turn an idle server into
 a busy one (qmx_server.cpp, the run loop's wait; MI355X numbers in profiles/r6/spin)."""
+import os
 import time
 
 import httpx
@@ -54,3 +55,43 @@ def test_idle_loops_block_with_the_spin_window(monkeypatch, spin_us, engine):
         live.close()
     # two io loops spinning would be ~2 s of CPU per second; blocked loops, a few ms
     assert cpu < 0.15 * wall, (spin_us, cpu, wall)
+
+
+def test_light_host_sessions_config(monkeypatch):
+    """runtime.light_host_sessions reaches the native server's config (unset: -1, which
+    leaves the choice to QMX_LIGHT_HOST — `serve` sets 2 for its workers, bench.py 0)."""
+    from quorum_amd.runtime.native_server import native_config
+    from quorum_amd.utils.config import RuntimeConfig
+
+    monkeypatch.delenv("QMX_LIGHT_HOST", raising=False)
+    cfg = cfg_parallel(2, block={"skip_final_aggregation": True})
+    assert RuntimeConfig.from_config(cfg).light_host_sessions is None
+    assert native_config(cfg, "127.0.0.1", 8001, "cpu", 0, 1)["light_host"] == -1
+    cfg["runtime"] = {"light_host_sessions": 3}
+    assert RuntimeConfig.from_config(cfg).light_host_sessions == 3
+    assert native_config(cfg, "127.0.0.1", 8001, "cpu", 0, 1)["light_host"] == 3
+
+
+def test_serve_and_bench_latency_mode_defaults(monkeypatch):
+    """`serve` gives its native workers the latency mode (QMX_LIGHT_HOST=2) unless the caller
+    set it; bench.py sets 0 first, so the headline measures the GPU path."""
+    import subprocess
+
+    from quorum_amd import serve
+
+    seen = {}
+
+    class P:
+        def __init__(self, cmd, env=None, **kw):
+            seen["env"] = env
+
+    monkeypatch.setattr(subprocess, "Popen", P)
+    monkeypatch.delenv("QMX_LIGHT_HOST", raising=False)
+    serve.spawn_workers("c.yaml", "127.0.0.1", 1, 1, "hip", 0, impl="native")
+    assert seen["env"]["QMX_LIGHT_HOST"] == "2"
+    monkeypatch.setenv("QMX_LIGHT_HOST", "0")
+    serve.spawn_workers("c.yaml", "127.0.0.1", 1, 1, "hip", 0, impl="native")
+    assert seen["env"]["QMX_LIGHT_HOST"] == "0"
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "bench.py")) as f:
+        src = f.read()
+    assert 'os.environ.setdefault("QMX_LIGHT_HOST", "0")' in src
